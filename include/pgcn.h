@@ -1,0 +1,207 @@
+/* include/pgcn.h -- the drop-in C ABI of the MI355X GCN engine (libpgcn.so).
+ *
+ * Two layers, both plain C: caller-owned device pointers, sizes, a hipStream_t passed as
+ * `void *`, int status returns (0 = OK, >0 = hipError_t, <0 = PGCN_E_*). Kernel entry
+ * points never allocate (workspace is passed in or owned by a handle created beforehand),
+ * are asynchronous on the given stream and are safe to capture into a hipGraph.
+ *
+ *  (1) Kernel ABI -- one entry per reference kernel family it replaces
+ *      (reference: src/module.cu, src/optim.cu, src/gcn.cu of parallel-GCN).
+ *  (2) Engine ABI -- the GCN object of include/gcn.cuh (ctor + train_epoch/eval/run),
+ *      plus the edge-cut multi-GPU variant (new: the reference is single-GPU).
+ *
+ * A C++ host API mirroring the reference classes (Module, Variable, GCN, Parser) sits on
+ * top of this ABI in parallel-gcn_amd/csrc/host/ (the .hpp files); INTEGRATION.md shows the bindings
+ * a reference maintainer would add.
+ */
+#ifndef PGCN_H
+#define PGCN_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PGCN_OK 0
+#define PGCN_E_INVALID (-1)   /* bad argument / shape */
+#define PGCN_E_NOMEM (-2)     /* device allocation failed */
+#define PGCN_E_IO (-3)        /* dataset could not be read (Parser::parse() == false) */
+#define PGCN_E_COMM (-4)      /* RCCL error */
+#define PGCN_E_NODEVICE (-5)  /* no HIP device: the product has no CPU fallback */
+
+const char *pgcn_status_string(int status);
+int pgcn_version(void);
+
+/* ===================================================================================== */
+/* (1) Kernel ABI                                                                          */
+/* ===================================================================================== */
+
+/* --- xorshift128+ (hpdga-spring23/src/rand.cpp:17-28), host helpers ------------------- */
+/* Default seed state of hpdga init_rand_state() (rand.cpp:6-14). */
+void pgcn_rng_seed(uint64_t state[2]);
+/* state <- state advanced by `k` draws (GF(2) jump-ahead; exact). */
+void pgcn_rng_jump(uint64_t state[2], uint64_t k);
+
+/* --- Graph (DevSparseIndex + precomputed Â values; include/sparse.cuh:21-29,
+ *     src/parser.cpp:164-181) ------------------------------------------------------------ */
+typedef struct pgcn_graph pgcn_graph;
+/* Uploads a CSR adjacency (implicit self loops already present, as the hpdga Parser builds
+ * it), computes coef = 1/sqrtf(deg_src*deg_dst) bit-exactly as hpdga module.cpp:88-90 and
+ * builds the wavefront work schedule. Host pointers. */
+int pgcn_graph_create(int n_nodes, const int *indptr, const int *indices, pgcn_graph **out);
+int pgcn_graph_destroy(pgcn_graph *g);
+long long pgcn_graph_nnz(const pgcn_graph *g);
+/* out[i, 0:dim] = sum_j coef_ij * in[j, 0:dim]  (GraphSum::forward/backward,
+ * src/module.cu:172-210; the backward is the same gather on grads because Â is symmetric).
+ * Row-major, leading dims ld_in/ld_out (multiples of 4, >= dim). Device pointers. */
+int pgcn_graphsum(const pgcn_graph *g, const float *in, int ld_in, float *out, int ld_out,
+                  int dim, void *stream);
+
+/* --- dense GEMMs on fp32 MFMA (Matmul, src/module.cu:274-472; dense X * W1) ------------- */
+/* C[M,N] = A[M,K] * op(B)   (op(B) = B[K,N] if trans_b == 0 else B^T with B stored [N,K]).
+ * Optional dropout on A: element (m,k) is kept iff bit (mask_base + m*mask_ld + k) of
+ * `a_mask` is set, kept values scaled by `a_scale` (a_mask NULL: no dropout). */
+int pgcn_gemm(int M, int N, int K, const float *A, int lda, const float *B, int ldb, int trans_b,
+              float *C, int ldc, const uint64_t *a_mask, long long mask_base, long long mask_ld,
+              float a_scale, void *stream);
+/* C[K,N] = A[M,K]^T * G[M,N], reduced over M deterministically (split-M slabs + ordered
+ * reduction; replaces the atomicAdd kernels matmul_kernel_backward_2 and
+ * sparse_matmul_kernel_backward). `workspace` >= pgcn_gemm_tn_workspace(M,N,K) bytes. */
+size_t pgcn_gemm_tn_workspace(int M, int N, int K);
+int pgcn_gemm_tn(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
+                 float *C, int ldc, const uint64_t *a_mask, long long mask_base,
+                 long long mask_ld, float a_scale, void *workspace, void *stream);
+
+/* --- sparse X (SparseMatmul, src/module.cu:104-163) ----------------------------------- */
+/* c[i,:] = sum_jj drop(a[jj]) * b[indices[jj], :], CSR order (bit-exact vs hpdga). */
+int pgcn_spmm_csr(int m, int p, const int *indptr, const int *indices, const float *a,
+                  const uint64_t *a_mask, float a_scale, const float *b, float *c, void *stream);
+/* bgrad[f,:] = sum over (i,jj) with indices[jj]==f, in CSR order: drop(a[jj]) * cgrad[i,:],
+ * using the transposed index (csc_ptr/csc_row/csc_pos) built by pgcn_csr_transpose. */
+int pgcn_spmm_csc_bwd(int n_features, int p, const int *csc_ptr, const int *csc_row,
+                      const int *csc_pos, const float *a, const uint64_t *a_mask, float a_scale,
+                      const float *cgrad, float *bgrad, void *stream);
+/* host helper: CSR (m rows, nnz, column ids < n_cols) -> CSC with original positions */
+int pgcn_csr_transpose(int m, int n_cols, const int *indptr, const int *indices, int *csc_ptr,
+                       int *csc_row, int *csc_pos);
+
+/* --- dropout (Dropout, src/module.cu:16-99; hpdga module.cpp:208-228) ------------------ */
+/* Bit-exact hpdga masks: chunk c holds the xorshift128+ state at the draw that element
+ * 64*c of the variable consumes.  One call generates words [c0, c0+n_chunks) and advances
+ * every chunk state by `period` draws via the byte tables built by pgcn_rng_jump_table. */
+int pgcn_rng_jump_table(uint64_t period, void *host_table /* 16*256*16 bytes */);
+int pgcn_dropout_mask(uint64_t *chunk_states, long long n_chunks, long long n_elems,
+                      long long elem0, float p, uint64_t *mask, const void *dev_jump_table,
+                      void *stream);
+/* x[i] *= bit(i) ? scale : 0 for i in [0,n) (also the backward on grads). */
+int pgcn_dropout_apply(float *x, long long n, const uint64_t *mask, float scale, void *stream);
+
+/* --- ReLU (src/module.cu:215-265) ------------------------------------------------------- */
+int pgcn_relu_fwd(float *x, long long n, uint8_t *mask, int training, void *stream);
+int pgcn_relu_bwd(float *g, long long n, const uint8_t *mask, void *stream);
+
+/* --- cross entropy + accuracy (src/module.cu:484-541, src/gcn.cu:264-289) -------------- */
+/* Rows with truth >= 0: logits max-shifted in place; if training grad = (softmax - 1[t])
+ * / count, zero elsewhere.  Writes per-block partial sums (loss, wrong) to `partials`
+ * (>= 2*pgcn_xent_blocks(n) floats); pgcn_finalize reduces them. */
+int pgcn_xent_blocks(int n);
+int pgcn_xent_fwd(float *logits, int ld, float *grad, const int *truth, int n, int c,
+                  int count, int training, float *partials, void *stream);
+/* out4[0] = loss/count + wd*sum(w^2)/2, out4[1] = (count-wrong)/count   (device) */
+int pgcn_finalize(const float *partials, int n_blocks, int count, const float *w_l2,
+                  long long n_l2, float weight_decay, float *out4, void *stream);
+
+/* --- Adam (src/optim.cu:42-95; hpdga optim.cpp:23-35) ---------------------------------- */
+int pgcn_adam(float *w, const float *g, float *m, float *v, long long n, float step_size,
+              float beta1, float beta2, float eps, float weight_decay, int decay, void *stream);
+/* host: lr*sqrtf(1-powf(b2,t))/(1-powf(b1,t)) exactly as hpdga optim.cpp:24 */
+float pgcn_adam_step_size(float lr, float beta1, float beta2, int t);
+
+/* ===================================================================================== */
+/* (2) Engine ABI                                                                          */
+/* ===================================================================================== */
+
+#define PGCN_MAX_LAYERS 16
+
+/* GCNParams + AdamParams (include/gcn.cuh:40-47, include/optim.cuh:16-19) */
+typedef struct {
+  int num_nodes, input_dim, output_dim; /* filled by the loader */
+  int n_layers;                          /* >= 2 */
+  int hidden_dims[PGCN_MAX_LAYERS];      /* n_layers - 1 */
+  float dropouts[PGCN_MAX_LAYERS];       /* n_layers */
+  int epochs, early_stopping;
+  float learning_rate, weight_decay, beta1, beta2, eps;
+} pgcn_params;
+
+/* hpdga defaults: 2 layers, hidden 16, dropout .5/.5, 100 epochs, Adam lr .01, wd 5e-4 */
+void pgcn_params_default(pgcn_params *p);
+
+/* GCNData in host memory (include/gcn.cuh:51-58): CSRs as the hpdga Parser builds them. */
+typedef struct {
+  int num_nodes;
+  const int *graph_indptr, *graph_indices;            /* n+1, nnz */
+  const int *feat_indptr, *feat_indices;              /* n+1, nnz_x */
+  const float *feat_values;                           /* nnz_x */
+  const int *label, *split;                           /* n, n */
+} pgcn_data;
+
+typedef struct pgcn_gcn pgcn_gcn;
+
+/* GCN::GCN (include/gcn.cuh:79) on HIP device `device`. */
+int pgcn_gcn_create(const pgcn_params *p, const pgcn_data *d, int device, pgcn_gcn **out);
+/* Edge-cut variant: this process is rank `rank` of `world` (one process per GPU); the
+ * graph is partitioned into contiguous nnz-balanced node ranges; GraphSum partials are
+ * combined with RCCL reduce-scatter, weight grads and scalars with all-reduce.
+ * `unique_id` = 128 bytes from pgcn_comm_unique_id on rank 0, shared by the caller. */
+int pgcn_comm_unique_id(void *unique_id_128);
+int pgcn_gcn_create_dist(const pgcn_params *p, const pgcn_data *d, int device, int rank,
+                         int world, const void *unique_id_128, pgcn_gcn **out);
+int pgcn_gcn_destroy(pgcn_gcn *g);
+/* GCN::train_epoch / GCN::eval (src/gcn.cu:293-343): out2 = {loss, accuracy} */
+int pgcn_gcn_train_epoch(pgcn_gcn *g, float out2[2]);
+int pgcn_gcn_eval(pgcn_gcn *g, int split, float out2[2]);
+/* One "epoch" as the reference times it (train_epoch + eval(2)) without a host sync;
+ * results land in an on-device ring read by pgcn_gcn_results. */
+int pgcn_gcn_epoch_async(pgcn_gcn *g);
+int pgcn_gcn_sync(pgcn_gcn *g);
+/* copies the last `n` epoch results {train_loss, train_acc, val_loss, val_acc} */
+int pgcn_gcn_results(pgcn_gcn *g, int n, float *host_out);
+/* GCN::run (src/gcn.cu:347-436): prints the reference's epoch lines when verbose */
+int pgcn_gcn_run(pgcn_gcn *g, int verbose);
+/* Variables in reference order (input, then per layer var1, weight, var2; see
+ * include/gcn.cuh:85). which: 0 data, 1 grad. Returns element count (>= 0) or status. For
+ * the edge-cut engine node-sized variables cover this rank's rows only. */
+long long pgcn_gcn_get_var(pgcn_gcn *g, int idx, int which, float *host_dst);
+int pgcn_gcn_num_vars(pgcn_gcn *g);
+/* per-call device timing of the GraphSum kernels (enable before the timed region) */
+int pgcn_gcn_profile(pgcn_gcn *g, int enable);
+int pgcn_gcn_profile_read(pgcn_gcn *g, double *graphsum_ms_total, long long *graphsum_calls,
+                          double *graphsum_bytes_total);
+/* this rank's node range [first, last) (edge-cut engine; whole graph otherwise) */
+int pgcn_gcn_node_range(pgcn_gcn *g, int *first, int *last);
+
+/* --- data (kept hpdga loader + synthetic inputs) ---------------------------------------- */
+typedef struct pgcn_dataset pgcn_dataset;
+/* Parser(GCNParams*, GCNData*, name).parse(): reads data/<name>.{graph,split,svmlight}
+ * under `root` with hpdga-spring23/src/parser.cpp:6-140 semantics. */
+int pgcn_dataset_load(const char *root, const char *name, pgcn_dataset **out);
+/* Seeded reddit-shaped synthetic: n nodes, f dense features, c classes,
+ * Chung-Lu power-law undirected graph with `undirected_edges` edges (2x directed slots). */
+int pgcn_dataset_synthetic(int n, int f, int c, long long undirected_edges, uint64_t seed,
+                           pgcn_dataset **out);
+int pgcn_dataset_view(const pgcn_dataset *ds, pgcn_data *view, int *input_dim, int *output_dim);
+int pgcn_dataset_free(pgcn_dataset *ds);
+
+/* --- edge-cut partition plan (host only; no device needed) ------------------------------ */
+/* contiguous nnz-balanced node ranges: bounds_out[world+1], padded rows per rank */
+int pgcn_partition_bounds(int n, const int *indptr, int world, int *bounds_out, int *maxrows);
+/* rank's column block of Â in padded row layout (world*maxrows rows, local column ids,
+ * global coefficients). Returns nnz (call with null arrays to size them) or a status < 0. */
+long long pgcn_partition_subgraph(int n, const int *indptr, const int *indices, int world,
+                                  int rank, int *sub_indptr, int *sub_indices, float *sub_vals);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PGCN_H */

@@ -1,0 +1,352 @@
+"""parallel-gcn_amd -- Python host glue for the MI355X GCN engine (libpgcn.so).
+
+The product is C++/HIP: kernels + host classes behind the C ABI in include/pgcn.h.  This
+module only binds that ABI with ctypes so tests, bench.py and __graft_entry__ can drive it;
+it mirrors the reference's host interface for the path (src/main.cpp:9-61,
+include/gcn.cuh:79-122): load a dataset with the kept hpdga Parser, build a GCN, call
+train_epoch() / eval(split) / run().
+
+There is no CPU fallback: importing this module without the built library raises, and
+creating an engine without a HIP device raises PgcnError(PGCN_E_NODEVICE).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libpgcn.so")
+
+PGCN_OK = 0
+PGCN_E_INVALID = -1
+PGCN_E_NOMEM = -2
+PGCN_E_IO = -3
+PGCN_E_COMM = -4
+PGCN_E_NODEVICE = -5
+MAX_LAYERS = 16
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"{LIB_PATH} is not built: run `make -C parallel-gcn_amd` "
+                      "(or __graft_entry__.build()); there is no fallback path")
+lib = ctypes.CDLL(LIB_PATH)
+
+c_int, c_ll, c_float, c_void_p = ctypes.c_int, ctypes.c_longlong, ctypes.c_float, ctypes.c_void_p
+c_size_t, c_u64, c_double = ctypes.c_size_t, ctypes.c_uint64, ctypes.c_double
+P = ctypes.POINTER
+
+
+class PgcnParams(ctypes.Structure):
+    _fields_ = [("num_nodes", c_int), ("input_dim", c_int), ("output_dim", c_int),
+                ("n_layers", c_int), ("hidden_dims", c_int * MAX_LAYERS),
+                ("dropouts", c_float * MAX_LAYERS), ("epochs", c_int), ("early_stopping", c_int),
+                ("learning_rate", c_float), ("weight_decay", c_float), ("beta1", c_float),
+                ("beta2", c_float), ("eps", c_float)]
+
+
+class PgcnData(ctypes.Structure):
+    _fields_ = [("num_nodes", c_int), ("graph_indptr", P(c_int)), ("graph_indices", P(c_int)),
+                ("feat_indptr", P(c_int)), ("feat_indices", P(c_int)),
+                ("feat_values", P(c_float)), ("label", P(c_int)), ("split", P(c_int))]
+
+
+def _sig(name, res, *args):
+    f = getattr(lib, name)
+    f.restype = res
+    f.argtypes = list(args)
+    return f
+
+
+_sig("pgcn_status_string", ctypes.c_char_p, c_int)
+_sig("pgcn_version", c_int)
+_sig("pgcn_rng_seed", None, P(c_u64))
+_sig("pgcn_rng_jump", None, P(c_u64), c_u64)
+_sig("pgcn_rng_jump_table", c_int, c_u64, c_void_p)
+_sig("pgcn_graph_create", c_int, c_int, c_void_p, c_void_p, P(c_void_p))
+_sig("pgcn_graph_destroy", c_int, c_void_p)
+_sig("pgcn_graph_nnz", c_ll, c_void_p)
+_sig("pgcn_graphsum", c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p)
+_sig("pgcn_gemm", c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p,
+     c_int, c_void_p, c_ll, c_ll, c_float, c_void_p)
+_sig("pgcn_gemm_tn_workspace", c_size_t, c_int, c_int, c_int)
+_sig("pgcn_gemm_tn", c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p,
+     c_int, c_void_p, c_ll, c_ll, c_float, c_void_p, c_void_p)
+_sig("pgcn_spmm_csr", c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_float,
+     c_void_p, c_void_p, c_void_p)
+_sig("pgcn_spmm_csc_bwd", c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+     c_float, c_void_p, c_void_p, c_void_p)
+_sig("pgcn_csr_transpose", c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p)
+_sig("pgcn_dropout_mask", c_int, c_void_p, c_ll, c_ll, c_ll, c_float, c_void_p, c_void_p, c_void_p)
+_sig("pgcn_dropout_apply", c_int, c_void_p, c_ll, c_void_p, c_float, c_void_p)
+_sig("pgcn_relu_fwd", c_int, c_void_p, c_ll, c_void_p, c_int, c_void_p)
+_sig("pgcn_relu_bwd", c_int, c_void_p, c_ll, c_void_p, c_void_p)
+_sig("pgcn_xent_blocks", c_int, c_int)
+_sig("pgcn_xent_fwd", c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+     c_void_p, c_void_p)
+_sig("pgcn_finalize", c_int, c_void_p, c_int, c_int, c_void_p, c_ll, c_float, c_void_p, c_void_p)
+_sig("pgcn_adam", c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_ll, c_float, c_float, c_float,
+     c_float, c_float, c_int, c_void_p)
+_sig("pgcn_adam_step_size", c_float, c_float, c_float, c_float, c_int)
+_sig("pgcn_params_default", None, P(PgcnParams))
+_sig("pgcn_gcn_create", c_int, P(PgcnParams), P(PgcnData), c_int, P(c_void_p))
+_sig("pgcn_comm_unique_id", c_int, c_void_p)
+_sig("pgcn_gcn_create_dist", c_int, P(PgcnParams), P(PgcnData), c_int, c_int, c_int, c_void_p,
+     P(c_void_p))
+_sig("pgcn_gcn_destroy", c_int, c_void_p)
+_sig("pgcn_gcn_train_epoch", c_int, c_void_p, P(c_float))
+_sig("pgcn_gcn_eval", c_int, c_void_p, c_int, P(c_float))
+_sig("pgcn_gcn_epoch_async", c_int, c_void_p)
+_sig("pgcn_gcn_sync", c_int, c_void_p)
+_sig("pgcn_gcn_results", c_int, c_void_p, c_int, P(c_float))
+_sig("pgcn_gcn_run", c_int, c_void_p, c_int)
+_sig("pgcn_gcn_get_var", c_ll, c_void_p, c_int, c_int, P(c_float))
+_sig("pgcn_gcn_num_vars", c_int, c_void_p)
+_sig("pgcn_gcn_profile", c_int, c_void_p, c_int)
+_sig("pgcn_gcn_profile_read", c_int, c_void_p, P(c_double), P(c_ll), P(c_double))
+_sig("pgcn_gcn_node_range", c_int, c_void_p, P(c_int), P(c_int))
+_sig("pgcn_dataset_load", c_int, ctypes.c_char_p, ctypes.c_char_p, P(c_void_p))
+_sig("pgcn_dataset_synthetic", c_int, c_int, c_int, c_int, c_ll, c_u64, P(c_void_p))
+_sig("pgcn_dataset_view", c_int, c_void_p, P(PgcnData), P(c_int), P(c_int))
+_sig("pgcn_dataset_free", c_int, c_void_p)
+_sig("pgcn_partition_bounds", c_int, c_int, c_void_p, c_int, c_void_p, P(c_int))
+_sig("pgcn_partition_subgraph", c_ll, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p,
+     c_void_p, c_void_p)
+
+
+class PgcnError(RuntimeError):
+    def __init__(self, status, where=""):
+        self.status = status
+        super().__init__(f"{where}: {lib.pgcn_status_string(status).decode()} ({status})")
+
+
+def check(status, where=""):
+    if status != PGCN_OK:
+        raise PgcnError(status, where)
+    return status
+
+
+def _ptr(a):
+    return a.ctypes.data_as(c_void_p)
+
+
+# --------------------------------------------------------------------------- data
+class Dataset:
+    """GCNData (include/gcn.cuh:51-58) owned by libpgcn: the hpdga loader or the synthetic
+    reddit-shaped generator.  Arrays are exposed as zero-copy numpy views."""
+
+    def __init__(self, handle):
+        self._h = c_void_p(handle)
+        self.view = PgcnData()
+        fi, fo = c_int(), c_int()
+        check(lib.pgcn_dataset_view(self._h, ctypes.byref(self.view), ctypes.byref(fi),
+                                    ctypes.byref(fo)), "dataset_view")
+        self.input_dim, self.output_dim = fi.value, fo.value
+        self.num_nodes = self.view.num_nodes
+        n = self.num_nodes
+
+        def arr(p, count, dt):
+            if count == 0:
+                return np.zeros(0, dt)
+            return np.ctypeslib.as_array(ctypes.cast(p, P(ctypes.c_int if dt == np.int32 else c_float)),
+                                         shape=(count,))
+        self.graph_indptr = arr(self.view.graph_indptr, n + 1, np.int32)
+        self.graph_indices = arr(self.view.graph_indices, int(self.graph_indptr[-1]), np.int32)
+        self.feat_indptr = arr(self.view.feat_indptr, n + 1, np.int32)
+        nnzx = int(self.feat_indptr[-1])
+        self.feat_indices = arr(self.view.feat_indices, nnzx, np.int32)
+        self.feat_values = arr(self.view.feat_values, nnzx, np.float32)
+        self.label = arr(self.view.label, n, np.int32)
+        self.split = arr(self.view.split, n, np.int32)
+
+    @staticmethod
+    def load(root, name):
+        """Parser(&params, &data, name).parse() with data/<name>.* under root."""
+        h = c_void_p()
+        check(lib.pgcn_dataset_load(root.encode(), name.encode(), ctypes.byref(h)),
+              f"Cannot read input: {name}")
+        return Dataset(h.value)
+
+    @staticmethod
+    def synthetic(n, f, c, undirected_edges, seed=1):
+        h = c_void_p()
+        check(lib.pgcn_dataset_synthetic(n, f, c, undirected_edges, seed, ctypes.byref(h)),
+              "dataset_synthetic")
+        return Dataset(h.value)
+
+    def __del__(self):
+        if getattr(self, "_h", None) and self._h.value:
+            lib.pgcn_dataset_free(self._h)
+            self._h = c_void_p()
+
+
+def make_params(ds, hidden_dims=(16,), dropouts=(0.5, 0.5), epochs=100, early_stopping=0,
+                learning_rate=0.01, weight_decay=5e-4, beta1=0.9, beta2=0.999, eps=1e-8):
+    p = PgcnParams()
+    lib.pgcn_params_default(ctypes.byref(p))
+    p.num_nodes, p.input_dim, p.output_dim = ds.num_nodes, ds.input_dim, ds.output_dim
+    p.n_layers = len(hidden_dims) + 1
+    assert len(dropouts) == p.n_layers
+    for i, h in enumerate(hidden_dims):
+        p.hidden_dims[i] = h
+    for i, d in enumerate(dropouts):
+        p.dropouts[i] = d
+    p.epochs, p.early_stopping = epochs, early_stopping
+    p.learning_rate, p.weight_decay, p.beta1, p.beta2, p.eps = (learning_rate, weight_decay,
+                                                               beta1, beta2, eps)
+    return p
+
+
+# --------------------------------------------------------------------------- engine
+class GCN:
+    """GCN(params, data) of include/gcn.cuh:79-122 on one GPU, or the edge-cut variant when
+    rank/world/unique_id are given (one process per GPU)."""
+
+    def __init__(self, params, ds, device=0, rank=None, world=None, unique_id=None):
+        self.ds = ds  # keep the host data alive while the engine is built
+        h = c_void_p()
+        if world is None:
+            check(lib.pgcn_gcn_create(ctypes.byref(params), ctypes.byref(ds.view), device,
+                                      ctypes.byref(h)), "gcn_create")
+        else:
+            uid = ctypes.create_string_buffer(bytes(unique_id), 128)
+            check(lib.pgcn_gcn_create_dist(ctypes.byref(params), ctypes.byref(ds.view), device,
+                                           rank, world, uid, ctypes.byref(h)), "gcn_create_dist")
+        self._h = h
+        self.params = params
+
+    def train_epoch(self):
+        out = (c_float * 2)()
+        check(lib.pgcn_gcn_train_epoch(self._h, out), "train_epoch")
+        return out[0], out[1]
+
+    def eval(self, split):
+        out = (c_float * 2)()
+        check(lib.pgcn_gcn_eval(self._h, split, out), "eval")
+        return out[0], out[1]
+
+    def epoch_async(self):
+        check(lib.pgcn_gcn_epoch_async(self._h), "epoch_async")
+
+    def sync(self):
+        check(lib.pgcn_gcn_sync(self._h), "sync")
+
+    def results(self, n):
+        out = np.zeros(4 * n, np.float32)
+        check(lib.pgcn_gcn_results(self._h, n, out.ctypes.data_as(P(c_float))), "results")
+        return out.reshape(n, 4)
+
+    def run(self, verbose=True):
+        check(lib.pgcn_gcn_run(self._h, 1 if verbose else 0), "run")
+
+    def num_vars(self):
+        return lib.pgcn_gcn_num_vars(self._h)
+
+    def get_var(self, idx, which=0):
+        n = lib.pgcn_gcn_get_var(self._h, idx, which, None)
+        if n < 0:
+            raise PgcnError(int(n), "get_var")
+        out = np.zeros(n, np.float32)
+        if n:
+            lib.pgcn_gcn_get_var(self._h, idx, which, out.ctypes.data_as(P(c_float)))
+        return out
+
+    def profile(self, on):
+        check(lib.pgcn_gcn_profile(self._h, 1 if on else 0), "profile")
+
+    def profile_read(self):
+        ms, calls, byts = c_double(), c_ll(), c_double()
+        check(lib.pgcn_gcn_profile_read(self._h, ctypes.byref(ms), ctypes.byref(calls),
+                                        ctypes.byref(byts)), "profile_read")
+        return ms.value, calls.value, byts.value
+
+    def node_range(self):
+        a, b = c_int(), c_int()
+        lib.pgcn_gcn_node_range(self._h, ctypes.byref(a), ctypes.byref(b))
+        return a.value, b.value
+
+    def close(self):
+        if self._h and self._h.value:
+            lib.pgcn_gcn_destroy(self._h)
+            self._h = c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def comm_unique_id():
+    buf = ctypes.create_string_buffer(128)
+    check(lib.pgcn_comm_unique_id(buf), "comm_unique_id")
+    return buf.raw
+
+
+# --------------------------------------------------------------------------- host helpers
+def rng_seed():
+    s = (c_u64 * 2)()
+    lib.pgcn_rng_seed(s)
+    return np.array([s[0], s[1]], np.uint64)
+
+
+def rng_jump(state, k):
+    s = (c_u64 * 2)(int(state[0]), int(state[1]))
+    lib.pgcn_rng_jump(s, int(k))
+    return np.array([s[0], s[1]], np.uint64)
+
+
+def rng_jump_table(period):
+    t = np.zeros(16 * 256 * 2, np.uint64)
+    check(lib.pgcn_rng_jump_table(int(period), _ptr(t)), "rng_jump_table")
+    return t
+
+
+def partition_bounds(indptr, world):
+    indptr = np.ascontiguousarray(indptr, np.int32)
+    b = np.zeros(world + 1, np.int32)
+    mr = c_int()
+    check(lib.pgcn_partition_bounds(len(indptr) - 1, _ptr(indptr), world, _ptr(b),
+                                    ctypes.byref(mr)), "partition_bounds")
+    return b, mr.value
+
+
+def partition_subgraph(indptr, indices, world, rank):
+    indptr = np.ascontiguousarray(indptr, np.int32)
+    indices = np.ascontiguousarray(indices, np.int32)
+    n = len(indptr) - 1
+    _, maxrows = partition_bounds(indptr, world)
+    nnz = lib.pgcn_partition_subgraph(n, _ptr(indptr), _ptr(indices), world, rank, None, None, None)
+    if nnz < 0:
+        raise PgcnError(int(nnz), "partition_subgraph")
+    sp = np.zeros(world * maxrows + 1, np.int32)
+    si = np.zeros(max(nnz, 1), np.int32)
+    sv = np.zeros(max(nnz, 1), np.float32)
+    lib.pgcn_partition_subgraph(n, _ptr(indptr), _ptr(indices), world, rank, _ptr(sp), _ptr(si),
+                                _ptr(sv))
+    return sp, si[:nnz], sv[:nnz]
+
+
+def csr_transpose(indptr, indices, n_cols):
+    indptr = np.ascontiguousarray(indptr, np.int32)
+    indices = np.ascontiguousarray(indices, np.int32)
+    m, nnz = len(indptr) - 1, int(indptr[-1])
+    cp = np.zeros(n_cols + 1, np.int32)
+    cr = np.zeros(max(nnz, 1), np.int32)
+    cpos = np.zeros(max(nnz, 1), np.int32)
+    check(lib.pgcn_csr_transpose(m, n_cols, _ptr(indptr), _ptr(indices), _ptr(cp), _ptr(cr),
+                                 _ptr(cpos)), "csr_transpose")
+    return cp, cr[:nnz], cpos[:nnz]
+
+
+EXPORTED = [
+    "pgcn_status_string", "pgcn_version", "pgcn_rng_seed", "pgcn_rng_jump", "pgcn_graph_create",
+    "pgcn_graph_destroy", "pgcn_graph_nnz", "pgcn_graphsum", "pgcn_gemm", "pgcn_gemm_tn_workspace",
+    "pgcn_gemm_tn", "pgcn_spmm_csr", "pgcn_spmm_csc_bwd", "pgcn_csr_transpose",
+    "pgcn_rng_jump_table", "pgcn_dropout_mask", "pgcn_dropout_apply", "pgcn_relu_fwd",
+    "pgcn_relu_bwd", "pgcn_xent_blocks", "pgcn_xent_fwd", "pgcn_finalize", "pgcn_adam",
+    "pgcn_adam_step_size", "pgcn_params_default", "pgcn_gcn_create", "pgcn_comm_unique_id",
+    "pgcn_gcn_create_dist", "pgcn_gcn_destroy", "pgcn_gcn_train_epoch", "pgcn_gcn_eval",
+    "pgcn_gcn_epoch_async", "pgcn_gcn_sync", "pgcn_gcn_results", "pgcn_gcn_run",
+    "pgcn_gcn_get_var", "pgcn_gcn_num_vars", "pgcn_gcn_profile", "pgcn_gcn_profile_read",
+    "pgcn_gcn_node_range", "pgcn_dataset_load", "pgcn_dataset_synthetic", "pgcn_dataset_view",
+    "pgcn_dataset_free", "pgcn_partition_bounds", "pgcn_partition_subgraph",
+]

@@ -1,0 +1,401 @@
+// parallel-gcn_amd/csrc/capi.cpp -- the extern "C" boundary declared in include/pgcn.h.
+#include <cstring>
+#include <memory>
+
+#include "../../include/pgcn.h"
+#include "common.hpp"
+#include "host/comm.hpp"
+#include "host/data.hpp"
+#include "host/gcn.hpp"
+#include "host/graph.hpp"
+#include "kernels.hpp"
+
+using namespace pgcn;
+
+struct pgcn_graph {
+  std::unique_ptr<DevGraph> g;
+};
+struct pgcn_gcn {
+  std::unique_ptr<GCN> g;
+};
+struct pgcn_dataset {
+  GCNData d;
+};
+
+namespace {
+void check_device() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+    throw Error(PGCN_E_NODEVICE, "no HIP device visible: the engine has no CPU fallback");
+}
+
+GCNParams to_params(const pgcn_params *p, const pgcn_data *d) {
+  GCNParams q;
+  q.num_nodes = d->num_nodes;
+  q.input_dim = p->input_dim;
+  q.output_dim = p->output_dim;
+  q.n_layers = p->n_layers;
+  q.hidden_dims.assign(p->hidden_dims, p->hidden_dims + std::max(0, p->n_layers - 1));
+  q.dropouts.assign(p->dropouts, p->dropouts + std::max(0, p->n_layers));
+  q.epochs = p->epochs;
+  q.early_stopping = p->early_stopping;
+  return q;
+}
+AdamParams to_adam(const pgcn_params *p) {
+  AdamParams a;
+  a.learning_rate = p->learning_rate;
+  a.weight_decay = p->weight_decay;
+  a.beta1 = p->beta1;
+  a.beta2 = p->beta2;
+  a.eps = p->eps;
+  return a;
+}
+// GCNData view -> owned GCNData (the engine uploads from it once)
+GCNData to_data(const pgcn_data *d, const pgcn_params *p) {
+  GCNData g;
+  const int n = d->num_nodes;
+  g.num_nodes = n;
+  g.input_dim = p->input_dim;
+  g.output_dim = p->output_dim;
+  g.graph.indptr.assign(d->graph_indptr, d->graph_indptr + n + 1);
+  g.graph.indices.assign(d->graph_indices, d->graph_indices + d->graph_indptr[n]);
+  g.feature_index.indptr.assign(d->feat_indptr, d->feat_indptr + n + 1);
+  g.feature_index.indices.assign(d->feat_indices, d->feat_indices + d->feat_indptr[n]);
+  g.feature_value.assign(d->feat_values, d->feat_values + d->feat_indptr[n]);
+  g.label.assign(d->label, d->label + n);
+  g.split.assign(d->split, d->split + n);
+  return g;
+}
+}  // namespace
+
+extern "C" {
+
+const char *pgcn_status_string(int s) {
+  switch (s) {
+    case PGCN_OK: return "ok";
+    case PGCN_E_INVALID: return "invalid argument";
+    case PGCN_E_NOMEM: return "out of device memory";
+    case PGCN_E_IO: return "cannot read input";
+    case PGCN_E_COMM: return "RCCL error";
+    case PGCN_E_NODEVICE: return "no HIP device";
+    default: return s > 0 ? hipGetErrorString((hipError_t)s) : "unknown";
+  }
+}
+
+int pgcn_version(void) { return 100; }
+
+// ---------------------------------------------------------------- graph + kernels
+int pgcn_graph_create(int n, const int *indptr, const int *indices, pgcn_graph **out) {
+  return guarded([&] {
+    PGCN_CHECK(n > 0 && indptr && indices && out, PGCN_E_INVALID, "graph_create args");
+    check_device();
+    std::vector<float> v = graph_coefs(n, indptr, indices);
+    auto h = std::make_unique<pgcn_graph>();
+    h->g = std::make_unique<DevGraph>(n, indptr, indices, v.data());
+    *out = h.release();
+  });
+}
+int pgcn_graph_destroy(pgcn_graph *g) {
+  delete g;
+  return PGCN_OK;
+}
+long long pgcn_graph_nnz(const pgcn_graph *g) { return g ? g->g->nnz() : -1; }
+
+int pgcn_graphsum(const pgcn_graph *g, const float *in, int ld_in, float *out, int ld_out,
+                  int dim, void *stream) {
+  return guarded([&] {
+    PGCN_CHECK(g && in && out && dim > 0, PGCN_E_INVALID, "graphsum args");
+    g->g->graphsum(in, ld_in, out, ld_out, dim, as_stream(stream));
+    PGCN_HIP(hipGetLastError());
+  });
+}
+
+int pgcn_gemm(int M, int N, int K, const float *A, int lda, const float *B, int ldb, int trans_b,
+              float *C, int ldc, const uint64_t *a_mask, long long mask_base, long long mask_ld,
+              float a_scale, void *stream) {
+  return guarded([&] {
+    PGCN_CHECK(A && B && C && M >= 0 && K > 0 && ldc >= N, PGCN_E_INVALID, "gemm args");
+    launch_gemm_nn(M, N, K, A, lda, B, ldb, trans_b, C, ldc, a_mask, mask_base, mask_ld, a_scale,
+                   as_stream(stream));
+    PGCN_HIP(hipGetLastError());
+  });
+}
+
+size_t pgcn_gemm_tn_workspace(int M, int N, int K) { return gemm_tn_workspace(M, N, K); }
+
+int pgcn_gemm_tn(int M, int N, int K, const float *A, int lda, const float *G, int ldg, float *C,
+                 int ldc, const uint64_t *a_mask, long long mask_base, long long mask_ld,
+                 float a_scale, void *workspace, void *stream) {
+  return guarded([&] {
+    PGCN_CHECK(A && G && C && workspace && K > 0 && ldc >= N, PGCN_E_INVALID, "gemm_tn args");
+    launch_gemm_tn(M, N, K, A, lda, G, ldg, C, ldc, a_mask, mask_base, mask_ld, a_scale,
+                   workspace, as_stream(stream));
+    PGCN_HIP(hipGetLastError());
+  });
+}
+
+int pgcn_spmm_csr(int m, int p, const int *indptr, const int *indices, const float *a,
+                  const uint64_t *a_mask, float a_scale, const float *b, float *c, void *stream) {
+  return guarded([&] {
+    launch_spmm_csr(m, p, p, indptr, indices, a, a_mask, 0, a_scale, b, c, as_stream(stream));
+    PGCN_HIP(hipGetLastError());
+  });
+}
+
+int pgcn_spmm_csc_bwd(int nf, int p, const int *csc_ptr, const int *csc_row, const int *csc_pos,
+                      const float *a, const uint64_t *a_mask, float a_scale, const float *cgrad,
+                      float *bgrad, void *stream) {
+  return guarded([&] {
+    launch_spmm_csc_bwd(nf, p, p, csc_ptr, csc_row, csc_pos, a, a_mask, 0, a_scale, cgrad, bgrad,
+                        as_stream(stream));
+    PGCN_HIP(hipGetLastError());
+  });
+}
+
+int pgcn_csr_transpose(int m, int n_cols, const int *indptr, const int *indices, int *csc_ptr,
+                       int *csc_row, int *csc_pos) {
+  return guarded([&] {
+    std::memset(csc_ptr, 0, sizeof(int) * (size_t)(n_cols + 1));
+    for (int k = 0; k < indptr[m]; k++) {
+      PGCN_CHECK(indices[k] >= 0 && indices[k] < n_cols, PGCN_E_INVALID, "column id");
+      csc_ptr[indices[k] + 1]++;
+    }
+    for (int f = 0; f < n_cols; f++) csc_ptr[f + 1] += csc_ptr[f];
+    std::vector<int> fill(csc_ptr, csc_ptr + n_cols);
+    for (int i = 0; i < m; i++)
+      for (int k = indptr[i]; k < indptr[i + 1]; k++) {
+        const int o = fill[(size_t)indices[k]]++;
+        csc_row[o] = i;
+        csc_pos[o] = k;
+      }
+  });
+}
+
+int pgcn_dropout_mask(uint64_t *chunk_states, long long n_chunks, long long n_elems,
+                      long long elem0, float p, uint64_t *mask, const void *dev_jump_table,
+                      void *stream) {
+  return guarded([&] {
+    launch_dropout_mask(chunk_states, n_chunks, elem0, n_elems, p, mask, dev_jump_table,
+                        as_stream(stream));
+    PGCN_HIP(hipGetLastError());
+  });
+}
+
+int pgcn_dropout_apply(float *x, long long n, const uint64_t *mask, float scale, void *stream) {
+  return guarded([&] {
+    launch_dropout_apply_based(x, n, mask, 0, scale, as_stream(stream));
+    PGCN_HIP(hipGetLastError());
+  });
+}
+
+int pgcn_relu_fwd(float *x, long long n, uint8_t *mask, int training, void *stream) {
+  return guarded([&] { launch_relu_fwd(x, n, mask, training, as_stream(stream)); });
+}
+int pgcn_relu_bwd(float *g, long long n, const uint8_t *mask, void *stream) {
+  return guarded([&] { launch_relu_bwd(g, n, mask, as_stream(stream)); });
+}
+
+int pgcn_xent_blocks(int n) { return xent_blocks(n); }
+
+int pgcn_xent_fwd(float *logits, int ld, float *grad, const int *truth, int n, int c, int count,
+                  int training, float *partials, void *stream) {
+  return guarded([&] {
+    launch_xent_fwd(logits, ld, grad, truth, n, c, count, training, partials, as_stream(stream));
+    PGCN_HIP(hipGetLastError());
+  });
+}
+
+int pgcn_finalize(const float *partials, int n_blocks, int count, const float *w_l2,
+                  long long n_l2, float weight_decay, float *out4, void *stream) {
+  return guarded([&] {
+    // out4[0..1] = {loss, acc}; out4[2..3] hold the raw sums (loss_sum, wrong)
+    launch_reduce_scalars(partials, n_blocks, w_l2, n_l2, out4 + 2, as_stream(stream));
+    launch_compose(out4 + 2, count, weight_decay, out4, as_stream(stream));
+  });
+}
+
+int pgcn_adam(float *w, const float *g, float *m, float *v, long long n, float step_size,
+              float beta1, float beta2, float eps, float weight_decay, int decay, void *stream) {
+  return guarded([&] {
+    launch_adam(w, g, m, v, n, step_size, beta1, beta2, eps, weight_decay, decay,
+                as_stream(stream));
+  });
+}
+
+float pgcn_adam_step_size(float lr, float beta1, float beta2, int t) {
+  return lr * sqrtf(1.0f - powf(beta2, (float)t)) / (1.0f - powf(beta1, (float)t));
+}
+
+// ---------------------------------------------------------------- engine
+void pgcn_params_default(pgcn_params *p) {
+  std::memset(p, 0, sizeof *p);
+  p->n_layers = 2;
+  p->hidden_dims[0] = 16;
+  p->dropouts[0] = 0.5f;
+  p->dropouts[1] = 0.5f;
+  p->epochs = 100;
+  p->early_stopping = 0;
+  p->learning_rate = 0.01f;
+  p->weight_decay = 5e-4f;
+  p->beta1 = 0.9f;
+  p->beta2 = 0.999f;
+  p->eps = 1e-8f;
+}
+
+int pgcn_gcn_create(const pgcn_params *p, const pgcn_data *d, int device, pgcn_gcn **out) {
+  return guarded([&] {
+    PGCN_CHECK(p && d && out, PGCN_E_INVALID, "gcn_create args");
+    check_device();
+    GCNData data = to_data(d, p);
+    auto h = std::make_unique<pgcn_gcn>();
+    h->g = std::make_unique<GCN>(to_params(p, d), to_adam(p), data, device, nullptr);
+    *out = h.release();
+  });
+}
+
+int pgcn_comm_unique_id(void *uid) {
+  return guarded([&] { Comm::unique_id(uid); });
+}
+
+int pgcn_gcn_create_dist(const pgcn_params *p, const pgcn_data *d, int device, int rank,
+                         int world, const void *uid, pgcn_gcn **out) {
+  return guarded([&] {
+    PGCN_CHECK(p && d && out && uid, PGCN_E_INVALID, "gcn_create_dist args");
+    check_device();
+    GCNData data = to_data(d, p);
+    DistSpec ds;
+    ds.rank = rank;
+    ds.world = world;
+    ds.unique_id = uid;
+    auto h = std::make_unique<pgcn_gcn>();
+    h->g = std::make_unique<GCN>(to_params(p, d), to_adam(p), data, device, &ds);
+    *out = h.release();
+  });
+}
+
+int pgcn_gcn_destroy(pgcn_gcn *g) {
+  delete g;
+  return PGCN_OK;
+}
+
+int pgcn_gcn_train_epoch(pgcn_gcn *g, float out2[2]) {
+  return guarded([&] {
+    auto r = g->g->train_epoch();
+    out2[0] = r.first;
+    out2[1] = r.second;
+  });
+}
+
+int pgcn_gcn_eval(pgcn_gcn *g, int split, float out2[2]) {
+  return guarded([&] {
+    auto r = g->g->eval(split);
+    out2[0] = r.first;
+    out2[1] = r.second;
+  });
+}
+
+int pgcn_gcn_epoch_async(pgcn_gcn *g) {
+  return guarded([&] { g->g->epoch_async(); });
+}
+int pgcn_gcn_sync(pgcn_gcn *g) {
+  return guarded([&] { g->g->sync(); });
+}
+int pgcn_gcn_results(pgcn_gcn *g, int n, float *host_out) {
+  return guarded([&] {
+    auto r = g->g->results(n);
+    std::memcpy(host_out, r.data(), r.size() * sizeof(float));
+  });
+}
+int pgcn_gcn_run(pgcn_gcn *g, int verbose) {
+  return guarded([&] { g->g->run(verbose != 0); });
+}
+long long pgcn_gcn_get_var(pgcn_gcn *g, int idx, int which, float *dst) {
+  long long n = -1;
+  const int st = guarded([&] {
+    auto v = g->g->get_var(idx, which);
+    if (dst && !v.empty()) std::memcpy(dst, v.data(), v.size() * sizeof(float));
+    n = (long long)v.size();
+  });
+  return st == PGCN_OK ? n : st;
+}
+int pgcn_gcn_num_vars(pgcn_gcn *g) { return g->g->num_vars(); }
+int pgcn_gcn_profile(pgcn_gcn *g, int enable) {
+  return guarded([&] { g->g->set_profile(enable != 0); });
+}
+int pgcn_gcn_profile_read(pgcn_gcn *g, double *ms, long long *calls, double *bytes) {
+  return guarded([&] { g->g->profile_read(ms, calls, bytes); });
+}
+int pgcn_gcn_node_range(pgcn_gcn *g, int *first, int *last) {
+  *first = g->g->partition().first();
+  *last = g->g->partition().last();
+  return PGCN_OK;
+}
+
+// ---------------------------------------------------------------- data
+int pgcn_dataset_load(const char *root, const char *name, pgcn_dataset **out) {
+  return guarded([&] {
+    auto h = std::make_unique<pgcn_dataset>();
+    Parser parser(&h->d, name, root ? root : ".");
+    if (!parser.parse()) throw Error(PGCN_E_IO, std::string("Cannot read input: ") + name);
+    *out = h.release();
+  });
+}
+
+int pgcn_dataset_synthetic(int n, int f, int c, long long undirected_edges, uint64_t seed,
+                           pgcn_dataset **out) {
+  return guarded([&] {
+    PGCN_CHECK(n > 1 && f > 0 && c > 0 && undirected_edges >= 0, PGCN_E_INVALID, "synthetic args");
+    auto h = std::make_unique<pgcn_dataset>();
+    make_synthetic(&h->d, n, f, c, undirected_edges, seed);
+    *out = h.release();
+  });
+}
+
+int pgcn_dataset_view(const pgcn_dataset *ds, pgcn_data *v, int *input_dim, int *output_dim) {
+  if (!ds || !v) return PGCN_E_INVALID;
+  v->num_nodes = ds->d.num_nodes;
+  v->graph_indptr = ds->d.graph.indptr.data();
+  v->graph_indices = ds->d.graph.indices.data();
+  v->feat_indptr = ds->d.feature_index.indptr.data();
+  v->feat_indices = ds->d.feature_index.indices.data();
+  v->feat_values = ds->d.feature_value.data();
+  v->label = ds->d.label.data();
+  v->split = ds->d.split.data();
+  if (input_dim) *input_dim = ds->d.input_dim;
+  if (output_dim) *output_dim = ds->d.output_dim;
+  return PGCN_OK;
+}
+
+int pgcn_dataset_free(pgcn_dataset *ds) {
+  delete ds;
+  return PGCN_OK;
+}
+
+// ---------------------------------------------------------------- partition (host only)
+int pgcn_partition_bounds(int n, const int *indptr, int world, int *bounds_out, int *maxrows) {
+  return guarded([&] {
+    Partition p = make_partition(n, indptr, world, 0);
+    std::memcpy(bounds_out, p.bounds.data(), sizeof(int) * (size_t)(world + 1));
+    if (maxrows) *maxrows = p.maxrows;
+  });
+}
+
+// Rank `rank`'s column block in the padded row layout (sizes: call with null arrays first
+// to get nnz; indptr needs world*maxrows+1 entries).
+long long pgcn_partition_subgraph(int n, const int *indptr, const int *indices, int world,
+                                  int rank, int *sub_indptr, int *sub_indices, float *sub_vals) {
+  long long nnz = -1;
+  const int st = guarded([&] {
+    Partition p = make_partition(n, indptr, world, rank);
+    std::vector<int> sp, si;
+    std::vector<float> sv;
+    partition_subgraph(p, n, indptr, indices, &sp, &si, &sv);
+    nnz = (long long)si.size();
+    if (sub_indptr) std::memcpy(sub_indptr, sp.data(), sp.size() * sizeof(int));
+    if (sub_indices) std::memcpy(sub_indices, si.data(), si.size() * sizeof(int));
+    if (sub_vals) std::memcpy(sub_vals, sv.data(), sv.size() * sizeof(float));
+  });
+  return st == PGCN_OK ? nnz : st;
+}
+
+}  // extern "C"

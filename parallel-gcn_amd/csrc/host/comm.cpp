@@ -1,0 +1,115 @@
+// parallel-gcn_amd/csrc/host/comm.cpp
+#include "comm.hpp"
+
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+
+#include "../common.hpp"
+#include "graph.hpp"
+
+namespace pgcn {
+
+int Partition::owner(int node) const {
+  return (int)(std::upper_bound(bounds.begin(), bounds.end(), node) - bounds.begin()) - 1;
+}
+
+Partition make_partition(int n, const int *indptr, int world, int rank) {
+  PGCN_CHECK(world >= 1 && rank >= 0 && rank < world && n >= world, PGCN_E_INVALID,
+             "partition: need 1 <= world <= n and 0 <= rank < world");
+  Partition p;
+  p.world = world;
+  p.rank = rank;
+  p.bounds.assign((size_t)world + 1, 0);
+  p.bounds[(size_t)world] = n;
+  const double total = (double)indptr[n];
+  for (int r = 1; r < world; r++) {
+    const double target = total * r / world;
+    int lo = (int)(std::lower_bound(indptr, indptr + n + 1, (long long)target,
+                                    [](int a, long long b) { return (long long)a < b; }) -
+                   indptr);
+    lo = std::max(lo, p.bounds[(size_t)r - 1] + 1);   // >= 1 node per rank
+    lo = std::min(lo, n - (world - r));
+    p.bounds[(size_t)r] = lo;
+  }
+  for (int r = 0; r < world; r++)
+    p.maxrows = std::max(p.maxrows, p.bounds[(size_t)r + 1] - p.bounds[(size_t)r]);
+  return p;
+}
+
+void partition_subgraph(const Partition &part, int n, const int *indptr, const int *indices,
+                        std::vector<int> *sub_indptr, std::vector<int> *sub_indices,
+                        std::vector<float> *sub_vals) {
+  const int lo = part.first(), hi = part.last();
+  const long long rows = (long long)part.world * part.maxrows;
+  std::vector<int> cnt((size_t)rows, 0);
+  auto padded = [&](int i) {
+    const int q = part.owner(i);
+    return (long long)q * part.maxrows + (i - part.bounds[(size_t)q]);
+  };
+  parallel_for(n, [&](long long b, long long e) {
+    for (long long i = b; i < e; i++) {
+      int c = 0;
+      for (int k = indptr[i]; k < indptr[i + 1]; k++) c += (indices[k] >= lo && indices[k] < hi);
+      cnt[(size_t)padded((int)i)] = c;
+    }
+  });
+  sub_indptr->assign((size_t)rows + 1, 0);
+  for (long long r = 0; r < rows; r++) (*sub_indptr)[(size_t)r + 1] = (*sub_indptr)[(size_t)r] + cnt[(size_t)r];
+  sub_indices->assign((size_t)sub_indptr->back(), 0);
+  sub_vals->assign((size_t)sub_indptr->back(), 0.0f);
+  parallel_for(n, [&](long long b, long long e) {
+    for (long long i = b; i < e; i++) {
+      long long o = (*sub_indptr)[(size_t)padded((int)i)];
+      const int di = indptr[i + 1] - indptr[i];
+      for (int k = indptr[i]; k < indptr[i + 1]; k++) {
+        const int j = indices[k];
+        if (j >= lo && j < hi) {
+          (*sub_indices)[(size_t)o] = j - lo;
+          (*sub_vals)[(size_t)o] = graph_coef(di, indptr[j + 1] - indptr[j]);
+          o++;
+        }
+      }
+    }
+  });
+}
+
+#define PGCN_NCCL(expr)                                                              \
+  do {                                                                               \
+    ncclResult_t r_ = (expr);                                                        \
+    if (r_ != ncclSuccess)                                                           \
+      throw Error(PGCN_E_COMM, std::string(#expr) + " -> " + ncclGetErrorString(r_)); \
+  } while (0)
+
+void Comm::unique_id(void *out128) {
+  ncclUniqueId id;
+  PGCN_NCCL(ncclGetUniqueId(&id));
+  static_assert(sizeof(ncclUniqueId) == 128, "unexpected ncclUniqueId size");
+  std::memcpy(out128, &id, sizeof id);
+}
+
+Comm::Comm(int rank, int world, const void *unique_id_128) : rank_(rank), world_(world) {
+  ncclUniqueId id;
+  std::memcpy(&id, unique_id_128, sizeof id);
+  ncclComm_t c;
+  PGCN_NCCL(ncclCommInitRank(&c, world, id, rank));
+  comm_ = c;
+}
+
+Comm::~Comm() {
+  if (comm_) (void)ncclCommDestroy(static_cast<ncclComm_t>(comm_));
+}
+
+void Comm::allreduce_sum(float *buf, size_t n, hipStream_t s) {
+  if (world_ == 1 || n == 0) return;
+  PGCN_NCCL(ncclAllReduce(buf, buf, n, ncclFloat32, ncclSum, static_cast<ncclComm_t>(comm_), s));
+}
+
+void Comm::reduce_scatter_sum(const float *send, float *recv, size_t recvcount, hipStream_t s) {
+  PGCN_NCCL(ncclReduceScatter(send, recv, recvcount, ncclFloat32, ncclSum,
+                              static_cast<ncclComm_t>(comm_), s));
+}
+
+}  // namespace pgcn

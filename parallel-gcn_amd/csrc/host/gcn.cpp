@@ -1,0 +1,502 @@
+// parallel-gcn_amd/csrc/host/gcn.cpp
+#include "gcn.hpp"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+
+#include "../kernels.hpp"
+#include "../rng.hpp"
+
+namespace pgcn {
+
+// ------------------------------------------------------------------------------------------
+// Adam (src/optim.cu:7-95; hpdga optim.cpp:16-35)
+// ------------------------------------------------------------------------------------------
+Adam::Adam(const std::vector<shared_ptr<Variable>> &weights, const std::vector<bool> &decays,
+           const AdamParams &p)
+    : params(p) {
+  PGCN_CHECK(weights.size() == decays.size(), PGCN_E_INVALID,
+             "Adam: weights and decays must have the same size");
+  for (size_t i = 0; i < weights.size(); i++) {
+    Var v;
+    v.w = weights[i];
+    v.m.allocate((size_t)v.w->size);
+    v.v.allocate((size_t)v.w->size);
+    v.m.zero();
+    v.v.zero();
+    v.decay = decays[i];
+    vars.push_back(std::move(v));
+  }
+}
+
+void Adam::step(const Stream &s) {
+  step_count++;
+  // hpdga optim.cpp:24, host float arithmetic with glibc powf/sqrtf
+  const float step_size = params.learning_rate *
+                          sqrtf(1.0f - powf(params.beta2, (float)step_count)) /
+                          (1.0f - powf(params.beta1, (float)step_count));
+  for (auto &v : vars)
+    launch_adam(v.w->dev_data.get(), v.w->dev_grad.get(), v.m.get(), v.v.get(), v.w->size,
+                step_size, params.beta1, params.beta2, params.eps, params.weight_decay,
+                v.decay ? 1 : 0, s.get());
+}
+
+// ------------------------------------------------------------------------------------------
+// GCN
+// ------------------------------------------------------------------------------------------
+namespace {
+// hpdga variable.cpp:15-19 (glorot), drawing from the shared xorshift state
+void glorot_host(std::vector<float> &w, int in_size, int out_size, uint64_t s[2]) {
+  const float range = sqrtf(6.0f / (float)(in_size + out_size));
+  for (auto &x : w) {
+    const float r = (float)xs_next(s) / (float)0x7fffffff;
+    x = (float)((((double)r - 0.5) * (double)range) * 2.0);
+  }
+}
+}  // namespace
+
+GCN::GCN(const GCNParams &params_, const AdamParams &adam, const GCNData &data, int device_,
+         const DistSpec *dist)
+    : params(params_), adam_params(adam), device(device_) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    throw Error(PGCN_E_NODEVICE, "no HIP device visible: the engine has no CPU fallback");
+  PGCN_CHECK(device >= 0 && device < ndev, PGCN_E_INVALID, "bad device index");
+  PGCN_HIP(hipSetDevice(device));
+  L = params.n_layers;
+  PGCN_CHECK(L >= 2 && L <= PGCN_MAX_LAYERS, PGCN_E_INVALID, "n_layers must be in [2,16]");
+  PGCN_CHECK((int)params.hidden_dims.size() == L - 1, PGCN_E_INVALID,
+             "Number of hidden dimensions must be 1 - n_layers");
+  PGCN_CHECK((int)params.dropouts.size() == L, PGCN_E_INVALID,
+             "Number of dropouts must match number of layers");
+  for (int h : params.hidden_dims)
+    PGCN_CHECK(h > 0 && h % 4 == 0 && h <= 128, PGCN_E_INVALID,
+               "hidden dims must be multiples of 4 in [4,128]");
+  PGCN_CHECK(params.output_dim >= 1 && params.output_dim <= 128, PGCN_E_INVALID,
+             "output_dim must be in [1,128]");
+  PGCN_CHECK(data.num_nodes == params.num_nodes, PGCN_E_INVALID, "num_nodes mismatch");
+  int lo_prio = 0, hi_prio = 0;
+  PGCN_HIP(hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
+  stream = Stream::create(hi_prio);  // the reference uses High priority streams
+  const int world = dist ? dist->world : 1, rank = dist ? dist->rank : 0;
+  part = make_partition(params.num_nodes, data.graph.indptr.data(), world, rank);
+  if (dist) {  // the edge-cut path (also at world == 1, which exercises it on one GPU)
+    comm = std::make_unique<Comm>(rank, world, dist->unique_id);
+    ctx.comm = comm.get();
+  }
+  build(data);
+}
+
+GCN::~GCN() {
+  if (stream.get()) (void)hipStreamSynchronize(stream.get());
+}
+
+void GCN::upload_features(const GCNData &data) {
+  const int first = part.first(), rows = part.local_rows(), F = params.input_dim;
+  const auto &fptr = data.feature_index.indptr;
+  feat_indptr_global = fptr;
+  nnz_x_global = fptr[(size_t)params.num_nodes];
+  feats.rows = rows;
+  feats.cols = F;
+  feats.dense = features_dense(data);
+  const long long p0 = fptr[(size_t)first], p1 = fptr[(size_t)first + rows];
+  feats.nnz = p1 - p0;
+  if (feats.dense) {
+    feats.ldx = round_up4(F);
+    std::vector<float> x((size_t)rows * feats.ldx, 0.0f);
+    parallel_for(rows, [&](long long b, long long e) {
+      for (long long i = b; i < e; i++)
+        std::memcpy(&x[(size_t)i * feats.ldx], &data.feature_value[(size_t)(first + i) * F],
+                    sizeof(float) * (size_t)F);
+    });
+    feats.x.allocate(x.size() + 4);
+    feats.x.upload(x);
+  } else {
+    std::vector<int> ip((size_t)rows + 1);
+    for (int i = 0; i <= rows; i++) ip[(size_t)i] = (int)(fptr[(size_t)first + i] - p0);
+    const int *idx = data.feature_index.indices.data() + p0;
+    feats.host_values.assign(data.feature_value.begin() + p0, data.feature_value.begin() + p1);
+    // transposed index for the weight gradient: stable counting sort by feature id
+    std::vector<int> cptr((size_t)F + 1, 0), crow((size_t)feats.nnz), cpos((size_t)feats.nnz);
+    for (long long k = 0; k < feats.nnz; k++) {
+      PGCN_CHECK(idx[k] >= 0 && idx[k] < F, PGCN_E_INVALID, "feature id out of range");
+      cptr[(size_t)idx[k] + 1]++;
+    }
+    for (int f = 0; f < F; f++) cptr[(size_t)f + 1] += cptr[(size_t)f];
+    std::vector<int> fill(cptr.begin(), cptr.end() - 1);
+    for (int i = 0; i < rows; i++)
+      for (int k = ip[(size_t)i]; k < ip[(size_t)i + 1]; k++) {
+        const int o = fill[(size_t)idx[k]]++;
+        crow[(size_t)o] = i;
+        cpos[(size_t)o] = k;
+      }
+    feats.indptr.allocate(ip.size());
+    feats.indptr.upload(ip);
+    feats.indices.allocate((size_t)feats.nnz + 1);
+    feats.indices.upload(idx, (size_t)feats.nnz);
+    feats.values.allocate((size_t)feats.nnz + 1);
+    feats.values.upload(feats.host_values);
+    feats.csc_ptr.allocate(cptr.size());
+    feats.csc_ptr.upload(cptr);
+    feats.csc_row.allocate(crow.size() + 1);
+    feats.csc_row.upload(crow);
+    feats.csc_pos.allocate(cpos.size() + 1);
+    feats.csc_pos.upload(cpos);
+  }
+}
+
+void GCN::init_dropout_rng(const GCNData &data, long long glorot_draws) {
+  const int N = params.num_nodes, first = part.first(), last = part.last();
+  std::vector<int> dims;
+  dims.push_back(params.input_dim);
+  for (int h : params.hidden_dims) dims.push_back(h);
+  dims.push_back(params.output_dim);
+  // draws per training epoch: the input dropout (nnz_X) then each hidden dropout (N*h_l)
+  unsigned long long period = (unsigned long long)nnz_x_global;
+  for (int l = 1; l < L; l++) period += (unsigned long long)N * dims[(size_t)l];
+  std::vector<uint64_t> table(16 * 256 * 2);
+  xs_byte_tables(xs_jump_matrix(period), table.data());
+  jump_table.allocate(table.size() * sizeof(uint64_t));
+  jump_table.upload(reinterpret_cast<const uint8_t *>(table.data()), table.size() * sizeof(uint64_t));
+  ctx.jump_table = jump_table.get();
+
+  uint64_t seed[2];
+  pgcn_rng_seed(seed);
+  unsigned long long offset = (unsigned long long)glorot_draws;
+  for (int l = 0; l < L; l++) {
+    auto r = std::make_shared<DropoutRng>();
+    if (l == 0) {
+      r->elem_begin = data.feature_index.indptr[(size_t)first];
+      r->elem_end = data.feature_index.indptr[(size_t)last];
+    } else {
+      r->elem_begin = (long long)first * dims[(size_t)l];
+      r->elem_end = (long long)last * dims[(size_t)l];
+    }
+    r->chunk_lo = r->elem_begin / kDropChunk;
+    const long long chunk_hi = ceil_div(r->elem_end, kDropChunk);
+    r->n_chunks = std::max(0LL, chunk_hi - r->chunk_lo);
+    r->mask_base = r->elem_begin - kDropChunk * r->chunk_lo;
+    std::vector<uint64_t> st((size_t)std::max(1LL, r->n_chunks) * 2, 0);
+    const unsigned long long base = offset + (unsigned long long)kDropChunk * r->chunk_lo;
+    parallel_for(r->n_chunks, [&](long long b, long long e) {
+      uint64_t s[2] = {seed[0], seed[1]};
+      xs_jump(s, base + (unsigned long long)kDropChunk * b);
+      for (long long c = b; c < e; c++) {
+        st[(size_t)c * 2] = s[0];
+        st[(size_t)c * 2 + 1] = s[1];
+        for (int k = 0; k < kDropChunk; k++) xs_advance(s);
+      }
+    });
+    r->states.allocate(st.size());
+    r->states.upload(st);
+    r->mask.allocate((size_t)std::max(1LL, r->n_chunks) + 1);
+    r->mask.zero();
+    rngs.push_back(r);
+    offset += (l == 0) ? (unsigned long long)nnz_x_global
+                       : (unsigned long long)N * dims[(size_t)l];
+  }
+}
+
+void GCN::build(const GCNData &data) {
+  const int N = params.num_nodes;
+  // adjacency
+  if (comm) {
+    std::vector<int> sp, si;
+    std::vector<float> sv;
+    partition_subgraph(part, N, data.graph.indptr.data(), data.graph.indices.data(), &sp, &si, &sv);
+    graph = std::make_unique<DevGraph>(part.world * part.maxrows, sp.data(), si.data(), sv.data());
+  } else {
+    std::vector<float> v = graph_coefs(N, data.graph.indptr.data(), data.graph.indices.data());
+    graph = std::make_unique<DevGraph>(N, data.graph.indptr.data(), data.graph.indices.data(),
+                                       v.data());
+  }
+  upload_features(data);
+  // truth per split for this rank's rows, padded with -1 (set_truth, src/gcn.cu:204-226)
+  const int first = part.first(), rows = part.local_rows(), prow = part.maxrows;
+  for (int s = 1; s <= 3; s++) {
+    std::vector<int> t((size_t)prow, -1);
+    for (int i = 0; i < rows; i++)
+      t[(size_t)i] = data.split[(size_t)first + i] == s ? data.label[(size_t)first + i] : -1;
+    truth[s].allocate(t.size());
+    truth[s].upload(t);
+    int c = 0;
+    for (int i = 0; i < N; i++) c += (data.split[(size_t)i] == s && data.label[(size_t)i] >= 0);
+    counts[s] = c;
+  }
+  // weights: glorot in layer order from the default seed (hpdga gcn.cpp:64-128)
+  std::vector<int> dims;
+  dims.push_back(params.input_dim);
+  for (int h : params.hidden_dims) dims.push_back(h);
+  dims.push_back(params.output_dim);
+  long long wtotal = 0;
+  for (int l = 0; l < L; l++) wtotal += (long long)dims[(size_t)l] * dims[(size_t)l + 1];
+  grad_arena.allocate((size_t)wtotal);
+  grad_arena.zero();
+  uint64_t rs[2];
+  pgcn_rng_seed(rs);
+  long long woff = 0;
+  std::vector<std::vector<float>> winit;
+  for (int l = 0; l < L; l++) {
+    auto w = std::make_shared<Variable>(dims[(size_t)l], dims[(size_t)l + 1], false);
+    std::vector<float> h((size_t)w->size);
+    glorot_host(h, dims[(size_t)l], dims[(size_t)l + 1], rs);
+    w->dev_data.upload(h);
+    w->dev_grad = grad_arena.slice((size_t)woff, (size_t)w->size);
+    woff += w->size;
+    weights.push_back(w);
+    decays.push_back(l == 0);
+  }
+  init_dropout_rng(data, wtotal);
+
+  // context buffers
+  xent_partials.allocate((size_t)xent_blocks(prow) * 2 + 2);
+  sums.allocate(4);
+  results_ring.allocate((size_t)ring_cap * 4);
+  results_ring.zero();
+  pinned = PinnedBuffer<float>(8);
+  size_t ws = 0;
+  for (int l = 0; l < L; l++)
+    ws = std::max(ws, gemm_tn_workspace(rows, dims[(size_t)l + 1], dims[(size_t)l]));
+  gemm_ws.allocate(ws / sizeof(float) + 64);
+  ctx.xent_partials = xent_partials.get();
+  ctx.xent_blocks = xent_blocks(prow);
+  ctx.gemm_workspace = gemm_ws.get();
+  ctx.gs_events = &gs_events;
+  ctx.gs_bytes = &gs_bytes;
+
+  // layers (src/gcn.cu:146-177)
+  variables.push_back(nullptr);  // "input": the features, kept in `feats`
+  insert_first_layer();
+  for (int l = 1; l < L - 1; l++)
+    insert_layer(params.hidden_dims[(size_t)l - 1], params.hidden_dims[(size_t)l],
+                 params.dropouts[(size_t)l], l);
+  insert_last_layer();
+  optimizer = Adam(weights, decays, adam_params);
+  PGCN_HIP(hipDeviceSynchronize());
+}
+
+// src/gcn.cu:47-81
+void GCN::insert_first_layer() {
+  const int prow = part.maxrows, h = params.hidden_dims.front();
+  auto drop = std::make_unique<Dropout>(nullptr, params.dropouts.front(), rngs[0], &ctx);
+  const Dropout *dptr = drop.get();
+  dropouts_.push_back(dptr);
+  modules.push_back(std::move(drop));
+  auto var1 = std::make_shared<Variable>(prow, h, true, round_up4(h));
+  variables.push_back(var1);
+  variables.push_back(weights[0]);
+  modules.push_back(std::make_unique<SparseMatmul>(&feats, weights[0], var1, dptr, &ctx));
+  auto var2 = std::make_shared<Variable>(prow, h, true, round_up4(h));
+  variables.push_back(var2);
+  modules.push_back(std::make_unique<GraphSum>(var1, var2, graph.get(), h, &ctx));
+  modules.push_back(std::make_unique<ReLU>(var2));
+}
+
+// src/gcn.cu:85-112
+void GCN::insert_layer(int in_dim, int out_dim, float dropout, int layer) {
+  const int prow = part.maxrows;
+  shared_ptr<Variable> prev = variables.back();
+  auto drop = std::make_unique<Dropout>(prev, dropout, rngs[(size_t)layer], &ctx);
+  dropouts_.push_back(drop.get());
+  modules.push_back(std::move(drop));
+  auto var1 = std::make_shared<Variable>(prow, out_dim, true, round_up4(out_dim));
+  variables.push_back(var1);
+  variables.push_back(weights[(size_t)layer]);
+  modules.push_back(std::make_unique<Matmul>(prev, weights[(size_t)layer], var1,
+                                             part.local_rows(), in_dim, out_dim, &ctx));
+  auto var2 = std::make_shared<Variable>(prow, out_dim, true, round_up4(out_dim));
+  variables.push_back(var2);
+  modules.push_back(std::make_unique<GraphSum>(var1, var2, graph.get(), out_dim, &ctx));
+  modules.push_back(std::make_unique<ReLU>(var2));
+}
+
+// src/gcn.cu:116-142
+void GCN::insert_last_layer() {
+  const int prow = part.maxrows, C = params.output_dim, hl = params.hidden_dims.back();
+  shared_ptr<Variable> prev = variables.back();
+  auto drop = std::make_unique<Dropout>(prev, params.dropouts.back(), rngs[(size_t)L - 1], &ctx);
+  dropouts_.push_back(drop.get());
+  modules.push_back(std::move(drop));
+  auto var1 = std::make_shared<Variable>(prow, C, true, round_up4(C));
+  variables.push_back(var1);
+  variables.push_back(weights.back());
+  modules.push_back(std::make_unique<Matmul>(prev, weights.back(), var1, part.local_rows(), hl,
+                                             C, &ctx));
+  auto out = std::make_shared<Variable>(prow, C, true, round_up4(C));
+  variables.push_back(out);
+  modules.push_back(std::make_unique<GraphSum>(var1, out, graph.get(), C, &ctx));
+  modules.push_back(std::make_unique<CrossEntropyLoss>(out, C, &ctx));
+}
+
+void GCN::set_split(int split) {
+  ctx.truth = truth[split].get();
+  ctx.count = counts[split];
+  modules.back()->set_num_samples(counts[split]);
+}
+
+// loss/acc of the pass just enqueued -> results_ring slot (finalize, src/gcn.cu:440-455)
+void GCN::finalize(int dst_offset) {
+  const auto &w1 = weights.front();
+  launch_reduce_scalars(xent_partials.get(), ctx.xent_blocks, w1->dev_data.get(), w1->size,
+                        sums.get(), stream.get());
+  if (comm) comm->allreduce_sum(sums.get(), 2, stream.get());
+  launch_compose(sums.get(), ctx.count, adam_params.weight_decay, results_ring.get() + dst_offset,
+                 stream.get());
+}
+
+void GCN::epoch_async() {
+  const long long slot = epoch_count % ring_cap;
+  // train_epoch (src/gcn.cu:307-343)
+  set_split(1);
+  for (const auto &m : modules) m->forward(true, stream);
+  finalize((int)(slot * 4));
+  for (int i = (int)modules.size() - 1; i >= 0; i--) modules[(size_t)i]->backward(stream);
+  if (comm) comm->allreduce_sum(grad_arena.get(), grad_arena.size(), stream.get());
+  optimizer.step(stream);
+  // eval(2) (src/gcn.cu:293-303)
+  set_split(2);
+  for (const auto &m : modules) m->forward(false, stream);
+  finalize((int)(slot * 4 + 2));
+  last_forward_training = false;
+  epoch_count++;
+}
+
+std::pair<float, float> GCN::train_epoch() {
+  const long long slot = epoch_count % ring_cap;
+  set_split(1);
+  for (const auto &m : modules) m->forward(true, stream);
+  finalize((int)(slot * 4));
+  for (int i = (int)modules.size() - 1; i >= 0; i--) modules[(size_t)i]->backward(stream);
+  if (comm) comm->allreduce_sum(grad_arena.get(), grad_arena.size(), stream.get());
+  optimizer.step(stream);
+  last_forward_training = true;
+  PGCN_HIP(hipMemcpyAsync(pinned.get(), results_ring.get() + slot * 4, 2 * sizeof(float),
+                          hipMemcpyDeviceToHost, stream.get()));
+  stream.sync();
+  return {pinned.get()[0], pinned.get()[1]};
+}
+
+std::pair<float, float> GCN::eval(int split) {
+  PGCN_CHECK(split >= 1 && split <= 3, PGCN_E_INVALID, "split must be 1, 2 or 3");
+  const long long slot = epoch_count % ring_cap;
+  set_split(split);
+  for (const auto &m : modules) m->forward(false, stream);
+  finalize((int)(slot * 4 + 2));
+  last_forward_training = false;
+  PGCN_HIP(hipMemcpyAsync(pinned.get(), results_ring.get() + slot * 4 + 2, 2 * sizeof(float),
+                          hipMemcpyDeviceToHost, stream.get()));
+  stream.sync();
+  if (split == 2) epoch_count++;  // a train_epoch + eval(2) pair fills one ring slot
+  return {pinned.get()[0], pinned.get()[1]};
+}
+
+void GCN::sync() { stream.sync(); }
+
+std::vector<float> GCN::results(int n) {
+  sync();
+  std::vector<float> all((size_t)ring_cap * 4);
+  results_ring.download(all.data(), all.size());
+  n = (int)std::min<long long>(n, std::min<long long>(epoch_count, ring_cap));
+  std::vector<float> out((size_t)n * 4);
+  for (int k = 0; k < n; k++) {
+    const long long e = epoch_count - n + k;
+    std::memcpy(&out[(size_t)k * 4], &all[(size_t)(e % ring_cap) * 4], 4 * sizeof(float));
+  }
+  return out;
+}
+
+// src/gcn.cu:347-436 / hpdga gcn.cpp:214-274
+void GCN::run(bool verbose) {
+  std::vector<float> loss_history;
+  double total = 0;
+  int epoch = 1;
+  for (; epoch <= params.epochs; epoch++) {
+    const auto t0 = std::chrono::high_resolution_clock::now();
+    auto tr = train_epoch();
+    auto va = eval(2);
+    const float dt = std::chrono::duration<float>(std::chrono::high_resolution_clock::now() - t0).count();
+    total += dt;
+    if (verbose)
+      printf("epoch=%d train_loss=%.5f train_acc=%.5f val_loss=%.5f val_acc=%.5f time=%.5f\n",
+             epoch, tr.first, tr.second, va.first, va.second, dt);
+    loss_history.push_back(va.first);
+    if (params.early_stopping > 0 && epoch >= params.early_stopping) {
+      float recent = 0.0f;
+      for (int i = epoch - params.early_stopping; i < epoch; i++) recent += loss_history[(size_t)i];
+      if (va.first > recent / (float)params.early_stopping) {
+        if (verbose) printf("Early stopping...\n");
+        break;
+      }
+    }
+  }
+  if (verbose) {
+    const int done = std::min(epoch, params.epochs);
+    printf("TMR_TRAIN average time: %.3fms\n", total * 1000.0 / done);
+    const auto t0 = std::chrono::high_resolution_clock::now();
+    auto te = eval(3);
+    const float dt = std::chrono::duration<float>(std::chrono::high_resolution_clock::now() - t0).count();
+    printf("test_loss=%.5f test_acc=%.5f time=%.5f\n", te.first, te.second, dt);
+  }
+}
+
+std::vector<float> GCN::get_var(int idx, int which) {
+  sync();
+  PGCN_CHECK(idx >= 0 && idx < (int)variables.size(), PGCN_E_INVALID, "variable index");
+  if (idx == 0) {  // the input features (dropped, if the last forward was a training one)
+    if (which) return {};
+    std::vector<float> x;
+    if (feats.dense) {
+      std::vector<float> raw((size_t)feats.rows * feats.ldx);
+      feats.x.download(raw.data(), raw.size());
+      x.resize((size_t)feats.rows * feats.cols);
+      for (int i = 0; i < feats.rows; i++)
+        std::memcpy(&x[(size_t)i * feats.cols], &raw[(size_t)i * feats.ldx],
+                    sizeof(float) * (size_t)feats.cols);
+    } else {
+      x = feats.host_values;
+    }
+    if (last_forward_training) {
+      const DropoutRng &r = *rngs[0];
+      std::vector<uint64_t> m((size_t)r.n_chunks);
+      r.mask.download(m.data(), m.size());
+      const float scale = dropouts_[0]->scale();
+      for (size_t k = 0; k < x.size(); k++) {
+        const long long b = r.mask_base + (long long)k;
+        x[k] *= ((m[(size_t)(b >> 6)] >> (b & 63)) & 1) ? scale : 0.0f;
+      }
+    }
+    return x;
+  }
+  const auto &v = variables[(size_t)idx];
+  std::vector<float> out = v->to_host(which);
+  const bool node_var = v->rows == part.maxrows &&
+                        std::find(weights.begin(), weights.end(), v) == weights.end();
+  if (node_var) out.resize((size_t)part.local_rows() * v->cols);
+  return out;
+}
+
+void GCN::set_profile(bool on) {
+  sync();
+  ctx.profile = on;
+  gs_events.clear();
+  gs_bytes.clear();
+}
+
+void GCN::profile_read(double *ms, long long *calls, double *bytes) {
+  sync();
+  double t = 0, b = 0;
+  for (size_t i = 0; i < gs_events.size(); i++) {
+    float e = 0;
+    PGCN_HIP(hipEventElapsedTime(&e, gs_events[i].first.get(), gs_events[i].second.get()));
+    t += e;
+    b += gs_bytes[i];
+  }
+  if (ms) *ms = t;
+  if (calls) *calls = (long long)gs_events.size();
+  if (bytes) *bytes = b;
+}
+
+}  // namespace pgcn

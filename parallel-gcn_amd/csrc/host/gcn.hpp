@@ -1,0 +1,123 @@
+// parallel-gcn_amd/csrc/host/gcn.hpp -- GCNParams / AdamParams / Adam / GCN.
+//
+// Mirrors include/gcn.cuh:40-122 and include/optim.cuh:16-50 of the reference (and
+// hpdga-spring23/include/gcn.h, optim.h): same parameter structs and defaults, the same
+// L-layer builders (insert_first_layer / insert_layer / insert_last_layer,
+// src/gcn.cu:47-142), the same module and variable order, train_epoch / eval / run.
+// Numerics follow the sequential CPU reference (hpdga-spring23), not the CUDA one: CPU
+// xorshift128+ dropout masks and glorot init, loss normalised by the labelled count.
+#pragma once
+#include <memory>
+#include <utility>
+#include <vector>
+
+#include "comm.hpp"
+#include "data.hpp"
+#include "graph.hpp"
+#include "module.hpp"
+#include "runtime.hpp"
+
+namespace pgcn {
+
+struct GCNParams {
+  int num_nodes = 0, input_dim = 0, output_dim = 0;
+  std::vector<int> hidden_dims = {16};
+  std::vector<float> dropouts = {0.5f, 0.5f};
+  int epochs = 100, early_stopping = 0;
+  int n_layers = 2;
+};
+
+struct AdamParams {
+  float learning_rate = 0.01f, beta1 = 0.9f, beta2 = 0.999f, eps = 1e-8f, weight_decay = 5e-4f;
+};
+
+// include/optim.cuh:23-50; hpdga optim.cpp:5-35.  Weight decay on W1 only
+// (src/gcn.cu:157-158, hpdga gcn.cpp:127).
+class Adam {
+  struct Var {
+    shared_ptr<Variable> w;
+    DeviceBuffer<float> m, v;
+    bool decay;
+  };
+  std::vector<Var> vars;
+  AdamParams params;
+  int step_count = 0;
+
+ public:
+  Adam() = default;
+  Adam(const std::vector<shared_ptr<Variable>> &weights, const std::vector<bool> &decays,
+       const AdamParams &p);
+  void step(const Stream &s);
+};
+
+struct DistSpec {
+  int rank = 0, world = 1;
+  const void *unique_id = nullptr;  // 128 bytes
+};
+
+class GCN {
+ public:
+  GCN(const GCNParams &params, const AdamParams &adam, const GCNData &data, int device,
+      const DistSpec *dist = nullptr);
+  ~GCN();
+  std::pair<float, float> train_epoch();
+  std::pair<float, float> eval(int split);
+  void epoch_async();  // train_epoch + eval(2) without a host sync
+  void sync();
+  std::vector<float> results(int n);  // last n epochs x {tl, ta, vl, va}
+  void run(bool verbose);
+
+  int num_vars() const { return (int)variables.size(); }
+  std::vector<float> get_var(int idx, int which);
+  void set_profile(bool on);
+  void profile_read(double *ms, long long *calls, double *bytes);
+  const Partition &partition() const { return part; }
+  const GCNParams &get_params() const { return params; }
+
+ private:
+  void build(const GCNData &data);
+  void upload_features(const GCNData &data);
+  void init_dropout_rng(const GCNData &data, long long glorot_draws);
+  void insert_first_layer();
+  void insert_layer(int in_dim, int out_dim, float dropout, int layer);
+  void insert_last_layer();
+  void set_split(int split);
+  void finalize(int slot_offset);
+
+  GCNParams params;
+  AdamParams adam_params;
+  int device;
+  int L;
+  Partition part;
+  std::unique_ptr<Comm> comm;
+  Stream stream;
+  ModuleContext ctx;
+
+  std::unique_ptr<DevGraph> graph;
+  DevFeatures feats;
+  DeviceBuffer<int> truth[4];
+  int counts[4] = {0, 0, 0, 0};
+  long long nnz_x_global = 0;
+  std::vector<int> feat_indptr_global;  // for the input dropout ranges
+
+  std::vector<shared_ptr<Variable>> variables;
+  std::vector<std::unique_ptr<Module>> modules;
+  std::vector<shared_ptr<Variable>> weights;
+  std::vector<bool> decays;
+  std::vector<shared_ptr<DropoutRng>> rngs;  // [0] input, then one per hidden layer
+  std::vector<const Dropout *> dropouts_;
+  Adam optimizer;
+  DeviceBuffer<float> grad_arena;  // all weight grads, one all-reduce
+  DeviceBuffer<uint8_t> jump_table;
+  DeviceBuffer<float> gemm_ws;
+  DeviceBuffer<float> xent_partials, sums, results_ring;
+  PinnedBuffer<float> pinned;
+  int ring_cap = 1024;
+  long long epoch_count = 0;
+  bool last_forward_training = false;
+
+  std::vector<std::pair<Event, Event>> gs_events;
+  std::vector<double> gs_bytes;
+};
+
+}  // namespace pgcn

@@ -1,0 +1,190 @@
+// parallel-gcn_amd/csrc/host/module.cpp
+#include "module.hpp"
+
+#include "../kernels.hpp"
+
+namespace pgcn {
+
+Variable::Variable(int rows_, int cols_, bool requires_grad, int ld_)
+    : rows(rows_), cols(cols_), ld(ld_ < 0 ? cols_ : ld_), size((long long)rows_ * cols_) {
+  const size_t n = (size_t)rows * (size_t)ld;
+  dev_data.allocate(n);
+  dev_data.zero();
+  if (requires_grad) {
+    dev_grad.allocate(n);
+    dev_grad.zero();
+  }
+}
+
+std::vector<float> Variable::to_host(int which) const {
+  const DeviceBuffer<float> &b = which ? dev_grad : dev_data;
+  std::vector<float> out;
+  if (!b) return out;
+  std::vector<float> raw((size_t)rows * ld);
+  b.download(raw.data(), raw.size());
+  out.resize((size_t)rows * cols);
+  for (int r = 0; r < rows; r++)
+    for (int c = 0; c < cols; c++) out[(size_t)r * cols + c] = raw[(size_t)r * ld + c];
+  return out;
+}
+
+// ------------------------------------------------------------------------------------------
+// Dropout (src/module.cu:6-99; hpdga module.cpp:196-228)
+// ------------------------------------------------------------------------------------------
+Dropout::Dropout(shared_ptr<Variable> in_, float p_, shared_ptr<DropoutRng> rng_,
+                 ModuleContext *ctx_)
+    : in(std::move(in_)), rng(std::move(rng_)), p(p_), ctx(ctx_) {}
+
+void Dropout::forward(bool training, const Stream &s) const {
+  if (!training) return;  // hpdga module.cpp:209
+  const DropoutRng &r = *rng;
+  launch_dropout_mask(r.states.get(), r.n_chunks, 64 * r.chunk_lo, r.elem_end, p, r.mask.get(),
+                      ctx->jump_table, s.get());
+  if (in) {
+    // a grad-carrying variable is dropped in place (module.cpp:215); its rows are the
+    // first (elem_end - elem_begin) elements of the local variable
+    launch_dropout_apply_based(in->dev_data.get(), r.elem_end - r.elem_begin, r.mask.get(),
+                               r.mask_base, scale(), s.get());
+  }
+}
+
+void Dropout::backward(const Stream &s) const {
+  if (!in || !in->dev_grad) return;  // module.cpp:222: no mask => nothing to do
+  const DropoutRng &r = *rng;
+  launch_dropout_apply_based(in->dev_grad.get(), r.elem_end - r.elem_begin, r.mask.get(),
+                             r.mask_base, scale(), s.get());
+}
+
+// ------------------------------------------------------------------------------------------
+// SparseMatmul (src/module.cu:104-163; hpdga module.cpp:49-72)
+// ------------------------------------------------------------------------------------------
+SparseMatmul::SparseMatmul(const DevFeatures *x_, shared_ptr<Variable> b_,
+                           shared_ptr<Variable> c_, const Dropout *drop_, ModuleContext *ctx_)
+    : x(x_), b(std::move(b_)), c(std::move(c_)), drop(drop_), ctx(ctx_) {}
+
+void SparseMatmul::forward(bool training, const Stream &s) const {
+  last_training = training;
+  const uint64_t *mask = training ? drop->state().mask.get() : nullptr;
+  const long long base = drop->state().mask_base;
+  const float scale = drop->scale();
+  if (x->dense) {
+    launch_gemm_nn(x->rows, b->cols, x->cols, x->x.get(), x->ldx, b->dev_data.get(), b->ld, 0,
+                   c->dev_data.get(), c->ld, mask, base, x->cols, scale, s.get());
+  } else {
+    launch_spmm_csr(x->rows, b->cols, c->ld, x->indptr.get(), x->indices.get(), x->values.get(),
+                    mask, base, scale, b->dev_data.get(), c->dev_data.get(), s.get());
+  }
+}
+
+void SparseMatmul::backward(const Stream &s) const {
+  // b.grad = drop(X)^T * c.grad  (the dropped X of the last training forward)
+  const uint64_t *mask = last_training ? drop->state().mask.get() : nullptr;
+  const long long base = drop->state().mask_base;
+  const float scale = drop->scale();
+  if (x->dense) {
+    launch_gemm_tn(x->rows, b->cols, x->cols, x->x.get(), x->ldx, c->dev_grad.get(), c->ld,
+                   b->dev_grad.get(), b->ld, mask, base, x->cols, scale, ctx->gemm_workspace,
+                   s.get());
+  } else {
+    launch_spmm_csc_bwd(x->cols, b->cols, c->ld, x->csc_ptr.get(), x->csc_row.get(),
+                        x->csc_pos.get(), x->values.get(), mask, base, scale, c->dev_grad.get(),
+                        b->dev_grad.get(), s.get());
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// GraphSum (src/module.cu:168-210; hpdga module.cpp:82-111)
+// ------------------------------------------------------------------------------------------
+GraphSum::GraphSum(shared_ptr<Variable> in_, shared_ptr<Variable> out_, DevGraph *graph_,
+                   int dim_, ModuleContext *ctx_)
+    : in(std::move(in_)), out(std::move(out_)), graph(graph_), dim(dim_), ctx(ctx_) {
+  if (ctx->comm) {
+    partial.allocate((size_t)graph->rows() * out->ld);
+    partial.zero();
+  }
+}
+
+void GraphSum::run(const float *src, float *dst, const Stream &s) const {
+  Event e0, e1;
+  if (ctx->profile) {
+    e0 = Event::create(true);
+    e1 = Event::create(true);
+    e0.record(s.get());
+  }
+  if (ctx->comm) {
+    // partial sums for every (padded) row from this rank's columns, then reduce-scatter
+    graph->graphsum(src, in->ld, partial.get(), out->ld, dim, s.get());
+    if (ctx->profile) e1.record(s.get());
+    ctx->comm->reduce_scatter_sum(partial.get(), dst, (size_t)out->rows * out->ld, s.get());
+  } else {
+    graph->graphsum(src, in->ld, dst, out->ld, dim, s.get());
+    if (ctx->profile) e1.record(s.get());
+  }
+  if (ctx->profile) {
+    ctx->gs_events->emplace_back(e0, e1);
+    ctx->gs_bytes->push_back(graph->algorithmic_bytes(dim, in->rows));
+  }
+}
+
+void GraphSum::forward(bool, const Stream &s) const {
+  run(in->dev_data.get(), out->dev_data.get(), s);
+}
+
+void GraphSum::backward(const Stream &s) const {
+  // the same gather on grads (Â symmetric): in.grad = Â out.grad (module.cpp:98-111)
+  run(out->dev_grad.get(), in->dev_grad.get(), s);
+}
+
+// ------------------------------------------------------------------------------------------
+// ReLU (src/module.cu:215-265)
+// ------------------------------------------------------------------------------------------
+ReLU::ReLU(shared_ptr<Variable> in_) : in(std::move(in_)) {
+  mask.allocate((size_t)in->rows * in->ld);
+  mask.zero();
+}
+
+void ReLU::forward(bool training, const Stream &s) const {
+  launch_relu_fwd(in->dev_data.get(), (long long)in->rows * in->ld, mask.get(), training, s.get());
+}
+
+void ReLU::backward(const Stream &s) const {
+  launch_relu_bwd(in->dev_grad.get(), (long long)in->rows * in->ld, mask.get(), s.get());
+}
+
+// ------------------------------------------------------------------------------------------
+// Matmul (src/module.cu:270-472; hpdga module.cpp:13-38)
+// ------------------------------------------------------------------------------------------
+Matmul::Matmul(shared_ptr<Variable> a_, shared_ptr<Variable> b_, shared_ptr<Variable> c_,
+               int m_, int n_, int p_, ModuleContext *ctx_)
+    : a(std::move(a_)), b(std::move(b_)), c(std::move(c_)), m(m_), n(n_), p(p_), ctx(ctx_) {}
+
+void Matmul::forward(bool, const Stream &s) const {
+  launch_gemm_nn(m, p, n, a->dev_data.get(), a->ld, b->dev_data.get(), b->ld, 0,
+                 c->dev_data.get(), c->ld, nullptr, 0, 0, 1.0f, s.get());
+}
+
+void Matmul::backward(const Stream &s) const {
+  // a.grad = c.grad * b^T   (b stored [n][p] => trans_b)
+  launch_gemm_nn(m, n, p, c->dev_grad.get(), c->ld, b->dev_data.get(), b->ld, 1,
+                 a->dev_grad.get(), a->ld, nullptr, 0, 0, 1.0f, s.get());
+  // b.grad = a^T * c.grad (deterministic split-M reduction)
+  launch_gemm_tn(m, p, n, a->dev_data.get(), a->ld, c->dev_grad.get(), c->ld, b->dev_grad.get(),
+                 b->ld, nullptr, 0, 0, 1.0f, ctx->gemm_workspace, s.get());
+}
+
+// ------------------------------------------------------------------------------------------
+// CrossEntropyLoss (src/module.cu:477-562; hpdga module.cpp:122-156)
+// ------------------------------------------------------------------------------------------
+CrossEntropyLoss::CrossEntropyLoss(shared_ptr<Variable> logits_, int num_classes_,
+                                   ModuleContext *ctx_)
+    : logits(std::move(logits_)), num_classes(num_classes_), ctx(ctx_) {}
+
+void CrossEntropyLoss::forward(bool training, const Stream &s) const {
+  launch_xent_fwd(logits->dev_data.get(), logits->ld, training ? logits->dev_grad.get() : nullptr,
+                  ctx->truth, logits->rows, num_classes, ctx->count, training ? 1 : 0,
+                  ctx->xent_partials, s.get());
+}
+
+void CrossEntropyLoss::backward(const Stream &) const {}  // module.cpp:155-156
+
+}  // namespace pgcn

@@ -1,0 +1,180 @@
+// parallel-gcn_amd/csrc/host/module.hpp -- Variable and the Module family.
+//
+// Same classes, constructor shapes and forward/backward contract as the reference's
+// include/variable.cuh:11-29 and include/module.cuh:21-145:
+//   virtual void forward(bool training, const Stream &) const;
+//   virtual void backward(const Stream &) const;
+// Each module launches its HIP kernels asynchronously on the stream it is given; data
+// stays on the device.  Differences from the reference, by design:
+//   * the input features X are never rewritten: the input Dropout only produces the mask
+//     bits that SparseMatmul applies on the fly (the reference mutates X in place and
+//     restores it with set_input_kernel every pass, src/gcn.cu:181-200);
+//   * dropout masks are the CPU reference's xorshift128+ masks, bit for bit;
+//   * weight gradients are reduced deterministically (no float atomics);
+//   * with an edge-cut communicator, GraphSum combines partial sums with an RCCL
+//     reduce-scatter and weight grads are all-reduced by the optimizer.
+#pragma once
+#include <memory>
+#include <vector>
+
+#include "comm.hpp"
+#include "graph.hpp"
+#include "runtime.hpp"
+
+namespace pgcn {
+
+using std::shared_ptr;
+
+// include/variable.cuh:11-29. Node-sized variables are [rows][ld] with ld = round_up(cols,4)
+// (padding columns are kept zero); weights are dense [rows][cols].
+class Variable {
+ public:
+  DeviceBuffer<float> dev_data, dev_grad;
+  int rows = 0, cols = 0, ld = 0;
+  long long size = 0;  // logical rows * cols
+  Variable(int rows_, int cols_, bool requires_grad, int ld_ = -1);
+  Variable() = default;
+  void zero(hipStream_t s) const { dev_data.zero_async(s); }
+  void zero_grad(hipStream_t s) const {
+    if (dev_grad) dev_grad.zero_async(s);
+  }
+  // logical (unpadded) copy to host, which: 0 data, 1 grad
+  std::vector<float> to_host(int which) const;
+};
+
+// Input features on the device (the feature half of DevGCNData, src/gcn.cu:30-43).
+struct DevFeatures {
+  bool dense = false;
+  int rows = 0, cols = 0;  // local rows, input_dim
+  long long nnz = 0;
+  // dense: [rows][ldx] fp32, CSR order == row-major order
+  DeviceBuffer<float> x;
+  int ldx = 0;
+  // sparse: CSR (+ transposed index for the weight gradient)
+  DeviceBuffer<int> indptr, indices, csc_ptr, csc_row, csc_pos;
+  DeviceBuffer<float> values;
+  std::vector<float> host_values;  // for reporting the dropped input (API parity)
+};
+
+// Dropout mask + xorshift chunk states for one Dropout module on this rank.
+struct DropoutRng {
+  DeviceBuffer<uint64_t> states;  // 2 per chunk
+  DeviceBuffer<uint64_t> mask;    // 1 word per chunk
+  long long chunk_lo = 0, n_chunks = 0;
+  long long elem_begin = 0, elem_end = 0;  // global element range of this rank
+  long long mask_base = 0;                 // bit of local element 0 in `mask`
+};
+
+class Module {
+ public:
+  virtual void forward(bool training, const Stream &s) const = 0;
+  virtual void backward(const Stream &s) const = 0;
+  virtual void set_num_samples(int) {}
+  virtual int get_num_samples() const { return 0; }
+  virtual ~Module() {}
+};
+
+// Shared per-GCN state the modules read (current split, comm, profiling, RNG table).
+struct ModuleContext {
+  const int *truth = nullptr;  // current split's truth (device)
+  int count = 0;               // labelled rows of the current split (global)
+  float *xent_partials = nullptr;
+  int xent_blocks = 0;
+  Comm *comm = nullptr;        // null on one GPU
+  const void *jump_table = nullptr;  // M^period byte tables (device)
+  void *gemm_workspace = nullptr;
+  // profiling of GraphSum calls
+  bool profile = false;
+  std::vector<std::pair<Event, Event>> *gs_events = nullptr;
+  std::vector<double> *gs_bytes = nullptr;
+  std::vector<Event> *event_pool = nullptr;
+};
+
+// include/module.cuh:33-43
+class Dropout : public Module {
+  shared_ptr<Variable> in;  // null for the input features
+  shared_ptr<DropoutRng> rng;
+  float p;
+  ModuleContext *ctx;
+
+ public:
+  Dropout(shared_ptr<Variable> in_, float p_, shared_ptr<DropoutRng> rng_, ModuleContext *ctx_);
+  void forward(bool training, const Stream &s) const override;
+  void backward(const Stream &s) const override;
+  float scale() const { return 1.0f / (1.0f - p); }
+  const DropoutRng &state() const { return *rng; }
+};
+
+// include/module.cuh:47-68: c = drop(X) * W
+class SparseMatmul : public Module {
+  const DevFeatures *x;
+  shared_ptr<Variable> b, c;
+  const Dropout *drop;  // the input Dropout (its mask, when training)
+  ModuleContext *ctx;
+  mutable bool last_training = false;
+
+ public:
+  SparseMatmul(const DevFeatures *x_, shared_ptr<Variable> b_, shared_ptr<Variable> c_,
+               const Dropout *drop_, ModuleContext *ctx_);
+  void forward(bool training, const Stream &s) const override;
+  void backward(const Stream &s) const override;
+};
+
+// include/module.cuh:72-86
+class GraphSum : public Module {
+  shared_ptr<Variable> in, out;
+  DevGraph *graph;
+  int dim;
+  ModuleContext *ctx;
+  DeviceBuffer<float> partial;  // [world*maxrows][ld] for the edge-cut reduce-scatter
+
+ public:
+  GraphSum(shared_ptr<Variable> in_, shared_ptr<Variable> out_, DevGraph *graph_, int dim_,
+           ModuleContext *ctx_);
+  void forward(bool training, const Stream &s) const override;
+  void backward(const Stream &s) const override;
+
+ private:
+  void run(const float *src, float *dst, const Stream &s) const;
+};
+
+// include/module.cuh:90-99
+class ReLU : public Module {
+  shared_ptr<Variable> in;
+  DeviceBuffer<uint8_t> mask;
+
+ public:
+  explicit ReLU(shared_ptr<Variable> in_);
+  void forward(bool training, const Stream &s) const override;
+  void backward(const Stream &s) const override;
+};
+
+// include/module.cuh:103-124: c = a * b
+class Matmul : public Module {
+  shared_ptr<Variable> a, b, c;
+  int m, n, p;
+  ModuleContext *ctx;
+
+ public:
+  Matmul(shared_ptr<Variable> a_, shared_ptr<Variable> b_, shared_ptr<Variable> c_, int m_,
+         int n_, int p_, ModuleContext *ctx_);
+  void forward(bool training, const Stream &s) const override;
+  void backward(const Stream &s) const override;
+};
+
+// include/module.cuh:128-145
+class CrossEntropyLoss : public Module {
+  shared_ptr<Variable> logits;
+  int num_classes;
+  ModuleContext *ctx;
+  int num_samples = 0;
+
+ public:
+  CrossEntropyLoss(shared_ptr<Variable> logits_, int num_classes_, ModuleContext *ctx_);
+  void forward(bool training, const Stream &s) const override;
+  void backward(const Stream &s) const override;
+  void set_num_samples(int n) override { num_samples = n; }
+  int get_num_samples() const override { return num_samples; }
+};
+
+}  // namespace pgcn

@@ -1,0 +1,322 @@
+// parallel-gcn_amd/csrc/k_elementwise.hip -- dropout (bit-exact hpdga masks), ReLU,
+// fused cross-entropy + accuracy, scalar finalisation and Adam, for gfx950.
+//
+// Reference kernels replaced: dropout_kernel_forward/backward (src/module.cu:16-99),
+// relu_kernel_forward/backward (:222-265), cross_entropy_loss_kernel (:484-541),
+// get_accuracy_kernel / get_l2_penalty_kernel (src/gcn.cu:230-289),
+// adam_step_kernel (src/optim.cu:42-55).
+//
+// Float contraction is OFF in this file: every product/sum rounds where the sequential
+// CPU reference (hpdga-spring23) rounds, so Adam and dropout are bit-exact.
+#include "common.hpp"
+#include "kernels.hpp"
+
+#pragma clang fp contract(off)
+
+namespace pgcn {
+
+// ------------------------------------------------------------------------------------------
+// Dropout masks: one thread per 64-draw chunk.  The chunk state is the xorshift128+ state at
+// the draw element 64*c consumes (hpdga module.cpp:213-217 consumes one draw per element, in
+// index order). After emitting the 64 mask bits the state is advanced by one epoch's worth
+// of draws (`period`) with 16 byte-table lookups (table = 64 KB, staged in LDS).
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_dropout_mask(uint64_t *__restrict__ states,
+                                                      long long n_chunks, long long elem0,
+                                                      long long elem_end, int threshold,
+                                                      uint64_t *__restrict__ mask,
+                                                      const uint4 *__restrict__ table) {
+  __shared__ uint4 lut[16 * 256];
+  for (int i = threadIdx.x; i < 16 * 256; i += blockDim.x) lut[i] = table[i];
+  __syncthreads();
+  for (long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x; c < n_chunks;
+       c += (long long)gridDim.x * blockDim.x) {
+    const uint64_t a0 = states[2 * c], a1 = states[2 * c + 1];
+    uint64_t s0 = a0, s1 = a1, word = 0;
+#pragma unroll 8
+    for (int j = 0; j < 64; j++) {
+      uint64_t t = s0;
+      const uint64_t u = s1;
+      s0 = u;
+      t ^= t << 23;
+      t ^= t >> 17;
+      t ^= u ^ (u >> 26);
+      s1 = t;
+      const int r = (int)((uint32_t)(t + u) & 0x7fffffffu);
+      word |= (uint64_t)(r >= threshold) << j;
+    }
+    const long long e = elem0 + 64 * c;  // first element of this chunk
+    if (e + 64 > elem_end) {
+      const long long valid = elem_end - e;
+      word = valid <= 0 ? 0 : (word & ((valid >= 64) ? ~0ull : ((1ull << valid) - 1)));
+    }
+    mask[c] = word;
+    // advance the chunk state by `period` draws: M^period * (a0, a1)
+    uint64_t n0 = 0, n1 = 0;
+#pragma unroll
+    for (int b = 0; b < 8; b++) {
+      const uint4 v = lut[b * 256 + ((a0 >> (8 * b)) & 0xff)];
+      n0 ^= ((uint64_t)v.y << 32) | v.x;
+      n1 ^= ((uint64_t)v.w << 32) | v.z;
+    }
+#pragma unroll
+    for (int b = 0; b < 8; b++) {
+      const uint4 v = lut[(8 + b) * 256 + ((a1 >> (8 * b)) & 0xff)];
+      n0 ^= ((uint64_t)v.y << 32) | v.x;
+      n1 ^= ((uint64_t)v.w << 32) | v.z;
+    }
+    states[2 * c] = n0;
+    states[2 * c + 1] = n1;
+  }
+}
+
+// x[i] *= bit(base + i) ? scale : 0   (Dropout::forward on a grad-carrying variable and
+// Dropout::backward on its grad; hpdga module.cpp:215, :226).
+__device__ __forceinline__ uint32_t mask_bits4(const uint64_t *__restrict__ mask, long long idx) {
+  const long long w = idx >> 6;
+  const int sh = (int)(idx & 63);
+  uint64_t v = mask[w] >> sh;
+  if (sh > 60) v |= mask[w + 1] << (64 - sh);
+  return (uint32_t)v & 0xfu;
+}
+
+__global__ __launch_bounds__(256) void k_dropout_apply(float *__restrict__ x, long long n,
+                                                       const uint64_t *__restrict__ mask,
+                                                       long long base, float scale) {
+  const long long n4 = n >> 2;
+  for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < n4;
+       q += (long long)gridDim.x * blockDim.x) {
+    const long long i = q << 2;
+    const uint32_t bits = mask_bits4(mask, base + i);
+    float4 v = reinterpret_cast<float4 *>(x)[q];
+    v.x *= (bits & 1) ? scale : 0.0f;
+    v.y *= (bits & 2) ? scale : 0.0f;
+    v.z *= (bits & 4) ? scale : 0.0f;
+    v.w *= (bits & 8) ? scale : 0.0f;
+    reinterpret_cast<float4 *>(x)[q] = v;
+  }
+  if (blockIdx.x == 0) {
+    for (long long i = (n4 << 2) + threadIdx.x; i < n; i += blockDim.x) {
+      const long long b = base + i;
+      x[i] *= ((mask[b >> 6] >> (b & 63)) & 1) ? scale : 0.0f;
+    }
+  }
+}
+
+// ReLU (hpdga module.cpp:173-188)
+__global__ __launch_bounds__(256) void k_relu_fwd(float *__restrict__ x, long long n,
+                                                  uint8_t *__restrict__ mask, int training) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const float v = x[i];
+    const bool keep = v > 0.0f;
+    if (training) mask[i] = keep;
+    if (!keep) x[i] = 0.0f;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_relu_bwd(float *__restrict__ g, long long n,
+                                                  const uint8_t *__restrict__ mask) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    if (!mask[i]) g[i] = 0.0f;
+}
+
+// ------------------------------------------------------------------------------------------
+// Block reductions (wave64 shuffles, fixed tree => deterministic)
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+template <int BLOCK>
+__device__ __forceinline__ float block_sum(float v, float *smem) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) smem[w] = v;
+  __syncthreads();
+  float r = 0.0f;
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int i = 0; i < BLOCK / 64; i++) r += smem[i];
+  }
+  return r;  // valid in thread 0
+}
+
+// ------------------------------------------------------------------------------------------
+// Cross entropy (hpdga module.cpp:122-153) + accuracy (hpdga gcn.cpp:150-164), one thread
+// per row. Labelled rows are max-shifted in place like the reference; the grad is written
+// divided by the labelled count (known per split on the host). Per-block partial sums
+// (loss, wrong) go to partials[2*block].
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_xent_fwd(float *__restrict__ logits, int ld,
+                                                  float *__restrict__ grad,
+                                                  const int *__restrict__ truth, int n, int c,
+                                                  float inv_count_f, int count, int training,
+                                                  float *__restrict__ partials) {
+  __shared__ float red[4];
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  float loss = 0.0f, wrong = 0.0f;
+  if (i < n) {
+    const int t = truth[i];
+    float *l = logits + (long long)i * ld;
+    float *g = grad ? grad + (long long)i * ld : nullptr;
+    if (t >= 0) {
+      float mx = -1e30f;
+      for (int j = 0; j < c; j++) mx = fmaxf(mx, l[j]);
+      float se = 0.0f;
+      for (int j = 0; j < c; j++) {
+        const float v = l[j] - mx;
+        l[j] = v;
+        se += expf(v);
+      }
+      const float lt = l[t];
+      loss = logf(se) - lt;
+      bool w = false;
+      for (int j = 0; j < c; j++) w |= l[j] > lt;
+      wrong = w ? 1.0f : 0.0f;
+      if (training) {
+        for (int j = 0; j < c; j++) {
+          float prob = expf(l[j]) / se;
+          if (j == t) prob = (float)((double)prob - 1.0);  // hpdga module.cpp:145 (double temp)
+          g[j] = prob / (float)count;
+        }
+        for (int j = c; j < ld; j++) g[j] = 0.0f;
+      }
+    } else if (training) {
+      for (int j = 0; j < ld; j++) g[j] = 0.0f;
+    }
+  }
+  (void)inv_count_f;
+  const float ls = block_sum<256>(loss, red);
+  const float ws = block_sum<256>(wrong, red);
+  if (threadIdx.x == 0) {
+    partials[2 * blockIdx.x] = ls;
+    partials[2 * blockIdx.x + 1] = ws;
+  }
+}
+
+// sums[0] = sum loss partials, sums[1] = sum wrong, sums[2] = sum w^2 (fixed order)
+__global__ __launch_bounds__(256) void k_reduce_scalars(const float *__restrict__ partials,
+                                                        int n_blocks,
+                                                        const float *__restrict__ w,
+                                                        long long n_w, float *__restrict__ sums) {
+  __shared__ float red[4];
+  float l = 0.0f, wr = 0.0f, q = 0.0f;
+  for (int b = threadIdx.x; b < n_blocks; b += blockDim.x) {
+    l += partials[2 * b];
+    wr += partials[2 * b + 1];
+  }
+  for (long long i = threadIdx.x; i < n_w; i += blockDim.x) {
+    const float x = w[i];
+    q += x * x;
+  }
+  l = block_sum<256>(l, red);
+  wr = block_sum<256>(wr, red);
+  q = block_sum<256>(q, red);
+  if (threadIdx.x == 0) {
+    sums[0] = l;
+    sums[1] = wr;
+    sums[2] = q;
+  }
+}
+
+// out2 = {loss_sum/count + wd*l2/2, (count-wrong)/count}   (hpdga gcn.cpp:167-198)
+__global__ void k_compose(const float *__restrict__ sums, int count, float wd,
+                          float *__restrict__ out2) {
+  if (threadIdx.x == 0) {
+    const float loss = sums[0] / (float)count;
+    const float l2 = wd * sums[2] / 2.0f;
+    out2[0] = loss + l2;
+    const int wrong = (int)sums[1];
+    out2[1] = (float)(count - wrong) / (float)count;
+  }
+}
+
+// Adam (hpdga optim.cpp:25-33): double temporaries where the reference has them.
+__global__ __launch_bounds__(256) void k_adam(float *__restrict__ w, const float *__restrict__ g,
+                                              float *__restrict__ m, float *__restrict__ v,
+                                              long long n, float step_size, float beta1,
+                                              float beta2, float eps, float wd, int decay) {
+  const double ob1 = 1.0 - (double)beta1, ob2 = 1.0 - (double)beta2;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    float grad = g[i];
+    const float wi = w[i];
+    if (decay) grad += wd * wi;
+    const float mi = (float)((double)(beta1 * m[i]) + ob1 * (double)grad);
+    const float vi = (float)((double)(beta2 * v[i]) + (ob2 * (double)grad) * (double)grad);
+    m[i] = mi;
+    v[i] = vi;
+    w[i] = wi - step_size * mi / (sqrtf(vi) + eps);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------------
+static int grid_for(long long work, int block = 256, int cap = 2048) {
+  long long g = ceil_div(work, block);
+  if (g < 1) g = 1;
+  return (int)(g > cap ? cap : g);
+}
+
+void launch_dropout_mask(uint64_t *states, long long n_chunks, long long elem0,
+                         long long elem_end, float p, uint64_t *mask, const void *table,
+                         hipStream_t s) {
+  if (n_chunks <= 0) return;
+  // hpdga module.cpp:211: threshold = int(p * MY_RAND_MAX) evaluated in float
+  const int threshold = (int)(p * (float)0x7fffffff);
+  const int grid = grid_for(n_chunks, 256, 1024);
+  hipLaunchKernelGGL(k_dropout_mask, dim3(grid), dim3(256), 0, s, states, n_chunks, elem0,
+                     elem_end, threshold, mask, static_cast<const uint4 *>(table));
+}
+
+void launch_dropout_apply_based(float *x, long long n, const uint64_t *mask, long long base,
+                                float scale, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_dropout_apply, dim3(grid_for(ceil_div(n, 4))), dim3(256), 0, s, x, n,
+                     mask, base, scale);
+}
+
+void launch_relu_fwd(float *x, long long n, uint8_t *mask, int training, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_relu_fwd, dim3(grid_for(n)), dim3(256), 0, s, x, n, mask, training);
+}
+
+void launch_relu_bwd(float *g, long long n, const uint8_t *mask, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_relu_bwd, dim3(grid_for(n)), dim3(256), 0, s, g, n, mask);
+}
+
+int xent_blocks(int n) { return (int)ceil_div(n, 256); }
+
+void launch_xent_fwd(float *logits, int ld, float *grad, const int *truth, int n, int c,
+                     int count, int training, float *partials, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_xent_fwd, dim3(xent_blocks(n)), dim3(256), 0, s, logits, ld, grad,
+                     truth, n, c, 1.0f / (float)(count > 0 ? count : 1), count, training,
+                     partials);
+}
+
+void launch_reduce_scalars(const float *partials, int n_blocks, const float *w, long long n_w,
+                           float *sums, hipStream_t s) {
+  hipLaunchKernelGGL(k_reduce_scalars, dim3(1), dim3(256), 0, s, partials, n_blocks, w, n_w,
+                     sums);
+}
+
+void launch_compose(const float *sums, int count, float wd, float *out2, hipStream_t s) {
+  hipLaunchKernelGGL(k_compose, dim3(1), dim3(64), 0, s, sums, count, wd, out2);
+}
+
+void launch_adam(float *w, const float *g, float *m, float *v, long long n, float step_size,
+                 float beta1, float beta2, float eps, float wd, int decay, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_adam, dim3(grid_for(n)), dim3(256), 0, s, w, g, m, v, n, step_size,
+                     beta1, beta2, eps, wd, decay);
+}
+
+}  // namespace pgcn

@@ -1,0 +1,274 @@
+// parallel-gcn_amd/csrc/k_gemm.hip -- the "XW" contractions on fp32 MFMA for gfx950.
+//
+// Replaces matmul_kernel_forward / matmul_kernel_backward_1 / matmul_kernel_backward_2
+// (src/module.cu:274-472; 16x16 CUDA-core tiles + float atomics) and, for dense feature
+// matrices (reddit), sparse_matmul_kernel_forward/backward (:108-163).
+//
+// All use v_mfma_f32_16x16x4_f32 (exact fp32 inputs, fp32 accumulate). Fragment maps
+// (cdna_hip_programming.md §3): A[i=l&15][k=l>>4], B[k=l>>4][j=l&15],
+// C/D[row=4*(l>>4)+r][col=l&15].
+//
+//  k_gemm_nn : C[M,N] = drop(A)[M,K] * B   -- A streamed once from HBM straight into
+//              registers (a wave owns 16 rows and ALL output columns, so A has no reuse
+//              and needs no LDS); B (the small weight) is staged in LDS in K chunks and
+//              shared by the block's waves.  The K index inside a 16-wide step is permuted
+//              so every lane issues one 16-byte load per step (A[row][k0+4g .. k0+4g+3]).
+//  k_gemm_tn : C[K,N] = drop(A)[M,K]^T * G[M,N] -- the long M reduction is split into row
+//              slabs; each block writes its slab's partial [K,N] and k_gemm_tn_reduce adds
+//              the slabs in slab order => deterministic (no float atomics).
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace pgcn {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+// 4 dropout bits for elements idx..idx+3 (may straddle a 64-bit word)
+__device__ __forceinline__ uint32_t mask4(const uint64_t *__restrict__ mask, long long idx) {
+  const long long w = idx >> 6;
+  const int sh = (int)(idx & 63);
+  uint64_t v = mask[w] >> sh;
+  if (sh > 60) v |= mask[w + 1] << (64 - sh);
+  return (uint32_t)v & 0xfu;
+}
+
+// ------------------------------------------------------------------------------------------
+// NN: block = 4 waves x 16 rows = 64 rows; NT output tiles of 16 columns per wave.
+// ------------------------------------------------------------------------------------------
+template <int NT>
+__global__ __launch_bounds__(256) void k_gemm_nn(int M, int N, int K,
+                                                 const float *__restrict__ A, int lda,
+                                                 const float *__restrict__ B, int ldb,
+                                                 int trans_b, float *__restrict__ C, int ldc,
+                                                 const uint64_t *__restrict__ a_mask,
+                                                 long long mask_base, long long mask_ld,
+                                                 float a_scale) {
+  constexpr int KC = 64;               // K rows of B per LDS chunk
+  constexpr int S = 16 * NT + 4;       // LDS row stride (== 4 mod 8: conflict-free reads)
+  __shared__ float bs[KC * S];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int g = lane >> 4, i = lane & 15;
+  const long long row = (long long)blockIdx.x * 64 + w * 16 + i;  // A row this lane loads
+  const bool row_ok = row < M;
+  const float *arow = A + (row_ok ? row : 0) * (long long)lda;
+  floatx4 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; t++) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  for (int k0 = 0; k0 < K; k0 += KC) {
+    __syncthreads();
+    // stage B[k0:k0+KC, 0:16NT] (zero outside [K, N])
+    for (int e = threadIdx.x; e < KC * 16 * NT; e += 256) {
+      const int kk = e / (16 * NT), j = e - kk * (16 * NT);
+      const int k = k0 + kk;
+      float val = 0.0f;
+      if (k < K && j < N) val = trans_b ? B[(long long)j * ldb + k] : B[(long long)k * ldb + j];
+      bs[kk * S + j] = val;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < KC / 16; s++) {
+      const int kb = k0 + 16 * s + 4 * g;  // this lane's 4 consecutive k
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (row_ok && kb < K) {
+        a = *reinterpret_cast<const float4 *>(arow + kb);
+        if (kb + 3 >= K) {
+          if (kb + 1 >= K) a.y = 0.f;
+          if (kb + 2 >= K) a.z = 0.f;
+          if (kb + 3 >= K) a.w = 0.f;
+        }
+        if (a_mask) {
+          const uint32_t bits = mask4(a_mask, mask_base + row * mask_ld + kb);
+          a.x *= (bits & 1) ? a_scale : 0.0f;
+          a.y *= (bits & 2) ? a_scale : 0.0f;
+          a.z *= (bits & 4) ? a_scale : 0.0f;
+          a.w *= (bits & 8) ? a_scale : 0.0f;
+        }
+      }
+      const float *brow = bs + (16 * s + 4 * g) * S + i;
+#pragma unroll
+      for (int t = 0; t < NT; t++) {
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, brow[0 * S + 16 * t], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, brow[1 * S + 16 * t], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, brow[2 * S + 16 * t], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, brow[3 * S + 16 * t], acc[t], 0, 0, 0);
+      }
+    }
+  }
+  // store: lane holds C[row0 + 4g + r][16t + i]
+  const long long crow0 = (long long)blockIdx.x * 64 + w * 16 + 4 * g;
+#pragma unroll
+  for (int t = 0; t < NT; t++) {
+    const int col = 16 * t + i;
+    if (col >= ldc) continue;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const long long rr = crow0 + r;
+      if (rr < M) C[rr * ldc + col] = acc[t][r];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// TN split-M: grid (slabs, k-groups). Block = 4 waves; wave w owns k-tiles
+// kt = kg*4*KTW + w + 4*q (q < KTW) and all NJ column tiles.
+// ------------------------------------------------------------------------------------------
+template <int NJ, int KTW>
+__global__ __launch_bounds__(256) void k_gemm_tn(int M, int N, int K, int slab,
+                                                 const float *__restrict__ A, int lda,
+                                                 const float *__restrict__ G, int ldg,
+                                                 const uint64_t *__restrict__ a_mask,
+                                                 long long mask_base, long long mask_ld,
+                                                 float a_scale, float *__restrict__ partial,
+                                                 int ldp) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int g = lane >> 4, i = lane & 15;
+  const long long m_begin = (long long)blockIdx.x * slab;
+  long long m_end = m_begin + slab;
+  if (m_end > M) m_end = M;
+  int kcol[KTW];
+#pragma unroll
+  for (int q = 0; q < KTW; q++) kcol[q] = ((int)blockIdx.y * 4 * KTW + w + 4 * q) * 16 + i;
+  floatx4 acc[KTW][NJ];
+#pragma unroll
+  for (int q = 0; q < KTW; q++)
+#pragma unroll
+    for (int t = 0; t < NJ; t++) acc[q][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  for (long long m = m_begin; m < m_end; m += 4) {
+    const long long mr = m + g;  // this lane's row of the reduction step
+    const bool ok = mr < m_end;
+    float b[NJ];
+#pragma unroll
+    for (int t = 0; t < NJ; t++) {
+      const int col = 16 * t + i;
+      b[t] = (ok && col < N) ? G[mr * ldg + col] : 0.0f;
+    }
+#pragma unroll
+    for (int q = 0; q < KTW; q++) {
+      const int k = kcol[q];
+      float a = 0.0f;
+      if (ok && k < K) {
+        a = A[mr * lda + k];
+        if (a_mask) {
+          const long long bi = mask_base + mr * mask_ld + k;
+          a *= ((a_mask[bi >> 6] >> (bi & 63)) & 1) ? a_scale : 0.0f;
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < NJ; t++)
+        acc[q][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b[t], acc[q][t], 0, 0, 0);
+    }
+  }
+  // partial[slab][k][j], k = ktile*16 + 4g + r, j = 16t + i
+  float *p = partial + (long long)blockIdx.x * K * ldp;
+#pragma unroll
+  for (int q = 0; q < KTW; q++) {
+    const int kt = (int)blockIdx.y * 4 * KTW + w + 4 * q;
+#pragma unroll
+    for (int t = 0; t < NJ; t++) {
+      const int col = 16 * t + i;
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int k = kt * 16 + 4 * g + r;
+        if (k < K && col < ldp) p[(long long)k * ldp + col] = acc[q][t][r];
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_gemm_tn_reduce(const float *__restrict__ partial,
+                                                        int n_slabs, int K, int N, int ldp,
+                                                        float *__restrict__ C, int ldc) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long long)K * ldp) return;
+  const int k = (int)(e / ldp), j = (int)(e - (long long)k * ldp);
+  float s = 0.0f;
+  for (int b = 0; b < n_slabs; b++) s += partial[(long long)b * K * ldp + e];
+  if (j < ldc) C[(long long)k * ldc + j] = j < N ? s : 0.0f;
+}
+
+// ------------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------------
+void launch_gemm_nn(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
+                    int trans_b, float *C, int ldc, const uint64_t *a_mask, long long mask_base,
+                    long long mask_ld, float a_scale, hipStream_t s) {
+  PGCN_CHECK(lda % 4 == 0 && lda >= K, PGCN_E_INVALID, "gemm: lda must be a multiple of 4 >= K");
+  PGCN_CHECK(N <= 128 && N >= 1, PGCN_E_INVALID, "gemm: N must be in [1,128]");
+  if (M <= 0) return;
+  const int nt = (N + 15) / 16;
+  const dim3 grid((unsigned)ceil_div(M, 64)), block(256);
+#define NN_CASE(T)                                                                            \
+  case T:                                                                                     \
+    hipLaunchKernelGGL(k_gemm_nn<T>, grid, block, 0, s, M, N, K, A, lda, B, ldb, trans_b, C, \
+                       ldc, a_mask, mask_base, mask_ld, a_scale);                             \
+    break;
+  switch (nt) {
+    NN_CASE(1) NN_CASE(2) NN_CASE(3) NN_CASE(4) NN_CASE(5) NN_CASE(6) NN_CASE(7) NN_CASE(8)
+  }
+#undef NN_CASE
+}
+
+struct TnPlan {
+  int nj, ktw, kgroups, slab, n_slabs, ldp;
+};
+
+static TnPlan tn_plan(int M, int N, int K) {
+  TnPlan p;
+  p.nj = (N + 15) / 16;
+  p.ldp = p.nj * 16;
+  const int kt = (K + 15) / 16;
+  // keep KTW*NJ*4 accumulators <= 64 VGPRs per lane
+  p.ktw = p.nj >= 8 ? 2 : (p.nj >= 4 ? 4 : (p.nj >= 2 ? 4 : 4));
+  if (p.ktw * 4 > kt) p.ktw = (kt + 3) / 4;
+  if (p.ktw < 1) p.ktw = 1;
+  p.kgroups = (kt + 4 * p.ktw - 1) / (4 * p.ktw);
+  // aim for >= ~1024 blocks over (slabs x kgroups), slabs >= 256 rows
+  long long target = 1024 / p.kgroups;
+  if (target < 1) target = 1;
+  long long slab = ceil_div(M, target);
+  slab = (slab + 3) / 4 * 4;
+  if (slab < 256) slab = 256;
+  p.slab = (int)slab;
+  p.n_slabs = (int)ceil_div(M, slab);
+  if (p.n_slabs < 1) p.n_slabs = 1;
+  return p;
+}
+
+size_t gemm_tn_workspace(int M, int N, int K) {
+  const TnPlan p = tn_plan(M, N, K);
+  return (size_t)p.n_slabs * (size_t)K * (size_t)p.ldp * sizeof(float);
+}
+
+void launch_gemm_tn(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
+                    float *C, int ldc, const uint64_t *a_mask, long long mask_base,
+                    long long mask_ld, float a_scale, void *workspace, hipStream_t s) {
+  PGCN_CHECK(N <= 128 && N >= 1, PGCN_E_INVALID, "gemm_tn: N must be in [1,128]");
+  const TnPlan p = tn_plan(M, N, K);
+  float *partial = static_cast<float *>(workspace);
+  if (M > 0) {
+    const dim3 grid((unsigned)p.n_slabs, (unsigned)p.kgroups), block(256);
+#define TN_CASE(NJ, KTW)                                                                    \
+  if (p.nj == NJ && p.ktw == KTW) {                                                         \
+    hipLaunchKernelGGL((k_gemm_tn<NJ, KTW>), grid, block, 0, s, M, N, K, p.slab, A, lda, G, \
+                       ldg, a_mask, mask_base, mask_ld, a_scale, partial, p.ldp);           \
+  } else
+    TN_CASE(1, 4) TN_CASE(1, 3) TN_CASE(1, 2) TN_CASE(1, 1)
+    TN_CASE(2, 4) TN_CASE(2, 3) TN_CASE(2, 2) TN_CASE(2, 1)
+    TN_CASE(3, 4) TN_CASE(3, 3) TN_CASE(3, 2) TN_CASE(3, 1)
+    TN_CASE(4, 4) TN_CASE(4, 3) TN_CASE(4, 2) TN_CASE(4, 1)
+    TN_CASE(5, 4) TN_CASE(5, 3) TN_CASE(5, 2) TN_CASE(5, 1)
+    TN_CASE(6, 4) TN_CASE(6, 3) TN_CASE(6, 2) TN_CASE(6, 1)
+    TN_CASE(7, 4) TN_CASE(7, 3) TN_CASE(7, 2) TN_CASE(7, 1)
+    TN_CASE(8, 2) TN_CASE(8, 1) {
+      throw Error(PGCN_E_INVALID, "gemm_tn: no kernel for this shape");
+    }
+#undef TN_CASE
+  }
+  const long long elems = (long long)K * p.ldp;
+  hipLaunchKernelGGL(k_gemm_tn_reduce, dim3((unsigned)ceil_div(elems, 256)), dim3(256), 0, s,
+                     partial, M > 0 ? p.n_slabs : 0, K, N, p.ldp, C, ldc);
+}
+
+}  // namespace pgcn

@@ -1,0 +1,59 @@
+// parallel-gcn_amd/csrc/kernels.hpp -- internal launcher interface of the HIP kernels.
+// (C ABI wrappers in capi.cpp; host classes in host/*.)
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace pgcn {
+
+// GraphSum work schedule for one row width (VEC float4 per row); device arrays.
+struct GraphSchedule {
+  int vec = 0;
+  int chunk = 0;          // max slots per work item
+  int n_items = 0;        // int4 {row, begin, end, slot(-1 = direct)}
+  int n_comb = 0;         // int4 {row, first_slot, count, 0}
+  long long n_slots = 0;  // partial rows (VEC float4 each)
+  const int4 *items = nullptr;
+  const int4 *comb = nullptr;
+};
+
+void launch_graphsum(const GraphSchedule &s, const int *indices, const float *vals,
+                     const float *in, int ld_in, float *out, int ld_out, float *partial,
+                     hipStream_t st);
+bool graphsum_vec_supported(int vec);
+
+void launch_gemm_nn(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
+                    int trans_b, float *C, int ldc, const uint64_t *a_mask, long long mask_base,
+                    long long mask_ld, float a_scale, hipStream_t s);
+size_t gemm_tn_workspace(int M, int N, int K);
+void launch_gemm_tn(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
+                    float *C, int ldc, const uint64_t *a_mask, long long mask_base,
+                    long long mask_ld, float a_scale, void *workspace, hipStream_t s);
+
+void launch_spmm_csr(int m, int p, int ldc, const int *indptr, const int *indices,
+                     const float *a, const uint64_t *mask, long long mask_base, float scale,
+                     const float *b, float *c, hipStream_t s);
+void launch_spmm_csc_bwd(int nf, int p, int ldg, const int *csc_ptr, const int *csc_row,
+                         const int *csc_pos, const float *a, const uint64_t *mask,
+                         long long mask_base, float scale, const float *cgrad, float *bgrad,
+                         hipStream_t s);
+
+void launch_dropout_mask(uint64_t *states, long long n_chunks, long long elem0,
+                         long long elem_end, float p, uint64_t *mask, const void *table,
+                         hipStream_t s);
+void launch_dropout_apply_based(float *x, long long n, const uint64_t *mask, long long base,
+                                float scale, hipStream_t s);
+void launch_relu_fwd(float *x, long long n, uint8_t *mask, int training, hipStream_t s);
+void launch_relu_bwd(float *g, long long n, const uint8_t *mask, hipStream_t s);
+int xent_blocks(int n);
+void launch_xent_fwd(float *logits, int ld, float *grad, const int *truth, int n, int c,
+                     int count, int training, float *partials, hipStream_t s);
+void launch_reduce_scalars(const float *partials, int n_blocks, const float *w, long long n_w,
+                           float *sums, hipStream_t s);
+void launch_compose(const float *sums, int count, float wd, float *out2, hipStream_t s);
+void launch_adam(float *w, const float *g, float *m, float *v, long long n, float step_size,
+                 float beta1, float beta2, float eps, float wd, int decay, hipStream_t s);
+
+}  // namespace pgcn

@@ -1,0 +1,34 @@
+import os
+import sys
+
+import pytest
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+import helpers  # noqa: E402
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
+
+
+@pytest.fixture(scope="session")
+def datasets(tmp_path_factory):
+    """Root directory holding data/<name>.* for cora, citeseer and pubmed (synthetic
+    features), materialised from tests/golden/data."""
+    root = str(tmp_path_factory.mktemp("datasets"))
+    names = {}
+    for n in ("cora", "citeseer", "pubmed_synth"):
+        names[n] = helpers.materialize_dataset(n, root)
+    return root, names
+
+
+@pytest.fixture(scope="session")
+def pgcn():
+    return helpers.pgcn()
+
+
+@pytest.fixture(scope="session")
+def loaded(datasets, pgcn):
+    root, names = datasets
+    return {k: pgcn.Dataset.load(root, v) for k, v in names.items()}

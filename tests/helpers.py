@@ -1,0 +1,189 @@
+"""Test helpers: load the engine package, the C oracle, the reference build, the fixtures.
+
+The oracle (oracle/liboracle.so, oracle/_ref/libhpdga_ref.so) is test infrastructure: it is
+loaded here, by __graft_entry__.smoke() and by bench.py's cpu_baseline leg only.
+"""
+import ctypes
+import gzip
+import importlib.util
+import os
+import shutil
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(REPO, "tests", "golden")
+ORACLE_SO = os.path.join(REPO, "oracle", "liboracle.so")
+REF_SO = os.path.join(REPO, "oracle", "_ref", "libhpdga_ref.so")
+
+_pkg = None
+
+
+def pgcn():
+    """The engine's Python glue (parallel-gcn_amd/__init__.py); raises if not built."""
+    global _pkg
+    if _pkg is None:
+        path = os.path.join(REPO, "parallel-gcn_amd", "__init__.py")
+        spec = importlib.util.spec_from_file_location("pgcn_amd", path)
+        mod = importlib.util.module_from_spec(spec)
+        sys.modules["pgcn_amd"] = mod
+        spec.loader.exec_module(mod)
+        _pkg = mod
+    return _pkg
+
+
+# --------------------------------------------------------------------------- oracle
+class OrParams(ctypes.Structure):
+    _fields_ = [("num_nodes", ctypes.c_int), ("input_dim", ctypes.c_int),
+                ("output_dim", ctypes.c_int), ("n_layers", ctypes.c_int),
+                ("hidden_dims", ctypes.c_int * 16), ("dropouts", ctypes.c_float * 16),
+                ("lr", ctypes.c_float), ("weight_decay", ctypes.c_float),
+                ("beta1", ctypes.c_float), ("beta2", ctypes.c_float), ("eps", ctypes.c_float)]
+
+
+_oracle = None
+
+
+def oracle():
+    global _oracle
+    if _oracle is None:
+        if not os.path.exists(ORACLE_SO):
+            import subprocess
+            subprocess.run(["make", "-C", os.path.join(REPO, "oracle")], check=True,
+                           stdout=subprocess.DEVNULL)
+        lib = ctypes.CDLL(ORACLE_SO)
+        vp, ip, fp = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+        lib.or_gcn_create.restype = vp
+        lib.or_gcn_create.argtypes = [ctypes.POINTER(OrParams)] + [vp] * 7
+        lib.or_gcn_get_var.restype = ctypes.c_long
+        lib.or_gcn_get_var.argtypes = [vp, ip, ip, vp]
+        lib.or_gcn_train_epoch.argtypes = [vp, vp]
+        lib.or_gcn_eval.argtypes = [vp, ip, vp]
+        lib.or_gcn_free.argtypes = [vp]
+        lib.or_gcn_rng_state.argtypes = [vp, vp]
+        lib.or_gcn_num_vars.argtypes = [vp]
+        lib.or_rng_next.restype = ctypes.c_uint32
+        lib.or_rng_next.argtypes = [vp]
+        lib.or_graph_coef.restype = fp
+        lib.or_xent_fwd.restype = fp
+        lib.or_accuracy.restype = fp
+        lib.or_l2_penalty.restype = fp
+        lib.or_adam_step_size.restype = fp
+        lib.or_adam_step_size.argtypes = [fp, fp, fp, ip]
+        _oracle = lib
+    return _oracle
+
+
+def ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class OracleGCN:
+    """The C restatement of hpdga's GCN (L layers; L = 2 is exactly the reference)."""
+
+    def __init__(self, ds, hidden_dims=(16,), dropouts=(0.5, 0.5), lr=0.01, wd=5e-4):
+        lib = oracle()
+        p = OrParams()
+        p.num_nodes, p.input_dim, p.output_dim = ds["n"], ds["f"], ds["c"]
+        p.n_layers = len(hidden_dims) + 1
+        for i, h in enumerate(hidden_dims):
+            p.hidden_dims[i] = h
+        for i, d in enumerate(dropouts):
+            p.dropouts[i] = d
+        p.lr, p.weight_decay, p.beta1, p.beta2, p.eps = lr, wd, 0.9, 0.999, 1e-8
+        self._keep = [np.ascontiguousarray(ds[k]) for k in
+                      ("graph_indptr", "graph_indices", "feat_indptr", "feat_indices",
+                       "feat_values", "label", "split")]
+        self.h = lib.or_gcn_create(ctypes.byref(p), *[ptr(a) for a in self._keep])
+        self.lib = lib
+
+    def train_epoch(self):
+        out = np.zeros(2, np.float32)
+        self.lib.or_gcn_train_epoch(self.h, ptr(out))
+        return float(out[0]), float(out[1])
+
+    def eval(self, split):
+        out = np.zeros(2, np.float32)
+        self.lib.or_gcn_eval(self.h, split, ptr(out))
+        return float(out[0]), float(out[1])
+
+    def var(self, idx, which=0):
+        n = self.lib.or_gcn_get_var(self.h, idx, which, None)
+        out = np.zeros(max(n, 0), np.float32)
+        if n > 0:
+            self.lib.or_gcn_get_var(self.h, idx, which, ptr(out))
+        return out
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.lib.or_gcn_free(self.h)
+            self.h = None
+
+
+def ds_dict(ds):
+    """pgcn Dataset -> plain dict of arrays for the oracle."""
+    return {"n": ds.num_nodes, "f": ds.input_dim, "c": ds.output_dim,
+            "graph_indptr": ds.graph_indptr, "graph_indices": ds.graph_indices,
+            "feat_indptr": ds.feat_indptr, "feat_indices": ds.feat_indices,
+            "feat_values": ds.feat_values, "label": ds.label, "split": ds.split}
+
+
+# --------------------------------------------------------------------------- reference
+_ref = None
+
+
+def ref_lib():
+    """oracle/_ref/libhpdga_ref.so: the reference's own sequential sources (None if absent)."""
+    global _ref
+    if _ref is None and os.path.exists(REF_SO):
+        lib = ctypes.CDLL(REF_SO)
+        vp, ip, fp, ll = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_longlong
+        lib.ref_create.restype = vp
+        lib.ref_create.argtypes = [ip, ip, ip, ip, fp, fp, fp, ip, vp, vp, ll, vp, vp, vp, ll, vp, vp]
+        lib.ref_train_epoch.argtypes = [vp, vp]
+        lib.ref_eval.argtypes = [vp, ip, vp]
+        lib.ref_get_var.restype = ll
+        lib.ref_get_var.argtypes = [vp, ip, ip, vp]
+        lib.ref_free.argtypes = [vp]
+        _ref = lib
+    return _ref
+
+
+# --------------------------------------------------------------------------- fixtures
+def golden(name):
+    return np.load(os.path.join(GOLDEN, f"{name}.npz"))
+
+
+def golden_lines(name):
+    return open(os.path.join(GOLDEN, f"{name}_epoch_lines.txt")).read().splitlines()
+
+
+def materialize_dataset(name, dest):
+    """Write data/<ds>.{graph,split,svmlight} under dest from the committed fixtures.
+    name: cora | citeseer | pubmed_synth (pubmed graph/split + seeded synthetic features)."""
+    data = os.path.join(dest, "data")
+    os.makedirs(data, exist_ok=True)
+    src = os.path.join(GOLDEN, "data")
+    if name == "pubmed_synth":
+        for ext in ("graph", "split"):
+            with gzip.open(os.path.join(src, f"pubmed.{ext}.gz")) as fi, \
+                    open(os.path.join(data, f"pubmed.{ext}"), "wb") as fo:
+                shutil.copyfileobj(fi, fo)
+        sys.path.insert(0, GOLDEN)
+        import make_golden
+        make_golden.pubmed_synth_svmlight(os.path.join(data, "pubmed.svmlight"))
+        return "pubmed"
+    for ext in ("graph", "split", "svmlight"):
+        with gzip.open(os.path.join(src, f"{name}.{ext}.gz")) as fi, \
+                open(os.path.join(data, f"{name}.{ext}"), "wb") as fo:
+            shutil.copyfileobj(fi, fo)
+    return name
+
+
+def parse_line(line):
+    out = {}
+    for tok in line.split():
+        k, v = tok.split("=")
+        out[k] = float(v)
+    return out
