@@ -28,6 +28,9 @@ import sys
 import time
 
 import numpy as np
+# torch before libpgcn.so: its bundled HIP runtime / RCCL (same SONAMEs) then serve both,
+# so the process holds one HIP runtime.  torch is only control plumbing here.
+import torch  # noqa: F401
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "tests"))

@@ -132,9 +132,14 @@ typedef struct {
   float dropouts[PGCN_MAX_LAYERS];       /* n_layers */
   int epochs, early_stopping;
   float learning_rate, weight_decay, beta1, beta2, eps;
+  /* 1: compute the output layer as (Â H) W instead of Â (H W) when hidden < classes, so its
+   * GraphSum gathers hidden-width rows.  Exact algebra (Â symmetric); only the fp32
+   * rounding order differs from the reference.  0: the reference's module order. */
+  int reassociate_last;
 } pgcn_params;
 
-/* hpdga defaults: 2 layers, hidden 16, dropout .5/.5, 100 epochs, Adam lr .01, wd 5e-4 */
+/* hpdga defaults: 2 layers, hidden 16, dropout .5/.5, 100 epochs, Adam lr .01, wd 5e-4,
+ * reassociate_last = 1 */
 void pgcn_params_default(pgcn_params *p);
 
 /* GCNData in host memory (include/gcn.cuh:51-58): CSRs as the hpdga Parser builds them. */

@@ -40,7 +40,7 @@ class PgcnParams(ctypes.Structure):
                 ("n_layers", c_int), ("hidden_dims", c_int * MAX_LAYERS),
                 ("dropouts", c_float * MAX_LAYERS), ("epochs", c_int), ("early_stopping", c_int),
                 ("learning_rate", c_float), ("weight_decay", c_float), ("beta1", c_float),
-                ("beta2", c_float), ("eps", c_float)]
+                ("beta2", c_float), ("eps", c_float), ("reassociate_last", c_int)]
 
 
 class PgcnData(ctypes.Structure):
@@ -179,9 +179,11 @@ class Dataset:
 
 
 def make_params(ds, hidden_dims=(16,), dropouts=(0.5, 0.5), epochs=100, early_stopping=0,
-                learning_rate=0.01, weight_decay=5e-4, beta1=0.9, beta2=0.999, eps=1e-8):
+                learning_rate=0.01, weight_decay=5e-4, beta1=0.9, beta2=0.999, eps=1e-8,
+                reassociate_last=True):
     p = PgcnParams()
     lib.pgcn_params_default(ctypes.byref(p))
+    p.reassociate_last = 1 if reassociate_last else 0
     p.num_nodes, p.input_dim, p.output_dim = ds.num_nodes, ds.input_dim, ds.output_dim
     p.n_layers = len(hidden_dims) + 1
     assert len(dropouts) == p.n_layers

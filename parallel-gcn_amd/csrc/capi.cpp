@@ -39,6 +39,7 @@ GCNParams to_params(const pgcn_params *p, const pgcn_data *d) {
   q.dropouts.assign(p->dropouts, p->dropouts + std::max(0, p->n_layers));
   q.epochs = p->epochs;
   q.early_stopping = p->early_stopping;
+  q.reassociate_last = p->reassociate_last != 0;
   return q;
 }
 AdamParams to_adam(const pgcn_params *p) {
@@ -91,7 +92,7 @@ int pgcn_graph_create(int n, const int *indptr, const int *indices, pgcn_graph *
     check_device();
     std::vector<float> v = graph_coefs(n, indptr, indices);
     auto h = std::make_unique<pgcn_graph>();
-    h->g = std::make_unique<DevGraph>(n, indptr, indices, v.data());
+    h->g = std::make_unique<DevGraph>(n, n, indptr, indices, v.data());
     *out = h.release();
   });
 }
@@ -240,6 +241,7 @@ void pgcn_params_default(pgcn_params *p) {
   p->beta1 = 0.9f;
   p->beta2 = 0.999f;
   p->eps = 1e-8f;
+  p->reassociate_last = 1;
 }
 
 int pgcn_gcn_create(const pgcn_params *p, const pgcn_data *d, int device, pgcn_gcn **out) {

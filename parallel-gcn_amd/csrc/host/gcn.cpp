@@ -207,10 +207,10 @@ void GCN::build(const GCNData &data) {
     std::vector<int> sp, si;
     std::vector<float> sv;
     partition_subgraph(part, N, data.graph.indptr.data(), data.graph.indices.data(), &sp, &si, &sv);
-    graph = std::make_unique<DevGraph>(part.world * part.maxrows, sp.data(), si.data(), sv.data());
+    graph = std::make_unique<DevGraph>(part.world * part.maxrows, part.local_rows(), sp.data(), si.data(), sv.data());
   } else {
     std::vector<float> v = graph_coefs(N, data.graph.indptr.data(), data.graph.indices.data());
-    graph = std::make_unique<DevGraph>(N, data.graph.indptr.data(), data.graph.indices.data(),
+    graph = std::make_unique<DevGraph>(N, N, data.graph.indptr.data(), data.graph.indices.data(),
                                        v.data());
   }
   upload_features(data);
@@ -320,6 +320,21 @@ void GCN::insert_last_layer() {
   auto drop = std::make_unique<Dropout>(prev, params.dropouts.back(), rngs[(size_t)L - 1], &ctx);
   dropouts_.push_back(drop.get());
   modules.push_back(std::move(drop));
+  if (params.reassociate_last && hl < C) {
+    // out = Â (H W) computed as (Â H) W: the same product (Â is symmetric, so the backward
+    // Â dOut W^T = Â (dOut W^T) and W.grad = H^T Â dOut = (Â H)^T dOut also match), but the
+    // GraphSum gathers rows of width hl instead of C.  Only the fp32 rounding order differs.
+    auto z = std::make_shared<Variable>(prow, hl, true, round_up4(hl));
+    variables.push_back(z);
+    variables.push_back(weights.back());
+    modules.push_back(std::make_unique<GraphSum>(prev, z, graph.get(), hl, &ctx));
+    auto out = std::make_shared<Variable>(prow, C, true, round_up4(C));
+    variables.push_back(out);
+    modules.push_back(std::make_unique<Matmul>(z, weights.back(), out, part.local_rows(), hl, C,
+                                               &ctx));
+    modules.push_back(std::make_unique<CrossEntropyLoss>(out, C, &ctx));
+    return;
+  }
   auto var1 = std::make_shared<Variable>(prow, C, true, round_up4(C));
   variables.push_back(var1);
   variables.push_back(weights.back());

@@ -25,6 +25,9 @@ struct GCNParams {
   std::vector<float> dropouts = {0.5f, 0.5f};
   int epochs = 100, early_stopping = 0;
   int n_layers = 2;
+  // compute the last layer as (Â H) W instead of Â (H W) when that narrows the GraphSum
+  // (hidden < classes); exact algebra, fp32 rounding order only (see insert_last_layer)
+  bool reassociate_last = false;
 };
 
 struct AdamParams {

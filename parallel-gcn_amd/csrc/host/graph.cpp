@@ -1,8 +1,10 @@
 // parallel-gcn_amd/csrc/host/graph.cpp
 #include "graph.hpp"
 
+#include <algorithm>
 #include <cmath>
 #include <functional>
+#include <numeric>
 #include <thread>
 
 namespace pgcn {
@@ -47,14 +49,80 @@ std::vector<float> graph_coefs(int n, const int *indptr, const int *indices) {
   return v;
 }
 
-DevGraph::DevGraph(int n_rows, const int *indptr, const int *indices, const float *vals)
-    : n_rows_(n_rows), nnz_(indptr[n_rows]), h_indptr_(indptr, indptr + n_rows + 1) {
+DevGraph::DevGraph(int n_rows, int n_cols, const int *indptr, const int *indices,
+                   const float *vals)
+    : n_rows_(n_rows), n_cols_(n_cols), nnz_(indptr[n_rows]), h_indptr_(indptr, indptr + n_rows + 1),
+      h_indices_(indices, indices + indptr[n_rows]), h_vals_(vals, vals + indptr[n_rows]) {
   indices_.allocate((size_t)nnz_ + 64);  // slack: unrolled loads never step past the end
   vals_.allocate((size_t)nnz_ + 64);
-  indices_.upload(indices, (size_t)nnz_);
-  vals_.upload(vals, (size_t)nnz_);
+  indices_.upload(h_indices_);
+  vals_.upload(h_vals_);
   PGCN_HIP(hipMemset(indices_.get() + nnz_, 0, 64 * sizeof(int)));
   PGCN_HIP(hipMemset(vals_.get() + nnz_, 0, 64 * sizeof(float)));
+}
+
+int DevGraph::column_blocks(int dim) {
+  const int vec = (dim + 3) / 4;
+  const double table = (double)n_cols_ * vec * 16.0;
+  return (graphsum_group_lanes(vec) < 64 && table > kL2Budget) ? kBlocks : 1;
+}
+
+// Cut the columns into kBlocks nnz-balanced ranges and store the edges block-major.
+void DevGraph::build_blocked() {
+  if (blocked_built_) return;
+  const int B = kBlocks;
+  // column occurrence counts -> nnz-balanced cuts
+  std::vector<long long> colcnt((size_t)n_cols_ + 1, 0);
+  for (long long k = 0; k < nnz_; k++) colcnt[(size_t)h_indices_[(size_t)k] + 1]++;
+  for (int c = 0; c < n_cols_; c++) colcnt[(size_t)c + 1] += colcnt[(size_t)c];
+  bcut_.assign((size_t)B + 1, 0);
+  bcut_[(size_t)B] = n_cols_;
+  for (int b = 1; b < B; b++) {
+    const long long target = (long long)((double)nnz_ * b / B);
+    int c = (int)(std::lower_bound(colcnt.begin(), colcnt.end(), target) - colcnt.begin());
+    c = std::max(c, bcut_[(size_t)b - 1]);
+    bcut_[(size_t)b] = std::min(c, n_cols_);
+  }
+  auto block_of = [&](int col) {
+    return (int)(std::upper_bound(bcut_.begin(), bcut_.end(), col) - bcut_.begin()) - 1;
+  };
+  // per-row counts per block
+  std::vector<int> cnt((size_t)n_rows_ * B, 0);
+  parallel_for(n_rows_, [&](long long b0, long long b1) {
+    for (long long i = b0; i < b1; i++)
+      for (int k = h_indptr_[(size_t)i]; k < h_indptr_[(size_t)i + 1]; k++)
+        cnt[(size_t)i * B + block_of(h_indices_[(size_t)k])]++;
+  });
+  // block-major segment offsets
+  bseg_.assign((size_t)B * (n_rows_ + 1), 0);
+  long long base = 0;
+  for (int b = 0; b < B; b++) {
+    long long *seg = &bseg_[(size_t)b * (n_rows_ + 1)];
+    seg[0] = base;
+    for (int i = 0; i < n_rows_; i++) seg[i + 1] = seg[i] + cnt[(size_t)i * B + b];
+    base = seg[n_rows_];
+  }
+  std::vector<int> bi((size_t)nnz_);
+  std::vector<float> bv((size_t)nnz_);
+  parallel_for(n_rows_, [&](long long b0, long long b1) {
+    for (long long i = b0; i < b1; i++) {
+      long long o[kBlocks];
+      for (int b = 0; b < B; b++) o[b] = bseg_[(size_t)b * (n_rows_ + 1) + i];
+      for (int k = h_indptr_[(size_t)i]; k < h_indptr_[(size_t)i + 1]; k++) {
+        const int b = block_of(h_indices_[(size_t)k]);
+        bi[(size_t)o[b]] = h_indices_[(size_t)k];
+        bv[(size_t)o[b]] = h_vals_[(size_t)k];
+        o[b]++;
+      }
+    }
+  });
+  bindices_.allocate((size_t)nnz_ + 64);
+  bvals_.allocate((size_t)nnz_ + 64);
+  bindices_.upload(bi);
+  bvals_.upload(bv);
+  PGCN_HIP(hipMemset(bindices_.get() + nnz_, 0, 64 * sizeof(int)));
+  PGCN_HIP(hipMemset(bvals_.get() + nnz_, 0, 64 * sizeof(float)));
+  blocked_built_ = true;
 }
 
 DevGraph::Sched &DevGraph::schedule(int vec) {
@@ -63,38 +131,89 @@ DevGraph::Sched &DevGraph::schedule(int vec) {
   PGCN_CHECK(graphsum_vec_supported(vec), PGCN_E_INVALID,
              "graphsum: row width not supported: " + std::to_string(4 * vec));
   auto sp = std::make_unique<Sched>();
-  const int nb = 64 / vec;
-  const int chunk = nb * 32;  // 32 wave iterations per work item
+  const int G = graphsum_group_lanes(vec);
+  const int nb = G / vec;
+  const int nbc = column_blocks(4 * vec);
   std::vector<int4> items, comb;
-  items.reserve((size_t)n_rows_ + (size_t)(nnz_ / chunk) + 1);
+  std::vector<int> block_items(1, 0);
   long long slots = 0;
-  for (int r = 0; r < n_rows_; r++) {
-    const int b = h_indptr_[r], e = h_indptr_[r + 1];
-    if (e - b <= chunk) {
-      items.push_back(make_int4(r, b, e, -1));
-    } else {
-      const int first = (int)slots;
-      int cnt = 0;
-      for (int p = b; p < e; p += chunk) {
-        items.push_back(make_int4(r, p, std::min(e, p + chunk), (int)slots++));
-        cnt++;
+  int chunk;
+  if (nbc == 1) {
+    chunk = nb * 32;  // 32 group iterations per work item
+    items.reserve((size_t)n_rows_ + (size_t)(nnz_ / chunk) + 1);
+    for (int r = 0; r < n_rows_; r++) {
+      const int b = h_indptr_[(size_t)r], e = h_indptr_[(size_t)r + 1];
+      if (e - b <= chunk) {
+        items.push_back(make_int4(r, b, e, -1));
+      } else {
+        const int first = (int)slots;
+        int cnt = 0;
+        for (int p = b; p < e; p += chunk) {
+          items.push_back(make_int4(r, p, std::min(e, p + chunk), (int)slots++));
+          cnt++;
+        }
+        comb.push_back(make_int4(r, first, cnt, 0));
       }
-      comb.push_back(make_int4(r, first, cnt, 0));
     }
+    // longest items first: the tail of the launch is short items
+    std::stable_sort(items.begin(), items.end(),
+                     [](const int4 &a, const int4 &b) { return (a.z - a.y) > (b.z - b.y); });
+    block_items.push_back((int)items.size());
+  } else {
+    build_blocked();
+    chunk = nb * 64;
+    const int B = kBlocks;
+    // slots: row-major, then block, then chunk -> a row's slots are contiguous and ordered
+    std::vector<long long> rslot((size_t)n_rows_ + 1, 0);
+    for (int i = 0; i < n_rows_; i++) {
+      long long s = 0;
+      for (int b = 0; b < B; b++) {
+        const long long len = bseg_[(size_t)b * (n_rows_ + 1) + i + 1] - bseg_[(size_t)b * (n_rows_ + 1) + i];
+        s += (len + chunk - 1) / chunk;
+      }
+      rslot[(size_t)i + 1] = rslot[(size_t)i] + s;
+    }
+    slots = rslot[(size_t)n_rows_];
+    PGCN_CHECK(slots < (1LL << 31) && nnz_ < (1LL << 31), PGCN_E_INVALID, "graph too large");
+    std::vector<long long> used((size_t)n_rows_, 0);
+    for (int b = 0; b < B; b++) {
+      const size_t start = items.size();
+      const long long *seg = &bseg_[(size_t)b * (n_rows_ + 1)];
+      for (int i = 0; i < n_rows_; i++) {
+        for (long long p = seg[i]; p < seg[i + 1]; p += chunk) {
+          const long long slot = rslot[(size_t)i] + used[(size_t)i]++;
+          items.push_back(make_int4(i, (int)p, (int)std::min(seg[i + 1], p + chunk), (int)slot));
+        }
+      }
+      std::stable_sort(items.begin() + (long)start, items.end(),
+                       [](const int4 &a, const int4 &c) { return (a.z - a.y) > (c.z - c.y); });
+      block_items.push_back((int)items.size());
+    }
+    comb.reserve((size_t)n_rows_);
+    for (int i = 0; i < n_rows_; i++)
+      comb.push_back(make_int4(i, (int)rslot[(size_t)i], (int)(rslot[(size_t)i + 1] - rslot[(size_t)i]), 0));
   }
+  int max_block = 0;
+  for (size_t b = 0; b + 1 < block_items.size(); b++)
+    max_block = std::max(max_block, block_items[b + 1] - block_items[b]);
   sp->s.vec = vec;
   sp->s.chunk = chunk;
+  sp->s.nbc = nbc;
   sp->s.n_items = (int)items.size();
+  sp->s.max_block_items = max_block;
   sp->s.n_comb = (int)comb.size();
   sp->s.n_slots = slots;
-  sp->items.allocate(items.size());
+  sp->items.allocate(std::max<size_t>(items.size(), 1));
   sp->items.upload(items);
+  sp->block_items.allocate(block_items.size());
+  sp->block_items.upload(block_items);
   if (!comb.empty()) {
     sp->comb.allocate(comb.size());
     sp->comb.upload(comb);
   }
   if (slots) sp->partial.allocate((size_t)slots * vec * 4);
   sp->s.items = sp->items.get();
+  sp->s.block_items = sp->block_items.get();
   sp->s.comb = sp->comb.get();
   auto &ref = *sp;
   scheds_[vec] = std::move(sp);
@@ -107,12 +226,14 @@ void DevGraph::graphsum(const float *in, int ld_in, float *out, int ld_out, int 
              PGCN_E_INVALID, "graphsum: leading dims must be multiples of 4 and >= dim");
   const int vec = (dim + 3) / 4;
   Sched &sc = schedule(vec);
-  launch_graphsum(sc.s, indices_.get(), vals_.get(), in, ld_in, out, ld_out, sc.partial.get(), s);
+  const bool blocked = sc.s.nbc > 1;
+  launch_graphsum(sc.s, blocked ? bindices_.get() : indices_.get(),
+                  blocked ? bvals_.get() : vals_.get(), in, ld_in, out, ld_out, sc.partial.get(), s);
 }
 
-double DevGraph::algorithmic_bytes(int dim, long long n_in_rows) const {
+double DevGraph::algorithmic_bytes(int dim) const {
   // 4(N+1) indptr + 8 nnz (index + value) + 4 N_in d (read) + 4 N d (write)
-  return 4.0 * (n_rows_ + 1) + 8.0 * (double)nnz_ + 4.0 * (double)n_in_rows * dim +
+  return 4.0 * (n_rows_ + 1) + 8.0 * (double)nnz_ + 4.0 * (double)n_cols_ * dim +
          4.0 * (double)n_rows_ * dim;
 }
 

@@ -4,6 +4,13 @@
 // separately uploaded dev_graph_value array (src/parser.cpp:164-181, src/gcn.cu:30-43).  Here
 // DevGraph owns the CSR column ids, the Â coefficients and, per row width, the wavefront
 // work schedule of k_graphsum (built once; the graph is static across epochs).
+//
+// Two device layouts:
+//  * plain  -- the CSR as given (row-major); work items are row chunks.
+//  * blocked -- for feature tables larger than one XCD's L2: the columns are cut into 8
+//    nnz-balanced blocks and the edges stored block-major (all of block 0's row segments,
+//    then block 1's, ...), so the index/value stream of one block is contiguous and the
+//    workgroups of one XCD gather from one 1/8 slice of the feature table.
 #pragma once
 #include <functional>
 #include <map>
@@ -27,30 +34,42 @@ void parallel_for(long long n, const std::function<void(long long, long long)> &
 
 class DevGraph {
  public:
-  // CSR with n_rows rows; `vals` aligned with `indices` (coefficients).
-  DevGraph(int n_rows, const int *indptr, const int *indices, const float *vals);
+  // CSR with n_rows rows and column ids < n_cols; `vals` aligned with `indices`.
+  DevGraph(int n_rows, int n_cols, const int *indptr, const int *indices, const float *vals);
   int rows() const { return n_rows_; }
+  int cols() const { return n_cols_; }
   long long nnz() const { return nnz_; }
-  const int *indices() const { return indices_.get(); }
-  const float *vals() const { return vals_.get(); }
-  const std::vector<int> &host_indptr() const { return h_indptr_; }
   // out[i,:dim] = sum_j val_ij * in[col_j,:dim]
   void graphsum(const float *in, int ld_in, float *out, int ld_out, int dim, hipStream_t s);
   // bytes the kernel must move at minimum (SURVEY.md §8d formula, per call)
-  double algorithmic_bytes(int dim, long long n_in_rows) const;
+  double algorithmic_bytes(int dim) const;
+  // schedule statistics (for tests / reports)
+  int column_blocks(int dim);
+
+  static constexpr int kBlocks = 8;              // one column block per XCD
+  static constexpr double kL2Budget = 4.0e6;     // table bytes that stay plain
 
  private:
   struct Sched {
     GraphSchedule s;
     DeviceBuffer<int4> items, comb;
+    DeviceBuffer<int> block_items;
     DeviceBuffer<float> partial;
   };
   Sched &schedule(int vec);
-  int n_rows_;
+  void build_blocked();
+  int n_rows_, n_cols_;
   long long nnz_;
-  std::vector<int> h_indptr_;
-  DeviceBuffer<int> indices_;
+  std::vector<int> h_indptr_, h_indices_;
+  std::vector<float> h_vals_;
+  DeviceBuffer<int> indices_;  // plain layout
   DeviceBuffer<float> vals_;
+  // blocked layout
+  bool blocked_built_ = false;
+  std::vector<int> bcut_;                 // kBlocks + 1 column boundaries
+  std::vector<long long> bseg_;           // (kBlocks) x (n_rows + 1) segment offsets
+  DeviceBuffer<int> bindices_;
+  DeviceBuffer<float> bvals_;
   std::map<int, std::unique_ptr<Sched>> scheds_;
 };
 

@@ -122,7 +122,7 @@ void GraphSum::run(const float *src, float *dst, const Stream &s) const {
   }
   if (ctx->profile) {
     ctx->gs_events->emplace_back(e0, e1);
-    ctx->gs_bytes->push_back(graph->algorithmic_bytes(dim, in->rows));
+    ctx->gs_bytes->push_back(graph->algorithmic_bytes(dim));
   }
 }
 

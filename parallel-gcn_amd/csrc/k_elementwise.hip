@@ -152,18 +152,34 @@ __device__ __forceinline__ float block_sum(float v, float *smem) {
 // divided by the labelled count (known per split on the host). Per-block partial sums
 // (loss, wrong) go to partials[2*block].
 // ------------------------------------------------------------------------------------------
+constexpr int XR = 128;  // rows per cross-entropy block
+
 __global__ __launch_bounds__(256) void k_xent_fwd(float *__restrict__ logits, int ld,
                                                   float *__restrict__ grad,
                                                   const int *__restrict__ truth, int n, int c,
-                                                  float inv_count_f, int count, int training,
+                                                  int count, int training,
                                                   float *__restrict__ partials) {
+  // The block's XR rows are staged through LDS with coalesced loads/stores (row stride
+  // ld+1 floats: conflict-free per-row reads); one thread per row computes in LDS.
+  extern __shared__ float smem[];
   __shared__ float red[4];
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int S = ld + 1;
+  float *L = smem;            // [XR][S] logits
+  float *Gr = smem + XR * S;  // [XR][S] grad
+  const long long row0 = (long long)blockIdx.x * XR;
+  const int rows = (int)min((long long)XR, (long long)n - row0);
+  const long long base = row0 * ld;
+  const int tile = rows * ld;
+  for (int e = threadIdx.x; e < tile; e += 256) {
+    const int r = e / ld, j = e - r * ld;
+    L[r * S + j] = logits[base + e];
+  }
+  __syncthreads();
   float loss = 0.0f, wrong = 0.0f;
-  if (i < n) {
-    const int t = truth[i];
-    float *l = logits + (long long)i * ld;
-    float *g = grad ? grad + (long long)i * ld : nullptr;
+  const int t = threadIdx.x < rows ? truth[row0 + threadIdx.x] : -1;
+  float *l = L + threadIdx.x * S;
+  float *g = Gr + threadIdx.x * S;
+  if (threadIdx.x < rows) {
     if (t >= 0) {
       float mx = -1e30f;
       for (int j = 0; j < c; j++) mx = fmaxf(mx, l[j]);
@@ -190,7 +206,12 @@ __global__ __launch_bounds__(256) void k_xent_fwd(float *__restrict__ logits, in
       for (int j = 0; j < ld; j++) g[j] = 0.0f;
     }
   }
-  (void)inv_count_f;
+  __syncthreads();
+  for (int e = threadIdx.x; e < tile; e += 256) {
+    const int r = e / ld, j = e - r * ld;
+    logits[base + e] = L[r * S + j];
+    if (training) grad[base + e] = Gr[r * S + j];
+  }
   const float ls = block_sum<256>(loss, red);
   const float ws = block_sum<256>(wrong, red);
   if (threadIdx.x == 0) {
@@ -292,14 +313,21 @@ void launch_relu_bwd(float *g, long long n, const uint8_t *mask, hipStream_t s) 
   hipLaunchKernelGGL(k_relu_bwd, dim3(grid_for(n)), dim3(256), 0, s, g, n, mask);
 }
 
-int xent_blocks(int n) { return (int)ceil_div(n, 256); }
+int xent_blocks(int n) { return (int)ceil_div(n, XR); }
 
 void launch_xent_fwd(float *logits, int ld, float *grad, const int *truth, int n, int c,
                      int count, int training, float *partials, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_xent_fwd, dim3(xent_blocks(n)), dim3(256), 0, s, logits, ld, grad,
-                     truth, n, c, 1.0f / (float)(count > 0 ? count : 1), count, training,
-                     partials);
+  PGCN_CHECK(ld <= 128 && c <= ld, PGCN_E_INVALID, "xent: classes must be <= 128");
+  const size_t lds = (size_t)2 * XR * (ld + 1) * sizeof(float);
+  static bool attr = false;
+  if (!attr) {  // up to 2*128*129*4 = 132 KB of the CU's 160 KB LDS
+    PGCN_HIP(hipFuncSetAttribute((const void *)k_xent_fwd,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_xent_fwd, dim3(xent_blocks(n)), dim3(256), lds, s, logits, ld, grad,
+                     truth, n, c, count, training, partials);
 }
 
 void launch_reduce_scalars(const float *partials, int n_blocks, const float *w, long long n_w,

@@ -110,10 +110,13 @@ __global__ __launch_bounds__(256) void k_gemm_nn(int M, int N, int K,
 }
 
 // ------------------------------------------------------------------------------------------
-// TN split-M: grid (slabs, k-groups). Block = 4 waves; wave w owns k-tiles
-// kt = kg*4*KTW + w + 4*q (q < KTW) and all NJ column tiles.
+// TN split-M.  Block = 4 waves over a slab of rows; the K columns are cut into 64-wide chunks.
+// Wave layout: WK waves along K x (4/WK) waves along rows.  Per step of 4 rows a lane
+// (g = lane>>4, i = lane&15) loads ONE float4 A[m+g][kc*64 + 4i .. +3] (a wave reads 4 rows
+// x 256 contiguous bytes) and feeds 4 MFMAs: MFMA t's A-operand row i is k = kc*64 + 4i + t,
+// its reduction index is the row g.  Partials go to partial[slab][k][ldp].
 // ------------------------------------------------------------------------------------------
-template <int NJ, int KTW>
+template <int NJ, int KCW, int WK>
 __global__ __launch_bounds__(256) void k_gemm_tn(int M, int N, int K, int slab,
                                                  const float *__restrict__ A, int lda,
                                                  const float *__restrict__ G, int ldg,
@@ -121,70 +124,112 @@ __global__ __launch_bounds__(256) void k_gemm_tn(int M, int N, int K, int slab,
                                                  long long mask_base, long long mask_ld,
                                                  float a_scale, float *__restrict__ partial,
                                                  int ldp) {
+  constexpr int WR = 4 / WK;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int g = lane >> 4, i = lane & 15;
+  const int wk = w % WK, wr = w / WK;
   const long long m_begin = (long long)blockIdx.x * slab;
   long long m_end = m_begin + slab;
   if (m_end > M) m_end = M;
-  int kcol[KTW];
+  floatx4 acc[KCW][4][NJ];
 #pragma unroll
-  for (int q = 0; q < KTW; q++) kcol[q] = ((int)blockIdx.y * 4 * KTW + w + 4 * q) * 16 + i;
-  floatx4 acc[KTW][NJ];
+  for (int c = 0; c < KCW; c++)
 #pragma unroll
-  for (int q = 0; q < KTW; q++)
+    for (int t = 0; t < 4; t++)
 #pragma unroll
-    for (int t = 0; t < NJ; t++) acc[q][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < NJ; j++) acc[c][t][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  for (long long m = m_begin; m < m_end; m += 4) {
-    const long long mr = m + g;  // this lane's row of the reduction step
+  for (long long m = m_begin + 4 * wr; m < m_end; m += 4 * WR) {
+    const long long mr = m + g;
     const bool ok = mr < m_end;
     float b[NJ];
 #pragma unroll
-    for (int t = 0; t < NJ; t++) {
-      const int col = 16 * t + i;
-      b[t] = (ok && col < N) ? G[mr * ldg + col] : 0.0f;
+    for (int j = 0; j < NJ; j++) {
+      const int col = 16 * j + i;
+      b[j] = (ok && col < N) ? G[mr * ldg + col] : 0.0f;
     }
 #pragma unroll
-    for (int q = 0; q < KTW; q++) {
-      const int k = kcol[q];
-      float a = 0.0f;
-      if (ok && k < K) {
-        a = A[mr * lda + k];
+    for (int c = 0; c < KCW; c++) {
+      const int kb = (wk + WK * c) * 64 + 4 * i;
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (ok && kb < K) {
+        a = *reinterpret_cast<const float4 *>(A + mr * lda + kb);
+        if (kb + 1 >= K) a.y = 0.f;
+        if (kb + 2 >= K) a.z = 0.f;
+        if (kb + 3 >= K) a.w = 0.f;
         if (a_mask) {
-          const long long bi = mask_base + mr * mask_ld + k;
-          a *= ((a_mask[bi >> 6] >> (bi & 63)) & 1) ? a_scale : 0.0f;
+          const uint32_t bits = mask4(a_mask, mask_base + mr * mask_ld + kb);
+          a.x *= (bits & 1) ? a_scale : 0.0f;
+          a.y *= (bits & 2) ? a_scale : 0.0f;
+          a.z *= (bits & 4) ? a_scale : 0.0f;
+          a.w *= (bits & 8) ? a_scale : 0.0f;
         }
       }
 #pragma unroll
-      for (int t = 0; t < NJ; t++)
-        acc[q][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b[t], acc[q][t], 0, 0, 0);
+      for (int j = 0; j < NJ; j++) {
+        acc[c][0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b[j], acc[c][0][j], 0, 0, 0);
+        acc[c][1][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b[j], acc[c][1][j], 0, 0, 0);
+        acc[c][2][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b[j], acc[c][2][j], 0, 0, 0);
+        acc[c][3][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b[j], acc[c][3][j], 0, 0, 0);
+      }
     }
   }
-  // partial[slab][k][j], k = ktile*16 + 4g + r, j = 16t + i
+  // row-group partial sums of one block meet in LDS (fixed order), then one slab partial
+  __shared__ float red[WR > 1 ? 4 * 64 * 16 : 1];
   float *p = partial + (long long)blockIdx.x * K * ldp;
 #pragma unroll
-  for (int q = 0; q < KTW; q++) {
-    const int kt = (int)blockIdx.y * 4 * KTW + w + 4 * q;
+  for (int c = 0; c < KCW; c++) {
 #pragma unroll
-    for (int t = 0; t < NJ; t++) {
-      const int col = 16 * t + i;
+    for (int j = 0; j < NJ; j++) {
 #pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int k = kt * 16 + 4 * g + r;
-        if (k < K && col < ldp) p[(long long)k * ldp + col] = acc[q][t][r];
+      for (int t = 0; t < 4; t++) {
+        floatx4 v = acc[c][t][j];
+        if constexpr (WR > 1) {
+          __syncthreads();
+#pragma unroll
+          for (int r = 0; r < 4; r++) red[(w * 64 + lane) * 4 + r] = v[r];
+          __syncthreads();
+          if (wr == 0) {
+#pragma unroll
+            for (int q = 1; q < WR; q++)
+#pragma unroll
+              for (int r = 0; r < 4; r++) v[r] += red[((wk + WK * q) * 64 + lane) * 4 + r];
+          }
+        }
+        if (wr == 0) {
+          const int col = 16 * j + i;
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            const int k = (wk + WK * c) * 64 + 4 * (4 * g + r) + t;
+            if (k < K && col < ldp) p[(long long)k * ldp + col] = v[r];
+          }
+        }
       }
     }
   }
 }
 
-__global__ __launch_bounds__(256) void k_gemm_tn_reduce(const float *__restrict__ partial,
-                                                        int n_slabs, int K, int N, int ldp,
+// pass 1: part2[rg][e] = sum of slabs [rg*SPG, (rg+1)*SPG) of element e (slab order)
+__global__ __launch_bounds__(256) void k_slab_reduce1(const float *__restrict__ partial,
+                                                      int n_slabs, long long elems, int spg,
+                                                      float *__restrict__ part2) {
+  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= elems) return;
+  const int s0 = blockIdx.y * spg, s1 = min(n_slabs, s0 + spg);
+  float s = 0.0f;
+  for (int b = s0; b < s1; b++) s += partial[(long long)b * elems + e];
+  part2[(long long)blockIdx.y * elems + e] = s;
+}
+
+// pass 2: C[k][j] = sum over groups in order
+__global__ __launch_bounds__(256) void k_gemm_tn_reduce(const float *__restrict__ part2,
+                                                        int n_groups, int K, int N, int ldp,
                                                         float *__restrict__ C, int ldc) {
   const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (long long)K * ldp) return;
   const int k = (int)(e / ldp), j = (int)(e - (long long)k * ldp);
   float s = 0.0f;
-  for (int b = 0; b < n_slabs; b++) s += partial[(long long)b * K * ldp + e];
+  for (int b = 0; b < n_groups; b++) s += part2[(long long)b * K * ldp + e];
   if (j < ldc) C[(long long)k * ldc + j] = j < N ? s : 0.0f;
 }
 
@@ -211,64 +256,67 @@ void launch_gemm_nn(int M, int N, int K, const float *A, int lda, const float *B
 }
 
 struct TnPlan {
-  int nj, ktw, kgroups, slab, n_slabs, ldp;
+  int nj, nkc, wk, kcw, slab, n_slabs, ldp, spg, n_groups;
 };
 
 static TnPlan tn_plan(int M, int N, int K) {
   TnPlan p;
   p.nj = (N + 15) / 16;
   p.ldp = p.nj * 16;
-  const int kt = (K + 15) / 16;
-  // keep KTW*NJ*4 accumulators <= 64 VGPRs per lane
-  p.ktw = p.nj >= 8 ? 2 : (p.nj >= 4 ? 4 : (p.nj >= 2 ? 4 : 4));
-  if (p.ktw * 4 > kt) p.ktw = (kt + 3) / 4;
-  if (p.ktw < 1) p.ktw = 1;
-  p.kgroups = (kt + 4 * p.ktw - 1) / (4 * p.ktw);
-  // aim for >= ~1024 blocks over (slabs x kgroups), slabs >= 256 rows
-  long long target = 1024 / p.kgroups;
-  if (target < 1) target = 1;
-  long long slab = ceil_div(M, target);
-  slab = (slab + 3) / 4 * 4;
-  if (slab < 256) slab = 256;
+  p.nkc = (K + 63) / 64;
+  p.wk = p.nkc >= 4 ? 4 : (p.nkc >= 2 ? 2 : 1);
+  p.kcw = (p.nkc + p.wk - 1) / p.wk;
+  const int wr = 4 / p.wk;
+  long long slab = ceil_div(M, 512);
+  const int q = 4 * wr;
+  slab = (slab + q - 1) / q * q;
+  if (slab < 64) slab = 64;
   p.slab = (int)slab;
-  p.n_slabs = (int)ceil_div(M, slab);
-  if (p.n_slabs < 1) p.n_slabs = 1;
+  p.n_slabs = (int)std::max(1LL, ceil_div(M, slab));
+  p.spg = 16;
+  p.n_groups = (p.n_slabs + p.spg - 1) / p.spg;
   return p;
 }
 
 size_t gemm_tn_workspace(int M, int N, int K) {
   const TnPlan p = tn_plan(M, N, K);
-  return (size_t)p.n_slabs * (size_t)K * (size_t)p.ldp * sizeof(float);
+  return ((size_t)p.n_slabs + (size_t)p.n_groups) * (size_t)K * (size_t)p.ldp * sizeof(float);
 }
 
 void launch_gemm_tn(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
                     float *C, int ldc, const uint64_t *a_mask, long long mask_base,
                     long long mask_ld, float a_scale, void *workspace, hipStream_t s) {
   PGCN_CHECK(N <= 128 && N >= 1, PGCN_E_INVALID, "gemm_tn: N must be in [1,128]");
+  PGCN_CHECK(lda % 4 == 0 && lda >= K, PGCN_E_INVALID, "gemm_tn: lda must be a multiple of 4 >= K");
   const TnPlan p = tn_plan(M, N, K);
   float *partial = static_cast<float *>(workspace);
-  if (M > 0) {
-    const dim3 grid((unsigned)p.n_slabs, (unsigned)p.kgroups), block(256);
-#define TN_CASE(NJ, KTW)                                                                    \
-  if (p.nj == NJ && p.ktw == KTW) {                                                         \
-    hipLaunchKernelGGL((k_gemm_tn<NJ, KTW>), grid, block, 0, s, M, N, K, p.slab, A, lda, G, \
-                       ldg, a_mask, mask_base, mask_ld, a_scale, partial, p.ldp);           \
-  } else
-    TN_CASE(1, 4) TN_CASE(1, 3) TN_CASE(1, 2) TN_CASE(1, 1)
-    TN_CASE(2, 4) TN_CASE(2, 3) TN_CASE(2, 2) TN_CASE(2, 1)
-    TN_CASE(3, 4) TN_CASE(3, 3) TN_CASE(3, 2) TN_CASE(3, 1)
-    TN_CASE(4, 4) TN_CASE(4, 3) TN_CASE(4, 2) TN_CASE(4, 1)
-    TN_CASE(5, 4) TN_CASE(5, 3) TN_CASE(5, 2) TN_CASE(5, 1)
-    TN_CASE(6, 4) TN_CASE(6, 3) TN_CASE(6, 2) TN_CASE(6, 1)
-    TN_CASE(7, 4) TN_CASE(7, 3) TN_CASE(7, 2) TN_CASE(7, 1)
-    TN_CASE(8, 2) TN_CASE(8, 1) {
-      throw Error(PGCN_E_INVALID, "gemm_tn: no kernel for this shape");
-    }
-#undef TN_CASE
-  }
+  float *part2 = partial + (size_t)p.n_slabs * K * p.ldp;
   const long long elems = (long long)K * p.ldp;
+  if (M > 0) {
+    const dim3 grid((unsigned)p.n_slabs), block(256);
+    bool done = false;
+#define TN_CASE(NJ, KCW, WK)                                                                   \
+  if (!done && p.nj == NJ && p.kcw == KCW && p.wk == WK) {                                    \
+    hipLaunchKernelGGL((k_gemm_tn<NJ, KCW, WK>), grid, block, 0, s, M, N, K, p.slab, A, lda, G, \
+                       ldg, a_mask, mask_base, mask_ld, a_scale, partial, p.ldp);              \
+    done = true;                                                                               \
+  }
+#define TN_NJ(NJ) TN_CASE(NJ, 1, 1) TN_CASE(NJ, 1, 2) TN_CASE(NJ, 1, 4) TN_CASE(NJ, 2, 4) \
+                  TN_CASE(NJ, 3, 4)
+    TN_NJ(1) TN_NJ(2) TN_NJ(3) TN_NJ(4)
+    TN_CASE(5, 1, 1) TN_CASE(5, 1, 2) TN_CASE(5, 1, 4)
+    TN_CASE(6, 1, 1) TN_CASE(6, 1, 2) TN_CASE(6, 1, 4)
+    TN_CASE(7, 1, 1) TN_CASE(7, 1, 2) TN_CASE(7, 1, 4)
+    TN_CASE(8, 1, 1) TN_CASE(8, 1, 2) TN_CASE(8, 1, 4)
+#undef TN_NJ
+#undef TN_CASE
+    PGCN_CHECK(done, PGCN_E_INVALID,
+               "gemm_tn: no kernel for N=" + std::to_string(N) + " K=" + std::to_string(K));
+    hipLaunchKernelGGL(k_slab_reduce1, dim3((unsigned)ceil_div(elems, 256), (unsigned)p.n_groups),
+                       dim3(256), 0, s, partial, p.n_slabs, elems, p.spg, part2);
+  }
   hipLaunchKernelGGL(k_gemm_tn_reduce, dim3((unsigned)ceil_div(elems, 256)), dim3(256), 0, s,
-                     partial, M > 0 ? p.n_slabs : 0, K, N, p.ldp, C, ldc);
+                     part2, M > 0 ? p.n_groups : 0, K, N, p.ldp, C, ldc);
 }
 
 }  // namespace pgcn

@@ -5,14 +5,19 @@
 // walk over the row) and hpdga GraphSum::forward/backward (module.cpp:82-111).
 //
 // Layout: node features are row-major [n][ld] fp32 with ld a multiple of 4 (16-B rows of
-// float4; padding columns are kept zero by every producer).  A wavefront owns one work item
-// = (row, slot range <= chunk); its 64 lanes are split into NB = 64/VEC neighbour groups of
-// VEC lanes, each lane holding one float4 of the row: one wave instruction gathers NB full
-// neighbour rows (NB*VEC*16 bytes, e.g. 16 rows x 64 B at dim 16) with coalesced 16-B lanes.
-// Neighbour groups are summed in a fixed tree (xor-shuffles when VEC is a power of two, LDS
-// otherwise), so the result is deterministic run to run.  Rows longer than one chunk are
-// split over several waves that write partial rows; a second kernel adds the partials in
-// slot order.  The schedule (items, combine list) is built once per (graph, VEC) on the host.
+// float4; padding columns are kept zero by every producer).
+//
+// Work items.  The adjacency is cut into NBC column blocks (NBC = 8 on large graphs:
+// one per XCD) and every (row, column block) segment into items of <= `chunk` slots
+// (host-built schedule, sorted longest first inside a block).  Workgroup w serves column
+// block w % NBC: consecutive workgroup ids are dealt round-robin to the 8 XCDs, so every
+// workgroup of one column block runs on the same XCD and that XCD's 4 MB L2 holds the
+// block's 1/8 slice of the gathered feature table (a speed property only -- results do not
+// depend on placement).  A group of G lanes owns one item: its lanes are NB = G/VEC
+// neighbour sub-groups of VEC lanes, each lane one float4 of a neighbour row, so one wave
+// instruction gathers 64/VEC whole neighbour rows with 16-B lanes.  Sub-groups are summed in
+// a fixed xor-tree => deterministic.  Each item writes its partial row to a slot; a combine
+// kernel adds a row's slots in slot order (skipped for rows that are one whole item).
 #include "common.hpp"
 #include "kernels.hpp"
 
@@ -33,21 +38,26 @@ __device__ __forceinline__ float4 f4_shfl_xor(float4 v, int m) {
                      __shfl_xor(v.w, m, 64));
 }
 
-template <int VEC>
-__global__ __launch_bounds__(256) void k_graphsum(const int4 *__restrict__ items, int n_items,
-                                                  const int *__restrict__ indices,
+// G lanes per item (G | 64); VEC float4 per row.
+template <int VEC, int G>
+__global__ __launch_bounds__(256) void k_graphsum(const int4 *__restrict__ items,
+                                                  const int *__restrict__ block_items,
+                                                  int nbc, const int *__restrict__ indices,
                                                   const float *__restrict__ vals,
                                                   const float4 *__restrict__ in, int ld4_in,
                                                   float4 *__restrict__ out, int ld4_out,
                                                   float4 *__restrict__ partial) {
-  constexpr int NB = 64 / VEC;
+  constexpr int NB = G / VEC;  // neighbours per group per iteration
+  constexpr int IPW = 64 / G;  // items per wave
   constexpr bool POW2 = (VEC & (VEC - 1)) == 0;
-  const int lane = threadIdx.x & 63;
-  const int wib = threadIdx.x >> 6;
-  const int nb = lane / VEC, v = lane - nb * VEC;
+  const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
+  const int q = lane / G, r = lane - q * G;
+  const int nb = r / VEC, v = r - nb * VEC;
   const bool active = nb < NB;
-  for (long long it = (long long)blockIdx.x * 4 + wib; it < n_items;
-       it += (long long)gridDim.x * 4) {
+  const int b = blockIdx.x % nbc;
+  const int wg = blockIdx.x / nbc, nwg = gridDim.x / nbc;
+  const int first = block_items[b], last = block_items[b + 1];
+  for (int it = first + (wg * 4 + wib) * IPW + q; it < last; it += nwg * 4 * IPW) {
     const int4 item = items[it];  // {row, begin, end, slot}
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     if (active) {
@@ -70,13 +80,13 @@ __global__ __launch_bounds__(256) void k_graphsum(const int4 *__restrict__ items
     }
     if constexpr (POW2) {
 #pragma unroll
-      for (int m = VEC; m < 64; m <<= 1) acc = f4_add(acc, f4_shfl_xor(acc, m));
+      for (int m = VEC; m < G; m <<= 1) acc = f4_add(acc, f4_shfl_xor(acc, m));
     } else {
-      // every lane gathers the NB partial float4s of its column v in group order
+      static_assert(POW2 || G == 64, "non power-of-two rows use whole-wave items");
       float4 tot = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
       for (int k = 0; k < NB; k++) {
-        const int src = k * VEC + (v < VEC ? v : 0);
+        const int src = k * VEC + v;
         tot = f4_add(tot, make_float4(__shfl(acc.x, src, 64), __shfl(acc.y, src, 64),
                                       __shfl(acc.z, src, 64), __shfl(acc.w, src, 64)));
       }
@@ -91,7 +101,7 @@ __global__ __launch_bounds__(256) void k_graphsum(const int4 *__restrict__ items
   }
 }
 
-// out[row] = sum of partial slots [first, first+count) in slot order
+// out[row] = sum of partial slots [first, first+count) in slot order (count may be 0)
 template <int VEC>
 __global__ __launch_bounds__(256) void k_graphsum_combine(const int4 *__restrict__ comb,
                                                           int n_comb,
@@ -102,20 +112,25 @@ __global__ __launch_bounds__(256) void k_graphsum_combine(const int4 *__restrict
   const int v = (int)(t - ci * VEC);
   if (ci >= n_comb) return;
   const int4 c = comb[ci];  // {row, first_slot, count, -}
-  float4 acc = partial[(long long)c.y * VEC + v];
-  for (int s = 1; s < c.z; s++) acc = f4_add(acc, partial[(long long)(c.y + s) * VEC + v]);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int s = 0; s < c.z; s++) acc = f4_add(acc, partial[(long long)(c.y + s) * VEC + v]);
   out[(long long)c.x * ld4_out + v] = acc;
 }
 
-template <int VEC>
+template <int VEC, int G>
 static void launch_vec(const GraphSchedule &s, const int *indices, const float *vals,
                        const float *in, int ld_in, float *out, int ld_out, float *partial,
                        hipStream_t st) {
   if (s.n_items > 0) {
-    long long blocks = ceil_div(s.n_items, 4);
-    if (blocks > 65535 * 16) blocks = 65535 * 16;
-    hipLaunchKernelGGL(k_graphsum<VEC>, dim3((unsigned)blocks), dim3(256), 0, st, s.items,
-                       s.n_items, indices, vals, reinterpret_cast<const float4 *>(in), ld_in / 4,
+    constexpr int per_wg = 4 * (64 / G);  // items one workgroup takes per sweep
+    long long per_block = ceil_div(s.max_block_items, per_wg);
+    // enough workgroups per column block to fill the block's XCD several times over
+    const long long cap = 4096 / s.nbc;
+    if (per_block > cap) per_block = cap;
+    if (per_block < 1) per_block = 1;
+    hipLaunchKernelGGL((k_graphsum<VEC, G>), dim3((unsigned)(per_block * s.nbc)), dim3(256), 0,
+                       st, s.items, s.block_items, s.nbc, indices, vals,
+                       reinterpret_cast<const float4 *>(in), ld_in / 4,
                        reinterpret_cast<float4 *>(out), ld_out / 4,
                        reinterpret_cast<float4 *>(partial));
   }
@@ -128,16 +143,23 @@ static void launch_vec(const GraphSchedule &s, const int *indices, const float *
   }
 }
 
+int graphsum_group_lanes(int vec) {
+  if (vec == 1) return 16;
+  if (vec == 2 || vec == 4) return 16;
+  return 64;
+}
+
 void launch_graphsum(const GraphSchedule &s, const int *indices, const float *vals,
                      const float *in, int ld_in, float *out, int ld_out, float *partial,
                      hipStream_t st) {
   switch (s.vec) {
-#define PGCN_VEC_CASE(V) \
-  case V:                \
-    launch_vec<V>(s, indices, vals, in, ld_in, out, ld_out, partial, st); break;
-    PGCN_VEC_CASE(1) PGCN_VEC_CASE(2) PGCN_VEC_CASE(3) PGCN_VEC_CASE(4) PGCN_VEC_CASE(5)
-    PGCN_VEC_CASE(6) PGCN_VEC_CASE(7) PGCN_VEC_CASE(8) PGCN_VEC_CASE(9) PGCN_VEC_CASE(10)
-    PGCN_VEC_CASE(11) PGCN_VEC_CASE(12) PGCN_VEC_CASE(16) PGCN_VEC_CASE(32)
+#define PGCN_VEC_CASE(V, G) \
+  case V:                   \
+    launch_vec<V, G>(s, indices, vals, in, ld_in, out, ld_out, partial, st); break;
+    PGCN_VEC_CASE(1, 16) PGCN_VEC_CASE(2, 16) PGCN_VEC_CASE(3, 64) PGCN_VEC_CASE(4, 16)
+    PGCN_VEC_CASE(5, 64) PGCN_VEC_CASE(6, 64) PGCN_VEC_CASE(7, 64) PGCN_VEC_CASE(8, 64)
+    PGCN_VEC_CASE(9, 64) PGCN_VEC_CASE(10, 64) PGCN_VEC_CASE(11, 64) PGCN_VEC_CASE(12, 64)
+    PGCN_VEC_CASE(16, 64) PGCN_VEC_CASE(32, 64)
 #undef PGCN_VEC_CASE
     default:
       throw Error(PGCN_E_INVALID, "graphsum: unsupported row width (float4 count " +

@@ -12,12 +12,16 @@ namespace pgcn {
 struct GraphSchedule {
   int vec = 0;
   int chunk = 0;          // max slots per work item
-  int n_items = 0;        // int4 {row, begin, end, slot(-1 = direct)}
+  int nbc = 1;            // column blocks (workgroup w serves block w % nbc)
+  int n_items = 0;        // int4 {row, begin, end, slot(-1 = direct)}, grouped by block
+  int max_block_items = 0;
   int n_comb = 0;         // int4 {row, first_slot, count, 0}
   long long n_slots = 0;  // partial rows (VEC float4 each)
   const int4 *items = nullptr;
+  const int *block_items = nullptr;  // nbc + 1 offsets into items
   const int4 *comb = nullptr;
 };
+int graphsum_group_lanes(int vec);
 
 void launch_graphsum(const GraphSchedule &s, const int *indices, const float *vals,
                      const float *in, int ld_in, float *out, int ld_out, float *partial,

@@ -2,6 +2,9 @@ import os
 import sys
 
 import pytest
+# torch first: its bundled libamdhip64.so.7 / librccl.so.1 then satisfy libpgcn.so's
+# dependencies (same SONAMEs), so one process never holds two HIP runtimes.
+import torch  # noqa: F401
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 

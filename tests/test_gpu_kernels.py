@@ -1,0 +1,332 @@
+"""Kernel-level parity of the HIP path through the C ABI (include/pgcn.h) vs the oracle.
+
+Device memory comes from torch (plumbing only); every compute call goes through libpgcn.so.
+Tolerances: integer/bit work bit-exact (dropout masks, RNG states, CSR transposes); Adam
+bit-exact (double temporaries as hpdga optim.cpp); sparse-X SpMM bit-exact (CSR order, no
+FMA); GraphSum / MFMA GEMMs within 1e-5 relative to sum|terms| (fp32 reordering only).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+import helpers
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def vp(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def random_graph(n, avg_deg, seed, hubs=0, hub_deg=0, empty_rows=0):
+    """Symmetric random graph in the hpdga CSR form (self loop first, duplicates allowed)."""
+    rng = np.random.default_rng(seed)
+    m = n * avg_deg // 2
+    u = rng.integers(0, n, m)
+    v = rng.integers(0, n, m)
+    if hubs:
+        hu = rng.integers(0, n, hubs)
+        extra_u = np.repeat(hu, hub_deg)
+        extra_v = rng.integers(0, n, hubs * hub_deg)
+        u, v = np.concatenate([u, extra_u]), np.concatenate([v, extra_v])
+    keep = u != v
+    u, v = u[keep], v[keep]
+    src = np.concatenate([u, v, np.arange(n)])
+    dst = np.concatenate([v, u, np.arange(n)])
+    order = np.lexsort((dst, src != dst, src))  # self loop first within a row
+    src, dst = src[order], dst[order]
+    indptr = np.zeros(n + 1, np.int64)
+    np.add.at(indptr, src + 1, 1)
+    indptr = np.cumsum(indptr).astype(np.int32)
+    return indptr, dst.astype(np.int32)
+
+
+def oracle_graphsum(indptr, indices, x, dim):
+    lib = helpers.oracle()
+    n = len(indptr) - 1
+    out = np.zeros((n, dim), np.float32)
+    xin = np.ascontiguousarray(x[:, :dim], np.float32)
+    lib.or_graphsum(n, helpers.ptr(indptr), helpers.ptr(indices), helpers.ptr(xin),
+                    helpers.ptr(out), dim)
+    return out
+
+
+def abs_bound(indptr, indices, x, dim):
+    """sum_j |coef_ij * x_j| per output element (scale of the fp32 reordering error)."""
+    n = len(indptr) - 1
+    deg = np.diff(indptr).astype(np.float64)
+    rows = np.repeat(np.arange(n), np.diff(indptr))
+    coef = 1.0 / np.sqrt(deg[rows] * deg[indices])
+    out = np.zeros((n, dim))
+    np.add.at(out, rows, np.abs(coef)[:, None] * np.abs(x[indices, :dim]))
+    return out
+
+
+@pytest.mark.parametrize("n,deg,dim,hubs", [
+    (3000, 6, 16, 0),        # cora-like, plain schedule
+    (120000, 40, 16, 20),    # table > 4 MB: XCD-blocked schedule, hub rows split in chunks
+    (20000, 12, 41, 5),      # C = 41 (ld 44): whole-wave items
+    (5000, 8, 3, 2),         # pubmed-like C = 3
+    (5000, 8, 7, 2),         # cora C = 7
+    (20000, 10, 128, 3),     # 4-layer hidden 128
+])
+def test_graphsum_vs_oracle(pgcn, n, deg, dim, hubs):
+    indptr, indices = random_graph(n, deg, seed=n + dim, hubs=hubs, hub_deg=3000)
+    ld = (dim + 3) // 4 * 4
+    rng = np.random.default_rng(7)
+    x = np.zeros((n, ld), np.float32)
+    x[:, :dim] = rng.standard_normal((n, dim)).astype(np.float32)
+    g = ctypes.c_void_p()
+    pgcn.check(pgcn.lib.pgcn_graph_create(n, helpers.ptr(indptr), helpers.ptr(indices),
+                                          ctypes.byref(g)), "graph_create")
+    xin = torch.from_numpy(x).to(DEV)
+    out = torch.full((n, ld), float("nan"), device=DEV)
+    for _ in range(2):  # twice: partial buffers and schedules are reused across calls
+        pgcn.check(pgcn.lib.pgcn_graphsum(g, vp(xin), ld, vp(out), ld, dim, stream()), "graphsum")
+    torch.cuda.synchronize()
+    ours = out.cpu().numpy()
+    ref = oracle_graphsum(indptr, indices, x, dim)
+    bound = abs_bound(indptr, indices, x, dim)
+    err = np.abs(ours[:, :dim] - ref)
+    assert (err <= 1e-5 * bound + 1e-30).all(), f"max err/bound {(err / (bound + 1e-30)).max():.3g}"
+    np.testing.assert_array_equal(ours[:, dim:], 0.0)  # padding columns stay zero
+    # deterministic: identical bits on a rerun
+    out2 = torch.empty_like(out)
+    pgcn.lib.pgcn_graphsum(g, vp(xin), ld, vp(out2), ld, dim, stream())
+    torch.cuda.synchronize()
+    assert torch.equal(out, out2)
+    pgcn.lib.pgcn_graph_destroy(g)
+
+
+def test_graphsum_linearity_large(pgcn):
+    """Size-independent property at reddit-like density: GraphSum(a x + b y) == a GS(x) + b GS(y)."""
+    n = 200000
+    indptr, indices = random_graph(n, 100, seed=3, hubs=10, hub_deg=20000)
+    g = ctypes.c_void_p()
+    pgcn.check(pgcn.lib.pgcn_graph_create(n, helpers.ptr(indptr), helpers.ptr(indices),
+                                          ctypes.byref(g)), "graph_create")
+    x = torch.randn(n, 16, device=DEV)
+    y = torch.randn(n, 16, device=DEV)
+    outs = []
+    for inp in (x, y, 2.0 * x - 3.0 * y):
+        o = torch.empty(n, 16, device=DEV)
+        pgcn.lib.pgcn_graphsum(g, vp(inp), 16, vp(o), 16, 16, stream())
+        outs.append(o)
+    torch.cuda.synchronize()
+    lhs, rhs = outs[2], 2.0 * outs[0] - 3.0 * outs[1]
+    scale = (outs[0].abs() + outs[1].abs()).max()
+    assert (lhs - rhs).abs().max() <= 1e-5 * scale
+    # ones in -> row sums of coefficients (checked against float64 numpy)
+    ones = torch.ones(n, 16, device=DEV)
+    o = torch.empty(n, 16, device=DEV)
+    pgcn.lib.pgcn_graphsum(g, vp(ones), 16, vp(o), 16, 16, stream())
+    torch.cuda.synchronize()
+    deg = np.diff(indptr).astype(np.float64)
+    rows = np.repeat(np.arange(n), np.diff(indptr))
+    rs = np.bincount(rows, weights=1.0 / np.sqrt(deg[rows] * deg[indices]), minlength=n)
+    np.testing.assert_allclose(o[:, 0].cpu().numpy(), rs, rtol=2e-5)
+    pgcn.lib.pgcn_graph_destroy(g)
+
+
+def mask_bits(mask_words, n):
+    b = np.unpackbits(mask_words.view(np.uint8), bitorder="little")
+    return b[:n].astype(bool)
+
+
+def test_dropout_masks_bit_exact(pgcn):
+    """Chunk states + GPU mask kernel reproduce the sequential xorshift128+ stream exactly,
+    across two 'epochs' (state advance by the period through the byte tables)."""
+    lib = helpers.oracle()
+    offset, n, period = 12345, 100_003, 250_007
+    # sequential reference: draws offset .. offset+n (epoch 1) and offset+period .. (epoch 2)
+    s = np.zeros(2, np.uint64)
+    lib.or_rng_seed(helpers.ptr(s))
+    seq = np.array([lib.or_rng_next(helpers.ptr(s)) for _ in range(offset + period + n)], np.int64)
+    thr = int(np.float32(0.5) * np.float32(0x7FFFFFFF))
+    ref1 = seq[offset:offset + n] >= thr
+    ref2 = seq[offset + period:offset + period + n] >= thr
+    nch = (n + 63) // 64
+    states = np.zeros((nch, 2), np.uint64)
+    st = pgcn.rng_jump(pgcn.rng_seed(), offset)
+    for c in range(nch):
+        states[c] = st
+        st = pgcn.rng_jump(st, 64)
+    table = torch.from_numpy(pgcn.rng_jump_table(period).view(np.int64)).to(DEV)
+    dstates = torch.from_numpy(states.view(np.int64)).to(DEV)
+    mask = torch.zeros(nch + 1, dtype=torch.int64, device=DEV)
+    for ref in (ref1, ref2):
+        pgcn.check(pgcn.lib.pgcn_dropout_mask(vp(dstates), nch, n, 0, 0.5, vp(mask), vp(table),
+                                              stream()), "dropout_mask")
+        torch.cuda.synchronize()
+        ours = mask_bits(mask.cpu().numpy()[:nch].view(np.uint64), n)
+        np.testing.assert_array_equal(ours, ref)
+
+
+def test_dropout_apply(pgcn):
+    n = 10_007
+    x = torch.randn(n, device=DEV)
+    words = torch.randint(-2**62, 2**62, ((n + 63) // 64 + 1,), dtype=torch.int64, device=DEV)
+    ref = x.cpu().numpy().copy()
+    bits = mask_bits(words.cpu().numpy().view(np.uint64), n)
+    ref = ref * np.where(bits, np.float32(2.0), np.float32(0.0))
+    pgcn.lib.pgcn_dropout_apply(vp(x), n, vp(words), 2.0, stream())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(x.cpu().numpy(), ref.astype(np.float32))
+
+
+@pytest.mark.parametrize("M,N,K,drop", [(1000, 16, 602, True), (777, 41, 16, False),
+                                        (513, 16, 41, False), (300, 128, 128, False),
+                                        (64, 16, 1433, True)])
+def test_gemm_nn(pgcn, M, N, K, drop):
+    rng = np.random.default_rng(M + N + K)
+    lda = (K + 3) // 4 * 4
+    A = np.zeros((M, lda), np.float32)
+    A[:, :K] = rng.standard_normal((M, K))
+    B = rng.standard_normal((K, N)).astype(np.float32)
+    mask = rng.integers(0, 2**63, (M * K + 63) // 64 + 2, dtype=np.uint64)
+    Ae = A[:, :K].astype(np.float64)
+    if drop:
+        bits = mask_bits(mask, M * K).reshape(M, K)
+        Ae = Ae * np.where(bits, 2.0, 0.0)
+    ref = Ae @ B.astype(np.float64)
+    dA, dB = torch.from_numpy(A).to(DEV), torch.from_numpy(B).to(DEV)
+    dm = torch.from_numpy(mask.view(np.int64)).to(DEV)
+    ldc = (N + 3) // 4 * 4
+    C = torch.full((M, ldc), float("nan"), device=DEV)
+    pgcn.check(pgcn.lib.pgcn_gemm(M, N, K, vp(dA), lda, vp(dB), N, 0, vp(C), ldc,
+                                  vp(dm) if drop else None, 0, K, 2.0, stream()), "gemm")
+    # transposed B: C2 = A * (B^T)^T with B^T stored [N][K]
+    dBt = torch.from_numpy(np.ascontiguousarray(B.T)).to(DEV)
+    C2 = torch.empty((M, ldc), device=DEV)
+    pgcn.check(pgcn.lib.pgcn_gemm(M, N, K, vp(dA), lda, vp(dBt), K, 1, vp(C2), ldc,
+                                  vp(dm) if drop else None, 0, K, 2.0, stream()), "gemm_t")
+    torch.cuda.synchronize()
+    bound = np.abs(Ae) @ np.abs(B.astype(np.float64))
+    for out in (C, C2):
+        o = out.cpu().numpy()
+        assert (np.abs(o[:, :N] - ref) <= 1e-5 * bound + 1e-30).all()
+        np.testing.assert_array_equal(o[:, N:], 0.0)
+
+
+@pytest.mark.parametrize("M,N,K,drop", [(5000, 16, 602, True), (3000, 41, 16, False),
+                                        (2000, 128, 128, False), (100, 16, 1433, True),
+                                        (70000, 16, 602, False)])
+def test_gemm_tn(pgcn, M, N, K, drop):
+    rng = np.random.default_rng(M + 3 * N + K)
+    lda = (K + 3) // 4 * 4
+    A = np.zeros((M, lda), np.float32)
+    A[:, :K] = rng.standard_normal((M, K))
+    Gm = rng.standard_normal((M, N)).astype(np.float32)
+    mask = rng.integers(0, 2**63, (M * K + 63) // 64 + 2, dtype=np.uint64)
+    Ae = A[:, :K].astype(np.float64)
+    if drop:
+        Ae = Ae * np.where(mask_bits(mask, M * K).reshape(M, K), 2.0, 0.0)
+    ref = Ae.T @ Gm.astype(np.float64)
+    ws = torch.empty(pgcn.lib.pgcn_gemm_tn_workspace(M, N, K) // 4 + 16, device=DEV)
+    dA, dG = torch.from_numpy(A).to(DEV), torch.from_numpy(Gm).to(DEV)
+    dm = torch.from_numpy(mask.view(np.int64)).to(DEV)
+    C = torch.full((K, N), float("nan"), device=DEV)
+    pgcn.check(pgcn.lib.pgcn_gemm_tn(M, N, K, vp(dA), lda, vp(dG), N, vp(C), N,
+                                     vp(dm) if drop else None, 0, K, 2.0, vp(ws), stream()), "tn")
+    torch.cuda.synchronize()
+    bound = np.abs(Ae).T @ np.abs(Gm.astype(np.float64))
+    assert (np.abs(C.cpu().numpy() - ref) <= 1e-5 * bound + 1e-30).all()
+
+
+def test_spmm_csr_and_csc_bit_exact(pgcn, loaded):
+    """Sparse-X SpMM fwd and W-grad are bit-identical to hpdga's loops (cora features)."""
+    ds = loaded["cora"]
+    lib = helpers.oracle()
+    n, F, p = ds.num_nodes, ds.input_dim, 16
+    rng = np.random.default_rng(1)
+    W = rng.standard_normal((F, p)).astype(np.float32)
+    Gm = rng.standard_normal((n, p)).astype(np.float32)
+    ip, ix, xv = (np.ascontiguousarray(a) for a in (ds.feat_indptr, ds.feat_indices, ds.feat_values))
+    nnz = len(ix)
+    mask = rng.integers(0, 2**63, (nnz + 63) // 64 + 1, dtype=np.uint64)
+    xd = xv * np.where(mask_bits(mask, nnz), np.float32(2.0), np.float32(0.0)).astype(np.float32)
+    ref_c = np.zeros((n, p), np.float32)
+    lib.or_spmm_fwd(n, helpers.ptr(ip), helpers.ptr(ix), helpers.ptr(xd), helpers.ptr(W),
+                    helpers.ptr(ref_c), p)
+    ref_w = np.zeros((F, p), np.float32)
+    lib.or_spmm_bwd(n, F, helpers.ptr(ip), helpers.ptr(ix), helpers.ptr(xd), helpers.ptr(ref_w),
+                    helpers.ptr(Gm), p)
+    cp, cr, cpos = pgcn.csr_transpose(ip, ix, F)
+    t = {k: torch.from_numpy(v).to(DEV) for k, v in
+         dict(ip=ip, ix=ix, xv=xv, W=W, G=Gm, cp=cp, cr=cr, cpos=cpos).items()}
+    dm = torch.from_numpy(mask.view(np.int64)).to(DEV)
+    c = torch.empty((n, p), device=DEV)
+    wg = torch.empty((F, p), device=DEV)
+    pgcn.check(pgcn.lib.pgcn_spmm_csr(n, p, vp(t["ip"]), vp(t["ix"]), vp(t["xv"]), vp(dm), 2.0,
+                                      vp(t["W"]), vp(c), stream()), "spmm")
+    pgcn.check(pgcn.lib.pgcn_spmm_csc_bwd(F, p, vp(t["cp"]), vp(t["cr"]), vp(t["cpos"]),
+                                          vp(t["xv"]), vp(dm), 2.0, vp(t["G"]), vp(wg), stream()),
+               "csc")
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(c.cpu().numpy(), ref_c)
+    np.testing.assert_array_equal(wg.cpu().numpy(), ref_w)
+
+
+def test_adam_bit_exact(pgcn):
+    lib = helpers.oracle()
+    rng = np.random.default_rng(5)
+    n = 9632
+    w = rng.standard_normal(n).astype(np.float32) * 0.1
+    m = np.zeros(n, np.float32)
+    v = np.zeros(n, np.float32)
+    dw, dm_, dv = (torch.from_numpy(a.copy()).to(DEV) for a in (w, m, v))
+    for t in range(1, 6):
+        g = rng.standard_normal(n).astype(np.float32) * 0.01
+        ss = lib.or_adam_step_size(0.01, 0.9, 0.999, t)
+        assert np.float32(ss) == np.float32(pgcn.lib.pgcn_adam_step_size(0.01, 0.9, 0.999, t))
+        lib.or_adam_update(helpers.ptr(w), helpers.ptr(g), helpers.ptr(m), helpers.ptr(v),
+                           ctypes.c_long(n), ctypes.c_float(ss), ctypes.c_float(0.9),
+                           ctypes.c_float(0.999), ctypes.c_float(1e-8), ctypes.c_float(5e-4), 1)
+        dg = torch.from_numpy(g).to(DEV)
+        pgcn.check(pgcn.lib.pgcn_adam(vp(dw), vp(dg), vp(dm_), vp(dv), n, ss, 0.9, 0.999, 1e-8,
+                                      5e-4, 1, stream()), "adam")
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(dw.cpu().numpy(), w)
+    np.testing.assert_array_equal(dm_.cpu().numpy(), m)
+    np.testing.assert_array_equal(dv.cpu().numpy(), v)
+
+
+@pytest.mark.parametrize("n,c", [(2708, 7), (50000, 41), (1000, 3)])
+def test_xent_vs_oracle(pgcn, n, c):
+    lib = helpers.oracle()
+    rng = np.random.default_rng(n)
+    ld = (c + 3) // 4 * 4
+    logits = np.zeros((n, ld), np.float32)
+    logits[:, :c] = rng.standard_normal((n, c)) * 3
+    truth = np.where(rng.random(n) < 0.4, rng.integers(0, c, n), -1).astype(np.int32)
+    count = int((truth >= 0).sum())
+    ref_l = np.ascontiguousarray(logits[:, :c])
+    ref_g = np.zeros((n, c), np.float32)
+    ref_loss = lib.or_xent_fwd(helpers.ptr(ref_l), helpers.ptr(ref_g), helpers.ptr(truth), n, c, 1)
+    ref_acc = lib.or_accuracy(helpers.ptr(ref_l), helpers.ptr(truth), n, c)
+    dl = torch.from_numpy(logits).to(DEV)
+    dg = torch.full((n, ld), float("nan"), device=DEV)
+    dt = torch.from_numpy(truth).to(DEV)
+    nb = pgcn.lib.pgcn_xent_blocks(n)
+    part = torch.zeros(2 * nb + 2, device=DEV)
+    out4 = torch.zeros(4, device=DEV)
+    w = torch.zeros(1, device=DEV)
+    pgcn.check(pgcn.lib.pgcn_xent_fwd(vp(dl), ld, vp(dg), vp(dt), n, c, count, 1, vp(part),
+                                      stream()), "xent")
+    pgcn.check(pgcn.lib.pgcn_finalize(vp(part), nb, count, vp(w), 1, 0.0, vp(out4), stream()),
+               "finalize")
+    torch.cuda.synchronize()
+    o = out4.cpu().numpy()
+    assert abs(o[0] - ref_loss) <= 1e-5 * abs(ref_loss)
+    assert abs(o[1] - ref_acc) * count <= 1.0 + 1e-6
+    np.testing.assert_allclose(dl.cpu().numpy()[:, :c], ref_l, rtol=0, atol=0)  # shift exact
+    np.testing.assert_allclose(dg.cpu().numpy()[:, :c], ref_g, rtol=1e-5, atol=1e-9)
+    np.testing.assert_array_equal(dg.cpu().numpy()[:, c:], 0.0)
