@@ -206,6 +206,11 @@ int pgcn_partition_bounds(int n, const int *indptr, int world, int *bounds_out, 
 long long pgcn_partition_subgraph(int n, const int *indptr, const int *indices, int world,
                                   int rank, int *sub_indptr, int *sub_indices, float *sub_vals);
 
+/* --- diagnostics (profiling ablations; not for production use) ------------------------ */
+/* "graphsum_variant": 0 normal, 1 skip the feature gather, 2 fold gathers into 4096 rows;
+ * "graphsum_plain": 1 disables the XCD column blocking for schedules built afterwards. */
+int pgcn_debug_set(const char *key, int value);
+
 #ifdef __cplusplus
 }
 #endif

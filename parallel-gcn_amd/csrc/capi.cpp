@@ -12,6 +12,11 @@
 
 using namespace pgcn;
 
+namespace pgcn {
+extern int g_graphsum_variant;      // k_graphsum.hip (diagnostics)
+extern int g_graphsum_force_plain;  // host/graph.cpp (diagnostics)
+}  // namespace pgcn
+
 struct pgcn_graph {
   std::unique_ptr<DevGraph> g;
 };
@@ -370,6 +375,15 @@ int pgcn_dataset_view(const pgcn_dataset *ds, pgcn_data *v, int *input_dim, int 
 
 int pgcn_dataset_free(pgcn_dataset *ds) {
   delete ds;
+  return PGCN_OK;
+}
+
+// ---------------------------------------------------------------- diagnostics
+int pgcn_debug_set(const char *key, int value) {
+  if (!key) return PGCN_E_INVALID;
+  if (!std::strcmp(key, "graphsum_variant")) pgcn::g_graphsum_variant = value;
+  else if (!std::strcmp(key, "graphsum_plain")) pgcn::g_graphsum_force_plain = value;
+  else return PGCN_E_INVALID;
   return PGCN_OK;
 }
 

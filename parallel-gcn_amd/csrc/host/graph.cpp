@@ -61,9 +61,12 @@ DevGraph::DevGraph(int n_rows, int n_cols, const int *indptr, const int *indices
   PGCN_HIP(hipMemset(vals_.get() + nnz_, 0, 64 * sizeof(float)));
 }
 
+int g_graphsum_force_plain = 0;  // diagnostics only (pgcn_debug_set)
+
 int DevGraph::column_blocks(int dim) {
   const int vec = (dim + 3) / 4;
   const double table = (double)n_cols_ * vec * 16.0;
+  if (g_graphsum_force_plain) return 1;
   return (graphsum_group_lanes(vec) < 64 && table > kL2Budget) ? kBlocks : 1;
 }
 
@@ -93,17 +96,20 @@ void DevGraph::build_blocked() {
       for (int k = h_indptr_[(size_t)i]; k < h_indptr_[(size_t)i + 1]; k++)
         cnt[(size_t)i * B + block_of(h_indices_[(size_t)k])]++;
   });
-  // block-major segment offsets
+  // block-major segment offsets; every segment padded to a multiple of 4 slots so that the
+  // d=16 kernel reads 4 (index, value) pairs with one aligned 16-byte load per lane.  Padding
+  // slots carry value 0 and the block's first column (an L2-hot row).
   bseg_.assign((size_t)B * (n_rows_ + 1), 0);
   long long base = 0;
   for (int b = 0; b < B; b++) {
     long long *seg = &bseg_[(size_t)b * (n_rows_ + 1)];
     seg[0] = base;
-    for (int i = 0; i < n_rows_; i++) seg[i + 1] = seg[i] + cnt[(size_t)i * B + b];
+    for (int i = 0; i < n_rows_; i++) seg[i + 1] = seg[i] + ((cnt[(size_t)i * B + b] + 3) & ~3);
     base = seg[n_rows_];
   }
-  std::vector<int> bi((size_t)nnz_);
-  std::vector<float> bv((size_t)nnz_);
+  bnnz_ = base;
+  std::vector<int> bi((size_t)bnnz_);
+  std::vector<float> bv((size_t)bnnz_, 0.0f);
   parallel_for(n_rows_, [&](long long b0, long long b1) {
     for (long long i = b0; i < b1; i++) {
       long long o[kBlocks];
@@ -114,14 +120,17 @@ void DevGraph::build_blocked() {
         bv[(size_t)o[b]] = h_vals_[(size_t)k];
         o[b]++;
       }
+      for (int b = 0; b < B; b++)
+        for (long long p = o[b]; p < bseg_[(size_t)b * (n_rows_ + 1) + i + 1]; p++)
+          bi[(size_t)p] = bcut_[(size_t)b] < n_cols_ ? bcut_[(size_t)b] : 0;
     }
   });
-  bindices_.allocate((size_t)nnz_ + 64);
-  bvals_.allocate((size_t)nnz_ + 64);
+  bindices_.allocate((size_t)bnnz_ + 64);
+  bvals_.allocate((size_t)bnnz_ + 64);
   bindices_.upload(bi);
   bvals_.upload(bv);
-  PGCN_HIP(hipMemset(bindices_.get() + nnz_, 0, 64 * sizeof(int)));
-  PGCN_HIP(hipMemset(bvals_.get() + nnz_, 0, 64 * sizeof(float)));
+  PGCN_HIP(hipMemset(bindices_.get() + bnnz_, 0, 64 * sizeof(int)));
+  PGCN_HIP(hipMemset(bvals_.get() + bnnz_, 0, 64 * sizeof(float)));
   blocked_built_ = true;
 }
 

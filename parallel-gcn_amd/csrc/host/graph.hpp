@@ -68,6 +68,7 @@ class DevGraph {
   bool blocked_built_ = false;
   std::vector<int> bcut_;                 // kBlocks + 1 column boundaries
   std::vector<long long> bseg_;           // (kBlocks) x (n_rows + 1) segment offsets
+  long long bnnz_ = 0;                    // blocked slots incl. padding
   DeviceBuffer<int> bindices_;
   DeviceBuffer<float> bvals_;
   std::map<int, std::unique_ptr<Sched>> scheds_;

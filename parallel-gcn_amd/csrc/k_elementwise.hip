@@ -152,7 +152,7 @@ __device__ __forceinline__ float block_sum(float v, float *smem) {
 // divided by the labelled count (known per split on the host). Per-block partial sums
 // (loss, wrong) go to partials[2*block].
 // ------------------------------------------------------------------------------------------
-constexpr int XR = 128;  // rows per cross-entropy block
+constexpr int XR = 64;  // rows per cross-entropy block (one computing wave)
 
 __global__ __launch_bounds__(256) void k_xent_fwd(float *__restrict__ logits, int ld,
                                                   float *__restrict__ grad,
@@ -318,14 +318,9 @@ int xent_blocks(int n) { return (int)ceil_div(n, XR); }
 void launch_xent_fwd(float *logits, int ld, float *grad, const int *truth, int n, int c,
                      int count, int training, float *partials, hipStream_t s) {
   if (n <= 0) return;
-  PGCN_CHECK(ld <= 128 && c <= ld, PGCN_E_INVALID, "xent: classes must be <= 128");
+  PGCN_CHECK(ld <= 124 && c <= ld, PGCN_E_INVALID, "xent: classes must be <= 124");
   const size_t lds = (size_t)2 * XR * (ld + 1) * sizeof(float);
-  static bool attr = false;
-  if (!attr) {  // up to 2*128*129*4 = 132 KB of the CU's 160 KB LDS
-    PGCN_HIP(hipFuncSetAttribute((const void *)k_xent_fwd,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    attr = true;
-  }
+  // <= 2*64*129*4 = 66 KB: within the default dynamic LDS limit for ld <= 124
   hipLaunchKernelGGL(k_xent_fwd, dim3(xent_blocks(n)), dim3(256), lds, s, logits, ld, grad,
                      truth, n, c, count, training, partials);
 }

@@ -128,6 +128,7 @@ __global__ __launch_bounds__(256) void k_gemm_tn(int M, int N, int K, int slab,
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int g = lane >> 4, i = lane & 15;
   const int wk = w % WK, wr = w / WK;
+  const int c0 = (int)blockIdx.y * WK * KCW;  // first 64-wide K chunk of this block
   const long long m_begin = (long long)blockIdx.x * slab;
   long long m_end = m_begin + slab;
   if (m_end > M) m_end = M;
@@ -150,7 +151,7 @@ __global__ __launch_bounds__(256) void k_gemm_tn(int M, int N, int K, int slab,
     }
 #pragma unroll
     for (int c = 0; c < KCW; c++) {
-      const int kb = (wk + WK * c) * 64 + 4 * i;
+      const int kb = (c0 + wk + WK * c) * 64 + 4 * i;
       float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
       if (ok && kb < K) {
         a = *reinterpret_cast<const float4 *>(A + mr * lda + kb);
@@ -200,7 +201,7 @@ __global__ __launch_bounds__(256) void k_gemm_tn(int M, int N, int K, int slab,
           const int col = 16 * j + i;
 #pragma unroll
           for (int r = 0; r < 4; r++) {
-            const int k = (wk + WK * c) * 64 + 4 * (4 * g + r) + t;
+            const int k = (c0 + wk + WK * c) * 64 + 4 * (4 * g + r) + t;
             if (k < K && col < ldp) p[(long long)k * ldp + col] = v[r];
           }
         }
@@ -256,7 +257,7 @@ void launch_gemm_nn(int M, int N, int K, const float *A, int lda, const float *B
 }
 
 struct TnPlan {
-  int nj, nkc, wk, kcw, slab, n_slabs, ldp, spg, n_groups;
+  int nj, nkc, wk, kcw, kgroups, slab, n_slabs, ldp, spg, n_groups;
 };
 
 static TnPlan tn_plan(int M, int N, int K) {
@@ -265,7 +266,8 @@ static TnPlan tn_plan(int M, int N, int K) {
   p.ldp = p.nj * 16;
   p.nkc = (K + 63) / 64;
   p.wk = p.nkc >= 4 ? 4 : (p.nkc >= 2 ? 2 : 1);
-  p.kcw = (p.nkc + p.wk - 1) / p.wk;
+  p.kcw = std::min(3, (p.nkc + p.wk - 1) / p.wk);
+  p.kgroups = (p.nkc + p.wk * p.kcw - 1) / (p.wk * p.kcw);
   const int wr = 4 / p.wk;
   long long slab = ceil_div(M, 512);
   const int q = 4 * wr;
@@ -293,7 +295,7 @@ void launch_gemm_tn(int M, int N, int K, const float *A, int lda, const float *G
   float *part2 = partial + (size_t)p.n_slabs * K * p.ldp;
   const long long elems = (long long)K * p.ldp;
   if (M > 0) {
-    const dim3 grid((unsigned)p.n_slabs), block(256);
+    const dim3 grid((unsigned)p.n_slabs, (unsigned)p.kgroups), block(256);
     bool done = false;
 #define TN_CASE(NJ, KCW, WK)                                                                   \
   if (!done && p.nj == NJ && p.kcw == KCW && p.wk == WK) {                                    \

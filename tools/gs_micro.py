@@ -1,0 +1,94 @@
+"""GraphSum ablation micro-benchmark on the reddit-shaped graph (run on the GPU box).
+
+Times pgcn_graphsum (kernel + combine) per call with HIP events on torch's stream for:
+dim 16 (blocked schedule), the same without XCD column blocking, no-gather and folded-table
+ablations, and dim 32 (128-B rows).  Prints one JSON object.
+"""
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+import helpers  # noqa: E402
+
+pg = helpers.pgcn()
+edges = 57307946
+ONLY = sys.argv[1] if len(sys.argv) > 1 else None  # run one configuration (for PMC passes)
+t0 = time.time()
+ds = pg.Dataset.synthetic(232965, 602, 41, edges, 1)
+n = ds.num_nodes
+ip = np.ascontiguousarray(ds.graph_indptr)
+ix = np.ascontiguousarray(ds.graph_indices)
+gen_s = time.time() - t0
+
+
+def make_graph():
+    g = ctypes.c_void_p()
+    pg.check(pg.lib.pgcn_graph_create(n, helpers.ptr(ip), helpers.ptr(ix), ctypes.byref(g)), "g")
+    return g
+
+
+def timeit(g, dim, reps=10):
+    ld = (dim + 3) // 4 * 4
+    x = torch.randn(n, ld, device="cuda")
+    o = torch.empty(n, ld, device="cuda")
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for _ in range(2):
+        pg.check(pg.lib.pgcn_graphsum(g, ctypes.c_void_p(x.data_ptr()), ld,
+                                      ctypes.c_void_p(o.data_ptr()), ld, dim, s), "gs")
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        pg.lib.pgcn_graphsum(g, ctypes.c_void_p(x.data_ptr()), ld, ctypes.c_void_p(o.data_ptr()),
+                             ld, dim, s)
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+res = {"nnz": int(ip[-1]), "gen_s": gen_s}
+if ONLY:
+    variant = {"nogather": 1, "table4096": 2}.get(ONLY, 0)
+    if ONLY == "plain":
+        pg.lib.pgcn_debug_set(b"graphsum_plain", 1)
+    pg.lib.pgcn_debug_set(b"graphsum_variant", variant)
+    g = make_graph()
+    res[ONLY + "_ms"] = timeit(g, 32 if ONLY == "d32" else 16, reps=5)
+    print(json.dumps(res))
+    sys.exit(0)
+g = make_graph()
+res["d16_blocked_ms"] = timeit(g, 16)
+pg.lib.pgcn_debug_set(b"graphsum_variant", 3)
+res["d16_blocked_v2_ms"] = timeit(g, 16)
+pg.lib.pgcn_debug_set(b"graphsum_variant", 5)
+res["d16_blocked_v3_ms"] = timeit(g, 16)
+pg.lib.pgcn_debug_set(b"graphsum_variant", 11)
+res["d16_v3_nogather_ms"] = timeit(g, 16)
+pg.lib.pgcn_debug_set(b"graphsum_variant", 14)
+res["d16_v3_noindexstream_ms"] = timeit(g, 16)
+pg.lib.pgcn_debug_set(b"graphsum_variant", 1)
+res["d16_nogather_ms"] = timeit(g, 16)
+pg.lib.pgcn_debug_set(b"graphsum_variant", 2)
+res["d16_table4096_ms"] = timeit(g, 16)
+pg.lib.pgcn_debug_set(b"graphsum_variant", 0)
+res["d32_blocked_ms"] = timeit(g, 32)
+res["d41_ms"] = timeit(g, 41, reps=3)
+pg.lib.pgcn_graph_destroy(g)
+pg.lib.pgcn_debug_set(b"graphsum_plain", 1)
+g = make_graph()
+res["d16_plain_ms"] = timeit(g, 16)
+res["d32_plain_ms"] = timeit(g, 32)
+pg.lib.pgcn_graph_destroy(g)
+pg.lib.pgcn_debug_set(b"graphsum_plain", 0)
+nnz = res["nnz"]
+for k in list(res):
+    if k.endswith("_ms") and k.startswith("d16"):
+        res[k.replace("_ms", "_alg_GBs")] = (4 * (n + 1) + 8 * nnz + 8 * n * 16) / (res[k] * 1e-3) / 1e9
+print(json.dumps(res))
