@@ -127,6 +127,7 @@ def main():
 
     def barrier():
         g.sync()
+        torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
 
@@ -136,11 +137,9 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         g.epoch_async()
-    g.sync()
-    elapsed = time.perf_counter() - t0
     barrier()
+    elapsed = time.perf_counter() - t0
     if dist is not None:
-        import torch
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())

@@ -1,0 +1,185 @@
+"""Host-side (no GPU) tests: the C ABI library, the kept hpdga loader, the RNG jump-ahead that
+drives the device dropout masks, the edge-cut partition plan and the synthetic generator.
+
+All run on CPU: libpgcn.so is loaded but no device call is made."""
+import ctypes
+import hashlib
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+import helpers
+
+HEADER = os.path.join(helpers.REPO, "include", "pgcn.h")
+
+
+def header_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(pgcn_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_header_symbol(pgcn):
+    decl = header_functions()
+    assert len(decl) >= 40
+    raw = ctypes.CDLL(pgcn.LIB_PATH)
+    missing = [s for s in decl if not hasattr(raw, s)]
+    assert not missing, f"declared in include/pgcn.h but not exported: {missing}"
+    assert sorted(pgcn.EXPORTED) == decl, "python glue and header disagree"
+
+
+def test_status_strings(pgcn):
+    for st in (pgcn.PGCN_OK, pgcn.PGCN_E_INVALID, pgcn.PGCN_E_NOMEM, pgcn.PGCN_E_IO,
+               pgcn.PGCN_E_COMM, pgcn.PGCN_E_NODEVICE):
+        assert pgcn.lib.pgcn_status_string(st)
+    assert pgcn.lib.pgcn_version() > 0
+
+
+def test_create_without_device_fails_loudly(pgcn, loaded):
+    """No CPU fallback: creating an engine on a host without a HIP device must raise."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a device is present")
+    ds = loaded["cora"]
+    with pytest.raises(pgcn.PgcnError):
+        pgcn.GCN(pgcn.make_params(ds), ds)
+
+
+@pytest.mark.parametrize("name", ["cora", "citeseer", "pubmed_synth"])
+def test_loader_matches_manifest(loaded, name):
+    """The kept hpdga Parser (src/parser.cpp:6-140) yields exactly the arrays the reference
+    build parsed (sha256 of the little-endian arrays, tests/golden/manifest.json)."""
+    man = json.load(open(os.path.join(helpers.GOLDEN, "manifest.json")))["datasets"][name]["parsed"]
+    ds = loaded[name]
+    for key, want in man.items():
+        a = np.ascontiguousarray(getattr(ds, key))
+        assert a.size == want["count"], key
+        assert hashlib.sha256(a.tobytes()).hexdigest() == want["sha256"], key
+
+
+def test_loader_missing_dataset_raises(pgcn, tmp_path):
+    with pytest.raises(pgcn.PgcnError):
+        pgcn.Dataset.load(str(tmp_path), "nonexistent")
+
+
+@pytest.mark.parametrize("k", [0, 1, 2, 63, 64, 1000, 123457])
+def test_rng_jump_matches_sequential_draws(pgcn, k):
+    """GF(2) jump-ahead (csrc/rng.cpp) == k sequential xorshift128+ draws of the oracle
+    (hpdga src/rand.cpp:5-24)."""
+    orc = helpers.oracle()
+    s = (ctypes.c_uint64 * 2)()
+    orc.or_rng_seed(s)
+    seed = pgcn.rng_seed()
+    assert [int(seed[0]), int(seed[1])] == [s[0], s[1]]
+    for _ in range(k):
+        orc.or_rng_next(s)
+    got = pgcn.rng_jump(seed, k)
+    assert [int(got[0]), int(got[1])] == [s[0], s[1]]
+
+
+def test_rng_jump_table_composes(pgcn):
+    """The 16 x 256 byte tables of M^period reproduce rng_jump(state, period) on random states."""
+    period = 98765
+    t = pgcn.rng_jump_table(period).reshape(16, 256, 2)
+    rs = np.random.default_rng(5)
+    for _ in range(8):
+        st = rs.integers(1, 2**63, size=2, dtype=np.uint64)
+        want = pgcn.rng_jump(st, period)
+        acc = np.zeros(2, np.uint64)
+        bits = int(st[0]) | (int(st[1]) << 64)
+        for byte in range(16):
+            acc ^= t[byte, (bits >> (8 * byte)) & 0xFF]
+        assert [int(acc[0]), int(acc[1])] == [int(want[0]), int(want[1])]
+
+
+def _coef_matrix(ds):
+    """Â as a scipy CSR with the hpdga coefficients (from the oracle's coefficient function)."""
+    import scipy.sparse as sp
+    ip, ix = ds.graph_indptr, ds.graph_indices
+    deg = np.diff(ip).astype(np.int64)
+    rows = np.repeat(np.arange(ds.num_nodes), deg)
+    vals = np.array([helpers.oracle().or_graph_coef(ip.ctypes.data_as(ctypes.c_void_p),
+                                                    int(r), int(c))
+                     for r, c in zip(rows[:64], ix[:64])], np.float32)
+    dd = (deg[rows] * deg[ix]).astype(np.float32)
+    full = (1.0 / np.sqrt(dd).astype(np.float64)).astype(np.float32)
+    np.testing.assert_array_equal(full[:64], vals)  # same rounding as the oracle's scalar path
+    return sp.csr_matrix((full, ix, ip), shape=(ds.num_nodes, ds.num_nodes))
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_partition_bounds_balanced(pgcn, loaded, world):
+    ds = loaded["pubmed_synth"]
+    ip = ds.graph_indptr
+    b, maxrows = pgcn.partition_bounds(ip, world)
+    assert b[0] == 0 and b[-1] == ds.num_nodes and np.all(np.diff(b) > 0)
+    assert maxrows == np.diff(b).max()
+    nnz = np.diff(ip[b])
+    # contiguous cuts can miss the ideal by at most one row's worth of slots
+    assert nnz.max() <= ip[-1] / world + np.diff(ip).max() + 1
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_partition_subgraphs_recompose_graphsum(pgcn, loaded, world):
+    """sum over ranks of (rank's column block of Â) x H[rank rows] == Â H, in the padded row
+    layout the reduce-scatter consumes."""
+    ds = loaded["cora"]
+    A = _coef_matrix(ds)
+    b, maxrows = pgcn.partition_bounds(ds.graph_indptr, world)
+    H = np.random.default_rng(0).standard_normal((ds.num_nodes, 7)).astype(np.float32)
+    acc = np.zeros((world * maxrows, 7), np.float64)
+    total = 0
+    for r in range(world):
+        sp_, si, sv = pgcn.partition_subgraph(ds.graph_indptr, ds.graph_indices, world, r)
+        total += len(si)
+        lo, hi = b[r], b[r + 1]
+        assert si.size == 0 or (si.min() >= 0 and si.max() < hi - lo)
+        import scipy.sparse as sps
+        blk = sps.csr_matrix((sv, si, sp_), shape=(world * maxrows, hi - lo))
+        acc += blk @ H[lo:hi].astype(np.float64)
+    assert total == ds.graph_indptr[-1]
+    want = A.astype(np.float64) @ H.astype(np.float64)
+    for r in range(world):
+        lo, hi = b[r], b[r + 1]
+        np.testing.assert_allclose(acc[r * maxrows:r * maxrows + hi - lo], want[lo:hi],
+                                   rtol=1e-5, atol=1e-6)
+        assert np.all(acc[r * maxrows + hi - lo:(r + 1) * maxrows] == 0)
+
+
+def test_csr_transpose(pgcn, loaded):
+    ds = loaded["citeseer"]
+    cp, cr, cpos = pgcn.csr_transpose(ds.feat_indptr, ds.feat_indices, ds.input_dim)
+    import scipy.sparse as sps
+    m = sps.csr_matrix((np.arange(1, len(ds.feat_indices) + 1), ds.feat_indices, ds.feat_indptr),
+                       shape=(ds.num_nodes, ds.input_dim)).tocsc()
+    np.testing.assert_array_equal(cp, m.indptr)
+    np.testing.assert_array_equal(cr, m.indices)
+    np.testing.assert_array_equal(cpos + 1, m.data)  # row-major slot of each CSC entry
+
+
+def test_synthetic_generator_properties(pgcn):
+    """Seeded reddit-shaped generator: symmetric, sorted rows with a self loop, deterministic,
+    labels in range, split counts proportional to reddit's 153431/23831/55703."""
+    n, f, c, e = 3000, 12, 5, 40000
+    a = pgcn.Dataset.synthetic(n, f, c, e, seed=7)
+    b = pgcn.Dataset.synthetic(n, f, c, e, seed=7)
+    for key in ("graph_indptr", "graph_indices", "feat_values", "label", "split"):
+        np.testing.assert_array_equal(getattr(a, key), getattr(b, key))
+    ip, ix = a.graph_indptr, a.graph_indices
+    assert ip[-1] == 2 * e + n
+    import scipy.sparse as sps
+    m = sps.csr_matrix((np.ones(len(ix)), ix, ip), shape=(n, n))
+    assert (m != m.T).nnz == 0
+    assert np.all(m.diagonal() == 1)
+    for i in range(0, n, 97):  # self loop first, then neighbours ascending (hpdga row order)
+        row = ix[ip[i]:ip[i + 1]]
+        assert row[0] == i and np.all(np.diff(row[1:]) >= 0)
+    assert a.label.min() >= 0 and a.label.max() < c
+    cnt = np.bincount(a.split, minlength=4)[1:4] / n
+    np.testing.assert_allclose(cnt, np.array([153431, 23831, 55703]) / 232965, atol=0.02)
+    assert np.array_equal(a.feat_indptr, np.arange(n + 1) * f)
+    other = pgcn.Dataset.synthetic(n, f, c, e, seed=8)
+    assert not np.array_equal(other.graph_indices[:1000], ix[:1000])

@@ -114,3 +114,49 @@ def test_final_weights(engine_runs, name):
         scale = np.abs(ref).max()
         # 100 Adam epochs amplify fp32 reordering; the contract is the loss lines above
         assert np.abs(ours - ref).max() <= 1e-2 * scale
+
+
+@pytest.mark.parametrize("name", ["cora", "pubmed_synth"])
+def test_edge_cut_engine_world1(loaded, pgcn, name):
+    """The multi-GPU engine (partitioned graph, RCCL reduce-scatter / all-reduce) with a
+    one-rank communicator: the same epoch lines as the reference."""
+    ds = loaded[name]
+    g = pgcn.GCN(pgcn.make_params(ds), ds, device=0, rank=0, world=1,
+                 unique_id=pgcn.comm_unique_id())
+    assert g.node_range() == (0, ds.num_nodes)
+    gold = helpers.golden(name)["epoch_lines"].reshape(-1, 4)
+    for e in range(20):
+        tl, ta = g.train_epoch()
+        vl, va = g.eval(2)
+        for ours, ref in ((tl, gold[e, 0]), (vl, gold[e, 2])):
+            assert abs(ours - ref) <= 1e-4 * abs(ref), (e, ours, ref)
+    g.close()
+
+
+def test_deep_model_matches_oracle(loaded, pgcn):
+    """4-layer, hidden 128 (the deep configuration of SURVEY.md §8a): the engine's L-layer
+    stack against the oracle's L-layer restatement of the same module order."""
+    ds = loaded["citeseer"]
+    dims, drops = (128, 128, 128), (0.5, 0.5, 0.5, 0.5)
+    g = pgcn.GCN(pgcn.make_params(ds, hidden_dims=dims, dropouts=drops), ds)
+    ref = helpers.OracleGCN(helpers.ds_dict(ds), hidden_dims=dims, dropouts=drops)
+    for e in range(10):
+        ours = g.train_epoch() + g.eval(2)
+        want = ref.train_epoch() + ref.eval(2)
+        for k in (0, 2):
+            assert abs(ours[k] - want[k]) <= 1e-4 * abs(want[k]), (e, k, ours, want)
+    g.close()
+
+
+def test_async_epochs_match_sync(loaded, pgcn):
+    """epoch_async (the bench loop: no host sync per epoch) produces the same lines."""
+    ds = loaded["cora"]
+    g = pgcn.GCN(pgcn.make_params(ds), ds)
+    for _ in range(10):
+        g.epoch_async()
+    g.sync()
+    res = g.results(10)
+    gold = helpers.golden("cora")["epoch_lines"].reshape(-1, 4)
+    np.testing.assert_allclose(res[:, 0], gold[:10, 0], rtol=1e-4)
+    np.testing.assert_allclose(res[:, 2], gold[:10, 2], rtol=1e-4)
+    g.close()
