@@ -15,6 +15,7 @@ using namespace pgcn;
 namespace pgcn {
 extern int g_graphsum_variant;      // k_graphsum.hip (diagnostics)
 extern int g_graphsum_force_plain;  // host/graph.cpp (diagnostics)
+extern int g_graphsum_lds;          // host/graph.cpp (diagnostics)
 }  // namespace pgcn
 
 struct pgcn_graph {
@@ -98,6 +99,8 @@ int pgcn_graph_create(int n, const int *indptr, const int *indices, pgcn_graph *
     std::vector<float> v = graph_coefs(n, indptr, indices);
     auto h = std::make_unique<pgcn_graph>();
     h->g = std::make_unique<DevGraph>(n, n, indptr, indices, v.data());
+    std::vector<float> sc = degree_scales(n, indptr);
+    h->g->set_scales(sc, sc);
     *out = h.release();
   });
 }
@@ -383,6 +386,7 @@ int pgcn_debug_set(const char *key, int value) {
   if (!key) return PGCN_E_INVALID;
   if (!std::strcmp(key, "graphsum_variant")) pgcn::g_graphsum_variant = value;
   else if (!std::strcmp(key, "graphsum_plain")) pgcn::g_graphsum_force_plain = value;
+  else if (!std::strcmp(key, "graphsum_lds")) pgcn::g_graphsum_lds = value;
   else return PGCN_E_INVALID;
   return PGCN_OK;
 }

@@ -208,10 +208,21 @@ void GCN::build(const GCNData &data) {
     std::vector<float> sv;
     partition_subgraph(part, N, data.graph.indptr.data(), data.graph.indices.data(), &sp, &si, &sv);
     graph = std::make_unique<DevGraph>(part.world * part.maxrows, part.local_rows(), sp.data(), si.data(), sv.data());
+    // vals = s_row * s_col with s = 1/sqrt(global degree): padded row q*maxrows + k is global
+    // row bounds[q] + k; local column c is global node first() + c
+    const std::vector<float> sg = degree_scales(N, data.graph.indptr.data());
+    std::vector<float> rs((size_t)part.world * part.maxrows, 0.0f), cs((size_t)part.local_rows());
+    for (int q = 0; q < part.world; q++)
+      for (int i = part.bounds[(size_t)q]; i < part.bounds[(size_t)q + 1]; i++)
+        rs[(size_t)q * part.maxrows + (i - part.bounds[(size_t)q])] = sg[(size_t)i];
+    for (int c = 0; c < part.local_rows(); c++) cs[(size_t)c] = sg[(size_t)part.first() + c];
+    graph->set_scales(std::move(rs), std::move(cs));
   } else {
     std::vector<float> v = graph_coefs(N, data.graph.indptr.data(), data.graph.indices.data());
     graph = std::make_unique<DevGraph>(N, N, data.graph.indptr.data(), data.graph.indices.data(),
                                        v.data());
+    const std::vector<float> sg = degree_scales(N, data.graph.indptr.data());
+    graph->set_scales(sg, sg);
   }
   upload_features(data);
   // truth per split for this rank's rows, padded with -1 (set_truth, src/gcn.cu:204-226)

@@ -15,13 +15,14 @@ float graph_coef(int deg_src, int deg_dst) {
   return (float)(1.0 / (double)sqrtf((float)(deg_src * deg_dst)));
 }
 
-void parallel_for(long long n, const std::function<void(long long, long long)> &f, int threads) {
+void parallel_for(long long n, const std::function<void(long long, long long)> &f, int threads,
+                  long long min_parallel) {
   if (threads <= 0) {
     threads = (int)std::thread::hardware_concurrency();
     if (threads > 16) threads = 16;  // the GPU box grants 16 CPUs per GPU
     if (threads < 1) threads = 1;
   }
-  if (n < 100000 || threads == 1) {
+  if (n < min_parallel || threads == 1) {
     f(0, n);
     return;
   }
@@ -49,6 +50,15 @@ std::vector<float> graph_coefs(int n, const int *indptr, const int *indices) {
   return v;
 }
 
+std::vector<float> degree_scales(int n, const int *indptr) {
+  std::vector<float> s((size_t)n);
+  for (int i = 0; i < n; i++) {
+    const int d = indptr[i + 1] - indptr[i];
+    s[(size_t)i] = d > 0 ? (float)(1.0 / std::sqrt((double)d)) : 0.0f;
+  }
+  return s;
+}
+
 DevGraph::DevGraph(int n_rows, int n_cols, const int *indptr, const int *indices,
                    const float *vals)
     : n_rows_(n_rows), n_cols_(n_cols), nnz_(indptr[n_rows]), h_indptr_(indptr, indptr + n_rows + 1),
@@ -70,11 +80,10 @@ int DevGraph::column_blocks(int dim) {
   return (graphsum_group_lanes(vec) < 64 && table > kL2Budget) ? kBlocks : 1;
 }
 
-// Cut the columns into kBlocks nnz-balanced ranges and store the edges block-major.
-void DevGraph::build_blocked() {
-  if (blocked_built_) return;
+// Cut the columns into kBlocks nnz-balanced ranges.
+void DevGraph::compute_cuts() {
+  if (!bcut_.empty()) return;
   const int B = kBlocks;
-  // column occurrence counts -> nnz-balanced cuts
   std::vector<long long> colcnt((size_t)n_cols_ + 1, 0);
   for (long long k = 0; k < nnz_; k++) colcnt[(size_t)h_indices_[(size_t)k] + 1]++;
   for (int c = 0; c < n_cols_; c++) colcnt[(size_t)c + 1] += colcnt[(size_t)c];
@@ -86,6 +95,13 @@ void DevGraph::build_blocked() {
     c = std::max(c, bcut_[(size_t)b - 1]);
     bcut_[(size_t)b] = std::min(c, n_cols_);
   }
+}
+
+// Store the edges block-major (per column block, rows in order).
+void DevGraph::build_blocked() {
+  if (blocked_built_) return;
+  const int B = kBlocks;
+  compute_cuts();
   auto block_of = [&](int col) {
     return (int)(std::upper_bound(bcut_.begin(), bcut_.end(), col) - bcut_.begin()) - 1;
   };
@@ -229,10 +245,162 @@ DevGraph::Sched &DevGraph::schedule(int vec) {
   return ref;
 }
 
+void DevGraph::set_scales(std::vector<float> row_scale, std::vector<float> col_scale) {
+  PGCN_CHECK((int)row_scale.size() == n_rows_ && (int)col_scale.size() == n_cols_,
+             PGCN_E_INVALID, "set_scales: sizes");
+  h_row_scale_ = std::move(row_scale);
+  h_col_scale_ = std::move(col_scale);
+  lds_.reset();
+}
+
+int g_graphsum_lds = 1;  // diagnostics (pgcn_debug_set "graphsum_lds"): 0 disables the LDS path
+
+// LDS-staged d = 16 schedule (see k_graphsum_lds.hip for the layout it feeds).
+void DevGraph::build_lds() {
+  compute_cuts();
+  const int B = kBlocks, SR = LDS_SR, CW = LDS_CW, NS = LDS_SLOTS;
+  auto L = std::make_unique<LdsSched>();
+  // slices of each column block
+  std::vector<int> nsl((size_t)B);
+  int t_max = 1;
+  for (int b = 0; b < B; b++) {
+    nsl[(size_t)b] = (bcut_[(size_t)b + 1] - bcut_[(size_t)b] + SR - 1) / SR;
+    t_max = std::max(t_max, nsl[(size_t)b]);
+  }
+  std::vector<int2> slices((size_t)B * t_max, make_int2(0, 0));
+  for (int b = 0; b < B; b++)
+    for (int t = 0; t < nsl[(size_t)b]; t++) {
+      const int c0 = bcut_[(size_t)b] + t * SR;
+      slices[(size_t)b * t_max + t] = make_int2(c0, std::min(SR, bcut_[(size_t)b + 1] - c0));
+    }
+  // rowsets: rows by degree (descending), 16 per rowset, dealt round-robin to batches
+  std::vector<int> order((size_t)n_rows_);
+  std::iota(order.begin(), order.end(), 0);
+  std::stable_sort(order.begin(), order.end(), [&](int a, int c) {
+    return h_indptr_[(size_t)a + 1] - h_indptr_[(size_t)a] > h_indptr_[(size_t)c + 1] - h_indptr_[(size_t)c];
+  });
+  const long long nrs = ((long long)n_rows_ + 15) / 16;
+  const long long cap = (long long)CW * NS;
+  const int nbat = (int)std::max<long long>((nrs + cap - 1) / cap, 256 / B);
+  const long long n_wg = (long long)nbat * B;
+  std::vector<int> rows((size_t)nbat * CW * NS * 16, -1);
+  for (long long r = 0; r < nrs; r++) {
+    const long long bat = r % nbat, q = r / nbat, w = q % CW, j = q / CW;
+    for (int g = 0; g < 16; g++) {
+      const long long i = 16 * r + g;
+      rows[(size_t)(((bat * CW + w) * NS + j) * 16 + g)] = i < n_rows_ ? order[(size_t)i] : -1;
+    }
+  }
+  // column-sorted copy of every row (a row's edges inside a slice are then one run)
+  std::vector<int> sidx(h_indices_);
+  parallel_for(n_rows_, [&](long long b0, long long b1) {
+    for (long long i = b0; i < b1; i++)
+      std::sort(sidx.begin() + h_indptr_[(size_t)i], sidx.begin() + h_indptr_[(size_t)i + 1]);
+  });
+  std::vector<unsigned short> counts((size_t)n_wg * t_max * CW * NS, 0);
+  std::vector<long long> kbs((size_t)n_wg * CW, 0);
+  // walks (wg, wave): for each slice, each rowset slot, the 16 rows' runs in that slice
+  auto walk = [&](long long wg, int w, unsigned short *out_entries) {
+    const int b = (int)(wg % B), bat = (int)(wg / B);
+    const int *rw = &rows[(size_t)(((long long)bat * CW + w) * NS) * 16];
+    int cur[LDS_SLOTS * 16], end[LDS_SLOTS * 16];
+    for (int k = 0; k < NS * 16; k++) {
+      const int r = rw[k];
+      if (r < 0) {
+        cur[k] = end[k] = 0;
+        continue;
+      }
+      const int *rb = &sidx[(size_t)h_indptr_[(size_t)r]], *re = &sidx[(size_t)h_indptr_[(size_t)r + 1]];
+      cur[k] = (int)(std::lower_bound(rb, re, bcut_[(size_t)b]) - sidx.data());
+      end[k] = h_indptr_[(size_t)r + 1];
+    }
+    long long kb_total = 0;
+    for (int t = 0; t < nsl[(size_t)b]; t++) {
+      const int2 sc = slices[(size_t)b * t_max + t];
+      const int c1 = sc.x + sc.y;
+      for (int j = 0; j < NS; j++) {
+        int n[16], m = 0;
+        for (int g = 0; g < 16; g++) {
+          const int k = j * 16 + g;
+          int e = cur[k];
+          while (e < end[k] && sidx[(size_t)e] < c1) e++;
+          n[g] = e - cur[k];
+          m = std::max(m, n[g]);
+        }
+        PGCN_CHECK(m < 65536, PGCN_E_INVALID, "graphsum_lds: slice run too long");
+        counts[(size_t)(((wg * t_max + t) * CW + w) * NS + j)] = (unsigned short)m;
+        const int nkb = (m + 3) / 4;
+        if (out_entries) {
+          for (int kb = 0; kb < nkb; kb++)
+            for (int g = 0; g < 16; g++)
+              for (int u = 0; u < 4; u++) {
+                const int s = 4 * kb + u;
+                const int k = j * 16 + g;
+                out_entries[(kb_total + kb) * 64 + g * 4 + u] =
+                    (unsigned short)(s < n[g] ? (sidx[(size_t)cur[k] + s] - sc.x) * 4 : SR * 4);
+              }
+        }
+        for (int g = 0; g < 16; g++) cur[j * 16 + g] += n[g];
+        kb_total += nkb;
+      }
+    }
+    return kb_total;
+  };
+  parallel_for(n_wg * CW, [&](long long a, long long e) {
+    for (long long x = a; x < e; x++) kbs[(size_t)x] = walk(x / CW, (int)(x % CW), nullptr);
+  }, 0, 64);
+  std::vector<long long> off((size_t)n_wg * CW + 1, 0);
+  for (size_t x = 0; x < kbs.size(); x++) off[x + 1] = off[x] + kbs[x];
+  const long long total_kb = off.back();
+  std::vector<unsigned short> ent((size_t)std::max<long long>(total_kb, 1) * 64, 0);
+  parallel_for(n_wg * CW, [&](long long a, long long e) {
+    for (long long x = a; x < e; x++) walk(x / CW, (int)(x % CW), &ent[(size_t)off[(size_t)x] * 64]);
+  }, 0, 64);
+  // + 1 KB slack: ring refills read whole 512-B chunks past a wave's last entry block
+  L->entries.allocate(ent.size() / 4 + 128);
+  L->entries.upload(reinterpret_cast<const uint2 *>(ent.data()), ent.size() / 4);
+  L->wave_off.allocate(off.size());
+  L->wave_off.upload(off);
+  L->counts.allocate(counts.size());
+  L->counts.upload(counts);
+  L->slices.allocate(slices.size());
+  L->slices.upload(slices);
+  L->n_slices.allocate(nsl.size());
+  L->n_slices.upload(nsl);
+  L->rows.allocate(rows.size());
+  L->rows.upload(rows);
+  L->row_scale.allocate(h_row_scale_.size());
+  L->row_scale.upload(h_row_scale_);
+  L->col_scale.allocate(h_col_scale_.size());
+  L->col_scale.upload(h_col_scale_);
+  L->scratch.allocate((size_t)n_cols_ * 16 + 64);
+  L->partial.allocate((size_t)B * n_rows_ * 16);
+  L->s.n_rows = n_rows_;
+  L->s.n_cols = n_cols_;
+  L->s.n_batches = nbat;
+  L->s.t_max = t_max;
+  L->s.entries = L->entries.get();
+  L->s.wave_off = L->wave_off.get();
+  L->s.counts = L->counts.get();
+  L->s.slices = L->slices.get();
+  L->s.n_slices = L->n_slices.get();
+  L->s.rows = L->rows.get();
+  L->s.row_scale = L->row_scale.get();
+  L->s.col_scale = L->col_scale.get();
+  lds_ = std::move(L);
+}
+
 void DevGraph::graphsum(const float *in, int ld_in, float *out, int ld_out, int dim,
                         hipStream_t s) {
   PGCN_CHECK(ld_in % 4 == 0 && ld_out % 4 == 0 && ld_in >= dim && ld_out >= dim,
              PGCN_E_INVALID, "graphsum: leading dims must be multiples of 4 and >= dim");
+  if (dim == 16 && g_graphsum_lds && !h_row_scale_.empty() && !g_graphsum_force_plain &&
+      (double)n_cols_ * 64.0 > kL2Budget) {
+    if (!lds_) build_lds();
+    launch_graphsum_lds(lds_->s, in, ld_in, out, ld_out, lds_->scratch.get(),
+                        lds_->partial.get(), s);
+    return;
+  }
   const int vec = (dim + 3) / 4;
   Sched &sc = schedule(vec);
   const bool blocked = sc.s.nbc > 1;

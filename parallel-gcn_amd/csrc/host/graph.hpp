@@ -30,7 +30,10 @@ std::vector<float> graph_coefs(int n, const int *indptr, const int *indices);
 
 // Runs f(begin, end) over [0, n) on up to `threads` host threads.
 void parallel_for(long long n, const std::function<void(long long, long long)> &f,
-                  int threads = 0);
+                  int threads = 0, long long min_parallel = 100000);
+
+// s[i] = 1/sqrt(deg_i) with deg = row length of the (symmetric) CSR: Â = D^-1/2 A D^-1/2.
+std::vector<float> degree_scales(int n, const int *indptr);
 
 class DevGraph {
  public:
@@ -46,7 +49,11 @@ class DevGraph {
   // schedule statistics (for tests / reports)
   int column_blocks(int dim);
 
-  static constexpr int kBlocks = 8;              // one column block per XCD
+  // Enables the d = 16 LDS path (k_graphsum_lds): out_i = row_scale_i * sum_j col_scale_j
+  // in_j over the CSR pattern, i.e. vals_ij = row_scale_i * col_scale_j.
+  void set_scales(std::vector<float> row_scale, std::vector<float> col_scale);
+
+  static constexpr int kBlocks = kGraphBlocks;   // one column block per XCD
   static constexpr double kL2Budget = 4.0e6;     // table bytes that stay plain
 
  private:
@@ -58,6 +65,19 @@ class DevGraph {
   };
   Sched &schedule(int vec);
   void build_blocked();
+  void compute_cuts();
+  void build_lds();
+  struct LdsSched {
+    LdsSchedule s;
+    DeviceBuffer<uint2> entries;
+    DeviceBuffer<long long> wave_off;
+    DeviceBuffer<unsigned short> counts;
+    DeviceBuffer<int2> slices;
+    DeviceBuffer<int> n_slices, rows;
+    DeviceBuffer<float> row_scale, col_scale, scratch, partial;
+  };
+  std::unique_ptr<LdsSched> lds_;
+  std::vector<float> h_row_scale_, h_col_scale_;
   int n_rows_, n_cols_;
   long long nnz_;
   std::vector<int> h_indptr_, h_indices_;

@@ -28,6 +28,29 @@ void launch_graphsum(const GraphSchedule &s, const int *indices, const float *va
                      hipStream_t st);
 bool graphsum_vec_supported(int vec);
 
+// ---- d = 16 GraphSum with LDS-staged feature slices (k_graphsum_lds.hip) ----------------
+constexpr int kGraphBlocks = 8;                      // column blocks (one per XCD)
+constexpr int LDS_SR = 1024;                         // feature rows per LDS slice (64 KB)
+constexpr int LDS_ROWS = LDS_SR + 4;                 // + zero rows for padding entries
+constexpr int LDS_CW = 16;                           // waves per workgroup (all compute)
+constexpr int LDS_SLOTS = 16;                        // rowsets (16 rows) per compute wave
+constexpr int LDS_THREADS = 64 * LDS_CW;
+struct LdsSchedule {
+  int n_rows = 0, n_cols = 0;
+  int n_batches = 0;  // workgroups = n_batches * kGraphBlocks
+  int t_max = 0;      // max slices per column block
+  const uint2 *entries = nullptr;            // [kb][16 lane groups] x 4 uint16 row offsets
+  const long long *wave_off = nullptr;       // [wg][LDS_CW] first kb of each wave's stream
+  const unsigned short *counts = nullptr;    // [wg][t_max][LDS_CW][LDS_SLOTS] steps
+  const int2 *slices = nullptr;              // [block][t_max] {first column, rows}
+  const int *n_slices = nullptr;             // [block]
+  const int *rows = nullptr;                 // [batch][LDS_CW][LDS_SLOTS][16] row or -1
+  const float *row_scale = nullptr;          // 1/sqrt(deg) of output rows
+  const float *col_scale = nullptr;          // 1/sqrt(deg) of input rows
+};
+void launch_graphsum_lds(const LdsSchedule &s, const float *in, int ld_in, float *out,
+                         int ld_out, float *scratch_in, float *partial, hipStream_t st);
+
 void launch_gemm_nn(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
                     int trans_b, float *C, int ldc, const uint64_t *a_mask, long long mask_base,
                     long long mask_ld, float a_scale, hipStream_t s);

@@ -64,31 +64,26 @@ if ONLY:
     print(json.dumps(res))
     sys.exit(0)
 g = make_graph()
-res["d16_blocked_ms"] = timeit(g, 16)
-pg.lib.pgcn_debug_set(b"graphsum_variant", 3)
-res["d16_blocked_v2_ms"] = timeit(g, 16)
-pg.lib.pgcn_debug_set(b"graphsum_variant", 5)
-res["d16_blocked_v3_ms"] = timeit(g, 16)
-pg.lib.pgcn_debug_set(b"graphsum_variant", 11)
-res["d16_v3_nogather_ms"] = timeit(g, 16)
-pg.lib.pgcn_debug_set(b"graphsum_variant", 14)
-res["d16_v3_noindexstream_ms"] = timeit(g, 16)
-pg.lib.pgcn_debug_set(b"graphsum_variant", 1)
-res["d16_nogather_ms"] = timeit(g, 16)
-pg.lib.pgcn_debug_set(b"graphsum_variant", 2)
-res["d16_table4096_ms"] = timeit(g, 16)
-pg.lib.pgcn_debug_set(b"graphsum_variant", 0)
-res["d32_blocked_ms"] = timeit(g, 32)
-res["d41_ms"] = timeit(g, 41, reps=3)
-pg.lib.pgcn_graph_destroy(g)
-pg.lib.pgcn_debug_set(b"graphsum_plain", 1)
-g = make_graph()
-res["d16_plain_ms"] = timeit(g, 16)
-res["d32_plain_ms"] = timeit(g, 32)
-pg.lib.pgcn_graph_destroy(g)
-pg.lib.pgcn_debug_set(b"graphsum_plain", 0)
-nnz = res["nnz"]
-for k in list(res):
-    if k.endswith("_ms") and k.startswith("d16"):
-        res[k.replace("_ms", "_alg_GBs")] = (4 * (n + 1) + 8 * nnz + 8 * n * 16) / (res[k] * 1e-3) / 1e9
+ld = 16
+x = torch.randn(n, ld, device="cuda")
+st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def run_once(dim=16):
+    o = torch.empty(n, ld, device="cuda")
+    pg.check(pg.lib.pgcn_graphsum(g, ctypes.c_void_p(x.data_ptr()), ld,
+                                  ctypes.c_void_p(o.data_ptr()), ld, dim, st), "gs")
+    torch.cuda.synchronize()
+    return o
+
+
+t1 = time.time()
+o_lds = run_once()
+res["lds_build_plus_first_call_s"] = time.time() - t1
+res["d16_lds_ms"] = timeit(g, 16)
+pg.lib.pgcn_debug_set(b"graphsum_lds", 0)
+o_v3 = run_once()
+res["d16_v3_ms"] = timeit(g, 16)
+rel = ((o_lds - o_v3).abs().max() / o_v3.abs().max()).item()
+res["lds_vs_v3_max_rel"] = rel
 print(json.dumps(res))
