@@ -16,6 +16,7 @@ namespace pgcn {
 extern int g_graphsum_variant;      // k_graphsum.hip (diagnostics)
 extern int g_graphsum_force_plain;  // host/graph.cpp (diagnostics)
 extern int g_graphsum_lds;          // host/graph.cpp (diagnostics)
+extern int g_graphsum_lds_order;    // host/graph.cpp (diagnostics)
 }  // namespace pgcn
 
 struct pgcn_graph {
@@ -387,6 +388,7 @@ int pgcn_debug_set(const char *key, int value) {
   if (!std::strcmp(key, "graphsum_variant")) pgcn::g_graphsum_variant = value;
   else if (!std::strcmp(key, "graphsum_plain")) pgcn::g_graphsum_force_plain = value;
   else if (!std::strcmp(key, "graphsum_lds")) pgcn::g_graphsum_lds = value;
+  else if (!std::strcmp(key, "graphsum_lds_order")) pgcn::g_graphsum_lds_order = value;
   else return PGCN_E_INVALID;
   return PGCN_OK;
 }

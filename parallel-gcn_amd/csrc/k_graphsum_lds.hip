@@ -77,31 +77,18 @@ __device__ __forceinline__ void glds16(const void *gsrc, unsigned lds_dst) {
       : "memory");
 }
 
-// s_waitcnt vmcnt(n) for a runtime n (immediate operand: dispatch; larger n clamps to 12,
-// which only waits longer)
-__device__ __forceinline__ void wait_vm(int n) {
-  switch (n < 12 ? n : 12) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
-    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-  }
-}
-
 constexpr int LDS_TABLE_F4 = 2 * LDS_ROWS * 4;       // two slice buffers (float4 units)
 constexpr int LDS_RING_CHUNK = 512;                  // bytes: 4 entry blocks of 128 B
 constexpr int LDS_RING_SLOTS = 3;                    // chunks per wave: 2 in flight + 1 read
-constexpr int LDS_TOTAL_F4 = LDS_TABLE_F4 + LDS_CW * LDS_RING_SLOTS * LDS_RING_CHUNK / 16;
+constexpr int LDS_RING_BYTES = LDS_RING_SLOTS * LDS_RING_CHUNK;
+constexpr int LDS_TOTAL_F4 = LDS_TABLE_F4 + LDS_CW * LDS_RING_BYTES / 16;
 
+// Wave roles: waves 0 .. LDS_CW-1 sum (each owns LDS_SLOTS rowsets and an entry ring); wave
+// LDS_CW copies slice t+1 into the other buffer while slice t is summed.  The copies and the
+// ring refills are LDS-DMA issued from inline asm, invisible to hipcc's waitcnt bookkeeping;
+// each wave counts its own: a summing wave only ever has ring refills outstanding (constant
+// vmcnt(2) = "the chunk refilled two chunks ago has landed"), the loader waits vmcnt(0) once
+// per slice.  One barrier per slice (raw s_barrier: no compiler-inserted vmcnt(0)).
 __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
     const uint2 *__restrict__ entries, const long long *__restrict__ wave_off,
     const unsigned short *__restrict__ counts, int t_max, const int2 *__restrict__ slices,
@@ -115,105 +102,96 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
   const int lane = threadIdx.x & 63;
   const int g = lane >> 2, v = lane & 3;
   const int T = n_slices[b];
-  const int2 *sl = slices + (long long)b * t_max;
   const unsigned lds_base = __builtin_amdgcn_readfirstlane(
       (unsigned)reinterpret_cast<size_t>((__attribute__((address_space(3))) float4 *)lds));
-  constexpr int kPieces = LDS_SR / 16 / LDS_CW;  // 1-KB table pieces per wave per slice
-  static_assert(kPieces * 16 * LDS_CW == LDS_SR, "slice rows split evenly over waves");
-  // this wave's share of slice t -> buffer buf (rows 16*(wave*kPieces + i) .. +16)
-  auto stage = [&](int t, int buf) {
-    const int2 sc = sl[t];
-    const int last = n_cols - 1;
-#pragma unroll
-    for (int i = 0; i < kPieces; i++) {
-      const int row0 = 16 * (wave * kPieces + i);
-      int r = sc.x + row0 + g;
-      r = r < last ? r : last;  // rows past the slice end are never referenced
-      glds16(in + (long long)r * 4 + v, lds_base + (unsigned)((buf * LDS_ROWS + row0) * 64));
-    }
-  };
-  // zero rows LDS_SR .. LDS_SR+3 of both buffers (padding entries point at row LDS_SR)
+  // zero rows LDS_SR .. LDS_SR+3 of both buffers (padding entries point at them)
   if (threadIdx.x < 32) {
     const int buf = threadIdx.x >> 4, q = threadIdx.x & 15;
     lds[(buf * LDS_ROWS + LDS_SR) * 4 + q] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  // entry stream of this wave: kb blocks [kb0, kb1), 128 B each, ring of 512-B chunks
+
+  if (wave == LDS_CW) {  // ------------------------------------------------ loader wave
+    const int2 *sl = slices + (long long)b * t_max;
+    const int last = n_cols - 1;
+    for (int t = 0; t < T; t++) {
+      // slice t -> buffer t & 1 (free: every wave passed the barrier after slice t - 2)
+      const int2 sc = sl[t];
+      const unsigned dst = lds_base + (unsigned)((t & 1) * LDS_ROWS * 64);
+#pragma unroll 8
+      for (int i = 0; i < LDS_SR / 16; i++) {
+        int r = sc.x + 16 * i + g;
+        r = r < last ? r : last;  // rows past the slice end are never referenced
+        glds16(in + (long long)r * 4 + v, dst + (unsigned)(i * 1024));
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // slice t ready (t = 0) / slice t-1 summed
+      asm volatile("" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();  // matches the summing waves' last slice
+    return;
+  }
+
+  // ------------------------------------------------------------------------- summing waves
   const long long wid = (long long)blockIdx.x * LDS_CW + wave;
   const long long kb0 = wave_off[wid], kb1 = wave_off[wid + 1];
   const long long nchunk = (kb1 - kb0 + 3) >> 2;
   const char *ebytes = reinterpret_cast<const char *>(entries) + kb0 * 128;
-  const unsigned ring_base = lds_base + LDS_TABLE_F4 * 16 +
-                             (unsigned)(wave * LDS_RING_SLOTS * LDS_RING_CHUNK);
-  const uint2 *ring = reinterpret_cast<const uint2 *>(lds + LDS_TABLE_F4) +
-                      wave * (LDS_RING_SLOTS * LDS_RING_CHUNK / 8) + g;
-  // Every glds this wave issues is numbered (`issued`); slot_seq[s] = number of the piece that
-  // fills ring slot s.  Waiting for slot s = vmcnt(#pieces issued after it) (in-order retire).
-  int issued = 0, table_seq = -1;
-  int slot_seq[LDS_RING_SLOTS] = {0, 0, 0};
-  auto issue = [&](long long c, int slot) {  // chunk c (clamped: a dummy refill past the end)
+  const unsigned ring_dst = lds_base + LDS_TABLE_F4 * 16 + (unsigned)(wave * LDS_RING_BYTES);
+  const char *ring = reinterpret_cast<const char *>(lds + LDS_TABLE_F4) + wave * LDS_RING_BYTES +
+                     g * 8;
+  auto refill = [&](long long c) {  // chunk c -> ring slot c % 3 (clamped: dummy past the end)
     long long cc = c < nchunk ? c : nchunk - 1;
     cc = cc > 0 ? cc : 0;
-    if (lane < 32) glds16(ebytes + cc * LDS_RING_CHUNK + lane * 16,
-                          ring_base + (unsigned)(slot * LDS_RING_CHUNK));
-    slot_seq[slot] = issued++;
+    if (lane < 32)
+      glds16(ebytes + cc * LDS_RING_CHUNK + lane * 16,
+             ring_dst + (unsigned)((c % LDS_RING_SLOTS) * LDS_RING_CHUNK));
   };
-
-  if (T > 0) stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  issue(0, 0);
-  issue(1, 1);
+  refill(0);
+  refill(1);
+  refill(2);
+  asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // chunk 0
 
   float4 acc[LDS_SLOTS];
 #pragma unroll
   for (int j = 0; j < LDS_SLOTS; j++) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
   const unsigned short *cnt = counts + ((long long)blockIdx.x * t_max) * (LDS_CW * LDS_SLOTS) +
                               wave * LDS_SLOTS;
-  long long chunk = 0;
-  int slot = 0, pos = 0;  // ring slot of `chunk`; entry block inside the chunk
+  int blk = 0;    // entry blocks consumed (ring position = blk % 12 blocks)
+  int roff = 0;   // byte offset of block `blk` in the ring
+  uint2 e_next = *reinterpret_cast<const uint2 *>(ring);
 
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // zero rows written
+  __builtin_amdgcn_s_barrier();                       // slice 0 staged
+  asm volatile("" ::: "memory");
   for (int t = 0; t < T; t++) {
-    const int buf = t & 1;
-    if (t + 1 < T) {
-      stage(t + 1, buf ^ 1);
-      issued += kPieces;
-      table_seq = issued - 1;
-    }
-    const float4 *tb = lds + buf * LDS_ROWS * 4 + v;
-    // the wave's 16 step counts for this slice as 32-bit words (scalar loads: a vector load
-    // here would make hipcc wait vmcnt(0), draining the entry ring)
+    const float4 *tb = lds + (t & 1) * LDS_ROWS * 4 + v;
     const uint4 *c4 = reinterpret_cast<const uint4 *>(cnt + (long long)t * (LDS_CW * LDS_SLOTS));
-    const uint4 cw0 = c4[0], cw1 = c4[1];
+    const uint4 cw0 = c4[0], cw1 = c4[1];  // 16 step counts (scalar loads)
     const unsigned cw[8] = {cw0.x, cw0.y, cw0.z, cw0.w, cw1.x, cw1.y, cw1.z, cw1.w};
 #pragma unroll
     for (int j = 0; j < LDS_SLOTS; j++) {
-      const int n = (cw[j >> 1] >> (16 * (j & 1))) & 0xffff;  // steps of rowset j (uniform)
+      const int n = (cw[j >> 1] >> (16 * (j & 1))) & 0xffff;  // steps of rowset j
       for (int k = 0; k < n; k += 4) {
-        if (pos == 0) {  // entering `chunk`: refill the slot read two chunks ago, wait for it
+        const uint2 e = e_next;
+        ++blk;
+        roff = roff + 128 == LDS_RING_BYTES ? 0 : roff + 128;
+        if ((blk & 3) == 0) {  // entering chunk blk/4: refill the slot read before, wait for it
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          issue(chunk + 2, slot == 0 ? 2 : slot - 1);
-          wait_vm(issued - 1 - slot_seq[slot]);
+          refill((blk >> 2) + 2);
+          asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
         }
-        // all 4 entries of a block are valid: steps past a row's run point at the zero row
-        const uint2 e = ring[slot * (LDS_RING_CHUNK / 8) + pos * 16];
+        e_next = *reinterpret_cast<const uint2 *>(ring + roff);  // (past the end: unused)
+        // all 4 entries are valid: steps past a row's run point at a zero row
         const float4 x0 = tb[e.x & 0xffffu], x1 = tb[e.x >> 16];
         const float4 x2 = tb[e.y & 0xffffu], x3 = tb[e.y >> 16];
         f4_acc(acc[j], x0);
         f4_acc(acc[j], x1);
         f4_acc(acc[j], x2);
         f4_acc(acc[j], x3);
-        if (++pos == 4) {
-          pos = 0;
-          chunk++;
-          slot = slot == LDS_RING_SLOTS - 1 ? 0 : slot + 1;
-        }
       }
     }
-    // the next slice's table pieces must have landed (they are older than the last `since`
-    // ring pieces), and every wave must be done reading this slice
-    if (t + 1 < T) wait_vm(issued - 1 - table_seq);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_barrier();  // slice t summed; slice t+1 staged
     asm volatile("" ::: "memory");
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the dummy ring refills

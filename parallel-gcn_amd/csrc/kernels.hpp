@@ -32,9 +32,9 @@ bool graphsum_vec_supported(int vec);
 constexpr int kGraphBlocks = 8;                      // column blocks (one per XCD)
 constexpr int LDS_SR = 1024;                         // feature rows per LDS slice (64 KB)
 constexpr int LDS_ROWS = LDS_SR + 4;                 // + zero rows for padding entries
-constexpr int LDS_CW = 16;                           // waves per workgroup (all compute)
+constexpr int LDS_CW = 15;                           // summing waves per workgroup
 constexpr int LDS_SLOTS = 16;                        // rowsets (16 rows) per compute wave
-constexpr int LDS_THREADS = 64 * LDS_CW;
+constexpr int LDS_THREADS = 64 * (LDS_CW + 1);       // + one slice loader wave
 struct LdsSchedule {
   int n_rows = 0, n_cols = 0;
   int n_batches = 0;  // workgroups = n_batches * kGraphBlocks

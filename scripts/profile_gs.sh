@@ -1,21 +1,22 @@
 #!/bin/bash
-# PMC passes over single GraphSum configurations of tools/gs_micro.py
+# rocprofv3 PMC passes over the GraphSum micro-benchmark (tools/gs_micro.py <config>), one
+# counter group per pass, no trace domains beside --pmc.
+# usage: scripts/profile_gs.sh <outdir-under-gpurun_out> [config=lds]
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${1:-gsprof}
+CFG=${2:-lds}
 mkdir -p "$OUT"
-cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
-P1="SQ_WAVES SQ_INSTS_VMEM_RD SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES"
-P2="TA_TA_BUSY_sum TA_FLAT_READ_WAVEFRONTS_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TA_DATA_STALLED_BY_TC_CYCLES_sum"
-P3="TCP_TCC_READ_REQ_sum TCP_TCR_TCP_STALL_CYCLES_sum TCP_PENDING_STALL_CYCLES_sum TCP_READ_TAGCONFLICT_STALL_CYCLES_sum"
-P4="TCC_REQ_sum TCC_TAG_STALL_sum TCC_BUSY_sum TCC_EA0_RDREQ_sum"
-P5="SQ_WAVE_CYCLES SQ_INSTS_SMEM SQ_INSTS_LDS GRBM_GUI_ACTIVE"
-for cfg in d16 nogather table4096; do
-  i=0
-  for P in "$P1" "$P2" "$P3" "$P4" "$P5"; do
-    i=$((i+1))
-    timeout -k 10 300 rocprofv3 --pmc $P -d "$OUT/${cfg}_p$i" -o run -f csv -- python3 tools/gs_micro.py $cfg \
-        > "$OUT/${cfg}_p$i.log" 2>&1 || { echo "fail $cfg $i"; exit 1; }
-  done
-  echo "$cfg done"
-done
+ROOT=$(pwd)
+cd /tmp && export TMPDIR=/tmp && cd "$ROOT"
+run() {
+  local name=$1; shift
+  timeout -k 10 300 rocprofv3 "$@" -d "$OUT/$name" -o run -f csv -- python3 tools/gs_micro.py "$CFG" \
+      > "$OUT/$name.log" 2>&1
+  local rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || tail -20 "$OUT/$name.log"; return $rc
+}
+run trace --kernel-trace --stats || exit $?
+run lds --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAVE_CYCLES || exit $?
+run sq --pmc SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_BUSY_CYCLES SQ_INSTS_VALU || exit $?
+run fetch --pmc FETCH_SIZE || exit $?
+run write --pmc WRITE_SIZE || exit $?

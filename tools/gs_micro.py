@@ -56,6 +56,8 @@ def timeit(g, dim, reps=10):
 res = {"nnz": int(ip[-1]), "gen_s": gen_s}
 if ONLY:
     variant = {"nogather": 1, "table4096": 2}.get(ONLY, 0)
+    if ONLY == "v3":
+        pg.lib.pgcn_debug_set(b"graphsum_lds", 0)
     if ONLY == "plain":
         pg.lib.pgcn_debug_set(b"graphsum_plain", 1)
     pg.lib.pgcn_debug_set(b"graphsum_variant", variant)
