@@ -210,6 +210,9 @@ long long pgcn_partition_subgraph(int n, const int *indptr, const int *indices, 
 /* "graphsum_variant": 0 normal, 1 skip the feature gather, 2 fold gathers into 4096 rows;
  * "graphsum_plain": 1 disables the XCD column blocking for schedules built afterwards. */
 int pgcn_debug_set(const char *key, int value);
+/* copies up to max_elems of a diagnostic buffer ("graphsum_lds_stamps": per-wave cycle stamps
+ * of the last graphsum_lds_diag=4 launch); returns the buffer's element count or a status */
+long long pgcn_debug_read(const char *key, void *dst, long long max_elems);
 
 #ifdef __cplusplus
 }

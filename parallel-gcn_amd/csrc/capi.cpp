@@ -17,6 +17,8 @@ extern int g_graphsum_variant;      // k_graphsum.hip (diagnostics)
 extern int g_graphsum_force_plain;  // host/graph.cpp (diagnostics)
 extern int g_graphsum_lds;          // host/graph.cpp (diagnostics)
 extern int g_graphsum_lds_order;    // host/graph.cpp (diagnostics)
+extern int g_graphsum_lds_diag;     // k_graphsum_lds.hip (diagnostics)
+long long lds_stamps_read(void *dst, long long max_elems);
 }  // namespace pgcn
 
 struct pgcn_graph {
@@ -389,8 +391,18 @@ int pgcn_debug_set(const char *key, int value) {
   else if (!std::strcmp(key, "graphsum_plain")) pgcn::g_graphsum_force_plain = value;
   else if (!std::strcmp(key, "graphsum_lds")) pgcn::g_graphsum_lds = value;
   else if (!std::strcmp(key, "graphsum_lds_order")) pgcn::g_graphsum_lds_order = value;
+  else if (!std::strcmp(key, "graphsum_lds_diag")) pgcn::g_graphsum_lds_diag = value;
   else return PGCN_E_INVALID;
   return PGCN_OK;
+}
+
+long long pgcn_debug_read(const char *key, void *dst, long long max_elems) {
+  if (!key) return PGCN_E_INVALID;
+  long long r = PGCN_E_INVALID;
+  const int st = guarded([&] {
+    if (!std::strcmp(key, "graphsum_lds_stamps")) r = pgcn::lds_stamps_read(dst, max_elems);
+  });
+  return st != PGCN_OK ? st : r;
 }
 
 // ---------------------------------------------------------------- partition (host only)

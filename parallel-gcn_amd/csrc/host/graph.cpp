@@ -290,20 +290,97 @@ void DevGraph::build_lds() {
   // 256 CUs (one 156-KB-LDS workgroup per CU)
   const int nbat = (int)(((nrs + cap - 1) / cap + 31) / 32 * 32);
   const long long n_wg = (long long)nbat * B;
-  std::vector<int> rows((size_t)nbat * CW * NS * 16, -1);
-  for (long long r = 0; r < nrs; r++) {
-    const long long bat = r % nbat, q = r / nbat, w = q % CW, j = q / CW;
-    for (int g = 0; g < 16; g++) {
-      const long long i = 16 * r + g;
-      rows[(size_t)(((bat * CW + w) * NS + j) * 16 + g)] = i < n_rows_ ? order[(size_t)i] : -1;
-    }
-  }
   // column-sorted copy of every row (a row's edges inside a slice are then one run)
   std::vector<int> sidx(h_indices_);
   parallel_for(n_rows_, [&](long long b0, long long b1) {
     for (long long i = b0; i < b1; i++)
       std::sort(sidx.begin() + h_indptr_[(size_t)i], sidx.begin() + h_indptr_[(size_t)i + 1]);
   });
+  // entry blocks of every (rowset, slice): ceil(max over the rowset's rows of the run / 4)
+  int n_sl = 0;
+  std::vector<int> sl_first((size_t)B + 1, 0);  // global slice ids of block b
+  for (int b = 0; b < B; b++) sl_first[(size_t)b + 1] = sl_first[(size_t)b] + nsl[(size_t)b];
+  n_sl = sl_first[(size_t)B];
+  std::vector<int> sl_start((size_t)n_sl);
+  for (int b = 0; b < B; b++)
+    for (int t = 0; t < nsl[(size_t)b]; t++)
+      sl_start[(size_t)(sl_first[(size_t)b] + t)] = slices[(size_t)b * t_max + t].x;
+  std::vector<unsigned short> rs_blocks((size_t)nrs * n_sl, 0);
+  parallel_for(nrs, [&](long long r0, long long r1) {
+    std::vector<int> mx((size_t)n_sl);
+    for (long long r = r0; r < r1; r++) {
+      std::fill(mx.begin(), mx.end(), 0);
+      for (int g = 0; g < 16; g++) {
+        const long long i = 16 * r + g;
+        if (i >= n_rows_) break;
+        const int row = order[(size_t)i];
+        int s = 0, run = 0;
+        for (int k = h_indptr_[(size_t)row]; k < h_indptr_[(size_t)row + 1]; k++) {
+          const int c = sidx[(size_t)k];
+          int s2 = s;
+          while (s2 + 1 < n_sl && sl_start[(size_t)s2 + 1] <= c) s2++;
+          if (s2 != s) {
+            mx[(size_t)s] = std::max(mx[(size_t)s], run);
+            s = s2;
+            run = 0;
+          }
+          run++;
+        }
+        mx[(size_t)s] = std::max(mx[(size_t)s], run);
+      }
+      for (int s = 0; s < n_sl; s++) rs_blocks[(size_t)r * n_sl + s] = (unsigned short)std::min(65535, (mx[(size_t)s] + 3) / 4);
+    }
+  }, 0, 64);
+  // rowsets dealt round-robin (degree order) to batches; inside a batch each rowset goes to the
+  // wave (with a free slot) whose per-slice loads grow the sum over slices of the per-slice
+  // maximum least -- every slice ends in a workgroup barrier, so the slowest wave of each
+  // slice sets the pace.  Heaviest rowsets first.
+  std::vector<int> rows((size_t)nbat * CW * NS * 16, -1);
+  parallel_for(nbat, [&](long long b0, long long b1) {
+    std::vector<int> load((size_t)CW * n_sl), cur_max((size_t)n_sl);
+    for (long long bat = b0; bat < b1; bat++) {
+      std::vector<long long> mine;
+      for (long long r = bat; r < nrs; r += nbat) mine.push_back(r);
+      std::vector<long long> tot(mine.size(), 0);
+      for (size_t a = 0; a < mine.size(); a++)
+        for (int s = 0; s < n_sl; s++) tot[a] += rs_blocks[(size_t)mine[a] * n_sl + s];
+      std::vector<size_t> idx(mine.size());
+      std::iota(idx.begin(), idx.end(), 0);
+      std::stable_sort(idx.begin(), idx.end(), [&](size_t x, size_t y) { return tot[x] > tot[y]; });
+      std::fill(load.begin(), load.end(), 0);
+      std::fill(cur_max.begin(), cur_max.end(), 0);
+      std::vector<int> used((size_t)CW, 0);
+      for (size_t a : idx) {
+        const unsigned short *x = &rs_blocks[(size_t)mine[a] * n_sl];
+        long long best = -1;
+        int bw = -1;
+        for (int w = 0; w < CW; w++) {
+          if (used[(size_t)w] >= NS) continue;
+          long long inc = 0;
+          const int *lw = &load[(size_t)w * n_sl];
+          for (int s = 0; s < n_sl; s++) {
+            const int nl = lw[s] + x[s];
+            if (nl > cur_max[(size_t)s]) inc += nl - cur_max[(size_t)s];
+          }
+          if (bw < 0 || inc < best || (inc == best && used[(size_t)w] < used[(size_t)bw])) {
+            best = inc;
+            bw = w;
+          }
+        }
+        PGCN_CHECK(bw >= 0, PGCN_E_INVALID, "graphsum_lds: batch over capacity");
+        int *lw = &load[(size_t)bw * n_sl];
+        for (int s = 0; s < n_sl; s++) {
+          lw[s] += x[s];
+          cur_max[(size_t)s] = std::max(cur_max[(size_t)s], lw[s]);
+        }
+        const int j = used[(size_t)bw]++;
+        for (int g = 0; g < 16; g++) {
+          const long long i = 16 * mine[a] + g;
+          rows[(size_t)(((bat * CW + bw) * NS + j) * 16 + g)] = i < n_rows_ ? order[(size_t)i] : -1;
+        }
+      }
+    }
+  }, 0, 1);
   std::vector<unsigned short> counts((size_t)n_wg * t_max * CW * NS, 0);
   std::vector<long long> kbs((size_t)n_wg * CW, 0);
   // walks (wg, wave): for each slice, each rowset slot, the 16 rows' runs in that slice
@@ -343,7 +420,7 @@ void DevGraph::build_lds() {
               for (int u = 0; u < 4; u++) {
                 const int st = 4 * kb + u, k = j * 16 + g;
                 out_entries[(kb_total + kb) * 64 + g * 4 + u] =
-                    (unsigned short)(st < n[g] ? (sidx[(size_t)cur[k] + st] - sc.x) * 4 : SR * 4);
+                    (unsigned short)(st < n[g] ? (sidx[(size_t)cur[k] + st] - sc.x) * 64 : SR * 64);
               }
         } else if (out_entries && nkb > 0) {
           // Order each row's run (any fixed order sums the same terms) so that at every step
@@ -384,14 +461,14 @@ void DevGraph::build_lds() {
                       pick = r;
                 int val;
                 if (pick >= 0 && st < m) {
-                  val = byres[a][pick].back() * 4;
+                  val = byres[a][pick].back() * 64;
                   byres[a][pick].pop_back();
                   rem[a]--;
                   used |= 1 << pick;
                 } else {
                   int r = 0;
                   while (used >> r & 1) r++;
-                  val = (SR + r) * 4;
+                  val = (SR + r) * 64;
                   used |= 1 << r;
                 }
                 dst[(st >> 2) * 64 + grp[a] * 4 + (st & 3)] = (unsigned short)val;

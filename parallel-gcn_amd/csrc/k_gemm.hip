@@ -116,6 +116,8 @@ __global__ __launch_bounds__(256) void k_gemm_nn(int M, int N, int K,
 // x 256 contiguous bytes) and feeds 4 MFMAs: MFMA t's A-operand row i is k = kc*64 + 4i + t,
 // its reduction index is the row g.  Partials go to partial[slab][k][ldp].
 // ------------------------------------------------------------------------------------------
+constexpr int TN_U = 2;  // row steps whose loads are in flight together
+
 template <int NJ, int KCW, int WK>
 __global__ __launch_bounds__(256) void k_gemm_tn(int M, int N, int K, int slab,
                                                  const float *__restrict__ A, int lda,
@@ -140,40 +142,50 @@ __global__ __launch_bounds__(256) void k_gemm_tn(int M, int N, int K, int slab,
 #pragma unroll
       for (int j = 0; j < NJ; j++) acc[c][t][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  for (long long m = m_begin + 4 * wr; m < m_end; m += 4 * WR) {
-    const long long mr = m + g;
-    const bool ok = mr < m_end;
-    float b[NJ];
+  // TN_U row steps per iteration: all their loads are issued before any MFMA consumes them
+  for (long long m0 = m_begin + 4 * wr; m0 < m_end; m0 += 4 * WR * TN_U) {
+    float b[TN_U][NJ];
+    float4 a[TN_U][KCW];
 #pragma unroll
-    for (int j = 0; j < NJ; j++) {
-      const int col = 16 * j + i;
-      b[j] = (ok && col < N) ? G[mr * ldg + col] : 0.0f;
-    }
-#pragma unroll
-    for (int c = 0; c < KCW; c++) {
-      const int kb = (c0 + wk + WK * c) * 64 + 4 * i;
-      float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (ok && kb < K) {
-        a = *reinterpret_cast<const float4 *>(A + mr * lda + kb);
-        if (kb + 1 >= K) a.y = 0.f;
-        if (kb + 2 >= K) a.z = 0.f;
-        if (kb + 3 >= K) a.w = 0.f;
-        if (a_mask) {
-          const uint32_t bits = mask4(a_mask, mask_base + mr * mask_ld + kb);
-          a.x *= (bits & 1) ? a_scale : 0.0f;
-          a.y *= (bits & 2) ? a_scale : 0.0f;
-          a.z *= (bits & 4) ? a_scale : 0.0f;
-          a.w *= (bits & 8) ? a_scale : 0.0f;
-        }
-      }
+    for (int u = 0; u < TN_U; u++) {
+      const long long mr = m0 + 4 * WR * u + g;
+      const bool ok = mr < m_end;
 #pragma unroll
       for (int j = 0; j < NJ; j++) {
-        acc[c][0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b[j], acc[c][0][j], 0, 0, 0);
-        acc[c][1][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b[j], acc[c][1][j], 0, 0, 0);
-        acc[c][2][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b[j], acc[c][2][j], 0, 0, 0);
-        acc[c][3][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b[j], acc[c][3][j], 0, 0, 0);
+        const int col = 16 * j + i;
+        b[u][j] = (ok && col < N) ? G[mr * ldg + col] : 0.0f;
+      }
+#pragma unroll
+      for (int c = 0; c < KCW; c++) {
+        const int kb = (c0 + wk + WK * c) * 64 + 4 * i;
+        float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ok && kb < K) {
+          x = *reinterpret_cast<const float4 *>(A + mr * lda + kb);
+          if (kb + 1 >= K) x.y = 0.f;
+          if (kb + 2 >= K) x.z = 0.f;
+          if (kb + 3 >= K) x.w = 0.f;
+          if (a_mask) {
+            const uint32_t bits = mask4(a_mask, mask_base + mr * mask_ld + kb);
+            x.x *= (bits & 1) ? a_scale : 0.0f;
+            x.y *= (bits & 2) ? a_scale : 0.0f;
+            x.z *= (bits & 4) ? a_scale : 0.0f;
+            x.w *= (bits & 8) ? a_scale : 0.0f;
+          }
+        }
+        a[u][c] = x;
       }
     }
+#pragma unroll
+    for (int u = 0; u < TN_U; u++)
+#pragma unroll
+      for (int c = 0; c < KCW; c++)
+#pragma unroll
+        for (int j = 0; j < NJ; j++) {
+          acc[c][0][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][c].x, b[u][j], acc[c][0][j], 0, 0, 0);
+          acc[c][1][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][c].y, b[u][j], acc[c][1][j], 0, 0, 0);
+          acc[c][2][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][c].z, b[u][j], acc[c][2][j], 0, 0, 0);
+          acc[c][3][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][c].w, b[u][j], acc[c][3][j], 0, 0, 0);
+        }
   }
   // row-group partial sums of one block meet in LDS (fixed order), then one slab partial
   __shared__ float red[WR > 1 ? 4 * 64 * 16 : 1];
@@ -269,8 +281,8 @@ static TnPlan tn_plan(int M, int N, int K) {
   p.kcw = std::min(3, (p.nkc + p.wk - 1) / p.wk);
   p.kgroups = (p.nkc + p.wk * p.kcw - 1) / (p.wk * p.kcw);
   const int wr = 4 / p.wk;
-  long long slab = ceil_div(M, 512);
-  const int q = 4 * wr;
+  long long slab = ceil_div(M, 1024);  // ~4 blocks per CU: memory parallelism for the stream
+  const int q = 4 * wr * TN_U;
   slab = (slab + q - 1) / q * q;
   if (slab < 64) slab = 64;
   p.slab = (int)slab;

@@ -79,21 +79,31 @@ __device__ __forceinline__ void glds16(const void *gsrc, unsigned lds_dst) {
 
 constexpr int LDS_TABLE_F4 = 2 * LDS_ROWS * 4;       // two slice buffers (float4 units)
 constexpr int LDS_RING_CHUNK = 512;                  // bytes: 4 entry blocks of 128 B
-constexpr int LDS_RING_SLOTS = 3;                    // chunks per wave: 2 in flight + 1 read
+constexpr int LDS_RING_SLOTS = 4;                    // chunks per wave: 3 in flight + 1 read
 constexpr int LDS_RING_BYTES = LDS_RING_SLOTS * LDS_RING_CHUNK;
-constexpr int LDS_TOTAL_F4 = LDS_TABLE_F4 + LDS_CW * LDS_RING_BYTES / 16;
+constexpr int LDS_CNT_BYTES = 512;                   // one slice's step counts (480 B used)
+static_assert(LDS_CW * LDS_SLOTS * 2 <= LDS_CNT_BYTES, "counts area");
+constexpr int LDS_RING_F4 = LDS_TABLE_F4 + 2 * LDS_CNT_BYTES / 16;  // after 2 counts areas
+constexpr int LDS_TOTAL_F4 = LDS_RING_F4 + LDS_CW * LDS_RING_BYTES / 16;
 
 // Wave roles: waves 0 .. LDS_CW-1 sum (each owns LDS_SLOTS rowsets and an entry ring); wave
 // LDS_CW copies slice t+1 into the other buffer while slice t is summed.  The copies and the
 // ring refills are LDS-DMA issued from inline asm, invisible to hipcc's waitcnt bookkeeping;
 // each wave counts its own: a summing wave only ever has ring refills outstanding (constant
-// vmcnt(2) = "the chunk refilled two chunks ago has landed"), the loader waits vmcnt(0) once
+// vmcnt(3) = "the chunk refilled three chunks ago has landed"), the loader waits vmcnt(0) once
 // per slice.  One barrier per slice (raw s_barrier: no compiler-inserted vmcnt(0)).
+// DIAG 4: per-wave cycle stamps (s_memtime) -> stamps[wg][wave][8]:
+//   0 loop cycles, 1 barrier-wait cycles, 2 ring-wait cycles, 3 entry blocks, 4 slices
+__device__ __forceinline__ unsigned long long clk() { return __builtin_amdgcn_s_memtime(); }
+
+template <int DIAG>
 __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
     const uint2 *__restrict__ entries, const long long *__restrict__ wave_off,
     const unsigned short *__restrict__ counts, int t_max, const int2 *__restrict__ slices,
     const int *__restrict__ n_slices, const int *__restrict__ rows, const float4 *__restrict__ in,
-    int n_cols, float4 *__restrict__ partial, long long part_stride) {
+    int n_cols, float4 *__restrict__ partial, long long part_stride,
+    unsigned long long *__restrict__ stamps) {
+  unsigned long long st_loop = 0, st_bar = 0, st_ring = 0;
   // ONE __shared__ object: [2][LDS_ROWS][4] float4 slice buffers, then the entry rings
   __shared__ float4 lds[LDS_TOTAL_F4];
   const int nb = kGraphBlocks;
@@ -113,21 +123,52 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
   if (wave == LDS_CW) {  // ------------------------------------------------ loader wave
     const int2 *sl = slices + (long long)b * t_max;
     const int last = n_cols - 1;
+    const char *cnt_src = reinterpret_cast<const char *>(counts) +
+                          (long long)blockIdx.x * t_max * (LDS_CW * LDS_SLOTS * 2);
+    int2 sc_next = T > 0 ? sl[0] : make_int2(0, 0);
     for (int t = 0; t < T; t++) {
-      // slice t -> buffer t & 1 (free: every wave passed the barrier after slice t - 2)
-      const int2 sc = sl[t];
+      // slice t -> buffer t & 1 (free: every wave passed the barrier after slice t - 2),
+      // with the summing waves' step counts for slice t
+      const int2 sc = sc_next;
+      if (t + 1 < T) sc_next = sl[t + 1];
+      if (lane * 16 < LDS_CW * LDS_SLOTS * 2)
+        glds16(cnt_src + (long long)t * (LDS_CW * LDS_SLOTS * 2) + lane * 16,
+               lds_base + (unsigned)(LDS_TABLE_F4 * 16 + (t & 1) * LDS_CNT_BYTES));
       const unsigned dst = lds_base + (unsigned)((t & 1) * LDS_ROWS * 64);
+      const int pieces = DIAG == 1 ? 4 : LDS_SR / 16;  // DIAG 1: stage 1/16 (timing only)
 #pragma unroll 8
-      for (int i = 0; i < LDS_SR / 16; i++) {
+      for (int i = 0; i < pieces; i++) {
         int r = sc.x + 16 * i + g;
         r = r < last ? r : last;  // rows past the slice end are never referenced
         glds16(in + (long long)r * 4 + v, dst + (unsigned)(i * 1024));
       }
+      if (LDS_SR % 16 && g < LDS_SR % 16) {  // last partial piece (keeps the zero rows)
+        int r = sc.x + 16 * (LDS_SR / 16) + g;
+        r = r < last ? r : last;
+        glds16(in + (long long)r * 4 + v, dst + (unsigned)((LDS_SR / 16) * 1024));
+      }
+      unsigned long long c0 = 0;
+      if constexpr (DIAG == 4) c0 = clk();
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      unsigned long long c1 = 0;
+      if constexpr (DIAG == 4) c1 = clk();
       __builtin_amdgcn_s_barrier();  // slice t ready (t = 0) / slice t-1 summed
       asm volatile("" ::: "memory");
+      if constexpr (DIAG == 4) {
+        const unsigned long long c2 = clk();
+        st_ring += c1 - c0;  // loader: staging wait
+        st_bar += c2 - c1;
+      }
     }
     __builtin_amdgcn_s_barrier();  // matches the summing waves' last slice
+    if constexpr (DIAG == 4) {
+      if (lane == 0) {
+        unsigned long long *o = stamps + ((long long)blockIdx.x * 16 + wave) * 8;
+        o[1] = st_bar;
+        o[2] = st_ring;
+        o[4] = T;
+      }
+    }
     return;
   }
 
@@ -136,10 +177,10 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
   const long long kb0 = wave_off[wid], kb1 = wave_off[wid + 1];
   const long long nchunk = (kb1 - kb0 + 3) >> 2;
   const char *ebytes = reinterpret_cast<const char *>(entries) + kb0 * 128;
-  const unsigned ring_dst = lds_base + LDS_TABLE_F4 * 16 + (unsigned)(wave * LDS_RING_BYTES);
-  const char *ring = reinterpret_cast<const char *>(lds + LDS_TABLE_F4) + wave * LDS_RING_BYTES +
+  const unsigned ring_dst = lds_base + LDS_RING_F4 * 16 + (unsigned)(wave * LDS_RING_BYTES);
+  const char *ring = reinterpret_cast<const char *>(lds + LDS_RING_F4) + wave * LDS_RING_BYTES +
                      g * 8;
-  auto refill = [&](long long c) {  // chunk c -> ring slot c % 3 (clamped: dummy past the end)
+  auto refill = [&](long long c) {  // chunk c -> ring slot c % 4 (clamped: dummy past the end)
     long long cc = c < nchunk ? c : nchunk - 1;
     cc = cc > 0 ? cc : 0;
     if (lane < 32)
@@ -149,13 +190,12 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
   refill(0);
   refill(1);
   refill(2);
-  asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // chunk 0
+  refill(3);
+  asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // chunk 0
 
   float4 acc[LDS_SLOTS];
 #pragma unroll
   for (int j = 0; j < LDS_SLOTS; j++) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-  const unsigned short *cnt = counts + ((long long)blockIdx.x * t_max) * (LDS_CW * LDS_SLOTS) +
-                              wave * LDS_SLOTS;
   int blk = 0;    // entry blocks consumed (ring position = blk % 12 blocks)
   int roff = 0;   // byte offset of block `blk` in the ring
   uint2 e_next = *reinterpret_cast<const uint2 *>(ring);
@@ -163,11 +203,19 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // zero rows written
   __builtin_amdgcn_s_barrier();                       // slice 0 staged
   asm volatile("" ::: "memory");
+  if constexpr (DIAG == 4) st_loop = clk();
   for (int t = 0; t < T; t++) {
-    const float4 *tb = lds + (t & 1) * LDS_ROWS * 4 + v;
-    const uint4 *c4 = reinterpret_cast<const uint4 *>(cnt + (long long)t * (LDS_CW * LDS_SLOTS));
-    const uint4 cw0 = c4[0], cw1 = c4[1];  // 16 step counts (scalar loads)
-    const unsigned cw[8] = {cw0.x, cw0.y, cw0.z, cw0.w, cw1.x, cw1.y, cw1.z, cw1.w};
+    // edge entries are byte offsets of slice rows: address = entry + (buffer base + 16 v)
+    const char *tb = reinterpret_cast<const char *>(lds + (t & 1) * LDS_ROWS * 4 + v);
+    // this wave's 16 step counts for slice t, staged by the loader (uniform: broadcast read)
+    const uint4 *c4 = reinterpret_cast<const uint4 *>(
+        reinterpret_cast<const char *>(lds + LDS_TABLE_F4) + (t & 1) * LDS_CNT_BYTES + wave * 32);
+    const uint4 cw0 = c4[0], cw1 = c4[1];
+    const unsigned cw[8] = {
+        (unsigned)__builtin_amdgcn_readfirstlane(cw0.x), (unsigned)__builtin_amdgcn_readfirstlane(cw0.y),
+        (unsigned)__builtin_amdgcn_readfirstlane(cw0.z), (unsigned)__builtin_amdgcn_readfirstlane(cw0.w),
+        (unsigned)__builtin_amdgcn_readfirstlane(cw1.x), (unsigned)__builtin_amdgcn_readfirstlane(cw1.y),
+        (unsigned)__builtin_amdgcn_readfirstlane(cw1.z), (unsigned)__builtin_amdgcn_readfirstlane(cw1.w)};
 #pragma unroll
     for (int j = 0; j < LDS_SLOTS; j++) {
       const int n = (cw[j >> 1] >> (16 * (j & 1))) & 0xffff;  // steps of rowset j
@@ -177,22 +225,53 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
         roff = roff + 128 == LDS_RING_BYTES ? 0 : roff + 128;
         if ((blk & 3) == 0) {  // entering chunk blk/4: refill the slot read before, wait for it
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          refill((blk >> 2) + 2);
-          asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+          refill((blk >> 2) + 3);
+          unsigned long long c0 = 0;
+          if constexpr (DIAG == 4) c0 = clk();
+          asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+          if constexpr (DIAG == 4) st_ring += clk() - c0;
         }
         e_next = *reinterpret_cast<const uint2 *>(ring + roff);  // (past the end: unused)
         // all 4 entries are valid: steps past a row's run point at a zero row
-        const float4 x0 = tb[e.x & 0xffffu], x1 = tb[e.x >> 16];
-        const float4 x2 = tb[e.y & 0xffffu], x3 = tb[e.y >> 16];
-        f4_acc(acc[j], x0);
-        f4_acc(acc[j], x1);
-        f4_acc(acc[j], x2);
-        f4_acc(acc[j], x3);
+        if constexpr (DIAG == 2) {  // diagnostic: no table reads
+          acc[j].x += __uint_as_float(e.x);
+          acc[j].y += __uint_as_float(e.y);
+        } else {
+          const float4 x0 = *reinterpret_cast<const float4 *>(tb + (e.x & 0xffffu));
+          const float4 x1 = *reinterpret_cast<const float4 *>(tb + (e.x >> 16));
+          const float4 x2 = *reinterpret_cast<const float4 *>(tb + (e.y & 0xffffu));
+          const float4 x3 = *reinterpret_cast<const float4 *>(tb + (e.y >> 16));
+          if constexpr (DIAG == 3) {  // diagnostic: one add per read
+            acc[j].x += x0.x;
+            acc[j].y += x1.y;
+            acc[j].z += x2.z;
+            acc[j].w += x3.w;
+          } else {
+            f4_acc(acc[j], x0);
+            f4_acc(acc[j], x1);
+            f4_acc(acc[j], x2);
+            f4_acc(acc[j], x3);
+          }
+        }
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    unsigned long long cb = 0;
+    if constexpr (DIAG == 4) cb = clk();
     __builtin_amdgcn_s_barrier();  // slice t summed; slice t+1 staged
     asm volatile("" ::: "memory");
+    if constexpr (DIAG == 4) st_bar += clk() - cb;
+  }
+  if constexpr (DIAG == 4) {
+    st_loop = clk() - st_loop;
+    if (lane == 0) {
+      unsigned long long *o = stamps + ((long long)blockIdx.x * 16 + wave) * 8;
+      o[0] = st_loop;
+      o[1] = st_bar;
+      o[2] = st_ring;
+      o[3] = (unsigned long long)blk;
+      o[4] = T;
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the dummy ring refills
   const int *rw = rows + (((long long)batch * LDS_CW + wave) * LDS_SLOTS) * 16 + g;
@@ -223,6 +302,28 @@ __global__ __launch_bounds__(256) void k_gs_lds_combine(const float4 *__restrict
   out[r * ld4_out + v] = a;
 }
 
+int g_graphsum_lds_diag = 0;  // diagnostics only ("graphsum_lds_diag")
+
+// DIAG 4 stamp buffer (diagnostics; read back with pgcn_debug_read("graphsum_lds_stamps"))
+static unsigned long long *g_stamps = nullptr;
+static long long g_stamps_n = 0;
+static unsigned long long *lds_stamps(long long n_wg) {
+  if (g_graphsum_lds_diag != 4) return nullptr;
+  const long long n = n_wg * 16 * 8;
+  if (n > g_stamps_n) {
+    if (g_stamps) PGCN_HIP(hipFree(g_stamps));
+    PGCN_HIP(hipMalloc(&g_stamps, n * sizeof(unsigned long long)));
+    g_stamps_n = n;
+  }
+  PGCN_HIP(hipMemset(g_stamps, 0, n * sizeof(unsigned long long)));
+  return g_stamps;
+}
+long long lds_stamps_read(void *dst, long long max_elems) {
+  const long long n = g_stamps_n < max_elems ? g_stamps_n : max_elems;
+  if (dst && n > 0) PGCN_HIP(hipMemcpy(dst, g_stamps, n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  return g_stamps_n;
+}
+
 void launch_graphsum_lds(const LdsSchedule &s, const float *in, int ld_in, float *out,
                          int ld_out, float *scratch_in, float *partial, hipStream_t st) {
   PGCN_CHECK(ld_in % 4 == 0 && ld_out % 4 == 0, PGCN_E_INVALID, "graphsum_lds: ld % 4");
@@ -230,10 +331,20 @@ void launch_graphsum_lds(const LdsSchedule &s, const float *in, int ld_in, float
   hipLaunchKernelGGL(k_gs_prescale, dim3((unsigned)ceil_div(pre, 256)), dim3(256), 0, st,
                      reinterpret_cast<const float4 *>(in), ld_in / 4, s.col_scale, s.n_cols,
                      reinterpret_cast<float4 *>(scratch_in));
-  hipLaunchKernelGGL(k_graphsum_lds, dim3((unsigned)(s.n_batches * kGraphBlocks)),
-                     dim3(LDS_THREADS), 0, st, s.entries, s.wave_off, s.counts, s.t_max,
-                     s.slices, s.n_slices, s.rows, reinterpret_cast<const float4 *>(scratch_in),
-                     s.n_cols, reinterpret_cast<float4 *>(partial), (long long)s.n_rows);
+#define GS_LDS(D)                                                                           \
+  hipLaunchKernelGGL(k_graphsum_lds<D>, dim3((unsigned)(s.n_batches * kGraphBlocks)),          \
+                     dim3(LDS_THREADS), 0, st, s.entries, s.wave_off, s.counts, s.t_max,        \
+                     s.slices, s.n_slices, s.rows, reinterpret_cast<const float4 *>(scratch_in), \
+                     s.n_cols, reinterpret_cast<float4 *>(partial), (long long)s.n_rows,          \
+                     lds_stamps(s.n_batches * kGraphBlocks))
+  switch (g_graphsum_lds_diag) {
+    case 1: GS_LDS(1); break;
+    case 2: GS_LDS(2); break;
+    case 3: GS_LDS(3); break;
+    case 4: GS_LDS(4); break;
+    default: GS_LDS(0); break;
+  }
+#undef GS_LDS
   const long long post = (long long)s.n_rows * 4;
   hipLaunchKernelGGL(k_gs_lds_combine, dim3((unsigned)ceil_div(post, 256)), dim3(256), 0, st,
                      reinterpret_cast<const float4 *>(partial), (long long)s.n_rows,

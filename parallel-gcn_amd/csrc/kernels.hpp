@@ -30,8 +30,9 @@ bool graphsum_vec_supported(int vec);
 
 // ---- d = 16 GraphSum with LDS-staged feature slices (k_graphsum_lds.hip) ----------------
 constexpr int kGraphBlocks = 8;                      // column blocks (one per XCD)
-constexpr int LDS_SR = 1024;                         // feature rows per LDS slice (64 KB)
-constexpr int LDS_ROWS = LDS_SR + 4;                 // + zero rows for padding entries
+constexpr int LDS_SR = 1020;                         // feature rows per LDS slice
+constexpr int LDS_ROWS = LDS_SR + 4;                 // + 4 zero rows = 1024 rows = 64 KB, so a
+                                                     //   row's byte offset fits an edge's 16 bits
 constexpr int LDS_CW = 15;                           // summing waves per workgroup
 constexpr int LDS_SLOTS = 16;                        // rowsets (16 rows) per compute wave
 constexpr int LDS_THREADS = 64 * (LDS_CW + 1);       // + one slice loader wave

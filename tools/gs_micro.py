@@ -83,6 +83,10 @@ t1 = time.time()
 o_lds = run_once()
 res["lds_build_plus_first_call_s"] = time.time() - t1
 res["d16_lds_ms"] = timeit(g, 16)
+for dg, name in ((1, "stage1of16"), (2, "noreads"), (3, "oneadd")):
+    pg.lib.pgcn_debug_set(b"graphsum_lds_diag", dg)
+    res[f"d16_lds_{name}_ms"] = timeit(g, 16)
+pg.lib.pgcn_debug_set(b"graphsum_lds_diag", 0)
 pg.lib.pgcn_debug_set(b"graphsum_lds", 0)
 o_v3 = run_once()
 res["d16_v3_ms"] = timeit(g, 16)
