@@ -196,8 +196,9 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
   float4 acc[LDS_SLOTS];
 #pragma unroll
   for (int j = 0; j < LDS_SLOTS; j++) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-  int blk = 0;    // entry blocks consumed (ring position = blk % 12 blocks)
-  int roff = 0;   // byte offset of block `blk` in the ring
+  int chunk = 0;  // ring chunk being read
+  int roff = 0;   // byte offset of the current entry block in the ring (power-of-two ring)
+  static_assert((LDS_RING_BYTES & (LDS_RING_BYTES - 1)) == 0, "ring wraps by masking");
   uint2 e_next = *reinterpret_cast<const uint2 *>(ring);
 
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // zero rows written
@@ -221,11 +222,11 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
       const int n = (cw[j >> 1] >> (16 * (j & 1))) & 0xffff;  // steps of rowset j
       for (int k = 0; k < n; k += 4) {
         const uint2 e = e_next;
-        ++blk;
-        roff = roff + 128 == LDS_RING_BYTES ? 0 : roff + 128;
-        if ((blk & 3) == 0) {  // entering chunk blk/4: refill the slot read before, wait for it
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          refill((blk >> 2) + 3);
+        roff = (roff + 128) & (LDS_RING_BYTES - 1);
+        if ((roff & (LDS_RING_CHUNK - 1)) == 0) {  // entering the next chunk: refill the slot
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read before, wait for it
+          ++chunk;
+          refill(chunk + 3);
           unsigned long long c0 = 0;
           if constexpr (DIAG == 4) c0 = clk();
           asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
@@ -269,7 +270,7 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
       o[0] = st_loop;
       o[1] = st_bar;
       o[2] = st_ring;
-      o[3] = (unsigned long long)blk;
+      o[3] = (unsigned long long)chunk * 4 + (roff & (LDS_RING_CHUNK - 1)) / 128;
       o[4] = T;
     }
   }
