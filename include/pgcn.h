@@ -73,6 +73,22 @@ int pgcn_gemm_tn(int M, int N, int K, const float *A, int lda, const float *G, i
                  float *C, int ldc, const uint64_t *a_mask, long long mask_base,
                  long long mask_ld, float a_scale, void *workspace, void *stream);
 
+/* X-stream forms of the two contractions over the dense feature matrix (N <= 16, K <= 640;
+ * SparseMatmul::forward/backward on dense X, src/module.cu:104-163), with the dropout keep
+ * bits in the "nibble" layout: mask_nib[m][j] (16 words per row) holds in nibble c the bits of
+ * A[m][64c + 4j .. 64c + 4j + 3].  pgcn_mask_nibbles builds it from the flat bitmap of
+ * pgcn_gemm (bit mask_base + m*mask_ld + k).  mask_nib NULL: no dropout.  The TN form needs
+ * pgcn_gemm_tn_workspace(M, N, K) bytes of workspace.  Same results as pgcn_gemm /
+ * pgcn_gemm_tn up to fp32 summation order. */
+int pgcn_mask_nibbles(const uint64_t *mask, long long mask_base, long long mask_ld, int M, int K,
+                      uint64_t *mask_nib, void *stream);
+int pgcn_gemm_xstream(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
+                      int trans_b, float *C, int ldc, const uint64_t *mask_nib, float a_scale,
+                      void *stream);
+int pgcn_gemm_tn_xstream(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
+                         float *C, int ldc, const uint64_t *mask_nib, float a_scale,
+                         void *workspace, void *stream);
+
 /* --- sparse X (SparseMatmul, src/module.cu:104-163) ----------------------------------- */
 /* c[i,:] = sum_jj drop(a[jj]) * b[indices[jj], :], CSR order (bit-exact vs hpdga). */
 int pgcn_spmm_csr(int m, int p, const int *indptr, const int *indices, const float *a,

@@ -15,6 +15,7 @@ using namespace pgcn;
 namespace pgcn {
 extern int g_graphsum_variant;      // k_graphsum.hip (diagnostics)
 extern int g_graphsum_force_plain;  // host/graph.cpp (diagnostics)
+extern int g_gemm_variant;          // k_gemm.hip (diagnostics)
 extern int g_graphsum_lds;          // host/graph.cpp (diagnostics)
 extern int g_graphsum_lds_order;    // host/graph.cpp (diagnostics)
 extern int g_graphsum_lds_diag;     // k_graphsum_lds.hip (diagnostics)
@@ -142,6 +143,38 @@ int pgcn_gemm_tn(int M, int N, int K, const float *A, int lda, const float *G, i
     PGCN_CHECK(A && G && C && workspace && K > 0 && ldc >= N, PGCN_E_INVALID, "gemm_tn args");
     launch_gemm_tn(M, N, K, A, lda, G, ldg, C, ldc, a_mask, mask_base, mask_ld, a_scale,
                    workspace, as_stream(stream));
+    PGCN_HIP(hipGetLastError());
+  });
+}
+
+int pgcn_mask_nibbles(const uint64_t *mask, long long mask_base, long long mask_ld, int M, int K,
+                      uint64_t *out, void *stream) {
+  return guarded([&] {
+    PGCN_CHECK(mask && out && M >= 0 && K > 0, PGCN_E_INVALID, "mask_nibbles args");
+    launch_mask_nibbles(mask, mask_base, mask_ld, M, K, out, as_stream(stream));
+    PGCN_HIP(hipGetLastError());
+  });
+}
+
+int pgcn_gemm_xstream(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
+                      int trans_b, float *C, int ldc, const uint64_t *mask_nib, float a_scale,
+                      void *stream) {
+  return guarded([&] {
+    PGCN_CHECK(A && B && C && M >= 0 && ldc >= N, PGCN_E_INVALID, "gemm_xstream args");
+    launch_xstream_nn(M, N, K, A, lda, B, ldb, trans_b, C, ldc, mask_nib, a_scale,
+                      as_stream(stream));
+    PGCN_HIP(hipGetLastError());
+  });
+}
+
+int pgcn_gemm_tn_xstream(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
+                         float *C, int ldc, const uint64_t *mask_nib, float a_scale,
+                         void *workspace, void *stream) {
+  return guarded([&] {
+    PGCN_CHECK(A && G && C && workspace && M >= 0 && ldc >= N, PGCN_E_INVALID,
+               "gemm_tn_xstream args");
+    launch_xstream_tn(M, N, K, A, lda, G, ldg, C, ldc, mask_nib, a_scale, workspace,
+                      as_stream(stream));
     PGCN_HIP(hipGetLastError());
   });
 }
@@ -392,6 +425,7 @@ int pgcn_debug_set(const char *key, int value) {
   else if (!std::strcmp(key, "graphsum_lds")) pgcn::g_graphsum_lds = value;
   else if (!std::strcmp(key, "graphsum_lds_order")) pgcn::g_graphsum_lds_order = value;
   else if (!std::strcmp(key, "graphsum_lds_diag")) pgcn::g_graphsum_lds_diag = value;
+  else if (!std::strcmp(key, "gemm_variant")) pgcn::g_gemm_variant = value;
   else return PGCN_E_INVALID;
   return PGCN_OK;
 }

@@ -114,6 +114,10 @@ void GCN::upload_features(const GCNData &data) {
     });
     feats.x.allocate(x.size() + 4);
     feats.x.upload(x);
+    if (xstream_ok(params.hidden_dims.front(), F)) {
+      feats.maskT.allocate((size_t)std::max(rows, 1) * 16);
+      feats.maskT.zero();
+    }
   } else {
     std::vector<int> ip((size_t)rows + 1);
     for (int i = 0; i <= rows; i++) ip[(size_t)i] = (int)(fptr[(size_t)first + i] - p0);

@@ -67,7 +67,11 @@ void SparseMatmul::forward(bool training, const Stream &s) const {
   const uint64_t *mask = training ? drop->state().mask.get() : nullptr;
   const long long base = drop->state().mask_base;
   const float scale = drop->scale();
-  if (x->dense) {
+  if (x->dense && x->maskT) {  // X-stream kernels (N <= 16, K <= 640)
+    if (mask) launch_mask_nibbles(mask, base, x->cols, x->rows, x->cols, x->maskT.get(), s.get());
+    launch_xstream_nn(x->rows, b->cols, x->cols, x->x.get(), x->ldx, b->dev_data.get(), b->ld, 0,
+                      c->dev_data.get(), c->ld, mask ? x->maskT.get() : nullptr, scale, s.get());
+  } else if (x->dense) {
     launch_gemm_nn(x->rows, b->cols, x->cols, x->x.get(), x->ldx, b->dev_data.get(), b->ld, 0,
                    c->dev_data.get(), c->ld, mask, base, x->cols, scale, s.get());
   } else {
@@ -81,7 +85,11 @@ void SparseMatmul::backward(const Stream &s) const {
   const uint64_t *mask = last_training ? drop->state().mask.get() : nullptr;
   const long long base = drop->state().mask_base;
   const float scale = drop->scale();
-  if (x->dense) {
+  if (x->dense && x->maskT) {  // the nibble mask of the last training forward
+    launch_xstream_tn(x->rows, b->cols, x->cols, x->x.get(), x->ldx, c->dev_grad.get(), c->ld,
+                      b->dev_grad.get(), b->ld, mask ? x->maskT.get() : nullptr, scale,
+                      ctx->gemm_workspace, s.get());
+  } else if (x->dense) {
     launch_gemm_tn(x->rows, b->cols, x->cols, x->x.get(), x->ldx, c->dev_grad.get(), c->ld,
                    b->dev_grad.get(), b->ld, mask, base, x->cols, scale, ctx->gemm_workspace,
                    s.get());

@@ -50,6 +50,9 @@ struct DevFeatures {
   // dense: [rows][ldx] fp32, CSR order == row-major order
   DeviceBuffer<float> x;
   int ldx = 0;
+  // dense + X-stream kernels: the input dropout's keep bits in the nibble layout
+  // (k_mask_nibbles, [rows][16] words), rebuilt by every training forward
+  DeviceBuffer<uint64_t> maskT;
   // sparse: CSR (+ transposed index for the weight gradient)
   DeviceBuffer<int> indptr, indices, csc_ptr, csc_row, csc_pos;
   DeviceBuffer<float> values;

@@ -110,6 +110,248 @@ __global__ __launch_bounds__(256) void k_gemm_nn(int M, int N, int K,
 }
 
 // ------------------------------------------------------------------------------------------
+// X-stream kernels (N <= 16): the two contractions that read the whole dense feature matrix
+// X [M][lda] every training epoch -- Z = drop(X) W (forward) and W.grad = drop(X)^T dZ
+// (backward).  X is read once per launch and never reused, so the design goal is bytes in
+// flight: operands go straight from HBM to VGPRs (no LDS round trip), many independent
+// 16-B loads per wave are issued before the MFMAs that consume them, and the loop keeps
+// the next steps' loads outstanding while the current step computes.
+//
+// Dropout bits come in the "nibble" layout built by k_mask_nibbles from the flat
+// element-order bitmap (the order hpdga's xorshift stream draws them, rng.cpp):
+//   maskT[m][j] (j = 0..15, uint64) nibble c = keep bits of X[m][64c + 4j .. 64c + 4j + 3]
+// so the 4 bits a lane needs for one float4 of row m are one nibble of ONE word it loads
+// with the row (K <= 1024).  128 B per row: +5 % over the X row's 2408 B on reddit.
+// ------------------------------------------------------------------------------------------
+constexpr int XS_MAX_KC = 10;  // K <= 640 (64-wide chunks) for the register-resident paths
+
+__device__ __forceinline__ void apply4(float4 &a, uint32_t bits, float scale) {
+  a.x *= (bits & 1) ? scale : 0.0f;
+  a.y *= (bits & 2) ? scale : 0.0f;
+  a.z *= (bits & 4) ? scale : 0.0f;
+  a.w *= (bits & 8) ? scale : 0.0f;
+}
+
+// maskT[m][j] from the flat bitmap (bit mask_base + m*mask_ld + k).  One thread per word.
+__global__ __launch_bounds__(256) void k_mask_nibbles(const uint64_t *__restrict__ mask,
+                                                      long long mask_base, long long mask_ld,
+                                                      int M, int K, uint64_t *__restrict__ out) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long long)M * 16) return;
+  const long long m = t >> 4;
+  const int j = (int)(t & 15);
+  uint64_t word = 0;
+  for (int c = 0; 64 * c + 4 * j < K; c++) {
+    const long long p = mask_base + m * mask_ld + 64 * c + 4 * j;
+    const long long w = p >> 6;
+    const int sh = (int)(p & 63);
+    uint64_t v = mask[w] >> sh;
+    if (sh > 60) v |= mask[w + 1] << (64 - sh);
+    uint64_t nib = v & 0xfu;
+    const int kb = 64 * c + 4 * j;  // keep bits of k >= K are 0
+    if (kb + 4 > K) nib &= (1ull << (K - kb)) - 1;
+    word |= nib << (4 * c);
+  }
+  out[t] = word;
+}
+
+// NN: Z[M][N<=16] = drop(X) W.  A wave owns a 16-row group at a time (grid-stride over
+// groups) and issues all of the group's A loads (one float4 per lane per 16-wide k-step:
+// lane (i, g) reads X[row i][16 s + 4 g ..]) before its first MFMA; 2 waves per SIMD keep one
+// group's loads in flight while the other computes.  B^T lives in LDS for the block's life:
+// bt[j][k], row stride S = 8 mod 16 dwords, so the per-step float4 B operand read
+// bt[i][16 s + 4 g ..] is conflict-free.  MFMA t of step s reduces k = 16 s + 4 g + t.
+template <int KC, bool MASKED>
+__global__ __launch_bounds__(256, 2) void k_xstream_nn(int M, int N, int K, int S,
+                                                       const float *__restrict__ A, int lda,
+                                                       const float *__restrict__ B, int ldb,
+                                                       int trans_b, float *__restrict__ C,
+                                                       int ldc, const uint64_t *__restrict__ maskT,
+                                                       float a_scale) {
+  constexpr int NS = 4 * KC;  // 16-wide k-steps (the last ones may be past K)
+  extern __shared__ float bt[];
+  for (int e = threadIdx.x; e < 16 * NS * 16; e += 256) {
+    const int k = e >> 4, j = e & 15;
+    float v = 0.0f;
+    if (k < K && j < N) v = trans_b ? B[(long long)j * ldb + k] : B[(long long)k * ldb + j];
+    bt[j * S + k] = v;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4, i = lane & 15;
+  const long long n_rg = (M + 15) / 16;
+  const long long wstride = (long long)gridDim.x * 4;
+  const float *bl = bt + i * S + 4 * g;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  for (long long rg = (long long)blockIdx.x * 4 + w; rg < n_rg; rg += wstride) {
+    const long long row = rg * 16 + i;
+    const bool row_ok = row < M;
+    const float *arow = A + (row_ok ? row : 0) * (long long)lda + 4 * g;
+    float4 a[NS];
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+      a[s] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (row_ok && 16 * s + 4 * g < K) a[s] = *reinterpret_cast<const float4 *>(arow + 16 * s);
+    }
+    uint64_t mw[4] = {0, 0, 0, 0};
+    if constexpr (MASKED) {
+      if (row_ok) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) mw[q] = maskT[row * 16 + 4 * q + g];
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep the B reads out of the load phase (VGPRs)
+    floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+      const int kb = 16 * s + 4 * g;
+      if (16 * s + 16 > K) {  // k >= K lanes of the tail steps (A's ld padding, may be NaN)
+        if (kb + 1 > K) a[s].x = 0.f;
+        if (kb + 2 > K) a[s].y = 0.f;
+        if (kb + 3 > K) a[s].z = 0.f;
+        if (kb + 4 > K) a[s].w = 0.f;
+      }
+      if constexpr (MASKED)
+        apply4(a[s], (uint32_t)(mw[s & 3] >> (4 * (s >> 2))) & 0xfu, a_scale);
+      const float4 b = *reinterpret_cast<const float4 *>(bl + 16 * s);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s].x, b.x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s].y, b.y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s].z, b.z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s].w, b.w, acc, 0, 0, 0);
+    }
+    // lane holds C[16 rg + 4g + r][i]
+    if (i < ldc) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const long long rr = rg * 16 + 4 * g + r;
+        if (rr < M) C[rr * ldc + i] = acc[r];
+      }
+    }
+  }
+}
+
+// TN: W.grad[K][N<=16] = drop(X)^T G.  A wave owns ALL K columns of 4 rows per step (one
+// step = 4 whole rows, contiguous); lane (i, g) holds X[m+g][64c + 4i ..] for chunk c and
+// feeds MFMA (c, t) with output row k = 64c + 4i + t, reduction index = row g; its keep bits
+// are nibble c of maskT[m+g][i] and its B operand G[m+g][i].  Steps are dealt round-robin to
+// the grid's waves; three register sets keep steps n+1 and n+2 loading while n computes.
+// Each block sums its 4 waves in LDS in wave order and writes one [K][16] partial; the
+// partials are reduced in block order (k_slab_reduce1 / k_gemm_tn_reduce): deterministic.
+template <int KC, bool MASKED>
+struct TnStep {
+  float4 a[KC];
+  uint64_t mw;
+  float bj;
+  // Unconditional loads (no exec branches): rows past M read row M-1 and get bj = 0; the
+  // columns of a lane past K read inside the row (clamped) and are zeroed in tn_compute.
+  __device__ __forceinline__ void load(long long m, long long M, int g, int i, int K,
+                                       const float *__restrict__ A, int lda,
+                                       const float *__restrict__ G, int ldg, int N,
+                                       const uint64_t *__restrict__ maskT) {
+    const long long mr = m + g;
+    const bool ok = mr < M;
+    const long long row = ok ? mr : M - 1;
+    const float *ar = A + row * (long long)lda;
+#pragma unroll
+    for (int c = 0; c < KC; c++) {
+      int kb = 64 * c + 4 * i;
+      kb = kb < lda - 4 ? kb : lda - 4;
+      a[c] = *reinterpret_cast<const float4 *>(ar + kb);
+    }
+    const float gv = G[row * ldg + (i < N ? i : 0)];
+    bj = (ok && i < N) ? gv : 0.0f;
+    if constexpr (MASKED) mw = maskT[row * 16 + i];
+  }
+};
+
+template <int KC, bool MASKED>
+__device__ __forceinline__ void tn_compute(TnStep<KC, MASKED> &st, floatx4 (&acc)[KC][4], int i,
+                                           int K, float a_scale) {
+#pragma unroll
+  for (int c = 0; c < KC; c++) {
+    float4 x = st.a[c];
+    const int kb = 64 * c + 4 * i;
+    if (64 * c + 64 > K) {
+      if (kb + 1 > K) x.x = 0.f;
+      if (kb + 2 > K) x.y = 0.f;
+      if (kb + 3 > K) x.z = 0.f;
+      if (kb + 4 > K) x.w = 0.f;
+    }
+    if constexpr (MASKED) apply4(x, (uint32_t)(st.mw >> (4 * c)) & 0xfu, a_scale);
+    acc[c][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(x.x, st.bj, acc[c][0], 0, 0, 0);
+    acc[c][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(x.y, st.bj, acc[c][1], 0, 0, 0);
+    acc[c][2] = __builtin_amdgcn_mfma_f32_16x16x4f32(x.z, st.bj, acc[c][2], 0, 0, 0);
+    acc[c][3] = __builtin_amdgcn_mfma_f32_16x16x4f32(x.w, st.bj, acc[c][3], 0, 0, 0);
+  }
+}
+
+constexpr int XS_TN_BLOCKS = 256;  // one 4-wave block per CU (1 wave per SIMD, ~300 registers)
+
+template <int KC, bool MASKED>
+__global__ __launch_bounds__(256, 1) void k_xstream_tn(int M, int N, int K,
+                                                       const float *__restrict__ A, int lda,
+                                                       const float *__restrict__ G, int ldg,
+                                                       const uint64_t *__restrict__ maskT,
+                                                       float a_scale, float *__restrict__ partial) {
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, i = lane & 15;
+  floatx4 acc[KC][4];
+#pragma unroll
+  for (int c = 0; c < KC; c++)
+#pragma unroll
+    for (int t = 0; t < 4; t++) acc[c][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const long long stride = (long long)gridDim.x * 4 * 4;  // rows between a wave's steps
+  const long long n_steps = (M + 3) / 4;
+  const long long wid = (long long)blockIdx.x * 4 + w;
+  const long long my_steps = wid < n_steps ? (n_steps - wid + gridDim.x * 4 - 1) / (gridDim.x * 4) : 0;
+  long long m = wid * 4;
+  // two register sets: step n+1 loads while step n computes (three spill at KC = 10)
+  TnStep<KC, MASKED> s0, s1;
+  s0.load(m, M, g, i, K, A, lda, G, ldg, N, maskT);
+  for (long long n = 0; n < my_steps; n += 2) {
+    s1.load(m + stride, M, g, i, K, A, lda, G, ldg, N, maskT);
+    __builtin_amdgcn_sched_barrier(0);
+    tn_compute(s0, acc, i, K, a_scale);
+    // (past the wave's last step s1 holds zeros: its MFMAs add nothing)
+    s0.load(m + 2 * stride, M, g, i, K, A, lda, G, ldg, N, maskT);
+    __builtin_amdgcn_sched_barrier(0);
+    tn_compute(s1, acc, i, K, a_scale);
+    m += 2 * stride;
+  }
+  // waves 1..3 hand their chunk tiles to wave 0 through LDS (fixed order)
+  __shared__ float red[3 * 64 * 16];
+  float *p = partial + (long long)blockIdx.x * K * 16;
+#pragma unroll
+  for (int c = 0; c < KC; c++) {
+    if (w > 0) {
+#pragma unroll
+      for (int t = 0; t < 4; t++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) red[((w - 1) * 64 + lane) * 16 + t * 4 + r] = acc[c][t][r];
+    }
+    __syncthreads();
+    if (w == 0) {
+#pragma unroll
+      for (int t = 0; t < 4; t++) {
+        floatx4 v = acc[c][t];
+#pragma unroll
+        for (int q = 0; q < 3; q++)
+#pragma unroll
+          for (int r = 0; r < 4; r++) v[r] += red[(q * 64 + lane) * 16 + t * 4 + r];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int k = 64 * c + 4 * (4 * g + r) + t;
+          if (k < K) p[(long long)k * 16 + i] = v[r];
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+int g_gemm_variant = 0;  // diagnostics ("gemm_variant"): 1 = the general kernels only
+
+// ------------------------------------------------------------------------------------------
 // TN split-M.  Block = 4 waves over a slab of rows; the K columns are cut into 64-wide chunks.
 // Wave layout: WK waves along K x (4/WK) waves along rows.  Per step of 4 rows a lane
 // (g = lane>>4, i = lane&15) loads ONE float4 A[m+g][kc*64 + 4i .. +3] (a wave reads 4 rows
@@ -249,12 +491,60 @@ __global__ __launch_bounds__(256) void k_gemm_tn_reduce(const float *__restrict_
 // ------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------
+bool xstream_ok(int N, int K) {
+  return g_gemm_variant != 1 && N >= 1 && N <= 16 && K >= 1 && (K + 63) / 64 <= XS_MAX_KC;
+}
+
+static int xs_stride(int K) {  // LDS row stride of B^T: >= 64*KC, = 8 mod 16 dwords
+  int s = (K + 63) / 64 * 64;
+  while (s % 16 != 8) s += 8;
+  return s;
+}
+
+void launch_mask_nibbles(const uint64_t *mask, long long mask_base, long long mask_ld, int M,
+                         int K, uint64_t *out, hipStream_t s) {
+  PGCN_CHECK(K >= 1 && K <= 1024, PGCN_E_INVALID, "mask_nibbles: K must be in [1,1024]");
+  if (M <= 0) return;
+  hipLaunchKernelGGL(k_mask_nibbles, dim3((unsigned)ceil_div((long long)M * 16, 256)), dim3(256),
+                     0, s, mask, mask_base, mask_ld, M, K, out);
+}
+
+void launch_xstream_nn(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
+                       int trans_b, float *C, int ldc, const uint64_t *maskT, float a_scale,
+                       hipStream_t s) {
+  PGCN_CHECK(xstream_ok(N, K), PGCN_E_INVALID, "xstream_nn: needs N <= 16, K <= 640");
+  PGCN_CHECK(lda % 4 == 0 && lda >= K, PGCN_E_INVALID, "gemm: lda must be a multiple of 4 >= K");
+  if (M <= 0) return;
+  const int kc = (K + 63) / 64, S = xs_stride(K);
+  const long long n_rg = ceil_div(M, 16);
+  const dim3 grid((unsigned)std::min<long long>(ceil_div(n_rg, 4), 2 * kCUs)), block(256);
+  const size_t lds = (size_t)16 * S * sizeof(float);
+#define XNN_CASE(KC)                                                                          \
+  case KC:                                                                                    \
+    if (maskT)                                                                                \
+      hipLaunchKernelGGL((k_xstream_nn<KC, true>), grid, block, lds, s, M, N, K, S, A, lda, B, \
+                         ldb, trans_b, C, ldc, maskT, a_scale);                               \
+    else                                                                                      \
+      hipLaunchKernelGGL((k_xstream_nn<KC, false>), grid, block, lds, s, M, N, K, S, A, lda,   \
+                         B, ldb, trans_b, C, ldc, maskT, a_scale);                            \
+    break;
+  switch (kc) {
+    XNN_CASE(1) XNN_CASE(2) XNN_CASE(3) XNN_CASE(4) XNN_CASE(5)
+    XNN_CASE(6) XNN_CASE(7) XNN_CASE(8) XNN_CASE(9) XNN_CASE(10)
+  }
+#undef XNN_CASE
+}
+
 void launch_gemm_nn(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
                     int trans_b, float *C, int ldc, const uint64_t *a_mask, long long mask_base,
                     long long mask_ld, float a_scale, hipStream_t s) {
   PGCN_CHECK(lda % 4 == 0 && lda >= K, PGCN_E_INVALID, "gemm: lda must be a multiple of 4 >= K");
   PGCN_CHECK(N <= 128 && N >= 1, PGCN_E_INVALID, "gemm: N must be in [1,128]");
   if (M <= 0) return;
+  if (!a_mask && xstream_ok(N, K)) {
+    launch_xstream_nn(M, N, K, A, lda, B, ldb, trans_b, C, ldc, nullptr, 1.0f, s);
+    return;
+  }
   const int nt = (N + 15) / 16;
   const dim3 grid((unsigned)ceil_div(M, 64)), block(256);
 #define NN_CASE(T)                                                                            \
@@ -292,9 +582,63 @@ static TnPlan tn_plan(int M, int N, int K) {
   return p;
 }
 
-size_t gemm_tn_workspace(int M, int N, int K) {
-  const TnPlan p = tn_plan(M, N, K);
+static TnPlan xs_tn_plan(int K) {  // k_xstream_tn: one [K][16] partial per block
+  TnPlan p{};
+  p.nj = 1;
+  p.ldp = 16;
+  p.nkc = (K + 63) / 64;
+  p.n_slabs = XS_TN_BLOCKS;
+  p.spg = 16;
+  p.n_groups = (p.n_slabs + p.spg - 1) / p.spg;
+  return p;
+}
+
+static size_t plan_bytes(const TnPlan &p, int K) {
   return ((size_t)p.n_slabs + (size_t)p.n_groups) * (size_t)K * (size_t)p.ldp * sizeof(float);
+}
+
+size_t gemm_tn_workspace(int M, int N, int K) {
+  size_t ws = plan_bytes(tn_plan(M, N, K), K);  // either kernel family may run
+  if (N <= 16) ws = std::max(ws, plan_bytes(xs_tn_plan(K), K));
+  return ws;
+}
+
+// ordered two-pass reduction of p.n_slabs partials [K][ldp] into C[K][ldc]
+static void tn_reduce(const TnPlan &p, int M, int N, int K, float *partial, float *C, int ldc,
+                      hipStream_t s) {
+  float *part2 = partial + (size_t)p.n_slabs * K * p.ldp;
+  const long long elems = (long long)K * p.ldp;
+  if (M > 0)
+    hipLaunchKernelGGL(k_slab_reduce1, dim3((unsigned)ceil_div(elems, 256), (unsigned)p.n_groups),
+                       dim3(256), 0, s, partial, p.n_slabs, elems, p.spg, part2);
+  hipLaunchKernelGGL(k_gemm_tn_reduce, dim3((unsigned)ceil_div(elems, 256)), dim3(256), 0, s,
+                     part2, M > 0 ? p.n_groups : 0, K, N, p.ldp, C, ldc);
+}
+
+void launch_xstream_tn(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
+                       float *C, int ldc, const uint64_t *maskT, float a_scale, void *workspace,
+                       hipStream_t s) {
+  PGCN_CHECK(xstream_ok(N, K), PGCN_E_INVALID, "xstream_tn: needs N <= 16, K <= 640");
+  PGCN_CHECK(lda % 4 == 0 && lda >= K, PGCN_E_INVALID, "gemm_tn: lda must be a multiple of 4 >= K");
+  const TnPlan p = xs_tn_plan(K);
+  float *partial = static_cast<float *>(workspace);
+  if (M > 0) {
+#define XTN_CASE(KC)                                                                           \
+  case KC:                                                                                     \
+    if (maskT)                                                                                 \
+      hipLaunchKernelGGL((k_xstream_tn<KC, true>), dim3(XS_TN_BLOCKS), dim3(256), 0, s, M, N, K, \
+                         A, lda, G, ldg, maskT, a_scale, partial);                             \
+    else                                                                                       \
+      hipLaunchKernelGGL((k_xstream_tn<KC, false>), dim3(XS_TN_BLOCKS), dim3(256), 0, s, M, N,  \
+                         K, A, lda, G, ldg, maskT, a_scale, partial);                          \
+    break;
+    switch (p.nkc) {
+      XTN_CASE(1) XTN_CASE(2) XTN_CASE(3) XTN_CASE(4) XTN_CASE(5)
+      XTN_CASE(6) XTN_CASE(7) XTN_CASE(8) XTN_CASE(9) XTN_CASE(10)
+    }
+#undef XTN_CASE
+  }
+  tn_reduce(p, M, N, K, partial, C, ldc, s);
 }
 
 void launch_gemm_tn(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
@@ -302,10 +646,12 @@ void launch_gemm_tn(int M, int N, int K, const float *A, int lda, const float *G
                     long long mask_ld, float a_scale, void *workspace, hipStream_t s) {
   PGCN_CHECK(N <= 128 && N >= 1, PGCN_E_INVALID, "gemm_tn: N must be in [1,128]");
   PGCN_CHECK(lda % 4 == 0 && lda >= K, PGCN_E_INVALID, "gemm_tn: lda must be a multiple of 4 >= K");
+  if (!a_mask && xstream_ok(N, K)) {
+    launch_xstream_tn(M, N, K, A, lda, G, ldg, C, ldc, nullptr, 1.0f, workspace, s);
+    return;
+  }
   const TnPlan p = tn_plan(M, N, K);
   float *partial = static_cast<float *>(workspace);
-  float *part2 = partial + (size_t)p.n_slabs * K * p.ldp;
-  const long long elems = (long long)K * p.ldp;
   if (M > 0) {
     const dim3 grid((unsigned)p.n_slabs, (unsigned)p.kgroups), block(256);
     bool done = false;
@@ -326,11 +672,8 @@ void launch_gemm_tn(int M, int N, int K, const float *A, int lda, const float *G
 #undef TN_CASE
     PGCN_CHECK(done, PGCN_E_INVALID,
                "gemm_tn: no kernel for N=" + std::to_string(N) + " K=" + std::to_string(K));
-    hipLaunchKernelGGL(k_slab_reduce1, dim3((unsigned)ceil_div(elems, 256), (unsigned)p.n_groups),
-                       dim3(256), 0, s, partial, p.n_slabs, elems, p.spg, part2);
   }
-  hipLaunchKernelGGL(k_gemm_tn_reduce, dim3((unsigned)ceil_div(elems, 256)), dim3(256), 0, s,
-                     part2, M > 0 ? p.n_groups : 0, K, N, p.ldp, C, ldc);
+  tn_reduce(p, M, N, K, partial, C, ldc, s);
 }
 
 }  // namespace pgcn

@@ -56,6 +56,16 @@ void launch_gemm_nn(int M, int N, int K, const float *A, int lda, const float *B
                     int trans_b, float *C, int ldc, const uint64_t *a_mask, long long mask_base,
                     long long mask_ld, float a_scale, hipStream_t s);
 size_t gemm_tn_workspace(int M, int N, int K);
+// X-stream kernels (k_gemm.hip): N <= 16, K <= 640, dropout bits in the nibble layout
+bool xstream_ok(int N, int K);
+void launch_mask_nibbles(const uint64_t *mask, long long mask_base, long long mask_ld, int M,
+                         int K, uint64_t *out, hipStream_t s);
+void launch_xstream_nn(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
+                       int trans_b, float *C, int ldc, const uint64_t *maskT, float a_scale,
+                       hipStream_t s);
+void launch_xstream_tn(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
+                       float *C, int ldc, const uint64_t *maskT, float a_scale, void *workspace,
+                       hipStream_t s);
 void launch_gemm_tn(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
                     float *C, int ldc, const uint64_t *a_mask, long long mask_base,
                     long long mask_ld, float a_scale, void *workspace, hipStream_t s);

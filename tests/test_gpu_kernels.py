@@ -182,33 +182,46 @@ def test_dropout_apply(pgcn):
     np.testing.assert_array_equal(x.cpu().numpy(), ref.astype(np.float32))
 
 
-@pytest.mark.parametrize("M,N,K,drop", [(1000, 16, 602, True), (777, 41, 16, False),
-                                        (513, 16, 41, False), (300, 128, 128, False),
-                                        (64, 16, 1433, True)])
-def test_gemm_nn(pgcn, M, N, K, drop):
+def mask_window(mask, base, M, K):
+    """bits base .. base + M*K of a flat bitmap as an (M, K) bool array"""
+    return mask_bits(mask, base + M * K)[base:].reshape(M, K)
+
+
+GEMM_VARIANTS = [0, 1]  # 0: N <= 16 streaming kernels where they apply; 1: general kernels
+
+
+@pytest.mark.parametrize("variant", GEMM_VARIANTS)
+@pytest.mark.parametrize("M,N,K,drop,base", [(1000, 16, 602, True, 0), (777, 41, 16, False, 0),
+                                             (513, 16, 41, False, 0), (300, 128, 128, False, 0),
+                                             (64, 16, 1433, True, 0), (2011, 16, 602, True, 37),
+                                             (99, 13, 70, True, 63), (5, 16, 602, True, 1)])
+def test_gemm_nn(pgcn, M, N, K, drop, base, variant):
     rng = np.random.default_rng(M + N + K)
     lda = (K + 3) // 4 * 4
     A = np.zeros((M, lda), np.float32)
     A[:, :K] = rng.standard_normal((M, K))
+    A[:, K:] = np.nan  # ld padding is never read into the result
     B = rng.standard_normal((K, N)).astype(np.float32)
-    mask = rng.integers(0, 2**63, (M * K + 63) // 64 + 2, dtype=np.uint64)
+    # exactly as many words as the bits need: the kernels must not read past the bitmap
+    mask = rng.integers(0, 2**63, (base + M * K + 63) // 64, dtype=np.uint64)
     Ae = A[:, :K].astype(np.float64)
     if drop:
-        bits = mask_bits(mask, M * K).reshape(M, K)
-        Ae = Ae * np.where(bits, 2.0, 0.0)
+        Ae = Ae * np.where(mask_window(mask, base, M, K), 2.0, 0.0)
+    pgcn.lib.pgcn_debug_set(b"gemm_variant", variant)
     ref = Ae @ B.astype(np.float64)
     dA, dB = torch.from_numpy(A).to(DEV), torch.from_numpy(B).to(DEV)
     dm = torch.from_numpy(mask.view(np.int64)).to(DEV)
     ldc = (N + 3) // 4 * 4
     C = torch.full((M, ldc), float("nan"), device=DEV)
     pgcn.check(pgcn.lib.pgcn_gemm(M, N, K, vp(dA), lda, vp(dB), N, 0, vp(C), ldc,
-                                  vp(dm) if drop else None, 0, K, 2.0, stream()), "gemm")
+                                  vp(dm) if drop else None, base, K, 2.0, stream()), "gemm")
     # transposed B: C2 = A * (B^T)^T with B^T stored [N][K]
     dBt = torch.from_numpy(np.ascontiguousarray(B.T)).to(DEV)
     C2 = torch.empty((M, ldc), device=DEV)
     pgcn.check(pgcn.lib.pgcn_gemm(M, N, K, vp(dA), lda, vp(dBt), K, 1, vp(C2), ldc,
-                                  vp(dm) if drop else None, 0, K, 2.0, stream()), "gemm_t")
+                                  vp(dm) if drop else None, base, K, 2.0, stream()), "gemm_t")
     torch.cuda.synchronize()
+    pgcn.lib.pgcn_debug_set(b"gemm_variant", 0)
     bound = np.abs(Ae) @ np.abs(B.astype(np.float64))
     for out in (C, C2):
         o = out.cpu().numpy()
@@ -216,29 +229,89 @@ def test_gemm_nn(pgcn, M, N, K, drop):
         np.testing.assert_array_equal(o[:, N:], 0.0)
 
 
-@pytest.mark.parametrize("M,N,K,drop", [(5000, 16, 602, True), (3000, 41, 16, False),
-                                        (2000, 128, 128, False), (100, 16, 1433, True),
-                                        (70000, 16, 602, False)])
-def test_gemm_tn(pgcn, M, N, K, drop):
+@pytest.mark.parametrize("variant", GEMM_VARIANTS)
+@pytest.mark.parametrize("M,N,K,drop,base", [(5000, 16, 602, True, 0), (3000, 41, 16, False, 0),
+                                             (2000, 128, 128, False, 0), (100, 16, 1433, True, 0),
+                                             (70000, 16, 602, False, 0), (4099, 16, 602, True, 29),
+                                             (333, 16, 200, True, 63), (7, 11, 602, True, 5)])
+def test_gemm_tn(pgcn, M, N, K, drop, base, variant):
     rng = np.random.default_rng(M + 3 * N + K)
     lda = (K + 3) // 4 * 4
     A = np.zeros((M, lda), np.float32)
     A[:, :K] = rng.standard_normal((M, K))
+    A[:, K:] = np.nan
     Gm = rng.standard_normal((M, N)).astype(np.float32)
-    mask = rng.integers(0, 2**63, (M * K + 63) // 64 + 2, dtype=np.uint64)
+    mask = rng.integers(0, 2**63, (base + M * K + 63) // 64, dtype=np.uint64)
     Ae = A[:, :K].astype(np.float64)
     if drop:
-        Ae = Ae * np.where(mask_bits(mask, M * K).reshape(M, K), 2.0, 0.0)
+        Ae = Ae * np.where(mask_window(mask, base, M, K), 2.0, 0.0)
     ref = Ae.T @ Gm.astype(np.float64)
+    pgcn.lib.pgcn_debug_set(b"gemm_variant", variant)
     ws = torch.empty(pgcn.lib.pgcn_gemm_tn_workspace(M, N, K) // 4 + 16, device=DEV)
     dA, dG = torch.from_numpy(A).to(DEV), torch.from_numpy(Gm).to(DEV)
     dm = torch.from_numpy(mask.view(np.int64)).to(DEV)
     C = torch.full((K, N), float("nan"), device=DEV)
     pgcn.check(pgcn.lib.pgcn_gemm_tn(M, N, K, vp(dA), lda, vp(dG), N, vp(C), N,
-                                     vp(dm) if drop else None, 0, K, 2.0, vp(ws), stream()), "tn")
+                                     vp(dm) if drop else None, base, K, 2.0, vp(ws), stream()),
+               "tn")
     torch.cuda.synchronize()
+    pgcn.lib.pgcn_debug_set(b"gemm_variant", 0)
     bound = np.abs(Ae).T @ np.abs(Gm.astype(np.float64))
     assert (np.abs(C.cpu().numpy() - ref) <= 1e-5 * bound + 1e-30).all()
+
+
+def nibble_mask_ref(mask, base, M, K):
+    """maskT[m][j] nibble c = keep bits of (m, 64c + 4j .. +3), zero past K (numpy)"""
+    bits = np.zeros((M, 1024), np.uint64)
+    bits[:, :K] = mask_window(mask, base, M, K)
+    nib = bits.reshape(M, 16, 16, 4)  # [m][c][j][t]: k = 64c + 4j + t
+    vals = (nib << np.arange(4, dtype=np.uint64)).sum(-1)  # [m][c][j]
+    out = np.zeros((M, 16), np.uint64)
+    for c in range(16):
+        out |= vals[:, c, :] << np.uint64(4 * c)
+    return out
+
+
+@pytest.mark.parametrize("M,N,K,base", [(3001, 16, 602, 0), (1000, 16, 602, 41), (77, 12, 100, 63),
+                                        (129, 16, 640, 5), (20, 3, 7, 0)])
+def test_gemm_xstream(pgcn, M, N, K, base):
+    """X-stream NN/TN kernels with nibble-layout dropout bits vs fp64 references."""
+    rng = np.random.default_rng(7 * M + K)
+    lda = (K + 3) // 4 * 4
+    A = np.zeros((M, lda), np.float32)
+    A[:, :K] = rng.standard_normal((M, K))
+    A[:, K:] = np.nan
+    B = rng.standard_normal((K, N)).astype(np.float32)
+    Gm = rng.standard_normal((M, N)).astype(np.float32)
+    mask = rng.integers(0, 2**63, (base + M * K + 63) // 64, dtype=np.uint64)
+    keep = mask_window(mask, base, M, K)
+    dA, dB, dG = (torch.from_numpy(a).to(DEV) for a in (A, B, Gm))
+    dm = torch.from_numpy(mask.view(np.int64)).to(DEV)
+    nib = torch.empty((M, 16), dtype=torch.int64, device=DEV)
+    pgcn.check(pgcn.lib.pgcn_mask_nibbles(vp(dm), base, K, M, K, vp(nib), stream()), "nib")
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(nib.cpu().numpy().view(np.uint64),
+                                  nibble_mask_ref(mask, base, M, K))
+    ldc = (N + 3) // 4 * 4
+    ws = torch.empty(pgcn.lib.pgcn_gemm_tn_workspace(M, N, K) // 4 + 16, device=DEV)
+    for drop in (False, True):
+        Ae = A[:, :K].astype(np.float64) * (np.where(keep, 2.0, 0.0) if drop else 1.0)
+        C = torch.full((M, ldc), float("nan"), device=DEV)
+        pgcn.check(pgcn.lib.pgcn_gemm_xstream(M, N, K, vp(dA), lda, vp(dB), N, 0, vp(C), ldc,
+                                              vp(nib) if drop else None, 2.0, stream()), "xnn")
+        W = torch.full((K, N), float("nan"), device=DEV)
+        pgcn.check(pgcn.lib.pgcn_gemm_tn_xstream(M, N, K, vp(dA), lda, vp(dG), N, vp(W), N,
+                                                 vp(nib) if drop else None, 2.0, vp(ws),
+                                                 stream()), "xtn")
+        torch.cuda.synchronize()
+        ref = Ae @ B.astype(np.float64)
+        bound = np.abs(Ae) @ np.abs(B.astype(np.float64))
+        o = C.cpu().numpy()
+        assert (np.abs(o[:, :N] - ref) <= 1e-5 * bound + 1e-30).all()
+        np.testing.assert_array_equal(o[:, N:], 0.0)
+        ref_t = Ae.T @ Gm.astype(np.float64)
+        bound_t = np.abs(Ae).T @ np.abs(Gm.astype(np.float64))
+        assert (np.abs(W.cpu().numpy() - ref_t) <= 1e-5 * bound_t + 1e-30).all()
 
 
 def test_spmm_csr_and_csc_bit_exact(pgcn, loaded):
