@@ -106,6 +106,9 @@ def main():
     if args.gpus != world and world != 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     dist = None
+    # this rank's GPU before anything touches HIP through torch (torch.cuda.synchronize()
+    # below would otherwise open a context on GPU 0 from every rank)
+    torch.cuda.set_device(local_rank)
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")

@@ -229,6 +229,11 @@ int pgcn_debug_set(const char *key, int value);
 /* copies up to max_elems of a diagnostic buffer ("graphsum_lds_stamps": per-wave cycle stamps
  * of the last graphsum_lds_diag=4 launch); returns the buffer's element count or a status */
 long long pgcn_debug_read(const char *key, void *dst, long long max_elems);
+/* Host-only check of the d = 16 LDS GraphSum schedule (window 1 or 2) of a CSR pattern: builds
+ * it, walks it as k_graphsum_lds consumes it over a seeded input and returns the max relative
+ * error of the row sums against a direct CSR sum, and the number of 4-step entry blocks. */
+int pgcn_debug_lds_check(int n_rows, int n_cols, const int *indptr, const int *indices,
+                         int window, double *max_rel_err, long long *n_blocks);
 
 #ifdef __cplusplus
 }

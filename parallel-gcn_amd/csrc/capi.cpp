@@ -9,6 +9,9 @@
 #include "host/gcn.hpp"
 #include "host/graph.hpp"
 #include "kernels.hpp"
+#include "rng.hpp"
+
+#include <cmath>
 
 using namespace pgcn;
 
@@ -19,6 +22,7 @@ extern int g_gemm_variant;          // k_gemm.hip (diagnostics)
 extern int g_graphsum_lds;          // host/graph.cpp (diagnostics)
 extern int g_graphsum_lds_order;    // host/graph.cpp (diagnostics)
 extern int g_graphsum_lds_diag;     // k_graphsum_lds.hip (diagnostics)
+extern int g_graphsum_lds_window;   // host/graph.cpp (diagnostics)
 long long lds_stamps_read(void *dst, long long max_elems);
 }  // namespace pgcn
 
@@ -425,9 +429,39 @@ int pgcn_debug_set(const char *key, int value) {
   else if (!std::strcmp(key, "graphsum_lds")) pgcn::g_graphsum_lds = value;
   else if (!std::strcmp(key, "graphsum_lds_order")) pgcn::g_graphsum_lds_order = value;
   else if (!std::strcmp(key, "graphsum_lds_diag")) pgcn::g_graphsum_lds_diag = value;
+  else if (!std::strcmp(key, "graphsum_lds_window")) pgcn::g_graphsum_lds_window = value;
   else if (!std::strcmp(key, "gemm_variant")) pgcn::g_gemm_variant = value;
   else return PGCN_E_INVALID;
   return PGCN_OK;
+}
+
+// CPU check of the d = 16 LDS schedule of a CSR pattern: builds it (window 1 or 2), walks it
+// as the kernel does over a seeded input and reports the max relative error of the sums
+// against a direct CSR sum, and the number of entry blocks.  No device needed.
+int pgcn_debug_lds_check(int n_rows, int n_cols, const int *indptr, const int *indices,
+                         int window, double *max_rel_err, long long *n_blocks) {
+  return guarded([&] {
+    PGCN_CHECK(n_rows > 0 && n_cols > 0 && indptr && indices, PGCN_E_INVALID, "lds_check args");
+    std::vector<int> ip(indptr, indptr + n_rows + 1), ix(indices, indices + indptr[n_rows]);
+    const std::vector<int> cut = column_cuts(n_cols, ix);
+    const LdsHost h = build_lds_host(n_rows, n_cols, ip, ix, cut, window);
+    std::vector<float> in((size_t)n_cols);
+    uint64_t st[2] = {12345, 67890};
+    for (auto &x : in) x = (float)((double)(xs_next(st) & 0xffffff) / (double)0x1000000 - 0.5);
+    std::vector<double> out((size_t)n_rows, 0.0);
+    lds_emulate(h, n_rows, in.data(), out.data());
+    double err = 0;
+    for (int r = 0; r < n_rows; r++) {
+      double ref = 0, mag = 0;
+      for (int k = ip[(size_t)r]; k < ip[(size_t)r + 1]; k++) {
+        ref += in[(size_t)ix[(size_t)k]];
+        mag += std::fabs(in[(size_t)ix[(size_t)k]]);
+      }
+      err = std::max(err, std::fabs(out[(size_t)r] - ref) / (mag + 1e-30));
+    }
+    if (max_rel_err) *max_rel_err = err;
+    if (n_blocks) *n_blocks = h.wave_off.back();
+  });
 }
 
 long long pgcn_debug_read(const char *key, void *dst, long long max_elems) {

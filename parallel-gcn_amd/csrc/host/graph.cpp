@@ -82,19 +82,7 @@ int DevGraph::column_blocks(int dim) {
 
 // Cut the columns into kBlocks nnz-balanced ranges.
 void DevGraph::compute_cuts() {
-  if (!bcut_.empty()) return;
-  const int B = kBlocks;
-  std::vector<long long> colcnt((size_t)n_cols_ + 1, 0);
-  for (long long k = 0; k < nnz_; k++) colcnt[(size_t)h_indices_[(size_t)k] + 1]++;
-  for (int c = 0; c < n_cols_; c++) colcnt[(size_t)c + 1] += colcnt[(size_t)c];
-  bcut_.assign((size_t)B + 1, 0);
-  bcut_[(size_t)B] = n_cols_;
-  for (int b = 1; b < B; b++) {
-    const long long target = (long long)((double)nnz_ * b / B);
-    int c = (int)(std::lower_bound(colcnt.begin(), colcnt.end(), target) - colcnt.begin());
-    c = std::max(c, bcut_[(size_t)b - 1]);
-    bcut_[(size_t)b] = std::min(c, n_cols_);
-  }
+  if (bcut_.empty()) bcut_ = column_cuts(n_cols_, h_indices_);
 }
 
 // Store the edges block-major (per column block, rows in order).
@@ -258,13 +246,18 @@ void DevGraph::set_scales(std::vector<float> row_scale, std::vector<float> col_s
 static const int kLdsLaneGroups[4][4] = {{0, 3, 5, 6}, {1, 2, 4, 7}, {8, 11, 13, 14}, {9, 10, 12, 15}};
 
 int g_graphsum_lds = 1;
+int g_graphsum_lds_window = 1;  // diagnostics ("graphsum_lds_window"): 2 = two-slot runs (exec-masked; slower on gfx950)
 int g_graphsum_lds_order = 1;  // diagnostics ("graphsum_lds_order"): 0 = runs in column order  // diagnostics (pgcn_debug_set "graphsum_lds"): 0 disables the LDS path
 
-// LDS-staged d = 16 schedule (see k_graphsum_lds.hip for the layout it feeds).
-void DevGraph::build_lds() {
-  compute_cuts();
-  const int B = kBlocks, SR = LDS_SR, CW = LDS_CW, NS = LDS_SLOTS;
-  auto L = std::make_unique<LdsSched>();
+// LDS-staged d = 16 schedule (see k_graphsum_lds.hip for the layout it feeds), host side:
+// a pure function of the CSR pattern and the column cuts (tested on the CPU by
+// lds_emulate, which walks it the way the kernel does).
+LdsHost build_lds_host(int n_rows, int n_cols, const std::vector<int> &h_indptr_,
+                       const std::vector<int> &h_indices_, const std::vector<int> &bcut_,
+                       int window) {
+  (void)n_cols;
+  const int n_rows_ = n_rows;
+  const int B = kGraphBlocks, SR = LDS_SR, CW = LDS_CW, NS = LDS_SLOTS;
   // slices of each column block
   std::vector<int> nsl((size_t)B);
   int t_max = 1;
@@ -482,39 +475,243 @@ void DevGraph::build_lds() {
     }
     return kb_total;
   };
+  // Window 2: per slice the wave runs its 16 slots as runs J = 0..15 in which every lane
+  // group takes an edge of slot J or, once its slot-J edges are done, of slot J+1 (exec
+  // masks pick the accumulator); run J ends when slot J is drained everywhere.  The cost per
+  // slot is then about the max over groups of the per-group total instead of the sum over
+  // slots of per-slot maxima (the lockstep padding of window 1).
+  auto walk2 = [&](long long wg, int w, unsigned short *out_entries, uint64_t *out_masks) {
+    const int b = (int)(wg % B), bat = (int)(wg / B);
+    const int *rw = &rows[(size_t)(((long long)bat * CW + w) * NS) * 16];
+    int cur[LDS_SLOTS * 16], end[LDS_SLOTS * 16];
+    for (int k = 0; k < NS * 16; k++) {
+      const int r = rw[k];
+      if (r < 0) {
+        cur[k] = end[k] = 0;
+        continue;
+      }
+      const int *rb = &sidx[(size_t)h_indptr_[(size_t)r]], *re = &sidx[(size_t)h_indptr_[(size_t)r + 1]];
+      cur[k] = (int)(std::lower_bound(rb, re, bcut_[(size_t)b]) - sidx.data());
+      end[k] = h_indptr_[(size_t)r + 1];
+    }
+    // byres[j][g][res]: slice-local rows of slot j, group g with row % 4 == res
+    std::vector<std::vector<int>> byres((size_t)NS * 16 * 4);
+    std::vector<int> cnt((size_t)NS * 16);
+    auto lst = [&](int j, int g, int r) -> std::vector<int> & { return byres[((size_t)j * 16 + g) * 4 + r]; };
+    long long kb_total = 0;
+    for (int t = 0; t < nsl[(size_t)b]; t++) {
+      const int2 sc = slices[(size_t)b * t_max + t];
+      const int c1 = sc.x + sc.y;
+      for (int j = 0; j < NS; j++)
+        for (int g = 0; g < 16; g++) {
+          const int k = j * 16 + g;
+          int e = cur[k];
+          for (int r = 0; r < 4; r++) lst(j, g, r).clear();
+          while (e < end[k] && sidx[(size_t)e] < c1) {
+            const int lr = sidx[(size_t)e] - sc.x;
+            lst(j, g, lr & 3).push_back(lr);
+            e++;
+          }
+          cnt[(size_t)k] = e - cur[k];
+          cur[k] = e;
+        }
+      auto drained = [&](int j) {
+        for (int g = 0; g < 16; g++)
+          if (cnt[(size_t)j * 16 + g]) return false;
+        return true;
+      };
+      int nblk[LDS_SLOTS] = {0};
+      int J = 0;
+      while (J < NS && drained(J)) J++;
+      while (J < NS) {
+        for (int st = 0; st < 4; st++) {
+          uint64_t m = 0;
+          for (int q = 0; q < 4; q++) {
+            const int *grp = kLdsLaneGroups[q];
+            int ord[4] = {0, 1, 2, 3};
+            std::sort(ord, ord + 4, [&](int x, int y) {
+              return cnt[(size_t)J * 16 + grp[x]] > cnt[(size_t)J * 16 + grp[y]];
+            });
+            int used = 0;
+            for (int oi = 0; oi < 4; oi++) {
+              const int g = grp[ord[oi]];
+              int slot = -1, res = -1;
+              for (int jj = J; jj <= std::min(J + 1, NS - 1) && slot < 0; jj++) {
+                if (!cnt[(size_t)jj * 16 + g]) continue;
+                for (int r = 0; r < 4; r++)  // a free bank quarter, the fullest list
+                  if (!(used >> r & 1) && !lst(jj, g, r).empty() &&
+                      (res < 0 || lst(jj, g, r).size() > lst(jj, g, res).size()))
+                    res = r;
+                if (res < 0)  // forced conflict: the fullest list
+                  for (int r = 0; r < 4; r++)
+                    if (!lst(jj, g, r).empty() && (res < 0 || lst(jj, g, r).size() > lst(jj, g, res).size()))
+                      res = r;
+                slot = jj;
+              }
+              int val;
+              if (slot >= 0) {
+                val = lst(slot, g, res).back() * 64;
+                lst(slot, g, res).pop_back();
+                cnt[(size_t)slot * 16 + g]--;
+                if (slot != J) m |= 0xfull << (4 * g);
+              } else {  // padding: a zero row of a free quarter
+                res = 0;
+                while (used >> res & 1) res++;
+                val = (SR + res) * 64;
+              }
+              used |= 1 << res;
+              if (out_entries) out_entries[(size_t)kb_total * 64 + g * 4 + st] = (unsigned short)val;
+            }
+          }
+          if (out_masks) out_masks[(size_t)kb_total * 4 + st] = m;
+        }
+        nblk[J]++;
+        kb_total++;
+        while (J < NS && drained(J)) J++;
+      }
+      for (int j = 0; j < NS; j++) {
+        PGCN_CHECK(nblk[j] < 65536, PGCN_E_INVALID, "graphsum_lds: run too long");
+        counts[(size_t)(((wg * t_max + t) * CW + w) * NS + j)] = (unsigned short)nblk[j];
+      }
+    }
+    return kb_total;
+  };
+  const bool win2 = window == 2;
   parallel_for(n_wg * CW, [&](long long a, long long e) {
-    for (long long x = a; x < e; x++) kbs[(size_t)x] = walk(x / CW, (int)(x % CW), nullptr);
+    for (long long x = a; x < e; x++)
+      kbs[(size_t)x] = win2 ? walk2(x / CW, (int)(x % CW), nullptr, nullptr)
+                            : walk(x / CW, (int)(x % CW), nullptr);
   }, 0, 64);
   std::vector<long long> off((size_t)n_wg * CW + 1, 0);
   for (size_t x = 0; x < kbs.size(); x++) off[x + 1] = off[x] + kbs[x];
   const long long total_kb = off.back();
   std::vector<unsigned short> ent((size_t)std::max<long long>(total_kb, 1) * 64, 0);
+  std::vector<uint64_t> msk(win2 ? (size_t)std::max<long long>(total_kb, 1) * 4 : 0, 0);
   parallel_for(n_wg * CW, [&](long long a, long long e) {
-    for (long long x = a; x < e; x++) walk(x / CW, (int)(x % CW), &ent[(size_t)off[(size_t)x] * 64]);
+    for (long long x = a; x < e; x++) {
+      if (win2)
+        walk2(x / CW, (int)(x % CW), &ent[(size_t)off[(size_t)x] * 64], &msk[(size_t)off[(size_t)x] * 4]);
+      else
+        walk(x / CW, (int)(x % CW), &ent[(size_t)off[(size_t)x] * 64]);
+    }
   }, 0, 64);
+  LdsHost h;
+  h.window = win2 ? 2 : 1;
+  h.n_batches = nbat;
+  h.t_max = t_max;
+  h.nsl = std::move(nsl);
+  h.slices = std::move(slices);
+  h.rows = std::move(rows);
+  h.counts = std::move(counts);
+  h.wave_off = std::move(off);
+  h.entries = std::move(ent);
+  h.masks = std::move(msk);
+  return h;
+}
+
+
+// Walks a schedule exactly as k_graphsum_lds consumes it (entry blocks in wave order, runs
+// per slice and slot, window-2 masks, zero rows) and adds each row's sum of in[col] into
+// out[row]; throws on any inconsistency the kernel would turn into a wrong sum.
+void lds_emulate(const LdsHost &h, int n_rows, const float *in, double *out) {
+  const int B = kGraphBlocks, CW = LDS_CW, NS = LDS_SLOTS;
+  const long long n_wg = (long long)h.n_batches * B;
+  std::vector<double> acc((size_t)NS * 16);
+  for (long long wg = 0; wg < n_wg; wg++) {
+    const int b = (int)(wg % B), bat = (int)(wg / B);
+    for (int w = 0; w < CW; w++) {
+      long long kb = h.wave_off[(size_t)(wg * CW + w)];
+      std::fill(acc.begin(), acc.end(), 0.0);
+      for (int t = 0; t < h.nsl[(size_t)b]; t++) {
+        const int2 sc = h.slices[(size_t)b * h.t_max + t];
+        for (int j = 0; j < NS; j++) {
+          const int n = h.counts[(size_t)(((wg * h.t_max + t) * CW + w) * NS + j)];
+          const int nblk = h.window == 2 ? n : (n + 3) / 4;
+          for (int k = 0; k < nblk; k++, kb++) {
+            for (int st = 0; st < 4; st++) {
+              const uint64_t m = h.window == 2 ? h.masks[(size_t)kb * 4 + st] : 0;
+              for (int g = 0; g < 16; g++) {
+                const int e = h.entries[(size_t)kb * 64 + g * 4 + st];
+                PGCN_CHECK(e % 64 == 0, PGCN_E_INVALID, "lds schedule: entry not a row offset");
+                const int row = e / 64;
+                PGCN_CHECK(row >= LDS_SR || row < sc.y, PGCN_E_INVALID,
+                           "lds schedule: entry past the slice");
+                const unsigned q = (unsigned)(m >> (4 * g)) & 0xfu;
+                PGCN_CHECK(q == 0 || q == 0xfu, PGCN_E_INVALID, "lds schedule: split lane group");
+                const int slot = q ? j + 1 : j;
+                PGCN_CHECK(slot < NS, PGCN_E_INVALID, "lds schedule: mask past the last slot");
+                if (row < LDS_SR) acc[(size_t)slot * 16 + g] += (double)in[sc.x + row];
+              }
+            }
+          }
+        }
+      }
+      PGCN_CHECK(kb == h.wave_off[(size_t)(wg * CW + w) + 1], PGCN_E_INVALID,
+                 "lds schedule: wave stream length");
+      for (int j = 0; j < NS; j++)
+        for (int g = 0; g < 16; g++) {
+          const int r = h.rows[(size_t)(((long long)bat * CW + w) * NS + j) * 16 + g];
+          if (r >= 0) {
+            PGCN_CHECK(r < n_rows, PGCN_E_INVALID, "lds schedule: row id");
+            out[r] += acc[(size_t)j * 16 + g];
+          } else {
+            PGCN_CHECK(acc[(size_t)j * 16 + g] == 0.0, PGCN_E_INVALID,
+                       "lds schedule: edges on an empty slot");
+          }
+        }
+    }
+  }
+}
+
+std::vector<int> column_cuts(int n_cols, const std::vector<int> &indices) {
+  const int B = kGraphBlocks;
+  const long long nnz = (long long)indices.size();
+  std::vector<long long> colcnt((size_t)n_cols + 1, 0);
+  for (long long k = 0; k < nnz; k++) colcnt[(size_t)indices[(size_t)k] + 1]++;
+  for (int c = 0; c < n_cols; c++) colcnt[(size_t)c + 1] += colcnt[(size_t)c];
+  std::vector<int> cut((size_t)B + 1, 0);
+  cut[(size_t)B] = n_cols;
+  for (int b = 1; b < B; b++) {
+    const long long target = (long long)((double)nnz * b / B);
+    int c = (int)(std::lower_bound(colcnt.begin(), colcnt.end(), target) - colcnt.begin());
+    c = std::max(c, cut[(size_t)b - 1]);
+    cut[(size_t)b] = std::min(c, n_cols);
+  }
+  return cut;
+}
+
+void DevGraph::build_lds() {
+  compute_cuts();
+  auto L = std::make_unique<LdsSched>();
+  LdsHost h = build_lds_host(n_rows_, n_cols_, h_indptr_, h_indices_, bcut_, g_graphsum_lds_window);
+  const bool win2 = h.window == 2;
   // + 1 KB slack: ring refills read whole 512-B chunks past a wave's last entry block
-  L->entries.allocate(ent.size() / 4 + 128);
-  L->entries.upload(reinterpret_cast<const uint2 *>(ent.data()), ent.size() / 4);
-  L->wave_off.allocate(off.size());
-  L->wave_off.upload(off);
-  L->counts.allocate(counts.size());
-  L->counts.upload(counts);
-  L->slices.allocate(slices.size());
-  L->slices.upload(slices);
-  L->n_slices.allocate(nsl.size());
-  L->n_slices.upload(nsl);
-  L->rows.allocate(rows.size());
-  L->rows.upload(rows);
+  L->entries.allocate(h.entries.size() / 4 + 128);
+  L->entries.upload(reinterpret_cast<const uint2 *>(h.entries.data()), h.entries.size() / 4);
+  if (win2) {  // + 64 B of slack: the mask loads touch the line after the last block's
+    L->masks.allocate(h.masks.size() + 8);
+    L->masks.upload(h.masks);
+  }
+  L->wave_off.allocate(h.wave_off.size());
+  L->wave_off.upload(h.wave_off);
+  L->counts.allocate(h.counts.size());
+  L->counts.upload(h.counts);
+  L->slices.allocate(h.slices.size());
+  L->slices.upload(h.slices);
+  L->n_slices.allocate(h.nsl.size());
+  L->n_slices.upload(h.nsl);
+  L->rows.allocate(h.rows.size());
+  L->rows.upload(h.rows);
   L->row_scale.allocate(h_row_scale_.size());
   L->row_scale.upload(h_row_scale_);
   L->col_scale.allocate(h_col_scale_.size());
   L->col_scale.upload(h_col_scale_);
   L->scratch.allocate((size_t)n_cols_ * 16 + 64);
-  L->partial.allocate((size_t)B * n_rows_ * 16);
+  L->partial.allocate((size_t)kBlocks * n_rows_ * 16);
   L->s.n_rows = n_rows_;
   L->s.n_cols = n_cols_;
-  L->s.n_batches = nbat;
-  L->s.t_max = t_max;
+  L->s.n_batches = h.n_batches;
+  L->s.t_max = h.t_max;
   L->s.entries = L->entries.get();
   L->s.wave_off = L->wave_off.get();
   L->s.counts = L->counts.get();
@@ -523,6 +720,8 @@ void DevGraph::build_lds() {
   L->s.rows = L->rows.get();
   L->s.row_scale = L->row_scale.get();
   L->s.col_scale = L->col_scale.get();
+  L->s.window = win2 ? 2 : 1;
+  L->s.masks = win2 ? L->masks.get() : nullptr;
   lds_ = std::move(L);
 }
 

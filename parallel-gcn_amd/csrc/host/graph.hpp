@@ -35,6 +35,25 @@ void parallel_for(long long n, const std::function<void(long long, long long)> &
 // s[i] = 1/sqrt(deg_i) with deg = row length of the (symmetric) CSR: Â = D^-1/2 A D^-1/2.
 std::vector<float> degree_scales(int n, const int *indptr);
 
+// Host image of the d = 16 LDS schedule (k_graphsum_lds.hip), before upload.
+struct LdsHost {
+  int window = 1, n_batches = 0, t_max = 0;
+  std::vector<int> nsl;                 // slices per column block
+  std::vector<int2> slices;             // [block][t_max] {first column, rows}
+  std::vector<int> rows;                // [batch][LDS_CW][LDS_SLOTS][16]
+  std::vector<unsigned short> counts;   // [wg][t_max][LDS_CW][LDS_SLOTS]
+  std::vector<long long> wave_off;      // [wg*LDS_CW + 1] entry-block offsets
+  std::vector<unsigned short> entries;  // [kb][16 groups][4 steps] byte offsets
+  std::vector<uint64_t> masks;          // window 2: [kb][4 steps] lane masks
+};
+// nnz-balanced column cuts (kGraphBlocks + 1 boundaries)
+std::vector<int> column_cuts(int n_cols, const std::vector<int> &indices);
+LdsHost build_lds_host(int n_rows, int n_cols, const std::vector<int> &indptr,
+                       const std::vector<int> &indices, const std::vector<int> &bcut, int window);
+// CPU walk of the schedule as the kernel consumes it: out[row] += sum of in[col] (throws on
+// an inconsistent schedule)
+void lds_emulate(const LdsHost &h, int n_rows, const float *in, double *out);
+
 class DevGraph {
  public:
   // CSR with n_rows rows and column ids < n_cols; `vals` aligned with `indices`.
@@ -70,6 +89,7 @@ class DevGraph {
   struct LdsSched {
     LdsSchedule s;
     DeviceBuffer<uint2> entries;
+    DeviceBuffer<uint64_t> masks;
     DeviceBuffer<long long> wave_off;
     DeviceBuffer<unsigned short> counts;
     DeviceBuffer<int2> slices;

@@ -77,6 +77,58 @@ __device__ __forceinline__ void glds16(const void *gsrc, unsigned lds_dst) {
       : "memory");
 }
 
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+// Window-2 step: lanes in `m` (slot J+1) add x into acc1, the others (slot J, or a padding
+// zero row) into acc0.  Exec is set by hand around four packed adds (the summing waves run
+// with all 64 lanes active, so exec is restored to all ones).
+__device__ __forceinline__ void win_add(f2v &a0l, f2v &a0h, f2v &a1l, f2v &a1h, const f4v &x,
+                                        uint64_t m) {
+  const f2v xl = __builtin_shufflevector(x, x, 0, 1), xh = __builtin_shufflevector(x, x, 2, 3);
+  asm volatile(
+      "s_mov_b64 exec, %[m]\n\t"
+      "v_pk_add_f32 %[a1l], %[a1l], %[xl]\n\t"
+      "v_pk_add_f32 %[a1h], %[a1h], %[xh]\n\t"
+      "s_not_b64 exec, %[m]\n\t"
+      "v_pk_add_f32 %[a0l], %[a0l], %[xl]\n\t"
+      "v_pk_add_f32 %[a0h], %[a0h], %[xh]\n\t"
+      "s_mov_b64 exec, -1"
+      : [a0l] "+v"(a0l), [a0h] "+v"(a0h), [a1l] "+v"(a1l), [a1h] "+v"(a1h)
+      : [m] "s"(m), [xl] "v"(xl), [xh] "v"(xh)
+      : "scc");  // s_not_b64 writes SCC (the loop branches on it)
+}
+
+// The 4 step masks of one entry block (32 B at p, uniform) into SGPRs.  A scalar load issued
+// from inline asm (the kernel's asm memory clobbers would otherwise turn a plain uniform load
+// into a vector load that upsets the hand-counted vmcnt of the entry ring); it waits for
+// itself (lgkmcnt(0): call it when no LDS read is outstanding) and touches the line two
+// blocks ahead, so the next loads hit the scalar cache.
+typedef unsigned u32x8 __attribute__((ext_vector_type(8)));
+template <bool g_touch>
+__device__ __forceinline__ void load_masks(const uint64_t *p, uint64_t (&m)[4]) {
+  u32x8 v;
+  unsigned touch;
+  if (g_touch)
+    asm volatile(
+        "s_load_dwordx8 %0, %2, 0x0\n\t"
+        "s_load_dword %1, %2, 0x40\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&s"(v), "=&s"(touch)
+        : "s"(p)
+        : "memory");
+  else
+    asm volatile(
+        "s_load_dwordx8 %0, %1, 0x0\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&s"(v)
+        : "s"(p)
+        : "memory");
+  (void)touch;
+#pragma unroll
+  for (int s = 0; s < 4; s++) m[s] = (uint64_t)v[2 * s] | ((uint64_t)v[2 * s + 1] << 32);
+}
+
 constexpr int LDS_TABLE_F4 = 2 * LDS_ROWS * 4;       // two slice buffers (float4 units)
 constexpr int LDS_RING_CHUNK = 512;                  // bytes: 4 entry blocks of 128 B
 constexpr int LDS_RING_SLOTS = 4;                    // chunks per wave: 3 in flight + 1 read
@@ -96,9 +148,10 @@ constexpr int LDS_TOTAL_F4 = LDS_RING_F4 + LDS_CW * LDS_RING_BYTES / 16;
 //   0 loop cycles, 1 barrier-wait cycles, 2 ring-wait cycles, 3 entry blocks, 4 slices
 __device__ __forceinline__ unsigned long long clk() { return __builtin_amdgcn_s_memtime(); }
 
-template <int DIAG>
+template <int DIAG, int WIN>
 __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
-    const uint2 *__restrict__ entries, const long long *__restrict__ wave_off,
+    const uint2 *__restrict__ entries, const uint64_t *__restrict__ masks,
+    const long long *__restrict__ wave_off,
     const unsigned short *__restrict__ counts, int t_max, const int2 *__restrict__ slices,
     const int *__restrict__ n_slices, const int *__restrict__ rows, const float4 *__restrict__ in,
     int n_cols, float4 *__restrict__ partial, long long part_stride,
@@ -205,6 +258,74 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
   __builtin_amdgcn_s_barrier();                       // slice 0 staged
   asm volatile("" ::: "memory");
   if constexpr (DIAG == 4) st_loop = clk();
+  // next entry block of the ring (and its refill when a chunk is entered)
+  auto next_block = [&]() {
+    roff = (roff + 128) & (LDS_RING_BYTES - 1);
+    if ((roff & (LDS_RING_CHUNK - 1)) == 0) {  // entering the next chunk: refill the slot
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read before, wait for it
+      ++chunk;
+      refill(chunk + 3);
+      unsigned long long c0 = 0;
+      if constexpr (DIAG == 4) c0 = clk();
+      asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      if constexpr (DIAG == 4) st_ring += clk() - c0;
+    }
+    e_next = *reinterpret_cast<const uint2 *>(ring + roff);  // (past the end: unused)
+  };
+  if constexpr (WIN == 2) {
+    // accumulators as packed halves (v_pk_add_f32 operands)
+    f2v al[LDS_SLOTS], ah[LDS_SLOTS];
+#pragma unroll
+    for (int j = 0; j < LDS_SLOTS; j++) al[j] = ah[j] = f2v{0.f, 0.f};
+    // this wave's per-step lane masks (uniform: scalar loads)
+    const uint64_t *mk = masks + kb0 * 4;
+    for (int t = 0; t < T; t++) {
+      const char *tb = reinterpret_cast<const char *>(lds + (t & 1) * LDS_ROWS * 4 + v);
+      const uint4 *c4 = reinterpret_cast<const uint4 *>(
+          reinterpret_cast<const char *>(lds + LDS_TABLE_F4) + (t & 1) * LDS_CNT_BYTES + wave * 32);
+      const uint4 cw0 = c4[0], cw1 = c4[1];
+      const unsigned cw[8] = {
+          (unsigned)__builtin_amdgcn_readfirstlane(cw0.x), (unsigned)__builtin_amdgcn_readfirstlane(cw0.y),
+          (unsigned)__builtin_amdgcn_readfirstlane(cw0.z), (unsigned)__builtin_amdgcn_readfirstlane(cw0.w),
+          (unsigned)__builtin_amdgcn_readfirstlane(cw1.x), (unsigned)__builtin_amdgcn_readfirstlane(cw1.y),
+          (unsigned)__builtin_amdgcn_readfirstlane(cw1.z), (unsigned)__builtin_amdgcn_readfirstlane(cw1.w)};
+#pragma unroll
+      for (int j = 0; j < LDS_SLOTS; j++) {
+        const int n = (cw[j >> 1] >> (16 * (j & 1))) & 0xffff;  // entry blocks of run j
+        for (int k = 0; k < n; k++) {
+          const uint2 e = e_next;
+          uint64_t m[4];
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (e_next has landed anyway)
+          load_masks<DIAG != 6>(mk, m);
+          mk += 4;
+          next_block();
+          const f4v x0 = *reinterpret_cast<const f4v *>(tb + (e.x & 0xffffu));
+          const f4v x1 = *reinterpret_cast<const f4v *>(tb + (e.x >> 16));
+          const f4v x2 = *reinterpret_cast<const f4v *>(tb + (e.y & 0xffffu));
+          const f4v x3 = *reinterpret_cast<const f4v *>(tb + (e.y >> 16));
+          if (j + 1 < LDS_SLOTS) {
+            win_add(al[j], ah[j], al[j + 1], ah[j + 1], x0, m[0]);
+            win_add(al[j], ah[j], al[j + 1], ah[j + 1], x1, m[1]);
+            win_add(al[j], ah[j], al[j + 1], ah[j + 1], x2, m[2]);
+            win_add(al[j], ah[j], al[j + 1], ah[j + 1], x3, m[3]);
+          } else {  // the last slot has no successor: all lanes add into it
+            al[j] += __builtin_shufflevector(x0, x0, 0, 1) + __builtin_shufflevector(x1, x1, 0, 1) +
+                     __builtin_shufflevector(x2, x2, 0, 1) + __builtin_shufflevector(x3, x3, 0, 1);
+            ah[j] += __builtin_shufflevector(x0, x0, 2, 3) + __builtin_shufflevector(x1, x1, 2, 3) +
+                     __builtin_shufflevector(x2, x2, 2, 3) + __builtin_shufflevector(x3, x3, 2, 3);
+          }
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      unsigned long long cb = 0;
+      if constexpr (DIAG == 4) cb = clk();
+      __builtin_amdgcn_s_barrier();  // slice t summed; slice t+1 staged
+      asm volatile("" ::: "memory");
+      if constexpr (DIAG == 4) st_bar += clk() - cb;
+    }
+#pragma unroll
+    for (int j = 0; j < LDS_SLOTS; j++) acc[j] = make_float4(al[j].x, al[j].y, ah[j].x, ah[j].y);
+  } else {
   for (int t = 0; t < T; t++) {
     // edge entries are byte offsets of slice rows: address = entry + (buffer base + 16 v)
     const char *tb = reinterpret_cast<const char *>(lds + (t & 1) * LDS_ROWS * 4 + v);
@@ -222,17 +343,7 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
       const int n = (cw[j >> 1] >> (16 * (j & 1))) & 0xffff;  // steps of rowset j
       for (int k = 0; k < n; k += 4) {
         const uint2 e = e_next;
-        roff = (roff + 128) & (LDS_RING_BYTES - 1);
-        if ((roff & (LDS_RING_CHUNK - 1)) == 0) {  // entering the next chunk: refill the slot
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read before, wait for it
-          ++chunk;
-          refill(chunk + 3);
-          unsigned long long c0 = 0;
-          if constexpr (DIAG == 4) c0 = clk();
-          asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-          if constexpr (DIAG == 4) st_ring += clk() - c0;
-        }
-        e_next = *reinterpret_cast<const uint2 *>(ring + roff);  // (past the end: unused)
+        next_block();
         // all 4 entries are valid: steps past a row's run point at a zero row
         if constexpr (DIAG == 2) {  // diagnostic: no table reads
           acc[j].x += __uint_as_float(e.x);
@@ -262,6 +373,7 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
     __builtin_amdgcn_s_barrier();  // slice t summed; slice t+1 staged
     asm volatile("" ::: "memory");
     if constexpr (DIAG == 4) st_bar += clk() - cb;
+  }
   }
   if constexpr (DIAG == 4) {
     st_loop = clk() - st_loop;
@@ -332,18 +444,25 @@ void launch_graphsum_lds(const LdsSchedule &s, const float *in, int ld_in, float
   hipLaunchKernelGGL(k_gs_prescale, dim3((unsigned)ceil_div(pre, 256)), dim3(256), 0, st,
                      reinterpret_cast<const float4 *>(in), ld_in / 4, s.col_scale, s.n_cols,
                      reinterpret_cast<float4 *>(scratch_in));
-#define GS_LDS(D)                                                                           \
-  hipLaunchKernelGGL(k_graphsum_lds<D>, dim3((unsigned)(s.n_batches * kGraphBlocks)),          \
-                     dim3(LDS_THREADS), 0, st, s.entries, s.wave_off, s.counts, s.t_max,        \
-                     s.slices, s.n_slices, s.rows, reinterpret_cast<const float4 *>(scratch_in), \
-                     s.n_cols, reinterpret_cast<float4 *>(partial), (long long)s.n_rows,          \
+#define GS_LDS(D, W)                                                                        \
+  hipLaunchKernelGGL((k_graphsum_lds<D, W>), dim3((unsigned)(s.n_batches * kGraphBlocks)),     \
+                     dim3(LDS_THREADS), 0, st, s.entries, s.masks, s.wave_off, s.counts,        \
+                     s.t_max, s.slices, s.n_slices, s.rows,                                    \
+                     reinterpret_cast<const float4 *>(scratch_in), s.n_cols,                   \
+                     reinterpret_cast<float4 *>(partial), (long long)s.n_rows,                 \
                      lds_stamps(s.n_batches * kGraphBlocks))
-  switch (g_graphsum_lds_diag) {
-    case 1: GS_LDS(1); break;
-    case 2: GS_LDS(2); break;
-    case 3: GS_LDS(3); break;
-    case 4: GS_LDS(4); break;
-    default: GS_LDS(0); break;
+  if (s.window == 2) {
+    if (g_graphsum_lds_diag == 4) GS_LDS(4, 2);
+    else if (g_graphsum_lds_diag == 6) GS_LDS(6, 2);  // no next-line touch
+    else GS_LDS(0, 2);
+  } else {
+    switch (g_graphsum_lds_diag) {
+      case 1: GS_LDS(1, 1); break;
+      case 2: GS_LDS(2, 1); break;
+      case 3: GS_LDS(3, 1); break;
+      case 4: GS_LDS(4, 1); break;
+      default: GS_LDS(0, 1); break;
+    }
   }
 #undef GS_LDS
   const long long post = (long long)s.n_rows * 4;

@@ -48,6 +48,10 @@ struct LdsSchedule {
   const int *rows = nullptr;                 // [batch][LDS_CW][LDS_SLOTS][16] row or -1
   const float *row_scale = nullptr;          // 1/sqrt(deg) of output rows
   const float *col_scale = nullptr;          // 1/sqrt(deg) of input rows
+  // window 2: counts are per window base J; per entry block 4 lane masks (one per step) of
+  // the lanes whose edge belongs to slot J+1 (the others add into slot J)
+  int window = 1;
+  const uint64_t *masks = nullptr;           // [kb][4]
 };
 void launch_graphsum_lds(const LdsSchedule &s, const float *in, int ld_in, float *out,
                          int ld_out, float *scratch_in, float *partial, hipStream_t st);

@@ -183,3 +183,44 @@ def test_synthetic_generator_properties(pgcn):
     assert np.array_equal(a.feat_indptr, np.arange(n + 1) * f)
     other = pgcn.Dataset.synthetic(n, f, c, e, seed=8)
     assert not np.array_equal(other.graph_indices[:1000], ix[:1000])
+
+
+def _lds_check(pgcn, ip, ix, n, window):
+    err, nb = ctypes.c_double(), ctypes.c_longlong()
+    pgcn.check(pgcn.lib.pgcn_debug_lds_check(n, n, helpers.ptr(ip), helpers.ptr(ix), window,
+                                             ctypes.byref(err), ctypes.byref(nb)), "lds_check")
+    return err.value, nb.value
+
+
+@pytest.mark.parametrize("window", [1, 2])
+def test_lds_schedule_walk_sums_every_edge(pgcn, window):
+    """The d = 16 LDS GraphSum schedule, walked on the CPU exactly as k_graphsum_lds consumes
+    it (entry blocks, per-slice runs, window-2 lane masks, zero rows), reproduces every row's
+    CSR sum; window 2 needs fewer entry blocks than window 1 on a power-law graph."""
+    ds = pgcn.Dataset.synthetic(70000, 8, 4, 2000000, 1)
+    ip = np.ascontiguousarray(ds.graph_indptr)
+    ix = np.ascontiguousarray(ds.graph_indices)
+    err, nb = _lds_check(pgcn, ip, ix, ds.num_nodes, window)
+    assert err < 1e-12
+    if window == 2:
+        _, nb1 = _lds_check(pgcn, ip, ix, ds.num_nodes, 1)
+        assert nb < 0.8 * nb1
+
+
+def test_lds_schedule_ragged_graph(pgcn):
+    """Isolated rows, a hub adjacent to everything, duplicate edges: both windows stay exact."""
+    rng = np.random.default_rng(5)
+    n = 5000
+    rows = [[] for _ in range(n)]
+    for i in range(n):
+        if i % 7 == 0:  # every 7th row empty
+            continue
+        k = int(rng.integers(1, 40))
+        rows[i] = sorted(rng.integers(0, n, k).tolist())  # duplicates kept
+    rows[1] = list(range(n))  # hub
+    ip = np.zeros(n + 1, np.int32)
+    ip[1:] = np.cumsum([len(r) for r in rows])
+    ix = np.ascontiguousarray(np.concatenate([np.array(r, np.int32) for r in rows if r]))
+    for window in (1, 2):
+        err, _ = _lds_check(pgcn, ip, ix, n, window)
+        assert err < 1e-12

@@ -77,8 +77,12 @@ def abs_bound(indptr, indices, x, dim):
     (5000, 8, 3, 2),         # pubmed-like C = 3
     (5000, 8, 7, 2),         # cora C = 7
     (20000, 10, 128, 3),     # 4-layer hidden 128
+    (120000, 40, 16, -2),    # LDS path, window-2 schedule (two-slot runs, exec-masked adds)
 ])
 def test_graphsum_vs_oracle(pgcn, n, deg, dim, hubs):
+    window = 2 if hubs < 0 else 1
+    hubs = abs(hubs)
+    pgcn.lib.pgcn_debug_set(b"graphsum_lds_window", window)  # schedules built from here on
     indptr, indices = random_graph(n, deg, seed=n + dim, hubs=hubs, hub_deg=3000)
     ld = (dim + 3) // 4 * 4
     rng = np.random.default_rng(7)
@@ -104,6 +108,7 @@ def test_graphsum_vs_oracle(pgcn, n, deg, dim, hubs):
     torch.cuda.synchronize()
     assert torch.equal(out, out2)
     pgcn.lib.pgcn_graph_destroy(g)
+    pgcn.lib.pgcn_debug_set(b"graphsum_lds_window", 1)
 
 
 def test_graphsum_linearity_large(pgcn):

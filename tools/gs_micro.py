@@ -83,6 +83,20 @@ t1 = time.time()
 o_lds = run_once()
 res["lds_build_plus_first_call_s"] = time.time() - t1
 res["d16_lds_ms"] = timeit(g, 16)
+
+# window 2 (two-slot runs, exec-masked adds) on a fresh graph
+pg.lib.pgcn_debug_set(b"graphsum_lds_window", 2)
+g2 = make_graph()
+o_w2 = torch.empty(n, ld, device="cuda")
+pg.check(pg.lib.pgcn_graphsum(g2, ctypes.c_void_p(x.data_ptr()), ld,
+                              ctypes.c_void_p(o_w2.data_ptr()), ld, 16, st), "gs")
+torch.cuda.synchronize()
+res["d16_lds_window2_ms"] = timeit(g2, 16)
+pg.lib.pgcn_debug_set(b"graphsum_lds_diag", 6)
+res["d16_lds_window2_notouch_ms"] = timeit(g2, 16)
+pg.lib.pgcn_debug_set(b"graphsum_lds_diag", 0)
+res["window2_vs_window1_max_rel"] = ((o_w2 - o_lds).abs().max() / o_lds.abs().max()).item()
+pg.lib.pgcn_debug_set(b"graphsum_lds_window", 1)
 for dg, name in ((1, "stage1of16"), (2, "noreads"), (3, "oneadd")):
     pg.lib.pgcn_debug_set(b"graphsum_lds_diag", dg)
     res[f"d16_lds_{name}_ms"] = timeit(g, 16)
