@@ -96,6 +96,8 @@ def main():
     ap.add_argument("--workload", default="reddit-114M", choices=sorted(WORKLOADS))
     ap.add_argument("--cpu-epochs", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--edge-cut", action="store_true",
+                    help="one GPU through the multi-GPU engine (partition, RCCL at world 1)")
     ap.add_argument("--profile-only", action="store_true",
                     help="only run warmup+steps (for rocprofv3), no JSON extras")
     args = ap.parse_args()
@@ -124,6 +126,9 @@ def main():
         uid = [pgcn.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         g = pgcn.GCN(params, ds, device=local_rank, rank=rank, world=world, unique_id=uid[0])
+    elif args.edge_cut:
+        g = pgcn.GCN(params, ds, device=local_rank, rank=0, world=1,
+                     unique_id=pgcn.comm_unique_id())
     else:
         g = pgcn.GCN(params, ds, device=local_rank)
     t_build = time.perf_counter() - t_build
@@ -186,7 +191,8 @@ def main():
         "config": {"workload": f"{args.workload} 2-layer GCN hidden=16 dropout=0.5 Adam",
                    "nodes": N_NODES, "features": N_FEAT, "classes": N_CLASS,
                    "adjacency_nnz": int(ds.graph_indptr[-1]),
-                   "parallelism": f"edge-cut x{world}" if world > 1 else "single GPU",
+                   "parallelism": (f"edge-cut x{world}" if world > 1 or args.edge_cut
+                                   else "single GPU"),
                    "step": "train_epoch + eval(2)"},
         "roofline": {"kernel": "graphsum", "bound": "hbm", "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,

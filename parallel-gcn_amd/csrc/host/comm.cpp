@@ -16,12 +16,14 @@ int Partition::owner(int node) const {
   return (int)(std::upper_bound(bounds.begin(), bounds.end(), node) - bounds.begin()) - 1;
 }
 
-Partition make_partition(int n, const int *indptr, int world, int rank) {
+Partition make_partition(int n, const int *indptr, int world, int rank, int chunks) {
   PGCN_CHECK(world >= 1 && rank >= 0 && rank < world && n >= world, PGCN_E_INVALID,
              "partition: need 1 <= world <= n and 0 <= rank < world");
+  PGCN_CHECK(chunks >= 1, PGCN_E_INVALID, "partition: chunks >= 1");
   Partition p;
   p.world = world;
   p.rank = rank;
+  p.chunks = chunks;
   p.bounds.assign((size_t)world + 1, 0);
   p.bounds[(size_t)world] = n;
   const double total = (double)indptr[n];
@@ -36,7 +38,45 @@ Partition make_partition(int n, const int *indptr, int world, int rank) {
   }
   for (int r = 0; r < world; r++)
     p.maxrows = std::max(p.maxrows, p.bounds[(size_t)r + 1] - p.bounds[(size_t)r]);
+  p.maxrows = (p.maxrows + chunks - 1) / chunks * chunks;
   return p;
+}
+
+void partition_subgraph_chunk(const Partition &part, int n, const int *indptr,
+                              const int *indices, int k, std::vector<int> *sub_indptr,
+                              std::vector<int> *sub_indices) {
+  (void)n;
+  const int lo = part.first(), hi = part.last(), W = part.world, h = part.chunk_rows();
+  const long long rows = (long long)W * h;
+  std::vector<int> cnt((size_t)rows, 0);
+  auto node = [&](long long r) {  // chunk row -> global node (-1: padding)
+    const int q = (int)(r / h), j = (int)(r % h);
+    const int i = part.bounds[(size_t)q] + k * h + j;
+    return i < part.bounds[(size_t)q + 1] ? i : -1;
+  };
+  parallel_for(rows, [&](long long b, long long e) {
+    for (long long r = b; r < e; r++) {
+      const int i = node(r);
+      if (i < 0) continue;
+      int c = 0;
+      for (int t = indptr[i]; t < indptr[i + 1]; t++) c += (indices[t] >= lo && indices[t] < hi);
+      cnt[(size_t)r] = c;
+    }
+  });
+  sub_indptr->assign((size_t)rows + 1, 0);
+  for (long long r = 0; r < rows; r++) (*sub_indptr)[(size_t)r + 1] = (*sub_indptr)[(size_t)r] + cnt[(size_t)r];
+  sub_indices->assign((size_t)sub_indptr->back(), 0);
+  parallel_for(rows, [&](long long b, long long e) {
+    for (long long r = b; r < e; r++) {
+      const int i = node(r);
+      if (i < 0) continue;
+      long long o = (*sub_indptr)[(size_t)r];
+      for (int t = indptr[i]; t < indptr[i + 1]; t++) {
+        const int j = indices[t];
+        if (j >= lo && j < hi) (*sub_indices)[(size_t)o++] = j - lo;
+      }
+    }
+  });
 }
 
 void partition_subgraph(const Partition &part, int n, const int *indptr, const int *indices,

@@ -19,14 +19,25 @@ struct Partition {
   int world = 1, rank = 0;
   std::vector<int> bounds;  // world + 1 node boundaries
   int maxrows = 0;          // padded rows per rank (equal reduce-scatter counts)
+  int chunks = 1;           // reduce-scatter row chunks (maxrows is a multiple of chunks)
+  int chunk_rows() const { return maxrows / chunks; }
   int first() const { return bounds[rank]; }
   int last() const { return bounds[rank + 1]; }
   int local_rows() const { return last() - first(); }
   int owner(int node) const;
 };
 
-// contiguous nnz-balanced ranges (every rank gets >= 1 node)
-Partition make_partition(int n, const int *indptr, int world, int rank);
+// contiguous nnz-balanced ranges (every rank gets >= 1 node); maxrows rounded up to a
+// multiple of `chunks`
+Partition make_partition(int n, const int *indptr, int world, int rank, int chunks = 1);
+
+// Chunk k of rank `part.rank`'s column block, rows in chunk-major padded order: row
+// q*h + j (h = chunk_rows()) is global node bounds[q] + k*h + j of owner q (no edges past the
+// owner's range).  Chunk k's reduce-scatter then hands rank q exactly its rows k*h .. k*h+h-1,
+// so the sum of chunk k can travel while chunk k+1 is computed.
+void partition_subgraph_chunk(const Partition &part, int n, const int *indptr,
+                              const int *indices, int k, std::vector<int> *sub_indptr,
+                              std::vector<int> *sub_indices);
 
 // Rank `part.rank`'s column block of Â in padded row layout: rows = world*maxrows (row of
 // global node i = owner(i)*maxrows + i - bounds[owner(i)]), columns = local node ids,

@@ -82,10 +82,13 @@ GCN::GCN(const GCNParams &params_, const AdamParams &adam, const GCNData &data, 
   PGCN_HIP(hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
   stream = Stream::create(hi_prio);  // the reference uses High priority streams
   const int world = dist ? dist->world : 1, rank = dist ? dist->rank : 0;
-  part = make_partition(params.num_nodes, data.graph.indptr.data(), world, rank);
+  part = make_partition(params.num_nodes, data.graph.indptr.data(), world, rank,
+                        dist ? kRsChunks : 1);
   if (dist) {  // the edge-cut path (also at world == 1, which exercises it on one GPU)
     comm = std::make_unique<Comm>(rank, world, dist->unique_id);
     ctx.comm = comm.get();
+    comm_stream = Stream::create(hi_prio);
+    ctx.comm_stream = comm_stream.get();
   }
   build(data);
 }
@@ -208,19 +211,40 @@ void GCN::build(const GCNData &data) {
   const int N = params.num_nodes;
   // adjacency
   if (comm) {
-    std::vector<int> sp, si;
-    std::vector<float> sv;
-    partition_subgraph(part, N, data.graph.indptr.data(), data.graph.indices.data(), &sp, &si, &sv);
-    graph = std::make_unique<DevGraph>(part.world * part.maxrows, part.local_rows(), sp.data(), si.data(), sv.data());
-    // vals = s_row * s_col with s = 1/sqrt(global degree): padded row q*maxrows + k is global
-    // row bounds[q] + k; local column c is global node first() + c
+    // one column block per reduce-scatter chunk (rows in chunk-major padded order,
+    // partition_subgraph_chunk); vals = s_row * s_col with s = 1/sqrt(global degree)
     const std::vector<float> sg = degree_scales(N, data.graph.indptr.data());
-    std::vector<float> rs((size_t)part.world * part.maxrows, 0.0f), cs((size_t)part.local_rows());
-    for (int q = 0; q < part.world; q++)
-      for (int i = part.bounds[(size_t)q]; i < part.bounds[(size_t)q + 1]; i++)
-        rs[(size_t)q * part.maxrows + (i - part.bounds[(size_t)q])] = sg[(size_t)i];
+    const int h = part.chunk_rows();
+    std::vector<float> cs((size_t)part.local_rows());
     for (int c = 0; c < part.local_rows(); c++) cs[(size_t)c] = sg[(size_t)part.first() + c];
-    graph->set_scales(std::move(rs), std::move(cs));
+    for (int k = 0; k < part.chunks; k++) {
+      std::vector<int> sp, si;
+      partition_subgraph_chunk(part, N, data.graph.indptr.data(), data.graph.indices.data(), k,
+                               &sp, &si);
+      std::vector<float> rs((size_t)part.world * h, 0.0f), sv(si.size());
+      for (int q = 0; q < part.world; q++)
+        for (int j = 0; j < h; j++) {
+          const int i = part.bounds[(size_t)q] + k * h + j;
+          if (i < part.bounds[(size_t)q + 1]) rs[(size_t)q * h + j] = sg[(size_t)i];
+        }
+      // the plain kernels' per-edge values: hpdga's coefficient (graph_coef), bit-exact
+      const int *ip = data.graph.indptr.data();
+      for (int q = 0; q < part.world; q++)
+        for (int j = 0; j < h; j++) {
+          const int i = part.bounds[(size_t)q] + k * h + j;
+          if (i >= part.bounds[(size_t)q + 1]) continue;
+          const size_t r = (size_t)q * h + j;
+          for (int t = sp[r]; t < sp[r + 1]; t++) {
+            const int gj = part.first() + si[(size_t)t];
+            sv[(size_t)t] = graph_coef(ip[i + 1] - ip[i], ip[gj + 1] - ip[gj]);
+          }
+        }
+      auto gk = std::make_unique<DevGraph>(part.world * h, part.local_rows(), sp.data(), si.data(),
+                                           sv.data());
+      gk->set_scales(std::move(rs), cs);
+      chunk_graphs.push_back(std::move(gk));
+    }
+    for (auto &gk : chunk_graphs) ctx.chunk_graphs.push_back(gk.get());
   } else {
     std::vector<float> v = graph_coefs(N, data.graph.indptr.data(), data.graph.indices.data());
     graph = std::make_unique<DevGraph>(N, N, data.graph.indptr.data(), data.graph.indices.data(),

@@ -19,6 +19,10 @@
 
 namespace pgcn {
 
+// GraphSum row chunks of the edge-cut engine: chunk k's reduce-scatter overlaps chunk k+1's
+// local sum (2: the LDS schedule keeps >= 1 workgroup per CU at 2 GPUs).
+constexpr int kRsChunks = 2;
+
 struct GCNParams {
   int num_nodes = 0, input_dim = 0, output_dim = 0;
   std::vector<int> hidden_dims = {16};
@@ -94,9 +98,11 @@ class GCN {
   Partition part;
   std::unique_ptr<Comm> comm;
   Stream stream;
+  Stream comm_stream;  // edge-cut: reduce-scatters run here, overlapping the next chunk's sum
   ModuleContext ctx;
 
-  std::unique_ptr<DevGraph> graph;
+  std::unique_ptr<DevGraph> graph;                    // one GPU: the whole Â
+  std::vector<std::unique_ptr<DevGraph>> chunk_graphs;  // edge-cut: Â's column block per RS chunk
   DevFeatures feats;
   DeviceBuffer<int> truth[4];
   int counts[4] = {0, 0, 0, 0};

@@ -107,8 +107,13 @@ GraphSum::GraphSum(shared_ptr<Variable> in_, shared_ptr<Variable> out_, DevGraph
                    int dim_, ModuleContext *ctx_)
     : in(std::move(in_)), out(std::move(out_)), graph(graph_), dim(dim_), ctx(ctx_) {
   if (ctx->comm) {
-    partial.allocate((size_t)graph->rows() * out->ld);
-    partial.zero();
+    for (DevGraph *gk : ctx->chunk_graphs) {
+      partial.emplace_back();
+      partial.back().allocate((size_t)gk->rows() * out->ld);
+      partial.back().zero();
+      computed.push_back(Event::create());
+    }
+    reduced = Event::create();
   }
 }
 
@@ -119,18 +124,32 @@ void GraphSum::run(const float *src, float *dst, const Stream &s) const {
     e1 = Event::create(true);
     e0.record(s.get());
   }
+  double bytes = 0;
   if (ctx->comm) {
-    // partial sums for every (padded) row from this rank's columns, then reduce-scatter
-    graph->graphsum(src, in->ld, partial.get(), out->ld, dim, s.get());
+    // Per row chunk: partial sums of the chunk's (padded) rows from this rank's columns on
+    // the compute stream, then its reduce-scatter on the comm stream, which hands every rank
+    // its own rows of the chunk while the next chunk is summed.
+    const size_t h = (size_t)out->rows / ctx->chunk_graphs.size();
+    for (size_t k = 0; k < ctx->chunk_graphs.size(); k++) {
+      DevGraph *gk = ctx->chunk_graphs[k];
+      gk->graphsum(src, in->ld, partial[k].get(), out->ld, dim, s.get());
+      bytes += gk->algorithmic_bytes(dim);
+      computed[k].record(s.get());
+      computed[k].wait_on(ctx->comm_stream);
+      ctx->comm->reduce_scatter_sum(partial[k].get(), dst + k * h * out->ld, h * out->ld,
+                                    ctx->comm_stream);
+    }
     if (ctx->profile) e1.record(s.get());
-    ctx->comm->reduce_scatter_sum(partial.get(), dst, (size_t)out->rows * out->ld, s.get());
+    reduced.record(ctx->comm_stream);
+    reduced.wait_on(s.get());  // dst complete, partials free for the next call
   } else {
     graph->graphsum(src, in->ld, dst, out->ld, dim, s.get());
+    bytes = graph->algorithmic_bytes(dim);
     if (ctx->profile) e1.record(s.get());
   }
   if (ctx->profile) {
     ctx->gs_events->emplace_back(e0, e1);
-    ctx->gs_bytes->push_back(graph->algorithmic_bytes(dim));
+    ctx->gs_bytes->push_back(bytes);
   }
 }
 

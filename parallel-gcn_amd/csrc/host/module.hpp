@@ -84,6 +84,8 @@ struct ModuleContext {
   float *xent_partials = nullptr;
   int xent_blocks = 0;
   Comm *comm = nullptr;        // null on one GPU
+  hipStream_t comm_stream = nullptr;      // edge-cut: stream of the reduce-scatters
+  std::vector<DevGraph *> chunk_graphs;   // edge-cut: Â column block per RS row chunk
   const void *jump_table = nullptr;  // M^period byte tables (device)
   void *gemm_workspace = nullptr;
   // profiling of GraphSum calls
@@ -129,7 +131,10 @@ class GraphSum : public Module {
   DevGraph *graph;
   int dim;
   ModuleContext *ctx;
-  DeviceBuffer<float> partial;  // [world*maxrows][ld] for the edge-cut reduce-scatter
+  // edge-cut: per row chunk, the [world*chunk_rows][ld] partial sums and their events
+  std::vector<DeviceBuffer<float>> partial;
+  std::vector<Event> computed;
+  Event reduced;
 
  public:
   GraphSum(shared_ptr<Variable> in_, shared_ptr<Variable> out_, DevGraph *graph_, int dim_,

@@ -143,12 +143,30 @@ constexpr int LDS_TOTAL_F4 = LDS_RING_F4 + LDS_CW * LDS_RING_BYTES / 16;
 // ring refills are LDS-DMA issued from inline asm, invisible to hipcc's waitcnt bookkeeping;
 // each wave counts its own: a summing wave only ever has ring refills outstanding (constant
 // vmcnt(3) = "the chunk refilled three chunks ago has landed"), the loader waits vmcnt(0) once
-// per slice.  One barrier per slice (raw s_barrier: no compiler-inserted vmcnt(0)).
+// per slice.  Slices are handed over through LDS words (lds_wait_ge), not barriers.
 // DIAG 4: per-wave cycle stamps (s_memtime) -> stamps[wg][wave][8]:
-//   0 loop cycles, 1 barrier-wait cycles, 2 ring-wait cycles, 3 entry blocks, 4 slices
+//   0 loop cycles, 1 hand-off wait cycles, 2 ring-wait cycles, 3 entry blocks, 4 slices
 __device__ __forceinline__ unsigned long long clk() { return __builtin_amdgcn_s_memtime(); }
 
-template <int DIAG, int WIN>
+// Slice hand-off words in LDS (the spare tail of counts area 0): loaded[b] = t + 1 once slice t
+// sits in buffer b; done[b] counts summing-wave completions of the slices held in buffer b.
+// Replaces a workgroup barrier per slice, so summing waves may drift up to one slice apart
+// (per-slice imbalance between waves no longer stalls everyone; r01 stamps: 18 % of the loop).
+constexpr int LDS_FLAG_BYTE = LDS_CW * LDS_SLOTS * 2;  // 480: first byte past the counts
+static_assert(LDS_FLAG_BYTE + 16 <= 512, "flag words fit the counts area tail");
+__device__ __forceinline__ unsigned lds_wait_ge(const unsigned *p, unsigned target) {
+  unsigned spins = 0;
+  while (true) {
+    const unsigned v = __builtin_amdgcn_readfirstlane(__atomic_load_n(p, __ATOMIC_RELAXED));
+    if (v >= target) break;
+    __builtin_amdgcn_s_sleep(1);
+    spins++;
+  }
+  asm volatile("" ::: "memory");
+  return spins;
+}
+
+template <int DIAG, int WIN, int SYNC>
 __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
     const uint2 *__restrict__ entries, const uint64_t *__restrict__ masks,
     const long long *__restrict__ wave_off,
@@ -172,6 +190,13 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
     const int buf = threadIdx.x >> 4, q = threadIdx.x & 15;
     lds[(buf * LDS_ROWS + LDS_SR) * 4 + q] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
+  unsigned *const flags = reinterpret_cast<unsigned *>(
+      reinterpret_cast<char *>(lds + LDS_TABLE_F4) + LDS_FLAG_BYTE);
+  unsigned *const loaded = flags, *const done = flags + 2;
+  if (threadIdx.x < 4) flags[threadIdx.x] = 0u;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // zero rows and hand-off words set (the only barrier)
+  asm volatile("" ::: "memory");
 
   if (wave == LDS_CW) {  // ------------------------------------------------ loader wave
     const int2 *sl = slices + (long long)b * t_max;
@@ -180,8 +205,14 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
                           (long long)blockIdx.x * t_max * (LDS_CW * LDS_SLOTS * 2);
     int2 sc_next = T > 0 ? sl[0] : make_int2(0, 0);
     for (int t = 0; t < T; t++) {
-      // slice t -> buffer t & 1 (free: every wave passed the barrier after slice t - 2),
-      // with the summing waves' step counts for slice t
+      // slice t -> buffer t & 1 once every summing wave is done with slice t - 2, with the
+      // summing waves' step counts for slice t
+      if (SYNC == 1 && t >= 2) {
+        unsigned long long cw0 = 0;
+        if constexpr (DIAG == 4) cw0 = clk();
+        lds_wait_ge(done + (t & 1), (unsigned)(LDS_CW * (t / 2)));
+        if constexpr (DIAG == 4) st_bar += clk() - cw0;
+      }
       const int2 sc = sc_next;
       if (t + 1 < T) sc_next = sl[t + 1];
       if (lane * 16 < LDS_CW * LDS_SLOTS * 2)
@@ -202,18 +233,20 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
       }
       unsigned long long c0 = 0;
       if constexpr (DIAG == 4) c0 = clk();
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      unsigned long long c1 = 0;
-      if constexpr (DIAG == 4) c1 = clk();
-      __builtin_amdgcn_s_barrier();  // slice t ready (t = 0) / slice t-1 summed
-      asm volatile("" ::: "memory");
-      if constexpr (DIAG == 4) {
-        const unsigned long long c2 = clk();
-        st_ring += c1 - c0;  // loader: staging wait
-        st_bar += c2 - c1;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // slice t and its counts landed
+      if constexpr (DIAG == 4) st_ring += clk() - c0;   // loader: staging wait
+      if constexpr (SYNC == 1) {
+        if (lane == 0) __atomic_store_n(loaded + (t & 1), (unsigned)(t + 1), __ATOMIC_RELAXED);
+        asm volatile("" ::: "memory");
+      } else {  // SYNC 0: one workgroup barrier per slice
+        unsigned long long c1 = 0;
+        if constexpr (DIAG == 4) c1 = clk();
+        __builtin_amdgcn_s_barrier();  // slice t ready (t = 0) / slice t-1 summed
+        asm volatile("" ::: "memory");
+        if constexpr (DIAG == 4) st_bar += clk() - c1;
       }
     }
-    __builtin_amdgcn_s_barrier();  // matches the summing waves' last slice
+    if constexpr (SYNC == 0) __builtin_amdgcn_s_barrier();  // the summing waves' last slice
     if constexpr (DIAG == 4) {
       if (lane == 0) {
         unsigned long long *o = stamps + ((long long)blockIdx.x * 16 + wave) * 8;
@@ -254,10 +287,33 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
   static_assert((LDS_RING_BYTES & (LDS_RING_BYTES - 1)) == 0, "ring wraps by masking");
   uint2 e_next = *reinterpret_cast<const uint2 *>(ring);
 
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // zero rows written
-  __builtin_amdgcn_s_barrier();                       // slice 0 staged
-  asm volatile("" ::: "memory");
   if constexpr (DIAG == 4) st_loop = clk();
+  // slice t staged (counts included) / this wave is done with slice t
+  auto slice_ready = [&](int t) {
+    unsigned long long cw0 = 0;
+    if constexpr (DIAG == 4) cw0 = clk();
+    if constexpr (SYNC == 1) {
+      lds_wait_ge(loaded + (t & 1), (unsigned)(t + 1));
+    } else if (t == 0) {
+      __builtin_amdgcn_s_barrier();  // slice 0 staged
+      asm volatile("" ::: "memory");
+    }
+    if constexpr (DIAG == 4) st_bar += clk() - cw0;
+  };
+  auto slice_done = [&](int t) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every read of slice t returned
+    if constexpr (SYNC == 1) {
+      if (lane == 0)
+        __hip_atomic_fetch_add(done + (t & 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      asm volatile("" ::: "memory");
+    } else {
+      unsigned long long cb = 0;
+      if constexpr (DIAG == 4) cb = clk();
+      __builtin_amdgcn_s_barrier();  // slice t summed; slice t+1 staged
+      asm volatile("" ::: "memory");
+      if constexpr (DIAG == 4) st_bar += clk() - cb;
+    }
+  };
   // next entry block of the ring (and its refill when a chunk is entered)
   auto next_block = [&]() {
     roff = (roff + 128) & (LDS_RING_BYTES - 1);
@@ -280,6 +336,7 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
     // this wave's per-step lane masks (uniform: scalar loads)
     const uint64_t *mk = masks + kb0 * 4;
     for (int t = 0; t < T; t++) {
+      slice_ready(t);
       const char *tb = reinterpret_cast<const char *>(lds + (t & 1) * LDS_ROWS * 4 + v);
       const uint4 *c4 = reinterpret_cast<const uint4 *>(
           reinterpret_cast<const char *>(lds + LDS_TABLE_F4) + (t & 1) * LDS_CNT_BYTES + wave * 32);
@@ -316,17 +373,13 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
           }
         }
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      unsigned long long cb = 0;
-      if constexpr (DIAG == 4) cb = clk();
-      __builtin_amdgcn_s_barrier();  // slice t summed; slice t+1 staged
-      asm volatile("" ::: "memory");
-      if constexpr (DIAG == 4) st_bar += clk() - cb;
+      slice_done(t);
     }
 #pragma unroll
     for (int j = 0; j < LDS_SLOTS; j++) acc[j] = make_float4(al[j].x, al[j].y, ah[j].x, ah[j].y);
   } else {
   for (int t = 0; t < T; t++) {
+    slice_ready(t);
     // edge entries are byte offsets of slice rows: address = entry + (buffer base + 16 v)
     const char *tb = reinterpret_cast<const char *>(lds + (t & 1) * LDS_ROWS * 4 + v);
     // this wave's 16 step counts for slice t, staged by the loader (uniform: broadcast read)
@@ -367,12 +420,7 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
         }
       }
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    unsigned long long cb = 0;
-    if constexpr (DIAG == 4) cb = clk();
-    __builtin_amdgcn_s_barrier();  // slice t summed; slice t+1 staged
-    asm volatile("" ::: "memory");
-    if constexpr (DIAG == 4) st_bar += clk() - cb;
+    slice_done(t);
   }
   }
   if constexpr (DIAG == 4) {
@@ -416,6 +464,7 @@ __global__ __launch_bounds__(256) void k_gs_lds_combine(const float4 *__restrict
 }
 
 int g_graphsum_lds_diag = 0;  // diagnostics only ("graphsum_lds_diag")
+int g_graphsum_lds_sync = 1;  // diagnostics ("graphsum_lds_sync"): 0 = a barrier per slice
 
 // DIAG 4 stamp buffer (diagnostics; read back with pgcn_debug_read("graphsum_lds_stamps"))
 static unsigned long long *g_stamps = nullptr;
@@ -444,24 +493,28 @@ void launch_graphsum_lds(const LdsSchedule &s, const float *in, int ld_in, float
   hipLaunchKernelGGL(k_gs_prescale, dim3((unsigned)ceil_div(pre, 256)), dim3(256), 0, st,
                      reinterpret_cast<const float4 *>(in), ld_in / 4, s.col_scale, s.n_cols,
                      reinterpret_cast<float4 *>(scratch_in));
-#define GS_LDS(D, W)                                                                        \
-  hipLaunchKernelGGL((k_graphsum_lds<D, W>), dim3((unsigned)(s.n_batches * kGraphBlocks)),     \
+#define GS_LDS(D, W, Y)                                                                     \
+  hipLaunchKernelGGL((k_graphsum_lds<D, W, Y>), dim3((unsigned)(s.n_batches * kGraphBlocks)),  \
                      dim3(LDS_THREADS), 0, st, s.entries, s.masks, s.wave_off, s.counts,        \
                      s.t_max, s.slices, s.n_slices, s.rows,                                    \
                      reinterpret_cast<const float4 *>(scratch_in), s.n_cols,                   \
                      reinterpret_cast<float4 *>(partial), (long long)s.n_rows,                 \
                      lds_stamps(s.n_batches * kGraphBlocks))
+  const int diag = g_graphsum_lds_diag;
   if (s.window == 2) {
-    if (g_graphsum_lds_diag == 4) GS_LDS(4, 2);
-    else if (g_graphsum_lds_diag == 6) GS_LDS(6, 2);  // no next-line touch
-    else GS_LDS(0, 2);
+    if (diag == 4) GS_LDS(4, 2, 1);
+    else if (diag == 6) GS_LDS(6, 2, 1);  // no next-line touch
+    else GS_LDS(0, 2, 1);
+  } else if (g_graphsum_lds_sync == 0) {  // r01: a workgroup barrier per slice
+    if (diag == 4) GS_LDS(4, 1, 0);
+    else GS_LDS(0, 1, 0);
   } else {
-    switch (g_graphsum_lds_diag) {
-      case 1: GS_LDS(1, 1); break;
-      case 2: GS_LDS(2, 1); break;
-      case 3: GS_LDS(3, 1); break;
-      case 4: GS_LDS(4, 1); break;
-      default: GS_LDS(0, 1); break;
+    switch (diag) {
+      case 1: GS_LDS(1, 1, 1); break;
+      case 2: GS_LDS(2, 1, 1); break;
+      case 3: GS_LDS(3, 1, 1); break;
+      case 4: GS_LDS(4, 1, 1); break;
+      default: GS_LDS(0, 1, 1); break;
     }
   }
 #undef GS_LDS

@@ -133,6 +133,23 @@ def test_edge_cut_engine_world1(loaded, pgcn, name):
     g.close()
 
 
+def test_edge_cut_world1_large_matches_single(pgcn):
+    """Edge-cut engine at world 1 on a graph whose feature table takes the LDS GraphSum path:
+    the chunked partial sums + reduce-scatters (two row chunks, comm stream) give the same
+    losses as the single-GPU engine."""
+    ds = pgcn.Dataset.synthetic(150000, 64, 8, 6000000, 3)
+    p = pgcn.make_params(ds)
+    single = pgcn.GCN(p, ds, device=0)
+    cut = pgcn.GCN(p, ds, device=0, rank=0, world=1, unique_id=pgcn.comm_unique_id())
+    for e in range(4):
+        a = single.train_epoch() + single.eval(2)
+        b = cut.train_epoch() + cut.eval(2)
+        for k in (0, 2):
+            assert abs(a[k] - b[k]) <= 1e-4 * abs(a[k]), (e, k, a, b)
+    single.close()
+    cut.close()
+
+
 def test_deep_model_matches_oracle(loaded, pgcn):
     """4-layer, hidden 128 (the deep configuration of SURVEY.md §8a): the engine's L-layer
     stack against the oracle's L-layer restatement of the same module order."""

@@ -83,6 +83,11 @@ t1 = time.time()
 o_lds = run_once()
 res["lds_build_plus_first_call_s"] = time.time() - t1
 res["d16_lds_ms"] = timeit(g, 16)
+pg.lib.pgcn_debug_set(b"graphsum_lds_sync", 0)
+res["d16_lds_barriers_ms"] = timeit(g, 16)
+res["d16_lds_again_ms"] = timeit(g, 16)
+pg.lib.pgcn_debug_set(b"graphsum_lds_sync", 1)
+res["d16_lds_flags_again_ms"] = timeit(g, 16)
 
 # window 2 (two-slot runs, exec-masked adds) on a fresh graph
 pg.lib.pgcn_debug_set(b"graphsum_lds_window", 2)
