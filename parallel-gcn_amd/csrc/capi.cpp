@@ -24,6 +24,7 @@ extern int g_graphsum_lds_order;    // host/graph.cpp (diagnostics)
 extern int g_graphsum_lds_diag;     // k_graphsum_lds.hip (diagnostics)
 extern int g_graphsum_lds_window;   // host/graph.cpp (diagnostics)
 extern int g_graphsum_lds_sync;     // k_graphsum_lds.hip (diagnostics)
+extern int g_graphsum_lds_opt;      // k_graphsum_lds.hip (diagnostics)
 long long lds_stamps_read(void *dst, long long max_elems);
 }  // namespace pgcn
 
@@ -432,6 +433,7 @@ int pgcn_debug_set(const char *key, int value) {
   else if (!std::strcmp(key, "graphsum_lds_diag")) pgcn::g_graphsum_lds_diag = value;
   else if (!std::strcmp(key, "graphsum_lds_window")) pgcn::g_graphsum_lds_window = value;
   else if (!std::strcmp(key, "graphsum_lds_sync")) pgcn::g_graphsum_lds_sync = value;
+  else if (!std::strcmp(key, "graphsum_lds_opt")) pgcn::g_graphsum_lds_opt = value;
   else if (!std::strcmp(key, "gemm_variant")) pgcn::g_gemm_variant = value;
   else return PGCN_E_INVALID;
   return PGCN_OK;

@@ -246,7 +246,10 @@ void DevGraph::set_scales(std::vector<float> row_scale, std::vector<float> col_s
 static const int kLdsLaneGroups[4][4] = {{0, 3, 5, 6}, {1, 2, 4, 7}, {8, 11, 13, 14}, {9, 10, 12, 15}};
 
 int g_graphsum_lds = 1;
-int g_graphsum_lds_window = 1;  // diagnostics ("graphsum_lds_window"): 2 = two-slot runs (exec-masked; slower on gfx950)
+// "graphsum_lds_window": 1 = slots one after another; 2 = two-slot runs (exec-masked; slower on
+// gfx950); 3 = slot pairs interleaved block by block (two blocks of LDS reads in flight; r01:
+// same time as 1 -- the kernel is not bound by per-wave LDS latency)
+int g_graphsum_lds_window = 1;
 int g_graphsum_lds_order = 1;  // diagnostics ("graphsum_lds_order"): 0 = runs in column order  // diagnostics (pgcn_debug_set "graphsum_lds"): 0 disables the LDS path
 
 // LDS-staged d = 16 schedule (see k_graphsum_lds.hip for the layout it feeds), host side:
@@ -376,6 +379,7 @@ LdsHost build_lds_host(int n_rows, int n_cols, const std::vector<int> &h_indptr_
   }, 0, 1);
   std::vector<unsigned short> counts((size_t)n_wg * t_max * CW * NS, 0);
   std::vector<long long> kbs((size_t)n_wg * CW, 0);
+  const bool win2 = window == 2, pair = window == 3;
   // walks (wg, wave): for each slice, each rowset slot, the 16 rows' runs in that slice
   auto walk = [&](long long wg, int w, unsigned short *out_entries) {
     const int b = (int)(wg % B), bat = (int)(wg / B);
@@ -392,9 +396,13 @@ LdsHost build_lds_host(int n_rows, int n_cols, const std::vector<int> &h_indptr_
       end[k] = h_indptr_[(size_t)r + 1];
     }
     long long kb_total = 0;
+    // window 3: a slice's blocks are built per slot, then emitted in slot-pair order
+    std::vector<unsigned short> sb[LDS_SLOTS];
+    int sb_n[LDS_SLOTS];
     for (int t = 0; t < nsl[(size_t)b]; t++) {
       const int2 sc = slices[(size_t)b * t_max + t];
       const int c1 = sc.x + sc.y;
+      const long long kb_slice = kb_total;
       for (int j = 0; j < NS; j++) {
         int n[16], m = 0;
         for (int g = 0; g < 16; g++) {
@@ -407,19 +415,27 @@ LdsHost build_lds_host(int n_rows, int n_cols, const std::vector<int> &h_indptr_
         PGCN_CHECK(m < 65536, PGCN_E_INVALID, "graphsum_lds: slice run too long");
         counts[(size_t)(((wg * t_max + t) * CW + w) * NS + j)] = (unsigned short)m;
         const int nkb = (m + 3) / 4;
-        if (out_entries && nkb > 0 && !g_graphsum_lds_order) {
+        unsigned short *slot_out = nullptr;  // this slot's nkb blocks
+        if (out_entries && pair) {
+          sb[j].assign((size_t)nkb * 64, 0);
+          sb_n[j] = nkb;
+          slot_out = sb[j].data();
+        } else if (out_entries) {
+          slot_out = out_entries + kb_total * 64;
+        }
+        if (slot_out && nkb > 0 && !g_graphsum_lds_order) {
           for (int kb = 0; kb < nkb; kb++)
             for (int g = 0; g < 16; g++)
               for (int u = 0; u < 4; u++) {
                 const int st = 4 * kb + u, k = j * 16 + g;
-                out_entries[(kb_total + kb) * 64 + g * 4 + u] =
+                slot_out[kb * 64 + g * 4 + u] =
                     (unsigned short)(st < n[g] ? (sidx[(size_t)cur[k] + st] - sc.x) * 64 : SR * 64);
               }
-        } else if (out_entries && nkb > 0) {
+        } else if (slot_out && nkb > 0) {
           // Order each row's run (any fixed order sums the same terms) so that at every step
           // the 4 rows served by one ds_read_b128 lane group read 4 different bank quarters
           // (64-B row r occupies quarter r % 4); padding takes a zero row of a free quarter.
-          unsigned short *dst = out_entries + kb_total * 64;
+          unsigned short *dst = slot_out;
           for (int q = 0; q < 4; q++) {
             const int *grp = kLdsLaneGroups[q];
             std::vector<int> byres[4][4];  // [member][residue] -> local columns
@@ -471,6 +487,23 @@ LdsHost build_lds_host(int n_rows, int n_cols, const std::vector<int> &h_indptr_
         }
         for (int g = 0; g < 16; g++) cur[j * 16 + g] += n[g];
         kb_total += nkb;
+      }
+      if (out_entries && pair) {  // slots 2p, 2p+1: A0 B0 A1 B1 ..., then the longer's rest
+        unsigned short *o = out_entries + kb_slice * 64;
+        auto put = [&](int j, int i) {
+          std::copy(sb[j].begin() + (size_t)i * 64, sb[j].begin() + (size_t)(i + 1) * 64, o);
+          o += 64;
+        };
+        for (int p = 0; p < NS / 2; p++) {
+          const int a = 2 * p, c = 2 * p + 1, both = std::min(sb_n[a], sb_n[c]);
+          for (int i = 0; i < both; i++) {
+            put(a, i);
+            put(c, i);
+          }
+          for (int i = both; i < sb_n[a]; i++) put(a, i);
+          for (int i = both; i < sb_n[c]; i++) put(c, i);
+        }
+        PGCN_CHECK(o == out_entries + kb_total * 64, PGCN_E_INVALID, "graphsum_lds: pair order");
       }
     }
     return kb_total;
@@ -576,7 +609,6 @@ LdsHost build_lds_host(int n_rows, int n_cols, const std::vector<int> &h_indptr_
     }
     return kb_total;
   };
-  const bool win2 = window == 2;
   parallel_for(n_wg * CW, [&](long long a, long long e) {
     for (long long x = a; x < e; x++)
       kbs[(size_t)x] = win2 ? walk2(x / CW, (int)(x % CW), nullptr, nullptr)
@@ -596,7 +628,7 @@ LdsHost build_lds_host(int n_rows, int n_cols, const std::vector<int> &h_indptr_
     }
   }, 0, 64);
   LdsHost h;
-  h.window = win2 ? 2 : 1;
+  h.window = win2 ? 2 : pair ? 3 : 1;
   h.n_batches = nbat;
   h.t_max = t_max;
   h.nsl = std::move(nsl);
@@ -624,16 +656,37 @@ void lds_emulate(const LdsHost &h, int n_rows, const float *in, double *out) {
       std::fill(acc.begin(), acc.end(), 0.0);
       for (int t = 0; t < h.nsl[(size_t)b]; t++) {
         const int2 sc = h.slices[(size_t)b * h.t_max + t];
-        for (int j = 0; j < NS; j++) {
-          const int n = h.counts[(size_t)(((wg * h.t_max + t) * CW + w) * NS + j)];
-          const int nblk = h.window == 2 ? n : (n + 3) / 4;
-          for (int k = 0; k < nblk; k++, kb++) {
+        // the order the kernel takes blocks in: (slot, block index within the slot)
+        std::vector<std::pair<int, int>> seq;
+        const unsigned short *cn = &h.counts[(size_t)(((wg * h.t_max + t) * CW + w) * NS)];
+        if (h.window == 3) {
+          for (int p = 0; p < NS / 2; p++) {
+            const int na = (cn[2 * p] + 3) / 4, nc = (cn[2 * p + 1] + 3) / 4;
+            for (int i = 0; i < std::min(na, nc); i++) {
+              seq.push_back({2 * p, i});
+              seq.push_back({2 * p + 1, i});
+            }
+            for (int i = std::min(na, nc); i < na; i++) seq.push_back({2 * p, i});
+            for (int i = std::min(na, nc); i < nc; i++) seq.push_back({2 * p + 1, i});
+          }
+        } else {
+          for (int j = 0; j < NS; j++) {
+            const int nblk = h.window == 2 ? cn[j] : (cn[j] + 3) / 4;
+            for (int k = 0; k < nblk; k++) seq.push_back({j, k});
+          }
+        }
+        for (const auto &jk : seq) {
+          const int j = jk.first, k = jk.second, n = cn[j];
+          {
             for (int st = 0; st < 4; st++) {
               const uint64_t m = h.window == 2 ? h.masks[(size_t)kb * 4 + st] : 0;
               for (int g = 0; g < 16; g++) {
                 const int e = h.entries[(size_t)kb * 64 + g * 4 + st];
                 PGCN_CHECK(e % 64 == 0, PGCN_E_INVALID, "lds schedule: entry not a row offset");
                 const int row = e / 64;
+                // steps past the run's count are padding (zero rows) in every window
+                PGCN_CHECK(h.window == 2 || 4 * k + st < n || row >= LDS_SR, PGCN_E_INVALID,
+                           "lds schedule: edge past the run's step count");
                 PGCN_CHECK(row >= LDS_SR || row < sc.y, PGCN_E_INVALID,
                            "lds schedule: entry past the slice");
                 const unsigned q = (unsigned)(m >> (4 * g)) & 0xfu;
@@ -644,6 +697,7 @@ void lds_emulate(const LdsHost &h, int n_rows, const float *in, double *out) {
               }
             }
           }
+          kb++;
         }
       }
       PGCN_CHECK(kb == h.wave_off[(size_t)(wg * CW + w) + 1], PGCN_E_INVALID,
@@ -706,7 +760,8 @@ void DevGraph::build_lds() {
   L->row_scale.upload(h_row_scale_);
   L->col_scale.allocate(h_col_scale_.size());
   L->col_scale.upload(h_col_scale_);
-  L->scratch.allocate((size_t)n_cols_ * 16 + 64);
+  // + LDS_ROWS rows: slice copies run whole pieces past the last column (never read)
+  L->scratch.allocate(((size_t)n_cols_ + LDS_ROWS) * 16 + 64);
   L->partial.allocate((size_t)kBlocks * n_rows_ * 16);
   L->s.n_rows = n_rows_;
   L->s.n_cols = n_cols_;
@@ -720,7 +775,7 @@ void DevGraph::build_lds() {
   L->s.rows = L->rows.get();
   L->s.row_scale = L->row_scale.get();
   L->s.col_scale = L->col_scale.get();
-  L->s.window = win2 ? 2 : 1;
+  L->s.window = h.window;
   L->s.masks = win2 ? L->masks.get() : nullptr;
   lds_ = std::move(L);
 }

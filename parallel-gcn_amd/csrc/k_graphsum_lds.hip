@@ -77,6 +77,23 @@ __device__ __forceinline__ void glds16(const void *gsrc, unsigned lds_dst) {
       : "memory");
 }
 
+// Four consecutive 1-KB pieces: gsrc .. gsrc + 3 KB -> lds_dst .. lds_dst + 3 KB.  The
+// instruction offset steps the global AND the LDS address (LDS = M0 + offset + 16 * lane),
+// so one M0 write and one address VGPR serve all four.
+__device__ __forceinline__ void glds16x4(const void *gsrc, unsigned lds_dst) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "global_load_lds_dwordx4 %1, off offset:1024\n\t"
+      "global_load_lds_dwordx4 %1, off offset:2048\n\t"
+      "global_load_lds_dwordx4 %1, off offset:3072\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_dst)
+      : "memory");
+}
+
 typedef float f2v __attribute__((ext_vector_type(2)));
 typedef float f4v __attribute__((ext_vector_type(4)));
 
@@ -173,7 +190,7 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
     const unsigned short *__restrict__ counts, int t_max, const int2 *__restrict__ slices,
     const int *__restrict__ n_slices, const int *__restrict__ rows, const float4 *__restrict__ in,
     int n_cols, float4 *__restrict__ partial, long long part_stride,
-    unsigned long long *__restrict__ stamps) {
+    unsigned long long *__restrict__ stamps, int opt) {
   unsigned long long st_loop = 0, st_bar = 0, st_ring = 0;
   // ONE __shared__ object: [2][LDS_ROWS][4] float4 slice buffers, then the entry rings
   __shared__ float4 lds[LDS_TOTAL_F4];
@@ -199,6 +216,9 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
   asm volatile("" ::: "memory");
 
   if (wave == LDS_CW) {  // ------------------------------------------------ loader wave
+    // the loader's few instructions go first on its SIMD (the summing waves there would
+    // otherwise delay every piece it issues; r01 stamps: slices landed late 21 % of the loop)
+    if (opt & 2) __builtin_amdgcn_s_setprio(3);
     const int2 *sl = slices + (long long)b * t_max;
     const int last = n_cols - 1;
     const char *cnt_src = reinterpret_cast<const char *>(counts) +
@@ -219,18 +239,29 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
         glds16(cnt_src + (long long)t * (LDS_CW * LDS_SLOTS * 2) + lane * 16,
                lds_base + (unsigned)(LDS_TABLE_F4 * 16 + (t & 1) * LDS_CNT_BYTES));
       const unsigned dst = lds_base + (unsigned)((t & 1) * LDS_ROWS * 64);
-      const int pieces = DIAG == 1 ? 4 : LDS_SR / 16;  // DIAG 1: stage 1/16 (timing only)
+      // The slice is LDS_SR consecutive 64-B rows of `in` (the prescaled table, allocated with
+      // LDS_ROWS rows of slack past n_cols: rows past a slice's end are copied, never read),
+      // so piece i (16 rows, 1 KB) sits 1 KB past piece i-1 in the table and in LDS.
+      const char *src = reinterpret_cast<const char *>(in + (long long)sc.x * 4) + lane * 16;
+      constexpr int full = LDS_SR / 16;
+      if (opt & 1) {
+        constexpr bool stage16 = DIAG == 1 || DIAG == 5 || DIAG == 7;
+        const int pieces4 = stage16 ? 1 : full / 4;  // DIAG 1/5/7: stage 1/16 (timing only)
+#pragma unroll 4
+        for (int i = 0; i < pieces4; i++) glds16x4(src + i * 4096, dst + (unsigned)(i * 4096));
+        if (!stage16)
+          for (int i = full / 4 * 4; i < full; i++) glds16(src + i * 1024, dst + (unsigned)(i * 1024));
+      } else {
+        const int pieces = DIAG == 1 ? 4 : full;
 #pragma unroll 8
-      for (int i = 0; i < pieces; i++) {
-        int r = sc.x + 16 * i + g;
-        r = r < last ? r : last;  // rows past the slice end are never referenced
-        glds16(in + (long long)r * 4 + v, dst + (unsigned)(i * 1024));
+        for (int i = 0; i < pieces; i++) {
+          int r = sc.x + 16 * i + g;
+          r = r < last ? r : last;
+          glds16(in + (long long)r * 4 + v, dst + (unsigned)(i * 1024));
+        }
       }
-      if (LDS_SR % 16 && g < LDS_SR % 16) {  // last partial piece (keeps the zero rows)
-        int r = sc.x + 16 * (LDS_SR / 16) + g;
-        r = r < last ? r : last;
-        glds16(in + (long long)r * 4 + v, dst + (unsigned)((LDS_SR / 16) * 1024));
-      }
+      if (LDS_SR % 16 && g < LDS_SR % 16)  // last partial piece (keeps the zero rows)
+        glds16(src + full * 1024, dst + (unsigned)(full * 1024));
       unsigned long long c0 = 0;
       if constexpr (DIAG == 4) c0 = clk();
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // slice t and its counts landed
@@ -269,15 +300,19 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
   auto refill = [&](long long c) {  // chunk c -> ring slot c % 4 (clamped: dummy past the end)
     long long cc = c < nchunk ? c : nchunk - 1;
     cc = cc > 0 ? cc : 0;
-    if (lane < 32)
+    if (DIAG != 7 && lane < 32)  // DIAG 7: no entry stream (timing only)
       glds16(ebytes + cc * LDS_RING_CHUNK + lane * 16,
              ring_dst + (unsigned)((c % LDS_RING_SLOTS) * LDS_RING_CHUNK));
   };
   refill(0);
   refill(1);
   refill(2);
-  refill(3);
-  asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // chunk 0
+  if constexpr (WIN == 3) {  // window 3 keeps two chunks in flight (see ahead())
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // chunk 0
+  } else {
+    refill(3);
+    asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // chunk 0
+  }
 
   float4 acc[LDS_SLOTS];
 #pragma unroll
@@ -328,7 +363,95 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
     }
     e_next = *reinterpret_cast<const uint2 *>(ring + roff);  // (past the end: unused)
   };
-  if constexpr (WIN == 2) {
+  if constexpr (WIN == 3) {
+    // Slot pairs (2p, 2p+1) interleaved block by block (host order: A0 B0 A1 B1 ..., then the
+    // longer slot's rest), so every iteration has 8 ds_read_b128 (two blocks) in flight where
+    // window 1 had 4: a slot runs ~1.4 blocks per slice on reddit, so pipelining inside one
+    // slot would not find a second block.  Two entry blocks are read ahead (q0, q1); the
+    // lookahead pointer drives the ring: entering chunk c refills chunk c + 2 into the slot of
+    // chunk c - 2, whose reads were all consumed (waited for) two blocks ago -- no drain.
+    uint2 q0 = e_next, q1;
+    auto ahead = [&]() -> uint2 {
+      roff = (roff + 128) & (LDS_RING_BYTES - 1);
+      if ((roff & (LDS_RING_CHUNK - 1)) == 0) {
+        ++chunk;
+        refill(chunk + 2);
+        unsigned long long c0 = 0;
+        if constexpr (DIAG == 4) c0 = clk();
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        if constexpr (DIAG == 4) st_ring += clk() - c0;
+      }
+      return *reinterpret_cast<const uint2 *>(ring + roff);
+    };
+    q1 = ahead();
+    for (int t = 0; t < T; t++) {
+      slice_ready(t);
+      const char *tb = reinterpret_cast<const char *>(lds + (t & 1) * LDS_ROWS * 4 + v);
+      auto rd = [&](unsigned off) { return *reinterpret_cast<const float4 *>(tb + off); };
+      const uint4 *c4 = reinterpret_cast<const uint4 *>(
+          reinterpret_cast<const char *>(lds + LDS_TABLE_F4) + (t & 1) * LDS_CNT_BYTES + wave * 32);
+      const uint4 cw0 = c4[0], cw1 = c4[1];
+      const unsigned cw[8] = {
+          (unsigned)__builtin_amdgcn_readfirstlane(cw0.x), (unsigned)__builtin_amdgcn_readfirstlane(cw0.y),
+          (unsigned)__builtin_amdgcn_readfirstlane(cw0.z), (unsigned)__builtin_amdgcn_readfirstlane(cw0.w),
+          (unsigned)__builtin_amdgcn_readfirstlane(cw1.x), (unsigned)__builtin_amdgcn_readfirstlane(cw1.y),
+          (unsigned)__builtin_amdgcn_readfirstlane(cw1.z), (unsigned)__builtin_amdgcn_readfirstlane(cw1.w)};
+      // the longer slot's rest: two blocks per iteration, then one
+      auto rest = [&](float4 &a, int r) {
+        for (; r >= 2; r -= 2) {
+          const uint2 e0 = q0, e1 = q1;
+          const float4 x0 = rd(e0.x & 0xffffu), x1 = rd(e0.x >> 16), x2 = rd(e0.y & 0xffffu),
+                       x3 = rd(e0.y >> 16), x4 = rd(e1.x & 0xffffu), x5 = rd(e1.x >> 16),
+                       x6 = rd(e1.y & 0xffffu), x7 = rd(e1.y >> 16);
+          q0 = ahead();
+          q1 = ahead();
+          f4_acc(a, x0);
+          f4_acc(a, x1);
+          f4_acc(a, x2);
+          f4_acc(a, x3);
+          f4_acc(a, x4);
+          f4_acc(a, x5);
+          f4_acc(a, x6);
+          f4_acc(a, x7);
+        }
+        if (r) {
+          const uint2 e0 = q0;
+          const float4 x0 = rd(e0.x & 0xffffu), x1 = rd(e0.x >> 16), x2 = rd(e0.y & 0xffffu),
+                       x3 = rd(e0.y >> 16);
+          q0 = q1;
+          q1 = ahead();
+          f4_acc(a, x0);
+          f4_acc(a, x1);
+          f4_acc(a, x2);
+          f4_acc(a, x3);
+        }
+      };
+#pragma unroll
+      for (int p = 0; p < LDS_SLOTS / 2; p++) {
+        const int na = ((cw[p] & 0xffffu) + 3) >> 2, nb2 = ((cw[p] >> 16) + 3) >> 2;
+        const int both = na < nb2 ? na : nb2;
+        for (int i = 0; i < both; i++) {
+          const uint2 e0 = q0, e1 = q1;
+          const float4 x0 = rd(e0.x & 0xffffu), x1 = rd(e0.x >> 16), x2 = rd(e0.y & 0xffffu),
+                       x3 = rd(e0.y >> 16), x4 = rd(e1.x & 0xffffu), x5 = rd(e1.x >> 16),
+                       x6 = rd(e1.y & 0xffffu), x7 = rd(e1.y >> 16);
+          q0 = ahead();
+          q1 = ahead();
+          f4_acc(acc[2 * p], x0);
+          f4_acc(acc[2 * p], x1);
+          f4_acc(acc[2 * p], x2);
+          f4_acc(acc[2 * p], x3);
+          f4_acc(acc[2 * p + 1], x4);
+          f4_acc(acc[2 * p + 1], x5);
+          f4_acc(acc[2 * p + 1], x6);
+          f4_acc(acc[2 * p + 1], x7);
+        }
+        if (na > nb2) rest(acc[2 * p], na - nb2);
+        else if (nb2 > na) rest(acc[2 * p + 1], nb2 - na);
+      }
+      slice_done(t);
+    }
+  } else if constexpr (WIN == 2) {
     // accumulators as packed halves (v_pk_add_f32 operands)
     f2v al[LDS_SLOTS], ah[LDS_SLOTS];
 #pragma unroll
@@ -398,7 +521,7 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
         const uint2 e = e_next;
         next_block();
         // all 4 entries are valid: steps past a row's run point at a zero row
-        if constexpr (DIAG == 2) {  // diagnostic: no table reads
+        if constexpr (DIAG == 2 || DIAG == 5 || DIAG == 7) {  // diagnostic: no table reads
           acc[j].x += __uint_as_float(e.x);
           acc[j].y += __uint_as_float(e.y);
         } else {
@@ -465,6 +588,9 @@ __global__ __launch_bounds__(256) void k_gs_lds_combine(const float4 *__restrict
 
 int g_graphsum_lds_diag = 0;  // diagnostics only ("graphsum_lds_diag")
 int g_graphsum_lds_sync = 1;  // diagnostics ("graphsum_lds_sync"): 0 = a barrier per slice
+// "graphsum_lds_opt": bit 0 = slice copies as 4-piece runs from one address VGPR (needs the
+// table's row slack), bit 1 = loader wave at raised issue priority
+int g_graphsum_lds_opt = 3;
 
 // DIAG 4 stamp buffer (diagnostics; read back with pgcn_debug_read("graphsum_lds_stamps"))
 static unsigned long long *g_stamps = nullptr;
@@ -499,9 +625,12 @@ void launch_graphsum_lds(const LdsSchedule &s, const float *in, int ld_in, float
                      s.t_max, s.slices, s.n_slices, s.rows,                                    \
                      reinterpret_cast<const float4 *>(scratch_in), s.n_cols,                   \
                      reinterpret_cast<float4 *>(partial), (long long)s.n_rows,                 \
-                     lds_stamps(s.n_batches * kGraphBlocks))
+                     lds_stamps(s.n_batches * kGraphBlocks), g_graphsum_lds_opt)
   const int diag = g_graphsum_lds_diag;
-  if (s.window == 2) {
+  if (s.window == 3) {
+    if (diag == 4) GS_LDS(4, 3, 1);
+    else GS_LDS(0, 3, 1);
+  } else if (s.window == 2) {
     if (diag == 4) GS_LDS(4, 2, 1);
     else if (diag == 6) GS_LDS(6, 2, 1);  // no next-line touch
     else GS_LDS(0, 2, 1);
@@ -513,6 +642,8 @@ void launch_graphsum_lds(const LdsSchedule &s, const float *in, int ld_in, float
       case 1: GS_LDS(1, 1, 1); break;
       case 2: GS_LDS(2, 1, 1); break;
       case 3: GS_LDS(3, 1, 1); break;
+      case 5: GS_LDS(5, 1, 1); break;  // no table reads, 1/16 staged
+      case 7: GS_LDS(7, 1, 1); break;  // as 5, no entry stream either
       case 4: GS_LDS(4, 1, 1); break;
       default: GS_LDS(0, 1, 1); break;
     }

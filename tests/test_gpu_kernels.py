@@ -16,6 +16,7 @@ import helpers
 pytestmark = pytest.mark.gpu
 
 DEV = "cuda"
+LDS_WINDOW_DEFAULT = 1  # host/graph.cpp g_graphsum_lds_window
 
 
 def vp(t):
@@ -78,10 +79,13 @@ def abs_bound(indptr, indices, x, dim):
     (5000, 8, 7, 2),         # cora C = 7
     (20000, 10, 128, 3),     # 4-layer hidden 128
     (120000, 40, 16, -2),    # LDS path, window-2 schedule (two-slot runs, exec-masked adds)
+    (120000, 40, 16, -3),    # LDS path, window-3 schedule (slot pairs interleaved)
 ])
 def test_graphsum_vs_oracle(pgcn, n, deg, dim, hubs):
-    window = 2 if hubs < 0 else 1
-    hubs = abs(hubs)
+    # LDS path (d = 16, table > L2): default window 1 (slots one after another); hubs < 0
+    # selects window -hubs (with 20 hubs)
+    window = -hubs if hubs < 0 else LDS_WINDOW_DEFAULT
+    hubs = 20 if hubs < 0 else hubs
     pgcn.lib.pgcn_debug_set(b"graphsum_lds_window", window)  # schedules built from here on
     indptr, indices = random_graph(n, deg, seed=n + dim, hubs=hubs, hub_deg=3000)
     ld = (dim + 3) // 4 * 4
@@ -108,7 +112,7 @@ def test_graphsum_vs_oracle(pgcn, n, deg, dim, hubs):
     torch.cuda.synchronize()
     assert torch.equal(out, out2)
     pgcn.lib.pgcn_graph_destroy(g)
-    pgcn.lib.pgcn_debug_set(b"graphsum_lds_window", 1)
+    pgcn.lib.pgcn_debug_set(b"graphsum_lds_window", LDS_WINDOW_DEFAULT)
 
 
 def test_graphsum_linearity_large(pgcn):
