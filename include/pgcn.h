@@ -85,6 +85,14 @@ int pgcn_mask_nibbles(const uint64_t *mask, long long mask_base, long long mask_
 int pgcn_gemm_xstream(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
                       int trans_b, float *C, int ldc, const uint64_t *mask_nib, float a_scale,
                       void *stream);
+/* Both first-layer products from one pass over A: C = A B (no dropout) and C2 = drop(A) B,
+ * C2 bit-identical to pgcn_gemm_xstream with the same mask.  The engine uses it for eval's
+ * forward together with the next training forward (same weights: no optimizer step between),
+ * replacing the reference's two separate SparseMatmul::forward passes (src/module.cu:104-126,
+ * called by src/gcn.cu:293-343). */
+int pgcn_gemm_xstream_dual(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
+                           int trans_b, float *C, float *C2, int ldc, const uint64_t *mask_nib,
+                           float a_scale, void *stream);
 int pgcn_gemm_tn_xstream(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
                          float *C, int ldc, const uint64_t *mask_nib, float a_scale,
                          void *workspace, void *stream);

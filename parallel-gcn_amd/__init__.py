@@ -73,6 +73,8 @@ _sig("pgcn_gemm_tn", c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_in
 _sig("pgcn_mask_nibbles", c_int, c_void_p, c_ll, c_ll, c_int, c_int, c_void_p, c_void_p)
 _sig("pgcn_gemm_xstream", c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int,
      c_void_p, c_int, c_void_p, c_float, c_void_p)
+_sig("pgcn_gemm_xstream_dual", c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int,
+     c_int, c_void_p, c_void_p, c_int, c_void_p, c_float, c_void_p)
 _sig("pgcn_gemm_tn_xstream", c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int,
      c_void_p, c_int, c_void_p, c_float, c_void_p, c_void_p)
 _sig("pgcn_spmm_csr", c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_float,
@@ -351,7 +353,8 @@ def csr_transpose(indptr, indices, n_cols):
 EXPORTED = [
     "pgcn_status_string", "pgcn_version", "pgcn_rng_seed", "pgcn_rng_jump", "pgcn_graph_create",
     "pgcn_graph_destroy", "pgcn_graph_nnz", "pgcn_graphsum", "pgcn_gemm", "pgcn_gemm_tn_workspace",
-    "pgcn_gemm_tn", "pgcn_mask_nibbles", "pgcn_gemm_xstream", "pgcn_gemm_tn_xstream",
+    "pgcn_gemm_tn", "pgcn_mask_nibbles", "pgcn_gemm_xstream", "pgcn_gemm_xstream_dual",
+    "pgcn_gemm_tn_xstream",
     "pgcn_spmm_csr", "pgcn_spmm_csc_bwd", "pgcn_csr_transpose",
     "pgcn_rng_jump_table", "pgcn_dropout_mask", "pgcn_dropout_apply", "pgcn_relu_fwd",
     "pgcn_relu_bwd", "pgcn_xent_blocks", "pgcn_xent_fwd", "pgcn_finalize", "pgcn_adam",

@@ -19,6 +19,7 @@ namespace pgcn {
 extern int g_graphsum_variant;      // k_graphsum.hip (diagnostics)
 extern int g_graphsum_force_plain;  // host/graph.cpp (diagnostics)
 extern int g_gemm_variant;          // k_gemm.hip (diagnostics)
+extern int g_train_ahead;           // host/gcn.cpp
 extern int g_graphsum_lds;          // host/graph.cpp (diagnostics)
 extern int g_graphsum_lds_order;    // host/graph.cpp (diagnostics)
 extern int g_graphsum_lds_diag;     // k_graphsum_lds.hip (diagnostics)
@@ -169,6 +170,18 @@ int pgcn_gemm_xstream(int M, int N, int K, const float *A, int lda, const float 
     PGCN_CHECK(A && B && C && M >= 0 && ldc >= N, PGCN_E_INVALID, "gemm_xstream args");
     launch_xstream_nn(M, N, K, A, lda, B, ldb, trans_b, C, ldc, mask_nib, a_scale,
                       as_stream(stream));
+    PGCN_HIP(hipGetLastError());
+  });
+}
+
+int pgcn_gemm_xstream_dual(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
+                           int trans_b, float *C, float *C2, int ldc, const uint64_t *mask_nib,
+                           float a_scale, void *stream) {
+  return guarded([&] {
+    PGCN_CHECK(A && B && C && C2 && mask_nib && M >= 0 && ldc >= N, PGCN_E_INVALID,
+               "gemm_xstream_dual args");
+    launch_xstream_nn(M, N, K, A, lda, B, ldb, trans_b, C, ldc, mask_nib, a_scale,
+                      as_stream(stream), C2);
     PGCN_HIP(hipGetLastError());
   });
 }
@@ -435,6 +448,7 @@ int pgcn_debug_set(const char *key, int value) {
   else if (!std::strcmp(key, "graphsum_lds_sync")) pgcn::g_graphsum_lds_sync = value;
   else if (!std::strcmp(key, "graphsum_lds_opt")) pgcn::g_graphsum_lds_opt = value;
   else if (!std::strcmp(key, "gemm_variant")) pgcn::g_gemm_variant = value;
+  else if (!std::strcmp(key, "train_ahead")) pgcn::g_train_ahead = value;
   else return PGCN_E_INVALID;
   return PGCN_OK;
 }

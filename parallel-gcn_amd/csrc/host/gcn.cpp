@@ -12,6 +12,10 @@
 
 namespace pgcn {
 
+// "train_ahead" (pgcn_debug_set, read at engine build): eval's first-layer forward also
+// computes the next training forward's product (SparseMatmul, one pass over dense X)
+int g_train_ahead = 1;
+
 // ------------------------------------------------------------------------------------------
 // Adam (src/optim.cu:7-95; hpdga optim.cpp:16-35)
 // ------------------------------------------------------------------------------------------
@@ -300,6 +304,7 @@ void GCN::build(const GCNData &data) {
   for (int l = 0; l < L; l++)
     ws = std::max(ws, gemm_tn_workspace(rows, dims[(size_t)l + 1], dims[(size_t)l]));
   gemm_ws.allocate(ws / sizeof(float) + 64);
+  ctx.train_ahead = g_train_ahead != 0;
   ctx.xent_partials = xent_partials.get();
   ctx.xent_blocks = xent_blocks(prow);
   ctx.gemm_workspace = gemm_ws.get();

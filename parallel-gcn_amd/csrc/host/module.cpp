@@ -1,6 +1,8 @@
 // parallel-gcn_amd/csrc/host/module.cpp
 #include "module.hpp"
 
+#include <utility>
+
 #include "../kernels.hpp"
 
 namespace pgcn {
@@ -35,11 +37,25 @@ Dropout::Dropout(shared_ptr<Variable> in_, float p_, shared_ptr<DropoutRng> rng_
                  ModuleContext *ctx_)
     : in(std::move(in_)), rng(std::move(rng_)), p(p_), ctx(ctx_) {}
 
-void Dropout::forward(bool training, const Stream &s) const {
-  if (!training) return;  // hpdga module.cpp:209
+void Dropout::draw(const Stream &s) const {
   const DropoutRng &r = *rng;
   launch_dropout_mask(r.states.get(), r.n_chunks, 64 * r.chunk_lo, r.elem_end, p, r.mask.get(),
                       ctx->jump_table, s.get());
+}
+
+void Dropout::draw_ahead(const Stream &s) const {
+  PGCN_CHECK(!ahead && !in, PGCN_E_INVALID, "dropout: one mask ahead, input dropout only");
+  draw(s);
+  ahead = true;
+}
+
+void Dropout::forward(bool training, const Stream &s) const {
+  if (!training) return;  // hpdga module.cpp:209
+  const DropoutRng &r = *rng;
+  if (ahead)
+    ahead = false;  // drawn by the eval forward before this one
+  else
+    draw(s);
   if (in) {
     // a grad-carrying variable is dropped in place (module.cpp:215); its rows are the
     // first (elem_end - elem_begin) elements of the local variable
@@ -67,10 +83,30 @@ void SparseMatmul::forward(bool training, const Stream &s) const {
   const uint64_t *mask = training ? drop->state().mask.get() : nullptr;
   const long long base = drop->state().mask_base;
   const float scale = drop->scale();
+  if (training && ahead_valid) {  // computed by the eval forward before this one
+    std::swap(c->dev_data, ahead);
+    ahead_valid = false;
+    return;
+  }
+  if (!training && ctx->train_ahead && x->dense && x->maskT && !drop->drawn_ahead()) {
+    // eval forward + the next training forward's product, one pass over X
+    if (!ahead) {
+      ahead.allocate(c->dev_data.size());
+      ahead.zero();  // rows past x->rows (edge-cut padding) and padding columns stay zero
+    }
+    drop->draw_ahead(s);
+    const uint64_t *m = drop->state().mask.get();
+    launch_mask_nibbles(m, base, x->cols, x->rows, x->cols, x->maskT.get(), s.get());
+    launch_xstream_nn(x->rows, b->cols, x->cols, x->x.get(), x->ldx, b->dev_data.get(), b->ld, 0,
+                      c->dev_data.get(), c->ld, x->maskT.get(), scale, s.get(), ahead.get());
+    ahead_valid = true;
+    return;
+  }
   if (x->dense && x->maskT) {  // X-stream kernels (N <= 16, K <= 640)
     if (mask) launch_mask_nibbles(mask, base, x->cols, x->rows, x->cols, x->maskT.get(), s.get());
     launch_xstream_nn(x->rows, b->cols, x->cols, x->x.get(), x->ldx, b->dev_data.get(), b->ld, 0,
-                      c->dev_data.get(), c->ld, mask ? x->maskT.get() : nullptr, scale, s.get());
+                      c->dev_data.get(), c->ld, mask ? x->maskT.get() : nullptr, scale, s.get(),
+                      nullptr);
   } else if (x->dense) {
     launch_gemm_nn(x->rows, b->cols, x->cols, x->x.get(), x->ldx, b->dev_data.get(), b->ld, 0,
                    c->dev_data.get(), c->ld, mask, base, x->cols, scale, s.get());

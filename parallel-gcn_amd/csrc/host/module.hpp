@@ -79,6 +79,7 @@ class Module {
 
 // Shared per-GCN state the modules read (current split, comm, profiling, RNG table).
 struct ModuleContext {
+  bool train_ahead = true;     // eval computes the next training forward's first product too
   const int *truth = nullptr;  // current split's truth (device)
   int count = 0;               // labelled rows of the current split (global)
   float *xent_partials = nullptr;
@@ -108,6 +109,14 @@ class Dropout : public Module {
   void backward(const Stream &s) const override;
   float scale() const { return 1.0f / (1.0f - p); }
   const DropoutRng &state() const { return *rng; }
+  // Draws the NEXT training forward's mask now (the xorshift stream position is the same
+  // whenever it is drawn); that forward then uses it instead of drawing again.
+  void draw_ahead(const Stream &s) const;
+  bool drawn_ahead() const { return ahead; }
+
+ private:
+  void draw(const Stream &s) const;
+  mutable bool ahead = false;
 };
 
 // include/module.cuh:47-68: c = drop(X) * W
@@ -117,6 +126,11 @@ class SparseMatmul : public Module {
   const Dropout *drop;  // the input Dropout (its mask, when training)
   ModuleContext *ctx;
   mutable bool last_training = false;
+  // train-ahead (dense X-stream path): an eval forward also computes the next training
+  // forward's drop(X) W into `ahead` (same weights: no optimizer step between them), which
+  // that forward then swaps in instead of streaming X again
+  mutable DeviceBuffer<float> ahead;
+  mutable bool ahead_valid = false;
 
  public:
   SparseMatmul(const DevFeatures *x_, shared_ptr<Variable> b_, shared_ptr<Variable> c_,

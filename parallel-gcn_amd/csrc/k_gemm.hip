@@ -161,13 +161,18 @@ __global__ __launch_bounds__(256) void k_mask_nibbles(const uint64_t *__restrict
 // group's loads in flight while the other computes.  B^T lives in LDS for the block's life:
 // bt[j][k], row stride S = 8 mod 16 dwords, so the per-step float4 B operand read
 // bt[i][16 s + 4 g ..] is conflict-free.  MFMA t of step s reduces k = 16 s + 4 g + t.
-template <int KC, bool MASKED>
+// DUAL (with MASKED): C = X W and C2 = drop(X) W from one pass over X -- the eval forward and
+// the next training forward of the first layer share their weights (no optimizer step between
+// them), so the engine computes both while X streams by once.  C2's MFMAs see exactly the
+// operands of the MASKED kernel, in the same order: bit-identical to it.
+template <int KC, bool MASKED, bool DUAL = false>
 __global__ __launch_bounds__(256, 2) void k_xstream_nn(int M, int N, int K, int S,
                                                        const float *__restrict__ A, int lda,
                                                        const float *__restrict__ B, int ldb,
                                                        int trans_b, float *__restrict__ C,
                                                        int ldc, const uint64_t *__restrict__ maskT,
-                                                       float a_scale) {
+                                                       float a_scale, float *__restrict__ C2 = nullptr) {
+  static_assert(!DUAL || MASKED, "dual: the second product is the masked one");
   constexpr int NS = 4 * KC;  // 16-wide k-steps (the last ones may be past K)
   extern __shared__ float bt[];
   for (int e = threadIdx.x; e < 16 * NS * 16; e += 256) {
@@ -201,7 +206,7 @@ __global__ __launch_bounds__(256, 2) void k_xstream_nn(int M, int N, int K, int 
       }
     }
     __builtin_amdgcn_sched_barrier(0);  // keep the B reads out of the load phase (VGPRs)
-    floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
+    floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f}, acc2 = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < NS; s++) {
       const int kb = 16 * s + 4 * g;
@@ -211,20 +216,30 @@ __global__ __launch_bounds__(256, 2) void k_xstream_nn(int M, int N, int K, int 
         if (kb + 3 > K) a[s].z = 0.f;
         if (kb + 4 > K) a[s].w = 0.f;
       }
+      const float4 b = *reinterpret_cast<const float4 *>(bl + 16 * s);
+      if constexpr (DUAL) {
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s].x, b.x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s].y, b.y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s].z, b.z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s].w, b.w, acc, 0, 0, 0);
+      }
       if constexpr (MASKED)
         apply4(a[s], (uint32_t)(mw[s & 3] >> (4 * (s >> 2))) & 0xfu, a_scale);
-      const float4 b = *reinterpret_cast<const float4 *>(bl + 16 * s);
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s].x, b.x, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s].y, b.y, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s].z, b.z, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s].w, b.w, acc, 0, 0, 0);
+      floatx4 &am = DUAL ? acc2 : acc;
+      am = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s].x, b.x, am, 0, 0, 0);
+      am = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s].y, b.y, am, 0, 0, 0);
+      am = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s].z, b.z, am, 0, 0, 0);
+      am = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s].w, b.w, am, 0, 0, 0);
     }
     // lane holds C[16 rg + 4g + r][i]
     if (i < ldc) {
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         const long long rr = rg * 16 + 4 * g + r;
-        if (rr < M) C[rr * ldc + i] = acc[r];
+        if (rr < M) {
+          C[rr * ldc + i] = acc[r];
+          if constexpr (DUAL) C2[rr * ldc + i] = acc2[r];
+        }
       }
     }
   }
@@ -511,8 +526,9 @@ void launch_mask_nibbles(const uint64_t *mask, long long mask_base, long long ma
 
 void launch_xstream_nn(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
                        int trans_b, float *C, int ldc, const uint64_t *maskT, float a_scale,
-                       hipStream_t s) {
+                       hipStream_t s, float *C2) {
   PGCN_CHECK(xstream_ok(N, K), PGCN_E_INVALID, "xstream_nn: needs N <= 16, K <= 640");
+  PGCN_CHECK(!C2 || maskT, PGCN_E_INVALID, "xstream_nn: the dual product needs the mask");
   PGCN_CHECK(lda % 4 == 0 && lda >= K, PGCN_E_INVALID, "gemm: lda must be a multiple of 4 >= K");
   if (M <= 0) return;
   const int kc = (K + 63) / 64, S = xs_stride(K);
@@ -521,12 +537,15 @@ void launch_xstream_nn(int M, int N, int K, const float *A, int lda, const float
   const size_t lds = (size_t)16 * S * sizeof(float);
 #define XNN_CASE(KC)                                                                          \
   case KC:                                                                                    \
-    if (maskT)                                                                                \
+    if (C2)                                                                                   \
+      hipLaunchKernelGGL((k_xstream_nn<KC, true, true>), grid, block, lds, s, M, N, K, S, A,  \
+                         lda, B, ldb, trans_b, C, ldc, maskT, a_scale, C2);                   \
+    else if (maskT)                                                                           \
       hipLaunchKernelGGL((k_xstream_nn<KC, true>), grid, block, lds, s, M, N, K, S, A, lda, B, \
-                         ldb, trans_b, C, ldc, maskT, a_scale);                               \
+                         ldb, trans_b, C, ldc, maskT, a_scale, nullptr);                      \
     else                                                                                      \
       hipLaunchKernelGGL((k_xstream_nn<KC, false>), grid, block, lds, s, M, N, K, S, A, lda,   \
-                         B, ldb, trans_b, C, ldc, maskT, a_scale);                            \
+                         B, ldb, trans_b, C, ldc, maskT, a_scale, nullptr);                   \
     break;
   switch (kc) {
     XNN_CASE(1) XNN_CASE(2) XNN_CASE(3) XNN_CASE(4) XNN_CASE(5)
@@ -542,7 +561,7 @@ void launch_gemm_nn(int M, int N, int K, const float *A, int lda, const float *B
   PGCN_CHECK(N <= 128 && N >= 1, PGCN_E_INVALID, "gemm: N must be in [1,128]");
   if (M <= 0) return;
   if (!a_mask && xstream_ok(N, K)) {
-    launch_xstream_nn(M, N, K, A, lda, B, ldb, trans_b, C, ldc, nullptr, 1.0f, s);
+    launch_xstream_nn(M, N, K, A, lda, B, ldb, trans_b, C, ldc, nullptr, 1.0f, s, nullptr);
     return;
   }
   const int nt = (N + 15) / 16;

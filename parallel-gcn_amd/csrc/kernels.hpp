@@ -66,7 +66,7 @@ void launch_mask_nibbles(const uint64_t *mask, long long mask_base, long long ma
                          int K, uint64_t *out, hipStream_t s);
 void launch_xstream_nn(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
                        int trans_b, float *C, int ldc, const uint64_t *maskT, float a_scale,
-                       hipStream_t s);
+                       hipStream_t s, float *C2 = nullptr);  // C2: drop(X) W beside C = X W
 void launch_xstream_tn(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
                        float *C, int ldc, const uint64_t *maskT, float a_scale, void *workspace,
                        hipStream_t s);

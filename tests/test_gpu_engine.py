@@ -177,3 +177,31 @@ def test_async_epochs_match_sync(loaded, pgcn):
     np.testing.assert_allclose(res[:, 0], gold[:10, 0], rtol=1e-4)
     np.testing.assert_allclose(res[:, 2], gold[:10, 2], rtol=1e-4)
     g.close()
+
+
+def test_train_ahead_bit_identical(pgcn):
+    """Train-ahead (eval's first-layer pass also computes the next training forward's
+    drop(X) W1, one stream over dense X) changes nothing: the same bits as separate passes,
+    including an eval repeated before the next training epoch and an epoch without eval."""
+    ds = pgcn.Dataset.synthetic(20000, 96, 8, 300000, 5)  # dense N(0,1) features
+    p = pgcn.make_params(ds)
+    runs = []
+    for ahead in (1, 0):
+        pgcn.lib.pgcn_debug_set(b"train_ahead", ahead)
+        g = pgcn.GCN(p, ds, device=0)
+        lines = []
+        for e in range(6):
+            lines.append(g.train_epoch())
+            if e != 3:  # epoch 3: no eval, so no product ahead
+                lines.append(g.eval(2))
+            if e == 1:
+                lines.append(g.eval(3))  # a second eval: the product ahead is kept
+        for _ in range(3):
+            g.epoch_async()
+        lines.append(tuple(g.results(3).ravel()))
+        lines.append(tuple(g.get_var(2).ravel()))  # W1
+        runs.append(lines)
+        g.close()
+    pgcn.lib.pgcn_debug_set(b"train_ahead", 1)
+    for a, b in zip(*runs):
+        np.testing.assert_array_equal(np.asarray(a, np.float32), np.asarray(b, np.float32))

@@ -284,7 +284,8 @@ def nibble_mask_ref(mask, base, M, K):
 @pytest.mark.parametrize("M,N,K,base", [(3001, 16, 602, 0), (1000, 16, 602, 41), (77, 12, 100, 63),
                                         (129, 16, 640, 5), (20, 3, 7, 0)])
 def test_gemm_xstream(pgcn, M, N, K, base):
-    """X-stream NN/TN kernels with nibble-layout dropout bits vs fp64 references."""
+    """X-stream NN/TN kernels with nibble-layout dropout bits vs fp64 references; the dual NN
+    kernel bit-identical to the plain and masked ones."""
     rng = np.random.default_rng(7 * M + K)
     lda = (K + 3) // 4 * 4
     A = np.zeros((M, lda), np.float32)
@@ -303,6 +304,7 @@ def test_gemm_xstream(pgcn, M, N, K, base):
                                   nibble_mask_ref(mask, base, M, K))
     ldc = (N + 3) // 4 * 4
     ws = torch.empty(pgcn.lib.pgcn_gemm_tn_workspace(M, N, K) // 4 + 16, device=DEV)
+    outs = {}
     for drop in (False, True):
         Ae = A[:, :K].astype(np.float64) * (np.where(keep, 2.0, 0.0) if drop else 1.0)
         C = torch.full((M, ldc), float("nan"), device=DEV)
@@ -321,6 +323,14 @@ def test_gemm_xstream(pgcn, M, N, K, base):
         ref_t = Ae.T @ Gm.astype(np.float64)
         bound_t = np.abs(Ae).T @ np.abs(Gm.astype(np.float64))
         assert (np.abs(W.cpu().numpy() - ref_t) <= 1e-5 * bound_t + 1e-30).all()
+        outs[drop] = C
+    # the dual kernel (eval + next training product in one pass) is bit-identical to both
+    C1 = torch.full((M, ldc), float("nan"), device=DEV)
+    C2 = torch.full((M, ldc), float("nan"), device=DEV)
+    pgcn.check(pgcn.lib.pgcn_gemm_xstream_dual(M, N, K, vp(dA), lda, vp(dB), N, 0, vp(C1), vp(C2),
+                                               ldc, vp(nib), 2.0, stream()), "xnn dual")
+    torch.cuda.synchronize()
+    assert torch.equal(C1, outs[False]) and torch.equal(C2, outs[True])
 
 
 def test_spmm_csr_and_csc_bit_exact(pgcn, loaded):
