@@ -242,6 +242,10 @@ long long pgcn_debug_read(const char *key, void *dst, long long max_elems);
  * error of the row sums against a direct CSR sum, and the number of 4-step entry blocks. */
 int pgcn_debug_lds_check(int n_rows, int n_cols, const int *indptr, const int *indices,
                          int window, double *max_rel_err, long long *n_blocks);
+/* Host-only: the same schedule's per-(workgroup, slice, wave, slot) step counts (uint16, up to
+ * cap) and its shape {n_batches, t_max, waves, slots, window}; returns the count or -1. */
+long long pgcn_debug_lds_counts(int n_rows, int n_cols, const int *indptr, const int *indices,
+                                int window, unsigned short *dst, long long cap, int *shape5);
 
 #ifdef __cplusplus
 }

@@ -118,6 +118,8 @@ _sig("pgcn_debug_set", c_int, ctypes.c_char_p, c_int)
 _sig("pgcn_debug_read", c_ll, ctypes.c_char_p, c_void_p, c_ll)
 _sig("pgcn_debug_lds_check", c_int, c_int, c_int, c_void_p, c_void_p, c_int, P(ctypes.c_double),
      P(c_ll))
+_sig("pgcn_debug_lds_counts", c_ll, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_ll,
+     c_void_p)
 _sig("pgcn_partition_bounds", c_int, c_int, c_void_p, c_int, c_void_p, P(c_int))
 _sig("pgcn_partition_subgraph", c_ll, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p,
      c_void_p, c_void_p)
@@ -364,5 +366,5 @@ EXPORTED = [
     "pgcn_gcn_get_var", "pgcn_gcn_num_vars", "pgcn_gcn_profile", "pgcn_gcn_profile_read",
     "pgcn_gcn_node_range", "pgcn_dataset_load", "pgcn_dataset_synthetic", "pgcn_dataset_view",
     "pgcn_dataset_free", "pgcn_partition_bounds", "pgcn_partition_subgraph", "pgcn_debug_set",
-    "pgcn_debug_read", "pgcn_debug_lds_check",
+    "pgcn_debug_read", "pgcn_debug_lds_check", "pgcn_debug_lds_counts",
 ]

@@ -20,6 +20,7 @@ extern int g_graphsum_variant;      // k_graphsum.hip (diagnostics)
 extern int g_graphsum_force_plain;  // host/graph.cpp (diagnostics)
 extern int g_gemm_variant;          // k_gemm.hip (diagnostics)
 extern int g_train_ahead;           // host/gcn.cpp
+extern int g_split_rows;            // host/gcn.cpp
 extern int g_graphsum_lds;          // host/graph.cpp (diagnostics)
 extern int g_graphsum_lds_order;    // host/graph.cpp (diagnostics)
 extern int g_graphsum_lds_diag;     // k_graphsum_lds.hip (diagnostics)
@@ -449,6 +450,7 @@ int pgcn_debug_set(const char *key, int value) {
   else if (!std::strcmp(key, "graphsum_lds_opt")) pgcn::g_graphsum_lds_opt = value;
   else if (!std::strcmp(key, "gemm_variant")) pgcn::g_gemm_variant = value;
   else if (!std::strcmp(key, "train_ahead")) pgcn::g_train_ahead = value;
+  else if (!std::strcmp(key, "split_rows")) pgcn::g_split_rows = value;
   else return PGCN_E_INVALID;
   return PGCN_OK;
 }
@@ -456,6 +458,29 @@ int pgcn_debug_set(const char *key, int value) {
 // CPU check of the d = 16 LDS schedule of a CSR pattern: builds it (window 1 or 2), walks it
 // as the kernel does over a seeded input and reports the max relative error of the sums
 // against a direct CSR sum, and the number of entry blocks.  No device needed.
+// Diagnostics: the LDS schedule's step counts [wg][t_max][LDS_CW][LDS_SLOTS] (uint16) and its
+// shape {n_batches, t_max, LDS_CW, LDS_SLOTS, window} (schedule-balance analysis on the host).
+long long pgcn_debug_lds_counts(int n_rows, int n_cols, const int *indptr, const int *indices,
+                                int window, unsigned short *dst, long long cap, int *shape5) {
+  long long n = -1;
+  const int st = guarded([&] {
+    PGCN_CHECK(n_rows > 0 && n_cols > 0 && indptr && indices, PGCN_E_INVALID, "lds_counts args");
+    std::vector<int> ip(indptr, indptr + n_rows + 1), ix(indices, indices + indptr[n_rows]);
+    const std::vector<int> cut = column_cuts(n_cols, ix);
+    const LdsHost h = build_lds_host(n_rows, n_cols, ip, ix, cut, window);
+    n = (long long)h.counts.size();
+    if (dst) std::copy(h.counts.begin(), h.counts.begin() + std::min(n, cap), dst);
+    if (shape5) {
+      shape5[0] = h.n_batches;
+      shape5[1] = h.t_max;
+      shape5[2] = LDS_CW;
+      shape5[3] = LDS_SLOTS;
+      shape5[4] = h.window;
+    }
+  });
+  return st == PGCN_OK ? n : -1;
+}
+
 int pgcn_debug_lds_check(int n_rows, int n_cols, const int *indptr, const int *indices,
                          int window, double *max_rel_err, long long *n_blocks) {
   return guarded([&] {

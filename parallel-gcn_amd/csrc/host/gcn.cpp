@@ -15,6 +15,9 @@ namespace pgcn {
 // "train_ahead" (pgcn_debug_set, read at engine build): eval's first-layer forward also
 // computes the next training forward's product (SparseMatmul, one pass over dense X)
 int g_train_ahead = 1;
+// "split_rows" (read at each split switch): the output layer's GraphSum forward computes only
+// the current split's labelled rows
+int g_split_rows = 1;
 
 // ------------------------------------------------------------------------------------------
 // Adam (src/optim.cu:7-95; hpdga optim.cpp:16-35)
@@ -265,6 +268,9 @@ void GCN::build(const GCNData &data) {
       t[(size_t)i] = data.split[(size_t)first + i] == s ? data.label[(size_t)first + i] : -1;
     truth[s].allocate(t.size());
     truth[s].upload(t);
+    split_rows_host[s].clear();
+    for (int i = 0; i < rows; i++)
+      if (t[(size_t)i] >= 0) split_rows_host[s].push_back(i);
     int c = 0;
     for (int i = 0; i < N; i++) c += (data.split[(size_t)i] == s && data.label[(size_t)i] >= 0);
     counts[s] = c;
@@ -371,7 +377,7 @@ void GCN::insert_last_layer() {
     auto z = std::make_shared<Variable>(prow, hl, true, round_up4(hl));
     variables.push_back(z);
     variables.push_back(weights.back());
-    modules.push_back(std::make_unique<GraphSum>(prev, z, graph.get(), hl, &ctx));
+    modules.push_back(std::make_unique<GraphSum>(prev, z, graph.get(), hl, &ctx, true));
     auto out = std::make_shared<Variable>(prow, C, true, round_up4(C));
     variables.push_back(out);
     modules.push_back(std::make_unique<Matmul>(z, weights.back(), out, part.local_rows(), hl, C,
@@ -386,7 +392,7 @@ void GCN::insert_last_layer() {
                                              C, &ctx));
   auto out = std::make_shared<Variable>(prow, C, true, round_up4(C));
   variables.push_back(out);
-  modules.push_back(std::make_unique<GraphSum>(var1, out, graph.get(), C, &ctx));
+  modules.push_back(std::make_unique<GraphSum>(var1, out, graph.get(), C, &ctx, true));
   modules.push_back(std::make_unique<CrossEntropyLoss>(out, C, &ctx));
 }
 
@@ -394,6 +400,19 @@ void GCN::set_split(int split) {
   ctx.truth = truth[split].get();
   ctx.count = counts[split];
   modules.back()->set_num_samples(counts[split]);
+  // output-layer row restriction: Â restricted to the split's labelled rows, built at the
+  // split's first use (single GPU; the edge-cut engine sums all rows)
+  ctx.split_graph = nullptr;
+  ctx.split_rows = nullptr;
+  if (g_split_rows && !comm && graph) {
+    if (!split_graphs[split]) {
+      split_graphs[split] = graph->row_subset(split_rows_host[split]);
+      split_rows_dev[split].allocate(std::max<size_t>(split_rows_host[split].size(), 1));
+      split_rows_dev[split].upload(split_rows_host[split]);
+    }
+    ctx.split_graph = split_graphs[split].get();
+    ctx.split_rows = split_rows_dev[split].get();
+  }
 }
 
 // loss/acc of the pass just enqueued -> results_ring slot (finalize, src/gcn.cu:440-455)

@@ -233,6 +233,29 @@ DevGraph::Sched &DevGraph::schedule(int vec) {
   return ref;
 }
 
+std::unique_ptr<DevGraph> DevGraph::row_subset(const std::vector<int> &rows) const {
+  std::vector<int> ip(rows.size() + 1, 0), ix;
+  std::vector<float> v;
+  for (size_t r = 0; r < rows.size(); r++) {
+    const int i = rows[r];
+    PGCN_CHECK(i >= 0 && i < n_rows_, PGCN_E_INVALID, "row_subset: row id");
+    ip[r + 1] = ip[r] + (h_indptr_[(size_t)i + 1] - h_indptr_[(size_t)i]);
+  }
+  ix.reserve((size_t)ip.back());
+  v.reserve((size_t)ip.back());
+  for (int i : rows) {
+    ix.insert(ix.end(), h_indices_.begin() + h_indptr_[(size_t)i], h_indices_.begin() + h_indptr_[(size_t)i + 1]);
+    v.insert(v.end(), h_vals_.begin() + h_indptr_[(size_t)i], h_vals_.begin() + h_indptr_[(size_t)i + 1]);
+  }
+  auto g = std::make_unique<DevGraph>((int)rows.size(), n_cols_, ip.data(), ix.data(), v.data());
+  if (!h_row_scale_.empty()) {
+    std::vector<float> rs(rows.size());
+    for (size_t r = 0; r < rows.size(); r++) rs[r] = h_row_scale_[(size_t)rows[r]];
+    g->set_scales(std::move(rs), h_col_scale_);
+  }
+  return g;
+}
+
 void DevGraph::set_scales(std::vector<float> row_scale, std::vector<float> col_scale) {
   PGCN_CHECK((int)row_scale.size() == n_rows_ && (int)col_scale.size() == n_cols_,
              PGCN_E_INVALID, "set_scales: sizes");

@@ -71,6 +71,9 @@ class DevGraph {
   // Enables the d = 16 LDS path (k_graphsum_lds): out_i = row_scale_i * sum_j col_scale_j
   // in_j over the CSR pattern, i.e. vals_ij = row_scale_i * col_scale_j.
   void set_scales(std::vector<float> row_scale, std::vector<float> col_scale);
+  // The rows `rows` (ascending) of this CSR as a graph of its own: same columns, values and
+  // scales, row r of the result = row rows[r] here.
+  std::unique_ptr<DevGraph> row_subset(const std::vector<int> &rows) const;
 
   static constexpr int kBlocks = kGraphBlocks;   // one column block per XCD
   static constexpr double kL2Budget = 4.0e6;     // table bytes that stay plain

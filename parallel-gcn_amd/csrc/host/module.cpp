@@ -140,8 +140,9 @@ void SparseMatmul::backward(const Stream &s) const {
 // GraphSum (src/module.cu:168-210; hpdga module.cpp:82-111)
 // ------------------------------------------------------------------------------------------
 GraphSum::GraphSum(shared_ptr<Variable> in_, shared_ptr<Variable> out_, DevGraph *graph_,
-                   int dim_, ModuleContext *ctx_)
-    : in(std::move(in_)), out(std::move(out_)), graph(graph_), dim(dim_), ctx(ctx_) {
+                   int dim_, ModuleContext *ctx_, bool last_layer_)
+    : in(std::move(in_)), out(std::move(out_)), graph(graph_), dim(dim_), ctx(ctx_),
+      last_layer(last_layer_) {
   if (ctx->comm) {
     for (DevGraph *gk : ctx->chunk_graphs) {
       partial.emplace_back();
@@ -190,7 +191,30 @@ void GraphSum::run(const float *src, float *dst, const Stream &s) const {
 }
 
 void GraphSum::forward(bool, const Stream &s) const {
-  run(in->dev_data.get(), out->dev_data.get(), s);
+  DevGraph *sg = last_layer && !ctx->comm ? ctx->split_graph : nullptr;
+  if (!sg) {
+    run(in->dev_data.get(), out->dev_data.get(), s);
+    return;
+  }
+  // output layer: only the split's labelled rows, summed compactly and scattered to their
+  // rows; the other rows keep their last (finite) values, which meet only zero loss-gradient
+  // rows in Matmul::backward and are skipped by the loss
+  const size_t need = (size_t)std::max(sg->rows(), 1) * out->ld;
+  if (compact.size() < need) compact.allocate(need);
+  Event e0, e1;
+  if (ctx->profile) {
+    e0 = Event::create(true);
+    e1 = Event::create(true);
+    e0.record(s.get());
+  }
+  sg->graphsum(in->dev_data.get(), in->ld, compact.get(), out->ld, dim, s.get());
+  if (ctx->profile) {
+    e1.record(s.get());
+    ctx->gs_events->emplace_back(e0, e1);
+    ctx->gs_bytes->push_back(sg->algorithmic_bytes(dim));
+  }
+  launch_scatter_rows(compact.get(), ctx->split_rows, sg->rows(), out->ld, out->dev_data.get(),
+                      s.get());
 }
 
 void GraphSum::backward(const Stream &s) const {

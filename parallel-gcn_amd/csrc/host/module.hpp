@@ -80,6 +80,11 @@ class Module {
 // Shared per-GCN state the modules read (current split, comm, profiling, RNG table).
 struct ModuleContext {
   bool train_ahead = true;     // eval computes the next training forward's first product too
+  // output-layer row restriction (single GPU): the last GraphSum's forward computes only the
+  // current split's labelled rows -- the only rows the loss, the accuracy and (through the
+  // loss gradient, zero elsewhere) the weight gradients depend on
+  DevGraph *split_graph = nullptr;  // Â restricted to those rows (null: all rows)
+  const int *split_rows = nullptr;  // their row ids (device)
   const int *truth = nullptr;  // current split's truth (device)
   int count = 0;               // labelled rows of the current split (global)
   float *xent_partials = nullptr;
@@ -145,6 +150,8 @@ class GraphSum : public Module {
   DevGraph *graph;
   int dim;
   ModuleContext *ctx;
+  bool last_layer;                   // the output layer's GraphSum (row restriction applies)
+  mutable DeviceBuffer<float> compact;  // restricted forward: [split rows][out->ld]
   // edge-cut: per row chunk, the [world*chunk_rows][ld] partial sums and their events
   std::vector<DeviceBuffer<float>> partial;
   std::vector<Event> computed;
@@ -152,7 +159,7 @@ class GraphSum : public Module {
 
  public:
   GraphSum(shared_ptr<Variable> in_, shared_ptr<Variable> out_, DevGraph *graph_, int dim_,
-           ModuleContext *ctx_);
+           ModuleContext *ctx_, bool last_layer_ = false);
   void forward(bool training, const Stream &s) const override;
   void backward(const Stream &s) const override;
 

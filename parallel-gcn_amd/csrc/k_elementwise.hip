@@ -19,15 +19,22 @@ namespace pgcn {
 // Dropout masks: one thread per 64-draw chunk.  The chunk state is the xorshift128+ state at
 // the draw element 64*c consumes (hpdga module.cpp:213-217 consumes one draw per element, in
 // index order). After emitting the 64 mask bits the state is advanced by one epoch's worth
-// of draws (`period`) with 16 byte-table lookups (table = 64 KB, staged in LDS).
+// of draws (`period`) with 32 nibble-table lookups.  The nibble tables (32 x 16 x 16 B = 8 KB
+// in LDS) are read out of the byte tables M^period (16 x 256 entries): by linearity over
+// GF(2), nibble p = v of the state maps to byte entry (p/2, v << 4(p%2)).  8 KB instead of
+// the 64-KB byte tables keeps 8 workgroups per CU resident: each draw is a serial chain of
+// 64-bit xor/shift ops, so the kernel needs the waves to hide it.
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_dropout_mask(uint64_t *__restrict__ states,
                                                       long long n_chunks, long long elem0,
                                                       long long elem_end, int threshold,
                                                       uint64_t *__restrict__ mask,
                                                       const uint4 *__restrict__ table) {
-  __shared__ uint4 lut[16 * 256];
-  for (int i = threadIdx.x; i < 16 * 256; i += blockDim.x) lut[i] = table[i];
+  __shared__ uint4 lut[32 * 16];
+  for (int i = threadIdx.x; i < 32 * 16; i += blockDim.x) {
+    const int p = i >> 4, v = i & 15;
+    lut[i] = table[(p >> 1) * 256 + (v << (4 * (p & 1)))];
+  }
   __syncthreads();
   for (long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x; c < n_chunks;
        c += (long long)gridDim.x * blockDim.x) {
@@ -54,14 +61,14 @@ __global__ __launch_bounds__(256) void k_dropout_mask(uint64_t *__restrict__ sta
     // advance the chunk state by `period` draws: M^period * (a0, a1)
     uint64_t n0 = 0, n1 = 0;
 #pragma unroll
-    for (int b = 0; b < 8; b++) {
-      const uint4 v = lut[b * 256 + ((a0 >> (8 * b)) & 0xff)];
+    for (int q = 0; q < 16; q++) {
+      const uint4 v = lut[q * 16 + ((a0 >> (4 * q)) & 0xf)];
       n0 ^= ((uint64_t)v.y << 32) | v.x;
       n1 ^= ((uint64_t)v.w << 32) | v.z;
     }
 #pragma unroll
-    for (int b = 0; b < 8; b++) {
-      const uint4 v = lut[(8 + b) * 256 + ((a1 >> (8 * b)) & 0xff)];
+    for (int q = 0; q < 16; q++) {
+      const uint4 v = lut[(16 + q) * 16 + ((a1 >> (4 * q)) & 0xf)];
       n0 ^= ((uint64_t)v.y << 32) | v.x;
       n1 ^= ((uint64_t)v.w << 32) | v.z;
     }
@@ -101,6 +108,27 @@ __global__ __launch_bounds__(256) void k_dropout_apply(float *__restrict__ x, lo
       x[i] *= ((mask[b >> 6] >> (b & 63)) & 1) ? scale : 0.0f;
     }
   }
+}
+
+// Row scatter of the output layer's restricted GraphSum: out[rows[r]] = src[r] (float4s).
+__global__ __launch_bounds__(256) void k_scatter_rows(const float4 *__restrict__ src,
+                                                      const int *__restrict__ rows, int n, int ld4,
+                                                      float4 *__restrict__ out) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long long)n * ld4) return;
+  const long long r = t / ld4;
+  const int q = (int)(t - r * ld4);
+  out[(long long)rows[r] * ld4 + q] = src[t];
+}
+
+void launch_scatter_rows(const float *src, const int *rows, int n, int ld, float *out,
+                         hipStream_t s) {
+  PGCN_CHECK(ld % 4 == 0, PGCN_E_INVALID, "scatter_rows: ld % 4");
+  if (n <= 0) return;
+  const long long tot = (long long)n * (ld / 4);
+  hipLaunchKernelGGL(k_scatter_rows, dim3((unsigned)ceil_div(tot, 256)), dim3(256), 0, s,
+                     reinterpret_cast<const float4 *>(src), rows, n, ld / 4,
+                     reinterpret_cast<float4 *>(out));
 }
 
 // ReLU (hpdga module.cpp:173-188)
@@ -148,69 +176,81 @@ __device__ __forceinline__ float block_sum(float v, float *smem) {
 
 // ------------------------------------------------------------------------------------------
 // Cross entropy (hpdga module.cpp:122-153) + accuracy (hpdga gcn.cpp:150-164), one thread
-// per row. Labelled rows are max-shifted in place like the reference; the grad is written
-// divided by the labelled count (known per split on the host). Per-block partial sums
-// (loss, wrong) go to partials[2*block].
+// per row, every thread of the block computing (XR = 256 rows).  Labelled rows are
+// max-shifted in place like the reference; the grad is written divided by the labelled count
+// (known per split on the host).  Rows go through ONE LDS tile [XR][ld+1] (row stride ld+1:
+// conflict-free per-row reads) with coalesced copies: logits in, shifted logits out, then the
+// grad computed in place and copied out.  Per-block partial sums (loss, wrong) go to
+// partials[2*block].
 // ------------------------------------------------------------------------------------------
-constexpr int XR = 64;  // rows per cross-entropy block (one computing wave)
+constexpr int XR = 256;  // rows per cross-entropy block (= threads)
 
 __global__ __launch_bounds__(256) void k_xent_fwd(float *__restrict__ logits, int ld,
                                                   float *__restrict__ grad,
                                                   const int *__restrict__ truth, int n, int c,
                                                   int count, int training,
                                                   float *__restrict__ partials) {
-  // The block's XR rows are staged through LDS with coalesced loads/stores (row stride
-  // ld+1 floats: conflict-free per-row reads); one thread per row computes in LDS.
   extern __shared__ float smem[];
   __shared__ float red[4];
   const int S = ld + 1;
-  float *L = smem;            // [XR][S] logits
-  float *Gr = smem + XR * S;  // [XR][S] grad
+  float *L = smem;  // [XR][S]
   const long long row0 = (long long)blockIdx.x * XR;
   const int rows = (int)min((long long)XR, (long long)n - row0);
   const long long base = row0 * ld;
   const int tile = rows * ld;
-  for (int e = threadIdx.x; e < tile; e += 256) {
-    const int r = e / ld, j = e - r * ld;
-    L[r * S + j] = logits[base + e];
-  }
+  // element e = r * ld + j of the tile; e advances by 256 per step (ld <= 124 < 256): no
+  // integer division in the copy loops
+  const int r_start = threadIdx.x / ld, j_start = threadIdx.x - r_start * ld;
+  const int dr = 256 / ld, dj = 256 - dr * ld;
+  auto walk = [&](auto &&f) {
+    int r = r_start, j = j_start;
+    for (int e = threadIdx.x; e < tile; e += 256) {
+      f(e, r * S + j);
+      j += dj;
+      r += dr;
+      if (j >= ld) {
+        j -= ld;
+        r++;
+      }
+    }
+  };
+  walk([&](int e, int o) { L[o] = logits[base + e]; });
   __syncthreads();
-  float loss = 0.0f, wrong = 0.0f;
+  float loss = 0.0f, wrong = 0.0f, se = 0.0f;
   const int t = threadIdx.x < rows ? truth[row0 + threadIdx.x] : -1;
   float *l = L + threadIdx.x * S;
-  float *g = Gr + threadIdx.x * S;
-  if (threadIdx.x < rows) {
-    if (t >= 0) {
-      float mx = -1e30f;
-      for (int j = 0; j < c; j++) mx = fmaxf(mx, l[j]);
-      float se = 0.0f;
-      for (int j = 0; j < c; j++) {
-        const float v = l[j] - mx;
-        l[j] = v;
-        se += expf(v);
-      }
-      const float lt = l[t];
-      loss = logf(se) - lt;
-      bool w = false;
-      for (int j = 0; j < c; j++) w |= l[j] > lt;
-      wrong = w ? 1.0f : 0.0f;
-      if (training) {
+  if (t >= 0) {
+    float mx = -1e30f;
+    for (int j = 0; j < c; j++) mx = fmaxf(mx, l[j]);
+    for (int j = 0; j < c; j++) {
+      const float v = l[j] - mx;
+      l[j] = v;
+      se += expf(v);
+    }
+    const float lt = l[t];
+    loss = logf(se) - lt;
+    bool w = false;
+    for (int j = 0; j < c; j++) w |= l[j] > lt;
+    wrong = w ? 1.0f : 0.0f;
+  }
+  __syncthreads();
+  walk([&](int e, int o) { logits[base + e] = L[o]; });
+  if (training) {
+    __syncthreads();  // the shifted logits have left the tile
+    if (threadIdx.x < rows) {
+      if (t >= 0) {
         for (int j = 0; j < c; j++) {
           float prob = expf(l[j]) / se;
           if (j == t) prob = (float)((double)prob - 1.0);  // hpdga module.cpp:145 (double temp)
-          g[j] = prob / (float)count;
+          l[j] = prob / (float)count;
         }
-        for (int j = c; j < ld; j++) g[j] = 0.0f;
+        for (int j = c; j < ld; j++) l[j] = 0.0f;
+      } else {
+        for (int j = 0; j < ld; j++) l[j] = 0.0f;
       }
-    } else if (training) {
-      for (int j = 0; j < ld; j++) g[j] = 0.0f;
     }
-  }
-  __syncthreads();
-  for (int e = threadIdx.x; e < tile; e += 256) {
-    const int r = e / ld, j = e - r * ld;
-    logits[base + e] = L[r * S + j];
-    if (training) grad[base + e] = Gr[r * S + j];
+    __syncthreads();
+    walk([&](int e, int o) { grad[base + e] = L[o]; });
   }
   const float ls = block_sum<256>(loss, red);
   const float ws = block_sum<256>(wrong, red);
@@ -221,11 +261,11 @@ __global__ __launch_bounds__(256) void k_xent_fwd(float *__restrict__ logits, in
 }
 
 // sums[0] = sum loss partials, sums[1] = sum wrong, sums[2] = sum w^2 (fixed order)
-__global__ __launch_bounds__(256) void k_reduce_scalars(const float *__restrict__ partials,
-                                                        int n_blocks,
-                                                        const float *__restrict__ w,
-                                                        long long n_w, float *__restrict__ sums) {
-  __shared__ float red[4];
+__global__ __launch_bounds__(1024) void k_reduce_scalars(const float *__restrict__ partials,
+                                                         int n_blocks,
+                                                         const float *__restrict__ w,
+                                                         long long n_w, float *__restrict__ sums) {
+  __shared__ float red[16];
   float l = 0.0f, wr = 0.0f, q = 0.0f;
   for (int b = threadIdx.x; b < n_blocks; b += blockDim.x) {
     l += partials[2 * b];
@@ -235,9 +275,9 @@ __global__ __launch_bounds__(256) void k_reduce_scalars(const float *__restrict_
     const float x = w[i];
     q += x * x;
   }
-  l = block_sum<256>(l, red);
-  wr = block_sum<256>(wr, red);
-  q = block_sum<256>(q, red);
+  l = block_sum<1024>(l, red);
+  wr = block_sum<1024>(wr, red);
+  q = block_sum<1024>(q, red);
   if (threadIdx.x == 0) {
     sums[0] = l;
     sums[1] = wr;
@@ -291,7 +331,7 @@ void launch_dropout_mask(uint64_t *states, long long n_chunks, long long elem0,
   if (n_chunks <= 0) return;
   // hpdga module.cpp:211: threshold = int(p * MY_RAND_MAX) evaluated in float
   const int threshold = (int)(p * (float)0x7fffffff);
-  const int grid = grid_for(n_chunks, 256, 1024);
+  const int grid = grid_for(n_chunks, 256, 8 * kCUs);  // 8 KB LDS: 8 workgroups per CU
   hipLaunchKernelGGL(k_dropout_mask, dim3(grid), dim3(256), 0, s, states, n_chunks, elem0,
                      elem_end, threshold, mask, static_cast<const uint4 *>(table));
 }
@@ -319,15 +359,20 @@ void launch_xent_fwd(float *logits, int ld, float *grad, const int *truth, int n
                      int count, int training, float *partials, hipStream_t s) {
   if (n <= 0) return;
   PGCN_CHECK(ld <= 124 && c <= ld, PGCN_E_INVALID, "xent: classes must be <= 124");
-  const size_t lds = (size_t)2 * XR * (ld + 1) * sizeof(float);
-  // <= 2*64*129*4 = 66 KB: within the default dynamic LDS limit for ld <= 124
+  const size_t lds = (size_t)XR * (ld + 1) * sizeof(float);  // <= 256*125*4 = 125 KB
+  static bool attr = false;
+  if (!attr) {
+    PGCN_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(k_xent_fwd),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, 125 * 1024));
+    attr = true;
+  }
   hipLaunchKernelGGL(k_xent_fwd, dim3(xent_blocks(n)), dim3(256), lds, s, logits, ld, grad,
                      truth, n, c, count, training, partials);
 }
 
 void launch_reduce_scalars(const float *partials, int n_blocks, const float *w, long long n_w,
                            float *sums, hipStream_t s) {
-  hipLaunchKernelGGL(k_reduce_scalars, dim3(1), dim3(256), 0, s, partials, n_blocks, w, n_w,
+  hipLaunchKernelGGL(k_reduce_scalars, dim3(1), dim3(1024), 0, s, partials, n_blocks, w, n_w,
                      sums);
 }
 

@@ -141,16 +141,22 @@ __global__ __launch_bounds__(256) void k_mask_nibbles(const uint64_t *__restrict
   const long long m = t >> 4;
   const int j = (int)(t & 15);
   uint64_t word = 0;
-  for (int c = 0; 64 * c + 4 * j < K; c++) {
-    const long long p = mask_base + m * mask_ld + 64 * c + 4 * j;
-    const long long w = p >> 6;
-    const int sh = (int)(p & 63);
-    uint64_t v = mask[w] >> sh;
-    if (sh > 60) v |= mask[w + 1] << (64 - sh);
-    uint64_t nib = v & 0xfu;
-    const int kb = 64 * c + 4 * j;  // keep bits of k >= K are 0
-    if (kb + 4 > K) nib &= (1ull << (K - kb)) - 1;
-    word |= nib << (4 * c);
+  // unrolled over the 16 possible chunks (K <= 1024) so that every load is issued before the
+  // first one is used (a K-bounded loop serialised them: ~1 TB/s)
+  const long long p0 = mask_base + m * mask_ld + 4 * j;
+#pragma unroll
+  for (int c = 0; c < 16; c++) {
+    const int kb = 64 * c + 4 * j;
+    if (kb < K) {
+      const long long p = p0 + 64 * c;
+      const long long w = p >> 6;
+      const int sh = (int)(p & 63);
+      uint64_t v = mask[w] >> sh;
+      if (sh > 60) v |= mask[w + 1] << (64 - sh);
+      uint64_t nib = v & 0xfu;
+      if (kb + 4 > K) nib &= (1ull << (K - kb)) - 1;  // keep bits of k >= K are 0
+      word |= nib << (4 * c);
+    }
   }
   out[t] = word;
 }

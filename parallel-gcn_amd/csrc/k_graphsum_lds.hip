@@ -245,7 +245,7 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
       const char *src = reinterpret_cast<const char *>(in + (long long)sc.x * 4) + lane * 16;
       constexpr int full = LDS_SR / 16;
       if (opt & 1) {
-        constexpr bool stage16 = DIAG == 1 || DIAG == 5 || DIAG == 7;
+        constexpr bool stage16 = DIAG == 1 || DIAG == 5 || DIAG >= 7;
         const int pieces4 = stage16 ? 1 : full / 4;  // DIAG 1/5/7: stage 1/16 (timing only)
 #pragma unroll 4
         for (int i = 0; i < pieces4; i++) glds16x4(src + i * 4096, dst + (unsigned)(i * 4096));
@@ -300,7 +300,7 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
   auto refill = [&](long long c) {  // chunk c -> ring slot c % 4 (clamped: dummy past the end)
     long long cc = c < nchunk ? c : nchunk - 1;
     cc = cc > 0 ? cc : 0;
-    if (DIAG != 7 && lane < 32)  // DIAG 7: no entry stream (timing only)
+    if (DIAG < 7 && lane < 32)  // DIAG 7-9: no entry stream (timing only)
       glds16(ebytes + cc * LDS_RING_CHUNK + lane * 16,
              ring_dst + (unsigned)((c % LDS_RING_SLOTS) * LDS_RING_CHUNK));
   };
@@ -514,14 +514,28 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
         (unsigned)__builtin_amdgcn_readfirstlane(cw0.z), (unsigned)__builtin_amdgcn_readfirstlane(cw0.w),
         (unsigned)__builtin_amdgcn_readfirstlane(cw1.x), (unsigned)__builtin_amdgcn_readfirstlane(cw1.y),
         (unsigned)__builtin_amdgcn_readfirstlane(cw1.z), (unsigned)__builtin_amdgcn_readfirstlane(cw1.w)};
+    if constexpr (DIAG == 9) {  // timing only: the slice's blocks as ONE loop (no slot visits)
+      int nb = 0;
+#pragma unroll
+      for (int j = 0; j < LDS_SLOTS; j++) nb += (((cw[j >> 1] >> (16 * (j & 1))) & 0xffff) + 3) >> 2;
+      for (int k = 0; k < nb; k++) {
+        const uint2 e = e_next;
+        next_block();
+        acc[0].x += __uint_as_float(e.x);
+        acc[0].y += __uint_as_float(e.y);
+      }
+      slice_done(t);
+      continue;
+    }
 #pragma unroll
     for (int j = 0; j < LDS_SLOTS; j++) {
-      const int n = (cw[j >> 1] >> (16 * (j & 1))) & 0xffff;  // steps of rowset j
+      int n = (cw[j >> 1] >> (16 * (j & 1))) & 0xffff;  // steps of rowset j
+      if constexpr (DIAG == 8) n = n < 4 ? n : 4;  // timing only: one block per visit
       for (int k = 0; k < n; k += 4) {
         const uint2 e = e_next;
         next_block();
         // all 4 entries are valid: steps past a row's run point at a zero row
-        if constexpr (DIAG == 2 || DIAG == 5 || DIAG == 7) {  // diagnostic: no table reads
+        if constexpr (DIAG == 2 || DIAG == 5 || DIAG == 7 || DIAG == 8) {  // no table reads
           acc[j].x += __uint_as_float(e.x);
           acc[j].y += __uint_as_float(e.y);
         } else {
@@ -644,6 +658,8 @@ void launch_graphsum_lds(const LdsSchedule &s, const float *in, int ld_in, float
       case 3: GS_LDS(3, 1, 1); break;
       case 5: GS_LDS(5, 1, 1); break;  // no table reads, 1/16 staged
       case 7: GS_LDS(7, 1, 1); break;  // as 5, no entry stream either
+      case 8: GS_LDS(8, 1, 1); break;  // as 7, one block per slot visit
+      case 9: GS_LDS(9, 1, 1); break;  // as 7, one loop over a slice's blocks
       case 4: GS_LDS(4, 1, 1); break;
       default: GS_LDS(0, 1, 1); break;
     }

@@ -67,6 +67,9 @@ void launch_mask_nibbles(const uint64_t *mask, long long mask_base, long long ma
 void launch_xstream_nn(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
                        int trans_b, float *C, int ldc, const uint64_t *maskT, float a_scale,
                        hipStream_t s, float *C2 = nullptr);  // C2: drop(X) W beside C = X W
+// out[rows[r]][0:ld] = src[r][0:ld]  (ld % 4 == 0)
+void launch_scatter_rows(const float *src, const int *rows, int n, int ld, float *out,
+                         hipStream_t s);
 void launch_xstream_tn(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
                        float *C, int ldc, const uint64_t *maskT, float a_scale, void *workspace,
                        hipStream_t s);
