@@ -404,6 +404,7 @@ void GCN::set_split(int split) {
   // split's first use (single GPU; the edge-cut engine sums all rows)
   ctx.split_graph = nullptr;
   ctx.split_rows = nullptr;
+  ctx.split_colgraph = nullptr;
   if (g_split_rows && !comm && graph) {
     if (!split_graphs[split]) {
       split_graphs[split] = graph->row_subset(split_rows_host[split]);
@@ -412,6 +413,10 @@ void GCN::set_split(int split) {
     }
     ctx.split_graph = split_graphs[split].get();
     ctx.split_rows = split_rows_dev[split].get();
+  }
+  if (g_split_rows && !comm && graph && split == 1) {  // backward only follows training
+    if (!split_colgraphs[split]) split_colgraphs[split] = graph->col_subset(split_rows_host[split]);
+    ctx.split_colgraph = split_colgraphs[split].get();
   }
 }
 

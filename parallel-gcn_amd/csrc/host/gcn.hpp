@@ -109,7 +109,7 @@ class GCN {
   // output-layer row restriction (set_split): per split, its labelled rows and Â on them
   std::vector<int> split_rows_host[4];
   DeviceBuffer<int> split_rows_dev[4];
-  std::unique_ptr<DevGraph> split_graphs[4];
+  std::unique_ptr<DevGraph> split_graphs[4], split_colgraphs[4];
   long long nnz_x_global = 0;
   std::vector<int> feat_indptr_global;  // for the input dropout ranges
 

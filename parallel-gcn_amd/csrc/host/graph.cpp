@@ -256,6 +256,40 @@ std::unique_ptr<DevGraph> DevGraph::row_subset(const std::vector<int> &rows) con
   return g;
 }
 
+std::unique_ptr<DevGraph> DevGraph::col_subset(const std::vector<int> &cols) const {
+  std::vector<int> pos((size_t)n_cols_, -1);
+  for (size_t c = 0; c < cols.size(); c++) {
+    PGCN_CHECK(cols[c] >= 0 && cols[c] < n_cols_ && (c == 0 || cols[c] > cols[c - 1]),
+               PGCN_E_INVALID, "col_subset: columns must be ascending ids");
+    pos[(size_t)cols[c]] = (int)c;
+  }
+  std::vector<int> ip((size_t)n_rows_ + 1, 0), ix;
+  std::vector<float> v;
+  for (int i = 0; i < n_rows_; i++) {
+    for (int k = h_indptr_[(size_t)i]; k < h_indptr_[(size_t)i + 1]; k++) {
+      const int c = pos[(size_t)h_indices_[(size_t)k]];
+      if (c < 0) continue;
+      ix.push_back(c);
+      v.push_back(h_vals_[(size_t)k]);
+    }
+    ip[(size_t)i + 1] = (int)ix.size();
+  }
+  if (ix.empty()) {  // keep a valid (empty) CSR
+    ix.push_back(0);
+    v.push_back(0.0f);
+  }
+  auto g = std::make_unique<DevGraph>(n_rows_, std::max((int)cols.size(), 1), ip.data(), ix.data(),
+                                      v.data());
+  if (!h_col_scale_.empty() && !cols.empty()) {
+    std::vector<float> cs(cols.size());
+    for (size_t c = 0; c < cols.size(); c++) cs[c] = h_col_scale_[(size_t)cols[c]];
+    g->set_scales(h_row_scale_, std::move(cs));
+  }
+  g->col_map_.allocate(std::max<size_t>(cols.size(), 1));
+  g->col_map_.upload(cols.empty() ? std::vector<int>{0} : cols);
+  return g;
+}
+
 void DevGraph::set_scales(std::vector<float> row_scale, std::vector<float> col_scale) {
   PGCN_CHECK((int)row_scale.size() == n_rows_ && (int)col_scale.size() == n_cols_,
              PGCN_E_INVALID, "set_scales: sizes");
@@ -811,8 +845,14 @@ void DevGraph::graphsum(const float *in, int ld_in, float *out, int ld_out, int 
       (double)n_cols_ * 64.0 > kL2Budget) {
     if (!lds_) build_lds();
     launch_graphsum_lds(lds_->s, in, ld_in, out, ld_out, lds_->scratch.get(),
-                        lds_->partial.get(), s);
+                        lds_->partial.get(), s, col_map_.get());
     return;
+  }
+  if (col_map_) {  // plain path of a column subset: compact the input rows first
+    const size_t need = (size_t)n_cols_ * ld_in;
+    if (col_in_.size() < need) col_in_.allocate(need);
+    launch_gather_rows(in, col_map_.get(), n_cols_, ld_in, col_in_.get(), s);
+    in = col_in_.get();
   }
   const int vec = (dim + 3) / 4;
   Sched &sc = schedule(vec);

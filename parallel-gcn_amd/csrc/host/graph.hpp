@@ -74,6 +74,10 @@ class DevGraph {
   // The rows `rows` (ascending) of this CSR as a graph of its own: same columns, values and
   // scales, row r of the result = row rows[r] here.
   std::unique_ptr<DevGraph> row_subset(const std::vector<int> &rows) const;
+  // The edges into the columns `cols` (ascending) as a graph over those columns only: its
+  // graphsum() reads input row cols[c] for column c (no compaction by the caller), so it
+  // equals this graph's graphsum on an input that is zero outside `cols`.
+  std::unique_ptr<DevGraph> col_subset(const std::vector<int> &cols) const;
 
   static constexpr int kBlocks = kGraphBlocks;   // one column block per XCD
   static constexpr double kL2Budget = 4.0e6;     // table bytes that stay plain
@@ -101,6 +105,9 @@ class DevGraph {
   };
   std::unique_ptr<LdsSched> lds_;
   std::vector<float> h_row_scale_, h_col_scale_;
+  // column subset: input row of compact column c (device), and the compacted input (plain path)
+  DeviceBuffer<int> col_map_;
+  DeviceBuffer<float> col_in_;
   int n_rows_, n_cols_;
   long long nnz_;
   std::vector<int> h_indptr_, h_indices_;

@@ -219,7 +219,25 @@ void GraphSum::forward(bool, const Stream &s) const {
 
 void GraphSum::backward(const Stream &s) const {
   // the same gather on grads (Â symmetric): in.grad = Â out.grad (module.cpp:98-111)
-  run(out->dev_grad.get(), in->dev_grad.get(), s);
+  DevGraph *cg = last_layer && !ctx->comm ? ctx->split_colgraph : nullptr;
+  if (!cg) {
+    run(out->dev_grad.get(), in->dev_grad.get(), s);
+    return;
+  }
+  // output layer: out.grad is the loss gradient, zero outside the split's labelled rows, so
+  // only the edges into those rows contribute (the column-subset graph gathers them itself)
+  Event e0, e1;
+  if (ctx->profile) {
+    e0 = Event::create(true);
+    e1 = Event::create(true);
+    e0.record(s.get());
+  }
+  cg->graphsum(out->dev_grad.get(), out->ld, in->dev_grad.get(), in->ld, dim, s.get());
+  if (ctx->profile) {
+    e1.record(s.get());
+    ctx->gs_events->emplace_back(e0, e1);
+    ctx->gs_bytes->push_back(cg->algorithmic_bytes(dim));
+  }
 }
 
 // ------------------------------------------------------------------------------------------

@@ -85,6 +85,9 @@ struct ModuleContext {
   // loss gradient, zero elsewhere) the weight gradients depend on
   DevGraph *split_graph = nullptr;  // Â restricted to those rows (null: all rows)
   const int *split_rows = nullptr;  // their row ids (device)
+  // ... and its backward: the loss gradient is zero outside those rows, so Â out.grad only
+  // needs the edges into them (Â's columns of the split)
+  DevGraph *split_colgraph = nullptr;
   const int *truth = nullptr;  // current split's truth (device)
   int count = 0;               // labelled rows of the current split (global)
   float *xent_partials = nullptr;

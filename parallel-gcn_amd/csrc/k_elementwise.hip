@@ -131,6 +131,27 @@ void launch_scatter_rows(const float *src, const int *rows, int n, int ld, float
                      reinterpret_cast<float4 *>(out));
 }
 
+// out[r] = src[rows[r]] (float4s): the input of a column-subset GraphSum on the plain path
+__global__ __launch_bounds__(256) void k_gather_rows(const float4 *__restrict__ src,
+                                                     const int *__restrict__ rows, int n, int ld4,
+                                                     float4 *__restrict__ out) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long long)n * ld4) return;
+  const long long r = t / ld4;
+  const int q = (int)(t - r * ld4);
+  out[t] = src[(long long)rows[r] * ld4 + q];
+}
+
+void launch_gather_rows(const float *src, const int *rows, int n, int ld, float *out,
+                        hipStream_t s) {
+  PGCN_CHECK(ld % 4 == 0, PGCN_E_INVALID, "gather_rows: ld % 4");
+  if (n <= 0) return;
+  const long long tot = (long long)n * (ld / 4);
+  hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)ceil_div(tot, 256)), dim3(256), 0, s,
+                     reinterpret_cast<const float4 *>(src), rows, n, ld / 4,
+                     reinterpret_cast<float4 *>(out));
+}
+
 // ReLU (hpdga module.cpp:173-188)
 __global__ __launch_bounds__(256) void k_relu_fwd(float *__restrict__ x, long long n,
                                                   uint8_t *__restrict__ mask, int training) {

@@ -41,15 +41,18 @@ namespace pgcn {
 typedef __attribute__((address_space(3))) void lds_void;
 
 // in'[r, 0:16] = scale[r] * in[r, 0:16]   (rows of 4 float4; ld4 = row stride in float4)
+// (col_map: the table's rows are rows col_map[r] of `in` -- a column-subset graph)
 __global__ __launch_bounds__(256) void k_gs_prescale(const float4 *__restrict__ in, int ld4_in,
                                                      const float *__restrict__ scale, int n,
-                                                     float4 *__restrict__ out) {
+                                                     float4 *__restrict__ out,
+                                                     const int *__restrict__ col_map) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long r = t >> 2;
   if (r >= n) return;
   const int v = (int)(t & 3);
   const float s = scale[r];
-  float4 x = in[r * ld4_in + v];
+  const long long src = col_map ? (long long)col_map[r] : r;
+  float4 x = in[src * ld4_in + v];
   x.x *= s;
   x.y *= s;
   x.z *= s;
@@ -627,12 +630,13 @@ long long lds_stamps_read(void *dst, long long max_elems) {
 }
 
 void launch_graphsum_lds(const LdsSchedule &s, const float *in, int ld_in, float *out,
-                         int ld_out, float *scratch_in, float *partial, hipStream_t st) {
+                         int ld_out, float *scratch_in, float *partial, hipStream_t st,
+                         const int *col_map) {
   PGCN_CHECK(ld_in % 4 == 0 && ld_out % 4 == 0, PGCN_E_INVALID, "graphsum_lds: ld % 4");
   const long long pre = (long long)s.n_cols * 4;
   hipLaunchKernelGGL(k_gs_prescale, dim3((unsigned)ceil_div(pre, 256)), dim3(256), 0, st,
                      reinterpret_cast<const float4 *>(in), ld_in / 4, s.col_scale, s.n_cols,
-                     reinterpret_cast<float4 *>(scratch_in));
+                     reinterpret_cast<float4 *>(scratch_in), col_map);
 #define GS_LDS(D, W, Y)                                                                     \
   hipLaunchKernelGGL((k_graphsum_lds<D, W, Y>), dim3((unsigned)(s.n_batches * kGraphBlocks)),  \
                      dim3(LDS_THREADS), 0, st, s.entries, s.masks, s.wave_off, s.counts,        \

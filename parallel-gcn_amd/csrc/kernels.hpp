@@ -54,7 +54,8 @@ struct LdsSchedule {
   const uint64_t *masks = nullptr;           // [kb][4]
 };
 void launch_graphsum_lds(const LdsSchedule &s, const float *in, int ld_in, float *out,
-                         int ld_out, float *scratch_in, float *partial, hipStream_t st);
+                         int ld_out, float *scratch_in, float *partial, hipStream_t st,
+                         const int *col_map = nullptr);
 
 void launch_gemm_nn(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
                     int trans_b, float *C, int ldc, const uint64_t *a_mask, long long mask_base,
@@ -67,6 +68,9 @@ void launch_mask_nibbles(const uint64_t *mask, long long mask_base, long long ma
 void launch_xstream_nn(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
                        int trans_b, float *C, int ldc, const uint64_t *maskT, float a_scale,
                        hipStream_t s, float *C2 = nullptr);  // C2: drop(X) W beside C = X W
+// out[r][0:ld] = src[rows[r]][0:ld]  (ld % 4 == 0)
+void launch_gather_rows(const float *src, const int *rows, int n, int ld, float *out,
+                        hipStream_t s);
 // out[rows[r]][0:ld] = src[r][0:ld]  (ld % 4 == 0)
 void launch_scatter_rows(const float *src, const int *rows, int n, int ld, float *out,
                          hipStream_t s);
