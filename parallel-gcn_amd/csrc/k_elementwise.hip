@@ -219,23 +219,41 @@ __global__ __launch_bounds__(256) void k_xent_fwd(float *__restrict__ logits, in
   const int rows = (int)min((long long)XR, (long long)n - row0);
   const long long base = row0 * ld;
   const int tile = rows * ld;
-  // element e = r * ld + j of the tile; e advances by 256 per step (ld <= 124 < 256): no
-  // integer division in the copy loops
-  const int r_start = threadIdx.x / ld, j_start = threadIdx.x - r_start * ld;
-  const int dr = 256 / ld, dj = 256 - dr * ld;
-  auto walk = [&](auto &&f) {
-    int r = r_start, j = j_start;
-    for (int e = threadIdx.x; e < tile; e += 256) {
-      f(e, r * S + j);
-      j += dj;
-      r += dr;
-      if (j >= ld) {
-        j -= ld;
-        r++;
+  // The tile is rows*ld contiguous floats (ld % 4 == 0, 16-B aligned): float4 copies,
+  // XU per thread in flight (all loads of a batch before its LDS stores); float4 q = row
+  // q / (ld/4), column 4 (q % (ld/4)) -- one division per float4, not per float.
+  const int ld4 = ld >> 2, tile4 = tile >> 2;
+  constexpr int XU = 8;
+  auto to_lds = [&](const float *src) {
+    for (int q0 = threadIdx.x; q0 < tile4; q0 += 256 * XU) {
+      float4 v[XU];
+#pragma unroll
+      for (int u = 0; u < XU; u++) {
+        const int q = q0 + 256 * u;
+        if (q < tile4) v[u] = reinterpret_cast<const float4 *>(src + base)[q];
+      }
+#pragma unroll
+      for (int u = 0; u < XU; u++) {
+        const int q = q0 + 256 * u;
+        if (q < tile4) {
+          const int r = q / ld4, j = 4 * (q - r * ld4);
+          float *d = L + r * S + j;
+          d[0] = v[u].x;
+          d[1] = v[u].y;
+          d[2] = v[u].z;
+          d[3] = v[u].w;
+        }
       }
     }
   };
-  walk([&](int e, int o) { L[o] = logits[base + e]; });
+  auto from_lds = [&](float *dst) {
+    for (int q = threadIdx.x; q < tile4; q += 256) {
+      const int r = q / ld4, j = 4 * (q - r * ld4);
+      const float *d = L + r * S + j;
+      reinterpret_cast<float4 *>(dst + base)[q] = make_float4(d[0], d[1], d[2], d[3]);
+    }
+  };
+  to_lds(logits);
   __syncthreads();
   float loss = 0.0f, wrong = 0.0f, se = 0.0f;
   const int t = threadIdx.x < rows ? truth[row0 + threadIdx.x] : -1;
@@ -255,7 +273,7 @@ __global__ __launch_bounds__(256) void k_xent_fwd(float *__restrict__ logits, in
     wrong = w ? 1.0f : 0.0f;
   }
   __syncthreads();
-  walk([&](int e, int o) { logits[base + e] = L[o]; });
+  from_lds(logits);
   if (training) {
     __syncthreads();  // the shifted logits have left the tile
     if (threadIdx.x < rows) {
@@ -271,7 +289,7 @@ __global__ __launch_bounds__(256) void k_xent_fwd(float *__restrict__ logits, in
       }
     }
     __syncthreads();
-    walk([&](int e, int o) { grad[base + e] = L[o]; });
+    from_lds(grad);
   }
   const float ls = block_sum<256>(loss, red);
   const float ws = block_sum<256>(wrong, red);
@@ -379,7 +397,8 @@ int xent_blocks(int n) { return (int)ceil_div(n, XR); }
 void launch_xent_fwd(float *logits, int ld, float *grad, const int *truth, int n, int c,
                      int count, int training, float *partials, hipStream_t s) {
   if (n <= 0) return;
-  PGCN_CHECK(ld <= 124 && c <= ld, PGCN_E_INVALID, "xent: classes must be <= 124");
+  PGCN_CHECK(ld <= 124 && c <= ld && ld % 4 == 0, PGCN_E_INVALID,
+             "xent: classes must be <= 124 (ld a multiple of 4)");
   const size_t lds = (size_t)XR * (ld + 1) * sizeof(float);  // <= 256*125*4 = 125 KB
   static bool attr = false;
   if (!attr) {

@@ -132,33 +132,44 @@ __device__ __forceinline__ void apply4(float4 &a, uint32_t bits, float scale) {
   a.w *= (bits & 8) ? scale : 0.0f;
 }
 
-// maskT[m][j] from the flat bitmap (bit mask_base + m*mask_ld + k).  One thread per word.
+// maskT[m][j] from the flat bitmap (bit mask_base + m*mask_ld + k).  A block covers 16 rows:
+// their bit range (16 * mask_ld bits, contiguous) is copied to LDS with coalesced loads, then
+// thread (row, j) assembles its word from LDS.
+constexpr int NIB_ROWS = 16;
+constexpr int NIB_WORDS = 16 * 1024 / 64 + 2;  // words of 16 rows of <= 1024 bits (+ edges)
+
 __global__ __launch_bounds__(256) void k_mask_nibbles(const uint64_t *__restrict__ mask,
                                                       long long mask_base, long long mask_ld,
                                                       int M, int K, uint64_t *__restrict__ out) {
-  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (long long)M * 16) return;
-  const long long m = t >> 4;
-  const int j = (int)(t & 15);
+  __shared__ uint64_t bits[NIB_WORDS];
+  const long long m0 = (long long)blockIdx.x * NIB_ROWS;
+  const long long p_first = mask_base + m0 * mask_ld;
+  const long long w_first = p_first >> 6;
+  const int rows = (int)min((long long)NIB_ROWS, (long long)M - m0);
+  const long long p_end = mask_base + (m0 + rows - 1) * mask_ld + K;  // one past the last bit
+  // words holding bits [p_first, p_end); a straddling last nibble past K peeks one word
+  // further (LDS, never loaded) into bits the K mask clears
+  const int n_words = (int)(((p_end + 63) >> 6) - w_first);
+  for (int i = threadIdx.x; i < n_words; i += 256) bits[i] = mask[w_first + i];
+  __syncthreads();
+  const int r = threadIdx.x >> 4, j = threadIdx.x & 15;
+  if (r >= rows) return;
+  const long long p0 = mask_base + (m0 + r) * mask_ld + 4 * j - (w_first << 6);  // local bit
   uint64_t word = 0;
-  // unrolled over the 16 possible chunks (K <= 1024) so that every load is issued before the
-  // first one is used (a K-bounded loop serialised them: ~1 TB/s)
-  const long long p0 = mask_base + m * mask_ld + 4 * j;
 #pragma unroll
   for (int c = 0; c < 16; c++) {
     const int kb = 64 * c + 4 * j;
     if (kb < K) {
       const long long p = p0 + 64 * c;
-      const long long w = p >> 6;
-      const int sh = (int)(p & 63);
-      uint64_t v = mask[w] >> sh;
-      if (sh > 60) v |= mask[w + 1] << (64 - sh);
+      const int w = (int)(p >> 6), sh = (int)(p & 63);
+      uint64_t v = bits[w] >> sh;
+      if (sh > 60) v |= bits[w + 1] << (64 - sh);
       uint64_t nib = v & 0xfu;
       if (kb + 4 > K) nib &= (1ull << (K - kb)) - 1;  // keep bits of k >= K are 0
       word |= nib << (4 * c);
     }
   }
-  out[t] = word;
+  out[(m0 + r) * 16 + j] = word;
 }
 
 // NN: Z[M][N<=16] = drop(X) W.  A wave owns a 16-row group at a time (grid-stride over
@@ -526,8 +537,9 @@ void launch_mask_nibbles(const uint64_t *mask, long long mask_base, long long ma
                          int K, uint64_t *out, hipStream_t s) {
   PGCN_CHECK(K >= 1 && K <= 1024, PGCN_E_INVALID, "mask_nibbles: K must be in [1,1024]");
   if (M <= 0) return;
-  hipLaunchKernelGGL(k_mask_nibbles, dim3((unsigned)ceil_div((long long)M * 16, 256)), dim3(256),
-                     0, s, mask, mask_base, mask_ld, M, K, out);
+  PGCN_CHECK(mask_ld >= K && mask_ld <= 1024, PGCN_E_INVALID, "mask_nibbles: K <= mask_ld <= 1024");
+  hipLaunchKernelGGL(k_mask_nibbles, dim3((unsigned)ceil_div(M, NIB_ROWS)), dim3(256), 0, s, mask,
+                     mask_base, mask_ld, M, K, out);
 }
 
 void launch_xstream_nn(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
