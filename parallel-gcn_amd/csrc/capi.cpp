@@ -21,6 +21,7 @@ extern int g_graphsum_force_plain;  // host/graph.cpp (diagnostics)
 extern int g_gemm_variant;          // k_gemm.hip (diagnostics)
 extern int g_train_ahead;           // host/gcn.cpp
 extern int g_split_rows;            // host/gcn.cpp
+extern int g_lds_blocks;            // host/graph.cpp
 extern int g_graphsum_lds;          // host/graph.cpp (diagnostics)
 extern int g_graphsum_lds_order;    // host/graph.cpp (diagnostics)
 extern int g_graphsum_lds_diag;     // k_graphsum_lds.hip (diagnostics)
@@ -451,6 +452,10 @@ int pgcn_debug_set(const char *key, int value) {
   else if (!std::strcmp(key, "gemm_variant")) pgcn::g_gemm_variant = value;
   else if (!std::strcmp(key, "train_ahead")) pgcn::g_train_ahead = value;
   else if (!std::strcmp(key, "split_rows")) pgcn::g_split_rows = value;
+  else if (!std::strcmp(key, "lds_blocks")) {
+    if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8) return PGCN_E_INVALID;
+    pgcn::g_lds_blocks = value;
+  }
   else return PGCN_E_INVALID;
   return PGCN_OK;
 }
@@ -466,7 +471,7 @@ long long pgcn_debug_lds_counts(int n_rows, int n_cols, const int *indptr, const
   const int st = guarded([&] {
     PGCN_CHECK(n_rows > 0 && n_cols > 0 && indptr && indices, PGCN_E_INVALID, "lds_counts args");
     std::vector<int> ip(indptr, indptr + n_rows + 1), ix(indices, indices + indptr[n_rows]);
-    const std::vector<int> cut = column_cuts(n_cols, ix);
+    const std::vector<int> cut = column_cuts(n_cols, ix, lds_blocks(n_rows, n_cols));
     const LdsHost h = build_lds_host(n_rows, n_cols, ip, ix, cut, window);
     n = (long long)h.counts.size();
     if (dst) std::copy(h.counts.begin(), h.counts.begin() + std::min(n, cap), dst);
@@ -486,7 +491,7 @@ int pgcn_debug_lds_check(int n_rows, int n_cols, const int *indptr, const int *i
   return guarded([&] {
     PGCN_CHECK(n_rows > 0 && n_cols > 0 && indptr && indices, PGCN_E_INVALID, "lds_check args");
     std::vector<int> ip(indptr, indptr + n_rows + 1), ix(indices, indices + indptr[n_rows]);
-    const std::vector<int> cut = column_cuts(n_cols, ix);
+    const std::vector<int> cut = column_cuts(n_cols, ix, lds_blocks(n_rows, n_cols));
     const LdsHost h = build_lds_host(n_rows, n_cols, ip, ix, cut, window);
     std::vector<float> in((size_t)n_cols);
     uint64_t st[2] = {12345, 67890};

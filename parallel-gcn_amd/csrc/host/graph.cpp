@@ -317,7 +317,8 @@ LdsHost build_lds_host(int n_rows, int n_cols, const std::vector<int> &h_indptr_
                        int window) {
   (void)n_cols;
   const int n_rows_ = n_rows;
-  const int B = kGraphBlocks, SR = LDS_SR, CW = LDS_CW, NS = LDS_SLOTS;
+  const int B = (int)bcut_.size() - 1, SR = LDS_SR, CW = LDS_CW, NS = LDS_SLOTS;
+  PGCN_CHECK(B >= 1 && kCUs % B == 0, PGCN_E_INVALID, "graphsum_lds: column blocks");
   // slices of each column block
   std::vector<int> nsl((size_t)B);
   int t_max = 1;
@@ -339,9 +340,10 @@ LdsHost build_lds_host(int n_rows, int n_cols, const std::vector<int> &h_indptr_
   });
   const long long nrs = ((long long)n_rows_ + 15) / 16;
   const long long cap = (long long)CW * NS;
-  // batches in multiples of 32: kBlocks x batches workgroups then fill whole rounds of the
+  // batches in multiples of kCUs / B: the B x batches workgroups then fill whole rounds of the
   // 256 CUs (one 156-KB-LDS workgroup per CU)
-  const int nbat = (int)(((nrs + cap - 1) / cap + 31) / 32 * 32);
+  const int per_round = kCUs / B;
+  const int nbat = (int)(((nrs + cap - 1) / cap + per_round - 1) / per_round * per_round);
   const long long n_wg = (long long)nbat * B;
   // column-sorted copy of every row (a row's edges inside a slice are then one run)
   std::vector<int> sidx(h_indices_);
@@ -685,6 +687,7 @@ LdsHost build_lds_host(int n_rows, int n_cols, const std::vector<int> &h_indptr_
     }
   }, 0, 64);
   LdsHost h;
+  h.n_blocks = B;
   h.window = win2 ? 2 : pair ? 3 : 1;
   h.n_batches = nbat;
   h.t_max = t_max;
@@ -703,7 +706,7 @@ LdsHost build_lds_host(int n_rows, int n_cols, const std::vector<int> &h_indptr_
 // per slice and slot, window-2 masks, zero rows) and adds each row's sum of in[col] into
 // out[row]; throws on any inconsistency the kernel would turn into a wrong sum.
 void lds_emulate(const LdsHost &h, int n_rows, const float *in, double *out) {
-  const int B = kGraphBlocks, CW = LDS_CW, NS = LDS_SLOTS;
+  const int B = h.n_blocks, CW = LDS_CW, NS = LDS_SLOTS;
   const long long n_wg = (long long)h.n_batches * B;
   std::vector<double> acc((size_t)NS * 16);
   for (long long wg = 0; wg < n_wg; wg++) {
@@ -774,8 +777,18 @@ void lds_emulate(const LdsHost &h, int n_rows, const float *in, double *out) {
   }
 }
 
-std::vector<int> column_cuts(int n_cols, const std::vector<int> &indices) {
-  const int B = kGraphBlocks;
+// "lds_blocks": column blocks of the LDS schedule; 0 = by shape (r01, reddit): 4 blocks when the
+// graph has about as many rows as columns (the full graph and its column subsets: one round of
+// 256 workgroups, half the partials; the same kernel time, combine 18 -> 11 us), 8 for a small
+// row subset (its 256 workgroups then stream half the table each: val rows 0.11 vs 0.22 ms)
+int g_lds_blocks = 0;
+int lds_blocks(int n_rows, int n_cols) {
+  if (g_lds_blocks) return g_lds_blocks;
+  return (double)n_rows >= 0.9 * (double)n_cols ? 4 : 8;
+}
+
+std::vector<int> column_cuts(int n_cols, const std::vector<int> &indices, int n_blocks) {
+  const int B = n_blocks;
   const long long nnz = (long long)indices.size();
   std::vector<long long> colcnt((size_t)n_cols + 1, 0);
   for (long long k = 0; k < nnz; k++) colcnt[(size_t)indices[(size_t)k] + 1]++;
@@ -792,9 +805,9 @@ std::vector<int> column_cuts(int n_cols, const std::vector<int> &indices) {
 }
 
 void DevGraph::build_lds() {
-  compute_cuts();
+  if (lds_cut_.empty()) lds_cut_ = column_cuts(n_cols_, h_indices_, lds_blocks(n_rows_, n_cols_));
   auto L = std::make_unique<LdsSched>();
-  LdsHost h = build_lds_host(n_rows_, n_cols_, h_indptr_, h_indices_, bcut_, g_graphsum_lds_window);
+  LdsHost h = build_lds_host(n_rows_, n_cols_, h_indptr_, h_indices_, lds_cut_, g_graphsum_lds_window);
   const bool win2 = h.window == 2;
   // + 1 KB slack: ring refills read whole 512-B chunks past a wave's last entry block
   L->entries.allocate(h.entries.size() / 4 + 128);
@@ -819,7 +832,8 @@ void DevGraph::build_lds() {
   L->col_scale.upload(h_col_scale_);
   // + LDS_ROWS rows: slice copies run whole pieces past the last column (never read)
   L->scratch.allocate(((size_t)n_cols_ + LDS_ROWS) * 16 + 64);
-  L->partial.allocate((size_t)kBlocks * n_rows_ * 16);
+  L->partial.allocate((size_t)h.n_blocks * n_rows_ * 16);
+  L->s.n_blocks = h.n_blocks;
   L->s.n_rows = n_rows_;
   L->s.n_cols = n_cols_;
   L->s.n_batches = h.n_batches;

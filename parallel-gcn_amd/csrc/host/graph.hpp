@@ -37,7 +37,7 @@ std::vector<float> degree_scales(int n, const int *indptr);
 
 // Host image of the d = 16 LDS schedule (k_graphsum_lds.hip), before upload.
 struct LdsHost {
-  int window = 1, n_batches = 0, t_max = 0;
+  int window = 1, n_batches = 0, t_max = 0, n_blocks = kGraphBlocks;
   std::vector<int> nsl;                 // slices per column block
   std::vector<int2> slices;             // [block][t_max] {first column, rows}
   std::vector<int> rows;                // [batch][LDS_CW][LDS_SLOTS][16]
@@ -47,7 +47,10 @@ struct LdsHost {
   std::vector<uint64_t> masks;          // window 2: [kb][4 steps] lane masks
 };
 // nnz-balanced column cuts (kGraphBlocks + 1 boundaries)
-std::vector<int> column_cuts(int n_cols, const std::vector<int> &indices);
+std::vector<int> column_cuts(int n_cols, const std::vector<int> &indices,
+                             int n_blocks = kGraphBlocks);
+// column blocks of the LDS GraphSum schedule of an n_rows x n_cols graph (XCD-affine: 4 or 8)
+int lds_blocks(int n_rows, int n_cols);
 LdsHost build_lds_host(int n_rows, int n_cols, const std::vector<int> &indptr,
                        const std::vector<int> &indices, const std::vector<int> &bcut, int window);
 // CPU walk of the schedule as the kernel consumes it: out[row] += sum of in[col] (throws on
@@ -117,6 +120,7 @@ class DevGraph {
   // blocked layout
   bool blocked_built_ = false;
   std::vector<int> bcut_;                 // kBlocks + 1 column boundaries
+  std::vector<int> lds_cut_;              // LDS schedule: lds_blocks() + 1 boundaries
   std::vector<long long> bseg_;           // (kBlocks) x (n_rows + 1) segment offsets
   long long bnnz_ = 0;                    // blocked slots incl. padding
   DeviceBuffer<int> bindices_;

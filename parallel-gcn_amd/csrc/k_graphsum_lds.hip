@@ -193,11 +193,11 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
     const unsigned short *__restrict__ counts, int t_max, const int2 *__restrict__ slices,
     const int *__restrict__ n_slices, const int *__restrict__ rows, const float4 *__restrict__ in,
     int n_cols, float4 *__restrict__ partial, long long part_stride,
-    unsigned long long *__restrict__ stamps, int opt) {
+    unsigned long long *__restrict__ stamps, int opt, int n_blocks) {
   unsigned long long st_loop = 0, st_bar = 0, st_ring = 0;
   // ONE __shared__ object: [2][LDS_ROWS][4] float4 slice buffers, then the entry rings
   __shared__ float4 lds[LDS_TOTAL_F4];
-  const int nb = kGraphBlocks;
+  const int nb = n_blocks;
   const int b = blockIdx.x % nb, batch = blockIdx.x / nb;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -638,12 +638,12 @@ void launch_graphsum_lds(const LdsSchedule &s, const float *in, int ld_in, float
                      reinterpret_cast<const float4 *>(in), ld_in / 4, s.col_scale, s.n_cols,
                      reinterpret_cast<float4 *>(scratch_in), col_map);
 #define GS_LDS(D, W, Y)                                                                     \
-  hipLaunchKernelGGL((k_graphsum_lds<D, W, Y>), dim3((unsigned)(s.n_batches * kGraphBlocks)),  \
+  hipLaunchKernelGGL((k_graphsum_lds<D, W, Y>), dim3((unsigned)(s.n_batches * s.n_blocks)),    \
                      dim3(LDS_THREADS), 0, st, s.entries, s.masks, s.wave_off, s.counts,        \
                      s.t_max, s.slices, s.n_slices, s.rows,                                    \
                      reinterpret_cast<const float4 *>(scratch_in), s.n_cols,                   \
                      reinterpret_cast<float4 *>(partial), (long long)s.n_rows,                 \
-                     lds_stamps(s.n_batches * kGraphBlocks), g_graphsum_lds_opt)
+                     lds_stamps(s.n_batches * s.n_blocks), g_graphsum_lds_opt, s.n_blocks)
   const int diag = g_graphsum_lds_diag;
   if (s.window == 3) {
     if (diag == 4) GS_LDS(4, 3, 1);
@@ -672,7 +672,7 @@ void launch_graphsum_lds(const LdsSchedule &s, const float *in, int ld_in, float
   const long long post = (long long)s.n_rows * 4;
   hipLaunchKernelGGL(k_gs_lds_combine, dim3((unsigned)ceil_div(post, 256)), dim3(256), 0, st,
                      reinterpret_cast<const float4 *>(partial), (long long)s.n_rows,
-                     kGraphBlocks, s.row_scale, s.n_rows, reinterpret_cast<float4 *>(out),
+                     s.n_blocks, s.row_scale, s.n_rows, reinterpret_cast<float4 *>(out),
                      ld_out / 4);
   PGCN_HIP(hipGetLastError());
 }

@@ -38,7 +38,8 @@ constexpr int LDS_SLOTS = 16;                        // rowsets (16 rows) per co
 constexpr int LDS_THREADS = 64 * (LDS_CW + 1);       // + one slice loader wave
 struct LdsSchedule {
   int n_rows = 0, n_cols = 0;
-  int n_batches = 0;  // workgroups = n_batches * kGraphBlocks
+  int n_batches = 0;  // workgroups = n_batches * n_blocks
+  int n_blocks = kGraphBlocks;  // column blocks (workgroup w serves block w % n_blocks)
   int t_max = 0;      // max slices per column block
   const uint2 *entries = nullptr;            // [kb][16 lane groups] x 4 uint16 row offsets
   const long long *wave_off = nullptr;       // [wg][LDS_CW] first kb of each wave's stream

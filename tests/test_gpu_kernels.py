@@ -115,6 +115,31 @@ def test_graphsum_vs_oracle(pgcn, n, deg, dim, hubs):
     pgcn.lib.pgcn_debug_set(b"graphsum_lds_window", LDS_WINDOW_DEFAULT)
 
 
+@pytest.mark.parametrize("blocks", [2, 8])
+def test_graphsum_lds_column_blocks(pgcn, blocks):
+    """The LDS schedule with other column-block counts than the shape rule picks (4 for square
+    graphs, 8 for row subsets): the same sums (XCD mapping: workgroup w serves block w % B)."""
+    pgcn.lib.pgcn_debug_set(b"lds_blocks", blocks)
+    try:
+        n, dim = 120000, 16
+        indptr, indices = random_graph(n, 40, seed=blocks, hubs=20, hub_deg=3000)
+        x = np.random.default_rng(3).standard_normal((n, dim)).astype(np.float32)
+        g = ctypes.c_void_p()
+        pgcn.check(pgcn.lib.pgcn_graph_create(n, helpers.ptr(indptr), helpers.ptr(indices),
+                                              ctypes.byref(g)), "graph_create")
+        xin = torch.from_numpy(x).to(DEV)
+        out = torch.full((n, dim), float("nan"), device=DEV)
+        pgcn.check(pgcn.lib.pgcn_graphsum(g, vp(xin), dim, vp(out), dim, dim, stream()), "gs")
+        torch.cuda.synchronize()
+        ref = oracle_graphsum(indptr, indices, x, dim)
+        bound = abs_bound(indptr, indices, x, dim)
+        err = np.abs(out.cpu().numpy() - ref)
+        assert (err <= 1e-5 * bound + 1e-30).all()
+        pgcn.lib.pgcn_graph_destroy(g)
+    finally:
+        pgcn.lib.pgcn_debug_set(b"lds_blocks", 0)
+
+
 def test_graphsum_linearity_large(pgcn):
     """Size-independent property at reddit-like density: GraphSum(a x + b y) == a GS(x) + b GS(y)."""
     n = 200000

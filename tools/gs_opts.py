@@ -67,9 +67,12 @@ def stamps():
 res = {}
 o_ref = torch.empty(n, 16, device="cuda")
 windows = [int(w) for w in os.environ.get("GS_WINDOWS", "1").split()]
-for wi, window in enumerate(windows):
-    # a fresh graph per window: the LDS schedule is built at its first d = 16 call
+blocks = [int(b) for b in os.environ.get("GS_BLOCKS", "0").split()]  # 0: by shape
+configs = [(w, b) for w in windows for b in blocks]
+for wi, (window, nblk) in enumerate(configs):
+    # a fresh graph per configuration: the LDS schedule is built at its first d = 16 call
     pg.lib.pgcn_debug_set(b"graphsum_lds_window", window)
+    pg.lib.pgcn_debug_set(b"lds_blocks", nblk)
     if g.value:
         pg.lib.pgcn_graph_destroy(g)
     pg.check(pg.lib.pgcn_graph_create(n, helpers.ptr(ip), helpers.ptr(ix), ctypes.byref(g)), "g")
@@ -86,8 +89,8 @@ for wi, window in enumerate(windows):
         r = {"ms": timeit(), "max_rel_vs_v3": ((o - o_ref).abs().max() / o_ref.abs().max()).item()}
         r["ms_again"] = timeit()
         r.update(stamps())
-        res[f"w{window}_opt{opt}"] = r
-        print(json.dumps({f"w{window}_opt{opt}": r}), file=sys.stderr, flush=True)
+        res[f"w{window}_b{nblk}_opt{opt}"] = r
+        print(json.dumps({f"w{window}_b{nblk}_opt{opt}": r}), file=sys.stderr, flush=True)
 # ablations (window 1 schedule, timing only): DIAG 1 = 1/16 of each slice staged, 2 = no table
 # reads, 3 = one add per read, 5 = 1 + 2, 7 = 5 without the entry stream
 diags = [int(d) for d in os.environ.get("GS_DIAGS", "").split()]
