@@ -88,6 +88,12 @@ GCN::GCN(const GCNParams &params_, const AdamParams &adam, const GCNData &data, 
   int lo_prio = 0, hi_prio = 0;
   PGCN_HIP(hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
   stream = Stream::create(hi_prio);  // the reference uses High priority streams
+  // side stream: the next epoch's input-dropout mask is drawn here while the weight-gradient
+  // pass streams X (compute-bound RNG beside an HBM-bound GEMM)
+  side_stream = Stream::create(lo_prio);
+  ctx.side_stream = side_stream.get();
+  ctx.mask_ready = Event::create();
+  ctx.tn_start = Event::create();
   const int world = dist ? dist->world : 1, rank = dist ? dist->rank : 0;
   part = make_partition(params.num_nodes, data.graph.indptr.data(), world, rank,
                         dist ? kRsChunks : 1);
@@ -102,6 +108,8 @@ GCN::GCN(const GCNParams &params_, const AdamParams &adam, const GCNData &data, 
 
 GCN::~GCN() {
   if (stream.get()) (void)hipStreamSynchronize(stream.get());
+  if (side_stream.get()) (void)hipStreamSynchronize(side_stream.get());
+  if (comm_stream.get()) (void)hipStreamSynchronize(comm_stream.get());
 }
 
 void GCN::upload_features(const GCNData &data) {
@@ -476,7 +484,10 @@ std::pair<float, float> GCN::eval(int split) {
   return {pinned.get()[0], pinned.get()[1]};
 }
 
-void GCN::sync() { stream.sync(); }
+void GCN::sync() {
+  stream.sync();
+  side_stream.sync();
+}
 
 std::vector<float> GCN::results(int n) {
   sync();

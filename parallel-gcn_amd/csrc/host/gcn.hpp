@@ -99,6 +99,7 @@ class GCN {
   std::unique_ptr<Comm> comm;
   Stream stream;
   Stream comm_stream;  // edge-cut: reduce-scatters run here, overlapping the next chunk's sum
+  Stream side_stream;  // the next epoch's input-dropout mask, beside the weight-gradient pass
   ModuleContext ctx;
 
   std::unique_ptr<DevGraph> graph;                    // one GPU: the whole Â

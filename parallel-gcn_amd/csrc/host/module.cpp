@@ -37,25 +37,42 @@ Dropout::Dropout(shared_ptr<Variable> in_, float p_, shared_ptr<DropoutRng> rng_
                  ModuleContext *ctx_)
     : in(std::move(in_)), rng(std::move(rng_)), p(p_), ctx(ctx_) {}
 
-void Dropout::draw(const Stream &s) const {
+void Dropout::draw(hipStream_t s, uint64_t *mask) const {
   const DropoutRng &r = *rng;
-  launch_dropout_mask(r.states.get(), r.n_chunks, 64 * r.chunk_lo, r.elem_end, p, r.mask.get(),
-                      ctx->jump_table, s.get());
+  launch_dropout_mask(r.states.get(), r.n_chunks, 64 * r.chunk_lo, r.elem_end, p, mask,
+                      ctx->jump_table, s);
 }
 
-void Dropout::draw_ahead(const Stream &s) const {
+void Dropout::draw_ahead(hipStream_t s, const Event *ready) const {
   PGCN_CHECK(!ahead && !in, PGCN_E_INVALID, "dropout: one mask ahead, input dropout only");
-  draw(s);
+  // into its own buffer: `mask` stays the last training forward's (backward, get_var)
+  if (!rng->mask_ahead) {
+    rng->mask_ahead.allocate(rng->mask.size());
+    rng->mask_ahead.zero();
+  }
+  draw(s, rng->mask_ahead.get());
+  if (ready) ready->record(s);
+  ahead_ready = ready;
   ahead = true;
+}
+
+void Dropout::wait_ahead(hipStream_t s) const {
+  if (ahead && ahead_ready) {
+    ahead_ready->wait_on(s);
+    ahead_ready = nullptr;
+  }
 }
 
 void Dropout::forward(bool training, const Stream &s) const {
   if (!training) return;  // hpdga module.cpp:209
   const DropoutRng &r = *rng;
-  if (ahead)
-    ahead = false;  // drawn by the eval forward before this one
-  else
-    draw(s);
+  if (ahead) {  // drawn ahead (during the last weight-gradient pass, or by the eval forward)
+    wait_ahead(s.get());
+    std::swap(rng->mask, rng->mask_ahead);
+    ahead = false;
+  } else {
+    draw(s.get(), rng->mask.get());
+  }
   if (in) {
     // a grad-carrying variable is dropped in place (module.cpp:215); its rows are the
     // first (elem_end - elem_begin) elements of the local variable
@@ -88,14 +105,18 @@ void SparseMatmul::forward(bool training, const Stream &s) const {
     ahead_valid = false;
     return;
   }
-  if (!training && ctx->train_ahead && x->dense && x->maskT && !drop->drawn_ahead()) {
-    // eval forward + the next training forward's product, one pass over X
+  if (!training && ctx->train_ahead && x->dense && x->maskT && !ahead_valid) {
+    // eval forward + the next training forward's product, one pass over X (the next mask is
+    // usually drawn already, on the side stream during the last weight-gradient pass)
     if (!ahead) {
       ahead.allocate(c->dev_data.size());
       ahead.zero();  // rows past x->rows (edge-cut padding) and padding columns stay zero
     }
-    drop->draw_ahead(s);
-    const uint64_t *m = drop->state().mask.get();
+    if (drop->drawn_ahead())
+      drop->wait_ahead(s.get());
+    else
+      drop->draw_ahead(s.get());
+    const uint64_t *m = drop->mask_ahead();
     launch_mask_nibbles(m, base, x->cols, x->rows, x->cols, x->maskT.get(), s.get());
     launch_xstream_nn(x->rows, b->cols, x->cols, x->x.get(), x->ldx, b->dev_data.get(), b->ld, 0,
                       c->dev_data.get(), c->ld, x->maskT.get(), scale, s.get(), ahead.get());
@@ -122,6 +143,14 @@ void SparseMatmul::backward(const Stream &s) const {
   const long long base = drop->state().mask_base;
   const float scale = drop->scale();
   if (x->dense && x->maskT) {  // the nibble mask of the last training forward
+    if (ctx->train_ahead && ctx->side_stream && !drop->drawn_ahead()) {
+      // the next epoch's input mask, drawn on the side stream while this pass streams X
+      // (maskT, which this pass reads, is rebuilt from it only by the next eval / training
+      // forward on this stream)
+      ctx->tn_start.record(s.get());
+      ctx->tn_start.wait_on(ctx->side_stream);
+      drop->draw_ahead(ctx->side_stream, &ctx->mask_ready);
+    }
     launch_xstream_tn(x->rows, b->cols, x->cols, x->x.get(), x->ldx, c->dev_grad.get(), c->ld,
                       b->dev_grad.get(), b->ld, mask ? x->maskT.get() : nullptr, scale,
                       ctx->gemm_workspace, s.get());

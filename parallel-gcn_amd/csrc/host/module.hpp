@@ -62,7 +62,8 @@ struct DevFeatures {
 // Dropout mask + xorshift chunk states for one Dropout module on this rank.
 struct DropoutRng {
   DeviceBuffer<uint64_t> states;  // 2 per chunk
-  DeviceBuffer<uint64_t> mask;    // 1 word per chunk
+  DeviceBuffer<uint64_t> mask;    // 1 word per chunk: the last training forward's mask
+  DeviceBuffer<uint64_t> mask_ahead;  // the next one, when drawn ahead (input dropout)
   long long chunk_lo = 0, n_chunks = 0;
   long long elem_begin = 0, elem_end = 0;  // global element range of this rank
   long long mask_base = 0;                 // bit of local element 0 in `mask`
@@ -80,6 +81,8 @@ class Module {
 // Shared per-GCN state the modules read (current split, comm, profiling, RNG table).
 struct ModuleContext {
   bool train_ahead = true;     // eval computes the next training forward's first product too
+  hipStream_t side_stream = nullptr;  // train-ahead: the next input mask is drawn here ...
+  Event tn_start, mask_ready;         // ... after tn_start (main), signalling mask_ready
   // output-layer row restriction (single GPU): the last GraphSum's forward computes only the
   // current split's labelled rows -- the only rows the loss, the accuracy and (through the
   // loss gradient, zero elsewhere) the weight gradients depend on
@@ -118,13 +121,18 @@ class Dropout : public Module {
   float scale() const { return 1.0f / (1.0f - p); }
   const DropoutRng &state() const { return *rng; }
   // Draws the NEXT training forward's mask now (the xorshift stream position is the same
-  // whenever it is drawn); that forward then uses it instead of drawing again.
-  void draw_ahead(const Stream &s) const;
+  // whenever it is drawn); that forward then uses it instead of drawing again.  With `ready`,
+  // the draw runs on stream s and `ready` is recorded after it: users of the mask on another
+  // stream wait for it (wait_ahead).
+  void draw_ahead(hipStream_t s, const Event *ready = nullptr) const;
   bool drawn_ahead() const { return ahead; }
+  void wait_ahead(hipStream_t s) const;
+  const uint64_t *mask_ahead() const { return rng->mask_ahead.get(); }
 
  private:
-  void draw(const Stream &s) const;
+  void draw(hipStream_t s, uint64_t *mask) const;
   mutable bool ahead = false;
+  mutable const Event *ahead_ready = nullptr;  // recorded after an ahead draw on a side stream
 };
 
 // include/module.cuh:47-68: c = drop(X) * W

@@ -39,8 +39,9 @@ __global__ __launch_bounds__(256) void k_dropout_mask(uint64_t *__restrict__ sta
   for (long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x; c < n_chunks;
        c += (long long)gridDim.x * blockDim.x) {
     const uint64_t a0 = states[2 * c], a1 = states[2 * c + 1];
-    uint64_t s0 = a0, s1 = a1, word = 0;
-#pragma unroll 8
+    uint64_t s0 = a0, s1 = a1;
+    uint32_t lo = 0, hi = 0;  // mask bits 0-31 / 32-63 (constant shifts: fully unrolled)
+#pragma unroll
     for (int j = 0; j < 64; j++) {
       uint64_t t = s0;
       const uint64_t u = s1;
@@ -50,8 +51,13 @@ __global__ __launch_bounds__(256) void k_dropout_mask(uint64_t *__restrict__ sta
       t ^= u ^ (u >> 26);
       s1 = t;
       const int r = (int)((uint32_t)(t + u) & 0x7fffffffu);
-      word |= (uint64_t)(r >= threshold) << j;
+      const uint32_t bit = r >= threshold ? 1u : 0u;
+      if (j < 32)
+        lo |= bit << j;
+      else
+        hi |= bit << (j - 32);
     }
+    uint64_t word = ((uint64_t)hi << 32) | lo;
     const long long e = elem0 + 64 * c;  // first element of this chunk
     if (e + 64 > elem_end) {
       const long long valid = elem_end - e;

@@ -317,6 +317,11 @@ __device__ __forceinline__ void tn_compute(TnStep<KC, MASKED> &st, floatx4 (&acc
   }
 }
 
+// register sets in flight per wave in k_xstream_tn: 3 = steps n+1 and n+2 load while step n
+// computes (480 of the 512 registers at KC = 10, accumulators in AGPRs); 2 = one step ahead
+#ifndef PGCN_TN_SETS
+#define PGCN_TN_SETS 3
+#endif
 constexpr int XS_TN_BLOCKS = 256;  // one 4-wave block per CU (1 wave per SIMD, ~300 registers)
 
 template <int KC, bool MASKED>
@@ -337,7 +342,25 @@ __global__ __launch_bounds__(256, 1) void k_xstream_tn(int M, int N, int K,
   const long long wid = (long long)blockIdx.x * 4 + w;
   const long long my_steps = wid < n_steps ? (n_steps - wid + gridDim.x * 4 - 1) / (gridDim.x * 4) : 0;
   long long m = wid * 4;
-  // two register sets: step n+1 loads while step n computes (three spill at KC = 10)
+#if PGCN_TN_SETS == 3
+  // three register sets: steps n+1 and n+2 load while step n computes
+  TnStep<KC, MASKED> s0, s1, s2;
+  s0.load(m, M, g, i, K, A, lda, G, ldg, N, maskT);
+  s1.load(m + stride, M, g, i, K, A, lda, G, ldg, N, maskT);
+  for (long long n = 0; n < my_steps; n += 3) {
+    s2.load(m + 2 * stride, M, g, i, K, A, lda, G, ldg, N, maskT);
+    __builtin_amdgcn_sched_barrier(0);
+    tn_compute(s0, acc, i, K, a_scale);
+    s0.load(m + 3 * stride, M, g, i, K, A, lda, G, ldg, N, maskT);
+    __builtin_amdgcn_sched_barrier(0);
+    tn_compute(s1, acc, i, K, a_scale);
+    s1.load(m + 4 * stride, M, g, i, K, A, lda, G, ldg, N, maskT);
+    __builtin_amdgcn_sched_barrier(0);
+    tn_compute(s2, acc, i, K, a_scale);
+    m += 3 * stride;
+  }
+#else
+  // two register sets: step n+1 loads while step n computes
   TnStep<KC, MASKED> s0, s1;
   s0.load(m, M, g, i, K, A, lda, G, ldg, N, maskT);
   for (long long n = 0; n < my_steps; n += 2) {
@@ -350,6 +373,7 @@ __global__ __launch_bounds__(256, 1) void k_xstream_tn(int M, int N, int K,
     tn_compute(s1, acc, i, K, a_scale);
     m += 2 * stride;
   }
+#endif
   // waves 1..3 hand their chunk tiles to wave 0 through LDS (fixed order)
   __shared__ float red[3 * 64 * 16];
   float *p = partial + (long long)blockIdx.x * K * 16;
