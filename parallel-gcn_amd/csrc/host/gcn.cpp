@@ -15,6 +15,7 @@ namespace pgcn {
 // "train_ahead" (pgcn_debug_set, read at engine build): eval's first-layer forward also
 // computes the next training forward's product (SparseMatmul, one pass over dense X)
 int g_train_ahead = 1;
+int g_mask_side = 0;  // "mask_side" (read at engine build): see ModuleContext::mask_side
 // "split_rows" (read at each split switch): the output layer's GraphSum forward computes only
 // the current split's labelled rows
 int g_split_rows = 1;
@@ -319,6 +320,7 @@ void GCN::build(const GCNData &data) {
     ws = std::max(ws, gemm_tn_workspace(rows, dims[(size_t)l + 1], dims[(size_t)l]));
   gemm_ws.allocate(ws / sizeof(float) + 64);
   ctx.train_ahead = g_train_ahead != 0;
+  ctx.mask_side = g_mask_side != 0;
   ctx.xent_partials = xent_partials.get();
   ctx.xent_blocks = xent_blocks(prow);
   ctx.gemm_workspace = gemm_ws.get();

@@ -37,10 +37,10 @@ Dropout::Dropout(shared_ptr<Variable> in_, float p_, shared_ptr<DropoutRng> rng_
                  ModuleContext *ctx_)
     : in(std::move(in_)), rng(std::move(rng_)), p(p_), ctx(ctx_) {}
 
-void Dropout::draw(hipStream_t s, uint64_t *mask) const {
+void Dropout::draw(hipStream_t s, uint64_t *mask, int max_blocks) const {
   const DropoutRng &r = *rng;
   launch_dropout_mask(r.states.get(), r.n_chunks, 64 * r.chunk_lo, r.elem_end, p, mask,
-                      ctx->jump_table, s);
+                      ctx->jump_table, s, max_blocks);
 }
 
 void Dropout::draw_ahead(hipStream_t s, const Event *ready) const {
@@ -50,7 +50,8 @@ void Dropout::draw_ahead(hipStream_t s, const Event *ready) const {
     rng->mask_ahead.allocate(rng->mask.size());
     rng->mask_ahead.zero();
   }
-  draw(s, rng->mask_ahead.get());
+  // on a side stream: two workgroups per CU, leaving room for the main stream's kernels
+  draw(s, rng->mask_ahead.get(), ready ? 2 * kCUs : 0);
   if (ready) ready->record(s);
   ahead_ready = ready;
   ahead = true;
@@ -143,7 +144,7 @@ void SparseMatmul::backward(const Stream &s) const {
   const long long base = drop->state().mask_base;
   const float scale = drop->scale();
   if (x->dense && x->maskT) {  // the nibble mask of the last training forward
-    if (ctx->train_ahead && ctx->side_stream && !drop->drawn_ahead()) {
+    if (ctx->train_ahead && ctx->mask_side && ctx->side_stream && !drop->drawn_ahead()) {
       // the next epoch's input mask, drawn on the side stream while this pass streams X
       // (maskT, which this pass reads, is rebuilt from it only by the next eval / training
       // forward on this stream)

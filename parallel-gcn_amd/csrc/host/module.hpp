@@ -81,7 +81,11 @@ class Module {
 // Shared per-GCN state the modules read (current split, comm, profiling, RNG table).
 struct ModuleContext {
   bool train_ahead = true;     // eval computes the next training forward's first product too
-  hipStream_t side_stream = nullptr;  // train-ahead: the next input mask is drawn here ...
+  // train-ahead option "mask_side": the next input mask is drawn on a side stream beside the
+  // weight-gradient pass (r01: no gain -- the RNG kernel and the pass slow each other down and
+  // the reduce kernels after the pass starve), else by the eval forward on the main stream
+  bool mask_side = false;
+  hipStream_t side_stream = nullptr;  // ... drawn here ...
   Event tn_start, mask_ready;         // ... after tn_start (main), signalling mask_ready
   // output-layer row restriction (single GPU): the last GraphSum's forward computes only the
   // current split's labelled rows -- the only rows the loss, the accuracy and (through the
@@ -130,7 +134,7 @@ class Dropout : public Module {
   const uint64_t *mask_ahead() const { return rng->mask_ahead.get(); }
 
  private:
-  void draw(hipStream_t s, uint64_t *mask) const;
+  void draw(hipStream_t s, uint64_t *mask, int max_blocks = 0) const;
   mutable bool ahead = false;
   mutable const Event *ahead_ready = nullptr;  // recorded after an ahead draw on a side stream
 };

@@ -25,6 +25,27 @@ namespace pgcn {
 // the 64-KB byte tables keeps 8 workgroups per CU resident: each draw is a serial chain of
 // 64-bit xor/shift ops, so the kernel needs the waves to hide it.
 // ------------------------------------------------------------------------------------------
+// 64 draws from xorshift128+ state (s0, s1) -> 64 keep bits (bit j: draw j >= threshold)
+struct Xs64 {
+  uint64_t s0, s1;
+  uint32_t lo = 0, hi = 0;  // mask bits 0-31 / 32-63 (constant shifts: the loop is unrolled)
+  __device__ __forceinline__ void step(int j, int threshold) {
+    uint64_t t = s0;
+    const uint64_t u = s1;
+    s0 = u;
+    t ^= t << 23;
+    t ^= t >> 17;
+    t ^= u ^ (u >> 26);
+    s1 = t;
+    const int r = (int)((uint32_t)(t + u) & 0x7fffffffu);
+    const uint32_t bit = r >= threshold ? 1u : 0u;
+    if (j < 32)
+      lo |= bit << j;
+    else
+      hi |= bit << (j - 32);
+  }
+};
+
 __global__ __launch_bounds__(256) void k_dropout_mask(uint64_t *__restrict__ states,
                                                       long long n_chunks, long long elem0,
                                                       long long elem_end, int threshold,
@@ -36,35 +57,14 @@ __global__ __launch_bounds__(256) void k_dropout_mask(uint64_t *__restrict__ sta
     lut[i] = table[(p >> 1) * 256 + (v << (4 * (p & 1)))];
   }
   __syncthreads();
-  for (long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x; c < n_chunks;
-       c += (long long)gridDim.x * blockDim.x) {
-    const uint64_t a0 = states[2 * c], a1 = states[2 * c + 1];
-    uint64_t s0 = a0, s1 = a1;
-    uint32_t lo = 0, hi = 0;  // mask bits 0-31 / 32-63 (constant shifts: fully unrolled)
-#pragma unroll
-    for (int j = 0; j < 64; j++) {
-      uint64_t t = s0;
-      const uint64_t u = s1;
-      s0 = u;
-      t ^= t << 23;
-      t ^= t >> 17;
-      t ^= u ^ (u >> 26);
-      s1 = t;
-      const int r = (int)((uint32_t)(t + u) & 0x7fffffffu);
-      const uint32_t bit = r >= threshold ? 1u : 0u;
-      if (j < 32)
-        lo |= bit << j;
-      else
-        hi |= bit << (j - 32);
-    }
-    uint64_t word = ((uint64_t)hi << 32) | lo;
+  // mask word of chunk c, then its state advanced by `period` draws: M^period * (a0, a1)
+  auto emit = [&](long long c, uint64_t a0, uint64_t a1, uint64_t word) {
     const long long e = elem0 + 64 * c;  // first element of this chunk
     if (e + 64 > elem_end) {
       const long long valid = elem_end - e;
       word = valid <= 0 ? 0 : (word & ((valid >= 64) ? ~0ull : ((1ull << valid) - 1)));
     }
     mask[c] = word;
-    // advance the chunk state by `period` draws: M^period * (a0, a1)
     uint64_t n0 = 0, n1 = 0;
 #pragma unroll
     for (int q = 0; q < 16; q++) {
@@ -80,6 +80,24 @@ __global__ __launch_bounds__(256) void k_dropout_mask(uint64_t *__restrict__ sta
     }
     states[2 * c] = n0;
     states[2 * c + 1] = n1;
+  };
+  // two chunks per thread and iteration: two independent xorshift chains interleaved (each
+  // draw is a serial chain of 64-bit ops; the pair hides their latency at low occupancy)
+  const long long G = (long long)gridDim.x * blockDim.x;
+  for (long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x; c < n_chunks; c += 2 * G) {
+    const long long c2 = c + G;
+    const bool two = c2 < n_chunks;
+    const long long cb = two ? c2 : c;
+    const uint64_t a0 = states[2 * c], a1 = states[2 * c + 1];
+    const uint64_t b0 = states[2 * cb], b1 = states[2 * cb + 1];
+    Xs64 x{a0, a1}, y{b0, b1};
+#pragma unroll
+    for (int j = 0; j < 64; j++) {
+      x.step(j, threshold);
+      y.step(j, threshold);
+    }
+    emit(c, a0, a1, ((uint64_t)x.hi << 32) | x.lo);
+    if (two) emit(c2, b0, b1, ((uint64_t)y.hi << 32) | y.lo);
   }
 }
 
@@ -372,11 +390,12 @@ static int grid_for(long long work, int block = 256, int cap = 2048) {
 
 void launch_dropout_mask(uint64_t *states, long long n_chunks, long long elem0,
                          long long elem_end, float p, uint64_t *mask, const void *table,
-                         hipStream_t s) {
+                         hipStream_t s, int max_blocks) {
   if (n_chunks <= 0) return;
   // hpdga module.cpp:211: threshold = int(p * MY_RAND_MAX) evaluated in float
   const int threshold = (int)(p * (float)0x7fffffff);
-  const int grid = grid_for(n_chunks, 256, 8 * kCUs);  // 8 KB LDS: 8 workgroups per CU
+  // 8 KB LDS: up to 8 workgroups per CU (a side-stream draw takes fewer: max_blocks)
+  const int grid = grid_for(ceil_div(n_chunks, 2), 256, max_blocks > 0 ? max_blocks : 8 * kCUs);
   hipLaunchKernelGGL(k_dropout_mask, dim3(grid), dim3(256), 0, s, states, n_chunks, elem0,
                      elem_end, threshold, mask, static_cast<const uint4 *>(table));
 }

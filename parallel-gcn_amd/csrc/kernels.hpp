@@ -92,7 +92,7 @@ void launch_spmm_csc_bwd(int nf, int p, int ldg, const int *csc_ptr, const int *
 
 void launch_dropout_mask(uint64_t *states, long long n_chunks, long long elem0,
                          long long elem_end, float p, uint64_t *mask, const void *table,
-                         hipStream_t s);
+                         hipStream_t s, int max_blocks = 0);
 void launch_dropout_apply_based(float *x, long long n, const uint64_t *mask, long long base,
                                 float scale, hipStream_t s);
 void launch_relu_fwd(float *x, long long n, uint8_t *mask, int training, hipStream_t s);

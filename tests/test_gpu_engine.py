@@ -197,8 +197,9 @@ def test_train_ahead_bit_identical(pgcn):
     ds = pgcn.Dataset.synthetic(20000, 96, 8, 300000, 5)  # dense N(0,1) features
     p = pgcn.make_params(ds)
     runs = []
-    for ahead in (1, 0):
+    for ahead, side in ((1, 0), (1, 1), (0, 0)):
         pgcn.lib.pgcn_debug_set(b"train_ahead", ahead)
+        pgcn.lib.pgcn_debug_set(b"mask_side", side)  # next mask drawn beside the W1-grad pass
         g = pgcn.GCN(p, ds, device=0)
         lines = []
         for e in range(6):
@@ -214,8 +215,10 @@ def test_train_ahead_bit_identical(pgcn):
         runs.append(lines)
         g.close()
     pgcn.lib.pgcn_debug_set(b"train_ahead", 1)
-    for a, b in zip(*runs):
-        np.testing.assert_array_equal(np.asarray(a, np.float32), np.asarray(b, np.float32))
+    pgcn.lib.pgcn_debug_set(b"mask_side", 0)
+    for other in runs[1:]:
+        for a, b in zip(runs[0], other):
+            np.testing.assert_array_equal(np.asarray(a, np.float32), np.asarray(b, np.float32))
 
 
 def test_split_rows_restriction_matches_all_rows(pgcn):
