@@ -439,6 +439,9 @@ LdsHost build_lds_host(int n_rows, int n_cols, const std::vector<int> &h_indptr_
   std::vector<unsigned short> counts((size_t)n_wg * t_max * CW * NS, 0);
   std::vector<long long> kbs((size_t)n_wg * CW, 0);
   const bool win2 = window == 2, pair = window == 3;
+  // steps per entry block: 4 (128-B blocks), window 4: 8 (256-B blocks, the kernel runs exact
+  // step counts: the last block of a run takes 1..8 steps)
+  const int SPB = window == 4 ? 8 : 4, BLK = 16 * SPB;
   // walks (wg, wave): for each slice, each rowset slot, the 16 rows' runs in that slice
   auto walk = [&](long long wg, int w, unsigned short *out_entries) {
     const int b = (int)(wg % B), bat = (int)(wg / B);
@@ -473,21 +476,21 @@ LdsHost build_lds_host(int n_rows, int n_cols, const std::vector<int> &h_indptr_
         }
         PGCN_CHECK(m < 65536, PGCN_E_INVALID, "graphsum_lds: slice run too long");
         counts[(size_t)(((wg * t_max + t) * CW + w) * NS + j)] = (unsigned short)m;
-        const int nkb = (m + 3) / 4;
+        const int nkb = (m + SPB - 1) / SPB;
         unsigned short *slot_out = nullptr;  // this slot's nkb blocks
         if (out_entries && pair) {
           sb[j].assign((size_t)nkb * 64, 0);
           sb_n[j] = nkb;
           slot_out = sb[j].data();
         } else if (out_entries) {
-          slot_out = out_entries + kb_total * 64;
+          slot_out = out_entries + kb_total * BLK;
         }
         if (slot_out && nkb > 0 && !g_graphsum_lds_order) {
           for (int kb = 0; kb < nkb; kb++)
             for (int g = 0; g < 16; g++)
-              for (int u = 0; u < 4; u++) {
-                const int st = 4 * kb + u, k = j * 16 + g;
-                slot_out[kb * 64 + g * 4 + u] =
+              for (int u = 0; u < SPB; u++) {
+                const int st = SPB * kb + u, k = j * 16 + g;
+                slot_out[kb * BLK + g * SPB + u] =
                     (unsigned short)(st < n[g] ? (sidx[(size_t)cur[k] + st] - sc.x) * 64 : SR * 64);
               }
         } else if (slot_out && nkb > 0) {
@@ -507,7 +510,7 @@ LdsHost build_lds_host(int n_rows, int n_cols, const std::vector<int> &h_indptr_
               }
               rem[a] = n[g];
             }
-            for (int st = 0; st < 4 * nkb; st++) {
+            for (int st = 0; st < SPB * nkb; st++) {
               int used = 0, ord[4] = {0, 1, 2, 3};
               // rows with no slack left choose first, then rows with more edges left
               std::sort(ord, ord + 4, [&](int x, int y) {
@@ -539,7 +542,7 @@ LdsHost build_lds_host(int n_rows, int n_cols, const std::vector<int> &h_indptr_
                   val = (SR + r) * 64;
                   used |= 1 << r;
                 }
-                dst[(st >> 2) * 64 + grp[a] * 4 + (st & 3)] = (unsigned short)val;
+                dst[(st / SPB) * BLK + grp[a] * SPB + (st % SPB)] = (unsigned short)val;
               }
             }
           }
@@ -676,19 +679,19 @@ LdsHost build_lds_host(int n_rows, int n_cols, const std::vector<int> &h_indptr_
   std::vector<long long> off((size_t)n_wg * CW + 1, 0);
   for (size_t x = 0; x < kbs.size(); x++) off[x + 1] = off[x] + kbs[x];
   const long long total_kb = off.back();
-  std::vector<unsigned short> ent((size_t)std::max<long long>(total_kb, 1) * 64, 0);
+  std::vector<unsigned short> ent((size_t)std::max<long long>(total_kb, 1) * BLK, 0);
   std::vector<uint64_t> msk(win2 ? (size_t)std::max<long long>(total_kb, 1) * 4 : 0, 0);
   parallel_for(n_wg * CW, [&](long long a, long long e) {
     for (long long x = a; x < e; x++) {
       if (win2)
         walk2(x / CW, (int)(x % CW), &ent[(size_t)off[(size_t)x] * 64], &msk[(size_t)off[(size_t)x] * 4]);
       else
-        walk(x / CW, (int)(x % CW), &ent[(size_t)off[(size_t)x] * 64]);
+        walk(x / CW, (int)(x % CW), &ent[(size_t)off[(size_t)x] * BLK]);
     }
   }, 0, 64);
   LdsHost h;
   h.n_blocks = B;
-  h.window = win2 ? 2 : pair ? 3 : 1;
+  h.window = win2 ? 2 : pair ? 3 : window == 4 ? 4 : 1;
   h.n_batches = nbat;
   h.t_max = t_max;
   h.nsl = std::move(nsl);
@@ -707,6 +710,7 @@ LdsHost build_lds_host(int n_rows, int n_cols, const std::vector<int> &h_indptr_
 // out[row]; throws on any inconsistency the kernel would turn into a wrong sum.
 void lds_emulate(const LdsHost &h, int n_rows, const float *in, double *out) {
   const int B = h.n_blocks, CW = LDS_CW, NS = LDS_SLOTS;
+  const int SPB = h.window == 4 ? 8 : 4, BLK = 16 * SPB;
   const long long n_wg = (long long)h.n_batches * B;
   std::vector<double> acc((size_t)NS * 16);
   for (long long wg = 0; wg < n_wg; wg++) {
@@ -731,21 +735,21 @@ void lds_emulate(const LdsHost &h, int n_rows, const float *in, double *out) {
           }
         } else {
           for (int j = 0; j < NS; j++) {
-            const int nblk = h.window == 2 ? cn[j] : (cn[j] + 3) / 4;
+            const int nblk = h.window == 2 ? cn[j] : (cn[j] + SPB - 1) / SPB;
             for (int k = 0; k < nblk; k++) seq.push_back({j, k});
           }
         }
         for (const auto &jk : seq) {
           const int j = jk.first, k = jk.second, n = cn[j];
           {
-            for (int st = 0; st < 4; st++) {
+            for (int st = 0; st < SPB; st++) {
               const uint64_t m = h.window == 2 ? h.masks[(size_t)kb * 4 + st] : 0;
               for (int g = 0; g < 16; g++) {
-                const int e = h.entries[(size_t)kb * 64 + g * 4 + st];
+                const int e = h.entries[(size_t)kb * BLK + g * SPB + st];
                 PGCN_CHECK(e % 64 == 0, PGCN_E_INVALID, "lds schedule: entry not a row offset");
                 const int row = e / 64;
                 // steps past the run's count are padding (zero rows) in every window
-                PGCN_CHECK(h.window == 2 || 4 * k + st < n || row >= LDS_SR, PGCN_E_INVALID,
+                PGCN_CHECK(h.window == 2 || SPB * k + st < n || row >= LDS_SR, PGCN_E_INVALID,
                            "lds schedule: edge past the run's step count");
                 PGCN_CHECK(row >= LDS_SR || row < sc.y, PGCN_E_INVALID,
                            "lds schedule: entry past the slice");

@@ -295,11 +295,13 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
   // ------------------------------------------------------------------------- summing waves
   const long long wid = (long long)blockIdx.x * LDS_CW + wave;
   const long long kb0 = wave_off[wid], kb1 = wave_off[wid + 1];
-  const long long nchunk = (kb1 - kb0 + 3) >> 2;
-  const char *ebytes = reinterpret_cast<const char *>(entries) + kb0 * 128;
+  // entry blocks: 128 B (4 steps), window 4: 256 B (8 steps); a ring chunk is 512 B
+  constexpr int BLKB = WIN == 4 ? 256 : 128, BPC = LDS_RING_CHUNK / BLKB;
+  const long long nchunk = (kb1 - kb0 + BPC - 1) / BPC;
+  const char *ebytes = reinterpret_cast<const char *>(entries) + kb0 * BLKB;
   const unsigned ring_dst = lds_base + LDS_RING_F4 * 16 + (unsigned)(wave * LDS_RING_BYTES);
   const char *ring = reinterpret_cast<const char *>(lds + LDS_RING_F4) + wave * LDS_RING_BYTES +
-                     g * 8;
+                     g * (BLKB / 16);
   auto refill = [&](long long c) {  // chunk c -> ring slot c % 4 (clamped: dummy past the end)
     long long cc = c < nchunk ? c : nchunk - 1;
     cc = cc > 0 ? cc : 0;
@@ -366,7 +368,77 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
     }
     e_next = *reinterpret_cast<const uint2 *>(ring + roff);  // (past the end: unused)
   };
-  if constexpr (WIN == 3) {
+  if constexpr (WIN == 4) {
+    // 8-step blocks (256 B: lane group g's 8 uint16 offsets at 16 g), exact step counts: a
+    // run of n steps takes n / 8 full blocks and one block of n % 8 steps.  Half the blocks
+    // (and the per-block loop / ring work) of window 1, and LDS reads only for real steps.
+    uint4 e4 = *reinterpret_cast<const uint4 *>(ring);
+    auto next4 = [&]() {
+      roff = (roff + BLKB) & (LDS_RING_BYTES - 1);
+      if ((roff & (LDS_RING_CHUNK - 1)) == 0) {  // entering the next chunk: refill the slot
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        ++chunk;
+        refill(chunk + 3);
+        unsigned long long c0 = 0;
+        if constexpr (DIAG == 4) c0 = clk();
+        asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        if constexpr (DIAG == 4) st_ring += clk() - c0;
+      }
+      e4 = *reinterpret_cast<const uint4 *>(ring + roff);
+    };
+    for (int t = 0; t < T; t++) {
+      slice_ready(t);
+      const char *tb = reinterpret_cast<const char *>(lds + (t & 1) * LDS_ROWS * 4 + v);
+      auto rd = [&](unsigned off) { return *reinterpret_cast<const float4 *>(tb + off); };
+      const uint4 *c4 = reinterpret_cast<const uint4 *>(
+          reinterpret_cast<const char *>(lds + LDS_TABLE_F4) + (t & 1) * LDS_CNT_BYTES + wave * 32);
+      const uint4 cw0 = c4[0], cw1 = c4[1];
+      const unsigned cw[8] = {
+          (unsigned)__builtin_amdgcn_readfirstlane(cw0.x), (unsigned)__builtin_amdgcn_readfirstlane(cw0.y),
+          (unsigned)__builtin_amdgcn_readfirstlane(cw0.z), (unsigned)__builtin_amdgcn_readfirstlane(cw0.w),
+          (unsigned)__builtin_amdgcn_readfirstlane(cw1.x), (unsigned)__builtin_amdgcn_readfirstlane(cw1.y),
+          (unsigned)__builtin_amdgcn_readfirstlane(cw1.z), (unsigned)__builtin_amdgcn_readfirstlane(cw1.w)};
+#pragma unroll
+      for (int j = 0; j < LDS_SLOTS; j++) {
+        int n = (cw[j >> 1] >> (16 * (j & 1))) & 0xffff;  // steps of rowset j
+        for (; n >= 8; n -= 8) {
+          const uint4 e = e4;
+          next4();
+          const float4 x0 = rd(e.x & 0xffffu), x1 = rd(e.x >> 16), x2 = rd(e.y & 0xffffu),
+                       x3 = rd(e.y >> 16), x4 = rd(e.z & 0xffffu), x5 = rd(e.z >> 16),
+                       x6 = rd(e.w & 0xffffu), x7 = rd(e.w >> 16);
+          f4_acc(acc[j], x0);
+          f4_acc(acc[j], x1);
+          f4_acc(acc[j], x2);
+          f4_acc(acc[j], x3);
+          f4_acc(acc[j], x4);
+          f4_acc(acc[j], x5);
+          f4_acc(acc[j], x6);
+          f4_acc(acc[j], x7);
+        }
+        if (n) {  // the last 1..7 steps (uniform branches)
+          const uint4 e = e4;
+          next4();
+          unsigned w0 = e.x, w1 = e.y;
+          if (n >= 4) {
+            const float4 x0 = rd(w0 & 0xffffu), x1 = rd(w0 >> 16), x2 = rd(w1 & 0xffffu),
+                         x3 = rd(w1 >> 16);
+            f4_acc(acc[j], x0);
+            f4_acc(acc[j], x1);
+            f4_acc(acc[j], x2);
+            f4_acc(acc[j], x3);
+            w0 = e.z;
+            w1 = e.w;
+            n -= 4;
+          }
+          if (n >= 1) f4_acc(acc[j], rd(w0 & 0xffffu));
+          if (n >= 2) f4_acc(acc[j], rd(w0 >> 16));
+          if (n >= 3) f4_acc(acc[j], rd(w1 & 0xffffu));
+        }
+      }
+      slice_done(t);
+    }
+  } else if constexpr (WIN == 3) {
     // Slot pairs (2p, 2p+1) interleaved block by block (host order: A0 B0 A1 B1 ..., then the
     // longer slot's rest), so every iteration has 8 ds_read_b128 (two blocks) in flight where
     // window 1 had 4: a slot runs ~1.4 blocks per slice on reddit, so pipelining inside one
@@ -551,6 +623,30 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
             acc[j].y += x1.y;
             acc[j].z += x2.z;
             acc[j].w += x3.w;
+          } else if constexpr (DIAG == 10) {  // timing only: every row read twice (LDS load x2)
+            const float4 y0 = *reinterpret_cast<const float4 *>(tb + (e.x & 0xffffu) + 16384);
+            const float4 y1 = *reinterpret_cast<const float4 *>(tb + (e.x >> 16) + 16384);
+            const float4 y2 = *reinterpret_cast<const float4 *>(tb + (e.y & 0xffffu) + 16384);
+            const float4 y3 = *reinterpret_cast<const float4 *>(tb + (e.y >> 16) + 16384);
+            f4_acc(acc[j], x0);
+            f4_acc(acc[j], x1);
+            f4_acc(acc[j], x2);
+            f4_acc(acc[j], x3);
+            f4_acc(acc[j], y0);
+            f4_acc(acc[j], y1);
+            f4_acc(acc[j], y2);
+            f4_acc(acc[j], y3);
+          } else if constexpr (DIAG == 11) {  // timing only: twice the adds (VALU load x2)
+            float4 z = x0;
+            f4_acc(z, x1);
+            f4_acc(z, x2);
+            f4_acc(z, x3);
+            f4_acc(acc[j], x0);
+            f4_acc(acc[j], x1);
+            f4_acc(acc[j], x2);
+            f4_acc(acc[j], x3);
+            f4_acc(acc[(j + 1) % LDS_SLOTS], z);
+            asm volatile("" ::"v"(z.x), "v"(z.y), "v"(z.z), "v"(z.w));
           } else {
             f4_acc(acc[j], x0);
             f4_acc(acc[j], x1);
@@ -645,7 +741,10 @@ void launch_graphsum_lds(const LdsSchedule &s, const float *in, int ld_in, float
                      reinterpret_cast<float4 *>(partial), (long long)s.n_rows,                 \
                      lds_stamps(s.n_batches * s.n_blocks), g_graphsum_lds_opt, s.n_blocks)
   const int diag = g_graphsum_lds_diag;
-  if (s.window == 3) {
+  if (s.window == 4) {
+    if (diag == 4) GS_LDS(4, 4, 1);
+    else GS_LDS(0, 4, 1);
+  } else if (s.window == 3) {
     if (diag == 4) GS_LDS(4, 3, 1);
     else GS_LDS(0, 3, 1);
   } else if (s.window == 2) {
@@ -664,6 +763,8 @@ void launch_graphsum_lds(const LdsSchedule &s, const float *in, int ld_in, float
       case 7: GS_LDS(7, 1, 1); break;  // as 5, no entry stream either
       case 8: GS_LDS(8, 1, 1); break;  // as 7, one block per slot visit
       case 9: GS_LDS(9, 1, 1); break;  // as 7, one loop over a slice's blocks
+      case 10: GS_LDS(10, 1, 1); break;  // every row read twice (LDS load x2)
+      case 11: GS_LDS(11, 1, 1); break;  // twice the adds (VALU load x2)
       case 4: GS_LDS(4, 1, 1); break;
       default: GS_LDS(0, 1, 1); break;
     }

@@ -80,6 +80,8 @@ def abs_bound(indptr, indices, x, dim):
     (20000, 10, 128, 3),     # 4-layer hidden 128
     (120000, 40, 16, -2),    # LDS path, window-2 schedule (two-slot runs, exec-masked adds)
     (120000, 40, 16, -3),    # LDS path, window-3 schedule (slot pairs interleaved)
+    (120000, 40, 16, -4),    # LDS path, window-4 schedule (8-step blocks, exact step counts)
+    (120000, 40, 16, -1),    # LDS path, window-1 schedule (4-step blocks)
 ])
 def test_graphsum_vs_oracle(pgcn, n, deg, dim, hubs):
     # LDS path (d = 16, table > L2): default window 1 (slots one after another); hubs < 0
@@ -339,7 +341,15 @@ def test_gemm_xstream(pgcn, M, N, K, base):
         pgcn.check(pgcn.lib.pgcn_gemm_tn_xstream(M, N, K, vp(dA), lda, vp(dG), N, vp(W), N,
                                                  vp(nib) if drop else None, 2.0, vp(ws),
                                                  stream()), "xtn")
+        # the LDS-DMA ring variant of the TN kernel (option; taken for K in 577..640, N = 16)
+        W2 = torch.full((K, N), float("nan"), device=DEV)
+        pgcn.lib.pgcn_debug_set(b"xstream_tn_lds", 1)
+        pgcn.check(pgcn.lib.pgcn_gemm_tn_xstream(M, N, K, vp(dA), lda, vp(dG), N, vp(W2), N,
+                                                 vp(nib) if drop else None, 2.0, vp(ws),
+                                                 stream()), "xtn lds")
+        pgcn.lib.pgcn_debug_set(b"xstream_tn_lds", 0)
         torch.cuda.synchronize()
+        np.testing.assert_allclose(W2.cpu().numpy(), W.cpu().numpy(), rtol=1e-5, atol=1e-5)
         ref = Ae @ B.astype(np.float64)
         bound = np.abs(Ae) @ np.abs(B.astype(np.float64))
         o = C.cpu().numpy()
