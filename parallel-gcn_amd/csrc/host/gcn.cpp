@@ -16,6 +16,9 @@ namespace pgcn {
 // computes the next training forward's product (SparseMatmul, one pass over dense X)
 int g_train_ahead = 1;
 int g_mask_side = 0;  // "mask_side" (read at engine build): see ModuleContext::mask_side
+// "eval_ax" (read at engine build): eval's first layer as (Â X) W1 from Â X computed once
+// (Â and X are constants: exact algebra, fp32 rounding order differs)
+int g_eval_ax = 1;
 // "split_rows" (read at each split switch): the output layer's GraphSum forward computes only
 // the current split's labelled rows
 int g_split_rows = 1;
@@ -269,6 +272,17 @@ void GCN::build(const GCNData &data) {
     graph->set_scales(sg, sg);
   }
   upload_features(data);
+  // eval_ax: Â X once (16 columns per d = 16 GraphSum; the last chunk overlaps the one
+  // before it so it never reads past a row), single GPU, dense X on the X-stream path
+  if (g_eval_ax && !comm && graph && feats.dense && feats.maskT && feats.cols >= 16) {
+    feats.ax.allocate(feats.x.size());
+    feats.ax.zero();
+    for (int c0 = 0; c0 < feats.cols; c0 += 16) {
+      const int c = std::min(c0, feats.ldx - 16);
+      graph->graphsum(feats.x.get() + c, feats.ldx, feats.ax.get() + c, feats.ldx, 16, stream.get());
+    }
+    stream.sync();
+  }
   // truth per split for this rank's rows, padded with -1 (set_truth, src/gcn.cu:204-226)
   const int first = part.first(), rows = part.local_rows(), prow = part.maxrows;
   for (int s = 1; s <= 3; s++) {
@@ -348,10 +362,17 @@ void GCN::insert_first_layer() {
   auto var1 = std::make_shared<Variable>(prow, h, true, round_up4(h));
   variables.push_back(var1);
   variables.push_back(weights[0]);
-  modules.push_back(std::make_unique<SparseMatmul>(&feats, weights[0], var1, dptr, &ctx));
+  auto sm = std::make_unique<SparseMatmul>(&feats, weights[0], var1, dptr, &ctx);
+  SparseMatmul *smp = sm.get();
+  modules.push_back(std::move(sm));
   auto var2 = std::make_shared<Variable>(prow, h, true, round_up4(h));
   variables.push_back(var2);
-  modules.push_back(std::make_unique<GraphSum>(var1, var2, graph.get(), h, &ctx));
+  auto gs = std::make_unique<GraphSum>(var1, var2, graph.get(), h, &ctx);
+  if (feats.ax) {  // eval: (Â X) W1 -> var2 directly, the GraphSum is skipped
+    smp->eval_out = var2;
+    gs->first_layer = true;
+  }
+  modules.push_back(std::move(gs));
   modules.push_back(std::make_unique<ReLU>(var2));
 }
 

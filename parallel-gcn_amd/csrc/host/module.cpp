@@ -101,6 +101,11 @@ void SparseMatmul::forward(bool training, const Stream &s) const {
   const uint64_t *mask = training ? drop->state().mask.get() : nullptr;
   const long long base = drop->state().mask_base;
   const float scale = drop->scale();
+  if (!training && x->ax && eval_out) {  // eval_ax: (Â X) W1 straight into the GraphSum's output
+    launch_xstream_nn(x->rows, b->cols, x->cols, x->ax.get(), x->ldx, b->dev_data.get(), b->ld, 0,
+                      eval_out->dev_data.get(), eval_out->ld, nullptr, 1.0f, s.get(), nullptr);
+    return;
+  }
   if (training && ahead_valid) {  // computed by the eval forward before this one
     std::swap(c->dev_data, ahead);
     ahead_valid = false;
@@ -220,7 +225,8 @@ void GraphSum::run(const float *src, float *dst, const Stream &s) const {
   }
 }
 
-void GraphSum::forward(bool, const Stream &s) const {
+void GraphSum::forward(bool training, const Stream &s) const {
+  if (!training && first_layer) return;  // eval_ax: SparseMatmul wrote Â X W1 already
   DevGraph *sg = last_layer && !ctx->comm ? ctx->split_graph : nullptr;
   if (!sg) {
     run(in->dev_data.get(), out->dev_data.get(), s);

@@ -50,6 +50,9 @@ struct DevFeatures {
   // dense: [rows][ldx] fp32, CSR order == row-major order
   DeviceBuffer<float> x;
   int ldx = 0;
+  // eval_ax: Â X ([rows][ldx], computed once at engine build; Â and X are constants), so
+  // eval's first layer is (Â X) W1 -- one GEMM pass instead of X W1 and a GraphSum
+  DeviceBuffer<float> ax;
   // dense + X-stream kernels: the input dropout's keep bits in the nibble layout
   // (k_mask_nibbles, [rows][16] words), rebuilt by every training forward
   DeviceBuffer<uint64_t> maskT;
@@ -155,6 +158,8 @@ class SparseMatmul : public Module {
  public:
   SparseMatmul(const DevFeatures *x_, shared_ptr<Variable> b_, shared_ptr<Variable> c_,
                const Dropout *drop_, ModuleContext *ctx_);
+  // eval_ax: the first GraphSum's output, written by an eval forward from Â X
+  shared_ptr<Variable> eval_out;
   void forward(bool training, const Stream &s) const override;
   void backward(const Stream &s) const override;
 };
@@ -166,6 +171,9 @@ class GraphSum : public Module {
   int dim;
   ModuleContext *ctx;
   bool last_layer;                   // the output layer's GraphSum (row restriction applies)
+ public:
+  bool first_layer = false;          // eval_ax: its eval forward was done by SparseMatmul
+ private:
   mutable DeviceBuffer<float> compact;  // restricted forward: [split rows][out->ld]
   // edge-cut: per row chunk, the [world*chunk_rows][ld] partial sums and their events
   std::vector<DeviceBuffer<float>> partial;

@@ -197,6 +197,7 @@ def test_train_ahead_bit_identical(pgcn):
     ds = pgcn.Dataset.synthetic(20000, 96, 8, 300000, 5)  # dense N(0,1) features
     p = pgcn.make_params(ds)
     runs = []
+    pgcn.lib.pgcn_debug_set(b"eval_ax", 0)  # eval streams X (else it reads Â X instead)
     for ahead, side in ((1, 0), (1, 1), (0, 0)):
         pgcn.lib.pgcn_debug_set(b"train_ahead", ahead)
         pgcn.lib.pgcn_debug_set(b"mask_side", side)  # next mask drawn beside the W1-grad pass
@@ -216,6 +217,7 @@ def test_train_ahead_bit_identical(pgcn):
         g.close()
     pgcn.lib.pgcn_debug_set(b"train_ahead", 1)
     pgcn.lib.pgcn_debug_set(b"mask_side", 0)
+    pgcn.lib.pgcn_debug_set(b"eval_ax", 1)
     for other in runs[1:]:
         for a, b in zip(runs[0], other):
             np.testing.assert_array_equal(np.asarray(a, np.float32), np.asarray(b, np.float32))
@@ -242,3 +244,22 @@ def test_split_rows_restriction_matches_all_rows(pgcn):
     np.testing.assert_allclose(ta, tb, rtol=1e-5, atol=2e-4)
     np.testing.assert_allclose(w1a, w1b, rtol=1e-4, atol=1e-6)
     np.testing.assert_allclose(w2a, w2b, rtol=1e-4, atol=1e-6)
+
+
+def test_eval_ax_matches_graphsum_of_xw(pgcn):
+    """eval's first layer from Â X computed once at build ((Â X) W1 instead of Â (X W1): the same
+    product, another fp32 rounding order) gives the same eval losses and accuracies, and leaves
+    training untouched (bit-identical training lines), on a graph that takes the LDS path."""
+    ds = pgcn.Dataset.synthetic(80000, 40, 8, 2000000, 9)  # dense features, F = 40
+    p = pgcn.make_params(ds)
+    runs = []
+    for on in (1, 0):
+        pgcn.lib.pgcn_debug_set(b"eval_ax", on)
+        g = pgcn.GCN(p, ds, device=0)
+        runs.append(np.array([g.train_epoch() + g.eval(2) for _ in range(4)], np.float64))
+        g.close()
+    pgcn.lib.pgcn_debug_set(b"eval_ax", 1)
+    a, b = runs
+    np.testing.assert_array_equal(a[0, :2], b[0, :2])  # epoch 1's training pass: same bits
+    np.testing.assert_allclose(a[:, [0, 2]], b[:, [0, 2]], rtol=1e-5)
+    np.testing.assert_allclose(a[:, [1, 3]], b[:, [1, 3]], atol=2e-4)
