@@ -18,7 +18,10 @@ STRONG (value = epochs of the whole graph per second, all ranks together).
 Extra fields: "roofline" for the dominant kernel (GraphSum: algorithmic bytes per call over
 its HIP-event-timed duration on the engine's stream, peak 8 TB/s) and "cpu_baseline" (the
 reference's own sequential code, oracle/_ref/libhpdga_ref.so, on a bounded sample of the
-same workload on this host, 1 thread).
+same workload on this host, 1 thread).  "engine_options" lists the epoch reorganisations the
+engine applies (train-ahead, output-layer row restriction, eval's first layer
+from Â X computed once; all exact algebra, no work whose result reaches the loss, accuracy or
+weights is skipped) and "value_reorganisations_off" times the same epoch with them off.
 """
 import argparse
 import ctypes
@@ -100,6 +103,8 @@ def main():
                     help="one GPU through the multi-GPU engine (partition, RCCL at world 1)")
     ap.add_argument("--profile-only", action="store_true",
                     help="only run warmup+steps (for rocprofv3), no JSON extras")
+    ap.add_argument("--no-plain", action="store_true",
+                    help="skip the secondary measurement with the epoch reorganisations off")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -203,6 +208,32 @@ def main():
         "setup_s": {"generate": t_gen, "build": t_build},
     }
     g.close()
+    # the same epoch with the engine's epoch reorganisations off (train-ahead, output-layer
+    # row restriction, eval from Â X): every module runs the reference's full
+    # per-epoch work, for comparison (same synthetic data, fewer steps)
+    opts = {"train_ahead": 1, "split_rows": 0 if world > 1 else 1,
+            "eval_ax": 0 if world > 1 else 1, "reassociate_last": 1}
+    out["engine_options"] = opts
+    if not args.no_plain and world == 1 and not args.edge_cut:
+        for k in ("train_ahead", "split_rows", "eval_ax"):
+            pgcn.lib.pgcn_debug_set(k.encode(), 0)
+        g2 = pgcn.GCN(params, ds, device=local_rank)
+        steps2 = max(1, min(args.steps, 10))
+        for _ in range(2):
+            g2.epoch_async()
+        g2.sync()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps2):
+            g2.epoch_async()
+        g2.sync()
+        torch.cuda.synchronize()
+        el2 = time.perf_counter() - t0
+        g2.close()
+        for k in ("train_ahead", "split_rows", "eval_ax"):
+            pgcn.lib.pgcn_debug_set(k.encode(), 1)
+        out["value_reorganisations_off"] = steps2 / el2
+        out["reorganisations_off_steps"] = steps2
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         kind, times = cpu_baseline(ds, args.cpu_epochs)
         out["cpu_baseline"] = {"value": len(times) / sum(times), "unit": "epochs/s", "cores": 1,

@@ -1,0 +1,46 @@
+"""HBM traffic per GraphSum call from rocprofv3 PMC passes (diagnostic tool, run on the host
+after scripts/profile.sh's fetch/write passes).
+
+usage: python3 tools/traffic.py gpurun_out/<dir> [epoch_calls]
+
+A GraphSum call is k_gs_prescale + k_graphsum_lds + k_gs_lds_combine (the three launches the
+bench's HIP events bracket).  Only the last `epoch_calls` calls (default 20: 4 epochs x 5) are
+counted, so the engine-build calls (Â X precompute) are left out.  Bytes follow
+MI355X_MICROARCH.md's HBM section: FETCH_SIZE x 2 (gfx950 tallies the 128-B requests of
+16-B/lane streams at 64 B) + WRITE_SIZE, both in KB.  Prints one JSON object.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+root = sys.argv[1]
+n_calls = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+
+
+def per_dispatch(counter):
+    rows = []
+    for f in glob.glob(os.path.join(root, "*", "run_counter_collection.csv")):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] == counter:
+                rows.append((int(r["Dispatch_Id"]), r["Kernel_Name"], float(r["Counter_Value"])))
+    rows.sort()
+    return rows
+
+
+out = {}
+for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+    rows = [r for r in per_dispatch(counter)
+            if any(k in r[1] for k in ("k_gs_prescale", "k_graphsum_lds", "k_gs_lds_combine"))]
+    calls, cur = [], 0.0
+    for _, name, v in rows:
+        cur += v
+        if "k_gs_lds_combine" in name:
+            calls.append(cur)
+            cur = 0.0
+    calls = calls[-n_calls:]
+    out[counter + "_KB_per_call"] = sum(calls) / max(len(calls), 1)
+    out[counter + "_calls"] = len(calls)
+out["hbm_bytes_per_call"] = (2 * out["FETCH_SIZE_KB_per_call"] + out["WRITE_SIZE_KB_per_call"]) * 1024
+print(json.dumps(out))
