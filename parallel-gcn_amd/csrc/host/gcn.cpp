@@ -292,8 +292,14 @@ void GCN::build(const GCNData &data) {
     truth[s].allocate(t.size());
     truth[s].upload(t);
     split_rows_host[s].clear();
+    std::vector<int> tc;
     for (int i = 0; i < rows; i++)
-      if (t[(size_t)i] >= 0) split_rows_host[s].push_back(i);
+      if (t[(size_t)i] >= 0) {
+        split_rows_host[s].push_back(i);
+        tc.push_back(t[(size_t)i]);
+      }
+    truth_compact[s].allocate(std::max<size_t>(tc.size(), 1));
+    if (!tc.empty()) truth_compact[s].upload(tc);
     int c = 0;
     for (int i = 0; i < N; i++) c += (data.split[(size_t)i] == s && data.label[(size_t)i] >= 0);
     counts[s] = c;
@@ -411,9 +417,18 @@ void GCN::insert_last_layer() {
     modules.push_back(std::make_unique<GraphSum>(prev, z, graph.get(), hl, &ctx, true));
     auto out = std::make_shared<Variable>(prow, C, true, round_up4(C));
     variables.push_back(out);
-    modules.push_back(std::make_unique<Matmul>(z, weights.back(), out, part.local_rows(), hl, C,
-                                               &ctx));
+    auto mm = std::make_unique<Matmul>(z, weights.back(), out, part.local_rows(), hl, C, &ctx);
+    mm->last_layer = true;
+    modules.push_back(std::move(mm));
     modules.push_back(std::make_unique<CrossEntropyLoss>(out, C, &ctx));
+    if (!comm && graph) {  // compact output layer buffers (split rows, see ModuleContext)
+      size_t mx = 1;
+      for (int sp = 1; sp <= 3; sp++) mx = std::max(mx, split_rows_host[sp].size());
+      compact_z = std::make_unique<Variable>((int)mx, hl, true, round_up4(hl));
+      compact_out = std::make_unique<Variable>((int)mx, C, true, round_up4(C));
+      ctx.compact_z = compact_z.get();
+      ctx.compact_out = compact_out.get();
+    }
     return;
   }
   auto var1 = std::make_shared<Variable>(prow, C, true, round_up4(C));
@@ -448,6 +463,17 @@ void GCN::set_split(int split) {
   if (g_split_rows && !comm && graph && split == 1) {  // backward only follows training
     if (!split_colgraphs[split]) split_colgraphs[split] = graph->col_subset(split_rows_host[split]);
     ctx.split_colgraph = split_colgraphs[split].get();
+  }
+  // compact output layer: with the row restriction on the reassociated output layer
+  const int n_s = (int)split_rows_host[split].size();
+  if (ctx.split_graph && ctx.compact_z && n_s > 0) {
+    ctx.compact_n = n_s;
+    ctx.compact_truth = truth_compact[split].get();
+    ctx.xent_blocks = xent_blocks(n_s);
+  } else {
+    ctx.compact_n = 0;
+    ctx.compact_truth = nullptr;
+    ctx.xent_blocks = xent_blocks(part.maxrows);
   }
 }
 

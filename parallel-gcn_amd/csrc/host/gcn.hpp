@@ -111,6 +111,8 @@ class GCN {
   std::vector<int> split_rows_host[4];
   DeviceBuffer<int> split_rows_dev[4];
   std::unique_ptr<DevGraph> split_graphs[4], split_colgraphs[4];
+  DeviceBuffer<int> truth_compact[4];                // the split's labels, compact row order
+  std::unique_ptr<Variable> compact_z, compact_out;  // compact output layer (ModuleContext)
   long long nnz_x_global = 0;
   std::vector<int> feat_indptr_global;  // for the input dropout ranges
 

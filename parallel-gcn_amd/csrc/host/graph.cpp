@@ -856,20 +856,21 @@ void DevGraph::build_lds() {
 }
 
 void DevGraph::graphsum(const float *in, int ld_in, float *out, int ld_out, int dim,
-                        hipStream_t s) {
+                        hipStream_t s, bool compact_in) {
+  const int *col_map = compact_in ? nullptr : col_map_.get();
   PGCN_CHECK(ld_in % 4 == 0 && ld_out % 4 == 0 && ld_in >= dim && ld_out >= dim,
              PGCN_E_INVALID, "graphsum: leading dims must be multiples of 4 and >= dim");
   if (dim == 16 && g_graphsum_lds && !h_row_scale_.empty() && !g_graphsum_force_plain &&
       (double)n_cols_ * 64.0 > kL2Budget) {
     if (!lds_) build_lds();
     launch_graphsum_lds(lds_->s, in, ld_in, out, ld_out, lds_->scratch.get(),
-                        lds_->partial.get(), s, col_map_.get());
+                        lds_->partial.get(), s, col_map);
     return;
   }
-  if (col_map_) {  // plain path of a column subset: compact the input rows first
+  if (col_map) {  // plain path of a column subset: compact the input rows first
     const size_t need = (size_t)n_cols_ * ld_in;
     if (col_in_.size() < need) col_in_.allocate(need);
-    launch_gather_rows(in, col_map_.get(), n_cols_, ld_in, col_in_.get(), s);
+    launch_gather_rows(in, col_map, n_cols_, ld_in, col_in_.get(), s);
     in = col_in_.get();
   }
   const int vec = (dim + 3) / 4;

@@ -65,7 +65,9 @@ class DevGraph {
   int cols() const { return n_cols_; }
   long long nnz() const { return nnz_; }
   // out[i,:dim] = sum_j val_ij * in[col_j,:dim]
-  void graphsum(const float *in, int ld_in, float *out, int ld_out, int dim, hipStream_t s);
+  // compact_in (column subsets): `in` holds the subset's columns as its rows (no gather)
+  void graphsum(const float *in, int ld_in, float *out, int ld_out, int dim, hipStream_t s,
+                bool compact_in = false);
   // bytes the kernel must move at minimum (SURVEY.md §8d formula, per call)
   double algorithmic_bytes(int dim) const;
   // schedule statistics (for tests / reports)

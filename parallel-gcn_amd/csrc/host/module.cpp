@@ -235,22 +235,28 @@ void GraphSum::forward(bool training, const Stream &s) const {
   // output layer: only the split's labelled rows, summed compactly and scattered to their
   // rows; the other rows keep their last (finite) values, which meet only zero loss-gradient
   // rows in Matmul::backward and are skipped by the loss
-  const size_t need = (size_t)std::max(sg->rows(), 1) * out->ld;
-  if (compact.size() < need) compact.allocate(need);
+  float *dst;
+  if (ctx->compact_n) {  // the output Matmul and the loss read the compact rows themselves
+    dst = ctx->compact_z->dev_data.get();
+  } else {
+    const size_t need = (size_t)std::max(sg->rows(), 1) * out->ld;
+    if (compact.size() < need) compact.allocate(need);
+    dst = compact.get();
+  }
   Event e0, e1;
   if (ctx->profile) {
     e0 = Event::create(true);
     e1 = Event::create(true);
     e0.record(s.get());
   }
-  sg->graphsum(in->dev_data.get(), in->ld, compact.get(), out->ld, dim, s.get());
+  sg->graphsum(in->dev_data.get(), in->ld, dst, out->ld, dim, s.get());
   if (ctx->profile) {
     e1.record(s.get());
     ctx->gs_events->emplace_back(e0, e1);
     ctx->gs_bytes->push_back(sg->algorithmic_bytes(dim));
   }
-  launch_scatter_rows(compact.get(), ctx->split_rows, sg->rows(), out->ld, out->dev_data.get(),
-                      s.get());
+  if (!ctx->compact_n)
+    launch_scatter_rows(dst, ctx->split_rows, sg->rows(), out->ld, out->dev_data.get(), s.get());
 }
 
 void GraphSum::backward(const Stream &s) const {
@@ -268,7 +274,10 @@ void GraphSum::backward(const Stream &s) const {
     e1 = Event::create(true);
     e0.record(s.get());
   }
-  cg->graphsum(out->dev_grad.get(), out->ld, in->dev_grad.get(), in->ld, dim, s.get());
+  // (compact: the Matmul left out.grad in compact rows, which the column-subset graph reads
+  // as its columns directly; else it gathers them from the full rows)
+  const float *g_in = ctx->compact_n ? ctx->compact_z->dev_grad.get() : out->dev_grad.get();
+  cg->graphsum(g_in, out->ld, in->dev_grad.get(), in->ld, dim, s.get(), ctx->compact_n > 0);
   if (ctx->profile) {
     e1.record(s.get());
     ctx->gs_events->emplace_back(e0, e1);
@@ -300,16 +309,21 @@ Matmul::Matmul(shared_ptr<Variable> a_, shared_ptr<Variable> b_, shared_ptr<Vari
     : a(std::move(a_)), b(std::move(b_)), c(std::move(c_)), m(m_), n(n_), p(p_), ctx(ctx_) {}
 
 void Matmul::forward(bool, const Stream &s) const {
-  launch_gemm_nn(m, p, n, a->dev_data.get(), a->ld, b->dev_data.get(), b->ld, 0,
-                 c->dev_data.get(), c->ld, nullptr, 0, 0, 1.0f, s.get());
+  const bool cmp = last_layer && ctx->compact_n;  // compact output layer: the split's rows
+  const Variable &A = cmp ? *ctx->compact_z : *a, &C = cmp ? *ctx->compact_out : *c;
+  launch_gemm_nn(cmp ? ctx->compact_n : m, p, n, A.dev_data.get(), A.ld, b->dev_data.get(), b->ld,
+                 0, C.dev_data.get(), C.ld, nullptr, 0, 0, 1.0f, s.get());
 }
 
 void Matmul::backward(const Stream &s) const {
+  const bool cmp = last_layer && ctx->compact_n;
+  const Variable &A = cmp ? *ctx->compact_z : *a, &C = cmp ? *ctx->compact_out : *c;
+  const int rows = cmp ? ctx->compact_n : m;
   // a.grad = c.grad * b^T   (b stored [n][p] => trans_b)
-  launch_gemm_nn(m, n, p, c->dev_grad.get(), c->ld, b->dev_data.get(), b->ld, 1,
-                 a->dev_grad.get(), a->ld, nullptr, 0, 0, 1.0f, s.get());
+  launch_gemm_nn(rows, n, p, C.dev_grad.get(), C.ld, b->dev_data.get(), b->ld, 1,
+                 A.dev_grad.get(), A.ld, nullptr, 0, 0, 1.0f, s.get());
   // b.grad = a^T * c.grad (deterministic split-M reduction)
-  launch_gemm_tn(m, p, n, a->dev_data.get(), a->ld, c->dev_grad.get(), c->ld, b->dev_grad.get(),
+  launch_gemm_tn(rows, p, n, A.dev_data.get(), A.ld, C.dev_grad.get(), C.ld, b->dev_grad.get(),
                  b->ld, nullptr, 0, 0, 1.0f, ctx->gemm_workspace, s.get());
 }
 
@@ -321,9 +335,11 @@ CrossEntropyLoss::CrossEntropyLoss(shared_ptr<Variable> logits_, int num_classes
     : logits(std::move(logits_)), num_classes(num_classes_), ctx(ctx_) {}
 
 void CrossEntropyLoss::forward(bool training, const Stream &s) const {
-  launch_xent_fwd(logits->dev_data.get(), logits->ld, training ? logits->dev_grad.get() : nullptr,
-                  ctx->truth, logits->rows, num_classes, ctx->count, training ? 1 : 0,
-                  ctx->xent_partials, s.get());
+  const Variable &L = ctx->compact_n ? *ctx->compact_out : *logits;
+  launch_xent_fwd(L.dev_data.get(), L.ld, training ? L.dev_grad.get() : nullptr,
+                  ctx->compact_n ? ctx->compact_truth : ctx->truth,
+                  ctx->compact_n ? ctx->compact_n : logits->rows, num_classes, ctx->count,
+                  training ? 1 : 0, ctx->xent_partials, s.get());
 }
 
 void CrossEntropyLoss::backward(const Stream &) const {}  // module.cpp:155-156

@@ -98,6 +98,13 @@ struct ModuleContext {
   // ... and its backward: the loss gradient is zero outside those rows, so Â out.grad only
   // needs the edges into them (Â's columns of the split)
   DevGraph *split_colgraph = nullptr;
+  // compact output layer (reassociated order + row restriction): the last GraphSum writes the
+  // split's rows compactly ([compact_n][ld]) and the output Matmul and the loss work on those
+  // rows only; compact_n = 0: all rows
+  int compact_n = 0;
+  const int *compact_truth = nullptr;  // the split's labels in compact row order
+  Variable *compact_z = nullptr;       // last GraphSum output / Matmul input (+ grad)
+  Variable *compact_out = nullptr;     // logits (+ grad)
   const int *truth = nullptr;  // current split's truth (device)
   int count = 0;               // labelled rows of the current split (global)
   float *xent_partials = nullptr;
@@ -208,6 +215,7 @@ class Matmul : public Module {
   ModuleContext *ctx;
 
  public:
+  bool last_layer = false;  // the output layer's Matmul (compact rows apply)
   Matmul(shared_ptr<Variable> a_, shared_ptr<Variable> b_, shared_ptr<Variable> c_, int m_,
          int n_, int p_, ModuleContext *ctx_);
   void forward(bool training, const Stream &s) const override;
