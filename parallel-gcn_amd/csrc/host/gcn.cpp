@@ -19,6 +19,8 @@ int g_mask_side = 0;  // "mask_side" (read at engine build): see ModuleContext::
 // "eval_ax" (read at engine build): eval's first layer as (Â X) W1 from Â X computed once
 // (Â and X are constants: exact algebra, fp32 rounding order differs)
 int g_eval_ax = 1;
+// "epoch_graph" (read per epoch_async): replay a captured per-epoch hipGraph when eligible;
+int g_epoch_graph = 0;  // measured no faster than eager launches (r01: GPU-bound epochs)
 // "split_rows" (read at each split switch): the output layer's GraphSum forward computes only
 // the current split's labelled rows
 int g_split_rows = 1;
@@ -43,16 +45,26 @@ Adam::Adam(const std::vector<shared_ptr<Variable>> &weights, const std::vector<b
   }
 }
 
+float Adam::step_size(int t) const {
+  // hpdga optim.cpp:24, host float arithmetic with glibc powf/sqrtf
+  return params.learning_rate * sqrtf(1.0f - powf(params.beta2, (float)t)) /
+         (1.0f - powf(params.beta1, (float)t));
+}
+
 void Adam::step(const Stream &s) {
   step_count++;
-  // hpdga optim.cpp:24, host float arithmetic with glibc powf/sqrtf
-  const float step_size = params.learning_rate *
-                          sqrtf(1.0f - powf(params.beta2, (float)step_count)) /
-                          (1.0f - powf(params.beta1, (float)step_count));
+  const float st = step_size(step_count);
   for (auto &v : vars)
-    launch_adam(v.w->dev_data.get(), v.w->dev_grad.get(), v.m.get(), v.v.get(), v.w->size,
-                step_size, params.beta1, params.beta2, params.eps, params.weight_decay,
-                v.decay ? 1 : 0, s.get());
+    launch_adam(v.w->dev_data.get(), v.w->dev_grad.get(), v.m.get(), v.v.get(), v.w->size, st,
+                params.beta1, params.beta2, params.eps, params.weight_decay, v.decay ? 1 : 0,
+                s.get());
+}
+
+void Adam::step_graph(const Stream &s, const float *table, const int *ctr, int cap) const {
+  for (auto &v : vars)
+    launch_adam(v.w->dev_data.get(), v.w->dev_grad.get(), v.m.get(), v.v.get(), v.w->size, 0.0f,
+                params.beta1, params.beta2, params.eps, params.weight_decay, v.decay ? 1 : 0,
+                s.get(), table, ctr, cap);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -112,6 +124,7 @@ GCN::GCN(const GCNParams &params_, const AdamParams &adam, const GCNData &data, 
 
 GCN::~GCN() {
   if (stream.get()) (void)hipStreamSynchronize(stream.get());
+  drop_epoch_graph();
   if (side_stream.get()) (void)hipStreamSynchronize(side_stream.get());
   if (comm_stream.get()) (void)hipStreamSynchronize(comm_stream.get());
 }
@@ -477,29 +490,99 @@ void GCN::set_split(int split) {
   }
 }
 
-// loss/acc of the pass just enqueued -> results_ring slot (finalize, src/gcn.cu:440-455)
-void GCN::finalize(int dst_offset) {
+// loss/acc of the pass just enqueued -> results_ring slot (finalize, src/gcn.cu:440-455);
+// graph: the slot from the device epoch counter
+void GCN::finalize(int dst_offset, bool graph) {
   const auto &w1 = weights.front();
   launch_reduce_scalars(xent_partials.get(), ctx.xent_blocks, w1->dev_data.get(), w1->size,
                         sums.get(), stream.get());
   if (comm) comm->allreduce_sum(sums.get(), 2, stream.get());
-  launch_compose(sums.get(), ctx.count, adam_params.weight_decay, results_ring.get() + dst_offset,
-                 stream.get());
+  if (graph)
+    launch_compose(sums.get(), ctx.count, adam_params.weight_decay, results_ring.get() + dst_offset,
+                   stream.get(), dev_ctr.get(), ring_cap);
+  else
+    launch_compose(sums.get(), ctx.count, adam_params.weight_decay, results_ring.get() + dst_offset,
+                   stream.get());
+}
+
+// train_epoch (src/gcn.cu:307-343) + eval(2) (src/gcn.cu:293-303), host-sync free
+void GCN::enqueue_epoch(bool graph) {
+  const int slot4 = graph ? 0 : (int)(epoch_count % ring_cap) * 4;
+  set_split(1);
+  for (const auto &m : modules) m->forward(true, stream);
+  finalize(slot4, graph);
+  for (int i = (int)modules.size() - 1; i >= 0; i--) modules[(size_t)i]->backward(stream);
+  if (comm) comm->allreduce_sum(grad_arena.get(), grad_arena.size(), stream.get());
+  if (graph)
+    optimizer.step_graph(stream, step_table.get(), dev_ctr.get(), kStepTable);
+  else
+    optimizer.step(stream);
+  set_split(2);
+  for (const auto &m : modules) m->forward(false, stream);
+  finalize(slot4 + 2, graph);
+  if (graph) launch_counters(dev_ctr.get(), 0, 0, 0, stream.get());
+}
+
+// A replayed epoch must launch exactly what an eager one would: no host-side state may change
+// between epochs.  Excluded: the edge-cut engine (RCCL calls), GraphSum profiling (host
+// events), and train-ahead over dense X without eval_ax (it swaps buffers on the host between
+// eval and the next training forward), mask_side (side stream).
+bool GCN::graph_eligible() const {
+  if (!g_epoch_graph || !warm || comm || ctx.profile || ctx.mask_side) return false;
+  if (ctx.train_ahead && feats.dense && feats.maskT && !feats.ax) return false;
+  return true;
+}
+
+void GCN::drop_epoch_graph() {
+  if (epoch_exec) (void)hipGraphExecDestroy(epoch_exec);
+  if (epoch_graph) (void)hipGraphDestroy(epoch_graph);
+  epoch_exec = nullptr;
+  epoch_graph = nullptr;
+}
+
+void GCN::capture_epoch() {
+  if (!dev_ctr) {
+    dev_ctr.allocate(2);
+    step_table.allocate(kStepTable);
+  }
+  PGCN_HIP(hipStreamBeginCapture(stream.get(), hipStreamCaptureModeThreadLocal));
+  try {
+    enqueue_epoch(true);
+  } catch (...) {
+    hipGraph_t g = nullptr;
+    (void)hipStreamEndCapture(stream.get(), &g);
+    if (g) (void)hipGraphDestroy(g);
+    throw;
+  }
+  PGCN_HIP(hipStreamEndCapture(stream.get(), &epoch_graph));
+  PGCN_HIP(hipGraphInstantiate(&epoch_exec, epoch_graph, nullptr, nullptr, 0));
 }
 
 void GCN::epoch_async() {
-  const long long slot = epoch_count % ring_cap;
-  // train_epoch (src/gcn.cu:307-343)
-  set_split(1);
-  for (const auto &m : modules) m->forward(true, stream);
-  finalize((int)(slot * 4));
-  for (int i = (int)modules.size() - 1; i >= 0; i--) modules[(size_t)i]->backward(stream);
-  if (comm) comm->allreduce_sum(grad_arena.get(), grad_arena.size(), stream.get());
-  optimizer.step(stream);
-  // eval(2) (src/gcn.cu:293-303)
-  set_split(2);
-  for (const auto &m : modules) m->forward(false, stream);
-  finalize((int)(slot * 4 + 2));
+  if (!graph_eligible()) {
+    enqueue_epoch(false);
+    ctr_valid = false;
+    warm = true;
+  } else {
+    if (!epoch_exec) capture_epoch();
+    // the step size table covers this epoch's Adam step (index = steps done % cap)
+    const long long t = optimizer.steps(), block = t / kStepTable;
+    if (block != table_block) {
+      stream.sync();  // replays already queued read the old table
+      std::vector<float> tab(kStepTable);
+      for (int i = 0; i < kStepTable; i++)
+        tab[(size_t)i] = optimizer.step_size((int)(block * kStepTable + i + 1));
+      step_table.upload(tab);
+      table_block = block;
+    }
+    if (!ctr_valid) {
+      launch_counters(dev_ctr.get(), 1, (int)t, (int)epoch_count, stream.get());
+      ctr_valid = true;
+    }
+    PGCN_HIP(hipGraphLaunch(epoch_exec, stream.get()));
+    optimizer.advance();
+    set_split(2);  // host context as after an eager epoch
+  }
   last_forward_training = false;
   epoch_count++;
 }
@@ -512,6 +595,7 @@ std::pair<float, float> GCN::train_epoch() {
   for (int i = (int)modules.size() - 1; i >= 0; i--) modules[(size_t)i]->backward(stream);
   if (comm) comm->allreduce_sum(grad_arena.get(), grad_arena.size(), stream.get());
   optimizer.step(stream);
+  ctr_valid = false;
   last_forward_training = true;
   PGCN_HIP(hipMemcpyAsync(pinned.get(), results_ring.get() + slot * 4, 2 * sizeof(float),
                           hipMemcpyDeviceToHost, stream.get()));
@@ -526,6 +610,7 @@ std::pair<float, float> GCN::eval(int split) {
   for (const auto &m : modules) m->forward(false, stream);
   finalize((int)(slot * 4 + 2));
   last_forward_training = false;
+  ctr_valid = false;
   PGCN_HIP(hipMemcpyAsync(pinned.get(), results_ring.get() + slot * 4 + 2, 2 * sizeof(float),
                           hipMemcpyDeviceToHost, stream.get()));
   stream.sync();

@@ -55,6 +55,12 @@ class Adam {
   Adam(const std::vector<shared_ptr<Variable>> &weights, const std::vector<bool> &decays,
        const AdamParams &p);
   void step(const Stream &s);
+  // epoch graphs: the same launches reading the step size from table[ctr[0] % cap] on the
+  // device (the host counts the step with advance() at every replay)
+  void step_graph(const Stream &s, const float *table, const int *ctr, int cap) const;
+  void advance() { step_count++; }
+  int steps() const { return step_count; }
+  float step_size(int t) const;  // hpdga optim.cpp:24, step t (1-based)
 };
 
 struct DistSpec {
@@ -89,7 +95,11 @@ class GCN {
   void insert_layer(int in_dim, int out_dim, float dropout, int layer);
   void insert_last_layer();
   void set_split(int split);
-  void finalize(int slot_offset);
+  void finalize(int slot_offset, bool graph = false);
+  void enqueue_epoch(bool graph);
+  bool graph_eligible() const;
+  void capture_epoch();
+  void drop_epoch_graph();
 
   GCNParams params;
   AdamParams adam_params;
@@ -131,6 +141,20 @@ class GCN {
   int ring_cap = 1024;
   long long epoch_count = 0;
   bool last_forward_training = false;
+
+  // Per-epoch hipGraph: epoch_async() replays one captured
+  // train_epoch + eval(2).  Everything that changes between epochs lives on the device:
+  // the dropout RNG chunk states advance themselves, the Adam step size comes from a host-
+  // computed table indexed by a device step counter, the results-ring slot from a device
+  // epoch counter, both advanced by the epoch's last kernel.
+  hipGraph_t epoch_graph = nullptr;
+  hipGraphExec_t epoch_exec = nullptr;
+  DeviceBuffer<int> dev_ctr;          // {Adam steps done, epochs done}
+  DeviceBuffer<float> step_table;     // step sizes of steps table_block * cap + 1 ...
+  static constexpr int kStepTable = 4096;
+  long long table_block = -1;
+  bool ctr_valid = false;             // dev_ctr equals the host counters
+  bool warm = false;                  // one eager epoch_async ran (lazy buffers exist)
 
   std::vector<std::pair<Event, Event>> gs_events;
   std::vector<double> gs_bytes;

@@ -350,8 +350,10 @@ __global__ __launch_bounds__(1024) void k_reduce_scalars(const float *__restrict
 
 // out2 = {loss_sum/count + wd*l2/2, (count-wrong)/count}   (hpdga gcn.cpp:167-198)
 __global__ void k_compose(const float *__restrict__ sums, int count, float wd,
-                          float *__restrict__ out2) {
+                          float *__restrict__ out2, const int *__restrict__ ctr, int ring_cap) {
   if (threadIdx.x == 0) {
+    // epoch graphs: the results-ring slot from the device epoch counter (ctr[1])
+    if (ctr) out2 += 4 * (ctr[1] % ring_cap);
     const float loss = sums[0] / (float)count;
     const float l2 = wd * sums[2] / 2.0f;
     out2[0] = loss + l2;
@@ -364,7 +366,11 @@ __global__ void k_compose(const float *__restrict__ sums, int count, float wd,
 __global__ __launch_bounds__(256) void k_adam(float *__restrict__ w, const float *__restrict__ g,
                                               float *__restrict__ m, float *__restrict__ v,
                                               long long n, float step_size, float beta1,
-                                              float beta2, float eps, float wd, int decay) {
+                                              float beta2, float eps, float wd, int decay,
+                                              const float *__restrict__ step_table,
+                                              const int *__restrict__ ctr, int table_cap) {
+  // epoch graphs: the step size of step ctr[0] + 1, computed on the host (optim.cpp:24)
+  if (step_table) step_size = step_table[ctr[0] % table_cap];
   const double ob1 = 1.0 - (double)beta1, ob2 = 1.0 - (double)beta2;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x) {
@@ -441,15 +447,34 @@ void launch_reduce_scalars(const float *partials, int n_blocks, const float *w, 
                      sums);
 }
 
-void launch_compose(const float *sums, int count, float wd, float *out2, hipStream_t s) {
-  hipLaunchKernelGGL(k_compose, dim3(1), dim3(64), 0, s, sums, count, wd, out2);
+void launch_compose(const float *sums, int count, float wd, float *out2, hipStream_t s,
+                    const int *ctr, int ring_cap) {
+  hipLaunchKernelGGL(k_compose, dim3(1), dim3(64), 0, s, sums, count, wd, out2, ctr, ring_cap);
+}
+
+// epoch graphs: the device copy of the host's (Adam step, epoch) counters
+__global__ void k_counters(int *ctr, int set, int step, int epoch) {
+  if (threadIdx.x == 0) {
+    if (set) {
+      ctr[0] = step;
+      ctr[1] = epoch;
+    } else {
+      ctr[0] += 1;
+      ctr[1] += 1;
+    }
+  }
+}
+
+void launch_counters(int *ctr, int set, int step, int epoch, hipStream_t s) {
+  hipLaunchKernelGGL(k_counters, dim3(1), dim3(64), 0, s, ctr, set, step, epoch);
 }
 
 void launch_adam(float *w, const float *g, float *m, float *v, long long n, float step_size,
-                 float beta1, float beta2, float eps, float wd, int decay, hipStream_t s) {
+                 float beta1, float beta2, float eps, float wd, int decay, hipStream_t s,
+                 const float *step_table, const int *ctr, int table_cap) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_adam, dim3(grid_for(n)), dim3(256), 0, s, w, g, m, v, n, step_size,
-                     beta1, beta2, eps, wd, decay);
+                     beta1, beta2, eps, wd, decay, step_table, ctr, table_cap);
 }
 
 }  // namespace pgcn

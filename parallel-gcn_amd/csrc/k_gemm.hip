@@ -685,7 +685,15 @@ __global__ __launch_bounds__(256) void k_slab_reduce1(const float *__restrict__ 
   if (e >= elems) return;
   const int s0 = blockIdx.y * spg, s1 = min(n_slabs, s0 + spg);
   float s = 0.0f;
-  for (int b = s0; b < s1; b++) s += partial[(long long)b * elems + e];
+  // loads in batches of 16 before their (ordered) adds: one memory latency per batch
+  for (int b0 = s0; b0 < s1; b0 += 16) {
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 16; u++) v[u] = b0 + u < s1 ? partial[(long long)(b0 + u) * elems + e] : 0.0f;
+#pragma unroll
+    for (int u = 0; u < 16; u++)
+      if (b0 + u < s1) s += v[u];
+  }
   part2[(long long)blockIdx.y * elems + e] = s;
 }
 

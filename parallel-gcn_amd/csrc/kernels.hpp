@@ -102,8 +102,14 @@ void launch_xent_fwd(float *logits, int ld, float *grad, const int *truth, int n
                      int count, int training, float *partials, hipStream_t s);
 void launch_reduce_scalars(const float *partials, int n_blocks, const float *w, long long n_w,
                            float *sums, hipStream_t s);
-void launch_compose(const float *sums, int count, float wd, float *out2, hipStream_t s);
+// ctr (epoch graphs, device {Adam step, epoch} counters): slot 4 * (ctr[1] % ring_cap) of out2
+void launch_compose(const float *sums, int count, float wd, float *out2, hipStream_t s,
+                    const int *ctr = nullptr, int ring_cap = 1);
+// step_table (epoch graphs): step_size = step_table[ctr[0] % table_cap]
 void launch_adam(float *w, const float *g, float *m, float *v, long long n, float step_size,
-                 float beta1, float beta2, float eps, float wd, int decay, hipStream_t s);
+                 float beta1, float beta2, float eps, float wd, int decay, hipStream_t s,
+                 const float *step_table = nullptr, const int *ctr = nullptr, int table_cap = 1);
+// set: ctr = {step, epoch}; else both += 1 (the end of a graph-replayed epoch)
+void launch_counters(int *ctr, int set, int step, int epoch, hipStream_t s);
 
 }  // namespace pgcn

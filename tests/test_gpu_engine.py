@@ -263,3 +263,47 @@ def test_eval_ax_matches_graphsum_of_xw(pgcn):
     np.testing.assert_array_equal(a[0, :2], b[0, :2])  # epoch 1's training pass: same bits
     np.testing.assert_allclose(a[:, [0, 2]], b[:, [0, 2]], rtol=1e-5)
     np.testing.assert_allclose(a[:, [1, 3]], b[:, [1, 3]], atol=2e-4)
+
+
+def _graph_vs_eager(pgcn, ds, schedule, n_res=8):
+    runs = []
+    for on in (0, 1):
+        pgcn.lib.pgcn_debug_set(b"epoch_graph", on)
+        g = pgcn.GCN(pgcn.make_params(ds), ds, device=0)
+        lines = []
+        for step in schedule:
+            if step == "train":
+                lines.append(g.train_epoch())
+            elif step == "eval3":
+                lines.append(g.eval(3))
+            else:
+                for _ in range(step):
+                    g.epoch_async()
+                lines.append(tuple(g.results(min(step, n_res)).ravel()))
+        lines.append(tuple(g.get_var(2).ravel()))  # W1
+        lines.append(tuple(g.get_var(5 if g.num_vars() == 7 else g.num_vars() - 2).ravel()))
+        runs.append(lines)
+        g.close()
+    pgcn.lib.pgcn_debug_set(b"epoch_graph", 0)  # the engine default
+    for a, b in zip(*runs):
+        np.testing.assert_array_equal(np.asarray(a, np.float32), np.asarray(b, np.float32))
+
+
+def test_epoch_graph_bit_identical_cora(loaded, pgcn):
+    """The per-epoch hipGraph replay (epoch_async) gives the same bits as eager epochs, with
+    eager train_epoch/eval calls in between (device counters re-synced), over 4,200 epochs
+    (the Adam step-size table block of 4,096 steps and the 1,024-slot results ring wrap)."""
+    _graph_vs_eager(pgcn, loaded["cora"], [3, "train", "eval3", 5, "train", 4200, 2])
+
+
+def test_epoch_graph_bit_identical_dense_lds(pgcn):
+    """The same on a dense-feature graph that takes the LDS GraphSum, eval_ax and the compact
+    output layer (the reddit configuration), and with eval_ax off, where train-ahead swaps
+    buffers on the host and the engine stays eager (same bits either way)."""
+    ds = pgcn.Dataset.synthetic(80000, 40, 8, 2000000, 11)
+    _graph_vs_eager(pgcn, ds, [2, "train", 6, "eval3", 3])
+    pgcn.lib.pgcn_debug_set(b"eval_ax", 0)
+    try:
+        _graph_vs_eager(pgcn, ds, [2, "train", 4])
+    finally:
+        pgcn.lib.pgcn_debug_set(b"eval_ax", 1)

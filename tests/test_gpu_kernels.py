@@ -402,6 +402,37 @@ def test_spmm_csr_and_csc_bit_exact(pgcn, loaded):
     np.testing.assert_array_equal(wg.cpu().numpy(), ref_w)
 
 
+@pytest.mark.parametrize("p", [16, 41, 128])
+def test_spmm_csc_long_columns_bit_exact(pgcn, p):
+    """The W-grad kernel on columns of ~1,000 entries (several 256-entry LDS chunks), widths
+    that are not 16 (several column groups; an ld that is not a multiple of 4): the same bits
+    as hpdga's scatter loop."""
+    lib = helpers.oracle()
+    rng = np.random.default_rng(p)
+    n, F = 3000, 37
+    dense = rng.random((n, F)) < 0.33
+    ip = np.concatenate([[0], np.cumsum(dense.sum(1))]).astype(np.int32)
+    ix = np.nonzero(dense)[1].astype(np.int32)
+    xv = rng.standard_normal(len(ix)).astype(np.float32)
+    nnz = len(ix)
+    Gm = rng.standard_normal((n, p)).astype(np.float32)
+    mask = rng.integers(0, 2**63, (nnz + 63) // 64 + 1, dtype=np.uint64)
+    xd = xv * np.where(mask_bits(mask, nnz), np.float32(2.0), np.float32(0.0)).astype(np.float32)
+    ref_w = np.zeros((F, p), np.float32)
+    lib.or_spmm_bwd(n, F, helpers.ptr(ip), helpers.ptr(ix), helpers.ptr(xd), helpers.ptr(ref_w),
+                    helpers.ptr(Gm), p)
+    cp, cr, cpos = pgcn.csr_transpose(ip, ix, F)
+    t = {k: torch.from_numpy(v).to(DEV) for k, v in
+         dict(xv=xv, G=Gm, cp=cp, cr=cr, cpos=cpos).items()}
+    dm = torch.from_numpy(mask.view(np.int64)).to(DEV)
+    wg = torch.full((F, p), float("nan"), device=DEV)
+    pgcn.check(pgcn.lib.pgcn_spmm_csc_bwd(F, p, vp(t["cp"]), vp(t["cr"]), vp(t["cpos"]),
+                                          vp(t["xv"]), vp(dm), 2.0, vp(t["G"]), vp(wg), stream()),
+               "csc")
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(wg.cpu().numpy(), ref_w)
+
+
 def test_adam_bit_exact(pgcn):
     lib = helpers.oracle()
     rng = np.random.default_rng(5)

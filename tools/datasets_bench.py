@@ -1,0 +1,95 @@
+"""Epochs/s on the small datasets (cora, citeseer, pubmed_synth) on one GPU, beside the
+reference's own sequential epoch on this host ("epochs/sec on
+citeseer/cora/pubmed/reddit").  Diagnostic tool; bench.py stays the reddit headline.
+
+usage: python3 tools/datasets_bench.py [--epochs 200] [--graph 0|1|both] [--out file.json]
+
+Two GPU numbers per dataset:
+  * "async": epoch_async() back to back (metrics go to the device results ring, one host
+    sync at the end) -- the engine's throughput;
+  * "reference_loop": train_epoch() + eval(2) with their host reads of loss/accuracy every
+    epoch, i.e. the reference's own run() loop (src/gcn.cu:363-375), timed per epoch and
+    reported as 100 / sum of epoch times like TMR_TRAIN.
+The CPU leg is oracle/_ref (the reference's hpdga sources, 1 thread) when built, else the C
+restatement.  Inputs come from the committed fixtures (tests/golden/data).
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+import torch  # noqa: F401  (one HIP runtime per process: torch's)
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+import helpers  # noqa: E402
+
+
+def gpu_rates(pg, ds, epochs, graph):
+    pg.lib.pgcn_debug_set(b"epoch_graph", graph)
+    g = pg.GCN(pg.make_params(ds), ds, device=0)
+    for _ in range(5):
+        g.epoch_async()
+    g.sync()
+    t0 = time.perf_counter()
+    for _ in range(epochs):
+        g.epoch_async()
+    g.sync()
+    async_rate = epochs / (time.perf_counter() - t0)
+    res = g.results(1)
+    total = 0.0
+    for _ in range(min(epochs, 100)):
+        t0 = time.perf_counter()
+        g.train_epoch()
+        g.eval(2)
+        total += time.perf_counter() - t0
+    g.close()
+    pg.lib.pgcn_debug_set(b"epoch_graph", 0)
+    return async_rate, min(epochs, 100) / total, res
+
+
+def cpu_rate(ds, reps):
+    import bench
+    kind, times = bench.cpu_baseline(ds, reps)
+    return kind, len(times) / sum(times)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--epochs", type=int, default=200)
+    ap.add_argument("--graph", default="both", choices=["0", "1", "both"])
+    ap.add_argument("--cpu-reps", type=int, default=5)
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--only", default=None, help="one dataset (e.g. under rocprofv3)")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+    sys.path.insert(0, REPO)
+    pg = helpers.pgcn()
+    modes = [0, 1] if args.graph == "both" else [int(args.graph)]
+    out = {}
+    with tempfile.TemporaryDirectory() as root:
+        for name in ((args.only,) if args.only else ("cora", "citeseer", "pubmed_synth")):
+            dname = helpers.materialize_dataset(name, root)
+            ds = pg.Dataset.load(root, dname)
+            row = {"nodes": int(ds.num_nodes), "adjacency_nnz": int(ds.graph_indptr[-1])}
+            for m in modes:
+                a, r, res = gpu_rates(pg, ds, args.epochs, m)
+                key = "graph" if m else "eager"
+                row[f"{key}_async_epochs_s"] = a
+                row[f"{key}_reference_loop_epochs_s"] = r
+                row[f"{key}_last"] = [float(v) for v in np.asarray(res).ravel()]
+            if not args.no_cpu:
+                kind, c = cpu_rate(ds, args.cpu_reps)
+                row["cpu_epochs_s"] = c
+                row["cpu_kind"] = kind
+            out[name] = row
+            print(name, json.dumps(row), flush=True)
+    if args.out:
+        json.dump(out, open(args.out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
