@@ -286,8 +286,9 @@ void GCN::build(const GCNData &data) {
   }
   upload_features(data);
   // eval_ax: Â X once (16 columns per d = 16 GraphSum; the last chunk overlaps the one
-  // before it so it never reads past a row), single GPU, dense X on the X-stream path
-  if (g_eval_ax && !comm && graph && feats.dense && feats.maskT && feats.cols >= 16) {
+  // before it so it never reads past a row), single GPU, dense X (eval's (Â X) W1 runs on the
+  // X-stream kernel for hidden <= 16, the MFMA GEMM for wider first layers)
+  if (g_eval_ax && !comm && graph && feats.dense && feats.cols >= 16) {
     feats.ax.allocate(feats.x.size());
     feats.ax.zero();
     for (int c0 = 0; c0 < feats.cols; c0 += 16) {

@@ -102,8 +102,12 @@ void SparseMatmul::forward(bool training, const Stream &s) const {
   const long long base = drop->state().mask_base;
   const float scale = drop->scale();
   if (!training && x->ax && eval_out) {  // eval_ax: (Â X) W1 straight into the GraphSum's output
-    launch_xstream_nn(x->rows, b->cols, x->cols, x->ax.get(), x->ldx, b->dev_data.get(), b->ld, 0,
-                      eval_out->dev_data.get(), eval_out->ld, nullptr, 1.0f, s.get(), nullptr);
+    if (xstream_ok(b->cols, x->cols))
+      launch_xstream_nn(x->rows, b->cols, x->cols, x->ax.get(), x->ldx, b->dev_data.get(), b->ld,
+                        0, eval_out->dev_data.get(), eval_out->ld, nullptr, 1.0f, s.get(), nullptr);
+    else
+      launch_gemm_nn(x->rows, b->cols, x->cols, x->ax.get(), x->ldx, b->dev_data.get(), b->ld, 0,
+                     eval_out->dev_data.get(), eval_out->ld, nullptr, 0, 0, 1.0f, s.get());
     return;
   }
   if (training && ahead_valid) {  // computed by the eval forward before this one

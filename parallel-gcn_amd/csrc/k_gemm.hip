@@ -795,6 +795,7 @@ static TnPlan tn_plan(int M, int N, int K) {
   p.nkc = (K + 63) / 64;
   p.wk = p.nkc >= 4 ? 4 : (p.nkc >= 2 ? 2 : 1);
   p.kcw = std::min(3, (p.nkc + p.wk - 1) / p.wk);
+  if (p.nj > 4) p.kcw = 1;  // accumulators: 16 * kcw * nj registers (instantiated: kcw 1)
   p.kgroups = (p.nkc + p.wk * p.kcw - 1) / (p.wk * p.kcw);
   const int wr = 4 / p.wk;
   long long slab = ceil_div(M, 1024);  // ~4 blocks per CU: memory parallelism for the stream

@@ -246,12 +246,14 @@ def test_split_rows_restriction_matches_all_rows(pgcn):
     np.testing.assert_allclose(w2a, w2b, rtol=1e-4, atol=1e-6)
 
 
-def test_eval_ax_matches_graphsum_of_xw(pgcn):
+@pytest.mark.parametrize("hidden", [16, 64])
+def test_eval_ax_matches_graphsum_of_xw(pgcn, hidden):
     """eval's first layer from Â X computed once at build ((Â X) W1 instead of Â (X W1): the same
     product, another fp32 rounding order) gives the same eval losses and accuracies, and leaves
-    training untouched (bit-identical training lines), on a graph that takes the LDS path."""
+    training untouched (bit-identical training lines), on a graph that takes the LDS path
+    (hidden 16: X-stream kernel; hidden 64: MFMA GEMM for (Â X) W1)."""
     ds = pgcn.Dataset.synthetic(80000, 40, 8, 2000000, 9)  # dense features, F = 40
-    p = pgcn.make_params(ds)
+    p = pgcn.make_params(ds, hidden_dims=(hidden,))
     runs = []
     for on in (1, 0):
         pgcn.lib.pgcn_debug_set(b"eval_ax", on)

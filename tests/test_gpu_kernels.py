@@ -269,7 +269,8 @@ def test_gemm_nn(pgcn, M, N, K, drop, base, variant):
 @pytest.mark.parametrize("M,N,K,drop,base", [(5000, 16, 602, True, 0), (3000, 41, 16, False, 0),
                                              (2000, 128, 128, False, 0), (100, 16, 1433, True, 0),
                                              (70000, 16, 602, False, 0), (4099, 16, 602, True, 29),
-                                             (333, 16, 200, True, 63), (7, 11, 602, True, 5)])
+                                             (333, 16, 200, True, 63), (7, 11, 602, True, 5),
+                                             (3000, 128, 602, True, 0), (2000, 80, 300, True, 3)])
 def test_gemm_tn(pgcn, M, N, K, drop, base, variant):
     rng = np.random.default_rng(M + 3 * N + K)
     lda = (K + 3) // 4 * 4
