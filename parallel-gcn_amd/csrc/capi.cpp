@@ -27,6 +27,7 @@ extern int g_eval_ax;               // host/gcn.cpp
 extern int g_epoch_graph;           // host/gcn.cpp
 extern int g_lds_blocks;            // host/graph.cpp
 extern int g_graphsum_lds;          // host/graph.cpp (diagnostics)
+extern int g_graphsum_lds_wide;     // host/graph.cpp
 extern int g_graphsum_lds_order;    // host/graph.cpp (diagnostics)
 extern int g_graphsum_lds_diag;     // k_graphsum_lds.hip (diagnostics)
 extern int g_graphsum_lds_window;   // host/graph.cpp (diagnostics)
@@ -448,6 +449,7 @@ int pgcn_debug_set(const char *key, int value) {
   if (!std::strcmp(key, "graphsum_variant")) pgcn::g_graphsum_variant = value;
   else if (!std::strcmp(key, "graphsum_plain")) pgcn::g_graphsum_force_plain = value;
   else if (!std::strcmp(key, "graphsum_lds")) pgcn::g_graphsum_lds = value;
+  else if (!std::strcmp(key, "graphsum_lds_wide")) pgcn::g_graphsum_lds_wide = value;
   else if (!std::strcmp(key, "graphsum_lds_order")) pgcn::g_graphsum_lds_order = value;
   else if (!std::strcmp(key, "graphsum_lds_diag")) pgcn::g_graphsum_lds_diag = value;
   else if (!std::strcmp(key, "graphsum_lds_window")) pgcn::g_graphsum_lds_window = value;

@@ -303,6 +303,7 @@ void DevGraph::set_scales(std::vector<float> row_scale, std::vector<float> col_s
 static const int kLdsLaneGroups[4][4] = {{0, 3, 5, 6}, {1, 2, 4, 7}, {8, 11, 13, 14}, {9, 10, 12, 15}};
 
 int g_graphsum_lds = 1;
+int g_graphsum_lds_wide = 1;  // "graphsum_lds_wide": rows wider than 16 as 16-column LDS passes
 // "graphsum_lds_window": 1 = slots one after another; 2 = two-slot runs (exec-masked; slower on
 // gfx950); 3 = slot pairs interleaved block by block (two blocks of LDS reads in flight; r01:
 // same time as 1 -- the kernel is not bound by per-wave LDS latency)
@@ -860,11 +861,19 @@ void DevGraph::graphsum(const float *in, int ld_in, float *out, int ld_out, int 
   const int *col_map = compact_in ? nullptr : col_map_.get();
   PGCN_CHECK(ld_in % 4 == 0 && ld_out % 4 == 0 && ld_in >= dim && ld_out >= dim,
              PGCN_E_INVALID, "graphsum: leading dims must be multiples of 4 and >= dim");
-  if (dim == 16 && g_graphsum_lds && !h_row_scale_.empty() && !g_graphsum_force_plain &&
-      (double)n_cols_ * 64.0 > kL2Budget) {
+  if ((dim == 16 || (dim > 16 && g_graphsum_lds_wide)) && g_graphsum_lds &&
+      !h_row_scale_.empty() && !g_graphsum_force_plain && (double)n_cols_ * 64.0 > kL2Budget) {
     if (!lds_) build_lds();
-    launch_graphsum_lds(lds_->s, in, ld_in, out, ld_out, lds_->scratch.get(),
-                        lds_->partial.get(), s, col_map);
+    // wider rows: one LDS pass per 16 columns (the last pass overlaps the one before it so it
+    // stays inside both leading dims; overlapped columns are recomputed to the same bits).
+    // d = 128 on reddit: 8 passes ~2.7 ms against ~7 ms for the gather kernel, whose 512-B
+    // rows come from the Infinity Cache at ~7.7 TB/s
+    const int ldm = std::min(ld_in, ld_out);
+    for (int c0 = 0; c0 < dim; c0 += 16) {
+      const int c = std::min(c0, ldm - 16);
+      launch_graphsum_lds(lds_->s, in + c, ld_in, out + c, ld_out, lds_->scratch.get(),
+                          lds_->partial.get(), s, col_map);
+    }
     return;
   }
   if (col_map) {  // plain path of a column subset: compact the input rows first

@@ -142,6 +142,29 @@ def test_graphsum_lds_column_blocks(pgcn, blocks):
         pgcn.lib.pgcn_debug_set(b"lds_blocks", 0)
 
 
+@pytest.mark.parametrize("dim,ld", [(128, 128), (41, 44), (24, 24)])
+def test_graphsum_lds_wide_rows(pgcn, dim, ld):
+    """Rows wider than 16 on a graph that takes the LDS GraphSum: one 16-column LDS pass per
+    chunk (the last one overlapping), against the oracle; padding columns stay zero."""
+    n = 120000
+    indptr, indices = random_graph(n, 30, seed=dim, hubs=10, hub_deg=3000)
+    x = np.zeros((n, ld), np.float32)
+    x[:, :dim] = np.random.default_rng(dim).standard_normal((n, dim))
+    g = ctypes.c_void_p()
+    pgcn.check(pgcn.lib.pgcn_graph_create(n, helpers.ptr(indptr), helpers.ptr(indices),
+                                          ctypes.byref(g)), "graph_create")
+    xin = torch.from_numpy(x).to(DEV)
+    out = torch.full((n, ld), float("nan"), device=DEV)
+    pgcn.check(pgcn.lib.pgcn_graphsum(g, vp(xin), ld, vp(out), ld, dim, stream()), "gs")
+    torch.cuda.synchronize()
+    ours = out.cpu().numpy()
+    ref = oracle_graphsum(indptr, indices, x, dim)
+    bound = abs_bound(indptr, indices, x, dim)
+    assert (np.abs(ours[:, :dim] - ref) <= 1e-5 * bound + 1e-30).all()
+    np.testing.assert_array_equal(ours[:, dim:], 0.0)
+    pgcn.lib.pgcn_graph_destroy(g)
+
+
 def test_graphsum_linearity_large(pgcn):
     """Size-independent property at reddit-like density: GraphSum(a x + b y) == a GS(x) + b GS(y)."""
     n = 200000
