@@ -215,6 +215,16 @@ typedef struct pgcn_dataset pgcn_dataset;
 /* Parser(GCNParams*, GCNData*, name).parse(): reads data/<name>.{graph,split,svmlight}
  * under `root` with hpdga-spring23/src/parser.cpp:6-140 semantics. */
 int pgcn_dataset_load(const char *root, const char *name, pgcn_dataset **out);
+/* The same load through the binary cache <root>/data/<name>.pgcnbin:
+ * read when its recorded size + mtime of the three text files match, else the text is parsed
+ * (identical arrays) and the cache rewritten, best effort.  *from_cache (may be NULL) = 1 on a
+ * cache hit.  Errors as pgcn_dataset_load. */
+int pgcn_dataset_load_cached(const char *root, const char *name, pgcn_dataset **out,
+                             int *from_cache);
+/* Write / read the parsed arrays as one binary file (any dataset, synthetic ones included).
+ * PGCN_E_IO on a write failure or an invalid / truncated / corrupted file. */
+int pgcn_dataset_save(const pgcn_dataset *ds, const char *path);
+int pgcn_dataset_load_binary(const char *path, pgcn_dataset **out);
 /* Seeded reddit-shaped synthetic: n nodes, f dense features, c classes,
  * Chung-Lu power-law undirected graph with `undirected_edges` edges (2x directed slots). */
 int pgcn_dataset_synthetic(int n, int f, int c, long long undirected_edges, uint64_t seed,

@@ -111,6 +111,9 @@ _sig("pgcn_gcn_profile", c_int, c_void_p, c_int)
 _sig("pgcn_gcn_profile_read", c_int, c_void_p, P(c_double), P(c_ll), P(c_double))
 _sig("pgcn_gcn_node_range", c_int, c_void_p, P(c_int), P(c_int))
 _sig("pgcn_dataset_load", c_int, ctypes.c_char_p, ctypes.c_char_p, P(c_void_p))
+_sig("pgcn_dataset_load_cached", c_int, ctypes.c_char_p, ctypes.c_char_p, P(c_void_p), P(c_int))
+_sig("pgcn_dataset_save", c_int, c_void_p, ctypes.c_char_p)
+_sig("pgcn_dataset_load_binary", c_int, ctypes.c_char_p, P(c_void_p))
 _sig("pgcn_dataset_synthetic", c_int, c_int, c_int, c_int, c_ll, c_u64, P(c_void_p))
 _sig("pgcn_dataset_view", c_int, c_void_p, P(PgcnData), P(c_int), P(c_int))
 _sig("pgcn_dataset_free", c_int, c_void_p)
@@ -176,6 +179,25 @@ class Dataset:
         h = c_void_p()
         check(lib.pgcn_dataset_load(root.encode(), name.encode(), ctypes.byref(h)),
               f"Cannot read input: {name}")
+        return Dataset(h.value)
+
+    @staticmethod
+    def load_cached(root, name):
+        """load() through the binary cache data/<name>.pgcnbin (written on a miss).
+        Returns (dataset, from_cache)."""
+        h, hit = c_void_p(), c_int()
+        check(lib.pgcn_dataset_load_cached(root.encode(), name.encode(), ctypes.byref(h),
+                                           ctypes.byref(hit)), f"Cannot read input: {name}")
+        return Dataset(h.value), bool(hit.value)
+
+    def save(self, path):
+        check(lib.pgcn_dataset_save(self._h, path.encode()), f"dataset_save {path}")
+
+    @staticmethod
+    def load_binary(path):
+        h = c_void_p()
+        check(lib.pgcn_dataset_load_binary(path.encode(), ctypes.byref(h)),
+              f"dataset_load_binary {path}")
         return Dataset(h.value)
 
     @staticmethod
@@ -364,7 +386,8 @@ EXPORTED = [
     "pgcn_gcn_create_dist", "pgcn_gcn_destroy", "pgcn_gcn_train_epoch", "pgcn_gcn_eval",
     "pgcn_gcn_epoch_async", "pgcn_gcn_sync", "pgcn_gcn_results", "pgcn_gcn_run",
     "pgcn_gcn_get_var", "pgcn_gcn_num_vars", "pgcn_gcn_profile", "pgcn_gcn_profile_read",
-    "pgcn_gcn_node_range", "pgcn_dataset_load", "pgcn_dataset_synthetic", "pgcn_dataset_view",
+    "pgcn_gcn_node_range", "pgcn_dataset_load", "pgcn_dataset_load_cached", "pgcn_dataset_save",
+    "pgcn_dataset_load_binary", "pgcn_dataset_synthetic", "pgcn_dataset_view",
     "pgcn_dataset_free", "pgcn_partition_bounds", "pgcn_partition_subgraph", "pgcn_debug_set",
     "pgcn_debug_read", "pgcn_debug_lds_check", "pgcn_debug_lds_counts",
 ]

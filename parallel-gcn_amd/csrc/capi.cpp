@@ -413,6 +413,36 @@ int pgcn_dataset_load(const char *root, const char *name, pgcn_dataset **out) {
   });
 }
 
+int pgcn_dataset_load_cached(const char *root, const char *name, pgcn_dataset **out,
+                             int *from_cache) {
+  return guarded([&] {
+    auto h = std::make_unique<pgcn_dataset>();
+    bool hit = false;
+    if (!load_dataset_cached(&h->d, root ? root : ".", name, &hit))
+      throw Error(PGCN_E_IO, std::string("Cannot read input: ") + name);
+    if (from_cache) *from_cache = hit ? 1 : 0;
+    *out = h.release();
+  });
+}
+
+int pgcn_dataset_save(const pgcn_dataset *ds, const char *path) {
+  return guarded([&] {
+    PGCN_CHECK(ds && path, PGCN_E_INVALID, "dataset_save: null argument");
+    if (!save_binary(ds->d, path, nullptr))
+      throw Error(PGCN_E_IO, std::string("cannot write ") + path);
+  });
+}
+
+int pgcn_dataset_load_binary(const char *path, pgcn_dataset **out) {
+  return guarded([&] {
+    PGCN_CHECK(path && out, PGCN_E_INVALID, "dataset_load_binary: null argument");
+    auto h = std::make_unique<pgcn_dataset>();
+    if (!load_binary(&h->d, path, nullptr))
+      throw Error(PGCN_E_IO, std::string("not a valid dataset cache: ") + path);
+    *out = h.release();
+  });
+}
+
 int pgcn_dataset_synthetic(int n, int f, int c, long long undirected_edges, uint64_t seed,
                            pgcn_dataset **out) {
   return guarded([&] {

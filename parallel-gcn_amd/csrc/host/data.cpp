@@ -13,6 +13,8 @@
 #include <fstream>
 #include <sstream>
 
+#include <sys/stat.h>
+
 #include "graph.hpp"  // parallel_for
 
 namespace pgcn {
@@ -283,6 +285,134 @@ void make_synthetic(GCNData *d, int n, int f, int c, long long undirected_edges,
   d->num_nodes = n;
   d->input_dim = f;
   d->output_dim = c;
+}
+
+// ------------------------------------------------------------------------------------------
+// binary dataset cache
+// ------------------------------------------------------------------------------------------
+namespace {
+constexpr char kMagic[8] = {'P', 'G', 'C', 'N', 'D', 'S', '0', '1'};
+
+struct BinHeader {
+  char magic[8];
+  long long num_nodes, input_dim, output_dim, graph_nnz, feat_nnz;
+  long long stamp[6];  // (size, mtime_ns) of .graph, .split, .svmlight
+  unsigned long long checksum;
+};
+
+uint64_t fnv1a(uint64_t h, const void *p, size_t n) {
+  const unsigned char *b = static_cast<const unsigned char *>(p);
+  for (size_t i = 0; i < n; i++) h = (h ^ b[i]) * 1099511628211ull;
+  return h;
+}
+
+template <class T>
+uint64_t hash_vec(uint64_t h, const std::vector<T> &v) {
+  return fnv1a(h, v.data(), v.size() * sizeof(T));
+}
+
+uint64_t payload_hash(const GCNData &d) {
+  uint64_t h = 14695981039346656037ull;
+  h = hash_vec(h, d.graph.indptr);
+  h = hash_vec(h, d.graph.indices);
+  h = hash_vec(h, d.feature_index.indptr);
+  h = hash_vec(h, d.feature_index.indices);
+  h = hash_vec(h, d.feature_value);
+  h = hash_vec(h, d.label);
+  h = hash_vec(h, d.split);
+  return h;
+}
+
+template <class T>
+bool write_vec(std::FILE *f, const std::vector<T> &v) {
+  return v.empty() || std::fwrite(v.data(), sizeof(T), v.size(), f) == v.size();
+}
+
+template <class T>
+bool read_vec(std::FILE *f, std::vector<T> &v, long long n) {
+  if (n < 0) return false;
+  v.resize((size_t)n);
+  return n == 0 || std::fread(v.data(), sizeof(T), (size_t)n, f) == (size_t)n;
+}
+}  // namespace
+
+bool stamp_file(const std::string &path, FileStamp *st) {
+  struct stat sb;
+  if (::stat(path.c_str(), &sb) != 0) return false;
+  st->size = (long long)sb.st_size;
+  st->mtime_ns = (long long)sb.st_mtim.tv_sec * 1000000000LL + (long long)sb.st_mtim.tv_nsec;
+  return true;
+}
+
+bool save_binary(const GCNData &d, const std::string &path, const FileStamp stamps[3]) {
+  BinHeader h{};
+  std::memcpy(h.magic, kMagic, 8);
+  h.num_nodes = d.num_nodes;
+  h.input_dim = d.input_dim;
+  h.output_dim = d.output_dim;
+  h.graph_nnz = (long long)d.graph.indices.size();
+  h.feat_nnz = (long long)d.feature_index.indices.size();
+  for (int i = 0; i < 3; i++) {
+    h.stamp[2 * i] = stamps ? stamps[i].size : -1;
+    h.stamp[2 * i + 1] = stamps ? stamps[i].mtime_ns : -1;
+  }
+  h.checksum = payload_hash(d);
+  const std::string tmp = path + ".tmp";
+  std::FILE *f = std::fopen(tmp.c_str(), "wb");
+  if (!f) return false;
+  bool ok = std::fwrite(&h, sizeof(h), 1, f) == 1 && write_vec(f, d.graph.indptr) &&
+            write_vec(f, d.graph.indices) && write_vec(f, d.feature_index.indptr) &&
+            write_vec(f, d.feature_index.indices) && write_vec(f, d.feature_value) &&
+            write_vec(f, d.label) && write_vec(f, d.split);
+  ok = (std::fclose(f) == 0) && ok;
+  if (ok) ok = std::rename(tmp.c_str(), path.c_str()) == 0;  // readers never see a partial file
+  if (!ok) std::remove(tmp.c_str());
+  return ok;
+}
+
+bool load_binary(GCNData *d, const std::string &path, const FileStamp *stamps) {
+  std::FILE *f = std::fopen(path.c_str(), "rb");
+  if (!f) return false;
+  BinHeader h{};
+  GCNData t;
+  bool ok = std::fread(&h, sizeof(h), 1, f) == 1 && std::memcmp(h.magic, kMagic, 8) == 0 &&
+            h.num_nodes >= 0 && h.num_nodes < INT_MAX;
+  if (ok && stamps)
+    for (int i = 0; i < 3; i++)
+      ok = ok && h.stamp[2 * i] == stamps[i].size && h.stamp[2 * i + 1] == stamps[i].mtime_ns;
+  const long long n = h.num_nodes;
+  ok = ok && read_vec(f, t.graph.indptr, n + 1) && read_vec(f, t.graph.indices, h.graph_nnz) &&
+       read_vec(f, t.feature_index.indptr, n + 1) &&
+       read_vec(f, t.feature_index.indices, h.feat_nnz) &&
+       read_vec(f, t.feature_value, h.feat_nnz) && read_vec(f, t.label, n) &&
+       read_vec(f, t.split, n);
+  ok = ok && std::fgetc(f) == EOF;  // nothing trailing
+  std::fclose(f);
+  ok = ok && t.graph.indptr.back() == h.graph_nnz && t.feature_index.indptr.back() == h.feat_nnz;
+  if (!ok || payload_hash(t) != h.checksum) return false;
+  t.num_nodes = (int)n;
+  t.input_dim = (int)h.input_dim;
+  t.output_dim = (int)h.output_dim;
+  *d = std::move(t);
+  return true;
+}
+
+bool load_dataset_cached(GCNData *d, const std::string &root, const std::string &name,
+                         bool *from_cache) {
+  const std::string base = root + "/data/" + name;
+  FileStamp st[3];
+  const bool stamped = stamp_file(base + ".graph", &st[0]) && stamp_file(base + ".split", &st[1]) &&
+                       stamp_file(base + ".svmlight", &st[2]);
+  const std::string cache = base + ".pgcnbin";
+  if (from_cache) *from_cache = false;
+  if (stamped && load_binary(d, cache, st)) {
+    if (from_cache) *from_cache = true;
+    return true;
+  }
+  Parser parser(d, name, root);
+  if (!parser.parse()) return false;
+  if (stamped) (void)save_binary(*d, cache, st);  // best effort (read-only data dirs)
+  return true;
 }
 
 }  // namespace pgcn

@@ -45,6 +45,23 @@ class Parser {
 void make_synthetic(GCNData *d, int n, int f, int c, long long undirected_edges,
                     uint64_t seed);
 
+// Binary dataset cache: the parsed arrays of GCNData as one file
+// ("PGCNDS01" header, sizes, the source files' size + mtime stamps, raw little-endian arrays,
+// FNV-1a 64 checksum of the payload).  load_binary fails (returns false) on a missing file,
+// another version, stamps that differ from `stamps` (when given), a short file or a checksum
+// mismatch; the caller then parses the text.
+struct FileStamp {
+  long long size = -1, mtime_ns = -1;
+};
+bool stamp_file(const std::string &path, FileStamp *st);
+bool save_binary(const GCNData &d, const std::string &path, const FileStamp stamps[3]);
+bool load_binary(GCNData *d, const std::string &path, const FileStamp *stamps);
+// Parser + cache: <root>/data/<name>.pgcnbin is read when its stamps match the three text
+// files, else the text is parsed and the cache (re)written (best effort).  *from_cache tells
+// which happened.
+bool load_dataset_cached(GCNData *d, const std::string &root, const std::string &name,
+                         bool *from_cache);
+
 // True when every row lists all features 0..F-1 in order (a dense matrix in CSR form).
 bool features_dense(const GCNData &d);
 

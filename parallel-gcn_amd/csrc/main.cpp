@@ -1,4 +1,4 @@
-// parallel-gcn_amd/csrc/main.cpp -- `gcn-par <dataset> [file=<params>] [root=<dir>]`
+// parallel-gcn_amd/csrc/main.cpp -- `gcn-par <dataset> [file=<params>] [root=<dir>] [cache=1]`
 // The reference's entry point (src/main.cpp:9-61): parse the dataset with the kept loader,
 // build the GCN, run the epochs printing the reference's epoch lines.  Parameters come from
 // a key=value file with the reference's keys (parameters/parameters_<ds>.txt layout:
@@ -62,9 +62,11 @@ int main(int argc, char **argv) {
   }
   const char *name = argv[1];
   std::string root = ".", file;
+  bool cache = false;  // cache=1: read/write the binary dataset cache data/<name>.pgcnbin
   for (int i = 2; i < argc; i++) {
     if (!std::strncmp(argv[i], "file=", 5)) file = argv[i] + 5;
     if (!std::strncmp(argv[i], "root=", 5)) root = argv[i] + 5;
+    if (!std::strcmp(argv[i], "cache=1")) cache = true;
   }
   pgcn_params p;
   pgcn_params_default(&p);
@@ -73,7 +75,9 @@ int main(int argc, char **argv) {
     return EXIT_FAILURE;
   }
   pgcn_dataset *ds = nullptr;
-  if (pgcn_dataset_load(root.c_str(), name, &ds) != PGCN_OK) {
+  const int lst = cache ? pgcn_dataset_load_cached(root.c_str(), name, &ds, nullptr)
+                        : pgcn_dataset_load(root.c_str(), name, &ds);
+  if (lst != PGCN_OK) {
     fprintf(stderr, "Cannot read input: %s\n", name);
     return EXIT_FAILURE;
   }

@@ -65,6 +65,61 @@ def test_loader_missing_dataset_raises(pgcn, tmp_path):
         pgcn.Dataset.load(str(tmp_path), "nonexistent")
 
 
+DS_ARRAYS = ("graph_indptr", "graph_indices", "feat_indptr", "feat_indices", "feat_values",
+             "label", "split")
+
+
+def _same_dataset(a, b):
+    assert (a.num_nodes, a.input_dim, a.output_dim) == (b.num_nodes, b.input_dim, b.output_dim)
+    for k in DS_ARRAYS:
+        np.testing.assert_array_equal(getattr(a, k), getattr(b, k), err_msg=k)
+
+
+@pytest.mark.parametrize("name", ["cora", "citeseer"])
+def test_binary_cache_roundtrip(pgcn, name, tmp_path):
+    """the binary cache gives the parser's arrays bit for bit; a miss parses
+    and writes it, a hit reads it, a touched text file or a corrupted cache falls back to
+    the parser (same arrays every time)."""
+    import shutil
+    root = str(tmp_path)
+    dname = helpers.materialize_dataset(name, root)
+    text = pgcn.Dataset.load(root, dname)
+    d1, hit1 = pgcn.Dataset.load_cached(root, dname)
+    cache = os.path.join(root, "data", dname + ".pgcnbin")
+    assert not hit1 and os.path.exists(cache)
+    d2, hit2 = pgcn.Dataset.load_cached(root, dname)
+    assert hit2
+    _same_dataset(text, d1)
+    _same_dataset(text, d2)
+    # a text file changed after the cache was written: stamps differ -> parse again
+    gpath = os.path.join(root, "data", dname + ".graph")
+    st = os.stat(gpath)
+    os.utime(gpath, ns=(st.st_atime_ns, st.st_mtime_ns + 1_000_000_000))
+    d3, hit3 = pgcn.Dataset.load_cached(root, dname)
+    assert not hit3
+    _same_dataset(text, d3)
+    # corrupted payload (checksum) and truncated file: rejected, the parser runs
+    blob = bytearray(open(cache, "rb").read())
+    blob[-5] ^= 0xFF
+    open(cache, "wb").write(bytes(blob))
+    with pytest.raises(pgcn.PgcnError):
+        pgcn.Dataset.load_binary(cache)
+    d4, hit4 = pgcn.Dataset.load_cached(root, dname)
+    assert not hit4
+    _same_dataset(text, d4)
+    open(cache, "wb").write(bytes(blob[: len(blob) // 2]))
+    with pytest.raises(pgcn.PgcnError):
+        pgcn.Dataset.load_binary(cache)
+    # save/load_binary of any dataset (a synthetic one too)
+    syn = pgcn.Dataset.synthetic(500, 12, 4, 3000, seed=3)
+    path = os.path.join(root, "syn.pgcnbin")
+    syn.save(path)
+    _same_dataset(syn, pgcn.Dataset.load_binary(path))
+    shutil.rmtree(os.path.join(root, "data"))
+    with pytest.raises(pgcn.PgcnError):
+        pgcn.Dataset.load_cached(root, dname)
+
+
 @pytest.mark.parametrize("k", [0, 1, 2, 63, 64, 1000, 123457])
 def test_rng_jump_matches_sequential_draws(pgcn, k):
     """GF(2) jump-ahead (csrc/rng.cpp) == k sequential xorshift128+ draws of the oracle
