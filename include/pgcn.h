@@ -40,6 +40,8 @@ int pgcn_version(void);
 /* --- xorshift128+ (hpdga-spring23/src/rand.cpp:17-28), host helpers ------------------- */
 /* Default seed state of hpdga init_rand_state() (rand.cpp:6-14). */
 void pgcn_rng_seed(uint64_t state[2]);
+/* the same two draws after srand(seed), on a private glibc random_r state */
+void pgcn_rng_seed_glibc(unsigned int seed, uint64_t state[2]);
 /* state <- state advanced by `k` draws (GF(2) jump-ahead; exact). */
 void pgcn_rng_jump(uint64_t state[2], uint64_t k);
 
@@ -160,6 +162,10 @@ typedef struct {
    * GraphSum gathers hidden-width rows.  Exact algebra (Â symmetric); only the fp32
    * rounding order differs from the reference.  0: the reference's module order. */
   int reassociate_last;
+  /* PART2 `seed` (src/parser.cpp:234): 0 = hpdga's unseeded glibc rand() (init_rand_state,
+   * hpdga rand.cpp:6-14); else the xorshift state is the first two rand() values after
+   * srand(seed).  Glorot init and every dropout mask follow from it. */
+  unsigned int seed;
 } pgcn_params;
 
 /* hpdga defaults: 2 layers, hidden 16, dropout .5/.5, 100 epochs, Adam lr .01, wd 5e-4,
@@ -224,6 +230,9 @@ int pgcn_dataset_load_cached(const char *root, const char *name, pgcn_dataset **
 /* Write / read the parsed arrays as one binary file (any dataset, synthetic ones included).
  * PGCN_E_IO on a write failure or an invalid / truncated / corrupted file. */
 int pgcn_dataset_save(const pgcn_dataset *ds, const char *path);
+/* PART2 NO_FEATURE (src/parser.cpp:100-104): every feature value of `ds` becomes 1.0 (the
+ * feature ids stay, so input_dim is unchanged). */
+int pgcn_dataset_binarize(pgcn_dataset *ds);
 int pgcn_dataset_load_binary(const char *path, pgcn_dataset **out);
 /* Seeded reddit-shaped synthetic: n nodes, f dense features, c classes,
  * Chung-Lu power-law undirected graph with `undirected_edges` edges (2x directed slots). */

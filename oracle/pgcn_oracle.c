@@ -9,6 +9,7 @@
  * Build: gcc -O2 -ffp-contract=off (oracle/Makefile).  x86-64 gcc emits no FMA without
  * -mfma, like the reference's own -O3 -std=c++11 build (hpdga-spring23/Makefile:1-3).
  */
+#define _DEFAULT_SOURCE /* initstate_r / random_r (glibc) */
 #include "pgcn_oracle.h"
 
 #include <math.h>
@@ -24,6 +25,21 @@
 void or_rng_seed(uint64_t s[2]) {
   s[0] = 1804289383u;
   s[1] = 846930886u;
+}
+
+/* The same two draws after srand(seed) (the PART2 `seed` parameter, src/parser.cpp:234):
+ * glibc's rand() is random() on a TYPE_3 (128-byte) state, reproduced here on a private
+ * state so the process's own rand() is untouched.  seed 0 and 1 give the unseeded values. */
+void or_rng_seed_glibc(unsigned seed, uint64_t s[2]) {
+  char buf[128];
+  struct random_data rd;
+  int32_t x = 0, y = 0;
+  memset(&rd, 0, sizeof(rd));
+  initstate_r(seed, buf, sizeof(buf), &rd);
+  random_r(&rd, &x);
+  random_r(&rd, &y);
+  s[0] = (uint32_t)x;
+  s[1] = (uint32_t)y;
 }
 
 /* hpdga-spring23/src/rand.cpp:17-28 */
@@ -322,7 +338,10 @@ or_gcn *or_gcn_create(const or_params *p, const int *g_indptr, const int *g_indi
   DUP(g->split, split, N, int);
 #undef DUP
   g->truth = (int *)calloc((size_t)N, sizeof(int));
-  or_rng_seed(g->rng); /* init_rand_state(), gcn.cpp:65 */
+  if (p->seed) /* init_rand_state(), gcn.cpp:65 */
+    or_rng_seed_glibc(p->seed, g->rng);
+  else
+    or_rng_seed(g->rng);
 
   int dims[OR_MAX_LAYERS + 1];
   dims[0] = p->input_dim;

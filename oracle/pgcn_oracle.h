@@ -21,6 +21,7 @@ extern "C" {
 
 /* ---- RNG: xorshift128+ (hpdga-spring23/src/rand.cpp:6-28) ---- */
 void or_rng_seed(uint64_t s[2]);
+void or_rng_seed_glibc(unsigned seed, uint64_t s[2]);
 uint32_t or_rng_next(uint64_t s[2]);
 
 /* ---- per-op restatements (each cites the reference lines it follows in the .c) ---- */
@@ -53,6 +54,7 @@ typedef struct {
   int hidden_dims[OR_MAX_LAYERS]; /* n_layers - 1 entries */
   float dropouts[OR_MAX_LAYERS];  /* n_layers entries */
   float lr, weight_decay, beta1, beta2, eps;
+  unsigned seed; /* 0: hpdga's unseeded rand(); else srand(seed) before init_rand_state */
 } or_params;
 
 typedef struct or_gcn or_gcn;

@@ -40,7 +40,8 @@ class PgcnParams(ctypes.Structure):
                 ("n_layers", c_int), ("hidden_dims", c_int * MAX_LAYERS),
                 ("dropouts", c_float * MAX_LAYERS), ("epochs", c_int), ("early_stopping", c_int),
                 ("learning_rate", c_float), ("weight_decay", c_float), ("beta1", c_float),
-                ("beta2", c_float), ("eps", c_float), ("reassociate_last", c_int)]
+                ("beta2", c_float), ("eps", c_float), ("reassociate_last", c_int),
+                ("seed", ctypes.c_uint)]
 
 
 class PgcnData(ctypes.Structure):
@@ -59,6 +60,7 @@ def _sig(name, res, *args):
 _sig("pgcn_status_string", ctypes.c_char_p, c_int)
 _sig("pgcn_version", c_int)
 _sig("pgcn_rng_seed", None, P(c_u64))
+_sig("pgcn_rng_seed_glibc", None, ctypes.c_uint, P(c_u64))
 _sig("pgcn_rng_jump", None, P(c_u64), c_u64)
 _sig("pgcn_rng_jump_table", c_int, c_u64, c_void_p)
 _sig("pgcn_graph_create", c_int, c_int, c_void_p, c_void_p, P(c_void_p))
@@ -113,6 +115,7 @@ _sig("pgcn_gcn_node_range", c_int, c_void_p, P(c_int), P(c_int))
 _sig("pgcn_dataset_load", c_int, ctypes.c_char_p, ctypes.c_char_p, P(c_void_p))
 _sig("pgcn_dataset_load_cached", c_int, ctypes.c_char_p, ctypes.c_char_p, P(c_void_p), P(c_int))
 _sig("pgcn_dataset_save", c_int, c_void_p, ctypes.c_char_p)
+_sig("pgcn_dataset_binarize", c_int, c_void_p)
 _sig("pgcn_dataset_load_binary", c_int, ctypes.c_char_p, P(c_void_p))
 _sig("pgcn_dataset_synthetic", c_int, c_int, c_int, c_int, c_ll, c_u64, P(c_void_p))
 _sig("pgcn_dataset_view", c_int, c_void_p, P(PgcnData), P(c_int), P(c_int))
@@ -190,6 +193,11 @@ class Dataset:
                                            ctypes.byref(hit)), f"Cannot read input: {name}")
         return Dataset(h.value), bool(hit.value)
 
+    def binarize(self):
+        """PART2 NO_FEATURE (src/parser.cpp:100-104): every feature value becomes 1.0 (the
+        arrays of this object are views, so they change in place)."""
+        check(lib.pgcn_dataset_binarize(self._h), "dataset_binarize")
+
     def save(self, path):
         check(lib.pgcn_dataset_save(self._h, path.encode()), f"dataset_save {path}")
 
@@ -215,10 +223,11 @@ class Dataset:
 
 def make_params(ds, hidden_dims=(16,), dropouts=(0.5, 0.5), epochs=100, early_stopping=0,
                 learning_rate=0.01, weight_decay=5e-4, beta1=0.9, beta2=0.999, eps=1e-8,
-                reassociate_last=True):
+                reassociate_last=True, seed=0):
     p = PgcnParams()
     lib.pgcn_params_default(ctypes.byref(p))
     p.reassociate_last = 1 if reassociate_last else 0
+    p.seed = seed
     p.num_nodes, p.input_dim, p.output_dim = ds.num_nodes, ds.input_dim, ds.output_dim
     p.n_layers = len(hidden_dims) + 1
     assert len(dropouts) == p.n_layers
@@ -319,9 +328,12 @@ def comm_unique_id():
 
 
 # --------------------------------------------------------------------------- host helpers
-def rng_seed():
+def rng_seed(seed=0):
     s = (c_u64 * 2)()
-    lib.pgcn_rng_seed(s)
+    if seed:
+        lib.pgcn_rng_seed_glibc(seed, s)
+    else:
+        lib.pgcn_rng_seed(s)
     return np.array([s[0], s[1]], np.uint64)
 
 
@@ -375,7 +387,8 @@ def csr_transpose(indptr, indices, n_cols):
 
 
 EXPORTED = [
-    "pgcn_status_string", "pgcn_version", "pgcn_rng_seed", "pgcn_rng_jump", "pgcn_graph_create",
+    "pgcn_status_string", "pgcn_version", "pgcn_rng_seed", "pgcn_rng_seed_glibc", "pgcn_rng_jump",
+    "pgcn_graph_create",
     "pgcn_graph_destroy", "pgcn_graph_nnz", "pgcn_graphsum", "pgcn_gemm", "pgcn_gemm_tn_workspace",
     "pgcn_gemm_tn", "pgcn_mask_nibbles", "pgcn_gemm_xstream", "pgcn_gemm_xstream_dual",
     "pgcn_gemm_tn_xstream",
@@ -387,7 +400,8 @@ EXPORTED = [
     "pgcn_gcn_epoch_async", "pgcn_gcn_sync", "pgcn_gcn_results", "pgcn_gcn_run",
     "pgcn_gcn_get_var", "pgcn_gcn_num_vars", "pgcn_gcn_profile", "pgcn_gcn_profile_read",
     "pgcn_gcn_node_range", "pgcn_dataset_load", "pgcn_dataset_load_cached", "pgcn_dataset_save",
-    "pgcn_dataset_load_binary", "pgcn_dataset_synthetic", "pgcn_dataset_view",
+    "pgcn_dataset_load_binary", "pgcn_dataset_binarize", "pgcn_dataset_synthetic",
+    "pgcn_dataset_view",
     "pgcn_dataset_free", "pgcn_partition_bounds", "pgcn_partition_subgraph", "pgcn_debug_set",
     "pgcn_debug_read", "pgcn_debug_lds_check", "pgcn_debug_lds_counts",
 ]

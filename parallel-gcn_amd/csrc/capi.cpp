@@ -64,6 +64,7 @@ GCNParams to_params(const pgcn_params *p, const pgcn_data *d) {
   q.epochs = p->epochs;
   q.early_stopping = p->early_stopping;
   q.reassociate_last = p->reassociate_last != 0;
+  q.seed = p->seed;
   return q;
 }
 AdamParams to_adam(const pgcn_params *p) {
@@ -312,6 +313,7 @@ void pgcn_params_default(pgcn_params *p) {
   p->beta2 = 0.999f;
   p->eps = 1e-8f;
   p->reassociate_last = 1;
+  p->seed = 0;
 }
 
 int pgcn_gcn_create(const pgcn_params *p, const pgcn_data *d, int device, pgcn_gcn **out) {
@@ -431,6 +433,12 @@ int pgcn_dataset_save(const pgcn_dataset *ds, const char *path) {
     if (!save_binary(ds->d, path, nullptr))
       throw Error(PGCN_E_IO, std::string("cannot write ") + path);
   });
+}
+
+int pgcn_dataset_binarize(pgcn_dataset *ds) {
+  if (!ds) return PGCN_E_INVALID;
+  std::fill(ds->d.feature_value.begin(), ds->d.feature_value.end(), 1.0f);
+  return PGCN_OK;
 }
 
 int pgcn_dataset_load_binary(const char *path, pgcn_dataset **out) {

@@ -96,8 +96,8 @@ GCN::GCN(const GCNParams &params_, const AdamParams &adam, const GCNData &data, 
   PGCN_CHECK((int)params.dropouts.size() == L, PGCN_E_INVALID,
              "Number of dropouts must match number of layers");
   for (int h : params.hidden_dims)
-    PGCN_CHECK(h > 0 && h % 4 == 0 && h <= 128, PGCN_E_INVALID,
-               "hidden dims must be multiples of 4 in [4,128]");
+    PGCN_CHECK(h > 0 && h % 4 == 0 && h <= 4096, PGCN_E_INVALID,
+               "hidden dims must be multiples of 4 in [4,4096]");
   PGCN_CHECK(params.output_dim >= 1 && params.output_dim <= 128, PGCN_E_INVALID,
              "output_dim must be in [1,128]");
   PGCN_CHECK(data.num_nodes == params.num_nodes, PGCN_E_INVALID, "num_nodes mismatch");
@@ -203,7 +203,8 @@ void GCN::init_dropout_rng(const GCNData &data, long long glorot_draws) {
   ctx.jump_table = jump_table.get();
 
   uint64_t seed[2];
-  pgcn_rng_seed(seed);
+  if (params.seed) pgcn_rng_seed_glibc(params.seed, seed);
+  else pgcn_rng_seed(seed);
   unsigned long long offset = (unsigned long long)glorot_draws;
   for (int l = 0; l < L; l++) {
     auto r = std::make_shared<DropoutRng>();
@@ -328,7 +329,8 @@ void GCN::build(const GCNData &data) {
   grad_arena.allocate((size_t)wtotal);
   grad_arena.zero();
   uint64_t rs[2];
-  pgcn_rng_seed(rs);
+  if (params.seed) pgcn_rng_seed_glibc(params.seed, rs);
+  else pgcn_rng_seed(rs);
   long long woff = 0;
   std::vector<std::vector<float>> winit;
   for (int l = 0; l < L; l++) {

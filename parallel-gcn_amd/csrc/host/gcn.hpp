@@ -32,6 +32,7 @@ struct GCNParams {
   // compute the last layer as (Â H) W instead of Â (H W) when that narrows the GraphSum
   // (hidden < classes); exact algebra, fp32 rounding order only (see insert_last_layer)
   bool reassociate_last = false;
+  unsigned seed = 0;  // PART2 `seed`: 0 = hpdga's unseeded rand(), else srand(seed)
 };
 
 struct AdamParams {

@@ -876,6 +876,16 @@ void DevGraph::graphsum(const float *in, int ld_in, float *out, int ld_out, int 
     }
     return;
   }
+  if (dim > 16 && !graphsum_vec_supported((dim + 3) / 4)) {
+    // widths without a kernel instantiation (PART2 hidden 72, 600): 16-column passes, the
+    // last one overlapping the one before it (recomputed columns get the same bits)
+    const int ldm = std::min(ld_in, ld_out);
+    for (int c0 = 0; c0 < dim; c0 += 16) {
+      const int c = std::min(c0, ldm - 16);
+      graphsum(in + c, ld_in, out + c, ld_out, 16, s, compact_in);
+    }
+    return;
+  }
   if (col_map) {  // plain path of a column subset: compact the input rows first
     const size_t need = (size_t)n_cols_ * ld_in;
     if (col_in_.size() < need) col_in_.allocate(need);

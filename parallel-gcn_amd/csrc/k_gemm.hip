@@ -42,7 +42,8 @@ __global__ __launch_bounds__(256) void k_gemm_nn(int M, int N, int K,
                                                  int trans_b, float *__restrict__ C, int ldc,
                                                  const uint64_t *__restrict__ a_mask,
                                                  long long mask_base, long long mask_ld,
-                                                 float a_scale) {
+                                                 float a_scale, int nst) {
+  // nst: columns of C this launch writes (ldc, or a 128-column slab's share of it)
   constexpr int KC = 64;               // K rows of B per LDS chunk
   constexpr int S = 16 * NT + 4;       // LDS row stride (== 4 mod 8: conflict-free reads)
   __shared__ float bs[KC * S];
@@ -100,7 +101,7 @@ __global__ __launch_bounds__(256) void k_gemm_nn(int M, int N, int K,
 #pragma unroll
   for (int t = 0; t < NT; t++) {
     const int col = 16 * t + i;
-    if (col >= ldc) continue;
+    if (col >= nst) continue;
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       const long long rr = crow0 + r;
@@ -700,13 +701,13 @@ __global__ __launch_bounds__(256) void k_slab_reduce1(const float *__restrict__ 
 // pass 2: C[k][j] = sum over groups in order
 __global__ __launch_bounds__(256) void k_gemm_tn_reduce(const float *__restrict__ part2,
                                                         int n_groups, int K, int N, int ldp,
-                                                        float *__restrict__ C, int ldc) {
+                                                        float *__restrict__ C, int ldc, int nst) {
   const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= (long long)K * ldp) return;
   const int k = (int)(e / ldp), j = (int)(e - (long long)k * ldp);
   float s = 0.0f;
   for (int b = 0; b < n_groups; b++) s += part2[(long long)b * K * ldp + e];
-  if (j < ldc) C[(long long)k * ldc + j] = j < N ? s : 0.0f;
+  if (j < nst) C[(long long)k * ldc + j] = j < N ? s : 0.0f;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -761,13 +762,34 @@ void launch_xstream_nn(int M, int N, int K, const float *A, int lda, const float
 #undef XNN_CASE
 }
 
+static void gemm_nn_slab(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
+                         int trans_b, float *C, int ldc, const uint64_t *a_mask,
+                         long long mask_base, long long mask_ld, float a_scale, hipStream_t s,
+                         int nst);
+
 void launch_gemm_nn(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
                     int trans_b, float *C, int ldc, const uint64_t *a_mask, long long mask_base,
                     long long mask_ld, float a_scale, hipStream_t s) {
   PGCN_CHECK(lda % 4 == 0 && lda >= K, PGCN_E_INVALID, "gemm: lda must be a multiple of 4 >= K");
-  PGCN_CHECK(N <= 128 && N >= 1, PGCN_E_INVALID, "gemm: N must be in [1,128]");
+  PGCN_CHECK(N >= 1, PGCN_E_INVALID, "gemm: N must be >= 1");
   if (M <= 0) return;
-  if (!a_mask && xstream_ok(N, K)) {
+  if (N > 128) {  // wide outputs (PART2 hidden 600): 128-column slabs of B and C, each slab
+    // writing its own columns only (the last one also C's padding columns)
+    for (int j0 = 0; j0 < N; j0 += 128)
+      gemm_nn_slab(M, std::min(128, N - j0), K, A, lda,
+                   trans_b ? B + (long long)j0 * ldb : B + j0, ldb, trans_b, C + j0, ldc, a_mask,
+                   mask_base, mask_ld, a_scale, s, j0 + 128 >= N ? ldc - j0 : 128);
+    return;
+  }
+  gemm_nn_slab(M, N, K, A, lda, B, ldb, trans_b, C, ldc, a_mask, mask_base, mask_ld, a_scale, s,
+               ldc);
+}
+
+static void gemm_nn_slab(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
+                         int trans_b, float *C, int ldc, const uint64_t *a_mask,
+                         long long mask_base, long long mask_ld, float a_scale, hipStream_t s,
+                         int nst) {
+  if (!a_mask && xstream_ok(N, K) && nst == ldc) {
     launch_xstream_nn(M, N, K, A, lda, B, ldb, trans_b, C, ldc, nullptr, 1.0f, s, nullptr);
     return;
   }
@@ -776,7 +798,7 @@ void launch_gemm_nn(int M, int N, int K, const float *A, int lda, const float *B
 #define NN_CASE(T)                                                                            \
   case T:                                                                                     \
     hipLaunchKernelGGL(k_gemm_nn<T>, grid, block, 0, s, M, N, K, A, lda, B, ldb, trans_b, C, \
-                       ldc, a_mask, mask_base, mask_ld, a_scale);                             \
+                       ldc, a_mask, mask_base, mask_ld, a_scale, nst);                        \
     break;
   switch (nt) {
     NN_CASE(1) NN_CASE(2) NN_CASE(3) NN_CASE(4) NN_CASE(5) NN_CASE(6) NN_CASE(7) NN_CASE(8)
@@ -825,6 +847,7 @@ static size_t plan_bytes(const TnPlan &p, int K) {
 }
 
 size_t gemm_tn_workspace(int M, int N, int K) {
+  N = std::min(N, 128);  // wider outputs run in 128-column slabs
   size_t ws = plan_bytes(tn_plan(M, N, K), K);  // either kernel family may run
   if (N <= 16) ws = std::max(ws, plan_bytes(xs_tn_plan(K), K));
   return ws;
@@ -832,14 +855,15 @@ size_t gemm_tn_workspace(int M, int N, int K) {
 
 // ordered two-pass reduction of p.n_slabs partials [K][ldp] into C[K][ldc]
 static void tn_reduce(const TnPlan &p, int M, int N, int K, float *partial, float *C, int ldc,
-                      hipStream_t s) {
+                      hipStream_t s, int nst = -1) {
+  if (nst < 0) nst = ldc;
   float *part2 = partial + (size_t)p.n_slabs * K * p.ldp;
   const long long elems = (long long)K * p.ldp;
   if (M > 0)
     hipLaunchKernelGGL(k_slab_reduce1, dim3((unsigned)ceil_div(elems, 256), (unsigned)p.n_groups),
                        dim3(256), 0, s, partial, p.n_slabs, elems, p.spg, part2);
   hipLaunchKernelGGL(k_gemm_tn_reduce, dim3((unsigned)ceil_div(elems, 256)), dim3(256), 0, s,
-                     part2, M > 0 ? p.n_groups : 0, K, N, p.ldp, C, ldc);
+                     part2, M > 0 ? p.n_groups : 0, K, N, p.ldp, C, ldc, nst);
 }
 
 void launch_xstream_tn(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
@@ -876,12 +900,32 @@ void launch_xstream_tn(int M, int N, int K, const float *A, int lda, const float
   tn_reduce(p, M, N, K, partial, C, ldc, s);
 }
 
+static void gemm_tn_slab(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
+                         float *C, int ldc, const uint64_t *a_mask, long long mask_base,
+                         long long mask_ld, float a_scale, void *workspace, hipStream_t s,
+                         int nst);
+
 void launch_gemm_tn(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
                     float *C, int ldc, const uint64_t *a_mask, long long mask_base,
                     long long mask_ld, float a_scale, void *workspace, hipStream_t s) {
-  PGCN_CHECK(N <= 128 && N >= 1, PGCN_E_INVALID, "gemm_tn: N must be in [1,128]");
+  PGCN_CHECK(N >= 1, PGCN_E_INVALID, "gemm_tn: N must be >= 1");
   PGCN_CHECK(lda % 4 == 0 && lda >= K, PGCN_E_INVALID, "gemm_tn: lda must be a multiple of 4 >= K");
-  if (!a_mask && xstream_ok(N, K)) {
+  if (N > 128) {  // 128-column slabs of G and C, one after another through the workspace,
+    // each writing its own columns only (the last one also C's padding columns)
+    for (int j0 = 0; j0 < N; j0 += 128)
+      gemm_tn_slab(M, std::min(128, N - j0), K, A, lda, G + j0, ldg, C + j0, ldc, a_mask,
+                   mask_base, mask_ld, a_scale, workspace, s, j0 + 128 >= N ? ldc - j0 : 128);
+    return;
+  }
+  gemm_tn_slab(M, N, K, A, lda, G, ldg, C, ldc, a_mask, mask_base, mask_ld, a_scale, workspace, s,
+               ldc);
+}
+
+static void gemm_tn_slab(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
+                         float *C, int ldc, const uint64_t *a_mask, long long mask_base,
+                         long long mask_ld, float a_scale, void *workspace, hipStream_t s,
+                         int nst) {
+  if (!a_mask && xstream_ok(N, K) && nst == ldc) {
     launch_xstream_tn(M, N, K, A, lda, G, ldg, C, ldc, nullptr, 1.0f, workspace, s);
     return;
   }
@@ -908,7 +952,7 @@ void launch_gemm_tn(int M, int N, int K, const float *A, int lda, const float *G
     PGCN_CHECK(done, PGCN_E_INVALID,
                "gemm_tn: no kernel for N=" + std::to_string(N) + " K=" + std::to_string(K));
   }
-  tn_reduce(p, M, N, K, partial, C, ldc, s);
+  tn_reduce(p, M, N, K, partial, C, ldc, s, nst);
 }
 
 }  // namespace pgcn

@@ -3,8 +3,9 @@
 // build the GCN, run the epochs printing the reference's epoch lines.  Parameters come from
 // a key=value file with the reference's keys (parameters/parameters_<ds>.txt layout:
 // n_layers, hidden_dims, dropouts, epochs, early_stopping, learning_rate, weight_decay,
-// beta1, beta2, eps; the CUDA launch knobs num_blocks_factor/num_threads/seed are accepted
-// and ignored) -- our own tiny parser, GetPot is not vendored.
+// beta1, beta2, eps, seed (srand seed of the xorshift state); the CUDA launch knobs
+// num_blocks_factor/num_threads are accepted and ignored) -- our own tiny parser, GetPot is
+// not vendored.  no_feature=1 is the PART2 NO_FEATURE build (feature values 1.0).
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -51,6 +52,7 @@ static bool load_params(const char *path, pgcn_params *p) {
     else if (k == "beta1") p->beta1 = std::strtof(v.c_str(), nullptr);
     else if (k == "beta2") p->beta2 = std::strtof(v.c_str(), nullptr);
     else if (k == "eps") p->eps = std::strtof(v.c_str(), nullptr);
+    else if (k == "seed") p->seed = (unsigned)std::strtoul(v.c_str(), nullptr, 10);
   }
   return true;
 }
@@ -63,10 +65,12 @@ int main(int argc, char **argv) {
   const char *name = argv[1];
   std::string root = ".", file;
   bool cache = false;  // cache=1: read/write the binary dataset cache data/<name>.pgcnbin
+  bool no_feature = false;  // no_feature=1: the PART2 NO_FEATURE build (feature values 1.0)
   for (int i = 2; i < argc; i++) {
     if (!std::strncmp(argv[i], "file=", 5)) file = argv[i] + 5;
     if (!std::strncmp(argv[i], "root=", 5)) root = argv[i] + 5;
     if (!std::strcmp(argv[i], "cache=1")) cache = true;
+    if (!std::strcmp(argv[i], "no_feature=1")) no_feature = true;
   }
   pgcn_params p;
   pgcn_params_default(&p);
@@ -81,6 +85,7 @@ int main(int argc, char **argv) {
     fprintf(stderr, "Cannot read input: %s\n", name);
     return EXIT_FAILURE;
   }
+  if (no_feature) pgcn_dataset_binarize(ds);
   pgcn_data view;
   pgcn_dataset_view(ds, &view, &p.input_dim, &p.output_dim);
   p.num_nodes = view.num_nodes;

@@ -7,6 +7,7 @@
 // reproduce the CPU masks; this engine reproduces them bit-for-bit.
 #include "rng.hpp"
 
+#include <cstdlib>
 #include <cstring>
 
 namespace pgcn {
@@ -93,6 +94,20 @@ void pgcn_rng_seed(uint64_t state[2]) {
   // hpdga-spring23/src/rand.cpp:6-14: x = rand(), y = rand() of an unseeded glibc rand().
   state[0] = 1804289383u;
   state[1] = 846930886u;
+}
+
+void pgcn_rng_seed_glibc(unsigned int seed, uint64_t state[2]) {
+  // srand(seed); x = rand(); y = rand(): glibc rand() is random() on a TYPE_3 (128-byte)
+  // state; a private one leaves the process's rand() alone.  seed 0 and 1 = unseeded.
+  char buf[128];
+  struct random_data rd;
+  std::memset(&rd, 0, sizeof(rd));
+  int32_t x = 0, y = 0;
+  initstate_r(seed, buf, sizeof(buf), &rd);
+  random_r(&rd, &x);
+  random_r(&rd, &y);
+  state[0] = (uint32_t)x;
+  state[1] = (uint32_t)y;
 }
 
 void pgcn_rng_jump(uint64_t state[2], uint64_t k) { pgcn::xs_jump(state, k); }

@@ -39,7 +39,8 @@ class OrParams(ctypes.Structure):
                 ("output_dim", ctypes.c_int), ("n_layers", ctypes.c_int),
                 ("hidden_dims", ctypes.c_int * 16), ("dropouts", ctypes.c_float * 16),
                 ("lr", ctypes.c_float), ("weight_decay", ctypes.c_float),
-                ("beta1", ctypes.c_float), ("beta2", ctypes.c_float), ("eps", ctypes.c_float)]
+                ("beta1", ctypes.c_float), ("beta2", ctypes.c_float), ("eps", ctypes.c_float),
+                ("seed", ctypes.c_uint)]
 
 
 _oracle = None
@@ -82,7 +83,7 @@ def ptr(a):
 class OracleGCN:
     """The C restatement of hpdga's GCN (L layers; L = 2 is exactly the reference)."""
 
-    def __init__(self, ds, hidden_dims=(16,), dropouts=(0.5, 0.5), lr=0.01, wd=5e-4):
+    def __init__(self, ds, hidden_dims=(16,), dropouts=(0.5, 0.5), lr=0.01, wd=5e-4, seed=0):
         lib = oracle()
         p = OrParams()
         p.num_nodes, p.input_dim, p.output_dim = ds["n"], ds["f"], ds["c"]
@@ -92,6 +93,7 @@ class OracleGCN:
         for i, d in enumerate(dropouts):
             p.dropouts[i] = d
         p.lr, p.weight_decay, p.beta1, p.beta2, p.eps = lr, wd, 0.9, 0.999, 1e-8
+        p.seed = seed
         self._keep = [np.ascontiguousarray(ds[k]) for k in
                       ("graph_indptr", "graph_indices", "feat_indptr", "feat_indices",
                        "feat_values", "label", "split")]

@@ -286,3 +286,31 @@ def test_lds_schedule_ragged_graph(pgcn):
     for window in (1, 2, 3, 4):
         err, _ = _lds_check(pgcn, ip, ix, n, window)
         assert err < 1e-12
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2, 1382895624, 311288059, 2108234352, 19990304])
+def test_rng_seed_glibc_matches_srand(pgcn, seed):
+    """PART2 `seed`: the xorshift state is the first two rand() values after srand(seed)
+    (hpdga rand.cpp:6-14 with the seed applied); seed 0/1 = the unseeded default.  Checked
+    against the C library itself, and the engine against the oracle."""
+    libc = ctypes.CDLL("libc.so.6")
+    libc.srand(ctypes.c_uint(seed))
+    want = [libc.rand(), libc.rand()]
+    libc.srand(ctypes.c_uint(1))
+    got = pgcn.rng_seed(seed) if seed else pgcn.rng_seed()
+    assert [int(got[0]), int(got[1])] == want
+    orc = helpers.oracle()
+    s = np.zeros(2, np.uint64)
+    orc.or_rng_seed_glibc(ctypes.c_uint(seed), helpers.ptr(s))
+    assert [int(s[0]), int(s[1])] == want
+
+
+def test_dataset_binarize(pgcn, tmp_path):
+    """PART2 NO_FEATURE (src/parser.cpp:100-104): values 1.0, ids and dims unchanged."""
+    root = str(tmp_path)
+    ds = pgcn.Dataset.load(root, helpers.materialize_dataset("cora", root))
+    ids, f = ds.feat_indices.copy(), ds.input_dim
+    ds.binarize()
+    assert (ds.feat_values == 1.0).all()
+    np.testing.assert_array_equal(ds.feat_indices, ids)
+    assert ds.input_dim == f

@@ -253,7 +253,9 @@ GEMM_VARIANTS = [0, 1]  # 0: N <= 16 streaming kernels where they apply; 1: gene
 @pytest.mark.parametrize("M,N,K,drop,base", [(1000, 16, 602, True, 0), (777, 41, 16, False, 0),
                                              (513, 16, 41, False, 0), (300, 128, 128, False, 0),
                                              (64, 16, 1433, True, 0), (2011, 16, 602, True, 37),
-                                             (99, 13, 70, True, 63), (5, 16, 602, True, 1)])
+                                             (99, 13, 70, True, 63), (5, 16, 602, True, 1),
+                                             (500, 200, 72, True, 5), (300, 300, 41, False, 0),
+                                             (257, 136, 16, False, 0)])
 def test_gemm_nn(pgcn, M, N, K, drop, base, variant):
     rng = np.random.default_rng(M + N + K)
     lda = (K + 3) // 4 * 4
@@ -293,7 +295,8 @@ def test_gemm_nn(pgcn, M, N, K, drop, base, variant):
                                              (2000, 128, 128, False, 0), (100, 16, 1433, True, 0),
                                              (70000, 16, 602, False, 0), (4099, 16, 602, True, 29),
                                              (333, 16, 200, True, 63), (7, 11, 602, True, 5),
-                                             (3000, 128, 602, True, 0), (2000, 80, 300, True, 3)])
+                                             (3000, 128, 602, True, 0), (2000, 80, 300, True, 3),
+                                             (1000, 200, 72, True, 3), (600, 136, 16, False, 0)])
 def test_gemm_tn(pgcn, M, N, K, drop, base, variant):
     rng = np.random.default_rng(M + 3 * N + K)
     lda = (K + 3) // 4 * 4
