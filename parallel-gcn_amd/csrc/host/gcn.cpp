@@ -53,16 +53,32 @@ float Adam::step_size(int t) const {
 
 void Adam::step(const Stream &s) {
   step_count++;
-  const float st = step_size(step_count);
-  for (auto &v : vars)
-    launch_adam(v.w->dev_data.get(), v.w->dev_grad.get(), v.m.get(), v.v.get(), v.w->size, st,
-                params.beta1, params.beta2, params.eps, params.weight_decay, v.decay ? 1 : 0,
-                s.get());
+  launch(s, step_size(step_count), nullptr, nullptr, 1);
 }
 
 void Adam::step_graph(const Stream &s, const float *table, const int *ctr, int cap) const {
+  launch(s, 0.0f, table, ctr, cap);
+}
+
+// every weight in one launch when they fit one AdamBatch (the 2-layer model: W1 and W2)
+void Adam::launch(const Stream &s, float st, const float *table, const int *ctr, int cap) const {
+  if (vars.size() <= (size_t)kAdamBatch) {
+    AdamBatch b{};
+    for (const auto &v : vars) {
+      b.w[b.count] = v.w->dev_data.get();
+      b.g[b.count] = v.w->dev_grad.get();
+      b.m[b.count] = v.m.get();
+      b.v[b.count] = v.v.get();
+      b.n[b.count] = v.w->size;
+      b.decay[b.count] = v.decay ? 1 : 0;
+      b.count++;
+    }
+    launch_adam_multi(b, st, params.beta1, params.beta2, params.eps, params.weight_decay, s.get(),
+                      table, ctr, cap);
+    return;
+  }
   for (auto &v : vars)
-    launch_adam(v.w->dev_data.get(), v.w->dev_grad.get(), v.m.get(), v.v.get(), v.w->size, 0.0f,
+    launch_adam(v.w->dev_data.get(), v.w->dev_grad.get(), v.m.get(), v.v.get(), v.w->size, st,
                 params.beta1, params.beta2, params.eps, params.weight_decay, v.decay ? 1 : 0,
                 s.get(), table, ctr, cap);
 }
@@ -497,6 +513,13 @@ void GCN::set_split(int split) {
 // graph: the slot from the device epoch counter
 void GCN::finalize(int dst_offset, bool graph) {
   const auto &w1 = weights.front();
+  if (!comm) {  // one launch: reduce + compose
+    launch_reduce_scalars(xent_partials.get(), ctx.xent_blocks, w1->dev_data.get(), w1->size,
+                          sums.get(), stream.get(), ctx.count, adam_params.weight_decay,
+                          results_ring.get() + dst_offset, graph ? dev_ctr.get() : nullptr,
+                          ring_cap);
+    return;
+  }
   launch_reduce_scalars(xent_partials.get(), ctx.xent_blocks, w1->dev_data.get(), w1->size,
                         sums.get(), stream.get());
   if (comm) comm->allreduce_sum(sums.get(), 2, stream.get());

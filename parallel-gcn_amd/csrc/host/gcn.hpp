@@ -62,6 +62,9 @@ class Adam {
   void advance() { step_count++; }
   int steps() const { return step_count; }
   float step_size(int t) const;  // hpdga optim.cpp:24, step t (1-based)
+
+ private:
+  void launch(const Stream &s, float st, const float *table, const int *ctr, int cap) const;
 };
 
 struct DistSpec {

@@ -327,7 +327,11 @@ __global__ __launch_bounds__(256) void k_xent_fwd(float *__restrict__ logits, in
 __global__ __launch_bounds__(1024) void k_reduce_scalars(const float *__restrict__ partials,
                                                          int n_blocks,
                                                          const float *__restrict__ w,
-                                                         long long n_w, float *__restrict__ sums) {
+                                                         long long n_w, float *__restrict__ sums,
+                                                         int count, float wd,
+                                                         float *__restrict__ out2,
+                                                         const int *__restrict__ ctr,
+                                                         int ring_cap) {
   __shared__ float red[16];
   float l = 0.0f, wr = 0.0f, q = 0.0f;
   for (int b = threadIdx.x; b < n_blocks; b += blockDim.x) {
@@ -345,6 +349,11 @@ __global__ __launch_bounds__(1024) void k_reduce_scalars(const float *__restrict
     sums[0] = l;
     sums[1] = wr;
     sums[2] = q;
+    if (out2) {  // one GPU: k_compose's arithmetic here, no second launch
+      if (ctr) out2 += 4 * (ctr[1] % ring_cap);
+      out2[0] = l / (float)count + wd * q / 2.0f;
+      out2[1] = (float)(count - (int)wr) / (float)count;
+    }
   }
 }
 
@@ -363,14 +372,10 @@ __global__ void k_compose(const float *__restrict__ sums, int count, float wd,
 }
 
 // Adam (hpdga optim.cpp:25-33): double temporaries where the reference has them.
-__global__ __launch_bounds__(256) void k_adam(float *__restrict__ w, const float *__restrict__ g,
-                                              float *__restrict__ m, float *__restrict__ v,
-                                              long long n, float step_size, float beta1,
-                                              float beta2, float eps, float wd, int decay,
-                                              const float *__restrict__ step_table,
-                                              const int *__restrict__ ctr, int table_cap) {
-  // epoch graphs: the step size of step ctr[0] + 1, computed on the host (optim.cpp:24)
-  if (step_table) step_size = step_table[ctr[0] % table_cap];
+__device__ __forceinline__ void adam_range(float *__restrict__ w, const float *__restrict__ g,
+                                           float *__restrict__ m, float *__restrict__ v,
+                                           long long n, float step_size, float beta1,
+                                           float beta2, float eps, float wd, int decay) {
   const double ob1 = 1.0 - (double)beta1, ob2 = 1.0 - (double)beta2;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x) {
@@ -384,6 +389,29 @@ __global__ __launch_bounds__(256) void k_adam(float *__restrict__ w, const float
     w[i] = wi - step_size * mi / (sqrtf(vi) + eps);
   }
 }
+
+// every weight of the model in one launch: tensor blockIdx.y
+__global__ __launch_bounds__(256) void k_adam_multi(AdamBatch b, float step_size, float beta1,
+                                                    float beta2, float eps, float wd,
+                                                    const float *__restrict__ step_table,
+                                                    const int *__restrict__ ctr, int table_cap) {
+  if (step_table) step_size = step_table[ctr[0] % table_cap];
+  const int t = blockIdx.y;
+  adam_range(b.w[t], b.g[t], b.m[t], b.v[t], b.n[t], step_size, beta1, beta2, eps, wd,
+             b.decay[t]);
+}
+
+__global__ __launch_bounds__(256) void k_adam(float *__restrict__ w, const float *__restrict__ g,
+                                              float *__restrict__ m, float *__restrict__ v,
+                                              long long n, float step_size, float beta1,
+                                              float beta2, float eps, float wd, int decay,
+                                              const float *__restrict__ step_table,
+                                              const int *__restrict__ ctr, int table_cap) {
+  // epoch graphs: the step size of step ctr[0] + 1, computed on the host (optim.cpp:24)
+  if (step_table) step_size = step_table[ctr[0] % table_cap];
+  adam_range(w, g, m, v, n, step_size, beta1, beta2, eps, wd, decay);
+}
+
 
 // ------------------------------------------------------------------------------------------
 // launchers
@@ -442,9 +470,10 @@ void launch_xent_fwd(float *logits, int ld, float *grad, const int *truth, int n
 }
 
 void launch_reduce_scalars(const float *partials, int n_blocks, const float *w, long long n_w,
-                           float *sums, hipStream_t s) {
+                           float *sums, hipStream_t s, int count, float wd, float *out2,
+                           const int *ctr, int ring_cap) {
   hipLaunchKernelGGL(k_reduce_scalars, dim3(1), dim3(1024), 0, s, partials, n_blocks, w, n_w,
-                     sums);
+                     sums, count, wd, out2, ctr, ring_cap);
 }
 
 void launch_compose(const float *sums, int count, float wd, float *out2, hipStream_t s,
@@ -467,6 +496,16 @@ __global__ void k_counters(int *ctr, int set, int step, int epoch) {
 
 void launch_counters(int *ctr, int set, int step, int epoch, hipStream_t s) {
   hipLaunchKernelGGL(k_counters, dim3(1), dim3(64), 0, s, ctr, set, step, epoch);
+}
+
+void launch_adam_multi(const AdamBatch &b, float step_size, float beta1, float beta2, float eps,
+                       float wd, hipStream_t s, const float *step_table, const int *ctr,
+                       int table_cap) {
+  if (b.count <= 0) return;
+  long long nmax = 0;
+  for (int t = 0; t < b.count; t++) nmax = std::max(nmax, b.n[t]);
+  hipLaunchKernelGGL(k_adam_multi, dim3(grid_for(nmax), b.count), dim3(256), 0, s, b, step_size,
+                     beta1, beta2, eps, wd, step_table, ctr, table_cap);
 }
 
 void launch_adam(float *w, const float *g, float *m, float *v, long long n, float step_size,

@@ -706,7 +706,16 @@ __global__ __launch_bounds__(256) void k_gemm_tn_reduce(const float *__restrict_
   if (e >= (long long)K * ldp) return;
   const int k = (int)(e / ldp), j = (int)(e - (long long)k * ldp);
   float s = 0.0f;
-  for (int b = 0; b < n_groups; b++) s += part2[(long long)b * K * ldp + e];
+  // loads in batches of 16 before their (ordered) adds: one memory latency per batch
+  const long long stride = (long long)K * ldp;
+  for (int b0 = 0; b0 < n_groups; b0 += 16) {
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 16; u++) v[u] = b0 + u < n_groups ? part2[(b0 + u) * stride + e] : 0.0f;
+#pragma unroll
+    for (int u = 0; u < 16; u++)
+      if (b0 + u < n_groups) s += v[u];
+  }
   if (j < nst) C[(long long)k * ldc + j] = j < N ? s : 0.0f;
 }
 

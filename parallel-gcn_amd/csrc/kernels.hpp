@@ -101,7 +101,8 @@ int xent_blocks(int n);
 void launch_xent_fwd(float *logits, int ld, float *grad, const int *truth, int n, int c,
                      int count, int training, float *partials, hipStream_t s);
 void launch_reduce_scalars(const float *partials, int n_blocks, const float *w, long long n_w,
-                           float *sums, hipStream_t s);
+                           float *sums, hipStream_t s, int count = 0, float wd = 0.0f,
+                           float *out2 = nullptr, const int *ctr = nullptr, int ring_cap = 1);
 // ctr (epoch graphs, device {Adam step, epoch} counters): slot 4 * (ctr[1] % ring_cap) of out2
 void launch_compose(const float *sums, int count, float wd, float *out2, hipStream_t s,
                     const int *ctr = nullptr, int ring_cap = 1);
@@ -109,6 +110,19 @@ void launch_compose(const float *sums, int count, float wd, float *out2, hipStre
 void launch_adam(float *w, const float *g, float *m, float *v, long long n, float step_size,
                  float beta1, float beta2, float eps, float wd, int decay, hipStream_t s,
                  const float *step_table = nullptr, const int *ctr = nullptr, int table_cap = 1);
+// all weights of the model in one launch (<= kAdamBatch tensors; tensor t = grid row t)
+constexpr int kAdamBatch = 8;
+struct AdamBatch {
+  float *w[kAdamBatch];
+  const float *g[kAdamBatch];
+  float *m[kAdamBatch], *v[kAdamBatch];
+  long long n[kAdamBatch];
+  int decay[kAdamBatch];
+  int count;
+};
+void launch_adam_multi(const AdamBatch &b, float step_size, float beta1, float beta2, float eps,
+                       float wd, hipStream_t s, const float *step_table = nullptr,
+                       const int *ctr = nullptr, int table_cap = 1);
 // set: ctr = {step, epoch}; else both += 1 (the end of a graph-replayed epoch)
 void launch_counters(int *ctr, int set, int step, int epoch, hipStream_t s);
 
