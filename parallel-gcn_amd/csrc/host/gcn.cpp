@@ -314,6 +314,28 @@ void GCN::build(const GCNData &data) {
     }
     stream.sync();
   }
+  // the same for the edge-cut engine: per 16-column chunk of X, every row chunk's partial
+  // sums from this rank's columns reduce-scattered exactly as GraphSum::run does (this rank
+  // receives its own rows), then placed into Â X's columns
+  if (g_eval_ax && comm && feats.dense && feats.cols >= 16) {
+    const int h = part.chunk_rows(), nk = (int)chunk_graphs.size();
+    feats.ax.allocate(feats.x.size());
+    feats.ax.zero();
+    DeviceBuffer<float> partial((size_t)part.world * h * 16), own((size_t)nk * h * 16);
+    for (int c0 = 0; c0 < feats.cols; c0 += 16) {
+      const int c = std::min(c0, feats.ldx - 16);
+      for (int k = 0; k < nk; k++) {
+        chunk_graphs[(size_t)k]->graphsum(feats.x.get() + c, feats.ldx, partial.get(), 16, 16,
+                                          stream.get());
+        comm->reduce_scatter_sum(partial.get(), own.get() + (size_t)k * h * 16, (size_t)h * 16,
+                                 stream.get());
+      }
+      PGCN_HIP(hipMemcpy2DAsync(feats.ax.get() + c, sizeof(float) * feats.ldx, own.get(),
+                                sizeof(float) * 16, sizeof(float) * 16, (size_t)part.local_rows(),
+                                hipMemcpyDeviceToDevice, stream.get()));
+    }
+    stream.sync();
+  }
   // truth per split for this rank's rows, padded with -1 (set_truth, src/gcn.cu:204-226)
   const int first = part.first(), rows = part.local_rows(), prow = part.maxrows;
   for (int s = 1; s <= 3; s++) {
