@@ -216,8 +216,7 @@ def main():
     # the same epoch with the engine's epoch reorganisations off (train-ahead, output-layer
     # row restriction, eval from Â X): every module runs the reference's full
     # per-epoch work, for comparison (same synthetic data, fewer steps)
-    opts = {"train_ahead": 1, "split_rows": 0 if world > 1 else 1,
-            "eval_ax": 1, "reassociate_last": 1}
+    opts = {"train_ahead": 1, "split_rows": 1, "eval_ax": 1, "reassociate_last": 1}
     out["engine_options"] = opts
     if not args.no_plain and world == 1 and not args.edge_cut:
         for k in ("train_ahead", "split_rows", "eval_ax"):

@@ -354,7 +354,12 @@ void GCN::build(const GCNData &data) {
     truth_compact[s].allocate(std::max<size_t>(tc.size(), 1));
     if (!tc.empty()) truth_compact[s].upload(tc);
     int c = 0;
-    for (int i = 0; i < N; i++) c += (data.split[(size_t)i] == s && data.label[(size_t)i] >= 0);
+    split_rows_global[s].clear();
+    for (int i = 0; i < N; i++)
+      if (data.split[(size_t)i] == s && data.label[(size_t)i] >= 0) {
+        c++;
+        if (comm) split_rows_global[s].push_back(i);  // edge-cut row restriction (set_split)
+      }
     counts[s] = c;
   }
   // weights: glorot in layer order from the default seed (hpdga gcn.cpp:64-128)
@@ -513,6 +518,33 @@ void GCN::set_split(int split) {
     }
     ctx.split_graph = split_graphs[split].get();
     ctx.split_rows = split_rows_dev[split].get();
+  }
+  ctx.chunk_split_graphs.clear();
+  ctx.chunk_split_rows.clear();
+  if (g_split_rows && comm && !chunk_graphs.empty()) {
+    // edge-cut: the output layer's forward sums only the split's labelled rows of every RS
+    // chunk (padded chunk row q*h + j = global node bounds[q] + k*h + j)
+    if (chunk_split_graphs[split].empty()) {
+      const int h = part.chunk_rows();
+      std::vector<char> in_split((size_t)params.num_nodes, 0);
+      for (int i : split_rows_global[split]) in_split[(size_t)i] = 1;
+      for (size_t k = 0; k < chunk_graphs.size(); k++) {
+        std::vector<int> rows;
+        for (int q = 0; q < part.world; q++)
+          for (int j = 0; j < h; j++) {
+            const long long i = (long long)part.bounds[(size_t)q] + (long long)k * h + j;
+            if (i < part.bounds[(size_t)q + 1] && in_split[(size_t)i]) rows.push_back(q * h + j);
+          }
+        chunk_split_graphs[split].push_back(chunk_graphs[k]->row_subset(rows));
+        chunk_split_rows[split].emplace_back();
+        chunk_split_rows[split].back().allocate(std::max<size_t>(rows.size(), 1));
+        if (!rows.empty()) chunk_split_rows[split].back().upload(rows);
+      }
+    }
+    for (size_t k = 0; k < chunk_graphs.size(); k++) {
+      ctx.chunk_split_graphs.push_back(chunk_split_graphs[split][k].get());
+      ctx.chunk_split_rows.push_back(chunk_split_rows[split][k].get());
+    }
   }
   if (g_split_rows && !comm && graph && split == 1) {  // backward only follows training
     if (!split_colgraphs[split]) split_colgraphs[split] = graph->col_subset(split_rows_host[split]);

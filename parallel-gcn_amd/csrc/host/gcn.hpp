@@ -123,8 +123,12 @@ class GCN {
   int counts[4] = {0, 0, 0, 0};
   // output-layer row restriction (set_split): per split, its labelled rows and Â on them
   std::vector<int> split_rows_host[4];
+  std::vector<int> split_rows_global[4];  // edge-cut: the split's labelled global node ids
   DeviceBuffer<int> split_rows_dev[4];
   std::unique_ptr<DevGraph> split_graphs[4], split_colgraphs[4];
+  // edge-cut: per split, per RS chunk, the chunk graph on the split's rows + their row ids
+  std::vector<std::unique_ptr<DevGraph>> chunk_split_graphs[4];
+  std::vector<DeviceBuffer<int>> chunk_split_rows[4];
   DeviceBuffer<int> truth_compact[4];                // the split's labels, compact row order
   std::unique_ptr<Variable> compact_z, compact_out;  // compact output layer (ModuleContext)
   long long nnz_x_global = 0;

@@ -193,7 +193,7 @@ GraphSum::GraphSum(shared_ptr<Variable> in_, shared_ptr<Variable> out_, DevGraph
   }
 }
 
-void GraphSum::run(const float *src, float *dst, const Stream &s) const {
+void GraphSum::run(const float *src, float *dst, const Stream &s, bool split) const {
   Event e0, e1;
   if (ctx->profile) {
     e0 = Event::create(true);
@@ -207,9 +207,23 @@ void GraphSum::run(const float *src, float *dst, const Stream &s) const {
     // its own rows of the chunk while the next chunk is summed.
     const size_t h = (size_t)out->rows / ctx->chunk_graphs.size();
     for (size_t k = 0; k < ctx->chunk_graphs.size(); k++) {
-      DevGraph *gk = ctx->chunk_graphs[k];
-      gk->graphsum(src, in->ld, partial[k].get(), out->ld, dim, s.get());
-      bytes += gk->algorithmic_bytes(dim);
+      if (split) {
+        // only the split's rows of the chunk; the chunk's other partial rows keep their last
+        // values (finite), which reach only rows the loss skips and whose loss gradient is 0
+        DevGraph *sk = ctx->chunk_split_graphs[k];
+        if (sk->rows() > 0) {
+          const size_t need = (size_t)sk->rows() * out->ld;
+          if (compact.size() < need) compact.allocate(need);
+          sk->graphsum(src, in->ld, compact.get(), out->ld, dim, s.get());
+          launch_scatter_rows(compact.get(), ctx->chunk_split_rows[k], sk->rows(), out->ld,
+                              partial[k].get(), s.get());
+          bytes += sk->algorithmic_bytes(dim);
+        }
+      } else {
+        DevGraph *gk = ctx->chunk_graphs[k];
+        gk->graphsum(src, in->ld, partial[k].get(), out->ld, dim, s.get());
+        bytes += gk->algorithmic_bytes(dim);
+      }
       computed[k].record(s.get());
       computed[k].wait_on(ctx->comm_stream);
       ctx->comm->reduce_scatter_sum(partial[k].get(), dst + k * h * out->ld, h * out->ld,
@@ -231,6 +245,10 @@ void GraphSum::run(const float *src, float *dst, const Stream &s) const {
 
 void GraphSum::forward(bool training, const Stream &s) const {
   if (!training && first_layer) return;  // eval_ax: SparseMatmul wrote Â X W1 already
+  if (last_layer && ctx->comm && !ctx->chunk_split_graphs.empty()) {
+    run(in->dev_data.get(), out->dev_data.get(), s, true);
+    return;
+  }
   DevGraph *sg = last_layer && !ctx->comm ? ctx->split_graph : nullptr;
   if (!sg) {
     run(in->dev_data.get(), out->dev_data.get(), s);

@@ -112,6 +112,10 @@ struct ModuleContext {
   Comm *comm = nullptr;        // null on one GPU
   hipStream_t comm_stream = nullptr;      // edge-cut: stream of the reduce-scatters
   std::vector<DevGraph *> chunk_graphs;   // edge-cut: Â column block per RS row chunk
+  // edge-cut output-layer row restriction: per RS chunk, the chunk graph restricted to the
+  // current split's labelled rows (padded chunk row ids in chunk_split_rows); empty: off
+  std::vector<DevGraph *> chunk_split_graphs;
+  std::vector<const int *> chunk_split_rows;
   const void *jump_table = nullptr;  // M^period byte tables (device)
   void *gemm_workspace = nullptr;
   // profiling of GraphSum calls
@@ -194,7 +198,8 @@ class GraphSum : public Module {
   void backward(const Stream &s) const override;
 
  private:
-  void run(const float *src, float *dst, const Stream &s) const;
+  // split: edge-cut output-layer forward over ctx->chunk_split_graphs (the split's rows)
+  void run(const float *src, float *dst, const Stream &s, bool split = false) const;
 };
 
 // include/module.cuh:90-99

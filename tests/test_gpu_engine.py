@@ -161,6 +161,30 @@ def test_edge_cut_world1_large_matches_single(pgcn):
     cut.close()
 
 
+@pytest.mark.parametrize("name", ["cora", "synthetic"])
+def test_edge_cut_split_rows_matches_all_rows(loaded, pgcn, name):
+    """Edge-cut engine: the output layer's forward over the split's rows of every reduce-
+    scatter chunk gives the same losses, accuracies and weights as summing all rows."""
+    ds = loaded["cora"] if name == "cora" else pgcn.Dataset.synthetic(150000, 32, 8, 5000000, 6)
+    p = pgcn.make_params(ds)
+    runs = []
+    for on in (1, 0):
+        pgcn.lib.pgcn_debug_set(b"split_rows", on)
+        g = pgcn.GCN(p, ds, device=0, rank=0, world=1, unique_id=pgcn.comm_unique_id())
+        lines = [g.train_epoch() + g.eval(2) for _ in range(4)]
+        for _ in range(2):
+            g.epoch_async()
+        lines += [tuple(r) for r in g.results(2)]
+        lines.append(g.eval(3) + (0.0, 0.0))
+        runs.append((np.array(lines, np.float64), g.get_var(2)))
+        g.close()
+    pgcn.lib.pgcn_debug_set(b"split_rows", 1)
+    (a, wa), (b, wb) = runs
+    np.testing.assert_allclose(a[:, [0, 2]], b[:, [0, 2]], rtol=1e-5)
+    np.testing.assert_allclose(a[:, [1, 3]], b[:, [1, 3]], atol=2e-3)
+    np.testing.assert_allclose(wa, wb, rtol=1e-4, atol=1e-6)
+
+
 def test_deep_model_matches_oracle(loaded, pgcn):
     """4-layer, hidden 128 (the deep configuration of SURVEY.md §8a): the engine's L-layer
     stack against the oracle's L-layer restatement of the same module order."""
