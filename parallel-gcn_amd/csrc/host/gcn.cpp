@@ -546,6 +546,13 @@ void GCN::set_split(int split) {
       ctx.chunk_split_rows.push_back(chunk_split_rows[split][k].get());
     }
   }
+  ctx.chunk_col_graphs.clear();
+  if (g_split_rows && comm && !chunk_graphs.empty() && split == 1 &&
+      !split_rows_host[1].empty()) {  // backward follows training
+    if (chunk_col_graphs.empty())
+      for (auto &gk : chunk_graphs) chunk_col_graphs.push_back(gk->col_subset(split_rows_host[1]));
+    for (auto &cg : chunk_col_graphs) ctx.chunk_col_graphs.push_back(cg.get());
+  }
   if (g_split_rows && !comm && graph && split == 1) {  // backward only follows training
     if (!split_colgraphs[split]) split_colgraphs[split] = graph->col_subset(split_rows_host[split]);
     ctx.split_colgraph = split_colgraphs[split].get();

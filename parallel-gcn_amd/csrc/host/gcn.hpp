@@ -129,6 +129,7 @@ class GCN {
   // edge-cut: per split, per RS chunk, the chunk graph on the split's rows + their row ids
   std::vector<std::unique_ptr<DevGraph>> chunk_split_graphs[4];
   std::vector<DeviceBuffer<int>> chunk_split_rows[4];
+  std::vector<std::unique_ptr<DevGraph>> chunk_col_graphs;  // training split's columns
   DeviceBuffer<int> truth_compact[4];                // the split's labels, compact row order
   std::unique_ptr<Variable> compact_z, compact_out;  // compact output layer (ModuleContext)
   long long nnz_x_global = 0;

@@ -193,7 +193,7 @@ GraphSum::GraphSum(shared_ptr<Variable> in_, shared_ptr<Variable> out_, DevGraph
   }
 }
 
-void GraphSum::run(const float *src, float *dst, const Stream &s, bool split) const {
+void GraphSum::run(const float *src, float *dst, const Stream &s, int mode) const {
   Event e0, e1;
   if (ctx->profile) {
     e0 = Event::create(true);
@@ -207,7 +207,7 @@ void GraphSum::run(const float *src, float *dst, const Stream &s, bool split) co
     // its own rows of the chunk while the next chunk is summed.
     const size_t h = (size_t)out->rows / ctx->chunk_graphs.size();
     for (size_t k = 0; k < ctx->chunk_graphs.size(); k++) {
-      if (split) {
+      if (mode == 1) {
         // only the split's rows of the chunk; the chunk's other partial rows keep their last
         // values (finite), which reach only rows the loss skips and whose loss gradient is 0
         DevGraph *sk = ctx->chunk_split_graphs[k];
@@ -220,7 +220,7 @@ void GraphSum::run(const float *src, float *dst, const Stream &s, bool split) co
           bytes += sk->algorithmic_bytes(dim);
         }
       } else {
-        DevGraph *gk = ctx->chunk_graphs[k];
+        DevGraph *gk = mode == 2 ? ctx->chunk_col_graphs[k] : ctx->chunk_graphs[k];
         gk->graphsum(src, in->ld, partial[k].get(), out->ld, dim, s.get());
         bytes += gk->algorithmic_bytes(dim);
       }
@@ -246,7 +246,7 @@ void GraphSum::run(const float *src, float *dst, const Stream &s, bool split) co
 void GraphSum::forward(bool training, const Stream &s) const {
   if (!training && first_layer) return;  // eval_ax: SparseMatmul wrote Â X W1 already
   if (last_layer && ctx->comm && !ctx->chunk_split_graphs.empty()) {
-    run(in->dev_data.get(), out->dev_data.get(), s, true);
+    run(in->dev_data.get(), out->dev_data.get(), s, 1);
     return;
   }
   DevGraph *sg = last_layer && !ctx->comm ? ctx->split_graph : nullptr;
@@ -283,6 +283,12 @@ void GraphSum::forward(bool training, const Stream &s) const {
 
 void GraphSum::backward(const Stream &s) const {
   // the same gather on grads (Â symmetric): in.grad = Â out.grad (module.cpp:98-111)
+  if (last_layer && ctx->comm && !ctx->chunk_col_graphs.empty()) {
+    // edge-cut: out.grad is zero outside the training split's rows, so each chunk graph keeps
+    // only the edges from those columns (all rows stay: the partials are written whole)
+    run(out->dev_grad.get(), in->dev_grad.get(), s, 2);
+    return;
+  }
   DevGraph *cg = last_layer && !ctx->comm ? ctx->split_colgraph : nullptr;
   if (!cg) {
     run(out->dev_grad.get(), in->dev_grad.get(), s);

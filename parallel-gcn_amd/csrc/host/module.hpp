@@ -116,6 +116,9 @@ struct ModuleContext {
   // current split's labelled rows (padded chunk row ids in chunk_split_rows); empty: off
   std::vector<DevGraph *> chunk_split_graphs;
   std::vector<const int *> chunk_split_rows;
+  // ... and its backward: per RS chunk, the chunk graph on the columns (local rows) of the
+  // training split, where the loss gradient is non-zero; empty: off
+  std::vector<DevGraph *> chunk_col_graphs;
   const void *jump_table = nullptr;  // M^period byte tables (device)
   void *gemm_workspace = nullptr;
   // profiling of GraphSum calls
@@ -198,8 +201,9 @@ class GraphSum : public Module {
   void backward(const Stream &s) const override;
 
  private:
-  // split: edge-cut output-layer forward over ctx->chunk_split_graphs (the split's rows)
-  void run(const float *src, float *dst, const Stream &s, bool split = false) const;
+  // mode (edge-cut output layer): 0 all rows, 1 forward over ctx->chunk_split_graphs (the
+  // split's rows), 2 backward over ctx->chunk_col_graphs (the split's columns)
+  void run(const float *src, float *dst, const Stream &s, int mode = 0) const;
 };
 
 // include/module.cuh:90-99
