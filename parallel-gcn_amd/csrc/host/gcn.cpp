@@ -506,7 +506,7 @@ void GCN::set_split(int split) {
   ctx.count = counts[split];
   modules.back()->set_num_samples(counts[split]);
   // output-layer row restriction: Â restricted to the split's labelled rows, built at the
-  // split's first use (single GPU; the edge-cut engine sums all rows)
+  // split's first use (single GPU; the edge-cut engine restricts its chunk graphs below)
   ctx.split_graph = nullptr;
   ctx.split_rows = nullptr;
   ctx.split_colgraph = nullptr;

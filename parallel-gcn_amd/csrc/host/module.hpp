@@ -90,9 +90,10 @@ struct ModuleContext {
   bool mask_side = false;
   hipStream_t side_stream = nullptr;  // ... drawn here ...
   Event tn_start, mask_ready;         // ... after tn_start (main), signalling mask_ready
-  // output-layer row restriction (single GPU): the last GraphSum's forward computes only the
-  // current split's labelled rows -- the only rows the loss, the accuracy and (through the
-  // loss gradient, zero elsewhere) the weight gradients depend on
+  // output-layer row restriction (single GPU; the edge-cut engine uses chunk_split_graphs):
+  // the last GraphSum's forward computes only the current split's labelled rows -- the only
+  // rows the loss, the accuracy and (through the loss gradient, zero elsewhere) the weight
+  // gradients depend on
   DevGraph *split_graph = nullptr;  // Â restricted to those rows (null: all rows)
   const int *split_rows = nullptr;  // their row ids (device)
   // ... and its backward: the loss gradient is zero outside those rows, so Â out.grad only
