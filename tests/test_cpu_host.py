@@ -314,3 +314,26 @@ def test_dataset_binarize(pgcn, tmp_path):
     assert (ds.feat_values == 1.0).all()
     np.testing.assert_array_equal(ds.feat_indices, ids)
     assert ds.input_dim == f
+
+
+def test_gcn_par_cli_loader_paths(tmp_path):
+    """gcn-par (the reference's entry point, src/main.cpp:9-61): a missing dataset is reported
+    like the reference; cache=1 writes the binary cache while loading, and the run then stops
+    at engine creation on a host without a HIP device (no CPU fallback)."""
+    import subprocess
+    import torch
+    exe = os.path.join(helpers.REPO, "parallel-gcn_amd", "bin", "gcn-par")
+    root = str(tmp_path)
+    r = subprocess.run([exe, "nonexistent", f"root={root}"], capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode != 0 and "Cannot read input: nonexistent" in r.stderr
+    if torch.cuda.is_available():
+        pytest.skip("a device is present: gcn-par would train")
+    name = helpers.materialize_dataset("cora", root)
+    params = os.path.join(root, "params.txt")
+    with open(params, "w") as f:
+        f.write("n_layers = 2\nhidden_dims = 72\ndropouts = 0.4,0.2\nseed = 1382895624\n")
+    r = subprocess.run([exe, name, f"root={root}", f"file={params}", "cache=1", "no_feature=1"],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0 and "GCN creation failed" in r.stderr
+    assert os.path.exists(os.path.join(root, "data", name + ".pgcnbin"))
