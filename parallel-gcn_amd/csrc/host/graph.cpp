@@ -789,7 +789,15 @@ void lds_emulate(const LdsHost &h, int n_rows, const float *in, double *out) {
 int g_lds_blocks = 0;
 int lds_blocks(int n_rows, int n_cols) {
   if (g_lds_blocks) return g_lds_blocks;
-  return (double)n_rows >= 0.9 * (double)n_cols ? 4 : 8;
+  if ((double)n_rows >= 0.9 * (double)n_cols) return 4;
+  // row subsets: 8 blocks, or more when few batches of rowsets would leave each workgroup a
+  // long sweep over its block's slices with little work per slice (the validation rows: 7
+  // batches -> 32 blocks, a quarter of the slices per workgroup)
+  const long long nrs = ((long long)n_rows + 15) / 16, cap = (long long)LDS_CW * LDS_SLOTS;
+  const long long nb = std::max(1LL, (nrs + cap - 1) / cap);
+  int B = 8;
+  while (B < 32 && nb * B * 2 <= kCUs) B *= 2;
+  return B;
 }
 
 std::vector<int> column_cuts(int n_cols, const std::vector<int> &indices, int n_blocks) {

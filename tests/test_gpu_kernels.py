@@ -117,7 +117,7 @@ def test_graphsum_vs_oracle(pgcn, n, deg, dim, hubs):
     pgcn.lib.pgcn_debug_set(b"graphsum_lds_window", LDS_WINDOW_DEFAULT)
 
 
-@pytest.mark.parametrize("blocks", [2, 8])
+@pytest.mark.parametrize("blocks", [2, 8, 16, 32])
 def test_graphsum_lds_column_blocks(pgcn, blocks):
     """The LDS schedule with other column-block counts than the shape rule picks (4 for square
     graphs, 8 for row subsets): the same sums (XCD mapping: workgroup w serves block w % B)."""
