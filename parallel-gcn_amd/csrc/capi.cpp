@@ -26,6 +26,7 @@ extern int g_xstream_tn_lds;        // k_gemm.hip
 extern int g_eval_ax;               // host/gcn.cpp
 extern int g_epoch_graph;           // host/gcn.cpp
 extern int g_lds_blocks;            // host/graph.cpp
+extern int g_lds_blocks_subset;     // host/graph.cpp (diagnostics)
 extern int g_graphsum_lds;          // host/graph.cpp (diagnostics)
 extern int g_graphsum_lds_wide;     // host/graph.cpp
 extern int g_graphsum_lds_order;    // host/graph.cpp (diagnostics)
@@ -500,9 +501,11 @@ int pgcn_debug_set(const char *key, int value) {
   else if (!std::strcmp(key, "xstream_tn_lds")) pgcn::g_xstream_tn_lds = value;
   else if (!std::strcmp(key, "eval_ax")) pgcn::g_eval_ax = value;
   else if (!std::strcmp(key, "epoch_graph")) pgcn::g_epoch_graph = value;
-  else if (!std::strcmp(key, "lds_blocks")) {
-    if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8) return PGCN_E_INVALID;
-    pgcn::g_lds_blocks = value;
+  else if (!std::strcmp(key, "lds_blocks") || !std::strcmp(key, "lds_blocks_subset")) {
+    if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8 && value != 16 &&
+        value != 32)
+      return PGCN_E_INVALID;
+    (key[10] ? pgcn::g_lds_blocks_subset : pgcn::g_lds_blocks) = value;
   }
   else return PGCN_E_INVALID;
   return PGCN_OK;

@@ -787,6 +787,8 @@ void lds_emulate(const LdsHost &h, int n_rows, const float *in, double *out) {
 // 256 workgroups, half the partials; the same kernel time, combine 18 -> 11 us), 8 for a small
 // row subset (its 256 workgroups then stream half the table each: val rows 0.11 vs 0.22 ms)
 int g_lds_blocks = 0;
+int g_lds_blocks_subset = 0;  // "lds_blocks_subset": override for large row subsets (diagnostics)
+
 int lds_blocks(int n_rows, int n_cols) {
   if (g_lds_blocks) return g_lds_blocks;
   if ((double)n_rows >= 0.9 * (double)n_cols) return 4;
@@ -797,6 +799,7 @@ int lds_blocks(int n_rows, int n_cols) {
   const long long nb = std::max(1LL, (nrs + cap - 1) / cap);
   int B = 8;
   while (B < 32 && nb * B * 2 <= kCUs) B *= 2;
+  if (B == 8 && g_lds_blocks_subset) return g_lds_blocks_subset;  // diagnostics
   return B;
 }
 

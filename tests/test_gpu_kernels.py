@@ -121,7 +121,7 @@ def test_graphsum_vs_oracle(pgcn, n, deg, dim, hubs):
 def test_graphsum_lds_column_blocks(pgcn, blocks):
     """The LDS schedule with other column-block counts than the shape rule picks (4 for square
     graphs, 8 for row subsets): the same sums (XCD mapping: workgroup w serves block w % B)."""
-    pgcn.lib.pgcn_debug_set(b"lds_blocks", blocks)
+    assert pgcn.lib.pgcn_debug_set(b"lds_blocks", blocks) == 0
     try:
         n, dim = 120000, 16
         indptr, indices = random_graph(n, 40, seed=blocks, hubs=20, hub_deg=3000)
