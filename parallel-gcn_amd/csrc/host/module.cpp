@@ -367,7 +367,7 @@ void CrossEntropyLoss::forward(bool training, const Stream &s) const {
   launch_xent_fwd(L.dev_data.get(), L.ld, training ? L.dev_grad.get() : nullptr,
                   ctx->compact_n ? ctx->compact_truth : ctx->truth,
                   ctx->compact_n ? ctx->compact_n : logits->rows, num_classes, ctx->count,
-                  training ? 1 : 0, ctx->xent_partials, s.get());
+                  training ? 1 : 0, ctx->xent_partials, s.get(), ctx->compact_n ? 0 : 1);
 }
 
 void CrossEntropyLoss::backward(const Stream &) const {}  // module.cpp:155-156

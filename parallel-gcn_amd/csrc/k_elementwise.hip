@@ -234,7 +234,9 @@ __global__ __launch_bounds__(256) void k_xent_fwd(float *__restrict__ logits, in
                                                   float *__restrict__ grad,
                                                   const int *__restrict__ truth, int n, int c,
                                                   int count, int training,
-                                                  float *__restrict__ partials) {
+                                                  float *__restrict__ partials, int write_back) {
+  // write_back 0: the shifted logits stay in LDS (the compact output layer's logits are read
+  // by nobody after the loss; hpdga's in-place shift is kept where the variable is visible)
   extern __shared__ float smem[];
   __shared__ float red[4];
   const int S = ld + 1;
@@ -297,7 +299,7 @@ __global__ __launch_bounds__(256) void k_xent_fwd(float *__restrict__ logits, in
     wrong = w ? 1.0f : 0.0f;
   }
   __syncthreads();
-  from_lds(logits);
+  if (write_back) from_lds(logits);
   if (training) {
     __syncthreads();  // the shifted logits have left the tile
     if (threadIdx.x < rows) {
@@ -454,7 +456,7 @@ void launch_relu_bwd(float *g, long long n, const uint8_t *mask, hipStream_t s) 
 int xent_blocks(int n) { return (int)ceil_div(n, XR); }
 
 void launch_xent_fwd(float *logits, int ld, float *grad, const int *truth, int n, int c,
-                     int count, int training, float *partials, hipStream_t s) {
+                     int count, int training, float *partials, hipStream_t s, int write_back) {
   if (n <= 0) return;
   PGCN_CHECK(ld <= 124 && c <= ld && ld % 4 == 0, PGCN_E_INVALID,
              "xent: classes must be <= 124 (ld a multiple of 4)");
@@ -466,7 +468,7 @@ void launch_xent_fwd(float *logits, int ld, float *grad, const int *truth, int n
     attr = true;
   }
   hipLaunchKernelGGL(k_xent_fwd, dim3(xent_blocks(n)), dim3(256), lds, s, logits, ld, grad,
-                     truth, n, c, count, training, partials);
+                     truth, n, c, count, training, partials, write_back);
 }
 
 void launch_reduce_scalars(const float *partials, int n_blocks, const float *w, long long n_w,

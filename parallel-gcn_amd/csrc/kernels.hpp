@@ -99,7 +99,7 @@ void launch_relu_fwd(float *x, long long n, uint8_t *mask, int training, hipStre
 void launch_relu_bwd(float *g, long long n, const uint8_t *mask, hipStream_t s);
 int xent_blocks(int n);
 void launch_xent_fwd(float *logits, int ld, float *grad, const int *truth, int n, int c,
-                     int count, int training, float *partials, hipStream_t s);
+                     int count, int training, float *partials, hipStream_t s, int write_back = 1);
 void launch_reduce_scalars(const float *partials, int n_blocks, const float *w, long long n_w,
                            float *sums, hipStream_t s, int count = 0, float wd = 0.0f,
                            float *out2 = nullptr, const int *ctr = nullptr, int ring_cap = 1);
