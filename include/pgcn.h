@@ -159,8 +159,9 @@ typedef struct {
   int epochs, early_stopping;
   float learning_rate, weight_decay, beta1, beta2, eps;
   /* 1: compute the output layer as (Â H) W instead of Â (H W) when hidden < classes, so its
-   * GraphSum gathers hidden-width rows.  Exact algebra (Â symmetric); only the fp32
-   * rounding order differs from the reference.  0: the reference's module order. */
+   * GraphSum gathers hidden-width rows.  Exact algebra when Â is symmetric (checked at engine
+   * build: a non-symmetric pattern keeps the reference's order); only the fp32 rounding order
+   * differs from the reference.  0: the reference's module order. */
   int reassociate_last;
   /* PART2 `seed` (src/parser.cpp:234): 0 = hpdga's unseeded glibc rand() (init_rand_state,
    * hpdga rand.cpp:6-14); else the xorshift state is the first two rand() values after
@@ -192,7 +193,24 @@ int pgcn_gcn_create(const pgcn_params *p, const pgcn_data *d, int device, pgcn_g
 int pgcn_comm_unique_id(void *unique_id_128);
 int pgcn_gcn_create_dist(const pgcn_params *p, const pgcn_data *d, int device, int rank,
                          int world, const void *unique_id_128, pgcn_gcn **out);
+/* In-process ranks ("fake RCCL"): `world` edge-cut engines in ONE process on
+ * one device, each created and driven by its own host thread (every call that runs a
+ * collective -- create, train_epoch, eval, epoch_async -- rendezvouses with the peers' same
+ * call).  Collectives are stream-ordered device sums of the peers' buffers in rank order, so
+ * the multi-rank engine (partition, chunked reduce-scatters, global dropout offsets, weight
+ * all-reduce) runs unchanged without RCCL.  The group may be destroyed after the engines are
+ * created (they keep it alive). */
+typedef struct pgcn_loopback pgcn_loopback;
+int pgcn_loopback_create(int world, pgcn_loopback **out);
+int pgcn_loopback_destroy(pgcn_loopback *group);
+int pgcn_gcn_create_loopback(const pgcn_params *p, const pgcn_data *d, int device, int rank,
+                             pgcn_loopback *group, pgcn_gcn **out);
 int pgcn_gcn_destroy(pgcn_gcn *g);
+/* Engine facts: "world", "rank", "comm" (0 none, 1 RCCL, 2 loopback), "reassociated",
+ * "graph_symmetric", "graphsum_lds" (width-16 GraphSums take the LDS kernel), "epochs",
+ * "eval_ax_us" (device time of the Â X precompute at engine build, µs; 0 when not used).
+ * Returns the value (>= 0) or PGCN_E_INVALID for an unknown key. */
+long long pgcn_gcn_query(pgcn_gcn *g, const char *key);
 /* GCN::train_epoch / GCN::eval (src/gcn.cu:293-343): out2 = {loss, accuracy} */
 int pgcn_gcn_train_epoch(pgcn_gcn *g, float out2[2]);
 int pgcn_gcn_eval(pgcn_gcn *g, int split, float out2[2]);
@@ -200,13 +218,16 @@ int pgcn_gcn_eval(pgcn_gcn *g, int split, float out2[2]);
  * results land in an on-device ring read by pgcn_gcn_results. */
 int pgcn_gcn_epoch_async(pgcn_gcn *g);
 int pgcn_gcn_sync(pgcn_gcn *g);
-/* copies the last `n` epoch results {train_loss, train_acc, val_loss, val_acc} */
+/* copies the last min(n, epochs run, 1024) epoch results {train_loss, train_acc, val_loss,
+ * val_acc}, oldest first; returns the number of rows copied (>= 0) or a status (< 0) */
 int pgcn_gcn_results(pgcn_gcn *g, int n, float *host_out);
 /* GCN::run (src/gcn.cu:347-436): prints the reference's epoch lines when verbose */
 int pgcn_gcn_run(pgcn_gcn *g, int verbose);
 /* Variables in reference order (input, then per layer var1, weight, var2; see
  * include/gcn.cuh:85). which: 0 data, 1 grad. Returns element count (>= 0) or status. For
- * the edge-cut engine node-sized variables cover this rank's rows only. */
+ * the edge-cut engine node-sized variables cover this rank's rows only.  PGCN_E_INVALID for
+ * the output layer's node variables after a forward with the diagnostic row restriction
+ * ("split_rows" on): their rows outside the split are stale. */
 long long pgcn_gcn_get_var(pgcn_gcn *g, int idx, int which, float *host_dst);
 int pgcn_gcn_num_vars(pgcn_gcn *g);
 /* per-call device timing of the GraphSum kernels (enable before the timed region) */

@@ -101,6 +101,11 @@ _sig("pgcn_comm_unique_id", c_int, c_void_p)
 _sig("pgcn_gcn_create_dist", c_int, P(PgcnParams), P(PgcnData), c_int, c_int, c_int, c_void_p,
      P(c_void_p))
 _sig("pgcn_gcn_destroy", c_int, c_void_p)
+_sig("pgcn_loopback_create", c_int, c_int, P(c_void_p))
+_sig("pgcn_loopback_destroy", c_int, c_void_p)
+_sig("pgcn_gcn_create_loopback", c_int, P(PgcnParams), P(PgcnData), c_int, c_int, c_void_p,
+     P(c_void_p))
+_sig("pgcn_gcn_query", c_ll, c_void_p, ctypes.c_char_p)
 _sig("pgcn_gcn_train_epoch", c_int, c_void_p, P(c_float))
 _sig("pgcn_gcn_eval", c_int, c_void_p, c_int, P(c_float))
 _sig("pgcn_gcn_epoch_async", c_int, c_void_p)
@@ -246,10 +251,15 @@ class GCN:
     """GCN(params, data) of include/gcn.cuh:79-122 on one GPU, or the edge-cut variant when
     rank/world/unique_id are given (one process per GPU)."""
 
-    def __init__(self, params, ds, device=0, rank=None, world=None, unique_id=None):
+    def __init__(self, params, ds, device=0, rank=None, world=None, unique_id=None,
+                 loopback=None):
         self.ds = ds  # keep the host data alive while the engine is built
         h = c_void_p()
-        if world is None:
+        if loopback is not None:
+            check(lib.pgcn_gcn_create_loopback(ctypes.byref(params), ctypes.byref(ds.view),
+                                               device, rank, loopback._h, ctypes.byref(h)),
+                  "gcn_create_loopback")
+        elif world is None:
             check(lib.pgcn_gcn_create(ctypes.byref(params), ctypes.byref(ds.view), device,
                                       ctypes.byref(h)), "gcn_create")
         else:
@@ -276,9 +286,13 @@ class GCN:
         check(lib.pgcn_gcn_sync(self._h), "sync")
 
     def results(self, n):
-        out = np.zeros(4 * n, np.float32)
-        check(lib.pgcn_gcn_results(self._h, n, out.ctypes.data_as(P(c_float))), "results")
-        return out.reshape(n, 4)
+        """The last min(n, epochs run, 1024) epoch lines [train_loss, train_acc, val_loss,
+        val_acc], oldest first."""
+        out = np.zeros(4 * max(n, 0), np.float32)
+        rows = lib.pgcn_gcn_results(self._h, n, out.ctypes.data_as(P(c_float)))
+        if rows < 0:
+            raise PgcnError(rows, "results")
+        return out[:4 * rows].reshape(rows, 4)
 
     def run(self, verbose=True):
         check(lib.pgcn_gcn_run(self._h, 1 if verbose else 0), "run")
@@ -304,6 +318,14 @@ class GCN:
                                         ctypes.byref(byts)), "profile_read")
         return ms.value, calls.value, byts.value
 
+    def query(self, key):
+        """Engine facts: world, rank, comm (0 none / 1 RCCL / 2 loopback), reassociated,
+        graph_symmetric, graphsum_lds, epochs."""
+        v = lib.pgcn_gcn_query(self._h, key.encode())
+        if v < 0:
+            raise PgcnError(int(v), f"query {key}")
+        return int(v)
+
     def node_range(self):
         a, b = c_int(), c_int()
         lib.pgcn_gcn_node_range(self._h, ctypes.byref(a), ctypes.byref(b))
@@ -319,6 +341,45 @@ class GCN:
             self.close()
         except Exception:
             pass
+
+
+class LoopbackGroup:
+    """`world` in-process edge-cut ranks on one device (pgcn_loopback_create).  Create the
+    engines with GCN(..., rank=r, loopback=group), each from its own thread (see run_ranks)."""
+
+    def __init__(self, world):
+        h = c_void_p()
+        check(lib.pgcn_loopback_create(world, ctypes.byref(h)), "loopback_create")
+        self._h = h
+        self.world = world
+
+    def __del__(self):
+        if getattr(self, "_h", None) and self._h.value:
+            lib.pgcn_loopback_destroy(self._h)
+            self._h = c_void_p()
+
+
+def run_ranks(world, fn):
+    """Calls fn(rank) for every rank in its own thread (ctypes releases the GIL during the
+    engine's calls, so the ranks' collectives rendezvous); returns the results in rank order
+    and re-raises the first exception."""
+    import threading
+    out, err = [None] * world, [None] * world
+
+    def body(r):
+        try:
+            out[r] = fn(r)
+        except BaseException as e:  # noqa: BLE001 -- re-raised below
+            err[r] = e
+    ts = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for e in err:
+        if e is not None:
+            raise e
+    return out
 
 
 def comm_unique_id():
@@ -396,7 +457,8 @@ EXPORTED = [
     "pgcn_rng_jump_table", "pgcn_dropout_mask", "pgcn_dropout_apply", "pgcn_relu_fwd",
     "pgcn_relu_bwd", "pgcn_xent_blocks", "pgcn_xent_fwd", "pgcn_finalize", "pgcn_adam",
     "pgcn_adam_step_size", "pgcn_params_default", "pgcn_gcn_create", "pgcn_comm_unique_id",
-    "pgcn_gcn_create_dist", "pgcn_gcn_destroy", "pgcn_gcn_train_epoch", "pgcn_gcn_eval",
+    "pgcn_gcn_create_dist", "pgcn_loopback_create", "pgcn_loopback_destroy",
+    "pgcn_gcn_create_loopback", "pgcn_gcn_query", "pgcn_gcn_destroy", "pgcn_gcn_train_epoch", "pgcn_gcn_eval",
     "pgcn_gcn_epoch_async", "pgcn_gcn_sync", "pgcn_gcn_results", "pgcn_gcn_run",
     "pgcn_gcn_get_var", "pgcn_gcn_num_vars", "pgcn_gcn_profile", "pgcn_gcn_profile_read",
     "pgcn_gcn_node_range", "pgcn_dataset_load", "pgcn_dataset_load_cached", "pgcn_dataset_save",

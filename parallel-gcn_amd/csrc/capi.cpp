@@ -21,6 +21,7 @@ extern int g_graphsum_force_plain;  // host/graph.cpp (diagnostics)
 extern int g_gemm_variant;          // k_gemm.hip (diagnostics)
 extern int g_train_ahead;           // host/gcn.cpp
 extern int g_split_rows;            // host/gcn.cpp
+extern int g_split_cols;            // host/gcn.cpp
 extern int g_mask_side;             // host/gcn.cpp
 extern int g_xstream_tn_lds;        // k_gemm.hip
 extern int g_eval_ax;               // host/gcn.cpp
@@ -45,6 +46,9 @@ struct pgcn_gcn {
 };
 struct pgcn_dataset {
   GCNData d;
+};
+struct pgcn_loopback {
+  std::shared_ptr<LoopbackGroup> g;
 };
 
 namespace {
@@ -348,6 +352,51 @@ int pgcn_gcn_create_dist(const pgcn_params *p, const pgcn_data *d, int device, i
   });
 }
 
+int pgcn_loopback_create(int world, pgcn_loopback **out) {
+  return guarded([&] {
+    PGCN_CHECK(out, PGCN_E_INVALID, "loopback_create args");
+    auto h = std::make_unique<pgcn_loopback>();
+    h->g = std::make_shared<LoopbackGroup>(world);
+    *out = h.release();
+  });
+}
+
+int pgcn_loopback_destroy(pgcn_loopback *g) {
+  delete g;  // engines keep the group alive until they are destroyed
+  return PGCN_OK;
+}
+
+int pgcn_gcn_create_loopback(const pgcn_params *p, const pgcn_data *d, int device, int rank,
+                             pgcn_loopback *group, pgcn_gcn **out) {
+  return guarded([&] {
+    PGCN_CHECK(p && d && out && group && group->g, PGCN_E_INVALID, "gcn_create_loopback args");
+    check_device();
+    GCNData data = to_data(d, p);
+    DistSpec ds;
+    ds.rank = rank;
+    ds.world = group->g->world();
+    ds.loopback = group->g;
+    auto h = std::make_unique<pgcn_gcn>();
+    h->g = std::make_unique<GCN>(to_params(p, d), to_adam(p), data, device, &ds);
+    *out = h.release();
+  });
+}
+
+long long pgcn_gcn_query(pgcn_gcn *g, const char *key) {
+  if (!g || !key) return PGCN_E_INVALID;
+  const GCN &e = *g->g;
+  const Comm *c = e.communicator();
+  if (!std::strcmp(key, "world")) return c ? c->world() : 1;
+  if (!std::strcmp(key, "rank")) return c ? c->rank() : 0;
+  if (!std::strcmp(key, "comm")) return c ? (!std::strcmp(c->kind(), "rccl") ? 1 : 2) : 0;
+  if (!std::strcmp(key, "reassociated")) return e.reassociated() ? 1 : 0;
+  if (!std::strcmp(key, "graph_symmetric")) return e.symmetric() ? 1 : 0;
+  if (!std::strcmp(key, "graphsum_lds")) return e.graphsum_lds() ? 1 : 0;
+  if (!std::strcmp(key, "epochs")) return e.epochs_run();
+  if (!std::strcmp(key, "eval_ax_us")) return (long long)(e.eval_ax_build_ms() * 1000.0f);
+  return PGCN_E_INVALID;
+}
+
 int pgcn_gcn_destroy(pgcn_gcn *g) {
   delete g;
   return PGCN_OK;
@@ -376,10 +425,14 @@ int pgcn_gcn_sync(pgcn_gcn *g) {
   return guarded([&] { g->g->sync(); });
 }
 int pgcn_gcn_results(pgcn_gcn *g, int n, float *host_out) {
-  return guarded([&] {
+  int rows = 0;
+  const int st = guarded([&] {
+    PGCN_CHECK(n >= 0 && (n == 0 || host_out), PGCN_E_INVALID, "gcn_results args");
     auto r = g->g->results(n);
     std::memcpy(host_out, r.data(), r.size() * sizeof(float));
+    rows = (int)(r.size() / 4);
   });
+  return st == PGCN_OK ? rows : st;
 }
 int pgcn_gcn_run(pgcn_gcn *g, int verbose) {
   return guarded([&] { g->g->run(verbose != 0); });
@@ -497,6 +550,7 @@ int pgcn_debug_set(const char *key, int value) {
   else if (!std::strcmp(key, "gemm_variant")) pgcn::g_gemm_variant = value;
   else if (!std::strcmp(key, "train_ahead")) pgcn::g_train_ahead = value;
   else if (!std::strcmp(key, "split_rows")) pgcn::g_split_rows = value;
+  else if (!std::strcmp(key, "split_cols")) pgcn::g_split_cols = value;
   else if (!std::strcmp(key, "mask_side")) pgcn::g_mask_side = value;
   else if (!std::strcmp(key, "xstream_tn_lds")) pgcn::g_xstream_tn_lds = value;
   else if (!std::strcmp(key, "eval_ax")) pgcn::g_eval_ax = value;

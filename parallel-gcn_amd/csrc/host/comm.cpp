@@ -4,10 +4,14 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <mutex>
 #include <string>
 
 #include "../common.hpp"
+#include "../kernels.hpp"
 #include "graph.hpp"
 
 namespace pgcn {
@@ -130,7 +134,7 @@ void Comm::unique_id(void *out128) {
   std::memcpy(out128, &id, sizeof id);
 }
 
-Comm::Comm(int rank, int world, const void *unique_id_128) : rank_(rank), world_(world) {
+RcclComm::RcclComm(int rank, int world, const void *unique_id_128) : Comm(rank, world) {
   ncclUniqueId id;
   std::memcpy(&id, unique_id_128, sizeof id);
   ncclComm_t c;
@@ -138,18 +142,118 @@ Comm::Comm(int rank, int world, const void *unique_id_128) : rank_(rank), world_
   comm_ = c;
 }
 
-Comm::~Comm() {
+RcclComm::~RcclComm() {
   if (comm_) (void)ncclCommDestroy(static_cast<ncclComm_t>(comm_));
 }
 
-void Comm::allreduce_sum(float *buf, size_t n, hipStream_t s) {
+void RcclComm::allreduce_sum(float *buf, size_t n, hipStream_t s) {
   if (world_ == 1 || n == 0) return;
   PGCN_NCCL(ncclAllReduce(buf, buf, n, ncclFloat32, ncclSum, static_cast<ncclComm_t>(comm_), s));
 }
 
-void Comm::reduce_scatter_sum(const float *send, float *recv, size_t recvcount, hipStream_t s) {
+void RcclComm::reduce_scatter_sum(const float *send, float *recv, size_t recvcount,
+                                  hipStream_t s) {
   PGCN_NCCL(ncclReduceScatter(send, recv, recvcount, ncclFloat32, ncclSum,
                               static_cast<ncclComm_t>(comm_), s));
+}
+
+// ------------------------------------------------------------------------------------------
+// Loopback (in-process) collectives
+// ------------------------------------------------------------------------------------------
+struct LoopbackGroup::Impl {
+  std::mutex mu;
+  std::condition_variable cv;
+  long long generation = 0;  // completed rendezvous
+  int arrived = 0;
+  std::vector<const void *> ptrs;
+  std::vector<hipEvent_t> evs;
+  std::vector<const void *> out_ptrs;  // the last completed rendezvous
+  std::vector<hipEvent_t> out_evs;
+};
+
+LoopbackGroup::LoopbackGroup(int world) : impl_(std::make_shared<Impl>()), world_(world) {
+  PGCN_CHECK(world >= 1 && world <= kLoopbackMaxRanks, PGCN_E_INVALID,
+             "loopback group: world must be in [1, 16]");
+  impl_->ptrs.assign((size_t)world, nullptr);
+  impl_->evs.assign((size_t)world, nullptr);
+}
+
+void LoopbackGroup::exchange(int rank, const void *ptr, hipEvent_t ev,
+                             std::vector<const void *> *ptrs, std::vector<hipEvent_t> *evs) {
+  Impl &m = *impl_;
+  std::unique_lock<std::mutex> lk(m.mu);
+  const long long gen = m.generation;
+  m.ptrs[(size_t)rank] = ptr;
+  m.evs[(size_t)rank] = ev;
+  if (++m.arrived == world_) {
+    m.out_ptrs = m.ptrs;
+    m.out_evs = m.evs;
+    m.arrived = 0;
+    m.generation++;
+    m.cv.notify_all();
+  } else {
+    const bool ok = m.cv.wait_for(lk, std::chrono::duration<double>(timeout_s),
+                                  [&] { return m.generation != gen; });
+    if (!ok) {
+      m.arrived--;
+      throw Error(PGCN_E_COMM, "loopback collective: peers did not arrive (rank " +
+                                   std::to_string(rank) + ")");
+    }
+  }
+  // the next rendezvous cannot complete before this rank arrives again, so out_* is stable
+  *ptrs = m.out_ptrs;
+  *evs = m.out_evs;
+}
+
+LoopbackComm::LoopbackComm(int rank, std::shared_ptr<LoopbackGroup> group)
+    : Comm(rank, group->world()), group_(std::move(group)) {
+  PGCN_CHECK(rank >= 0 && rank < world_, PGCN_E_INVALID, "loopback comm: rank");
+  PGCN_HIP(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
+  PGCN_HIP(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
+}
+
+LoopbackComm::~LoopbackComm() {
+  if (ready_) (void)hipEventDestroy(ready_);
+  if (done_) (void)hipEventDestroy(done_);
+  if (tmp_) (void)hipFree(tmp_);
+}
+
+// dst[0, count) = sum over ranks q (in rank order) of send_q[src_offset, src_offset + count)
+void LoopbackComm::collective(const float *send, float *dst, size_t count, size_t src_offset,
+                              hipStream_t s) {
+  std::vector<const void *> ptrs;
+  std::vector<hipEvent_t> evs;
+  PGCN_HIP(hipEventRecord(ready_, s));  // this rank's send buffer is complete
+  group_->exchange(rank_, send, ready_, &ptrs, &evs);
+  LoopbackSrcs srcs{};
+  for (int q = 0; q < world_; q++) {
+    if (q != rank_) PGCN_HIP(hipStreamWaitEvent(s, evs[(size_t)q], 0));
+    srcs.p[q] = static_cast<const float *>(ptrs[(size_t)q]) + src_offset;
+  }
+  srcs.n = world_;
+  launch_loopback_sum(srcs, dst, count, s);
+  PGCN_HIP(hipEventRecord(done_, s));  // this rank has read every peer's buffer
+  group_->exchange(rank_, nullptr, done_, &ptrs, &evs);
+  for (int q = 0; q < world_; q++)
+    if (q != rank_) PGCN_HIP(hipStreamWaitEvent(s, evs[(size_t)q], 0));
+}
+
+void LoopbackComm::allreduce_sum(float *buf, size_t n, hipStream_t s) {
+  if (world_ == 1 || n == 0) return;
+  if (tmp_n_ < n) {
+    if (tmp_) PGCN_HIP(hipFree(tmp_));
+    tmp_ = nullptr;
+    PGCN_HIP(hipMalloc(&tmp_, n * sizeof(float)));
+    tmp_n_ = n;
+  }
+  // every peer has read `buf` once collective() returns on the stream: then overwrite it
+  collective(buf, tmp_, n, 0, s);
+  PGCN_HIP(hipMemcpyAsync(buf, tmp_, n * sizeof(float), hipMemcpyDeviceToDevice, s));
+}
+
+void LoopbackComm::reduce_scatter_sum(const float *send, float *recv, size_t recvcount,
+                                      hipStream_t s) {
+  collective(send, recv, recvcount, (size_t)rank_ * recvcount, s);
 }
 
 }  // namespace pgcn

@@ -9,6 +9,7 @@
 // reduce-scatter per GraphSum call.  Weight gradients and loss scalars are all-reduced.
 #pragma once
 #include <cstddef>
+#include <memory>
 #include <vector>
 
 #include <hip/hip_runtime.h>
@@ -46,21 +47,79 @@ void partition_subgraph(const Partition &part, int n, const int *indptr, const i
                         std::vector<int> *sub_indptr, std::vector<int> *sub_indices,
                         std::vector<float> *sub_vals);
 
+// The collectives the edge-cut engine needs, stream-ordered like RCCL's: a call enqueues its
+// work on `s` and returns; buffers may be reused by later work on `s`.
 class Comm {
  public:
-  Comm(int rank, int world, const void *unique_id_128);
-  ~Comm();
+  Comm(int rank, int world) : rank_(rank), world_(world) {}
+  virtual ~Comm() = default;
   Comm(const Comm &) = delete;
   Comm &operator=(const Comm &) = delete;
   int rank() const { return rank_; }
   int world() const { return world_; }
-  void allreduce_sum(float *buf, size_t n, hipStream_t s);
-  void reduce_scatter_sum(const float *send, float *recv, size_t recvcount, hipStream_t s);
-  static void unique_id(void *out128);
+  virtual void allreduce_sum(float *buf, size_t n, hipStream_t s) = 0;
+  // recv[0, recvcount) = sum over ranks of send[rank * recvcount, (rank + 1) * recvcount)
+  virtual void reduce_scatter_sum(const float *send, float *recv, size_t recvcount,
+                                  hipStream_t s) = 0;
+  virtual const char *kind() const = 0;
+  static void unique_id(void *out128);  // RCCL unique id (rank 0 creates, all share)
+
+ protected:
+  int rank_, world_;
+};
+
+// One process per GPU over RCCL (xGMI on one node).
+class RcclComm : public Comm {
+ public:
+  RcclComm(int rank, int world, const void *unique_id_128);
+  ~RcclComm() override;
+  void allreduce_sum(float *buf, size_t n, hipStream_t s) override;
+  void reduce_scatter_sum(const float *send, float *recv, size_t recvcount,
+                          hipStream_t s) override;
+  const char *kind() const override { return "rccl"; }
 
  private:
-  int rank_, world_;
   void *comm_ = nullptr;  // ncclComm_t
+};
+
+// In-process "fake RCCL" (SURVEY.md §4): `world` engines in one process on one device, each
+// driven by its own host thread.  A collective is a host rendezvous of the ranks (each posts
+// its buffer and an event recorded after its producer), then every rank's stream waits for
+// all peers' events and sums the peers' buffers in rank order with a device kernel, then a
+// second rendezvous on "read done" events before any rank may overwrite its send buffer.
+// Same stream semantics as RCCL, so the edge-cut engine runs unchanged at world 2, 4, ... on
+// one GPU (RCCL itself refuses two ranks on one device).
+class LoopbackGroup {
+ public:
+  explicit LoopbackGroup(int world);
+  int world() const { return world_; }
+  // rendezvous `phase` of the current collective: publish (ptr, ev) of `rank`, wait for all
+  // ranks, return every rank's (ptr, ev).  Throws PGCN_E_COMM after `timeout_s` seconds.
+  void exchange(int rank, const void *ptr, hipEvent_t ev, std::vector<const void *> *ptrs,
+                std::vector<hipEvent_t> *evs);
+  double timeout_s = 60.0;
+
+ private:
+  struct Impl;
+  std::shared_ptr<Impl> impl_;
+  int world_;
+};
+
+class LoopbackComm : public Comm {
+ public:
+  LoopbackComm(int rank, std::shared_ptr<LoopbackGroup> group);
+  ~LoopbackComm() override;
+  void allreduce_sum(float *buf, size_t n, hipStream_t s) override;
+  void reduce_scatter_sum(const float *send, float *recv, size_t recvcount,
+                          hipStream_t s) override;
+  const char *kind() const override { return "loopback"; }
+
+ private:
+  void collective(const float *send, float *dst, size_t count, size_t src_offset, hipStream_t s);
+  std::shared_ptr<LoopbackGroup> group_;
+  hipEvent_t ready_ = nullptr, done_ = nullptr;
+  float *tmp_ = nullptr;  // all-reduce result before it overwrites `buf`
+  size_t tmp_n_ = 0;
 };
 
 }  // namespace pgcn

@@ -22,8 +22,14 @@ int g_eval_ax = 1;
 // "epoch_graph" (read per epoch_async): replay a captured per-epoch hipGraph when eligible;
 int g_epoch_graph = 0;  // measured no faster than eager launches (r01: GPU-bound epochs)
 // "split_rows" (read at each split switch): the output layer's GraphSum forward computes only
-// the current split's labelled rows
-int g_split_rows = 1;
+// the current split's labelled rows.  Off by default: the reference's forward produces the
+// logits of every row, and so does the default engine (r02); on, rows outside the split keep
+// stale logits (get_var refuses them)
+int g_split_rows = 0;
+// "split_cols" (read at each split switch): the output layer's GraphSum backward keeps only the
+// edges from the training split's columns.  The loss gradient is exactly zero on every other
+// row, so the skipped terms are exact zeros: in.grad is the full gradient of every row
+int g_split_cols = 1;
 
 // ------------------------------------------------------------------------------------------
 // Adam (src/optim.cu:7-95; hpdga optim.cpp:16-35)
@@ -130,7 +136,10 @@ GCN::GCN(const GCNParams &params_, const AdamParams &adam, const GCNData &data, 
   part = make_partition(params.num_nodes, data.graph.indptr.data(), world, rank,
                         dist ? kRsChunks : 1);
   if (dist) {  // the edge-cut path (also at world == 1, which exercises it on one GPU)
-    comm = std::make_unique<Comm>(rank, world, dist->unique_id);
+    if (dist->loopback)
+      comm = std::make_unique<LoopbackComm>(rank, dist->loopback);
+    else
+      comm = std::make_unique<RcclComm>(rank, world, dist->unique_id);
     ctx.comm = comm.get();
     comm_stream = Stream::create(hi_prio);
     ctx.comm_stream = comm_stream.get();
@@ -258,6 +267,7 @@ void GCN::init_dropout_rng(const GCNData &data, long long glorot_draws) {
 
 void GCN::build(const GCNData &data) {
   const int N = params.num_nodes;
+  graph_symmetric = csr_symmetric(N, data.graph.indptr.data(), data.graph.indices.data());
   // adjacency
   if (comm) {
     // one column block per reduce-scatter chunk (rows in chunk-major padded order,
@@ -305,14 +315,20 @@ void GCN::build(const GCNData &data) {
   // eval_ax: Â X once (16 columns per d = 16 GraphSum; the last chunk overlaps the one
   // before it so it never reads past a row), single GPU, dense X (eval's (Â X) W1 runs on the
   // X-stream kernel for hidden <= 16, the MFMA GEMM for wider first layers)
+  // (its device time is kept in ax_build_ms: bench.py amortises it over the reference's
+  // 100-epoch run)
+  Event ax0 = Event::create(true), ax1 = Event::create(true);
   if (g_eval_ax && !comm && graph && feats.dense && feats.cols >= 16) {
     feats.ax.allocate(feats.x.size());
     feats.ax.zero();
+    ax0.record(stream.get());
     for (int c0 = 0; c0 < feats.cols; c0 += 16) {
       const int c = std::min(c0, feats.ldx - 16);
       graph->graphsum(feats.x.get() + c, feats.ldx, feats.ax.get() + c, feats.ldx, 16, stream.get());
     }
+    ax1.record(stream.get());
     stream.sync();
+    PGCN_HIP(hipEventElapsedTime(&ax_build_ms, ax0.get(), ax1.get()));
   }
   // the same for the edge-cut engine: per 16-column chunk of X, every row chunk's partial
   // sums from this rank's columns reduce-scattered exactly as GraphSum::run does (this rank
@@ -322,6 +338,7 @@ void GCN::build(const GCNData &data) {
     feats.ax.allocate(feats.x.size());
     feats.ax.zero();
     DeviceBuffer<float> partial((size_t)part.world * h * 16), own((size_t)nk * h * 16);
+    ax0.record(stream.get());
     for (int c0 = 0; c0 < feats.cols; c0 += 16) {
       const int c = std::min(c0, feats.ldx - 16);
       for (int k = 0; k < nk; k++) {
@@ -334,7 +351,9 @@ void GCN::build(const GCNData &data) {
                                 sizeof(float) * 16, sizeof(float) * 16, (size_t)part.local_rows(),
                                 hipMemcpyDeviceToDevice, stream.get()));
     }
+    ax1.record(stream.get());
     stream.sync();
+    PGCN_HIP(hipEventElapsedTime(&ax_build_ms, ax0.get(), ax1.get()));
   }
   // truth per split for this rank's rows, padded with -1 (set_truth, src/gcn.cu:204-226)
   const int first = part.first(), rows = part.local_rows(), prow = part.maxrows;
@@ -466,15 +485,20 @@ void GCN::insert_last_layer() {
   auto drop = std::make_unique<Dropout>(prev, params.dropouts.back(), rngs[(size_t)L - 1], &ctx);
   dropouts_.push_back(drop.get());
   modules.push_back(std::move(drop));
-  if (params.reassociate_last && hl < C) {
+  if (params.reassociate_last && hl < C && graph_symmetric) {
     // out = Â (H W) computed as (Â H) W: the same product (Â is symmetric, so the backward
     // Â dOut W^T = Â (dOut W^T) and W.grad = H^T Â dOut = (Â H)^T dOut also match), but the
     // GraphSum gathers rows of width hl instead of C.  Only the fp32 rounding order differs.
+    // A non-symmetric pattern (directed edge list) keeps the reference's module order: there
+    // (Â H)^T dOut = H^T Â^T dOut is not the reference's H^T Â dOut (hpdga module.cpp:98-111).
+    reassociated_ = true;
     auto z = std::make_shared<Variable>(prow, hl, true, round_up4(hl));
+    restricted_vars.push_back((int)variables.size());
     variables.push_back(z);
     variables.push_back(weights.back());
     modules.push_back(std::make_unique<GraphSum>(prev, z, graph.get(), hl, &ctx, true));
     auto out = std::make_shared<Variable>(prow, C, true, round_up4(C));
+    restricted_vars.push_back((int)variables.size());
     variables.push_back(out);
     auto mm = std::make_unique<Matmul>(z, weights.back(), out, part.local_rows(), hl, C, &ctx);
     mm->last_layer = true;
@@ -496,6 +520,7 @@ void GCN::insert_last_layer() {
   modules.push_back(std::make_unique<Matmul>(prev, weights.back(), var1, part.local_rows(), hl,
                                              C, &ctx));
   auto out = std::make_shared<Variable>(prow, C, true, round_up4(C));
+  restricted_vars.push_back((int)variables.size());
   variables.push_back(out);
   modules.push_back(std::make_unique<GraphSum>(var1, out, graph.get(), C, &ctx, true));
   modules.push_back(std::make_unique<CrossEntropyLoss>(out, C, &ctx));
@@ -547,16 +572,17 @@ void GCN::set_split(int split) {
     }
   }
   ctx.chunk_col_graphs.clear();
-  if (g_split_rows && comm && !chunk_graphs.empty() && split == 1 &&
+  if (g_split_cols && comm && !chunk_graphs.empty() && split == 1 &&
       !split_rows_host[1].empty()) {  // backward follows training
     if (chunk_col_graphs.empty())
       for (auto &gk : chunk_graphs) chunk_col_graphs.push_back(gk->col_subset(split_rows_host[1]));
     for (auto &cg : chunk_col_graphs) ctx.chunk_col_graphs.push_back(cg.get());
   }
-  if (g_split_rows && !comm && graph && split == 1) {  // backward only follows training
+  if (g_split_cols && !comm && graph && split == 1) {  // backward only follows training
     if (!split_colgraphs[split]) split_colgraphs[split] = graph->col_subset(split_rows_host[split]);
     ctx.split_colgraph = split_colgraphs[split].get();
   }
+  out_restricted = ctx.split_graph != nullptr || !ctx.chunk_split_graphs.empty();
   // compact output layer: with the row restriction on the reassociated output layer
   const int n_s = (int)split_rows_host[split].size();
   if (ctx.split_graph && ctx.compact_z && n_s > 0) {
@@ -757,6 +783,11 @@ void GCN::run(bool verbose) {
   }
 }
 
+bool GCN::graphsum_lds() const {
+  if (graph) return graph->uses_lds(16);
+  return !chunk_graphs.empty() && chunk_graphs.front()->uses_lds(16);
+}
+
 std::vector<float> GCN::get_var(int idx, int which) {
   sync();
   PGCN_CHECK(idx >= 0 && idx < (int)variables.size(), PGCN_E_INVALID, "variable index");
@@ -785,6 +816,12 @@ std::vector<float> GCN::get_var(int idx, int which) {
     }
     return x;
   }
+  // the output-layer row restriction (split_rows) leaves these rows stale or unwritten
+  PGCN_CHECK(!out_restricted || std::find(restricted_vars.begin(), restricted_vars.end(), idx) ==
+                                    restricted_vars.end(),
+             PGCN_E_INVALID,
+             "get_var: the output layer ran restricted to the split's rows (split_rows on); its "
+             "other rows are stale");
   const auto &v = variables[(size_t)idx];
   std::vector<float> out = v->to_host(which);
   const bool node_var = v->rows == part.maxrows &&

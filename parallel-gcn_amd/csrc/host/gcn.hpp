@@ -69,7 +69,9 @@ class Adam {
 
 struct DistSpec {
   int rank = 0, world = 1;
-  const void *unique_id = nullptr;  // 128 bytes
+  const void *unique_id = nullptr;  // 128 bytes (RCCL)
+  // in-process ranks on one device (LoopbackComm) instead of RCCL; world = group->world()
+  std::shared_ptr<LoopbackGroup> loopback;
 };
 
 class GCN {
@@ -90,6 +92,15 @@ class GCN {
   void profile_read(double *ms, long long *calls, double *bytes);
   const Partition &partition() const { return part; }
   const GCNParams &get_params() const { return params; }
+  const Comm *communicator() const { return comm.get(); }
+  bool symmetric() const { return graph_symmetric; }
+  long long epochs_run() const { return epoch_count; }
+  // device time of the Â X precompute at build (eval_ax; 0 when off)
+  float eval_ax_build_ms() const { return ax_build_ms; }
+  // GraphSum calls of width 16 take the LDS-staged kernel (large tables)
+  bool graphsum_lds() const;
+  // the output layer runs as (Â H) W (reassociate_last requested, hidden < classes, Â symmetric)
+  bool reassociated() const { return reassociated_; }
 
  private:
   void build(const GCNData &data);
@@ -133,6 +144,9 @@ class GCN {
   DeviceBuffer<int> truth_compact[4];                // the split's labels, compact row order
   std::unique_ptr<Variable> compact_z, compact_out;  // compact output layer (ModuleContext)
   long long nnz_x_global = 0;
+  // Â equals its transpose (csr_symmetric at build): the reassociated output layer's
+  // W.grad = (Â H)^T dOut equals the reference's H^T Â dOut only then
+  bool graph_symmetric = false;
   std::vector<int> feat_indptr_global;  // for the input dropout ranges
 
   std::vector<shared_ptr<Variable>> variables;
@@ -150,6 +164,12 @@ class GCN {
   int ring_cap = 1024;
   long long epoch_count = 0;
   bool last_forward_training = false;
+  bool reassociated_ = false;
+  float ax_build_ms = 0.0f;
+  // the last forward ran the output layer over the split's rows only (split_rows): the
+  // variables in restricted_vars hold stale rows
+  bool out_restricted = false;
+  std::vector<int> restricted_vars;
 
   // Per-epoch hipGraph: epoch_async() replays one captured
   // train_epoch + eval(2).  Everything that changes between epochs lives on the device:

@@ -1,6 +1,8 @@
 // parallel-gcn_amd/csrc/host/graph.cpp
 #include "graph.hpp"
 
+#include <atomic>
+
 #include <algorithm>
 #include <cmath>
 #include <functional>
@@ -48,6 +50,41 @@ std::vector<float> graph_coefs(int n, const int *indptr, const int *indices) {
     }
   });
   return v;
+}
+
+namespace {
+inline uint64_t mix64(uint64_t x) {  // splitmix64 finaliser
+  x += 0x9e3779b97f4a7c15ull;
+  x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+  x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+  return x ^ (x >> 31);
+}
+}  // namespace
+
+bool csr_symmetric(int n, const int *indptr, const int *indices) {
+  const int nt = 16;
+  std::vector<uint64_t> acc((size_t)nt * 4, 0);
+  std::atomic<int> slot{0};
+  parallel_for(n, [&](long long b, long long e) {
+    const int t = slot++;
+    uint64_t f0 = 0, f1 = 0, r0 = 0, r1 = 0;
+    for (long long i = b; i < e; i++)
+      for (int k = indptr[i]; k < indptr[i + 1]; k++) {
+        const uint64_t a = (uint64_t)(uint32_t)i, c = (uint64_t)(uint32_t)indices[k];
+        f0 += mix64(a << 32 | c);
+        f1 += mix64((a << 32 | c) ^ 0x5851f42d4c957f2dull);
+        r0 += mix64(c << 32 | a);
+        r1 += mix64((c << 32 | a) ^ 0x5851f42d4c957f2dull);
+      }
+    acc[(size_t)t * 4] = f0;
+    acc[(size_t)t * 4 + 1] = f1;
+    acc[(size_t)t * 4 + 2] = r0;
+    acc[(size_t)t * 4 + 3] = r1;
+  }, nt);
+  uint64_t s[4] = {0, 0, 0, 0};
+  for (int t = 0; t < nt; t++)
+    for (int q = 0; q < 4; q++) s[q] += acc[(size_t)t * 4 + q];
+  return s[0] == s[2] && s[1] == s[3];
 }
 
 std::vector<float> degree_scales(int n, const int *indptr) {
@@ -867,13 +904,17 @@ void DevGraph::build_lds() {
   lds_ = std::move(L);
 }
 
+bool DevGraph::uses_lds(int dim) const {
+  return (dim == 16 || (dim > 16 && g_graphsum_lds_wide)) && g_graphsum_lds &&
+         !h_row_scale_.empty() && !g_graphsum_force_plain && (double)n_cols_ * 64.0 > kL2Budget;
+}
+
 void DevGraph::graphsum(const float *in, int ld_in, float *out, int ld_out, int dim,
                         hipStream_t s, bool compact_in) {
   const int *col_map = compact_in ? nullptr : col_map_.get();
   PGCN_CHECK(ld_in % 4 == 0 && ld_out % 4 == 0 && ld_in >= dim && ld_out >= dim,
              PGCN_E_INVALID, "graphsum: leading dims must be multiples of 4 and >= dim");
-  if ((dim == 16 || (dim > 16 && g_graphsum_lds_wide)) && g_graphsum_lds &&
-      !h_row_scale_.empty() && !g_graphsum_force_plain && (double)n_cols_ * 64.0 > kL2Budget) {
+  if (uses_lds(dim)) {
     if (!lds_) build_lds();
     // wider rows: one LDS pass per 16 columns (the last pass overlaps the one before it so it
     // stays inside both leading dims; overlapped columns are recomputed to the same bits).

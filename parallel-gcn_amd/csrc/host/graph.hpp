@@ -32,6 +32,11 @@ std::vector<float> graph_coefs(int n, const int *indptr, const int *indices);
 void parallel_for(long long n, const std::function<void(long long, long long)> &f,
                   int threads = 0, long long min_parallel = 100000);
 
+// True when the pattern equals its transpose, duplicates counted (the multiset of (i, j) is
+// the multiset of (j, i)): Â is then symmetric.  Two independent 64-bit hash sums over the
+// slots, O(nnz) on the host threads.
+bool csr_symmetric(int n, const int *indptr, const int *indices);
+
 // s[i] = 1/sqrt(deg_i) with deg = row length of the (symmetric) CSR: Â = D^-1/2 A D^-1/2.
 std::vector<float> degree_scales(int n, const int *indptr);
 
@@ -68,6 +73,8 @@ class DevGraph {
   // compact_in (column subsets): `in` holds the subset's columns as its rows (no gather)
   void graphsum(const float *in, int ld_in, float *out, int ld_out, int dim, hipStream_t s,
                 bool compact_in = false);
+  // graphsum() of this width runs the LDS-staged kernel (k_graphsum_lds)
+  bool uses_lds(int dim) const;
   // bytes the kernel must move at minimum (SURVEY.md §8d formula, per call)
   double algorithmic_bytes(int dim) const;
   // schedule statistics (for tests / reports)

@@ -155,6 +155,24 @@ void launch_scatter_rows(const float *src, const int *rows, int n, int ld, float
                      reinterpret_cast<float4 *>(out));
 }
 
+// loopback reduce-scatter / all-reduce: one element per thread, peers summed in rank order
+// (deterministic; RCCL's own order is unspecified)
+__global__ __launch_bounds__(256) void k_loopback_sum(LoopbackSrcs srcs, float *__restrict__ dst,
+                                                      size_t count) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  float acc = srcs.p[0][i];
+  for (int q = 1; q < srcs.n; q++) acc += srcs.p[q][i];
+  dst[i] = acc;
+}
+
+void launch_loopback_sum(const LoopbackSrcs &srcs, float *dst, size_t count, hipStream_t s) {
+  PGCN_CHECK(srcs.n >= 1 && srcs.n <= kLoopbackMaxRanks, PGCN_E_INVALID, "loopback_sum: ranks");
+  if (count == 0) return;
+  hipLaunchKernelGGL(k_loopback_sum, dim3((unsigned)ceil_div((long long)count, 256)), dim3(256), 0,
+                     s, srcs, dst, count);
+}
+
 // out[r] = src[rows[r]] (float4s): the input of a column-subset GraphSum on the plain path
 __global__ __launch_bounds__(256) void k_gather_rows(const float4 *__restrict__ src,
                                                      const int *__restrict__ rows, int n, int ld4,

@@ -72,6 +72,13 @@ void launch_xstream_nn(int M, int N, int K, const float *A, int lda, const float
 // out[r][0:ld] = src[rows[r]][0:ld]  (ld % 4 == 0)
 void launch_gather_rows(const float *src, const int *rows, int n, int ld, float *out,
                         hipStream_t s);
+// loopback collectives (host/comm.cpp): dst[i] = sum over q < n (in order) of p[q][i]
+constexpr int kLoopbackMaxRanks = 16;
+struct LoopbackSrcs {
+  const float *p[kLoopbackMaxRanks];
+  int n;
+};
+void launch_loopback_sum(const LoopbackSrcs &srcs, float *dst, size_t count, hipStream_t s);
 // out[rows[r]][0:ld] = src[r][0:ld]  (ld % 4 == 0)
 void launch_scatter_rows(const float *src, const int *rows, int n, int ld, float *out,
                          hipStream_t s);

@@ -11,7 +11,7 @@ step() {  # name, seconds, command...
 }
 [ -n "${SKIP_TESTS:-}" ] || step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" || exit $?
 if [ -z "${SKIP_TESTS:-}" ]; then
-  step pytest_gpu 900 python3 -m pytest tests -m gpu -q -x ${PYTEST_ARGS:-} || exit $?
+  step pytest_gpu 1000 python3 -u -m pytest tests -m gpu -v -x --timeout 240 --timeout-method thread ${PYTEST_ARGS:-} || exit $?
 fi
 step bench 600 python3 bench.py ${BENCH_ARGS:-} || exit $?
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null

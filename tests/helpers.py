@@ -3,6 +3,7 @@
 The oracle (oracle/liboracle.so, oracle/_ref/libhpdga_ref.so) is test infrastructure: it is
 loaded here, by __graft_entry__.smoke() and by bench.py's cpu_baseline leg only.
 """
+import contextlib
 import ctypes
 import gzip
 import importlib.util
@@ -189,3 +190,36 @@ def parse_line(line):
         k, v = tok.split("=")
         out[k] = float(v)
     return out
+
+
+# --------------------------------------------------------------------------- engine knobs
+# pgcn_debug_set defaults of the engine (parallel-gcn_amd/csrc/host/gcn.cpp)
+ENGINE_DEFAULTS = {"train_ahead": 1, "split_rows": 0, "split_cols": 1, "eval_ax": 1,
+                   "epoch_graph": 0, "mask_side": 0}
+
+
+@contextlib.contextmanager
+def knobs(pg, **kw):
+    """Sets engine knobs for the engines built inside the block, restores the defaults."""
+    try:
+        for k, v in kw.items():
+            assert pg.lib.pgcn_debug_set(k.encode(), int(v)) == 0, k
+        yield
+    finally:
+        for k in kw:
+            pg.lib.pgcn_debug_set(k.encode(), ENGINE_DEFAULTS.get(k, 0))
+
+
+def split_counts(ds):
+    lab, sp = np.asarray(ds.label), np.asarray(ds.split)
+    return {s: int(((sp == s) & (lab >= 0)).sum()) for s in (1, 2, 3)}
+
+
+def assert_line_close(ours, want, counts, rtol=1e-4, what=""):
+    """One epoch line (train_loss, train_acc, val_loss, val_acc) against the oracle's: losses
+    within rtol (the north star's 1e-4), accuracies within max(2 rows, 0.5 %) of the split."""
+    for k in (0, 2):
+        assert abs(ours[k] - want[k]) <= rtol * abs(want[k]), (what, k, ours, want)
+    for k, sp in ((1, 1), (3, 2)):
+        assert abs(ours[k] - want[k]) * counts[sp] <= max(2.0, 0.005 * counts[sp]) + 1e-3, \
+            (what, k, ours, want)

@@ -24,22 +24,17 @@ def _counts(ds):
     return {s: int(((sp == s) & (lab >= 0)).sum()) for s in (1, 2, 3)}
 
 
-def _run(loaded, pgcn, reassociate):
-    # the reference module order is compared tensor by tensor (every row of every variable):
-    # the output-layer row restriction (default on) leaves rows outside the split stale, so it
-    # is off here; the default engine (reassociated, restriction on) is compared on its lines
-    pgcn.lib.pgcn_debug_set(b"split_rows", 1 if reassociate else 0)
-    try:
-        return _run_all(loaded, pgcn, reassociate)
-    finally:
-        pgcn.lib.pgcn_debug_set(b"split_rows", 1)
-
-
-def _run_all(loaded, pgcn, reassociate):
+def _run_all(loaded, pgcn):
+    """The default engine (reassociate_last requested, output layer over every row).  With
+    hidden 16 above the class count of cora (7), citeseer (6) and pubmed (3) the output layer
+    keeps the reference's module order Â (H W2), so every intermediate is comparable tensor
+    by tensor; the reassociated order is covered by test_reassociated_* below and by
+    tests/test_gpu_parity_large.py."""
     out = {}
     for name in DATASETS:
         ds = loaded[name]
-        g = pgcn.GCN(pgcn.make_params(ds, reassociate_last=reassociate), ds)
+        g = pgcn.GCN(pgcn.make_params(ds), ds)
+        assert g.query("reassociated") == 0
         e1 = {}
         lines = []
         for e in range(100):
@@ -60,20 +55,12 @@ def _run_all(loaded, pgcn, reassociate):
 
 @pytest.fixture(scope="module")
 def engine_runs(loaded, pgcn):
-    """The reference's module order (Â (H W2)): every intermediate comparable."""
-    return _run(loaded, pgcn, False)
+    return _run_all(loaded, pgcn)
 
 
-@pytest.fixture(scope="module")
-def engine_runs_fast(loaded, pgcn):
-    """The default engine: output layer reassociated to (Â H) W2."""
-    return _run(loaded, pgcn, True)
-
-
-@pytest.mark.parametrize("fast", [False, True])
 @pytest.mark.parametrize("name", DATASETS)
-def test_epoch_lines(engine_runs, engine_runs_fast, name, fast):
-    runs = engine_runs_fast if fast else engine_runs
+def test_epoch_lines(engine_runs, name):
+    runs = engine_runs
     gold = helpers.golden(name)["epoch_lines"].reshape(-1, 4)
     ours = runs[name]["lines"]
     cnt = runs[name]["counts"]
@@ -88,6 +75,49 @@ def test_epoch_lines(engine_runs, engine_runs_fast, name, fast):
     gt = helpers.golden(name)["test_scalars"]
     assert abs(tl - gt[0]) <= 1e-4 * abs(gt[0])
     assert abs(ta - gt[1]) * cnt[3] <= max(2.0, 0.005 * cnt[3]) + 1e-3
+
+
+@pytest.mark.parametrize("split_rows", [0, 1])
+def test_reassociated_output_layer_cora(loaded, pgcn, split_rows):
+    """hidden 4 < 7 classes: the output layer runs as (Â H) W2 (cora's pattern is symmetric),
+    with the output-layer row restriction on or off, against the oracle's reference order
+    Â (H W2) at 1e-4; full logits after eval match the oracle's when the restriction is off,
+    and get_var refuses them when it is on (their other rows are stale)."""
+    ds = loaded["cora"]
+    with helpers.knobs(pgcn, split_rows=split_rows):
+        g = pgcn.GCN(pgcn.make_params(ds, hidden_dims=(4,)), ds)
+        assert g.query("graph_symmetric") == 1 and g.query("reassociated") == 1
+        ref = helpers.OracleGCN(helpers.ds_dict(ds), hidden_dims=(4,))
+        cnt = _counts(ds)
+        for e in range(30):
+            ours = g.train_epoch() + g.eval(2)
+            want = ref.train_epoch() + ref.eval(2)
+            helpers.assert_line_close(ours, want, cnt, what=f"epoch {e}")
+        if split_rows:
+            with pytest.raises(pgcn.PgcnError):
+                g.get_var(6)
+        else:
+            np.testing.assert_allclose(g.get_var(6), ref.var(6), rtol=1e-4, atol=1e-5)
+        np.testing.assert_allclose(g.get_var(5), ref.var(5), rtol=1e-3, atol=1e-6)
+        g.close()
+
+
+def test_reassociation_off_for_directed_pattern(loaded, pgcn):
+    """A non-symmetric pattern (one edge redirected, row lengths kept): (Â H) W2 would give the
+    W2 gradient H^T Â^T dOut instead of the reference's H^T Â dOut (hpdga module.cpp:98-111),
+    so the engine keeps the reference order; its lines match the oracle on the same arrays."""
+    ds = pgcn.Dataset.synthetic(3000, 24, 9, 6000, 17)
+    ip = ds.graph_indptr
+    row = int(np.argmax(np.diff(ip)))  # a row with several neighbours
+    ds.graph_indices[ip[row] + 1] = (ds.graph_indices[ip[row] + 1] + 7) % ds.num_nodes
+    g = pgcn.GCN(pgcn.make_params(ds, hidden_dims=(4,)), ds)
+    assert g.query("graph_symmetric") == 0 and g.query("reassociated") == 0
+    ref = helpers.OracleGCN(helpers.ds_dict(ds), hidden_dims=(4,))
+    cnt = _counts(ds)
+    for e in range(10):
+        helpers.assert_line_close(g.train_epoch() + g.eval(2), ref.train_epoch() + ref.eval(2),
+                                  cnt, what=f"epoch {e}")
+    g.close()
 
 
 @pytest.mark.parametrize("name", ["cora", "citeseer"])
@@ -119,12 +149,17 @@ def test_epoch1_tensors(engine_runs, name):
 
 @pytest.mark.parametrize("name", DATASETS)
 def test_final_weights(engine_runs, name):
+    """Weights after 100 Adam epochs against the reference build's.  Adam's update is
+    m/(sqrt(v)+eps): a gradient entry near zero flips the sign of its few-ulp steps, so single
+    entries may drift by a few step sizes (lr = 0.01); the bulk must stay at fp32 noise."""
     gold = helpers.golden(name)
     for ours, ref in ((engine_runs[name]["w1"], gold["final_W1"]),
                       (engine_runs[name]["w2"], gold["final_W2"])):
         scale = np.abs(ref).max()
-        # 100 Adam epochs amplify fp32 reordering; the contract is the loss lines above
-        assert np.abs(ours - ref).max() <= 1e-2 * scale
+        err = np.abs(ours - ref)
+        assert err.max() <= 5e-3 * scale, err.max() / scale
+        assert np.median(err) <= 1e-4 * scale, np.median(err) / scale
+        assert np.mean(err <= 1e-3 * scale) >= 0.99, np.mean(err <= 1e-3 * scale)
 
 
 @pytest.mark.parametrize("name", ["cora", "pubmed_synth"])
@@ -169,16 +204,15 @@ def test_edge_cut_split_rows_matches_all_rows(loaded, pgcn, name):
     p = pgcn.make_params(ds)
     runs = []
     for on in (1, 0):
-        pgcn.lib.pgcn_debug_set(b"split_rows", on)
-        g = pgcn.GCN(p, ds, device=0, rank=0, world=1, unique_id=pgcn.comm_unique_id())
-        lines = [g.train_epoch() + g.eval(2) for _ in range(4)]
-        for _ in range(2):
-            g.epoch_async()
-        lines += [tuple(r) for r in g.results(2)]
-        lines.append(g.eval(3) + (0.0, 0.0))
-        runs.append((np.array(lines, np.float64), g.get_var(2)))
-        g.close()
-    pgcn.lib.pgcn_debug_set(b"split_rows", 1)
+        with helpers.knobs(pgcn, split_rows=on):
+            g = pgcn.GCN(p, ds, device=0, rank=0, world=1, unique_id=pgcn.comm_unique_id())
+            lines = [g.train_epoch() + g.eval(2) for _ in range(4)]
+            for _ in range(2):
+                g.epoch_async()
+            lines += [tuple(r) for r in g.results(2)]
+            lines.append(g.eval(3) + (0.0, 0.0))
+            runs.append((np.array(lines, np.float64), g.get_var(2)))
+            g.close()
     (a, wa), (b, wb) = runs
     np.testing.assert_allclose(a[:, [0, 2]], b[:, [0, 2]], rtol=1e-5)
     np.testing.assert_allclose(a[:, [1, 3]], b[:, [1, 3]], atol=2e-3)
@@ -255,13 +289,13 @@ def test_split_rows_restriction_matches_all_rows(pgcn):
     p = pgcn.make_params(ds)
     runs = []
     for on in (1, 0):
-        pgcn.lib.pgcn_debug_set(b"split_rows", on)
-        g = pgcn.GCN(p, ds, device=0)
-        lines = [g.train_epoch() + g.eval(2) for _ in range(4)]
-        lines.append(g.eval(3))
-        runs.append((np.array(lines[:-1], np.float64), lines[-1], g.get_var(2), g.get_var(5)))
-        g.close()
-    pgcn.lib.pgcn_debug_set(b"split_rows", 1)
+        with helpers.knobs(pgcn, split_rows=on):
+            g = pgcn.GCN(p, ds, device=0)
+            lines = [g.train_epoch() + g.eval(2) for _ in range(4)]
+            lines.append(g.eval(3))
+            runs.append((np.array(lines[:-1], np.float64), lines[-1], g.get_var(2),
+                         g.get_var(5)))
+            g.close()
     (a, ta, w1a, w2a), (b, tb, w1b, w2b) = runs
     np.testing.assert_allclose(a[:, [0, 2]], b[:, [0, 2]], rtol=1e-5)
     np.testing.assert_allclose(a[:, [1, 3]], b[:, [1, 3]], atol=2e-4)  # a row may flip on a tie

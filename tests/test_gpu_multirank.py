@@ -1,0 +1,90 @@
+"""The edge-cut engine at world 2 and 4 on ONE GPU through the in-process loopback
+communicator (SURVEY.md §4 "fake RCCL"; RCCL itself refuses two ranks on one device).
+
+Each rank is an engine created and driven by its own host thread; its collectives are the
+loopback group's stream-ordered device sums.  Everything else is the multi-GPU path the
+8-GPU bench runs: nnz-balanced contiguous node ranges, chunked partial GraphSums reduce-
+scattered on the comm stream, dropout masks drawn at the global stream offsets of each rank's
+elements, per-rank Â X for eval, the training split's column-subset backward, the weight-
+gradient all-reduce.  Compared with the oracle (single process, the reference's algorithm)
+with dropout 0.5 at the north star's 1e-4 on the losses.
+"""
+import numpy as np
+import pytest
+
+import helpers
+
+pytestmark = pytest.mark.gpu
+
+
+def _run_world(pgcn, ds, world, epochs, params=None, asynchronous=0):
+    group = pgcn.LoopbackGroup(world)
+    p = params or pgcn.make_params(ds)
+
+    def rank_fn(r):
+        g = pgcn.GCN(p, ds, device=0, rank=r, loopback=group)
+        info = {k: g.query(k) for k in ("world", "rank", "comm", "graphsum_lds", "reassociated")}
+        lines = [g.train_epoch() + g.eval(2) for _ in range(epochs)]
+        for _ in range(asynchronous):
+            g.epoch_async()
+        if asynchronous:
+            lines += [tuple(x) for x in g.results(asynchronous)]
+        test = g.eval(3)
+        rng = g.node_range()
+        w1 = g.get_var(2)
+        g.close()
+        return dict(info=info, lines=lines, test=test, range=rng, w1=w1)
+    return pgcn.run_ranks(world, rank_fn)
+
+
+def _check_ranks(res, world, n):
+    bounds = [r["range"] for r in res]
+    assert bounds[0][0] == 0 and bounds[-1][1] == n
+    for a, b in zip(bounds, bounds[1:]):
+        assert a[1] == b[0] and a[0] < a[1]
+    for r, x in enumerate(res):
+        assert x["info"]["world"] == world and x["info"]["rank"] == r
+        assert x["info"]["comm"] == 2  # loopback
+        # every rank reports the same all-reduced scalars and holds the same weights
+        np.testing.assert_array_equal(np.asarray(x["lines"]), np.asarray(res[0]["lines"]))
+        np.testing.assert_array_equal(x["w1"], res[0]["w1"])
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_loopback_cora_matches_reference_lines(loaded, pgcn, world):
+    ds = loaded["cora"]
+    res = _run_world(pgcn, ds, world, 20, asynchronous=3)
+    _check_ranks(res, world, ds.num_nodes)
+    gold = helpers.golden("cora")["epoch_lines"].reshape(-1, 4)
+    cnt = helpers.split_counts(ds)
+    for e, ours in enumerate(res[0]["lines"]):
+        helpers.assert_line_close(ours, gold[e], cnt, what=f"world {world} epoch {e + 1}")
+
+
+@pytest.fixture(scope="module")
+def big_ds(pgcn):
+    # 140k nodes: at world 2 a rank's 70k columns take the LDS GraphSum, at world 4 (35k) the
+    # gather kernel
+    return pgcn.Dataset.synthetic(140000, 64, 41, 1500000, 31)
+
+
+@pytest.fixture(scope="module")
+def big_oracle(big_ds):
+    ref = helpers.OracleGCN(helpers.ds_dict(big_ds))
+    lines = [ref.train_epoch() + ref.eval(2) for _ in range(4)]
+    return lines, ref.eval(3)
+
+
+@pytest.mark.parametrize("world,split_rows", [(2, 0), (2, 1), (4, 0)])
+def test_loopback_lds_graph_matches_oracle(pgcn, big_ds, big_oracle, world, split_rows):
+    with helpers.knobs(pgcn, split_rows=split_rows):
+        res = _run_world(pgcn, big_ds, world, 4)
+    _check_ranks(res, world, big_ds.num_nodes)
+    assert res[0]["info"]["graphsum_lds"] == (1 if world == 2 else 0)
+    assert res[0]["info"]["reassociated"] == 1
+    cnt = helpers.split_counts(big_ds)
+    lines, test = big_oracle
+    for e, (ours, want) in enumerate(zip(res[0]["lines"], lines)):
+        helpers.assert_line_close(ours, want, cnt, what=f"world {world} epoch {e + 1}")
+    t = res[0]["test"]
+    helpers.assert_line_close(t + t, test * 2, {1: cnt[3], 2: cnt[3]}, what="test")
