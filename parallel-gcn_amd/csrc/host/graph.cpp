@@ -747,6 +747,10 @@ LdsHost build_lds_host(int n_rows, int n_cols, const std::vector<int> &h_indptr_
 // per slice and slot, window-2 masks, zero rows) and adds each row's sum of in[col] into
 // out[row]; throws on any inconsistency the kernel would turn into a wrong sum.
 void lds_emulate(const LdsHost &h, int n_rows, const float *in, double *out) {
+  if (h.window == kRingWindow) {
+    ring_emulate(h, n_rows, in, out);
+    return;
+  }
   const int B = h.n_blocks, CW = LDS_CW, NS = LDS_SLOTS;
   const int SPB = h.window == 4 ? 8 : 4, BLK = 16 * SPB;
   const long long n_wg = (long long)h.n_batches * B;
@@ -858,9 +862,16 @@ std::vector<int> column_cuts(int n_cols, const std::vector<int> &indices, int n_
 }
 
 void DevGraph::build_lds() {
-  if (lds_cut_.empty()) lds_cut_ = column_cuts(n_cols_, h_indices_, lds_blocks(n_rows_, n_cols_));
+  const bool ring = g_graphsum_lds_window == kRingWindow;
+  if (lds_cut_.empty() || ring != lds_ring_cut_) {
+    lds_cut_ = ring ? ring_cuts(n_cols_, h_indices_, lds_blocks(n_rows_, n_cols_))
+                    : column_cuts(n_cols_, h_indices_, lds_blocks(n_rows_, n_cols_));
+    lds_ring_cut_ = ring;
+  }
   auto L = std::make_unique<LdsSched>();
-  LdsHost h = build_lds_host(n_rows_, n_cols_, h_indptr_, h_indices_, lds_cut_, g_graphsum_lds_window);
+  LdsHost h = ring ? build_ring_host(n_rows_, n_cols_, h_indptr_, h_indices_, lds_cut_)
+                   : build_lds_host(n_rows_, n_cols_, h_indptr_, h_indices_, lds_cut_,
+                                    g_graphsum_lds_window);
   const bool win2 = h.window == 2;
   // + 1 KB slack: ring refills read whole 512-B chunks past a wave's last entry block
   L->entries.allocate(h.entries.size() / 4 + 128);
@@ -884,7 +895,9 @@ void DevGraph::build_lds() {
   L->col_scale.allocate(h_col_scale_.size());
   L->col_scale.upload(h_col_scale_);
   // + LDS_ROWS rows: slice copies run whole pieces past the last column (never read)
-  L->scratch.allocate(((size_t)n_cols_ + LDS_ROWS) * 16 + 64);
+  // ring: whole slices of RING_SR rows (the loader copies 8-KB plane pieces)
+  L->scratch.allocate(ring ? (size_t)ceil_div(n_cols_, RING_SR) * RING_SR * 16
+                           : ((size_t)n_cols_ + LDS_ROWS) * 16 + 64);
   L->partial.allocate((size_t)h.n_blocks * n_rows_ * 16);
   L->s.n_blocks = h.n_blocks;
   L->s.n_rows = n_rows_;
@@ -902,6 +915,10 @@ void DevGraph::build_lds() {
   L->s.window = h.window;
   L->s.masks = win2 ? L->masks.get() : nullptr;
   lds_ = std::move(L);
+}
+
+void DevGraph::prepare(int dim) {
+  if (uses_lds(dim) && !lds_) build_lds();
 }
 
 bool DevGraph::uses_lds(int dim) const {
@@ -923,8 +940,12 @@ void DevGraph::graphsum(const float *in, int ld_in, float *out, int ld_out, int 
     const int ldm = std::min(ld_in, ld_out);
     for (int c0 = 0; c0 < dim; c0 += 16) {
       const int c = std::min(c0, ldm - 16);
-      launch_graphsum_lds(lds_->s, in + c, ld_in, out + c, ld_out, lds_->scratch.get(),
-                          lds_->partial.get(), s, col_map);
+      if (lds_->s.window == kRingWindow)
+        launch_graphsum_ring(lds_->s, in + c, ld_in, out + c, ld_out, lds_->scratch.get(),
+                             lds_->partial.get(), s, col_map);
+      else
+        launch_graphsum_lds(lds_->s, in + c, ld_in, out + c, ld_out, lds_->scratch.get(),
+                            lds_->partial.get(), s, col_map);
     }
     return;
   }

@@ -61,6 +61,11 @@ LdsHost build_lds_host(int n_rows, int n_cols, const std::vector<int> &indptr,
 // CPU walk of the schedule as the kernel consumes it: out[row] += sum of in[col] (throws on
 // an inconsistent schedule)
 void lds_emulate(const LdsHost &h, int n_rows, const float *in, double *out);
+// ring schedule (host/ring.cpp): block cuts on RING_SR multiples, the schedule, its emulation
+std::vector<int> ring_cuts(int n_cols, const std::vector<int> &indices, int n_blocks);
+LdsHost build_ring_host(int n_rows, int n_cols, const std::vector<int> &indptr,
+                        const std::vector<int> &indices, const std::vector<int> &bcut);
+void ring_emulate(const LdsHost &h, int n_rows, const float *in, double *out);
 
 class DevGraph {
  public:
@@ -75,6 +80,9 @@ class DevGraph {
                 bool compact_in = false);
   // graphsum() of this width runs the LDS-staged kernel (k_graphsum_lds)
   bool uses_lds(int dim) const;
+  // builds the schedule a graphsum() of this width will use now (host work, kept out of timed
+  // device regions)
+  void prepare(int dim);
   // bytes the kernel must move at minimum (SURVEY.md §8d formula, per call)
   double algorithmic_bytes(int dim) const;
   // schedule statistics (for tests / reports)
@@ -130,6 +138,7 @@ class DevGraph {
   bool blocked_built_ = false;
   std::vector<int> bcut_;                 // kBlocks + 1 column boundaries
   std::vector<int> lds_cut_;              // LDS schedule: lds_blocks() + 1 boundaries
+  bool lds_ring_cut_ = false;             // lds_cut_ on RING_SR multiples (ring schedule)
   std::vector<long long> bseg_;           // (kBlocks) x (n_rows + 1) segment offsets
   long long bnnz_ = 0;                    // blocked slots incl. padding
   DeviceBuffer<int> bindices_;

@@ -35,6 +35,7 @@
 // the 8 partials of a row in block order and scales by s_i => deterministic.
 #include "common.hpp"
 #include "kernels.hpp"
+#include "lds_dma.hpp"
 
 namespace pgcn {
 
@@ -58,43 +59,6 @@ __global__ __launch_bounds__(256) void k_gs_prescale(const float4 *__restrict__ 
   x.z *= s;
   x.w *= s;
   out[r * 4 + v] = x;
-}
-
-__device__ __forceinline__ void f4_acc(float4 &a, const float4 &x) {
-  a.x += x.x;
-  a.y += x.y;
-  a.z += x.z;
-  a.w += x.w;
-}
-
-// One LDS-DMA piece: 16 B per active lane to LDS byte address lds_dst + 16 * lane.  Inline
-// asm keeps the DMA out of hipcc's waitcnt bookkeeping (it would otherwise drain it with
-// vmcnt(0) before unrelated LDS reads); completion is counted by hand (s_waitcnt vmcnt).
-__device__ __forceinline__ void glds16(const void *gsrc, unsigned lds_dst) {
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(gsrc), "s"(lds_dst)
-      : "memory");
-}
-
-// Four consecutive 1-KB pieces: gsrc .. gsrc + 3 KB -> lds_dst .. lds_dst + 3 KB.  The
-// instruction offset steps the global AND the LDS address (LDS = M0 + offset + 16 * lane),
-// so one M0 write and one address VGPR serve all four.
-__device__ __forceinline__ void glds16x4(const void *gsrc, unsigned lds_dst) {
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
-      "global_load_lds_dwordx4 %1, off offset:1024\n\t"
-      "global_load_lds_dwordx4 %1, off offset:2048\n\t"
-      "global_load_lds_dwordx4 %1, off offset:3072\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(gsrc), "s"(lds_dst)
-      : "memory");
 }
 
 typedef float f2v __attribute__((ext_vector_type(2)));
@@ -174,18 +138,6 @@ __device__ __forceinline__ unsigned long long clk() { return __builtin_amdgcn_s_
 // (per-slice imbalance between waves no longer stalls everyone; r01 stamps: 18 % of the loop).
 constexpr int LDS_FLAG_BYTE = LDS_CW * LDS_SLOTS * 2;  // 480: first byte past the counts
 static_assert(LDS_FLAG_BYTE + 16 <= 512, "flag words fit the counts area tail");
-__device__ __forceinline__ unsigned lds_wait_ge(const unsigned *p, unsigned target) {
-  unsigned spins = 0;
-  while (true) {
-    const unsigned v = __builtin_amdgcn_readfirstlane(__atomic_load_n(p, __ATOMIC_RELAXED));
-    if (v >= target) break;
-    __builtin_amdgcn_s_sleep(1);
-    spins++;
-  }
-  asm volatile("" ::: "memory");
-  return spins;
-}
-
 template <int DIAG, int WIN, int SYNC>
 __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
     const uint2 *__restrict__ entries, const uint64_t *__restrict__ masks,
@@ -708,7 +660,7 @@ int g_graphsum_lds_opt = 3;
 // DIAG 4 stamp buffer (diagnostics; read back with pgcn_debug_read("graphsum_lds_stamps"))
 static unsigned long long *g_stamps = nullptr;
 static long long g_stamps_n = 0;
-static unsigned long long *lds_stamps(long long n_wg) {
+unsigned long long *lds_stamps(long long n_wg) {
   if (g_graphsum_lds_diag != 4) return nullptr;
   const long long n = n_wg * 16 * 8;
   if (n > g_stamps_n) {
@@ -770,6 +722,11 @@ void launch_graphsum_lds(const LdsSchedule &s, const float *in, int ld_in, float
     }
   }
 #undef GS_LDS
+  launch_gs_lds_combine(s, partial, out, ld_out, st);
+}
+
+void launch_gs_lds_combine(const LdsSchedule &s, const float *partial, float *out, int ld_out,
+                           hipStream_t st) {
   const long long post = (long long)s.n_rows * 4;
   hipLaunchKernelGGL(k_gs_lds_combine, dim3((unsigned)ceil_div(post, 256)), dim3(256), 0, st,
                      reinterpret_cast<const float4 *>(partial), (long long)s.n_rows,

@@ -1,0 +1,279 @@
+// parallel-gcn_amd/csrc/k_graphsum_ring.hip -- GraphSum for 16-wide rows over a sliding
+// window of LDS-resident feature slices (the reddit hot path; schedule: host/ring.cpp).
+//
+// Replaces graphsum_kernel (src/module.cu:172-210) / hpdga GraphSum::forward/backward
+// (module.cpp:82-111) for d = 16 on graphs whose feature table exceeds an XCD's L2.
+//
+// Algebra as k_graphsum_lds: Â = D^-1/2 A D^-1/2, out_i = s_i * sum_{j in N(i)} (s_j in_j);
+// k_ring_prescale forms s ⊙ in once per call, k_gs_lds_combine adds a row's column-block
+// partials in block order and applies s_i (deterministic).
+//
+// Workgroup (batch, block b), one per CU: 15 summing waves + 1 loader wave, 159 KB of LDS:
+//   [4 quarter planes x RING_P rows x 16 B]  the ring of RING_K = 4 slices of RING_SR = 512
+//                                            rows (plane v = columns 4v..4v+3), + 4 zero rows
+//   [2 x 512 B]                              step counts of visits v (v & 1), hand-off words
+//   [15 x 2 KB]                              per-wave entry rings (LDS-DMA refilled)
+// Visit v (one per slice of the block) reads slices v, v+1, v+2 (ring buffers t % 4); the
+// loader stages slice v+3 into buffer (v+3) % 4 once every summing wave has finished visit
+// v-1 (the last reader of the slice that buffer held), with the counts of visit v+1.  Entries
+// are 16-bit plane offsets (ring row x 16 B): lane (g, v) reads plane v at entry + plane base.
+#include "common.hpp"
+#include "kernels.hpp"
+#include "lds_dma.hpp"
+
+namespace pgcn {
+
+constexpr int RING_PLANE_B = RING_P * 16;                   // 32,832 B per quarter plane
+constexpr int RING_TABLE_B = 4 * RING_PLANE_B;              // 131,328 B
+constexpr int RING_CNT_USED = LDS_CW * LDS_SLOTS * 2;       // 480 B of counts per visit
+constexpr int RING_CNT_B = 512;
+constexpr int RING_CNT_OFF = RING_TABLE_B;
+constexpr int RING_FLAG_OFF = RING_CNT_OFF + RING_CNT_USED;  // loaded, done[4] (tail of buffer 0)
+constexpr int RING_ERING_OFF = RING_CNT_OFF + 2 * RING_CNT_B;
+constexpr int RING_CHUNK = 512;                             // 4 entry blocks of 128 B
+constexpr int RING_ESLOTS = 4;                              // chunks: 3 in flight + 1 read
+constexpr int RING_ERING_B = RING_ESLOTS * RING_CHUNK;
+constexpr int RING_TOTAL_B = RING_ERING_OFF + LDS_CW * RING_ERING_B;  // 163,072 B
+static_assert(RING_TOTAL_B <= 160 * 1024, "LDS budget");
+static_assert(RING_FLAG_OFF + 5 * 4 <= RING_CNT_OFF + RING_CNT_B, "hand-off words fit");
+static_assert(RING_SR * 16 == 8192, "a slice's plane piece is 8 x 1-KB LDS-DMA pieces");
+static_assert(RING_K * RING_SR * 16 + 4 * 16 <= 65536, "ring rows addressable by 16 bits");
+
+// in'[r] = scale[r] * in[col_map ? col_map[r] : r], written to the slice-plane layout:
+// float4 (r / SR) * 4 SR + v SR + r % SR   (slice, plane v, row) -- the loader then copies each
+// of a slice's four 8-KB planes with contiguous LDS-DMA pieces.
+__global__ __launch_bounds__(256) void k_ring_prescale(const float4 *__restrict__ in, int ld4_in,
+                                                       const float *__restrict__ scale, int n,
+                                                       float4 *__restrict__ out,
+                                                       const int *__restrict__ col_map) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long r = t >> 2;
+  if (r >= n) return;
+  const int v = (int)(t & 3);
+  const float s = scale[r];
+  const long long src = col_map ? (long long)col_map[r] : r;
+  float4 x = in[src * ld4_in + v];
+  x.x *= s;
+  x.y *= s;
+  x.z *= s;
+  x.w *= s;
+  out[(r / RING_SR) * (4 * RING_SR) + v * RING_SR + r % RING_SR] = x;
+}
+
+// diagnostics ("graphsum_lds_diag", k_graphsum_lds.hip): 4 = per-wave cycle stamps into
+// stamps[wg][wave][8] (summing: 0 loop, 1 hand-off wait, 2 ring wait, 3 entry blocks, 4 visits;
+// loader: 1 wait for a free buffer, 2 wait for its pieces to land, 4 slices); 1 = no table reads;
+// 2 = the loader stages 1/8 of each slice (both timing only)
+extern int g_graphsum_lds_diag;
+unsigned long long *lds_stamps(long long n_wg);
+__device__ __forceinline__ unsigned long long ring_clk() { return __builtin_amdgcn_s_memtime(); }
+
+template <int DIAG>
+__global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
+    const uint2 *__restrict__ entries, const long long *__restrict__ wave_off,
+    const unsigned short *__restrict__ counts, int t_max, const int2 *__restrict__ slices,
+    const int *__restrict__ n_slices, const int *__restrict__ rows, const char *__restrict__ table,
+    float4 *__restrict__ partial, long long part_stride, int n_blocks,
+    unsigned long long *__restrict__ stamps) {
+  __shared__ float4 lds[RING_TOTAL_B / 16];
+  unsigned long long st_loop = 0, st_wait = 0, st_ring = 0;
+  const int nb = n_blocks;
+  const int b = blockIdx.x % nb, batch = blockIdx.x / nb;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 2, v = lane & 3;
+  const int T = n_slices[b];
+  char *const lb = reinterpret_cast<char *>(lds);
+  const unsigned lds_base = __builtin_amdgcn_readfirstlane(
+      (unsigned)reinterpret_cast<size_t>((__attribute__((address_space(3))) float4 *)lds));
+  // zero rows: ring rows K*SR .. K*SR+3 of every plane (padding entries read them)
+  if (threadIdx.x < 16)
+    lds[((threadIdx.x >> 2) * RING_PLANE_B + (RING_K * RING_SR + (threadIdx.x & 3)) * 16) / 16] =
+        make_float4(0.f, 0.f, 0.f, 0.f);
+  unsigned *const flags = reinterpret_cast<unsigned *>(lb + RING_FLAG_OFF);
+  unsigned *const loaded = flags, *const done = flags + 1;
+  if (threadIdx.x < 5) flags[threadIdx.x] = 0u;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // zero rows and hand-off words set (the only barrier)
+  asm volatile("" ::: "memory");
+
+  if (wave == LDS_CW) {  // ------------------------------------------------ loader wave
+    __builtin_amdgcn_s_setprio(3);
+    const int2 *sl = slices + (long long)b * t_max;
+    const char *cnt_src =
+        reinterpret_cast<const char *>(counts) + (long long)blockIdx.x * t_max * RING_CNT_USED;
+    const int iters = T + RING_W - 1;
+    for (int s = 0; s < iters; s++) {
+      // buffer s % K (and counts buffer (s - W + 1) & 1) free: visit s - K done everywhere
+      if (s >= RING_K) {
+        unsigned long long c0 = 0;
+        if constexpr (DIAG == 4) c0 = ring_clk();
+        lds_wait_ge(done + (s - RING_K) % RING_K, (unsigned)(LDS_CW * ((s - RING_K) / RING_K + 1)));
+        if constexpr (DIAG == 4) st_wait += ring_clk() - c0;
+      }
+      if (s < T) {
+        const char *src = table + (long long)sl[s].x * 64 + lane * 16;
+        const unsigned dst = lds_base + (unsigned)((s % RING_K) * RING_SR * 16);
+        if constexpr (DIAG == 2) {  // timing only: 1/8 of the slice
+          glds16x4(src, dst);
+        } else {
+#pragma unroll
+          for (int p = 0; p < 4; p++) {
+            glds16x4(src + p * (RING_SR * 16), dst + (unsigned)(p * RING_PLANE_B));
+            glds16x4(src + p * (RING_SR * 16) + 4096, dst + (unsigned)(p * RING_PLANE_B + 4096));
+          }
+        }
+      }
+      const int cv = s - (RING_W - 1);  // the visit whose last slice this is
+      if (cv >= 0 && lane * 16 < RING_CNT_USED)
+        glds16(cnt_src + (long long)cv * RING_CNT_USED + lane * 16,
+               lds_base + (unsigned)(RING_CNT_OFF + (cv & 1) * RING_CNT_B));
+      unsigned long long c1 = 0;
+      if constexpr (DIAG == 4) c1 = ring_clk();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // slice s and counts landed
+      if constexpr (DIAG == 4) st_ring += ring_clk() - c1;
+      if (lane == 0) __atomic_store_n(loaded, (unsigned)(s + 1), __ATOMIC_RELAXED);
+      asm volatile("" ::: "memory");
+    }
+    if constexpr (DIAG == 4) {
+      if (lane == 0) {
+        unsigned long long *o = stamps + ((long long)blockIdx.x * 16 + wave) * 8;
+        o[1] = st_wait;
+        o[2] = st_ring;
+        o[4] = T;
+      }
+    }
+    return;
+  }
+
+  // ------------------------------------------------------------------------- summing waves
+  const long long wid = (long long)blockIdx.x * LDS_CW + wave;
+  const long long kb0 = wave_off[wid], kb1 = wave_off[wid + 1];
+  const long long nchunk = (kb1 - kb0 + 3) / 4;
+  const char *ebytes = reinterpret_cast<const char *>(entries) + kb0 * 128;
+  const unsigned ring_dst = lds_base + (unsigned)(RING_ERING_OFF + wave * RING_ERING_B);
+  const char *ring = lb + RING_ERING_OFF + wave * RING_ERING_B + g * 8;
+  auto refill = [&](long long c) {  // chunk c -> ring slot c % 4 (clamped: dummy past the end)
+    long long cc = c < nchunk ? c : nchunk - 1;
+    cc = cc > 0 ? cc : 0;
+    if (lane < 32)
+      glds16(ebytes + cc * RING_CHUNK + lane * 16,
+             ring_dst + (unsigned)((c % RING_ESLOTS) * RING_CHUNK));
+  };
+  refill(0);
+  refill(1);
+  refill(2);
+  refill(3);
+  asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // chunk 0
+
+  float4 acc[LDS_SLOTS];
+#pragma unroll
+  for (int j = 0; j < LDS_SLOTS; j++) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+  int chunk = 0;
+  int roff = 0;
+  static_assert((RING_ERING_B & (RING_ERING_B - 1)) == 0, "ring wraps by masking");
+  uint2 e_next = *reinterpret_cast<const uint2 *>(ring);
+  auto next_block = [&]() {
+    roff = (roff + 128) & (RING_ERING_B - 1);
+    if ((roff & (RING_CHUNK - 1)) == 0) {  // entering the next chunk: refill the slot
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      ++chunk;
+      refill(chunk + 3);
+      unsigned long long c0 = 0;
+      if constexpr (DIAG == 4) c0 = ring_clk();
+      asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      if constexpr (DIAG == 4) st_ring += ring_clk() - c0;
+    }
+    e_next = *reinterpret_cast<const uint2 *>(ring + roff);
+  };
+  // lane (g, v) reads plane v: entry (ring row x 16 B) + this constant
+  const char *tb = lb + v * RING_PLANE_B;
+  auto rd = [&](unsigned off) { return *reinterpret_cast<const float4 *>(tb + off); };
+  if constexpr (DIAG == 4) st_loop = ring_clk();
+  long long nblk = 0;
+  for (int t = 0; t < T; t++) {
+    unsigned long long hw0 = 0;
+    if constexpr (DIAG == 4) hw0 = ring_clk();
+    lds_wait_ge(loaded, (unsigned)(t + RING_W));  // slices t .. t+2 and visit t's counts
+    if constexpr (DIAG == 4) st_wait += ring_clk() - hw0;
+    const uint4 *c4 = reinterpret_cast<const uint4 *>(lb + RING_CNT_OFF + (t & 1) * RING_CNT_B +
+                                                      wave * 32);
+    const uint4 cw0 = c4[0], cw1 = c4[1];
+    const unsigned cw[8] = {
+        (unsigned)__builtin_amdgcn_readfirstlane(cw0.x), (unsigned)__builtin_amdgcn_readfirstlane(cw0.y),
+        (unsigned)__builtin_amdgcn_readfirstlane(cw0.z), (unsigned)__builtin_amdgcn_readfirstlane(cw0.w),
+        (unsigned)__builtin_amdgcn_readfirstlane(cw1.x), (unsigned)__builtin_amdgcn_readfirstlane(cw1.y),
+        (unsigned)__builtin_amdgcn_readfirstlane(cw1.z), (unsigned)__builtin_amdgcn_readfirstlane(cw1.w)};
+#pragma unroll
+    for (int j = 0; j < LDS_SLOTS; j++) {
+      const int n = (cw[j >> 1] >> (16 * (j & 1))) & 0xffff;  // steps of rowset j (x 4)
+      for (int k = 0; k < n; k += 4) {
+        const uint2 e = e_next;
+        next_block();
+        if constexpr (DIAG == 4) nblk++;
+        if constexpr (DIAG == 1) {  // timing only: no table reads
+          acc[j].x += __uint_as_float(e.x);
+          acc[j].y += __uint_as_float(e.y);
+        } else {
+          const float4 x0 = rd(e.x & 0xffffu), x1 = rd(e.x >> 16), x2 = rd(e.y & 0xffffu),
+                       x3 = rd(e.y >> 16);
+          f4_acc(acc[j], x0);
+          f4_acc(acc[j], x1);
+          f4_acc(acc[j], x2);
+          f4_acc(acc[j], x3);
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every read of slice t returned
+    if (lane == 0)
+      __hip_atomic_fetch_add(done + t % RING_K, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    asm volatile("" ::: "memory");
+  }
+  if constexpr (DIAG == 4) {
+    st_loop = ring_clk() - st_loop;
+    if (lane == 0) {
+      unsigned long long *o = stamps + ((long long)blockIdx.x * 16 + wave) * 8;
+      o[0] = st_loop;
+      o[1] = st_wait;
+      o[2] = st_ring;
+      o[3] = (unsigned long long)nblk;
+      o[4] = T;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the dummy ring refills
+  const int *rw = rows + (((long long)batch * LDS_CW + wave) * LDS_SLOTS) * 16 + g;
+  float4 *pb = partial + (long long)b * part_stride * 4 + v;
+#pragma unroll
+  for (int j = 0; j < LDS_SLOTS; j++) {
+    const int r = rw[j * 16];
+    if (r >= 0) pb[(long long)r * 4] = acc[j];
+  }
+}
+
+void launch_graphsum_ring(const LdsSchedule &s, const float *in, int ld_in, float *out,
+                          int ld_out, float *scratch_in, float *partial, hipStream_t st,
+                          const int *col_map) {
+  PGCN_CHECK(ld_in % 4 == 0 && ld_out % 4 == 0, PGCN_E_INVALID, "graphsum_ring: ld % 4");
+  PGCN_CHECK(s.window == kRingWindow, PGCN_E_INVALID, "graphsum_ring: not a ring schedule");
+  const long long pre = (long long)s.n_cols * 4;
+  hipLaunchKernelGGL(k_ring_prescale, dim3((unsigned)ceil_div(pre, 256)), dim3(256), 0, st,
+                     reinterpret_cast<const float4 *>(in), ld_in / 4, s.col_scale, s.n_cols,
+                     reinterpret_cast<float4 *>(scratch_in), col_map);
+  const long long n_wg = (long long)s.n_batches * s.n_blocks;
+#define GS_RING(D)                                                                            \
+  hipLaunchKernelGGL(k_graphsum_ring<D>, dim3((unsigned)n_wg), dim3(LDS_THREADS), 0, st,         \
+                     s.entries, s.wave_off, s.counts, s.t_max, s.slices, s.n_slices, s.rows,      \
+                     reinterpret_cast<const char *>(scratch_in),                                 \
+                     reinterpret_cast<float4 *>(partial), (long long)s.n_rows, s.n_blocks,         \
+                     D == 4 ? lds_stamps(n_wg) : nullptr)
+  switch (g_graphsum_lds_diag) {
+    case 1: GS_RING(1); break;
+    case 2: GS_RING(2); break;
+    case 4: GS_RING(4); break;
+    default: GS_RING(0); break;
+  }
+#undef GS_RING
+  launch_gs_lds_combine(s, partial, out, ld_out, st);
+}
+
+}  // namespace pgcn

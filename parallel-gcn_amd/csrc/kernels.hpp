@@ -36,6 +36,14 @@ constexpr int LDS_ROWS = LDS_SR + 4;                 // + 4 zero rows = 1024 row
 constexpr int LDS_CW = 15;                           // summing waves per workgroup
 constexpr int LDS_SLOTS = 16;                        // rowsets (16 rows) per compute wave
 constexpr int LDS_THREADS = 64 * (LDS_CW + 1);       // + one slice loader wave
+// Sliding-window ring schedule (k_graphsum_ring.hip, host/ring.cpp): slices of RING_SR rows,
+// a ring of RING_K slices in LDS as 4 quarter planes of RING_P rows, visits read RING_W slices
+constexpr int RING_SR = 512;
+constexpr int RING_K = 4;
+constexpr int RING_W = RING_K - 1;
+constexpr int RING_P = RING_K * RING_SR + 4;  // + 4 zero rows; = 4 mod 16 (bank quarters)
+constexpr int kRingWindow = 5;                // LdsSchedule::window of a ring schedule
+static_assert(RING_P % 16 == 4, "plane stride: lane v's chunk = 4v + row (mod 16)");
 struct LdsSchedule {
   int n_rows = 0, n_cols = 0;
   int n_batches = 0;  // workgroups = n_batches * n_blocks
@@ -54,6 +62,12 @@ struct LdsSchedule {
   int window = 1;
   const uint64_t *masks = nullptr;           // [kb][4]
 };
+// ring schedule (window == kRingWindow): scratch_in holds ceil(n_cols / RING_SR) slices
+void launch_graphsum_ring(const LdsSchedule &s, const float *in, int ld_in, float *out,
+                          int ld_out, float *scratch_in, float *partial, hipStream_t st,
+                          const int *col_map = nullptr);
+void launch_gs_lds_combine(const LdsSchedule &s, const float *partial, float *out, int ld_out,
+                           hipStream_t st);
 void launch_graphsum_lds(const LdsSchedule &s, const float *in, int ld_in, float *out,
                          int ld_out, float *scratch_in, float *partial, hipStream_t st,
                          const int *col_map = nullptr);

@@ -247,21 +247,24 @@ def _lds_check(pgcn, ip, ix, n, window):
     return err.value, nb.value
 
 
-@pytest.mark.parametrize("window", [1, 2, 3, 4])
+@pytest.mark.parametrize("window", [1, 2, 3, 4, 5])
 def test_lds_schedule_walk_sums_every_edge(pgcn, window):
     """The d = 16 LDS GraphSum schedule, walked on the CPU exactly as k_graphsum_lds consumes
     it (entry blocks, per-slice runs, window-2 lane masks, window-3 slot-pair order, window-4
     8-step blocks, zero rows), reproduces every row's CSR sum; window 2 needs fewer entry blocks
     than window 1 on a power-law graph, window 3 exactly as many (same blocks, another order),
-    window 4 fewer (twice the steps per block)."""
+    window 4 fewer (twice the steps per block); window 5, the ring schedule (host/ring.cpp:
+    visits over 3 resident slices, plane offsets), at most 3/4 of window 1's blocks."""
     ds = pgcn.Dataset.synthetic(70000, 8, 4, 2000000, 1)
     ip = np.ascontiguousarray(ds.graph_indptr)
     ix = np.ascontiguousarray(ds.graph_indices)
     err, nb = _lds_check(pgcn, ip, ix, ds.num_nodes, window)
     assert err < 1e-12
-    if window in (2, 3, 4):
+    if window in (2, 3, 4, 5):
         _, nb1 = _lds_check(pgcn, ip, ix, ds.num_nodes, 1)
-        if window == 2:
+        if window == 5:
+            assert nb < 0.75 * nb1, (nb, nb1)
+        elif window == 2:
             assert nb < 0.8 * nb1
         elif window == 3:
             assert nb == nb1
@@ -283,7 +286,7 @@ def test_lds_schedule_ragged_graph(pgcn):
     ip = np.zeros(n + 1, np.int32)
     ip[1:] = np.cumsum([len(r) for r in rows])
     ix = np.ascontiguousarray(np.concatenate([np.array(r, np.int32) for r in rows if r]))
-    for window in (1, 2, 3, 4):
+    for window in (1, 2, 3, 4, 5):
         err, _ = _lds_check(pgcn, ip, ix, n, window)
         assert err < 1e-12
 

@@ -82,6 +82,7 @@ def abs_bound(indptr, indices, x, dim):
     (120000, 40, 16, -3),    # LDS path, window-3 schedule (slot pairs interleaved)
     (120000, 40, 16, -4),    # LDS path, window-4 schedule (8-step blocks, exact step counts)
     (120000, 40, 16, -1),    # LDS path, window-1 schedule (4-step blocks)
+    (120000, 40, 16, -5),    # LDS path, ring schedule (visits over 3 resident slices)
 ])
 def test_graphsum_vs_oracle(pgcn, n, deg, dim, hubs):
     # LDS path (d = 16, table > L2): default window 1 (slots one after another); hubs < 0
@@ -117,11 +118,14 @@ def test_graphsum_vs_oracle(pgcn, n, deg, dim, hubs):
     pgcn.lib.pgcn_debug_set(b"graphsum_lds_window", LDS_WINDOW_DEFAULT)
 
 
-@pytest.mark.parametrize("blocks", [2, 8, 16, 32])
-def test_graphsum_lds_column_blocks(pgcn, blocks):
+@pytest.mark.parametrize("blocks,window", [(2, 1), (8, 1), (16, 1), (32, 1), (8, 5), (32, 5)])
+def test_graphsum_lds_column_blocks(pgcn, blocks, window):
     """The LDS schedule with other column-block counts than the shape rule picks (4 for square
-    graphs, 8 for row subsets): the same sums (XCD mapping: workgroup w serves block w % B)."""
+    graphs, 8 for row subsets): the same sums (XCD mapping: workgroup w serves block w % B).
+    Ring schedule (window 5) at 32 blocks: 7-8 slices per block, so the ring's prologue and
+    drain (the loader's last W - 1 iterations) make up much of each sweep."""
     assert pgcn.lib.pgcn_debug_set(b"lds_blocks", blocks) == 0
+    pgcn.lib.pgcn_debug_set(b"graphsum_lds_window", window)
     try:
         n, dim = 120000, 16
         indptr, indices = random_graph(n, 40, seed=blocks, hubs=20, hub_deg=3000)
@@ -140,6 +144,7 @@ def test_graphsum_lds_column_blocks(pgcn, blocks):
         pgcn.lib.pgcn_graph_destroy(g)
     finally:
         pgcn.lib.pgcn_debug_set(b"lds_blocks", 0)
+        pgcn.lib.pgcn_debug_set(b"graphsum_lds_window", LDS_WINDOW_DEFAULT)
 
 
 @pytest.mark.parametrize("dim,ld", [(128, 128), (41, 44), (24, 24)])
