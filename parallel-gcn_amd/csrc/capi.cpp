@@ -33,6 +33,10 @@ extern int g_graphsum_lds_wide;     // host/graph.cpp
 extern int g_graphsum_lds_order;    // host/graph.cpp (diagnostics)
 extern int g_graphsum_lds_diag;     // k_graphsum_lds.hip (diagnostics)
 extern int g_graphsum_lds_window;   // host/graph.cpp (diagnostics)
+extern int g_ring_balance;          // host/ring.cpp
+extern int g_graphsum_ring_prio;    // k_graphsum_ring.hip
+extern int g_ring_spread;           // host/ring.cpp
+extern int g_parse_threads;         // host/data.cpp: pieces of the parallel text parse
 extern int g_graphsum_lds_sync;     // k_graphsum_lds.hip (diagnostics)
 extern int g_graphsum_lds_opt;      // k_graphsum_lds.hip (diagnostics)
 long long lds_stamps_read(void *dst, long long max_elems);
@@ -545,6 +549,10 @@ int pgcn_debug_set(const char *key, int value) {
   else if (!std::strcmp(key, "graphsum_lds_order")) pgcn::g_graphsum_lds_order = value;
   else if (!std::strcmp(key, "graphsum_lds_diag")) pgcn::g_graphsum_lds_diag = value;
   else if (!std::strcmp(key, "graphsum_lds_window")) pgcn::g_graphsum_lds_window = value;
+  else if (!std::strcmp(key, "parse_threads")) pgcn::g_parse_threads = value;
+  else if (!std::strcmp(key, "ring_balance")) pgcn::g_ring_balance = value;
+  else if (!std::strcmp(key, "graphsum_ring_prio")) pgcn::g_graphsum_ring_prio = value;
+  else if (!std::strcmp(key, "ring_spread")) pgcn::g_ring_spread = value;
   else if (!std::strcmp(key, "graphsum_lds_sync")) pgcn::g_graphsum_lds_sync = value;
   else if (!std::strcmp(key, "graphsum_lds_opt")) pgcn::g_graphsum_lds_opt = value;
   else if (!std::strcmp(key, "gemm_variant")) pgcn::g_gemm_variant = value;

@@ -12,6 +12,7 @@
 #include <cstring>
 #include <fstream>
 #include <sstream>
+#include <thread>
 
 #include <sys/stat.h>
 
@@ -72,6 +73,56 @@ Parser::Parser(GCNData *data, const std::string &name, const std::string &root)
       split_path_(root + "/data/" + name + ".split"),
       svm_path_(root + "/data/" + name + ".svmlight") {}
 
+int g_parse_threads = 0;  // "parse_threads": host threads of Parser::parse (0 = up to 16)
+
+namespace {
+
+// Line-aligned pieces of buf for parallel parsing: piece k is [cut[k], cut[k+1]) and ends right
+// after a '\n'; the text after the last '\n' belongs to no piece (the reference's getline/eof
+// loop drops an unterminated last line, hpdga parser.cpp:23-27).
+std::vector<size_t> line_pieces(const std::string &buf, int pieces) {
+  const size_t last = buf.rfind('\n');
+  const size_t end = last == std::string::npos ? 0 : last + 1;
+  std::vector<size_t> cut(1, 0);
+  for (int k = 1; k < pieces; k++) {
+    size_t c = std::max(cut.back(), end * (size_t)k / (size_t)pieces);
+    if (c > 0 && c < end && buf[c - 1] != '\n') {
+      const size_t nl = buf.find('\n', c);
+      c = nl == std::string::npos ? end : nl + 1;
+    }
+    cut.push_back(std::min(c, end));
+  }
+  cut.push_back(end);
+  return cut;
+}
+
+int parse_threads(size_t bytes) {
+  if (g_parse_threads > 0) return g_parse_threads;  // exactly this many pieces (tests)
+  int t = (int)std::thread::hardware_concurrency();
+  t = std::max(1, std::min(t, 16));  // the GPU box grants 16 CPUs per GPU
+  // pieces of at least 1 MB (small files: one piece, no threads)
+  return (int)std::max<size_t>(1, std::min<size_t>((size_t)t, bytes >> 20));
+}
+
+// Runs fn(piece, begin, end) for every '\n'-terminated line of each piece, pieces in
+// parallel; fn sees the lines of one piece in file order.
+template <class Fn>
+void parallel_lines(const std::string &buf, const std::vector<size_t> &cut, Fn fn) {
+  const int P = (int)cut.size() - 1;
+  parallel_for(P, [&](long long p0, long long p1) {
+    for (long long k = p0; k < p1; k++) {
+      size_t pos = cut[(size_t)k];
+      while (pos < cut[(size_t)k + 1]) {
+        const size_t nl = buf.find('\n', pos);  // inside the piece: pieces end after a '\n'
+        fn((int)k, buf.data() + pos, buf.data() + nl);
+        pos = nl + 1;
+      }
+    }
+  }, P, 2);
+}
+
+}  // namespace
+
 bool Parser::parse() {
   std::string g, s, v;
   // isValidInput(): all three files must open (hpdga parser.cpp:50-53)
@@ -79,69 +130,131 @@ bool Parser::parse() {
     return false;
   GCNData &d = *data_;
 
-  // parseGraph (hpdga parser.cpp:18-48)
-  d.graph.indptr.assign(1, 0);
-  d.graph.indices.clear();
-  int node = 0;
-  for_each_line(g, [&](const char *p, const char *end) {
-    d.graph.indices.push_back(node);  // implicit self connection
-    d.graph.indptr.push_back(d.graph.indptr.back() + 1);
-    node++;
-    int nb;
-    while (next_int(p, end, &nb)) {
-      d.graph.indices.push_back(nb);
-      d.graph.indptr.back() += 1;
-    }
-  });
-  d.num_nodes = node;
+  // parseGraph (hpdga parser.cpp:18-48).  Pieces parse in parallel; a line's implicit self
+  // connection is its global line number, so each piece first learns how many lines precede it.
+  {
+    const std::vector<size_t> cut = line_pieces(g, parse_threads(g.size()));
+    const int P = (int)cut.size() - 1;
+    std::vector<long long> first((size_t)P + 1, 0);
+    parallel_for(P, [&](long long p0, long long p1) {
+      for (long long k = p0; k < p1; k++)
+        first[(size_t)k + 1] = std::count(g.begin() + (long long)cut[(size_t)k],
+                                          g.begin() + (long long)cut[(size_t)k + 1], '\n');
+    }, P, 2);
+    for (int k = 0; k < P; k++) first[(size_t)k + 1] += first[(size_t)k];
+    PGCN_CHECK(first[(size_t)P] < INT_MAX, PGCN_E_INVALID, "parseGraph: too many lines");
+    std::vector<std::vector<int>> len((size_t)P), idx((size_t)P);
+    std::vector<int> line((size_t)P);
+    for (int k = 0; k < P; k++) line[(size_t)k] = (int)first[(size_t)k];
+    parallel_lines(g, cut, [&](int k, const char *p, const char *end) {
+      std::vector<int> &ix = idx[(size_t)k];
+      const size_t before = ix.size();
+      ix.push_back(line[(size_t)k]++);  // implicit self connection
+      int nb;
+      while (next_int(p, end, &nb)) ix.push_back(nb);
+      len[(size_t)k].push_back((int)(ix.size() - before));
+    });
+    const int n = (int)first[(size_t)P];
+    d.graph.indptr.assign((size_t)n + 1, 0);
+    std::vector<long long> base((size_t)P + 1, 0);
+    for (int k = 0; k < P; k++) base[(size_t)k + 1] = base[(size_t)k] + (long long)idx[(size_t)k].size();
+    PGCN_CHECK(base[(size_t)P] <= INT_MAX, PGCN_E_INVALID, "parseGraph: more than 2^31 slots");
+    d.graph.indices.resize((size_t)base[(size_t)P]);
+    parallel_for(P, [&](long long p0, long long p1) {
+      for (long long k = p0; k < p1; k++) {
+        std::copy(idx[(size_t)k].begin(), idx[(size_t)k].end(),
+                  d.graph.indices.begin() + base[(size_t)k]);
+        long long at = base[(size_t)k];
+        for (size_t i = 0; i < len[(size_t)k].size(); i++) {
+          at += len[(size_t)k][i];
+          d.graph.indptr[(size_t)first[(size_t)k] + i + 1] = (int)at;
+        }
+      }
+    }, P, 2);
+    d.num_nodes = n;
+  }
 
-  // parseNode (hpdga parser.cpp:59-104)
-  d.feature_index.indptr.assign(1, 0);
-  d.feature_index.indices.clear();
-  d.feature_value.clear();
-  d.label.clear();
-  int max_idx = 0, max_label = 0;
-  for_each_line(v, [&](const char *p, const char *end) {
-    d.feature_index.indptr.push_back(d.feature_index.indptr.back());
-    const char *q = p;
-    while (q < end && is_ws(*q)) q++;
-    if (q >= end) {  // nothing to extract: the sentry fails, label keeps its -1
-      d.label.push_back(-1);
-      return;
+  // parseNode (hpdga parser.cpp:59-104), pieces in parallel, concatenated in file order
+  {
+    const std::vector<size_t> cut = line_pieces(v, parse_threads(v.size()));
+    const int P = (int)cut.size() - 1;
+    struct Piece {
+      std::vector<int> len, label, idx;
+      std::vector<float> val;
+      int max_idx = 0, max_label = 0;
+    };
+    std::vector<Piece> pc((size_t)P);
+    parallel_lines(v, cut, [&](int k, const char *p, const char *end) {
+      Piece &o = pc[(size_t)k];
+      const size_t before = o.idx.size();
+      const char *q = p;
+      while (q < end && is_ws(*q)) q++;
+      if (q >= end) {  // nothing to extract: the sentry fails, label keeps its -1
+        o.label.push_back(-1);
+        o.len.push_back(0);
+        return;
+      }
+      int label;
+      if (!next_int(p, end, &label)) {  // a non-number: num_get stores 0 and fails
+        o.label.push_back(0);
+        o.len.push_back(0);
+        return;
+      }
+      o.label.push_back(label);
+      o.max_label = std::max(o.max_label, label);
+      // "k:v" tokens
+      while (true) {
+        while (p < end && is_ws(*p)) p++;
+        if (p >= end) break;
+        const char *tok = p;
+        while (p < end && !is_ws(*p)) p++;
+        const char *tend = p;
+        int kk = 0;
+        const char *t = tok;
+        next_int(t, tend, &kk);
+        if (t < tend) t++;  // the ':' (kv_ss >> col)
+        char num[64];
+        size_t nn = std::min((size_t)(tend - t), sizeof num - 1);
+        std::memcpy(num, t, nn);
+        num[nn] = 0;
+        o.val.push_back(std::strtof(num, nullptr));
+        o.idx.push_back(kk);
+        o.max_idx = std::max(o.max_idx, kk);
+      }
+      o.len.push_back((int)(o.idx.size() - before));
+    });
+    long long rows = 0, nnz = 0;
+    std::vector<long long> row0((size_t)P + 1, 0), nz0((size_t)P + 1, 0);
+    int max_idx = 0, max_label = 0;
+    for (int k = 0; k < P; k++) {
+      row0[(size_t)k + 1] = rows += (long long)pc[(size_t)k].label.size();
+      nz0[(size_t)k + 1] = nnz += (long long)pc[(size_t)k].idx.size();
+      max_idx = std::max(max_idx, pc[(size_t)k].max_idx);
+      max_label = std::max(max_label, pc[(size_t)k].max_label);
     }
-    int label;
-    if (!next_int(p, end, &label)) {  // a non-number: num_get stores 0 and fails
-      d.label.push_back(0);
-      return;
-    }
-    d.label.push_back(label);
-    max_label = std::max(max_label, label);
-    // "k:v" tokens
-    while (true) {
-      while (p < end && is_ws(*p)) p++;
-      if (p >= end) break;
-      const char *tok = p;
-      while (p < end && !is_ws(*p)) p++;
-      const char *tend = p;
-      int k = 0;
-      const char *t = tok;
-      next_int(t, tend, &k);
-      if (t < tend) t++;  // the ':' (kv_ss >> col)
-      char num[64];
-      size_t n = std::min((size_t)(tend - t), sizeof num - 1);
-      std::memcpy(num, t, n);
-      num[n] = 0;
-      const float val = std::strtof(num, nullptr);
-      d.feature_value.push_back(val);
-      d.feature_index.indices.push_back(k);
-      d.feature_index.indptr.back() += 1;
-      max_idx = std::max(max_idx, k);
-    }
-  });
-  d.input_dim = max_idx + 1;
-  d.output_dim = max_label + 1;
+    PGCN_CHECK(nnz <= INT_MAX, PGCN_E_INVALID, "parseNode: more than 2^31 features");
+    d.feature_index.indptr.assign((size_t)rows + 1, 0);
+    d.feature_index.indices.resize((size_t)nnz);
+    d.feature_value.resize((size_t)nnz);
+    d.label.resize((size_t)rows);
+    parallel_for(P, [&](long long p0, long long p1) {
+      for (long long k = p0; k < p1; k++) {
+        const Piece &o = pc[(size_t)k];
+        std::copy(o.idx.begin(), o.idx.end(), d.feature_index.indices.begin() + nz0[(size_t)k]);
+        std::copy(o.val.begin(), o.val.end(), d.feature_value.begin() + nz0[(size_t)k]);
+        std::copy(o.label.begin(), o.label.end(), d.label.begin() + row0[(size_t)k]);
+        long long at = nz0[(size_t)k];
+        for (size_t i = 0; i < o.len.size(); i++) {
+          at += o.len[i];
+          d.feature_index.indptr[(size_t)row0[(size_t)k] + i + 1] = (int)at;
+        }
+      }
+    }, P, 2);
+    d.input_dim = max_idx + 1;
+    d.output_dim = max_label + 1;
+  }
 
-  // parseSplit (hpdga parser.cpp:106-116): std::stoi per line
+  // parseSplit (hpdga parser.cpp:106-116): std::stoi per line (small: one pass)
   d.split.clear();
   bool ok = true;
   for_each_line(s, [&](const char *p, const char *end) {

@@ -343,8 +343,9 @@ int g_graphsum_lds = 1;
 int g_graphsum_lds_wide = 1;  // "graphsum_lds_wide": rows wider than 16 as 16-column LDS passes
 // "graphsum_lds_window": 1 = slots one after another; 2 = two-slot runs (exec-masked; slower on
 // gfx950); 3 = slot pairs interleaved block by block (two blocks of LDS reads in flight; r01:
-// same time as 1 -- the kernel is not bound by per-wave LDS latency)
-int g_graphsum_lds_window = 1;
+// same time as 1 -- the kernel is not bound by per-wave LDS latency);
+// 4 = 8-step blocks; 5 (default) = the sliding-window ring schedule (host/ring.cpp)
+int g_graphsum_lds_window = 5;
 int g_graphsum_lds_order = 1;  // diagnostics ("graphsum_lds_order"): 0 = runs in column order  // diagnostics (pgcn_debug_set "graphsum_lds"): 0 disables the LDS path
 
 // LDS-staged d = 16 schedule (see k_graphsum_lds.hip for the layout it feeds), host side:

@@ -74,7 +74,7 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
     const unsigned short *__restrict__ counts, int t_max, const int2 *__restrict__ slices,
     const int *__restrict__ n_slices, const int *__restrict__ rows, const char *__restrict__ table,
     float4 *__restrict__ partial, long long part_stride, int n_blocks,
-    unsigned long long *__restrict__ stamps) {
+    unsigned long long *__restrict__ stamps, int prio) {
   __shared__ float4 lds[RING_TOTAL_B / 16];
   unsigned long long st_loop = 0, st_wait = 0, st_ring = 0;
   const int nb = n_blocks;
@@ -186,11 +186,11 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
     }
     e_next = *reinterpret_cast<const uint2 *>(ring + roff);
   };
+  if constexpr (DIAG == 4) st_loop = ring_clk();
+  long long nblk = 0;
   // lane (g, v) reads plane v: entry (ring row x 16 B) + this constant
   const char *tb = lb + v * RING_PLANE_B;
   auto rd = [&](unsigned off) { return *reinterpret_cast<const float4 *>(tb + off); };
-  if constexpr (DIAG == 4) st_loop = ring_clk();
-  long long nblk = 0;
   for (int t = 0; t < T; t++) {
     unsigned long long hw0 = 0;
     if constexpr (DIAG == 4) hw0 = ring_clk();
@@ -225,9 +225,21 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every read of slice t returned
+    unsigned rank = 0;
     if (lane == 0)
-      __hip_atomic_fetch_add(done + t % RING_K, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      rank = __hip_atomic_fetch_add(done + t % RING_K, 1u, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_WORKGROUP);
     asm volatile("" ::: "memory");
+    if (prio) {
+      // The arbiter favours older waves, so the youngest waves of a workgroup fall behind
+      // and the visits' hand-offs make everyone wait for them (r02 stamps: 395 vs 576 cycles
+      // per block from the oldest to the youngest wave).  The last third of the waves to
+      // finish a visit run the next one at raised priority, the first third at the lowest.
+      rank = (unsigned)__builtin_amdgcn_readfirstlane((int)rank) - (unsigned)(LDS_CW * (t / RING_K));
+      if (rank >= (unsigned)(2 * LDS_CW / 3)) __builtin_amdgcn_s_setprio(2);
+      else if (rank >= (unsigned)(LDS_CW / 3)) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    }
   }
   if constexpr (DIAG == 4) {
     st_loop = ring_clk() - st_loop;
@@ -241,14 +253,31 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the dummy ring refills
+  // rows[] = row | log2(m) << 28: a row spread over m lane groups (host/ring.cpp) has its m
+  // partial sums added across lane groups g ^ 1, g ^ 2, .. (xor butterfly, fixed order for the
+  // writing lane group g % m == 0); m is uniform per rowset
   const int *rw = rows + (((long long)batch * LDS_CW + wave) * LDS_SLOTS) * 16 + g;
   float4 *pb = partial + (long long)b * part_stride * 4 + v;
 #pragma unroll
   for (int j = 0; j < LDS_SLOTS; j++) {
-    const int r = rw[j * 16];
-    if (r >= 0) pb[(long long)r * 4] = acc[j];
+    const int u = rw[j * 16];
+    const int sp = __builtin_amdgcn_readfirstlane((int)((unsigned)u >> 28));
+    float4 a = acc[j];
+    for (int k = 0; k < sp; k++) {
+      const int d = 4 << k;
+      a.x += __shfl_xor(a.x, d);
+      a.y += __shfl_xor(a.y, d);
+      a.z += __shfl_xor(a.z, d);
+      a.w += __shfl_xor(a.w, d);
+    }
+    const int r = u & kRingRowMask;
+    if (r != kRingEmpty && (g & ((1 << sp) - 1)) == 0) pb[(long long)r * 4] = a;
   }
 }
+
+// "graphsum_ring_prio": 1 = waves that finished a visit last run the next one at raised
+// issue priority (see the summing loop), 0 = fixed priority
+int g_graphsum_ring_prio = 1;
 
 void launch_graphsum_ring(const LdsSchedule &s, const float *in, int ld_in, float *out,
                           int ld_out, float *scratch_in, float *partial, hipStream_t st,
@@ -261,11 +290,11 @@ void launch_graphsum_ring(const LdsSchedule &s, const float *in, int ld_in, floa
                      reinterpret_cast<float4 *>(scratch_in), col_map);
   const long long n_wg = (long long)s.n_batches * s.n_blocks;
 #define GS_RING(D)                                                                            \
-  hipLaunchKernelGGL(k_graphsum_ring<D>, dim3((unsigned)n_wg), dim3(LDS_THREADS), 0, st,         \
+  hipLaunchKernelGGL((k_graphsum_ring<D>), dim3((unsigned)n_wg), dim3(LDS_THREADS), 0, st,         \
                      s.entries, s.wave_off, s.counts, s.t_max, s.slices, s.n_slices, s.rows,      \
                      reinterpret_cast<const char *>(scratch_in),                                 \
                      reinterpret_cast<float4 *>(partial), (long long)s.n_rows, s.n_blocks,         \
-                     D == 4 ? lds_stamps(n_wg) : nullptr)
+                     D == 4 ? lds_stamps(n_wg) : nullptr, g_graphsum_ring_prio)
   switch (g_graphsum_lds_diag) {
     case 1: GS_RING(1); break;
     case 2: GS_RING(2); break;

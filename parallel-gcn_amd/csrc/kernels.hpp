@@ -43,6 +43,9 @@ constexpr int RING_K = 4;
 constexpr int RING_W = RING_K - 1;
 constexpr int RING_P = RING_K * RING_SR + 4;  // + 4 zero rows; = 4 mod 16 (bank quarters)
 constexpr int kRingWindow = 5;                // LdsSchedule::window of a ring schedule
+// ring schedule rows[]: row id | log2(spread) << 28; kRingEmpty = no row (spread kept)
+constexpr int kRingRowMask = 0x0fffffff;
+constexpr int kRingEmpty = 0x0fffffff;
 static_assert(RING_P % 16 == 4, "plane stride: lane v's chunk = 4v + row (mod 16)");
 struct LdsSchedule {
   int n_rows = 0, n_cols = 0;

@@ -16,7 +16,7 @@ import helpers
 pytestmark = pytest.mark.gpu
 
 DEV = "cuda"
-LDS_WINDOW_DEFAULT = 1  # host/graph.cpp g_graphsum_lds_window
+LDS_WINDOW_DEFAULT = 5  # host/graph.cpp g_graphsum_lds_window (the ring schedule)
 
 
 def vp(t):

@@ -45,9 +45,20 @@ def timed(reps=20):
 
 
 out = {"window": window}
-for diag in (0, 1, 2, 0):
-    pg.lib.pgcn_debug_set(b"graphsum_lds_diag", diag)
-    out[f"diag{diag}_ms"] = timed()
+ref = None
+for pipe in [int(x) for x in os.environ.get("RING_PRIOS", "1,0").split(",")]:
+    pg.lib.pgcn_debug_set(b"graphsum_ring_prio", pipe)
+    for diag in (0, 1, 2, 0):
+        pg.lib.pgcn_debug_set(b"graphsum_lds_diag", diag)
+        out[f"prio{pipe}_diag{diag}_ms"] = timed()
+    pg.lib.pgcn_debug_set(b"graphsum_lds_diag", 0)
+    call()
+    torch.cuda.synchronize()
+    if ref is None:
+        ref = o.clone()
+    else:  # both loops add the same rows in the same order per accumulator
+        out["prio_max_abs_diff"] = float(torch.abs(o - ref).max())
+pg.lib.pgcn_debug_set(b"graphsum_ring_prio", int(os.environ.get("RING_PRIO", "1")))
 pg.lib.pgcn_debug_set(b"graphsum_lds_diag", 4)
 call()
 call()
@@ -69,6 +80,11 @@ out.update({
     "loader_free_wait_cyc_mean": load[:, 1].mean(), "loader_land_wait_cyc_mean": load[:, 2].mean(),
     "visits": summ[:, :, 4].mean(),
     "wg_loop_max_over_mean": float(summ[:, :, 0].max(1).max() / summ[:, :, 0].max(1).mean()),
+    "per_wave_wait_frac": [round(float(x), 3) for x in
+                           (summ[:, :, 1].sum(0) / summ[:, :, 0].sum(0))],
+    "per_wave_blocks": [round(float(x), 1) for x in summ[:, :, 3].mean(0)],
+    "per_wave_cyc_per_block": [round(float(x), 1) for x in
+                               ((summ[:, :, 0] - summ[:, :, 1]).sum(0) / summ[:, :, 3].sum(0))],
 })
 pg.lib.pgcn_debug_set(b"graphsum_lds_window", 1)
 print(json.dumps(out))
