@@ -874,8 +874,8 @@ void DevGraph::build_lds() {
                    : build_lds_host(n_rows_, n_cols_, h_indptr_, h_indices_, lds_cut_,
                                     g_graphsum_lds_window);
   const bool win2 = h.window == 2;
-  // + 1 KB slack: ring refills read whole 512-B chunks past a wave's last entry block
-  L->entries.allocate(h.entries.size() / 4 + 128);
+  // + 2 KB slack: ring refills read whole 512-B chunks (up to 3) past a wave's last block
+  L->entries.allocate(h.entries.size() / 4 + 256);  // 2 KB: ring refills run 3 chunks past
   L->entries.upload(reinterpret_cast<const uint2 *>(h.entries.data()), h.entries.size() / 4);
   if (win2) {  // + 64 B of slack: the mask loads touch the line after the last block's
     L->masks.allocate(h.masks.size() + 8);

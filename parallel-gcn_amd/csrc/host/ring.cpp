@@ -301,7 +301,7 @@ LdsHost build_ring_host(int n_rows, int n_cols, const std::vector<int> &indptr,
             load++;
           }
         }
-      for (int w = 0; w < CW; w++)
+      for (int w = 0; w < CW; w++) {
         for (int j = 0; j < NS; j++) {
           const int S = 4 * nb[(size_t)w * NS + j];
           PGCN_CHECK(S < 65536, PGCN_E_INVALID, "graphsum_ring: visit run too long");
@@ -370,6 +370,7 @@ LdsHost build_ring_host(int n_rows, int n_cols, const std::vector<int> &indptr,
           for (int g = 0; g < 16; g++)
             PGCN_CHECK(lj[g].due == 0, PGCN_E_INVALID, "graphsum_ring: edge past its slice's visit");
         }
+      }
     }
     for (auto &L : lanes)
       PGCN_CHECK(L.pending() == 0 && L.next >= L.end, PGCN_E_INVALID,
@@ -422,9 +423,13 @@ void ring_emulate(const LdsHost &h, int n_rows, const float *in, double *out) {
       std::fill(acc.begin(), acc.end(), 0.0);
       for (int v = 0; v < T; v++) {
         const unsigned short *cn = &h.counts[(size_t)(((wg * h.t_max + v) * CW + w) * NS)];
+        std::vector<int> seq;  // the rowset of each block, in stream order
         for (int j = 0; j < NS; j++) {
           PGCN_CHECK(cn[j] % 4 == 0, PGCN_E_INVALID, "ring schedule: steps not whole blocks");
-          for (int k = 0; k < cn[j] / 4; k++, kb++)
+          for (int k = 0; k < cn[j] / 4; k++) seq.push_back(j);
+        }
+        for (const int j : seq) {
+          {
             for (int st = 0; st < 4; st++)
               for (int g = 0; g < 16; g++) {
                 const int e = h.entries[(size_t)kb * 64 + g * 4 + st];
@@ -444,6 +449,8 @@ void ring_emulate(const LdsHost &h, int n_rows, const float *in, double *out) {
                 PGCN_CHECK(row < sc.y, PGCN_E_INVALID, "ring schedule: entry past the slice");
                 acc[(size_t)j * 16 + g] += (double)in[sc.x + row];
               }
+          }
+          kb++;
         }
       }
       PGCN_CHECK(kb == h.wave_off[(size_t)(wg * CW + w) + 1], PGCN_E_INVALID,

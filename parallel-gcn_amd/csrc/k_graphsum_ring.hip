@@ -148,17 +148,16 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
 
   // ------------------------------------------------------------------------- summing waves
   const long long wid = (long long)blockIdx.x * LDS_CW + wave;
-  const long long kb0 = wave_off[wid], kb1 = wave_off[wid + 1];
-  const long long nchunk = (kb1 - kb0 + 3) / 4;
-  const char *ebytes = reinterpret_cast<const char *>(entries) + kb0 * 128;
+  const long long kb0 = wave_off[wid];
+  // the wave's entry stream, 512-B chunks (4 entry blocks) into a 4-slot LDS ring; refills
+  // run up to 3 chunks past the stream's end (the entries array has 2 KB of slack)
+  const char *esrc = reinterpret_cast<const char *>(entries) + kb0 * 128 + lane * 16;
   const unsigned ring_dst = lds_base + (unsigned)(RING_ERING_OFF + wave * RING_ERING_B);
   const char *ring = lb + RING_ERING_OFF + wave * RING_ERING_B + g * 8;
-  auto refill = [&](long long c) {  // chunk c -> ring slot c % 4 (clamped: dummy past the end)
-    long long cc = c < nchunk ? c : nchunk - 1;
-    cc = cc > 0 ? cc : 0;
-    if (lane < 32)
-      glds16(ebytes + cc * RING_CHUNK + lane * 16,
-             ring_dst + (unsigned)((c % RING_ESLOTS) * RING_CHUNK));
+  auto refill = [&](int c) {  // chunk c -> ring slot c % 4
+    if (DIAG != 5 && DIAG != 6 && lane < 32)  // DIAG 5/6: no entry stream (timing only)
+      glds16(esrc, ring_dst + (unsigned)((c & (RING_ESLOTS - 1)) * RING_CHUNK));
+    esrc += RING_CHUNK;
   };
   refill(0);
   refill(1);
@@ -173,9 +172,12 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
   int roff = 0;
   static_assert((RING_ERING_B & (RING_ERING_B - 1)) == 0, "ring wraps by masking");
   uint2 e_next = *reinterpret_cast<const uint2 *>(ring);
+  // next entry block (its refill when a chunk is entered).  The slot refilled holds the chunk
+  // before this one: the read of its last entry block (the caller's current entry, which
+  // hipcc waits for only where it is first used) must have returned before the DMA lands.
   auto next_block = [&]() {
     roff = (roff + 128) & (RING_ERING_B - 1);
-    if ((roff & (RING_CHUNK - 1)) == 0) {  // entering the next chunk: refill the slot
+    if ((roff & (RING_CHUNK - 1)) == 0) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       ++chunk;
       refill(chunk + 3);
@@ -206,17 +208,22 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
         (unsigned)__builtin_amdgcn_readfirstlane(cw1.z), (unsigned)__builtin_amdgcn_readfirstlane(cw1.w)};
 #pragma unroll
     for (int j = 0; j < LDS_SLOTS; j++) {
-      const int n = (cw[j >> 1] >> (16 * (j & 1))) & 0xffff;  // steps of rowset j (x 4)
+      int n = (cw[j >> 1] >> (16 * (j & 1))) & 0xffff;  // steps of rowset j (x 4)
+      if constexpr (DIAG == 7) n = 0;  // timing only: visits without blocks
       for (int k = 0; k < n; k += 4) {
         const uint2 e = e_next;
         next_block();
+        // the next entry read goes out before this block's table reads: it returns first
+        // (LDS reads complete in order), so the next block finds it landed
+        asm volatile("" ::: "memory");
         if constexpr (DIAG == 4) nblk++;
-        if constexpr (DIAG == 1) {  // timing only: no table reads
+        if constexpr (DIAG == 1 || DIAG == 6) {  // timing only: no table reads
           acc[j].x += __uint_as_float(e.x);
           acc[j].y += __uint_as_float(e.y);
         } else {
           const float4 x0 = rd(e.x & 0xffffu), x1 = rd(e.x >> 16), x2 = rd(e.y & 0xffffu),
                        x3 = rd(e.y >> 16);
+          __builtin_amdgcn_s_waitcnt(0xC07F);  // one lgkmcnt(0) wait, then the adds
           f4_acc(acc[j], x0);
           f4_acc(acc[j], x1);
           f4_acc(acc[j], x2);
@@ -290,7 +297,7 @@ void launch_graphsum_ring(const LdsSchedule &s, const float *in, int ld_in, floa
                      reinterpret_cast<float4 *>(scratch_in), col_map);
   const long long n_wg = (long long)s.n_batches * s.n_blocks;
 #define GS_RING(D)                                                                            \
-  hipLaunchKernelGGL((k_graphsum_ring<D>), dim3((unsigned)n_wg), dim3(LDS_THREADS), 0, st,         \
+  hipLaunchKernelGGL((k_graphsum_ring<D>), dim3((unsigned)n_wg), dim3(LDS_THREADS), 0, st,   \
                      s.entries, s.wave_off, s.counts, s.t_max, s.slices, s.n_slices, s.rows,      \
                      reinterpret_cast<const char *>(scratch_in),                                 \
                      reinterpret_cast<float4 *>(partial), (long long)s.n_rows, s.n_blocks,         \
@@ -299,6 +306,9 @@ void launch_graphsum_ring(const LdsSchedule &s, const float *in, int ld_in, floa
     case 1: GS_RING(1); break;
     case 2: GS_RING(2); break;
     case 4: GS_RING(4); break;
+    case 5: GS_RING(5); break;  // no entry stream (zero entries: every step reads row 0)
+    case 6: GS_RING(6); break;  // no entry stream, no table reads
+    case 7: GS_RING(7); break;  // visits and hand-offs only
     default: GS_RING(0); break;
   }
 #undef GS_RING

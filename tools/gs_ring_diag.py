@@ -48,7 +48,7 @@ out = {"window": window}
 ref = None
 for pipe in [int(x) for x in os.environ.get("RING_PRIOS", "1,0").split(",")]:
     pg.lib.pgcn_debug_set(b"graphsum_ring_prio", pipe)
-    for diag in (0, 1, 2, 0):
+    for diag in [int(d) for d in os.environ.get("RING_DIAGS", "0,1,2,0").split(",")]:
         pg.lib.pgcn_debug_set(b"graphsum_lds_diag", diag)
         out[f"prio{pipe}_diag{diag}_ms"] = timed()
     pg.lib.pgcn_debug_set(b"graphsum_lds_diag", 0)

@@ -23,7 +23,8 @@ st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 pg.lib.pgcn_debug_set(b"graphsum_lds_window", 5)
 out = {}
 for cfg in sys.argv[1:]:
-    s, b, p = (int(v) for v in cfg.split(","))
+    vals = [int(v) for v in cfg.split(",")]
+    s, b, p = vals[:3]
     pg.lib.pgcn_debug_set(b"ring_spread", s)
     pg.lib.pgcn_debug_set(b"ring_balance", b)
     pg.lib.pgcn_debug_set(b"graphsum_ring_prio", p)
