@@ -54,6 +54,7 @@ WORKLOADS = {
     "reddit-11.6M": 11606919,
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+MFMA_F32_PEAK_TF = 157.3  # MI355X dense fp32 MFMA (= vector) peak (MI355X_MICROARCH.md)
 
 
 def load_pkg():
@@ -227,6 +228,7 @@ def main():
     for _ in range(2):
         g.epoch_async()
     gs_ms, gs_calls, gs_bytes = g.profile_read()
+    mm_ms, mm_calls, mm_flops = g.profile_read_mm()
     g.profile(False)
     g.close()
     avg_ms = gs_ms / max(gs_calls, 1)
@@ -275,6 +277,14 @@ def main():
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic, "avg_call_ms": avg_ms,
                      "algorithmic_bytes_per_call": bytes_per_call, "calls": gs_calls},
+        # the XW contractions (dense X W1, H W of the hidden layers and their gradients) on
+        # the fp32 MFMA kernels: flops over their event time, against the 157.3 TF fp32 peak
+        "mfma": ({"kernels": "k_xstream_nn/tn, k_gemm_nn/tn (v_mfma_f32_16x16x4f32)",
+                  "achieved": mm_flops / (mm_ms * 1e-3) / 1e12, "peak": MFMA_F32_PEAK_TF,
+                  "unit": "TFLOP/s",
+                  "frac": mm_flops / (mm_ms * 1e-3) / 1e12 / MFMA_F32_PEAK_TF,
+                  "ms_per_epoch": mm_ms / 2, "flops_per_epoch": mm_flops / 2,
+                  "calls": mm_calls} if mm_ms > 0 else None),
         "last_epoch": ({"train_loss": float(res[-1, 0]), "train_acc": float(res[-1, 1]),
                         "val_loss": float(res[-1, 2]), "val_acc": float(res[-1, 3])}
                        if len(res) else None),
@@ -297,7 +307,9 @@ def main():
         out["value_reference_order"] = secondary(
             {"train_ahead": 0, "split_rows": 0, "split_cols": 0, "eval_ax": 0})
         params.reassociate_last = 1
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and hidden != (16,):
+        out["cpu_baseline"] = None  # the reference's sequential build is the 2-layer H = 16 GCN
+    elif rank == 0 and world == 1 and not args.no_cpu_baseline:
         kind, times, ref_lines = cpu_baseline(ds, args.cpu_epochs)
         out["cpu_baseline"] = {"value": len(times) / sum(times), "unit": "epochs/s", "cores": 1,
                                "kind": kind,

@@ -234,6 +234,10 @@ int pgcn_gcn_num_vars(pgcn_gcn *g);
 int pgcn_gcn_profile(pgcn_gcn *g, int enable);
 int pgcn_gcn_profile_read(pgcn_gcn *g, double *graphsum_ms_total, long long *graphsum_calls,
                           double *graphsum_bytes_total);
+/* The same for the XW contractions on the MFMA kernels (dense X W1 / its weight gradient,
+ * H W / its two gradients): summed event time, launches, 2*M*N*K flops. */
+int pgcn_gcn_profile_read_mm(pgcn_gcn *g, double *ms_total, long long *calls,
+                             double *flops_total);
 /* this rank's node range [first, last) (edge-cut engine; whole graph otherwise) */
 int pgcn_gcn_node_range(pgcn_gcn *g, int *first, int *last);
 

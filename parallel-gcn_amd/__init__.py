@@ -116,6 +116,7 @@ _sig("pgcn_gcn_get_var", c_ll, c_void_p, c_int, c_int, P(c_float))
 _sig("pgcn_gcn_num_vars", c_int, c_void_p)
 _sig("pgcn_gcn_profile", c_int, c_void_p, c_int)
 _sig("pgcn_gcn_profile_read", c_int, c_void_p, P(c_double), P(c_ll), P(c_double))
+_sig("pgcn_gcn_profile_read_mm", c_int, c_void_p, P(c_double), P(c_ll), P(c_double))
 _sig("pgcn_gcn_node_range", c_int, c_void_p, P(c_int), P(c_int))
 _sig("pgcn_dataset_load", c_int, ctypes.c_char_p, ctypes.c_char_p, P(c_void_p))
 _sig("pgcn_dataset_load_cached", c_int, ctypes.c_char_p, ctypes.c_char_p, P(c_void_p), P(c_int))
@@ -318,6 +319,13 @@ class GCN:
                                         ctypes.byref(byts)), "profile_read")
         return ms.value, calls.value, byts.value
 
+    def profile_read_mm(self):
+        """(ms, launches, flops) of the profiled XW contractions (MFMA kernels)."""
+        ms, calls, fl = c_double(), c_ll(), c_double()
+        check(lib.pgcn_gcn_profile_read_mm(self._h, ctypes.byref(ms), ctypes.byref(calls),
+                                           ctypes.byref(fl)), "profile_read_mm")
+        return ms.value, calls.value, fl.value
+
     def query(self, key):
         """Engine facts: world, rank, comm (0 none / 1 RCCL / 2 loopback), reassociated,
         graph_symmetric, graphsum_lds, epochs."""
@@ -461,6 +469,7 @@ EXPORTED = [
     "pgcn_gcn_create_loopback", "pgcn_gcn_query", "pgcn_gcn_destroy", "pgcn_gcn_train_epoch", "pgcn_gcn_eval",
     "pgcn_gcn_epoch_async", "pgcn_gcn_sync", "pgcn_gcn_results", "pgcn_gcn_run",
     "pgcn_gcn_get_var", "pgcn_gcn_num_vars", "pgcn_gcn_profile", "pgcn_gcn_profile_read",
+    "pgcn_gcn_profile_read_mm",
     "pgcn_gcn_node_range", "pgcn_dataset_load", "pgcn_dataset_load_cached", "pgcn_dataset_save",
     "pgcn_dataset_load_binary", "pgcn_dataset_binarize", "pgcn_dataset_synthetic",
     "pgcn_dataset_view",

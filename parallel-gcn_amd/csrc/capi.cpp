@@ -457,6 +457,9 @@ int pgcn_gcn_profile(pgcn_gcn *g, int enable) {
 int pgcn_gcn_profile_read(pgcn_gcn *g, double *ms, long long *calls, double *bytes) {
   return guarded([&] { g->g->profile_read(ms, calls, bytes); });
 }
+int pgcn_gcn_profile_read_mm(pgcn_gcn *g, double *ms, long long *calls, double *flops) {
+  return guarded([&] { g->g->profile_read_mm(ms, calls, flops); });
+}
 int pgcn_gcn_node_range(pgcn_gcn *g, int *first, int *last) {
   *first = g->g->partition().first();
   *last = g->g->partition().last();

@@ -426,6 +426,8 @@ void GCN::build(const GCNData &data) {
   ctx.gemm_workspace = gemm_ws.get();
   ctx.gs_events = &gs_events;
   ctx.gs_bytes = &gs_bytes;
+  ctx.mm_events = &mm_events;
+  ctx.mm_flops = &mm_flops;
 
   // layers (src/gcn.cu:146-177)
   variables.push_back(nullptr);  // "input": the features, kept in `feats`
@@ -837,6 +839,22 @@ void GCN::set_profile(bool on) {
   ctx.profile = on;
   gs_events.clear();
   gs_bytes.clear();
+  mm_events.clear();
+  mm_flops.clear();
+}
+
+void GCN::profile_read_mm(double *ms, long long *calls, double *flops) {
+  sync();
+  double t = 0, f = 0;
+  for (size_t i = 0; i < mm_events.size(); i++) {
+    float e = 0;
+    PGCN_HIP(hipEventElapsedTime(&e, mm_events[i].first.get(), mm_events[i].second.get()));
+    t += e;
+    f += mm_flops[i];
+  }
+  if (ms) *ms = t;
+  if (calls) *calls = (long long)mm_events.size();
+  if (flops) *flops = f;
 }
 
 void GCN::profile_read(double *ms, long long *calls, double *bytes) {

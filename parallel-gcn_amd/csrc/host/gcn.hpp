@@ -89,6 +89,7 @@ class GCN {
   int num_vars() const { return (int)variables.size(); }
   std::vector<float> get_var(int idx, int which);
   void set_profile(bool on);
+  void profile_read_mm(double *ms, long long *calls, double *flops);  // XW contractions
   void profile_read(double *ms, long long *calls, double *bytes);
   const Partition &partition() const { return part; }
   const GCNParams &get_params() const { return params; }
@@ -186,6 +187,8 @@ class GCN {
   bool warm = false;                  // one eager epoch_async ran (lazy buffers exist)
 
   std::vector<std::pair<Event, Event>> gs_events;
+  std::vector<std::pair<Event, Event>> mm_events;
+  std::vector<double> mm_flops;
   std::vector<double> gs_bytes;
 };
 

@@ -7,6 +7,30 @@
 
 namespace pgcn {
 
+namespace {
+// Profiling scope of one XW contraction (MFMA kernels): HIP events around the launches on
+// the module's stream and the contraction's 2*M*N*K flops (ctx->profile only).
+struct MmProfile {
+  ModuleContext *ctx;
+  hipStream_t s;
+  double flops;
+  Event e0, e1;
+  MmProfile(ModuleContext *c, hipStream_t st, double f) : ctx(c), s(st), flops(f) {
+    if (!on()) return;
+    e0 = Event::create(true);
+    e1 = Event::create(true);
+    e0.record(s);
+  }
+  bool on() const { return ctx->profile && ctx->mm_events && flops > 0; }
+  ~MmProfile() {
+    if (!on()) return;
+    e1.record(s);
+    ctx->mm_events->emplace_back(e0, e1);
+    ctx->mm_flops->push_back(flops);
+  }
+};
+}  // namespace
+
 Variable::Variable(int rows_, int cols_, bool requires_grad, int ld_)
     : rows(rows_), cols(cols_), ld(ld_ < 0 ? cols_ : ld_), size((long long)rows_ * cols_) {
   const size_t n = (size_t)rows * (size_t)ld;
@@ -133,6 +157,7 @@ void SparseMatmul::forward(bool training, const Stream &s) const {
     ahead_valid = true;
     return;
   }
+  MmProfile prof(ctx, s.get(), x->dense ? 2.0 * x->rows * b->cols * x->cols : 0.0);
   if (x->dense && x->maskT) {  // X-stream kernels (N <= 16, K <= 640)
     if (mask) launch_mask_nibbles(mask, base, x->cols, x->rows, x->cols, x->maskT.get(), s.get());
     launch_xstream_nn(x->rows, b->cols, x->cols, x->x.get(), x->ldx, b->dev_data.get(), b->ld, 0,
@@ -152,6 +177,7 @@ void SparseMatmul::backward(const Stream &s) const {
   const uint64_t *mask = last_training ? drop->state().mask.get() : nullptr;
   const long long base = drop->state().mask_base;
   const float scale = drop->scale();
+  MmProfile prof(ctx, s.get(), x->dense ? 2.0 * x->rows * b->cols * x->cols : 0.0);
   if (x->dense && x->maskT) {  // the nibble mask of the last training forward
     if (ctx->train_ahead && ctx->mask_side && ctx->side_stream && !drop->drawn_ahead()) {
       // the next epoch's input mask, drawn on the side stream while this pass streams X
@@ -339,6 +365,7 @@ Matmul::Matmul(shared_ptr<Variable> a_, shared_ptr<Variable> b_, shared_ptr<Vari
 void Matmul::forward(bool, const Stream &s) const {
   const bool cmp = last_layer && ctx->compact_n;  // compact output layer: the split's rows
   const Variable &A = cmp ? *ctx->compact_z : *a, &C = cmp ? *ctx->compact_out : *c;
+  MmProfile prof(ctx, s.get(), 2.0 * (cmp ? ctx->compact_n : m) * p * n);
   launch_gemm_nn(cmp ? ctx->compact_n : m, p, n, A.dev_data.get(), A.ld, b->dev_data.get(), b->ld,
                  0, C.dev_data.get(), C.ld, nullptr, 0, 0, 1.0f, s.get());
 }
@@ -347,6 +374,7 @@ void Matmul::backward(const Stream &s) const {
   const bool cmp = last_layer && ctx->compact_n;
   const Variable &A = cmp ? *ctx->compact_z : *a, &C = cmp ? *ctx->compact_out : *c;
   const int rows = cmp ? ctx->compact_n : m;
+  MmProfile prof(ctx, s.get(), 2.0 * 2.0 * rows * p * n);
   // a.grad = c.grad * b^T   (b stored [n][p] => trans_b)
   launch_gemm_nn(rows, n, p, C.dev_grad.get(), C.ld, b->dev_data.get(), b->ld, 1,
                  A.dev_grad.get(), A.ld, nullptr, 0, 0, 1.0f, s.get());

@@ -126,6 +126,9 @@ struct ModuleContext {
   bool profile = false;
   std::vector<std::pair<Event, Event>> *gs_events = nullptr;
   std::vector<double> *gs_bytes = nullptr;
+  // ... and of the XW contractions on the MFMA kernels (dense X W, H W, their gradients)
+  std::vector<std::pair<Event, Event>> *mm_events = nullptr;
+  std::vector<double> *mm_flops = nullptr;
   std::vector<Event> *event_pool = nullptr;
 };
 
