@@ -33,6 +33,7 @@ on this host, 1 thread) and "parity" (those reference epochs' losses against a f
 first epochs on the same data: the reddit-114M epoch checked end to end).
 """
 import argparse
+import contextlib
 import json
 import os
 import subprocess
@@ -208,17 +209,20 @@ def main():
         return max_over_ranks(time.perf_counter() - t0)
 
     head_knobs = dict(kv.split("=") for kv in args.knob)
-    with helpers.knobs(pgcn, **{k: int(v) for k, v in head_knobs.items()}):
-        t_build = time.perf_counter()
-        g = engine()
-        t_build = time.perf_counter() - t_build
-    info = {k: g.query(k) for k in ("world", "comm", "reassociated", "graph_symmetric",
+    # the headline knobs stay set through its timing and profiling (some are read per launch)
+    head_ctx = contextlib.ExitStack()
+    head_ctx.enter_context(helpers.knobs(pgcn, **{k: int(v) for k, v in head_knobs.items()}))
+    t_build = time.perf_counter()
+    g = engine()
+    t_build = time.perf_counter() - t_build
+    info = {k: g.query(k) for k in ("world", "comm", "reassociated", "graph_symmetric", "fused_tails",
                                      "graphsum_lds")}
     ax_ms = max_over_ranks(g.query("eval_ax_us") / 1000.0)
     elapsed = timed(g, args.steps, args.warmup)
     res = g.results(min(args.steps, 4))
 
     if args.profile_only:
+        head_ctx.close()
         if rank == 0:
             print(json.dumps({"elapsed_s": elapsed, "steps": args.steps}))
         return
@@ -230,6 +234,7 @@ def main():
     gs_ms, gs_calls, gs_bytes = g.profile_read()
     mm_ms, mm_calls, mm_flops = g.profile_read_mm()
     g.profile(False)
+    head_ctx.close()
     g.close()
     avg_ms = gs_ms / max(gs_calls, 1)
     bytes_per_call = gs_bytes / max(gs_calls, 1)

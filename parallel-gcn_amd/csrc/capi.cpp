@@ -22,6 +22,7 @@ extern int g_gemm_variant;          // k_gemm.hip (diagnostics)
 extern int g_train_ahead;           // host/gcn.cpp
 extern int g_split_rows;            // host/gcn.cpp
 extern int g_split_cols;            // host/gcn.cpp
+extern int g_fuse_epilogue;         // host/gcn.cpp
 extern int g_mask_side;             // host/gcn.cpp
 extern int g_xstream_tn_lds;        // k_gemm.hip
 extern int g_eval_ax;               // host/gcn.cpp
@@ -35,6 +36,7 @@ extern int g_graphsum_lds_diag;     // k_graphsum_lds.hip (diagnostics)
 extern int g_graphsum_lds_window;   // host/graph.cpp (diagnostics)
 extern int g_ring_balance;          // host/ring.cpp
 extern int g_graphsum_ring_prio;    // k_graphsum_ring.hip
+extern int g_graphsum_ring_fused;   // k_graphsum_ring.hip
 extern int g_ring_spread;           // host/ring.cpp
 extern int g_parse_threads;         // host/data.cpp: pieces of the parallel text parse
 extern int g_graphsum_lds_sync;     // k_graphsum_lds.hip (diagnostics)
@@ -394,6 +396,7 @@ long long pgcn_gcn_query(pgcn_gcn *g, const char *key) {
   if (!std::strcmp(key, "rank")) return c ? c->rank() : 0;
   if (!std::strcmp(key, "comm")) return c ? (!std::strcmp(c->kind(), "rccl") ? 1 : 2) : 0;
   if (!std::strcmp(key, "reassociated")) return e.reassociated() ? 1 : 0;
+  if (!std::strcmp(key, "fused_tails")) return e.fused_tails();
   if (!std::strcmp(key, "graph_symmetric")) return e.symmetric() ? 1 : 0;
   if (!std::strcmp(key, "graphsum_lds")) return e.graphsum_lds() ? 1 : 0;
   if (!std::strcmp(key, "epochs")) return e.epochs_run();
@@ -555,6 +558,7 @@ int pgcn_debug_set(const char *key, int value) {
   else if (!std::strcmp(key, "parse_threads")) pgcn::g_parse_threads = value;
   else if (!std::strcmp(key, "ring_balance")) pgcn::g_ring_balance = value;
   else if (!std::strcmp(key, "graphsum_ring_prio")) pgcn::g_graphsum_ring_prio = value;
+  else if (!std::strcmp(key, "graphsum_ring_fused")) pgcn::g_graphsum_ring_fused = value;
   else if (!std::strcmp(key, "ring_spread")) pgcn::g_ring_spread = value;
   else if (!std::strcmp(key, "graphsum_lds_sync")) pgcn::g_graphsum_lds_sync = value;
   else if (!std::strcmp(key, "graphsum_lds_opt")) pgcn::g_graphsum_lds_opt = value;
@@ -562,6 +566,7 @@ int pgcn_debug_set(const char *key, int value) {
   else if (!std::strcmp(key, "train_ahead")) pgcn::g_train_ahead = value;
   else if (!std::strcmp(key, "split_rows")) pgcn::g_split_rows = value;
   else if (!std::strcmp(key, "split_cols")) pgcn::g_split_cols = value;
+  else if (!std::strcmp(key, "fuse_epilogue")) pgcn::g_fuse_epilogue = value;
   else if (!std::strcmp(key, "mask_side")) pgcn::g_mask_side = value;
   else if (!std::strcmp(key, "xstream_tn_lds")) pgcn::g_xstream_tn_lds = value;
   else if (!std::strcmp(key, "eval_ax")) pgcn::g_eval_ax = value;

@@ -30,6 +30,9 @@ int g_split_rows = 0;
 // edges from the training split's columns.  The loss gradient is exactly zero on every other
 // row, so the skipped terms are exact zeros: in.grad is the full gradient of every row
 int g_split_cols = 1;
+// "fuse_epilogue" (read at engine build): the ReLU / Dropout modules next to a GraphSum run in
+// its final-write epilogue (gs_epilogue.hpp), bit-identical to separate launches
+int g_fuse_epilogue = 1;
 
 // ------------------------------------------------------------------------------------------
 // Adam (src/optim.cu:7-95; hpdga optim.cpp:16-35)
@@ -436,8 +439,41 @@ void GCN::build(const GCNData &data) {
     insert_layer(params.hidden_dims[(size_t)l - 1], params.hidden_dims[(size_t)l],
                  params.dropouts[(size_t)l], l);
   insert_last_layer();
+  if (g_fuse_epilogue && !comm) fuse_epilogues();
   optimizer = Adam(weights, decays, adam_params);
   PGCN_HIP(hipDeviceSynchronize());
+}
+
+// GraphSum -> ReLU(out) [-> Dropout(out)] in the module list: the ReLU and the Dropout run in
+// the GraphSum's epilogue (forward); Dropout(in) <- ReLU(in) <- GraphSum, i.e. the backward
+// of a GraphSum followed by those of the Dropout and ReLU on its input: same (backward).
+// Only where the element order of the variable is its storage order (ld == cols).
+void GCN::fuse_epilogues() {
+  const size_t n = modules.size();
+  for (size_t i = 0; i < n; i++) {
+    auto *gs = dynamic_cast<GraphSum *>(modules[i].get());
+    if (!gs) continue;
+    const Variable *out = gs->output(), *in = gs->input();
+    if (i + 1 < n && out->ld == out->cols) {
+      auto *relu = dynamic_cast<ReLU *>(modules[i + 1].get());
+      if (relu && relu->variable() == out) {
+        gs->fwd_relu = relu;
+        auto *drop = i + 2 < n ? dynamic_cast<Dropout *>(modules[i + 2].get()) : nullptr;
+        if (drop && drop->variable() == out) gs->fwd_drop = drop;
+        fused_tails_++;
+      }
+    }
+    if (i >= 1 && in->ld == in->cols) {
+      auto *drop = dynamic_cast<Dropout *>(modules[i - 1].get());
+      const size_t ri = drop && drop->variable() == in ? i - 2 : i - 1;
+      auto *relu = ri < n ? dynamic_cast<ReLU *>(modules[ri].get()) : nullptr;
+      if (relu && relu->variable() == in) {
+        gs->bwd_relu = relu;
+        if (ri + 1 < i) gs->bwd_drop = drop;
+        fused_tails_++;
+      }
+    }
+  }
 }
 
 // src/gcn.cu:47-81

@@ -102,6 +102,7 @@ class GCN {
   bool graphsum_lds() const;
   // the output layer runs as (Â H) W (reassociate_last requested, hidden < classes, Â symmetric)
   bool reassociated() const { return reassociated_; }
+  int fused_tails() const { return fused_tails_; }
 
  private:
   void build(const GCNData &data);
@@ -110,6 +111,8 @@ class GCN {
   void insert_first_layer();
   void insert_layer(int in_dim, int out_dim, float dropout, int layer);
   void insert_last_layer();
+  void fuse_epilogues();
+  int fused_tails_ = 0;  // GraphSum epilogues carrying ReLU / Dropout work (forward + backward)
   void set_split(int split);
   void finalize(int slot_offset, bool graph = false);
   void enqueue_epoch(bool graph);

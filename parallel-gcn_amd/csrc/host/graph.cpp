@@ -891,6 +891,11 @@ void DevGraph::build_lds() {
   L->n_slices.upload(h.nsl);
   L->rows.allocate(h.rows.size());
   L->rows.upload(h.rows);
+  if (ring) {
+    L->arrive.allocate((size_t)h.n_batches);
+    L->arrive.zero();
+    L->s.arrive = L->arrive.get();
+  }
   L->row_scale.allocate(h_row_scale_.size());
   L->row_scale.upload(h_row_scale_);
   L->col_scale.allocate(h_col_scale_.size());
@@ -927,11 +932,20 @@ bool DevGraph::uses_lds(int dim) const {
          !h_row_scale_.empty() && !g_graphsum_force_plain && (double)n_cols_ * 64.0 > kL2Budget;
 }
 
+bool DevGraph::epilogue_ok(int dim, int ld_in, int ld_out) const {
+  (void)ld_in;
+  (void)ld_out;
+  if (uses_lds(dim)) return dim <= 16;
+  return !(dim > 16 && !graphsum_vec_supported((dim + 3) / 4));
+}
+
 void DevGraph::graphsum(const float *in, int ld_in, float *out, int ld_out, int dim,
-                        hipStream_t s, bool compact_in) {
+                        hipStream_t s, bool compact_in, const GsEpilogue *epi) {
   const int *col_map = compact_in ? nullptr : col_map_.get();
   PGCN_CHECK(ld_in % 4 == 0 && ld_out % 4 == 0 && ld_in >= dim && ld_out >= dim,
              PGCN_E_INVALID, "graphsum: leading dims must be multiples of 4 and >= dim");
+  PGCN_CHECK(!epi || epi->mode == 0 || epilogue_ok(dim, ld_in, ld_out), PGCN_E_INVALID,
+             "graphsum: epilogue on a multi-pass width");
   if (uses_lds(dim)) {
     if (!lds_) build_lds();
     // wider rows: one LDS pass per 16 columns (the last pass overlaps the one before it so it
@@ -943,10 +957,10 @@ void DevGraph::graphsum(const float *in, int ld_in, float *out, int ld_out, int 
       const int c = std::min(c0, ldm - 16);
       if (lds_->s.window == kRingWindow)
         launch_graphsum_ring(lds_->s, in + c, ld_in, out + c, ld_out, lds_->scratch.get(),
-                             lds_->partial.get(), s, col_map);
+                             lds_->partial.get(), s, col_map, epi);
       else
         launch_graphsum_lds(lds_->s, in + c, ld_in, out + c, ld_out, lds_->scratch.get(),
-                            lds_->partial.get(), s, col_map);
+                            lds_->partial.get(), s, col_map, epi);
     }
     return;
   }
@@ -970,7 +984,8 @@ void DevGraph::graphsum(const float *in, int ld_in, float *out, int ld_out, int 
   Sched &sc = schedule(vec);
   const bool blocked = sc.s.nbc > 1;
   launch_graphsum(sc.s, blocked ? bindices_.get() : indices_.get(),
-                  blocked ? bvals_.get() : vals_.get(), in, ld_in, out, ld_out, sc.partial.get(), s);
+                  blocked ? bvals_.get() : vals_.get(), in, ld_in, out, ld_out, sc.partial.get(), s,
+                  epi);
 }
 
 double DevGraph::algorithmic_bytes(int dim) const {

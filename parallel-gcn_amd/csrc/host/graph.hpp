@@ -76,8 +76,12 @@ class DevGraph {
   long long nnz() const { return nnz_; }
   // out[i,:dim] = sum_j val_ij * in[col_j,:dim]
   // compact_in (column subsets): `in` holds the subset's columns as its rows (no gather)
+  // epi: the element-wise tail applied to every output row as it is formed (one pass only:
+  // dim <= 16, or a width with a kernel of its own and no 16-column passes)
   void graphsum(const float *in, int ld_in, float *out, int ld_out, int dim, hipStream_t s,
-                bool compact_in = false);
+                bool compact_in = false, const GsEpilogue *epi = nullptr);
+  // graphsum() of this width can take an epilogue (one pass over the columns)
+  bool epilogue_ok(int dim, int ld_in, int ld_out) const;
   // graphsum() of this width runs the LDS-staged kernel (k_graphsum_lds)
   bool uses_lds(int dim) const;
   // builds the schedule a graphsum() of this width will use now (host work, kept out of timed
@@ -120,7 +124,7 @@ class DevGraph {
     DeviceBuffer<long long> wave_off;
     DeviceBuffer<unsigned short> counts;
     DeviceBuffer<int2> slices;
-    DeviceBuffer<int> n_slices, rows;
+    DeviceBuffer<int> n_slices, rows, arrive;
     DeviceBuffer<float> row_scale, col_scale, scratch, partial;
   };
   std::unique_ptr<LdsSched> lds_;

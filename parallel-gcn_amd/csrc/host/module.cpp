@@ -88,8 +88,18 @@ void Dropout::wait_ahead(hipStream_t s) const {
   }
 }
 
+void Dropout::draw_fused(hipStream_t s) const {
+  PGCN_CHECK(in && !ahead, PGCN_E_INVALID, "dropout: fused draw of a hidden dropout only");
+  draw(s, rng->mask.get());
+  skip_forward = true;
+}
+
 void Dropout::forward(bool training, const Stream &s) const {
   if (!training) return;  // hpdga module.cpp:209
+  if (skip_forward) {  // drawn and applied by the GraphSum before it (epilogue)
+    skip_forward = false;
+    return;
+  }
   const DropoutRng &r = *rng;
   if (ahead) {  // drawn ahead (during the last weight-gradient pass, or by the eval forward)
     wait_ahead(s.get());
@@ -108,6 +118,10 @@ void Dropout::forward(bool training, const Stream &s) const {
 
 void Dropout::backward(const Stream &s) const {
   if (!in || !in->dev_grad) return;  // module.cpp:222: no mask => nothing to do
+  if (skip_backward) {  // applied by the GraphSum backward before it (epilogue)
+    skip_backward = false;
+    return;
+  }
   const DropoutRng &r = *rng;
   launch_dropout_apply_based(in->dev_grad.get(), r.elem_end - r.elem_begin, r.mask.get(),
                              r.mask_base, scale(), s.get());
@@ -219,7 +233,48 @@ GraphSum::GraphSum(shared_ptr<Variable> in_, shared_ptr<Variable> out_, DevGraph
   }
 }
 
-void GraphSum::run(const float *src, float *dst, const Stream &s, int mode) const {
+// The fused forward tail: ReLU on `out` (its mask when training), then the hidden Dropout
+// (training), both skipped as modules for this pass.  mode 0 when `g` cannot take an epilogue.
+GsEpilogue GraphSum::forward_epilogue(bool training, const Stream &s, const DevGraph *g) const {
+  GsEpilogue e;
+  if (!fwd_relu || ctx->comm || !g || !g->epilogue_ok(dim, in->ld, out->ld)) return e;
+  e.mode = 1;
+  e.relu_mask = training ? fwd_relu->mask_ptr() : nullptr;
+  e.relu_ld = out->ld;
+  if (training && fwd_drop) {
+    fwd_drop->draw_fused(s.get());
+    const DropoutRng &r = fwd_drop->state();
+    e.drop_mask = r.mask.get();
+    e.drop_base = r.mask_base;
+    e.drop_cols = out->cols;
+    e.drop_scale = fwd_drop->scale();
+  }
+  fwd_relu->skip_forward = true;
+  return e;
+}
+
+// The fused backward tail: the Dropout backward on in.grad (mask of the last training
+// forward), then the ReLU backward, both skipped as modules for this pass.
+GsEpilogue GraphSum::backward_epilogue(const DevGraph *g) const {
+  GsEpilogue e;
+  if (!bwd_relu || ctx->comm || !g || !g->epilogue_ok(dim, out->ld, in->ld)) return e;
+  e.mode = 2;
+  e.relu_mask = bwd_relu->mask_ptr();
+  e.relu_ld = in->ld;
+  if (bwd_drop) {
+    const DropoutRng &r = bwd_drop->state();
+    e.drop_mask = r.mask.get();
+    e.drop_base = r.mask_base;
+    e.drop_cols = in->cols;
+    e.drop_scale = bwd_drop->scale();
+    bwd_drop->skip_backward = true;
+  }
+  bwd_relu->skip_backward = true;
+  return e;
+}
+
+void GraphSum::run(const float *src, float *dst, const Stream &s, int mode,
+                   const GsEpilogue *epi) const {
   Event e0, e1;
   if (ctx->profile) {
     e0 = Event::create(true);
@@ -259,7 +314,7 @@ void GraphSum::run(const float *src, float *dst, const Stream &s, int mode) cons
     reduced.record(ctx->comm_stream);
     reduced.wait_on(s.get());  // dst complete, partials free for the next call
   } else {
-    graph->graphsum(src, in->ld, dst, out->ld, dim, s.get());
+    graph->graphsum(src, in->ld, dst, out->ld, dim, s.get(), false, epi);
     bytes = graph->algorithmic_bytes(dim);
     if (ctx->profile) e1.record(s.get());
   }
@@ -277,7 +332,8 @@ void GraphSum::forward(bool training, const Stream &s) const {
   }
   DevGraph *sg = last_layer && !ctx->comm ? ctx->split_graph : nullptr;
   if (!sg) {
-    run(in->dev_data.get(), out->dev_data.get(), s);
+    const GsEpilogue epi = forward_epilogue(training, s, graph);
+    run(in->dev_data.get(), out->dev_data.get(), s, 0, &epi);
     return;
   }
   // output layer: only the split's labelled rows, summed compactly and scattered to their
@@ -317,7 +373,8 @@ void GraphSum::backward(const Stream &s) const {
   }
   DevGraph *cg = last_layer && !ctx->comm ? ctx->split_colgraph : nullptr;
   if (!cg) {
-    run(out->dev_grad.get(), in->dev_grad.get(), s);
+    const GsEpilogue epi = backward_epilogue(graph);
+    run(out->dev_grad.get(), in->dev_grad.get(), s, 0, &epi);
     return;
   }
   // output layer: out.grad is the loss gradient, zero outside the split's labelled rows, so
@@ -331,7 +388,8 @@ void GraphSum::backward(const Stream &s) const {
   // (compact: the Matmul left out.grad in compact rows, which the column-subset graph reads
   // as its columns directly; else it gathers them from the full rows)
   const float *g_in = ctx->compact_n ? ctx->compact_z->dev_grad.get() : out->dev_grad.get();
-  cg->graphsum(g_in, out->ld, in->dev_grad.get(), in->ld, dim, s.get(), ctx->compact_n > 0);
+  const GsEpilogue epi = backward_epilogue(cg);
+  cg->graphsum(g_in, out->ld, in->dev_grad.get(), in->ld, dim, s.get(), ctx->compact_n > 0, &epi);
   if (ctx->profile) {
     e1.record(s.get());
     ctx->gs_events->emplace_back(e0, e1);
@@ -348,10 +406,18 @@ ReLU::ReLU(shared_ptr<Variable> in_) : in(std::move(in_)) {
 }
 
 void ReLU::forward(bool training, const Stream &s) const {
+  if (skip_forward) {  // applied by the GraphSum before it (epilogue)
+    skip_forward = false;
+    return;
+  }
   launch_relu_fwd(in->dev_data.get(), (long long)in->rows * in->ld, mask.get(), training, s.get());
 }
 
 void ReLU::backward(const Stream &s) const {
+  if (skip_backward) {  // applied by the GraphSum backward before it (epilogue)
+    skip_backward = false;
+    return;
+  }
   launch_relu_bwd(in->dev_grad.get(), (long long)in->rows * in->ld, mask.get(), s.get());
 }
 

@@ -81,6 +81,8 @@ class Module {
   virtual ~Module() {}
 };
 
+class ReLU;
+
 // Shared per-GCN state the modules read (current split, comm, profiling, RNG table).
 struct ModuleContext {
   bool train_ahead = true;     // eval computes the next training forward's first product too
@@ -153,6 +155,12 @@ class Dropout : public Module {
   bool drawn_ahead() const { return ahead; }
   void wait_ahead(hipStream_t s) const;
   const uint64_t *mask_ahead() const { return rng->mask_ahead.get(); }
+  // Fused into the GraphSum next to it (GraphSum::forward/backward apply this module's work in
+  // their epilogue): the training forward's mask is drawn by draw_fused(), and the next
+  // forward / backward call of this module is skipped.
+  const Variable *variable() const { return in.get(); }
+  void draw_fused(hipStream_t s) const;
+  mutable bool skip_forward = false, skip_backward = false;
 
  private:
   void draw(hipStream_t s, uint64_t *mask, int max_blocks = 0) const;
@@ -203,11 +211,24 @@ class GraphSum : public Module {
            ModuleContext *ctx_, bool last_layer_ = false);
   void forward(bool training, const Stream &s) const override;
   void backward(const Stream &s) const override;
+  const Variable *input() const { return in.get(); }
+  const Variable *output() const { return out.get(); }
+  // Element-wise tails fused into this GraphSum's final writes (GCN::fuse_epilogues; null: the
+  // modules run on their own): forward, the ReLU (and Dropout) on `out` that follow it;
+  // backward, the Dropout (and ReLU) on `in` whose backward follows it
+  ReLU *fwd_relu = nullptr;
+  const Dropout *fwd_drop = nullptr;
+  ReLU *bwd_relu = nullptr;
+  const Dropout *bwd_drop = nullptr;
 
  private:
   // mode (edge-cut output layer): 0 all rows, 1 forward over ctx->chunk_split_graphs (the
   // split's rows), 2 backward over ctx->chunk_col_graphs (the split's columns)
-  void run(const float *src, float *dst, const Stream &s, int mode = 0) const;
+  void run(const float *src, float *dst, const Stream &s, int mode = 0,
+           const GsEpilogue *epi = nullptr) const;
+  // the fused tails of this call (mode 0 when none applies)
+  GsEpilogue forward_epilogue(bool training, const Stream &s, const DevGraph *g) const;
+  GsEpilogue backward_epilogue(const DevGraph *g) const;
 };
 
 // include/module.cuh:90-99
@@ -219,6 +240,9 @@ class ReLU : public Module {
   explicit ReLU(shared_ptr<Variable> in_);
   void forward(bool training, const Stream &s) const override;
   void backward(const Stream &s) const override;
+  const Variable *variable() const { return in.get(); }
+  uint8_t *mask_ptr() const { return const_cast<uint8_t *>(mask.get()); }
+  mutable bool skip_forward = false, skip_backward = false;  // done by a GraphSum epilogue
 };
 
 // include/module.cuh:103-124: c = a * b

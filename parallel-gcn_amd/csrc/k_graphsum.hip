@@ -19,6 +19,7 @@
 // a fixed xor-tree => deterministic.  Each item writes its partial row to a slot; a combine
 // kernel adds a row's slots in slot order (skipped for rows that are one whole item).
 #include "common.hpp"
+#include "gs_epilogue.hpp"
 #include "kernels.hpp"
 
 namespace pgcn {
@@ -47,7 +48,7 @@ __global__ __launch_bounds__(256) void k_graphsum(const int4 *__restrict__ items
                                                   const float *__restrict__ vals,
                                                   const float4 *__restrict__ in, int ld4_in,
                                                   float4 *__restrict__ out, int ld4_out,
-                                                  float4 *__restrict__ partial) {
+                                                  float4 *__restrict__ partial, GsEpilogue epi) {
   constexpr int NB = G / VEC;  // neighbours per group per iteration
   constexpr int IPW = 64 / G;  // items per wave
   constexpr bool POW2 = (VEC & (VEC - 1)) == 0;
@@ -103,10 +104,12 @@ __global__ __launch_bounds__(256) void k_graphsum(const int4 *__restrict__ items
       acc = tot;
     }
     if (nb == 0) {
-      if (item.w < 0)
+      if (item.w < 0) {
+        gs_epilogue(acc, item.x, 4 * v, epi);
         out[(long long)item.x * ld4_out + v] = acc;
-      else
+      } else {
         partial[(long long)item.w * VEC + v] = acc;
+      }
     }
   }
 }
@@ -140,7 +143,8 @@ __global__ __launch_bounds__(256) void k_graphsum16(const int4 *__restrict__ ite
                                                     const float *__restrict__ vals,
                                                     const float4 *__restrict__ in, int ld4_in,
                                                     float4 *__restrict__ out, int ld4_out,
-                                                    float4 *__restrict__ partial) {
+                                                    float4 *__restrict__ partial,
+                                                    GsEpilogue epi) {
   const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
   const int q = lane >> 4, r = lane & 15;
   const int nb = r >> 2, v = r & 3;
@@ -188,10 +192,12 @@ __global__ __launch_bounds__(256) void k_graphsum16(const int4 *__restrict__ ite
     acc = f4_add(acc, f4_shfl_xor(acc, 4));
     acc = f4_add(acc, f4_shfl_xor(acc, 8));
     if (nb == 0) {
-      if (item.w < 0)
+      if (item.w < 0) {
+        gs_epilogue(acc, item.x, 4 * v, epi);
         out[(long long)item.x * ld4_out + v] = acc;
-      else
+      } else {
         partial[(long long)item.w * 4 + v] = acc;
+      }
     }
   }
 }
@@ -205,7 +211,8 @@ __global__ __launch_bounds__(256) void k_graphsum16p(const int4 *__restrict__ it
                                                      const float *__restrict__ vals,
                                                      const float4 *__restrict__ in, int ld4_in,
                                                      float4 *__restrict__ out, int ld4_out,
-                                                     float4 *__restrict__ partial) {
+                                                     float4 *__restrict__ partial,
+                                                     GsEpilogue epi) {
   const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
   const int q = lane >> 4, r = lane & 15;
   const int nb = r >> 2, v = r & 3;
@@ -262,10 +269,12 @@ __global__ __launch_bounds__(256) void k_graphsum16p(const int4 *__restrict__ it
       float4 t = f4_add(acc, f4_shfl_xor(acc, 4));
       t = f4_add(t, f4_shfl_xor(t, 8));
       if (nb == 0) {
-        if (item.w < 0)
+        if (item.w < 0) {
+          gs_epilogue(t, item.x, 4 * v, epi);
           out[(long long)item.x * ld4_out + v] = t;
-        else
+        } else {
           partial[(long long)item.w * 4 + v] = t;
+        }
       }
       acc = make_float4(0.f, 0.f, 0.f, 0.f);
       if (!more) break;
@@ -282,7 +291,8 @@ template <int VEC>
 __global__ __launch_bounds__(256) void k_graphsum_combine(const int4 *__restrict__ comb,
                                                           int n_comb,
                                                           const float4 *__restrict__ partial,
-                                                          float4 *__restrict__ out, int ld4_out) {
+                                                          float4 *__restrict__ out, int ld4_out,
+                                                          GsEpilogue epi) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long ci = t / VEC;
   const int v = (int)(t - ci * VEC);
@@ -290,6 +300,7 @@ __global__ __launch_bounds__(256) void k_graphsum_combine(const int4 *__restrict
   const int4 c = comb[ci];  // {row, first_slot, count, -}
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int s = 0; s < c.z; s++) acc = f4_add(acc, partial[(long long)(c.y + s) * VEC + v]);
+  gs_epilogue(acc, c.x, 4 * v, epi);
   out[(long long)c.x * ld4_out + v] = acc;
 }
 
@@ -298,7 +309,7 @@ int g_graphsum_variant = 0;  // diagnostics only (pgcn_debug_set)
 template <int VEC, int G>
 static void launch_vec(const GraphSchedule &s, const int *indices, const float *vals,
                        const float *in, int ld_in, float *out, int ld_out, float *partial,
-                       hipStream_t st) {
+                       hipStream_t st, const GsEpilogue &epi) {
   if (s.n_items > 0) {
     constexpr int per_wg = 4 * (64 / G);  // items one workgroup takes per sweep
     long long per_block = ceil_div(s.max_block_items, per_wg);
@@ -311,7 +322,7 @@ static void launch_vec(const GraphSchedule &s, const int *indices, const float *
                      0, st, s.items, s.block_items, s.nbc, indices, vals,                   \
                      reinterpret_cast<const float4 *>(in), ld_in / 4,                       \
                      reinterpret_cast<float4 *>(out), ld_out / 4,                           \
-                     reinterpret_cast<float4 *>(partial))
+                     reinterpret_cast<float4 *>(partial), epi)
     if (g_graphsum_variant == 1 && VEC == 4) GS_LAUNCH(1);
     else if (g_graphsum_variant == 2 && VEC == 4) GS_LAUNCH(2);
     else if (VEC == 4 && s.nbc > 1 && g_graphsum_variant != 3) {
@@ -320,7 +331,7 @@ static void launch_vec(const GraphSchedule &s, const int *indices, const float *
                      s.items, s.block_items, s.nbc, indices, vals,                        \
                      reinterpret_cast<const float4 *>(in), ld_in / 4,                     \
                      reinterpret_cast<float4 *>(out), ld_out / 4,                         \
-                     reinterpret_cast<float4 *>(partial))
+                     reinterpret_cast<float4 *>(partial), epi)
       if (g_graphsum_variant == 11) GS16(1);
       else if (g_graphsum_variant == 14) GS16(4);
       else if (g_graphsum_variant != 6) GS16(0);
@@ -329,7 +340,7 @@ static void launch_vec(const GraphSchedule &s, const int *indices, const float *
                            s.items, s.block_items, s.nbc, indices, vals,
                            reinterpret_cast<const float4 *>(in), ld_in / 4,
                            reinterpret_cast<float4 *>(out), ld_out / 4,
-                           reinterpret_cast<float4 *>(partial));
+                           reinterpret_cast<float4 *>(partial), epi);
 #undef GS16
     }
     else GS_LAUNCH(0);
@@ -340,7 +351,7 @@ static void launch_vec(const GraphSchedule &s, const int *indices, const float *
     hipLaunchKernelGGL(k_graphsum_combine<VEC>, dim3((unsigned)ceil_div(threads, 256)),
                        dim3(256), 0, st, s.comb, s.n_comb,
                        reinterpret_cast<const float4 *>(partial), reinterpret_cast<float4 *>(out),
-                       ld_out / 4);
+                       ld_out / 4, epi);
   }
 }
 
@@ -352,11 +363,13 @@ int graphsum_group_lanes(int vec) {
 
 void launch_graphsum(const GraphSchedule &s, const int *indices, const float *vals,
                      const float *in, int ld_in, float *out, int ld_out, float *partial,
-                     hipStream_t st) {
+                     hipStream_t st, const GsEpilogue *epi) {
+  const GsEpilogue none{};
+  const GsEpilogue &e = epi ? *epi : none;
   switch (s.vec) {
 #define PGCN_VEC_CASE(V, G) \
   case V:                   \
-    launch_vec<V, G>(s, indices, vals, in, ld_in, out, ld_out, partial, st); break;
+    launch_vec<V, G>(s, indices, vals, in, ld_in, out, ld_out, partial, st, e); break;
     PGCN_VEC_CASE(1, 16) PGCN_VEC_CASE(2, 16) PGCN_VEC_CASE(3, 64) PGCN_VEC_CASE(4, 16)
     PGCN_VEC_CASE(5, 64) PGCN_VEC_CASE(6, 64) PGCN_VEC_CASE(7, 64) PGCN_VEC_CASE(8, 32)
     PGCN_VEC_CASE(9, 64) PGCN_VEC_CASE(10, 64) PGCN_VEC_CASE(11, 64) PGCN_VEC_CASE(12, 64)

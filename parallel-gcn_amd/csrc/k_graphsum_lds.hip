@@ -636,7 +636,8 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_lds(
 __global__ __launch_bounds__(256) void k_gs_lds_combine(const float4 *__restrict__ partial,
                                                         long long part_stride, int nb,
                                                         const float *__restrict__ scale, int n,
-                                                        float4 *__restrict__ out, int ld4_out) {
+                                                        float4 *__restrict__ out, int ld4_out,
+                                                        GsEpilogue epi) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long r = t >> 2;
   if (r >= n) return;
@@ -648,6 +649,7 @@ __global__ __launch_bounds__(256) void k_gs_lds_combine(const float4 *__restrict
   a.y *= s;
   a.z *= s;
   a.w *= s;
+  gs_epilogue(a, r, 4 * v, epi);
   out[r * ld4_out + v] = a;
 }
 
@@ -679,7 +681,7 @@ long long lds_stamps_read(void *dst, long long max_elems) {
 
 void launch_graphsum_lds(const LdsSchedule &s, const float *in, int ld_in, float *out,
                          int ld_out, float *scratch_in, float *partial, hipStream_t st,
-                         const int *col_map) {
+                         const int *col_map, const GsEpilogue *epi) {
   PGCN_CHECK(ld_in % 4 == 0 && ld_out % 4 == 0, PGCN_E_INVALID, "graphsum_lds: ld % 4");
   const long long pre = (long long)s.n_cols * 4;
   hipLaunchKernelGGL(k_gs_prescale, dim3((unsigned)ceil_div(pre, 256)), dim3(256), 0, st,
@@ -722,16 +724,17 @@ void launch_graphsum_lds(const LdsSchedule &s, const float *in, int ld_in, float
     }
   }
 #undef GS_LDS
-  launch_gs_lds_combine(s, partial, out, ld_out, st);
+  launch_gs_lds_combine(s, partial, out, ld_out, st, epi);
 }
 
 void launch_gs_lds_combine(const LdsSchedule &s, const float *partial, float *out, int ld_out,
-                           hipStream_t st) {
+                           hipStream_t st, const GsEpilogue *epi) {
+  const GsEpilogue none{};
   const long long post = (long long)s.n_rows * 4;
   hipLaunchKernelGGL(k_gs_lds_combine, dim3((unsigned)ceil_div(post, 256)), dim3(256), 0, st,
                      reinterpret_cast<const float4 *>(partial), (long long)s.n_rows,
                      s.n_blocks, s.row_scale, s.n_rows, reinterpret_cast<float4 *>(out),
-                     ld_out / 4);
+                     ld_out / 4, epi ? *epi : none);
   PGCN_HIP(hipGetLastError());
 }
 

@@ -18,6 +18,7 @@
 // v-1 (the last reader of the slice that buffer held), with the counts of visit v+1.  Entries
 // are 16-bit plane offsets (ring row x 16 B): lane (g, v) reads plane v at entry + plane base.
 #include "common.hpp"
+#include "gs_epilogue.hpp"
 #include "kernels.hpp"
 #include "lds_dma.hpp"
 
@@ -35,7 +36,7 @@ constexpr int RING_ESLOTS = 4;                              // chunks: 3 in flig
 constexpr int RING_ERING_B = RING_ESLOTS * RING_CHUNK;
 constexpr int RING_TOTAL_B = RING_ERING_OFF + LDS_CW * RING_ERING_B;  // 163,072 B
 static_assert(RING_TOTAL_B <= 160 * 1024, "LDS budget");
-static_assert(RING_FLAG_OFF + 5 * 4 <= RING_CNT_OFF + RING_CNT_B, "hand-off words fit");
+static_assert(RING_FLAG_OFF + 6 * 4 <= RING_CNT_OFF + RING_CNT_B, "hand-off + arrival words fit");
 static_assert(RING_SR * 16 == 8192, "a slice's plane piece is 8 x 1-KB LDS-DMA pieces");
 static_assert(RING_K * RING_SR * 16 + 4 * 16 <= 65536, "ring rows addressable by 16 bits");
 
@@ -68,13 +69,111 @@ extern int g_graphsum_lds_diag;
 unsigned long long *lds_stamps(long long n_wg);
 __device__ __forceinline__ unsigned long long ring_clk() { return __builtin_amdgcn_s_memtime(); }
 
+
+// Fused combine (arrive != null): the last of a batch's n_blocks workgroups to finish adds the
+// batch's rows' block partials in block order, scales them by s_i, applies the epilogue and
+// writes the output -- k_gs_lds_combine's arithmetic, bit for bit, without its launch.
+// Hand-off (MI355X_MICROARCH.md "visibility", valid-forms table row 1; no fences):
+//   * the partials are stored write-through (16-B sc1 stores) and every storing wave drains
+//     them (vmcnt(0)) before the workgroup barrier;
+//   * then ONE lane adds 1 to the batch's counter (agent-scope atomic); the workgroup whose add
+//     returns n_blocks - 1 is the last, tells its waves through an LDS word behind a second
+//     barrier, and resets the counter for the next call (kernels on one stream are ordered);
+//   * every load of the partials there is an sc1 load (bypasses the CU's L1).
+// No workgroup waits for another: a workgroup that is not last exits.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ring_part_rsrc(const float4 *partial,
+                                                                 long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float4 *>(partial), 0, (int)bytes,
+                                           0x00020000);
+}
+typedef unsigned ring_u4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void ring_st_sc1(__amdgpu_buffer_rsrc_t rs, unsigned off, float4 a) {
+  const ring_u4 u = {__float_as_uint(a.x), __float_as_uint(a.y), __float_as_uint(a.z),
+                     __float_as_uint(a.w)};
+  __builtin_amdgcn_raw_buffer_store_b128(u, rs, off, 0, 16);  // aux 16 = sc1
+}
+__device__ __forceinline__ float4 ring_ld_sc1(__amdgpu_buffer_rsrc_t rs, unsigned off) {
+  const ring_u4 u = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);
+  return make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z),
+                     __uint_as_float(u.w));
+}
+
+__device__ __forceinline__ void ring_combine_tail(int *__restrict__ arrive, int batch, int nb,
+                                                  unsigned *flags, int wave, int g, int v,
+                                                  const int *__restrict__ rows,
+                                                  __amdgpu_buffer_rsrc_t prs, long long part_stride,
+                                                  const float *__restrict__ row_scale,
+                                                  float4 *__restrict__ out, int ld4_out,
+                                                  const GsEpilogue &epi) {
+  if (!arrive) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 partial stores drained
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int old = __hip_atomic_fetch_add(arrive + batch, 1, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned last = old == nb - 1;
+    if (last) __hip_atomic_store(arrive + batch, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flags[5] = last;
+  }
+  __syncthreads();
+  if (!flags[5] || wave == LDS_CW) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // loads stay below the barrier
+  const int *rw = rows + (((long long)batch * LDS_CW + wave) * LDS_SLOTS) * 16 + g;
+  const unsigned bstride = (unsigned)part_stride * 64u;
+  // 4 rowsets at a time, 4 blocks' partials of each in flight (16 loads), added in block order
+  for (int j0 = 0; j0 < LDS_SLOTS; j0 += 4) {
+    int rr[4];
+    bool ok[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int u = rw[(j0 + q) * 16];
+      const int sp = (int)((unsigned)u >> 28);
+      rr[q] = u & kRingRowMask;
+      ok[q] = rr[q] != kRingEmpty && (g & ((1 << sp) - 1)) == 0;
+    }
+    float4 acc[4];
+    for (int b0 = 0; b0 < nb; b0 += 4) {
+      float4 t[4][4];
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int bb = 0; bb < 4; bb++)
+          t[q][bb] = ok[q] && b0 + bb < nb
+                         ? ring_ld_sc1(prs, (unsigned)(b0 + bb) * bstride +
+                                                ((unsigned)rr[q] * 4u + (unsigned)v) * 16u)
+                         : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int bb = 0; bb < 4; bb++) {
+          if (b0 + bb >= nb) continue;
+          if (b0 + bb == 0) acc[q] = t[q][0];
+          else f4_acc(acc[q], t[q][bb]);
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      if (!ok[q]) continue;
+      float4 a = acc[q];
+      const float s = row_scale[rr[q]];
+      a.x *= s;
+      a.y *= s;
+      a.z *= s;
+      a.w *= s;
+      gs_epilogue(a, rr[q], 4 * v, epi);
+      out[(long long)rr[q] * ld4_out + v] = a;
+    }
+  }
+}
+
 template <int DIAG>
 __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
     const uint2 *__restrict__ entries, const long long *__restrict__ wave_off,
     const unsigned short *__restrict__ counts, int t_max, const int2 *__restrict__ slices,
     const int *__restrict__ n_slices, const int *__restrict__ rows, const char *__restrict__ table,
     float4 *__restrict__ partial, long long part_stride, int n_blocks,
-    unsigned long long *__restrict__ stamps, int prio) {
+    unsigned long long *__restrict__ stamps, int prio, int *__restrict__ arrive,
+    const float *__restrict__ row_scale, float4 *__restrict__ out, int ld4_out, GsEpilogue epi) {
   __shared__ float4 lds[RING_TOTAL_B / 16];
   unsigned long long st_loop = 0, st_wait = 0, st_ring = 0;
   const int nb = n_blocks;
@@ -143,6 +242,9 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
         o[4] = T;
       }
     }
+    ring_combine_tail(arrive, batch, nb, flags, wave, g, v, rows,
+                      ring_part_rsrc(partial, (long long)nb * part_stride * 64), part_stride,
+                      row_scale, out, ld4_out, epi);
     return;
   }
 
@@ -265,6 +367,8 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
   // writing lane group g % m == 0); m is uniform per rowset
   const int *rw = rows + (((long long)batch * LDS_CW + wave) * LDS_SLOTS) * 16 + g;
   float4 *pb = partial + (long long)b * part_stride * 4 + v;
+  const __amdgpu_buffer_rsrc_t prs = ring_part_rsrc(partial, (long long)n_blocks * part_stride * 64);
+  const unsigned pb_off = ((unsigned)b * (unsigned)part_stride * 4u + (unsigned)v) * 16u;
 #pragma unroll
   for (int j = 0; j < LDS_SLOTS; j++) {
     const int u = rw[j * 16];
@@ -278,17 +382,27 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
       a.w += __shfl_xor(a.w, d);
     }
     const int r = u & kRingRowMask;
-    if (r != kRingEmpty && (g & ((1 << sp) - 1)) == 0) pb[(long long)r * 4] = a;
+    if (r != kRingEmpty && (g & ((1 << sp) - 1)) == 0) {
+      if (arrive) ring_st_sc1(prs, pb_off + (unsigned)r * 64u, a);  // read by another XCD
+      else pb[(long long)r * 4] = a;
+    }
   }
+  ring_combine_tail(arrive, batch, nb, flags, wave, g, v, rows, prs, part_stride, row_scale,
+                    out, ld4_out, epi);
 }
 
 // "graphsum_ring_prio": 1 = waves that finished a visit last run the next one at raised
 // issue priority (see the summing loop), 0 = fixed priority
 int g_graphsum_ring_prio = 1;
+// "graphsum_ring_fused": 1 = the batch's last workgroup combines the block partials (no
+// k_gs_lds_combine launch), 0 = separate combine kernel.  Off: correct (bit-identical, tested)
+// but slower on reddit-114M, 0.263 vs 0.230 ms per call (r02): the combine of all 61 batches
+// then runs at the kernel's end on 61 CUs instead of over the whole chip
+int g_graphsum_ring_fused = 0;
 
 void launch_graphsum_ring(const LdsSchedule &s, const float *in, int ld_in, float *out,
                           int ld_out, float *scratch_in, float *partial, hipStream_t st,
-                          const int *col_map) {
+                          const int *col_map, const GsEpilogue *epi) {
   PGCN_CHECK(ld_in % 4 == 0 && ld_out % 4 == 0, PGCN_E_INVALID, "graphsum_ring: ld % 4");
   PGCN_CHECK(s.window == kRingWindow, PGCN_E_INVALID, "graphsum_ring: not a ring schedule");
   const long long pre = (long long)s.n_cols * 4;
@@ -296,12 +410,15 @@ void launch_graphsum_ring(const LdsSchedule &s, const float *in, int ld_in, floa
                      reinterpret_cast<const float4 *>(in), ld_in / 4, s.col_scale, s.n_cols,
                      reinterpret_cast<float4 *>(scratch_in), col_map);
   const long long n_wg = (long long)s.n_batches * s.n_blocks;
+  const GsEpilogue none{};
+  int *arrive = g_graphsum_ring_fused && s.arrive ? s.arrive : nullptr;
 #define GS_RING(D)                                                                            \
   hipLaunchKernelGGL((k_graphsum_ring<D>), dim3((unsigned)n_wg), dim3(LDS_THREADS), 0, st,   \
                      s.entries, s.wave_off, s.counts, s.t_max, s.slices, s.n_slices, s.rows,      \
                      reinterpret_cast<const char *>(scratch_in),                                 \
                      reinterpret_cast<float4 *>(partial), (long long)s.n_rows, s.n_blocks,         \
-                     D == 4 ? lds_stamps(n_wg) : nullptr, g_graphsum_ring_prio)
+                     D == 4 ? lds_stamps(n_wg) : nullptr, g_graphsum_ring_prio, arrive,          \
+                     s.row_scale, reinterpret_cast<float4 *>(out), ld_out / 4, epi ? *epi : none)
   switch (g_graphsum_lds_diag) {
     case 1: GS_RING(1); break;
     case 2: GS_RING(2); break;
@@ -312,7 +429,8 @@ void launch_graphsum_ring(const LdsSchedule &s, const float *in, int ld_in, floa
     default: GS_RING(0); break;
   }
 #undef GS_RING
-  launch_gs_lds_combine(s, partial, out, ld_out, st);
+  if (!arrive) launch_gs_lds_combine(s, partial, out, ld_out, st, epi);
+  PGCN_HIP(hipGetLastError());
 }
 
 }  // namespace pgcn

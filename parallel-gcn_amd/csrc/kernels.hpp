@@ -6,6 +6,8 @@
 #include <cstddef>
 #include <cstdint>
 
+#include "gs_epilogue.hpp"
+
 namespace pgcn {
 
 // GraphSum work schedule for one row width (VEC float4 per row); device arrays.
@@ -25,7 +27,7 @@ int graphsum_group_lanes(int vec);
 
 void launch_graphsum(const GraphSchedule &s, const int *indices, const float *vals,
                      const float *in, int ld_in, float *out, int ld_out, float *partial,
-                     hipStream_t st);
+                     hipStream_t st, const GsEpilogue *epi = nullptr);
 bool graphsum_vec_supported(int vec);
 
 // ---- d = 16 GraphSum with LDS-staged feature slices (k_graphsum_lds.hip) ----------------
@@ -64,16 +66,19 @@ struct LdsSchedule {
   // the lanes whose edge belongs to slot J+1 (the others add into slot J)
   int window = 1;
   const uint64_t *masks = nullptr;           // [kb][4]
+  // ring schedule: per batch, the arrivals of its column blocks' workgroups (zeroed; the
+  // fused combine of k_graphsum_ring leaves it zeroed)
+  int *arrive = nullptr;
 };
 // ring schedule (window == kRingWindow): scratch_in holds ceil(n_cols / RING_SR) slices
 void launch_graphsum_ring(const LdsSchedule &s, const float *in, int ld_in, float *out,
                           int ld_out, float *scratch_in, float *partial, hipStream_t st,
-                          const int *col_map = nullptr);
+                          const int *col_map = nullptr, const GsEpilogue *epi = nullptr);
 void launch_gs_lds_combine(const LdsSchedule &s, const float *partial, float *out, int ld_out,
-                           hipStream_t st);
+                           hipStream_t st, const GsEpilogue *epi = nullptr);
 void launch_graphsum_lds(const LdsSchedule &s, const float *in, int ld_in, float *out,
                          int ld_out, float *scratch_in, float *partial, hipStream_t st,
-                         const int *col_map = nullptr);
+                         const int *col_map = nullptr, const GsEpilogue *epi = nullptr);
 
 void launch_gemm_nn(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
                     int trans_b, float *C, int ldc, const uint64_t *a_mask, long long mask_base,

@@ -405,3 +405,69 @@ def test_part2_configs_match_oracle(datasets, pgcn, name):
         for k, sp in ((1, 1), (3, 2)):
             assert abs(ours[k] - want[k]) * cnt[sp] <= max(2, 0.005 * cnt[sp]), (ours, want)
     g.close()
+
+
+def _fused_run(pgcn, ds, fuse, epochs, **make):
+    with helpers.knobs(pgcn, fuse_epilogue=fuse):
+        g = pgcn.GCN(pgcn.make_params(ds, **make), ds)
+    lines = [g.train_epoch() + g.eval(2) for _ in range(epochs)]
+    g.train_epoch()  # tensors of a training pass: relu/dropout forward and backward
+    out = dict(lines=np.array(lines, np.float32), tails=g.query("fused_tails"),
+               vars=[g.get_var(i) for i in (2, 3, 5)], grads=[g.get_var(i, 1) for i in (1, 3)])
+    g.close()
+    return out
+
+
+@pytest.mark.parametrize("case", ["cora", "cora_h4", "lds_dense"])
+def test_fused_epilogue_bit_identical(loaded, pgcn, case):
+    """ReLU + hidden Dropout in the first GraphSum's final write, and the Dropout + ReLU
+    backward in the output GraphSum's backward (reassociated order, cora_h4 / lds_dense) give
+    the same bits as the separate kernels: epoch lines, weights, the hidden activations and
+    their gradients (gs_epilogue.hpp; plain gather kernels on cora, LDS ring + combine on the
+    dense graph)."""
+    if case == "lds_dense":
+        ds, make, tails = pgcn.Dataset.synthetic(120000, 64, 41, 1500000, 21), {}, 2
+    else:
+        ds = loaded["cora"]
+        make, tails = ({"hidden_dims": (4,)}, 2) if case == "cora_h4" else ({}, 1)
+    on = _fused_run(pgcn, ds, 1, 4, **make)
+    off = _fused_run(pgcn, ds, 0, 4, **make)
+    assert on["tails"] == tails and off["tails"] == 0
+    np.testing.assert_array_equal(on["lines"], off["lines"])
+    for a, b in zip(on["vars"] + on["grads"], off["vars"] + off["grads"]):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_early_stopping_matches_reference(datasets, pgcn):
+    """GCN::run's early stopping (hpdga gcn.cpp:238-250, src/gcn.cu:377-395): after epoch e >=
+    k, stop when val_loss(e) > the mean of the last k val losses (the current one included,
+    summed in float in epoch order).  The reference's cora parameter file (k = 10, 1000 epochs,
+    hidden 72, seed) stops at the epoch the oracle's loss history gives (136); every
+    comparison up to it clears its threshold by >= 3e-4 relative, far above the engine's
+    loss error, so the stop epoch is a parity property."""
+    cfg, k = PART2["cora"], 10
+    root, names = datasets
+    ds = pgcn.Dataset.load(root, names["cora"])
+    ref = helpers.OracleGCN(helpers.ds_dict(ds), hidden_dims=cfg["hidden"],
+                            dropouts=cfg["dropouts"], wd=cfg["wd"], seed=cfg["seed"])
+    hist, stop, margin = [], None, 1.0
+    for epoch in range(1, 1001):
+        ref.train_epoch()
+        vl = np.float32(ref.eval(2)[0])
+        hist.append(vl)
+        if epoch >= k:
+            recent = np.float32(0.0)
+            for i in range(epoch - k, epoch):
+                recent = np.float32(recent + hist[i])
+            thr = np.float32(recent / np.float32(k))
+            margin = min(margin, abs(float(vl) - float(thr)) / float(vl))
+            if vl > thr:
+                stop = epoch
+                break
+    assert stop is not None and margin >= 3e-4, (stop, margin)
+    p = pgcn.make_params(ds, hidden_dims=cfg["hidden"], dropouts=cfg["dropouts"],
+                         weight_decay=cfg["wd"], seed=cfg["seed"], epochs=1000, early_stopping=k)
+    g = pgcn.GCN(p, ds)
+    g.run(verbose=False)
+    assert g.query("epochs") == stop
+    g.close()

@@ -170,6 +170,40 @@ def test_graphsum_lds_wide_rows(pgcn, dim, ld):
     pgcn.lib.pgcn_graph_destroy(g)
 
 
+@pytest.mark.parametrize("blocks", [0, 8, 32])
+def test_graphsum_ring_fused_combine(pgcn, blocks):
+    """Ring schedule with the combine fused into the kernel (the batch's last workgroup adds
+    the column blocks' partials, graphsum_ring_fused 1) against the separate k_gs_lds_combine
+    launch (0): identical bits, over back-to-back calls (the arrival counters reset
+    themselves), at the default 4 blocks and at 8 / 32 blocks (more workgroups per batch)."""
+    assert pgcn.lib.pgcn_debug_set(b"lds_blocks", blocks) == 0
+    try:
+        n, dim = 120000, 16
+        indptr, indices = random_graph(n, 40, seed=11 + blocks, hubs=20, hub_deg=3000)
+        x = torch.randn(n, dim, device=DEV)
+        g = ctypes.c_void_p()
+        pgcn.check(pgcn.lib.pgcn_graph_create(n, helpers.ptr(indptr), helpers.ptr(indices),
+                                              ctypes.byref(g)), "graph_create")
+        outs = {}
+        for fused in (0, 1):
+            pgcn.lib.pgcn_debug_set(b"graphsum_ring_fused", fused)
+            outs[fused] = []
+            for k in range(4):
+                o = torch.full((n, dim), float("nan"), device=DEV)
+                pgcn.check(pgcn.lib.pgcn_graphsum(g, vp(x), dim, vp(o), dim, dim, stream()), "gs")
+                outs[fused].append(o)
+        torch.cuda.synchronize()
+        for o in outs[1] + outs[0][1:]:
+            assert torch.equal(o, outs[0][0])
+        ref = oracle_graphsum(indptr, indices, x.cpu().numpy(), dim)
+        bound = abs_bound(indptr, indices, x.cpu().numpy(), dim)
+        assert (np.abs(outs[1][0].cpu().numpy() - ref) <= 1e-5 * bound + 1e-30).all()
+        pgcn.lib.pgcn_graph_destroy(g)
+    finally:
+        pgcn.lib.pgcn_debug_set(b"graphsum_ring_fused", 0)
+        pgcn.lib.pgcn_debug_set(b"lds_blocks", 0)
+
+
 def test_graphsum_linearity_large(pgcn):
     """Size-independent property at reddit-like density: GraphSum(a x + b y) == a GS(x) + b GS(y)."""
     n = 200000
