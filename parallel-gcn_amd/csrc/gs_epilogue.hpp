@@ -26,6 +26,11 @@ struct GsEpilogue {
   long long drop_base = 0;
   int drop_cols = 0;
   float drop_scale = 1.0f;
+  // the next GraphSum's prescaled input (ring schedule layout, k_ring_prescale): also write
+  // next_scale[r] * y to float4 (r / sr) * 4 sr + (c / 4) sr + r % sr of next_table
+  float4 *next_table = nullptr;
+  const float *next_scale = nullptr;
+  int next_sr = 0;
 };
 
 __device__ __forceinline__ uint32_t gs_epi_bits4(const uint64_t *__restrict__ mask, long long idx) {
@@ -64,6 +69,12 @@ __device__ __forceinline__ void gs_epilogue(float4 &a, long long r, int c0, cons
     if (!(m & 0xff00u)) a.y = 0.0f;
     if (!(m & 0xff0000u)) a.z = 0.0f;
     if (!(m & 0xff000000u)) a.w = 0.0f;
+  }
+  if (e.next_table) {  // as k_ring_prescale computes it from the stored output
+    const float s = e.next_scale[r];
+    const long long sr = e.next_sr;
+    e.next_table[(r / sr) * 4 * sr + (c0 >> 2) * sr + r % sr] =
+        make_float4(a.x * s, a.y * s, a.z * s, a.w * s);
   }
 }
 

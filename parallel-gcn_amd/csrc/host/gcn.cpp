@@ -461,6 +461,10 @@ void GCN::fuse_epilogues() {
         auto *drop = i + 2 < n ? dynamic_cast<Dropout *>(modules[i + 2].get()) : nullptr;
         if (drop && drop->variable() == out) gs->fwd_drop = drop;
         fused_tails_++;
+        // the next forward module reading `out` is a GraphSum (the reassociated output layer)
+        const size_t k = i + (gs->fwd_drop ? 3 : 2);
+        auto *next = k < n ? dynamic_cast<GraphSum *>(modules[k].get()) : nullptr;
+        if (next && next->input() == out) gs->fwd_next = next;
       }
     }
     if (i >= 1 && in->ld == in->cols) {
@@ -471,6 +475,9 @@ void GCN::fuse_epilogues() {
         gs->bwd_relu = relu;
         if (ri + 1 < i) gs->bwd_drop = drop;
         fused_tails_++;
+        // the next backward after ReLU(in)'s is a GraphSum's whose output is `in`
+        auto *next = ri >= 1 ? dynamic_cast<GraphSum *>(modules[ri - 1].get()) : nullptr;
+        if (next && next->output() == in) gs->bwd_next = next;
       }
     }
   }

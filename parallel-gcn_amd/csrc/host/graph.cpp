@@ -939,13 +939,22 @@ bool DevGraph::epilogue_ok(int dim, int ld_in, int ld_out) const {
   return !(dim > 16 && !graphsum_vec_supported((dim + 3) / 4));
 }
 
+float *DevGraph::ring_table(int dim, const float **next_scale) {
+  if (dim > 16 || !uses_lds(dim) || col_map_ || g_graphsum_lds_window != kRingWindow) return nullptr;
+  if (!lds_) build_lds();
+  if (lds_->s.window != kRingWindow) return nullptr;
+  *next_scale = lds_->s.col_scale;
+  return lds_->scratch.get();
+}
+
 void DevGraph::graphsum(const float *in, int ld_in, float *out, int ld_out, int dim,
-                        hipStream_t s, bool compact_in, const GsEpilogue *epi) {
+                        hipStream_t s, bool compact_in, const GsEpilogue *epi, bool prestaged) {
   const int *col_map = compact_in ? nullptr : col_map_.get();
   PGCN_CHECK(ld_in % 4 == 0 && ld_out % 4 == 0 && ld_in >= dim && ld_out >= dim,
              PGCN_E_INVALID, "graphsum: leading dims must be multiples of 4 and >= dim");
   PGCN_CHECK(!epi || epi->mode == 0 || epilogue_ok(dim, ld_in, ld_out), PGCN_E_INVALID,
              "graphsum: epilogue on a multi-pass width");
+  PGCN_CHECK(!prestaged || uses_lds(dim), PGCN_E_INVALID, "graphsum: prestaged input, plain path");
   if (uses_lds(dim)) {
     if (!lds_) build_lds();
     // wider rows: one LDS pass per 16 columns (the last pass overlaps the one before it so it
@@ -953,11 +962,13 @@ void DevGraph::graphsum(const float *in, int ld_in, float *out, int ld_out, int 
     // d = 128 on reddit: 8 passes ~2.7 ms against ~7 ms for the gather kernel, whose 512-B
     // rows come from the Infinity Cache at ~7.7 TB/s
     const int ldm = std::min(ld_in, ld_out);
+    PGCN_CHECK(!prestaged || (dim <= 16 && lds_->s.window == kRingWindow && !col_map),
+               PGCN_E_INVALID, "graphsum: prestaged input on a path without a ring table");
     for (int c0 = 0; c0 < dim; c0 += 16) {
       const int c = std::min(c0, ldm - 16);
       if (lds_->s.window == kRingWindow)
         launch_graphsum_ring(lds_->s, in + c, ld_in, out + c, ld_out, lds_->scratch.get(),
-                             lds_->partial.get(), s, col_map, epi);
+                             lds_->partial.get(), s, col_map, epi, prestaged);
       else
         launch_graphsum_lds(lds_->s, in + c, ld_in, out + c, ld_out, lds_->scratch.get(),
                             lds_->partial.get(), s, col_map, epi);

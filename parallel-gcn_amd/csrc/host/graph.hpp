@@ -79,7 +79,11 @@ class DevGraph {
   // epi: the element-wise tail applied to every output row as it is formed (one pass only:
   // dim <= 16, or a width with a kernel of its own and no 16-column passes)
   void graphsum(const float *in, int ld_in, float *out, int ld_out, int dim, hipStream_t s,
-                bool compact_in = false, const GsEpilogue *epi = nullptr);
+                bool compact_in = false, const GsEpilogue *epi = nullptr, bool prestaged = false);
+  // The ring schedule's prescaled-input table of a graphsum() of this width (one 16-column
+  // pass, no column map), for a producer's epilogue to fill (then graphsum(.., prestaged));
+  // null when this graph does not take that path.  next_scale = the table's column scales.
+  float *ring_table(int dim, const float **next_scale);
   // graphsum() of this width can take an epilogue (one pass over the columns)
   bool epilogue_ok(int dim, int ld_in, int ld_out) const;
   // graphsum() of this width runs the LDS-staged kernel (k_graphsum_lds)

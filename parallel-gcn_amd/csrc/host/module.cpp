@@ -233,6 +233,30 @@ GraphSum::GraphSum(shared_ptr<Variable> in_, shared_ptr<Variable> out_, DevGraph
   }
 }
 
+// "graphsum_prestage": a fused epilogue also writes the next GraphSum's prescaled input
+int g_graphsum_prestage = 1;
+
+DevGraph *GraphSum::forward_graph() const {
+  if (ctx->comm) return nullptr;
+  return last_layer && ctx->split_graph ? ctx->split_graph : graph;
+}
+
+DevGraph *GraphSum::backward_graph() const {
+  if (ctx->comm) return nullptr;
+  return last_layer && ctx->split_colgraph ? ctx->split_colgraph : graph;
+}
+
+void GraphSum::stage_next(GsEpilogue &e, GraphSum *next, DevGraph *ng, bool fwd) const {
+  if (!next || !ng || !g_graphsum_prestage) return;
+  const float *sc = nullptr;
+  float *t = ng->ring_table(next->dim, &sc);
+  if (!t) return;
+  e.next_table = reinterpret_cast<float4 *>(t);
+  e.next_scale = sc;
+  e.next_sr = RING_SR;
+  (fwd ? next->prestaged_fwd : next->prestaged_bwd) = true;
+}
+
 // The fused forward tail: ReLU on `out` (its mask when training), then the hidden Dropout
 // (training), both skipped as modules for this pass.  mode 0 when `g` cannot take an epilogue.
 GsEpilogue GraphSum::forward_epilogue(bool training, const Stream &s, const DevGraph *g) const {
@@ -250,6 +274,7 @@ GsEpilogue GraphSum::forward_epilogue(bool training, const Stream &s, const DevG
     e.drop_scale = fwd_drop->scale();
   }
   fwd_relu->skip_forward = true;
+  if (fwd_next) stage_next(e, fwd_next, fwd_next->forward_graph(), true);
   return e;
 }
 
@@ -270,11 +295,12 @@ GsEpilogue GraphSum::backward_epilogue(const DevGraph *g) const {
     bwd_drop->skip_backward = true;
   }
   bwd_relu->skip_backward = true;
+  if (bwd_next) stage_next(e, bwd_next, bwd_next->backward_graph(), false);
   return e;
 }
 
 void GraphSum::run(const float *src, float *dst, const Stream &s, int mode,
-                   const GsEpilogue *epi) const {
+                   const GsEpilogue *epi, bool prestaged) const {
   Event e0, e1;
   if (ctx->profile) {
     e0 = Event::create(true);
@@ -314,7 +340,7 @@ void GraphSum::run(const float *src, float *dst, const Stream &s, int mode,
     reduced.record(ctx->comm_stream);
     reduced.wait_on(s.get());  // dst complete, partials free for the next call
   } else {
-    graph->graphsum(src, in->ld, dst, out->ld, dim, s.get(), false, epi);
+    graph->graphsum(src, in->ld, dst, out->ld, dim, s.get(), false, epi, prestaged);
     bytes = graph->algorithmic_bytes(dim);
     if (ctx->profile) e1.record(s.get());
   }
@@ -325,6 +351,10 @@ void GraphSum::run(const float *src, float *dst, const Stream &s, int mode,
 }
 
 void GraphSum::forward(bool training, const Stream &s) const {
+  const bool pre = prestaged_fwd;  // this call's input table was written by the producer
+  prestaged_fwd = false;
+  PGCN_CHECK(!pre || (!ctx->comm && (training || !first_layer)), PGCN_E_INVALID,
+             "graphsum: prestaged input on a path that does not read it");
   if (!training && first_layer) return;  // eval_ax: SparseMatmul wrote Â X W1 already
   if (last_layer && ctx->comm && !ctx->chunk_split_graphs.empty()) {
     run(in->dev_data.get(), out->dev_data.get(), s, 1);
@@ -333,7 +363,7 @@ void GraphSum::forward(bool training, const Stream &s) const {
   DevGraph *sg = last_layer && !ctx->comm ? ctx->split_graph : nullptr;
   if (!sg) {
     const GsEpilogue epi = forward_epilogue(training, s, graph);
-    run(in->dev_data.get(), out->dev_data.get(), s, 0, &epi);
+    run(in->dev_data.get(), out->dev_data.get(), s, 0, &epi, pre);
     return;
   }
   // output layer: only the split's labelled rows, summed compactly and scattered to their
@@ -353,7 +383,7 @@ void GraphSum::forward(bool training, const Stream &s) const {
     e1 = Event::create(true);
     e0.record(s.get());
   }
-  sg->graphsum(in->dev_data.get(), in->ld, dst, out->ld, dim, s.get());
+  sg->graphsum(in->dev_data.get(), in->ld, dst, out->ld, dim, s.get(), false, nullptr, pre);
   if (ctx->profile) {
     e1.record(s.get());
     ctx->gs_events->emplace_back(e0, e1);
@@ -365,6 +395,9 @@ void GraphSum::forward(bool training, const Stream &s) const {
 
 void GraphSum::backward(const Stream &s) const {
   // the same gather on grads (Â symmetric): in.grad = Â out.grad (module.cpp:98-111)
+  const bool pre = prestaged_bwd;  // out.grad's input table was written by its producer
+  prestaged_bwd = false;
+  PGCN_CHECK(!pre || !ctx->comm, PGCN_E_INVALID, "graphsum: prestaged gradient, edge-cut");
   if (last_layer && ctx->comm && !ctx->chunk_col_graphs.empty()) {
     // edge-cut: out.grad is zero outside the training split's rows, so each chunk graph keeps
     // only the edges from those columns (all rows stay: the partials are written whole)
@@ -374,7 +407,7 @@ void GraphSum::backward(const Stream &s) const {
   DevGraph *cg = last_layer && !ctx->comm ? ctx->split_colgraph : nullptr;
   if (!cg) {
     const GsEpilogue epi = backward_epilogue(graph);
-    run(out->dev_grad.get(), in->dev_grad.get(), s, 0, &epi);
+    run(out->dev_grad.get(), in->dev_grad.get(), s, 0, &epi, pre);
     return;
   }
   // output layer: out.grad is the loss gradient, zero outside the split's labelled rows, so
@@ -389,7 +422,8 @@ void GraphSum::backward(const Stream &s) const {
   // as its columns directly; else it gathers them from the full rows)
   const float *g_in = ctx->compact_n ? ctx->compact_z->dev_grad.get() : out->dev_grad.get();
   const GsEpilogue epi = backward_epilogue(cg);
-  cg->graphsum(g_in, out->ld, in->dev_grad.get(), in->ld, dim, s.get(), ctx->compact_n > 0, &epi);
+  cg->graphsum(g_in, out->ld, in->dev_grad.get(), in->ld, dim, s.get(), ctx->compact_n > 0, &epi,
+               pre);
   if (ctx->profile) {
     e1.record(s.get());
     ctx->gs_events->emplace_back(e0, e1);

@@ -220,12 +220,22 @@ class GraphSum : public Module {
   const Dropout *fwd_drop = nullptr;
   ReLU *bwd_relu = nullptr;
   const Dropout *bwd_drop = nullptr;
+  // ... and the GraphSum that reads this one's fused output next (forward: `out`; backward:
+  // in.grad): the epilogue also writes its prescaled input table (ring schedule), so that
+  // GraphSum skips its prescale launch (prestaged_*, consumed by its next call)
+  GraphSum *fwd_next = nullptr, *bwd_next = nullptr;
+  mutable bool prestaged_fwd = false, prestaged_bwd = false;
+  // the graph this module's next forward / backward sums over (single GPU)
+  DevGraph *forward_graph() const;
+  DevGraph *backward_graph() const;
 
  private:
   // mode (edge-cut output layer): 0 all rows, 1 forward over ctx->chunk_split_graphs (the
   // split's rows), 2 backward over ctx->chunk_col_graphs (the split's columns)
   void run(const float *src, float *dst, const Stream &s, int mode = 0,
-           const GsEpilogue *epi = nullptr) const;
+           const GsEpilogue *epi = nullptr, bool prestaged = false) const;
+  // points the epilogue's next_table at `next`'s input table on graph `ng`, if it has one
+  void stage_next(GsEpilogue &e, GraphSum *next, DevGraph *ng, bool fwd) const;
   // the fused tails of this call (mode 0 when none applies)
   GsEpilogue forward_epilogue(bool training, const Stream &s, const DevGraph *g) const;
   GsEpilogue backward_epilogue(const DevGraph *g) const;

@@ -402,16 +402,19 @@ int g_graphsum_ring_fused = 0;
 
 void launch_graphsum_ring(const LdsSchedule &s, const float *in, int ld_in, float *out,
                           int ld_out, float *scratch_in, float *partial, hipStream_t st,
-                          const int *col_map, const GsEpilogue *epi) {
+                          const int *col_map, const GsEpilogue *epi, bool prestaged) {
   PGCN_CHECK(ld_in % 4 == 0 && ld_out % 4 == 0, PGCN_E_INVALID, "graphsum_ring: ld % 4");
   PGCN_CHECK(s.window == kRingWindow, PGCN_E_INVALID, "graphsum_ring: not a ring schedule");
   const long long pre = (long long)s.n_cols * 4;
-  hipLaunchKernelGGL(k_ring_prescale, dim3((unsigned)ceil_div(pre, 256)), dim3(256), 0, st,
-                     reinterpret_cast<const float4 *>(in), ld_in / 4, s.col_scale, s.n_cols,
-                     reinterpret_cast<float4 *>(scratch_in), col_map);
+  if (!prestaged)
+    hipLaunchKernelGGL(k_ring_prescale, dim3((unsigned)ceil_div(pre, 256)), dim3(256), 0, st,
+                       reinterpret_cast<const float4 *>(in), ld_in / 4, s.col_scale, s.n_cols,
+                       reinterpret_cast<float4 *>(scratch_in), col_map);
   const long long n_wg = (long long)s.n_batches * s.n_blocks;
   const GsEpilogue none{};
-  int *arrive = g_graphsum_ring_fused && s.arrive ? s.arrive : nullptr;
+  // (an epilogue that stages the next GraphSum's input may write this call's own table: that
+  // needs the separate combine, after every workgroup has read it)
+  int *arrive = g_graphsum_ring_fused && s.arrive && !(epi && epi->next_table) ? s.arrive : nullptr;
 #define GS_RING(D)                                                                            \
   hipLaunchKernelGGL((k_graphsum_ring<D>), dim3((unsigned)n_wg), dim3(LDS_THREADS), 0, st,   \
                      s.entries, s.wave_off, s.counts, s.t_max, s.slices, s.n_slices, s.rows,      \

@@ -71,9 +71,12 @@ struct LdsSchedule {
   int *arrive = nullptr;
 };
 // ring schedule (window == kRingWindow): scratch_in holds ceil(n_cols / RING_SR) slices
+// prestaged: scratch_in already holds this call's prescaled input (written by the epilogue of
+// the GraphSum that produced `in`), the prescale launch is skipped
 void launch_graphsum_ring(const LdsSchedule &s, const float *in, int ld_in, float *out,
                           int ld_out, float *scratch_in, float *partial, hipStream_t st,
-                          const int *col_map = nullptr, const GsEpilogue *epi = nullptr);
+                          const int *col_map = nullptr, const GsEpilogue *epi = nullptr,
+                          bool prestaged = false);
 void launch_gs_lds_combine(const LdsSchedule &s, const float *partial, float *out, int ld_out,
                            hipStream_t st, const GsEpilogue *epi = nullptr);
 void launch_graphsum_lds(const LdsSchedule &s, const float *in, int ld_in, float *out,

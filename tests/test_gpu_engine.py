@@ -407,11 +407,11 @@ def test_part2_configs_match_oracle(datasets, pgcn, name):
     g.close()
 
 
-def _fused_run(pgcn, ds, fuse, epochs, **make):
-    with helpers.knobs(pgcn, fuse_epilogue=fuse):
+def _fused_run(pgcn, ds, fuse, epochs, prestage=1, **make):
+    with helpers.knobs(pgcn, fuse_epilogue=fuse, graphsum_prestage=prestage):
         g = pgcn.GCN(pgcn.make_params(ds, **make), ds)
-    lines = [g.train_epoch() + g.eval(2) for _ in range(epochs)]
-    g.train_epoch()  # tensors of a training pass: relu/dropout forward and backward
+        lines = [g.train_epoch() + g.eval(2) for _ in range(epochs)]
+        g.train_epoch()  # tensors of a training pass: relu/dropout forward and backward
     out = dict(lines=np.array(lines, np.float32), tails=g.query("fused_tails"),
                vars=[g.get_var(i) for i in (2, 3, 5)], grads=[g.get_var(i, 1) for i in (1, 3)])
     g.close()
@@ -424,7 +424,8 @@ def test_fused_epilogue_bit_identical(loaded, pgcn, case):
     backward in the output GraphSum's backward (reassociated order, cora_h4 / lds_dense) give
     the same bits as the separate kernels: epoch lines, weights, the hidden activations and
     their gradients (gs_epilogue.hpp; plain gather kernels on cora, LDS ring + combine on the
-    dense graph)."""
+    dense graph, where the epilogue also writes the next GraphSum's prescaled input table and
+    that GraphSum skips its prescale: compared with graphsum_prestage 0 too)."""
     if case == "lds_dense":
         ds, make, tails = pgcn.Dataset.synthetic(120000, 64, 41, 1500000, 21), {}, 2
     else:
@@ -432,10 +433,12 @@ def test_fused_epilogue_bit_identical(loaded, pgcn, case):
         make, tails = ({"hidden_dims": (4,)}, 2) if case == "cora_h4" else ({}, 1)
     on = _fused_run(pgcn, ds, 1, 4, **make)
     off = _fused_run(pgcn, ds, 0, 4, **make)
+    no_stage = _fused_run(pgcn, ds, 1, 4, prestage=0, **make)
     assert on["tails"] == tails and off["tails"] == 0
-    np.testing.assert_array_equal(on["lines"], off["lines"])
-    for a, b in zip(on["vars"] + on["grads"], off["vars"] + off["grads"]):
-        np.testing.assert_array_equal(a, b)
+    for other in (off, no_stage):
+        np.testing.assert_array_equal(on["lines"], other["lines"])
+        for a, b in zip(on["vars"] + on["grads"], other["vars"] + other["grads"]):
+            np.testing.assert_array_equal(a, b)
 
 
 def test_early_stopping_matches_reference(datasets, pgcn):
