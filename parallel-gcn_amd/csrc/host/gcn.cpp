@@ -106,6 +106,97 @@ void glorot_host(std::vector<float> &w, int in_size, int out_size, uint64_t s[2]
 }
 }  // namespace
 
+// hpdga variable.cpp:15-19 (glorot) from the shared xorshift state (GCN and the C++ API)
+void glorot_fill(std::vector<float> &w, int in_size, int out_size, uint64_t s[2]) {
+  glorot_host(w, in_size, out_size, s);
+}
+
+// X on the device for rows [first, first + rows) of a CSR feature matrix (GCN::upload_features;
+// also the public C++ API's SparseMatmul).  dense: [rows][round_up4(F)] fp32 + the X-stream
+// nibble-mask buffer when hidden0 fits the X-stream kernels; sparse: CSR + transposed index.
+void build_dev_features(DevFeatures &feats, const int *fptr, const int *indices,
+                        const float *values, int first, int rows, int F, bool dense, int hidden0) {
+  feats.rows = rows;
+  feats.cols = F;
+  feats.dense = dense;
+  const long long p0 = fptr[(size_t)first], p1 = fptr[(size_t)first + rows];
+  feats.nnz = p1 - p0;
+  if (feats.dense) {
+    feats.ldx = round_up4(F);
+    std::vector<float> x((size_t)rows * feats.ldx, 0.0f);
+    parallel_for(rows, [&](long long b, long long e) {
+      for (long long i = b; i < e; i++)
+        std::memcpy(&x[(size_t)i * feats.ldx], &values[(size_t)(first + i) * F],
+                    sizeof(float) * (size_t)F);
+    });
+    feats.x.allocate(x.size() + 4);
+    feats.x.upload(x);
+    if (xstream_ok(hidden0, F)) {
+      feats.maskT.allocate((size_t)std::max(rows, 1) * 16);
+      feats.maskT.zero();
+    }
+  } else {
+    std::vector<int> ip((size_t)rows + 1);
+    for (int i = 0; i <= rows; i++) ip[(size_t)i] = (int)(fptr[(size_t)first + i] - p0);
+    const int *idx = indices + p0;
+    feats.host_values.assign(values + p0, values + p1);
+    // transposed index for the weight gradient: stable counting sort by feature id
+    std::vector<int> cptr((size_t)F + 1, 0), crow((size_t)feats.nnz), cpos((size_t)feats.nnz);
+    for (long long k = 0; k < feats.nnz; k++) {
+      PGCN_CHECK(idx[k] >= 0 && idx[k] < F, PGCN_E_INVALID, "feature id out of range");
+      cptr[(size_t)idx[k] + 1]++;
+    }
+    for (int f = 0; f < F; f++) cptr[(size_t)f + 1] += cptr[(size_t)f];
+    std::vector<int> fill(cptr.begin(), cptr.end() - 1);
+    for (int i = 0; i < rows; i++)
+      for (int k = ip[(size_t)i]; k < ip[(size_t)i + 1]; k++) {
+        const int o = fill[(size_t)idx[k]]++;
+        crow[(size_t)o] = i;
+        cpos[(size_t)o] = k;
+      }
+    feats.indptr.allocate(ip.size());
+    feats.indptr.upload(ip);
+    feats.indices.allocate((size_t)feats.nnz + 1);
+    feats.indices.upload(idx, (size_t)feats.nnz);
+    feats.values.allocate((size_t)feats.nnz + 1);
+    feats.values.upload(feats.host_values);
+    feats.csc_ptr.allocate(cptr.size());
+    feats.csc_ptr.upload(cptr);
+    feats.csc_row.allocate(crow.size() + 1);
+    feats.csc_row.upload(crow);
+    feats.csc_pos.allocate(cpos.size() + 1);
+    feats.csc_pos.upload(cpos);
+  }
+}
+
+// Chunk states of a dropout over global elements [elem_begin, elem_end) whose first training
+// forward draws stream positions offset + element (hpdga: one xorshift128+ draw per element,
+// module.cpp:208-219), each 64-element chunk's state jumped to from the seed state.
+void init_dropout_rng_range(DropoutRng &r, const uint64_t seed[2], unsigned long long offset,
+                            long long elem_begin, long long elem_end) {
+  r.elem_begin = elem_begin;
+  r.elem_end = elem_end;
+  r.chunk_lo = r.elem_begin / kDropChunk;
+  const long long chunk_hi = ceil_div(r.elem_end, kDropChunk);
+  r.n_chunks = std::max(0LL, chunk_hi - r.chunk_lo);
+  r.mask_base = r.elem_begin - kDropChunk * r.chunk_lo;
+  std::vector<uint64_t> st((size_t)std::max(1LL, r.n_chunks) * 2, 0);
+  const unsigned long long base = offset + (unsigned long long)kDropChunk * r.chunk_lo;
+  parallel_for(r.n_chunks, [&](long long b, long long e) {
+    uint64_t s[2] = {seed[0], seed[1]};
+    xs_jump(s, base + (unsigned long long)kDropChunk * b);
+    for (long long c = b; c < e; c++) {
+      st[(size_t)c * 2] = s[0];
+      st[(size_t)c * 2 + 1] = s[1];
+      for (int k = 0; k < kDropChunk; k++) xs_advance(s);
+    }
+  });
+  r.states.allocate(st.size());
+  r.states.upload(st);
+  r.mask.allocate((size_t)std::max(1LL, r.n_chunks) + 1);
+  r.mask.zero();
+}
+
 GCN::GCN(const GCNParams &params_, const AdamParams &adam, const GCNData &data, int device_,
          const DistSpec *dist)
     : params(params_), adam_params(adam), device(device_) {
@@ -158,61 +249,12 @@ GCN::~GCN() {
 }
 
 void GCN::upload_features(const GCNData &data) {
-  const int first = part.first(), rows = part.local_rows(), F = params.input_dim;
   const auto &fptr = data.feature_index.indptr;
   feat_indptr_global = fptr;
   nnz_x_global = fptr[(size_t)params.num_nodes];
-  feats.rows = rows;
-  feats.cols = F;
-  feats.dense = features_dense(data);
-  const long long p0 = fptr[(size_t)first], p1 = fptr[(size_t)first + rows];
-  feats.nnz = p1 - p0;
-  if (feats.dense) {
-    feats.ldx = round_up4(F);
-    std::vector<float> x((size_t)rows * feats.ldx, 0.0f);
-    parallel_for(rows, [&](long long b, long long e) {
-      for (long long i = b; i < e; i++)
-        std::memcpy(&x[(size_t)i * feats.ldx], &data.feature_value[(size_t)(first + i) * F],
-                    sizeof(float) * (size_t)F);
-    });
-    feats.x.allocate(x.size() + 4);
-    feats.x.upload(x);
-    if (xstream_ok(params.hidden_dims.front(), F)) {
-      feats.maskT.allocate((size_t)std::max(rows, 1) * 16);
-      feats.maskT.zero();
-    }
-  } else {
-    std::vector<int> ip((size_t)rows + 1);
-    for (int i = 0; i <= rows; i++) ip[(size_t)i] = (int)(fptr[(size_t)first + i] - p0);
-    const int *idx = data.feature_index.indices.data() + p0;
-    feats.host_values.assign(data.feature_value.begin() + p0, data.feature_value.begin() + p1);
-    // transposed index for the weight gradient: stable counting sort by feature id
-    std::vector<int> cptr((size_t)F + 1, 0), crow((size_t)feats.nnz), cpos((size_t)feats.nnz);
-    for (long long k = 0; k < feats.nnz; k++) {
-      PGCN_CHECK(idx[k] >= 0 && idx[k] < F, PGCN_E_INVALID, "feature id out of range");
-      cptr[(size_t)idx[k] + 1]++;
-    }
-    for (int f = 0; f < F; f++) cptr[(size_t)f + 1] += cptr[(size_t)f];
-    std::vector<int> fill(cptr.begin(), cptr.end() - 1);
-    for (int i = 0; i < rows; i++)
-      for (int k = ip[(size_t)i]; k < ip[(size_t)i + 1]; k++) {
-        const int o = fill[(size_t)idx[k]]++;
-        crow[(size_t)o] = i;
-        cpos[(size_t)o] = k;
-      }
-    feats.indptr.allocate(ip.size());
-    feats.indptr.upload(ip);
-    feats.indices.allocate((size_t)feats.nnz + 1);
-    feats.indices.upload(idx, (size_t)feats.nnz);
-    feats.values.allocate((size_t)feats.nnz + 1);
-    feats.values.upload(feats.host_values);
-    feats.csc_ptr.allocate(cptr.size());
-    feats.csc_ptr.upload(cptr);
-    feats.csc_row.allocate(crow.size() + 1);
-    feats.csc_row.upload(crow);
-    feats.csc_pos.allocate(cpos.size() + 1);
-    feats.csc_pos.upload(cpos);
-  }
+  build_dev_features(feats, fptr.data(), data.feature_index.indices.data(),
+                     data.feature_value.data(), part.first(), part.local_rows(), params.input_dim,
+                     features_dense(data), params.hidden_dims.front());
 }
 
 void GCN::init_dropout_rng(const GCNData &data, long long glorot_draws) {
@@ -236,32 +278,12 @@ void GCN::init_dropout_rng(const GCNData &data, long long glorot_draws) {
   unsigned long long offset = (unsigned long long)glorot_draws;
   for (int l = 0; l < L; l++) {
     auto r = std::make_shared<DropoutRng>();
-    if (l == 0) {
-      r->elem_begin = data.feature_index.indptr[(size_t)first];
-      r->elem_end = data.feature_index.indptr[(size_t)last];
-    } else {
-      r->elem_begin = (long long)first * dims[(size_t)l];
-      r->elem_end = (long long)last * dims[(size_t)l];
-    }
-    r->chunk_lo = r->elem_begin / kDropChunk;
-    const long long chunk_hi = ceil_div(r->elem_end, kDropChunk);
-    r->n_chunks = std::max(0LL, chunk_hi - r->chunk_lo);
-    r->mask_base = r->elem_begin - kDropChunk * r->chunk_lo;
-    std::vector<uint64_t> st((size_t)std::max(1LL, r->n_chunks) * 2, 0);
-    const unsigned long long base = offset + (unsigned long long)kDropChunk * r->chunk_lo;
-    parallel_for(r->n_chunks, [&](long long b, long long e) {
-      uint64_t s[2] = {seed[0], seed[1]};
-      xs_jump(s, base + (unsigned long long)kDropChunk * b);
-      for (long long c = b; c < e; c++) {
-        st[(size_t)c * 2] = s[0];
-        st[(size_t)c * 2 + 1] = s[1];
-        for (int k = 0; k < kDropChunk; k++) xs_advance(s);
-      }
-    });
-    r->states.allocate(st.size());
-    r->states.upload(st);
-    r->mask.allocate((size_t)std::max(1LL, r->n_chunks) + 1);
-    r->mask.zero();
+    if (l == 0)
+      init_dropout_rng_range(*r, seed, offset, data.feature_index.indptr[(size_t)first],
+                             data.feature_index.indptr[(size_t)last]);
+    else
+      init_dropout_rng_range(*r, seed, offset, (long long)first * dims[(size_t)l],
+                             (long long)last * dims[(size_t)l]);
     rngs.push_back(r);
     offset += (l == 0) ? (unsigned long long)nnz_x_global
                        : (unsigned long long)N * dims[(size_t)l];

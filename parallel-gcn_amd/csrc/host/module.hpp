@@ -134,6 +134,13 @@ struct ModuleContext {
   std::vector<Event> *event_pool = nullptr;
 };
 
+// Builders shared by GCN and the public C++ API (host/gcn.cpp)
+void build_dev_features(DevFeatures &feats, const int *fptr, const int *indices,
+                        const float *values, int first, int rows, int F, bool dense, int hidden0);
+void init_dropout_rng_range(DropoutRng &r, const uint64_t seed[2], unsigned long long offset,
+                            long long elem_begin, long long elem_end);
+void glorot_fill(std::vector<float> &w, int in_size, int out_size, uint64_t s[2]);
+
 // include/module.cuh:33-43
 class Dropout : public Module {
   shared_ptr<Variable> in;  // null for the input features

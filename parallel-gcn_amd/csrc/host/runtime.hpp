@@ -95,8 +95,9 @@ class PinnedBuffer {
 class Stream {
   struct Block {
     hipStream_t s = nullptr;
+    bool owner = true;
     ~Block() {
-      if (s) (void)hipStreamDestroy(s);
+      if (s && owner) (void)hipStreamDestroy(s);
     }
   };
   std::shared_ptr<Block> b_;
@@ -107,6 +108,14 @@ class Stream {
     Stream st;
     st.b_ = std::make_shared<Block>();
     PGCN_HIP(hipStreamCreateWithPriority(&st.b_->s, hipStreamNonBlocking, priority));
+    return st;
+  }
+  // a view of a stream owned elsewhere (the public C++ API's smart_stream)
+  static Stream wrap(hipStream_t s) {
+    Stream st;
+    st.b_ = std::make_shared<Block>();
+    st.b_->s = s;
+    st.b_->owner = false;
     return st;
   }
   hipStream_t get() const { return b_ ? b_->s : nullptr; }

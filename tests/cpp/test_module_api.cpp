@@ -1,0 +1,139 @@
+// tests/cpp/test_module_api.cpp -- drives the reference-shaped C++ API (include/pgcn.hpp).
+//
+//   test_module_api modules <root> <name> <epochs>
+//     assembles the 2-layer GCN from Variable / Module objects exactly as hpdga-spring23's
+//     GCN constructor does (src/gcn.cpp:64-128: Dropout, SparseMatmul, GraphSum, ReLU,
+//     Dropout, Matmul, GraphSum, CrossEntropyLoss, Adam over {W1 decayed, W2}) and runs its
+//     train_epoch / eval(2) (src/gcn.cpp:179-212: loss + l2 penalty of W1, accuracy);
+//   test_module_api gcn <root> <name> <epochs>
+//     the same epochs through pgcn::api::GCN (the fused engine).
+// Prints one line per epoch: "epoch=<e> <train_loss> <train_acc> <val_loss> <val_acc>" (%.9g);
+// tests/test_gpu_engine.py compares them with the reference's golden epoch lines.
+#include <pgcn.hpp>
+
+#include <cstdio>
+#include <cstdlib>
+#include <exception>
+#include <string>
+#include <vector>
+
+using namespace pgcn::api;
+
+static std::vector<integer> truth_of(const GCNData &d, natural split) {
+  std::vector<integer> t(d.label.size());
+  for (size_t i = 0; i < t.size(); i++) t[i] = d.split[i] == split ? d.label[i] : -1;
+  return t;
+}
+
+static int run(int argc, char **argv);
+
+int main(int argc, char **argv) {
+  try {
+    return run(argc, argv);
+  } catch (const std::exception &e) {
+    fprintf(stderr, "test_module_api: %s\n", e.what());
+    return 1;
+  }
+}
+
+static int run(int argc, char **argv) {
+  if (argc < 5) {
+    fprintf(stderr, "usage: %s modules|gcn <root> <name> <epochs>\n", argv[0]);
+    return 2;
+  }
+  const std::string mode = argv[1];
+  const int epochs = atoi(argv[4]);
+  GCNParams params;
+  GCNData data;
+  Parser parser(&params, &data, argv[3], argv[2]);
+  if (!parser.parse()) {
+    fprintf(stderr, "cannot read %s/data/%s.*\n", argv[2], argv[3]);
+    return 1;
+  }
+  AdamParams adam;  // lr 0.01, weight decay 5e-4 (hpdga defaults)
+  const natural N = params.num_nodes, F = params.input_dim, H = 16, C = params.output_dim;
+  const real p = 0.5f;
+  if (mode == "gcn") {
+    params.hidden_dims = {H};
+    GCN gcn(&params, &adam, &data);
+    for (int e = 1; e <= epochs; e++) {
+      const auto tr = gcn.train_epoch();
+      const auto va = gcn.eval(2);
+      printf("epoch=%d %.9g %.9g %.9g %.9g\n", e, tr.first, tr.second, va.first, va.second);
+    }
+    return 0;
+  }
+
+  Variable::initialize_random();
+  smart_stream stream;
+  smart_event ev_fwd, ev_input, ev_bwd, ev_mm_f, ev_mm_b, ev_ce;
+  DevSparseIndex feat_index(data.feature_index), graph(data.graph);
+  integer *dev_truth = nullptr;
+  (void)hipMalloc(&dev_truth, sizeof(integer) * N);
+  std::vector<real> h_graph_value = data.graph_value;
+  real *dev_graph_value = nullptr;
+  (void)hipMalloc(&dev_graph_value, sizeof(real) * h_graph_value.size());
+  (void)hipMemcpy(dev_graph_value, h_graph_value.data(), sizeof(real) * h_graph_value.size(),
+                  hipMemcpyHostToDevice);
+  real loss = 0.0f;
+
+  // hpdga GCN::GCN, module for module
+  std::vector<std::unique_ptr<Module>> modules;
+  auto input = std::make_shared<Variable>((natural)data.feature_index.indices.size(), false);
+  input->from_host(data.feature_value);
+  modules.push_back(std::make_unique<Dropout>(input, p));
+  auto l1_var1 = std::make_shared<Variable>(N * H);
+  auto W1 = std::make_shared<Variable>(F * H, true, true, F, H);
+  W1->glorot();
+  modules.push_back(std::make_unique<SparseMatmul>(input, W1, l1_var1, &feat_index, N, F, H,
+                                                   ev_fwd, ev_input));
+  auto l1_var2 = std::make_shared<Variable>(N * H);
+  modules.push_back(std::make_unique<GraphSum>(l1_var1, l1_var2, &graph, dev_graph_value, H,
+                                               false, ev_bwd));
+  modules.push_back(std::make_unique<ReLU>(l1_var2));
+  modules.push_back(std::make_unique<Dropout>(l1_var2, p));
+  auto l2_var1 = std::make_shared<Variable>(N * C);
+  auto W2 = std::make_shared<Variable>(H * C, true, true, H, C);
+  W2->glorot();
+  modules.push_back(std::make_unique<Matmul>(l1_var2, W2, l2_var1, N, H, C, ev_mm_f, ev_mm_b,
+                                             stream));
+  auto output = std::make_shared<Variable>(N * C);
+  modules.push_back(std::make_unique<GraphSum>(l2_var1, output, &graph, dev_graph_value, C,
+                                               false, ev_bwd));
+  auto ce = std::make_unique<CrossEntropyLoss>(output, dev_truth, &loss, C, ev_ce);
+  CrossEntropyLoss *cep = ce.get();
+  modules.push_back(std::move(ce));
+  Adam optimizer({W1, W2}, {true, false}, &adam);
+
+  auto l2_penalty = [&]() {  // hpdga gcn.cpp:166-173 (float, element order)
+    const std::vector<real> w = W1->to_host();
+    float l2 = 0.0f;
+    for (float x : w) l2 += x * x;
+    return adam.weight_decay * l2 / 2;
+  };
+  auto pass = [&](natural split, bool training) {
+    const std::vector<integer> t = truth_of(data, split);  // set_truth (src/gcn.cpp:136-147)
+    stream.sync();
+    (void)hipMemcpy(dev_truth, t.data(), sizeof(integer) * N, hipMemcpyHostToDevice);
+    natural labelled = 0;
+    for (integer x : t) labelled += x >= 0;
+    cep->set_num_samples(labelled);
+    for (auto &m : modules) m->forward(training, stream);
+    stream.sync();
+    const float l = loss + l2_penalty(), acc = cep->accuracy();
+    if (training) {
+      for (int i = (int)modules.size() - 1; i >= 0; i--) modules[(size_t)i]->backward(stream);
+      optimizer.step(stream);
+      stream.sync();
+    }
+    return std::make_pair(l, acc);
+  };
+  for (int e = 1; e <= epochs; e++) {
+    const auto tr = pass(1, true);
+    const auto va = pass(2, false);
+    printf("epoch=%d %.9g %.9g %.9g %.9g\n", e, tr.first, tr.second, va.first, va.second);
+  }
+  (void)hipFree(dev_truth);
+  (void)hipFree(dev_graph_value);
+  return 0;
+}

@@ -391,3 +391,22 @@ def test_gcn_par_cli_loader_paths(tmp_path):
                        capture_output=True, text=True, timeout=60)
     assert r.returncode != 0 and "GCN creation failed" in r.stderr
     assert os.path.exists(os.path.join(root, "data", name + ".pgcnbin"))
+
+
+def test_cpp_api_header_and_driver_without_device(datasets):
+    """include/pgcn.hpp (the reference-shaped C++ API) is self-contained C++17, and the C++
+    test driver built against it loads the dataset through api::Parser, then fails loudly
+    (the engine has no CPU fallback) when no HIP device is present."""
+    import subprocess
+    import torch
+    hdr = os.path.join(helpers.REPO, "include", "pgcn.hpp")
+    r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-D__HIP_PLATFORM_AMD__",
+                        "-I/opt/rocm/include", "-x", "c++", hdr], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    if torch.cuda.is_available():
+        pytest.skip("a device is present")
+    root, names = datasets
+    exe = os.path.join(helpers.REPO, "parallel-gcn_amd", "bin", "test_module_api")
+    r = subprocess.run([exe, "modules", root, names["cora"], "1"], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode != 0 and "no HIP device" in r.stderr, (r.returncode, r.stderr[-500:])

@@ -474,3 +474,28 @@ def test_early_stopping_matches_reference(datasets, pgcn):
     g.run(verbose=False)
     assert g.query("epochs") == stop
     g.close()
+
+
+@pytest.mark.parametrize("mode", ["modules", "gcn"])
+def test_cpp_module_api_matches_reference(datasets, pgcn, mode):
+    """The reference-shaped C++ API (include/pgcn.hpp) from a C++ program
+    (tests/cpp/test_module_api.cpp): "modules" assembles the 2-layer GCN from Variable,
+    Dropout, SparseMatmul, GraphSum, ReLU, Matmul, CrossEntropyLoss and Adam objects exactly
+    as hpdga-spring23's GCN constructor does and runs its train_epoch / eval(2); "gcn" runs
+    pgcn::api::GCN.  All 100 cora epoch lines against the reference's golden lines (losses
+    1e-4 relative, accuracies within the usual row tolerance)."""
+    import os
+    import subprocess
+    root, names = datasets
+    exe = os.path.join(os.path.dirname(helpers.__file__), "..", "parallel-gcn_amd", "bin",
+                       "test_module_api")
+    out = subprocess.run([exe, mode, root, names["cora"], "100"], capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = np.array([[float(x) for x in ln.split()[1:]] for ln in out.stdout.splitlines()
+                      if ln.startswith("epoch=")], np.float64)
+    assert lines.shape == (100, 4)
+    gold = helpers.golden("cora")["epoch_lines"].reshape(-1, 4)
+    cnt = helpers.split_counts(pgcn.Dataset.load(root, names["cora"]))
+    for e in range(100):
+        helpers.assert_line_close(lines[e], gold[e], cnt, what=f"{mode} epoch {e + 1}")
