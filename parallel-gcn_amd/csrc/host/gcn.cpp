@@ -33,6 +33,11 @@ int g_split_cols = 1;
 // "fuse_epilogue" (read at engine build): the ReLU / Dropout modules next to a GraphSum run in
 // its final-write epilogue (gs_epilogue.hpp), bit-identical to separate launches
 int g_fuse_epilogue = 1;
+// "mm_side" (read at engine build): Matmul weight gradients on the side stream (ModuleContext)
+// on graphs of at least kMmSideRows rows; 2 = on every graph.  r02: reddit-114M 488.4 vs 484.8
+// epochs/s; cora 5,957 vs 7,136 (the stream hand-offs cost more than 7 us of kernels hide)
+int g_mm_side = 1;
+constexpr int kMmSideRows = 65536;
 
 // ------------------------------------------------------------------------------------------
 // Adam (src/optim.cu:7-95; hpdga optim.cpp:16-35)
@@ -444,6 +449,14 @@ void GCN::build(const GCNData &data) {
   for (int l = 0; l < L; l++)
     ws = std::max(ws, gemm_tn_workspace(rows, dims[(size_t)l + 1], dims[(size_t)l]));
   gemm_ws.allocate(ws / sizeof(float) + 64);
+  if (g_mm_side == 2 || (g_mm_side == 1 && rows >= kMmSideRows)) {
+    // the side stream's Matmul weight gradients have a workspace of their own
+    gemm_ws_side.allocate(ws / sizeof(float) + 64);
+    ctx.mm_side = true;
+    ctx.gemm_workspace_side = gemm_ws_side.get();
+    ctx.mm_fork = Event::create();
+    ctx.side_join = Event::create();
+  }
   ctx.train_ahead = g_train_ahead != 0;
   ctx.mask_side = g_mask_side != 0;
   ctx.xent_partials = xent_partials.get();
@@ -687,6 +700,14 @@ void GCN::finalize(int dst_offset, bool graph) {
                    stream.get());
 }
 
+// the weight gradients a Matmul::backward left on the side stream are complete on `stream`
+void GCN::join_side() {
+  if (!ctx.side_pending) return;
+  ctx.side_join.record(side_stream.get());
+  ctx.side_join.wait_on(stream.get());
+  ctx.side_pending = false;
+}
+
 // train_epoch (src/gcn.cu:307-343) + eval(2) (src/gcn.cu:293-303), host-sync free
 void GCN::enqueue_epoch(bool graph) {
   const int slot4 = graph ? 0 : (int)(epoch_count % ring_cap) * 4;
@@ -694,6 +715,7 @@ void GCN::enqueue_epoch(bool graph) {
   for (const auto &m : modules) m->forward(true, stream);
   finalize(slot4, graph);
   for (int i = (int)modules.size() - 1; i >= 0; i--) modules[(size_t)i]->backward(stream);
+  join_side();
   if (comm) comm->allreduce_sum(grad_arena.get(), grad_arena.size(), stream.get());
   if (graph)
     optimizer.step_graph(stream, step_table.get(), dev_ctr.get(), kStepTable);
@@ -728,9 +750,13 @@ void GCN::capture_epoch() {
     step_table.allocate(kStepTable);
   }
   PGCN_HIP(hipStreamBeginCapture(stream.get(), hipStreamCaptureModeThreadLocal));
+  const bool side = ctx.mm_side;
+  ctx.mm_side = false;  // the captured epoch keeps every launch on the captured stream
   try {
     enqueue_epoch(true);
+    ctx.mm_side = side;
   } catch (...) {
+    ctx.mm_side = side;
     hipGraph_t g = nullptr;
     (void)hipStreamEndCapture(stream.get(), &g);
     if (g) (void)hipGraphDestroy(g);
@@ -775,6 +801,7 @@ std::pair<float, float> GCN::train_epoch() {
   for (const auto &m : modules) m->forward(true, stream);
   finalize((int)(slot * 4));
   for (int i = (int)modules.size() - 1; i >= 0; i--) modules[(size_t)i]->backward(stream);
+  join_side();
   if (comm) comm->allreduce_sum(grad_arena.get(), grad_arena.size(), stream.get());
   optimizer.step(stream);
   ctr_valid = false;

@@ -112,6 +112,7 @@ class GCN {
   void insert_layer(int in_dim, int out_dim, float dropout, int layer);
   void insert_last_layer();
   void fuse_epilogues();
+  void join_side();
   int fused_tails_ = 0;  // GraphSum epilogues carrying ReLU / Dropout work (forward + backward)
   void set_split(int split);
   void finalize(int slot_offset, bool graph = false);
@@ -162,7 +163,7 @@ class GCN {
   Adam optimizer;
   DeviceBuffer<float> grad_arena;  // all weight grads, one all-reduce
   DeviceBuffer<uint8_t> jump_table;
-  DeviceBuffer<float> gemm_ws;
+  DeviceBuffer<float> gemm_ws, gemm_ws_side;
   DeviceBuffer<float> xent_partials, sums, results_ring;
   PinnedBuffer<float> pinned;
   int ring_cap = 1024;

@@ -474,13 +474,24 @@ void Matmul::backward(const Stream &s) const {
   const bool cmp = last_layer && ctx->compact_n;
   const Variable &A = cmp ? *ctx->compact_z : *a, &C = cmp ? *ctx->compact_out : *c;
   const int rows = cmp ? ctx->compact_n : m;
+  const bool side = ctx->mm_side && ctx->side_stream && ctx->gemm_workspace_side && !ctx->profile;
   MmProfile prof(ctx, s.get(), 2.0 * 2.0 * rows * p * n);
+  if (side) {
+    // b.grad = a^T * c.grad on the side stream, from here (a.data and c.grad are final; nothing
+    // later in the backward pass writes them), joined before the optimizer (GCN)
+    ctx->mm_fork.record(s.get());
+    ctx->mm_fork.wait_on(ctx->side_stream);
+    launch_gemm_tn(rows, p, n, A.dev_data.get(), A.ld, C.dev_grad.get(), C.ld, b->dev_grad.get(),
+                   b->ld, nullptr, 0, 0, 1.0f, ctx->gemm_workspace_side, ctx->side_stream);
+    ctx->side_pending = true;
+  }
   // a.grad = c.grad * b^T   (b stored [n][p] => trans_b)
   launch_gemm_nn(rows, n, p, C.dev_grad.get(), C.ld, b->dev_data.get(), b->ld, 1,
                  A.dev_grad.get(), A.ld, nullptr, 0, 0, 1.0f, s.get());
   // b.grad = a^T * c.grad (deterministic split-M reduction)
-  launch_gemm_tn(rows, p, n, A.dev_data.get(), A.ld, C.dev_grad.get(), C.ld, b->dev_grad.get(),
-                 b->ld, nullptr, 0, 0, 1.0f, ctx->gemm_workspace, s.get());
+  if (!side)
+    launch_gemm_tn(rows, p, n, A.dev_data.get(), A.ld, C.dev_grad.get(), C.ld, b->dev_grad.get(),
+                   b->ld, nullptr, 0, 0, 1.0f, ctx->gemm_workspace, s.get());
 }
 
 // ------------------------------------------------------------------------------------------

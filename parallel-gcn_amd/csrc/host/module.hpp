@@ -92,6 +92,13 @@ struct ModuleContext {
   bool mask_side = false;
   hipStream_t side_stream = nullptr;  // ... drawn here ...
   Event tn_start, mask_ready;         // ... after tn_start (main), signalling mask_ready
+  // "mm_side": a Matmul's weight gradient (b.grad = a^T c.grad, needed only by the optimizer)
+  // runs on side_stream beside the rest of the backward pass (the reference's S2/S3 streams,
+  // src/module.cu:445-472); GCN joins it (side_join) before the all-reduce / optimizer
+  bool mm_side = false;
+  Event mm_fork, side_join;
+  void *gemm_workspace_side = nullptr;
+  bool side_pending = false;
   // output-layer row restriction (single GPU; the edge-cut engine uses chunk_split_graphs):
   // the last GraphSum's forward computes only the current split's labelled rows -- the only
   // rows the loss, the accuracy and (through the loss gradient, zero elsewhere) the weight

@@ -499,3 +499,21 @@ def test_cpp_module_api_matches_reference(datasets, pgcn, mode):
     cnt = helpers.split_counts(pgcn.Dataset.load(root, names["cora"]))
     for e in range(100):
         helpers.assert_line_close(lines[e], gold[e], cnt, what=f"{mode} epoch {e + 1}")
+
+
+@pytest.mark.parametrize("case", ["cora", "lds_dense"])
+def test_matmul_side_stream_bit_identical(loaded, pgcn, case):
+    """Matmul weight gradients on the side stream (mm_side, joined before the optimizer) give
+    the same bits as the in-order launches: epoch lines and weights after 4 epochs (cora: the
+    reference module order, W2.grad beside Dropout/ReLU/GraphSum backward; the dense LDS
+    graph: the reassociated output layer, W2.grad beside both backward GraphSums)."""
+    ds = loaded["cora"] if case == "cora" else pgcn.Dataset.synthetic(120000, 64, 41, 1500000, 21)
+    runs = []
+    for side in (2, 0):  # 2: on whatever the graph size
+        with helpers.knobs(pgcn, mm_side=side):
+            g = pgcn.GCN(pgcn.make_params(ds), ds)
+        lines = np.array([g.train_epoch() + g.eval(2) for _ in range(4)], np.float32)
+        runs.append((lines, g.get_var(2), g.get_var(5)))
+        g.close()
+    for a, b in zip(runs[0], runs[1]):
+        np.testing.assert_array_equal(a, b)

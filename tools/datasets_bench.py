@@ -53,7 +53,7 @@ def gpu_rates(pg, ds, epochs, graph):
 
 def cpu_rate(ds, reps):
     import bench
-    kind, times = bench.cpu_baseline(ds, reps)
+    kind, times, _ = bench.cpu_baseline(ds, reps)
     return kind, len(times) / sum(times)
 
 
