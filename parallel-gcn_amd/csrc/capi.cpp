@@ -24,6 +24,7 @@ extern int g_split_rows;            // host/gcn.cpp
 extern int g_split_cols;            // host/gcn.cpp
 extern int g_fuse_epilogue;         // host/gcn.cpp
 extern int g_mm_side;               // host/gcn.cpp
+extern int g_graphsum_ring_wide;    // host/graph.cpp
 extern int g_mask_side;             // host/gcn.cpp
 extern int g_xstream_tn_lds;        // k_gemm.hip
 extern int g_eval_ax;               // host/gcn.cpp
@@ -571,6 +572,7 @@ int pgcn_debug_set(const char *key, int value) {
   else if (!std::strcmp(key, "split_cols")) pgcn::g_split_cols = value;
   else if (!std::strcmp(key, "fuse_epilogue")) pgcn::g_fuse_epilogue = value;
   else if (!std::strcmp(key, "mm_side")) pgcn::g_mm_side = value;
+  else if (!std::strcmp(key, "graphsum_ring_wide")) pgcn::g_graphsum_ring_wide = value;
   else if (!std::strcmp(key, "mask_side")) pgcn::g_mask_side = value;
   else if (!std::strcmp(key, "xstream_tn_lds")) pgcn::g_xstream_tn_lds = value;
   else if (!std::strcmp(key, "eval_ax")) pgcn::g_eval_ax = value;

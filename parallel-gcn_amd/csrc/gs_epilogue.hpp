@@ -26,6 +26,7 @@ struct GsEpilogue {
   long long drop_base = 0;
   int drop_cols = 0;
   float drop_scale = 1.0f;
+  int col0 = 0;  // column of the output pointer's first column (16-column passes)
   // the next GraphSum's prescaled input (ring schedule layout, k_ring_prescale): also write
   // next_scale[r] * y to float4 (r / sr) * 4 sr + (c / 4) sr + r % sr of next_table
   float4 *next_table = nullptr;
@@ -41,9 +42,11 @@ __device__ __forceinline__ uint32_t gs_epi_bits4(const uint64_t *__restrict__ ma
   return (uint32_t)v & 0xfu;
 }
 
-// a = the float4 of columns c0 .. c0+3 of row r (c0 % 4 == 0)
+// a = the float4 of columns c0 .. c0+3 of row r (c0 % 4 == 0) of the output pointer, i.e.
+// columns e.col0 + c0 .. of the variable
 __device__ __forceinline__ void gs_epilogue(float4 &a, long long r, int c0, const GsEpilogue &e) {
   if (e.mode == 0) return;
+  c0 += e.col0;
   if (e.mode == 1) {
     const bool k0 = a.x > 0.0f, k1 = a.y > 0.0f, k2 = a.z > 0.0f, k3 = a.w > 0.0f;
     if (e.relu_mask) {

@@ -932,10 +932,19 @@ bool DevGraph::uses_lds(int dim) const {
          !h_row_scale_.empty() && !g_graphsum_force_plain && (double)n_cols_ * 64.0 > kL2Budget;
 }
 
+// "graphsum_ring_wide": rows wider than 16 on the ring schedule take one prescale and one
+// combine launch for all their 16-column passes (0: a prescale + ring + combine per pass)
+// r02: correct and slower on the 4-layer hidden-128 reddit model (1.677 vs 1.594 ms per call:
+// the 8 passes' partials, 480 MB, no longer stay in the Infinity Cache between a pass's ring
+// launch and its combine), so off; the per-pass combine carries the epilogue instead
+int g_graphsum_ring_wide = 0;
+
 bool DevGraph::epilogue_ok(int dim, int ld_in, int ld_out) const {
   (void)ld_in;
   (void)ld_out;
-  if (uses_lds(dim)) return dim <= 16;
+  // LDS path: every 16-column pass's combine applies the tail to its columns (a pass that
+  // overlaps the one before it recomputes those columns from the input: the same bits)
+  if (uses_lds(dim)) return true;
   return !(dim > 16 && !graphsum_vec_supported((dim + 3) / 4));
 }
 
@@ -964,14 +973,27 @@ void DevGraph::graphsum(const float *in, int ld_in, float *out, int ld_out, int 
     const int ldm = std::min(ld_in, ld_out);
     PGCN_CHECK(!prestaged || (dim <= 16 && lds_->s.window == kRingWindow && !col_map),
                PGCN_E_INVALID, "graphsum: prestaged input on a path without a ring table");
+    if (dim > 16 && lds_->s.window == kRingWindow && g_graphsum_ring_wide) {
+      const int n_pass = (dim + 15) / 16;
+      const long long tf = (long long)lds_->scratch.size(), pf = (long long)lds_->partial.size();
+      if ((long long)lds_->wide_tables.size() < n_pass * tf) {
+        lds_->wide_tables.allocate((size_t)(n_pass * tf));
+        lds_->wide_partials.allocate((size_t)(n_pass * pf));
+      }
+      launch_graphsum_ring_wide(lds_->s, in, ld_in, out, ld_out, dim, lds_->wide_tables.get(), tf,
+                                lds_->wide_partials.get(), pf, s, col_map, epi);
+      return;
+    }
     for (int c0 = 0; c0 < dim; c0 += 16) {
       const int c = std::min(c0, ldm - 16);
+      GsEpilogue ep = epi ? *epi : GsEpilogue{};
+      ep.col0 = c;
       if (lds_->s.window == kRingWindow)
         launch_graphsum_ring(lds_->s, in + c, ld_in, out + c, ld_out, lds_->scratch.get(),
-                             lds_->partial.get(), s, col_map, epi, prestaged);
+                             lds_->partial.get(), s, col_map, &ep, prestaged);
       else
         launch_graphsum_lds(lds_->s, in + c, ld_in, out + c, ld_out, lds_->scratch.get(),
-                            lds_->partial.get(), s, col_map, epi);
+                            lds_->partial.get(), s, col_map, &ep);
     }
     return;
   }

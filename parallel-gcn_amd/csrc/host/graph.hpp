@@ -130,6 +130,7 @@ class DevGraph {
     DeviceBuffer<int2> slices;
     DeviceBuffer<int> n_slices, rows, arrive;
     DeviceBuffer<float> row_scale, col_scale, scratch, partial;
+    DeviceBuffer<float> wide_tables, wide_partials;  // rows wider than 16: one per pass
   };
   std::unique_ptr<LdsSched> lds_;
   std::vector<float> h_row_scale_, h_col_scale_;

@@ -61,6 +61,86 @@ __global__ __launch_bounds__(256) void k_ring_prescale(const float4 *__restrict_
   out[(r / RING_SR) * (4 * RING_SR) + v * RING_SR + r % RING_SR] = x;
 }
 
+// Rows wider than 16 (host/graph.cpp): one launch forms every 16-column pass's table.  Pass p
+// holds columns 4 c4(p) .. 4 c4(p) + 15, c4(p) = 4p except the last pass, which starts at
+// last_c4 (it overlaps the one before it so it stays inside the leading dims).  Thread order:
+// row fastest, so each (pass, quarter) plane is written contiguously.
+__global__ __launch_bounds__(256) void k_ring_prescale_wide(const float4 *__restrict__ in,
+                                                            int ld4_in,
+                                                            const float *__restrict__ scale, int n,
+                                                            float4 *__restrict__ tables,
+                                                            long long table4, int n_pass,
+                                                            int last_c4,
+                                                            const int *__restrict__ col_map) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long pv = t / n;
+  const int r = (int)(t - pv * n);
+  if (pv >= 4LL * n_pass) return;
+  const int p = (int)(pv >> 2), v = (int)(pv & 3);
+  const int c4 = p < n_pass - 1 ? 4 * p : last_c4;
+  const float s = scale[r];
+  const long long src = col_map ? (long long)col_map[r] : r;
+  float4 x = in[src * ld4_in + c4 + v];
+  x.x *= s;
+  x.y *= s;
+  x.z *= s;
+  x.w *= s;
+  tables[p * table4 + (r / RING_SR) * (4 * RING_SR) + v * RING_SR + r % RING_SR] = x;
+}
+
+// ... and one launch adds every pass's block partials (block order, as k_gs_lds_combine), scales
+// by s_i, applies the epilogue and writes whole rows: out float4 q of row r comes from pass
+// p = min(q / 4, n_pass - 1) (the last pass's overlap is recomputed to the same bits).
+__global__ __launch_bounds__(256) void k_gs_lds_combine_wide(
+    const float4 *__restrict__ partial, long long pass4, long long part_stride, int nb,
+    const float *__restrict__ scale, int n, float4 *__restrict__ out, int ld4_out, int q_end,
+    int n_pass, int last_c4, GsEpilogue epi) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long r = t / q_end;
+  if (r >= n) return;
+  const int q = (int)(t - r * q_end);
+  const int p = min(q >> 2, n_pass - 1);
+  const int v = q - (p < n_pass - 1 ? 4 * p : last_c4);
+  const float4 *pp = partial + p * pass4 + v;
+  float4 a = pp[r * 4];
+  for (int b = 1; b < nb; b++) f4_acc(a, pp[((long long)b * part_stride + r) * 4]);
+  const float s = scale[r];
+  a.x *= s;
+  a.y *= s;
+  a.z *= s;
+  a.w *= s;
+  gs_epilogue(a, r, 4 * q, epi);
+  out[r * ld4_out + q] = a;
+}
+
+void launch_graphsum_ring_wide(const LdsSchedule &s, const float *in, int ld_in, float *out,
+                               int ld_out, int dim, float *tables, long long table_floats,
+                               float *partials, long long partial_floats, hipStream_t st,
+                               const int *col_map, const GsEpilogue *epi) {
+  const int ldm = ld_in < ld_out ? ld_in : ld_out;
+  PGCN_CHECK(ld_in % 4 == 0 && ld_out % 4 == 0 && ldm >= 16 && dim > 16 && dim <= ldm,
+             PGCN_E_INVALID, "graphsum_ring_wide: leading dims");
+  const int n_pass = (dim + 15) / 16, last_c4 = (ldm - 16) / 4 < 4 * (n_pass - 1) ? (ldm - 16) / 4
+                                                                                 : 4 * (n_pass - 1);
+  const long long pre = 4LL * n_pass * s.n_cols;
+  hipLaunchKernelGGL(k_ring_prescale_wide, dim3((unsigned)ceil_div(pre, 256)), dim3(256), 0, st,
+                     reinterpret_cast<const float4 *>(in), ld_in / 4, s.col_scale, s.n_cols,
+                     reinterpret_cast<float4 *>(tables), table_floats / 4, n_pass, last_c4,
+                     col_map);
+  for (int p = 0; p < n_pass; p++)
+    launch_graphsum_ring(s, nullptr, ld_in, nullptr, ld_out, tables + p * table_floats,
+                         partials + p * partial_floats, st, nullptr, nullptr, true, false);
+  const GsEpilogue none{};
+  const int q_end = (4 * (last_c4 + 4) < ldm ? 4 * (last_c4 + 4) : ldm) / 4;
+  const long long post = (long long)s.n_rows * q_end;
+  hipLaunchKernelGGL(k_gs_lds_combine_wide, dim3((unsigned)ceil_div(post, 256)), dim3(256), 0, st,
+                     reinterpret_cast<const float4 *>(partials), partial_floats / 4,
+                     (long long)s.n_rows, s.n_blocks, s.row_scale, s.n_rows,
+                     reinterpret_cast<float4 *>(out), ld_out / 4, q_end, n_pass, last_c4,
+                     epi ? *epi : none);
+  PGCN_HIP(hipGetLastError());
+}
+
 // diagnostics ("graphsum_lds_diag", k_graphsum_lds.hip): 4 = per-wave cycle stamps into
 // stamps[wg][wave][8] (summing: 0 loop, 1 hand-off wait, 2 ring wait, 3 entry blocks, 4 visits;
 // loader: 1 wait for a free buffer, 2 wait for its pieces to land, 4 slices); 1 = no table reads;
@@ -402,7 +482,8 @@ int g_graphsum_ring_fused = 0;
 
 void launch_graphsum_ring(const LdsSchedule &s, const float *in, int ld_in, float *out,
                           int ld_out, float *scratch_in, float *partial, hipStream_t st,
-                          const int *col_map, const GsEpilogue *epi, bool prestaged) {
+                          const int *col_map, const GsEpilogue *epi, bool prestaged,
+                          bool combine) {
   PGCN_CHECK(ld_in % 4 == 0 && ld_out % 4 == 0, PGCN_E_INVALID, "graphsum_ring: ld % 4");
   PGCN_CHECK(s.window == kRingWindow, PGCN_E_INVALID, "graphsum_ring: not a ring schedule");
   const long long pre = (long long)s.n_cols * 4;
@@ -414,7 +495,8 @@ void launch_graphsum_ring(const LdsSchedule &s, const float *in, int ld_in, floa
   const GsEpilogue none{};
   // (an epilogue that stages the next GraphSum's input may write this call's own table: that
   // needs the separate combine, after every workgroup has read it)
-  int *arrive = g_graphsum_ring_fused && s.arrive && !(epi && epi->next_table) ? s.arrive : nullptr;
+  int *arrive = g_graphsum_ring_fused && s.arrive && combine && !(epi && epi->next_table)
+                   ? s.arrive : nullptr;
 #define GS_RING(D)                                                                            \
   hipLaunchKernelGGL((k_graphsum_ring<D>), dim3((unsigned)n_wg), dim3(LDS_THREADS), 0, st,   \
                      s.entries, s.wave_off, s.counts, s.t_max, s.slices, s.n_slices, s.rows,      \
@@ -432,7 +514,7 @@ void launch_graphsum_ring(const LdsSchedule &s, const float *in, int ld_in, floa
     default: GS_RING(0); break;
   }
 #undef GS_RING
-  if (!arrive) launch_gs_lds_combine(s, partial, out, ld_out, st, epi);
+  if (!arrive && combine) launch_gs_lds_combine(s, partial, out, ld_out, st, epi);
   PGCN_HIP(hipGetLastError());
 }
 

@@ -76,7 +76,14 @@ struct LdsSchedule {
 void launch_graphsum_ring(const LdsSchedule &s, const float *in, int ld_in, float *out,
                           int ld_out, float *scratch_in, float *partial, hipStream_t st,
                           const int *col_map = nullptr, const GsEpilogue *epi = nullptr,
-                          bool prestaged = false);
+                          bool prestaged = false, bool combine = true);
+// rows wider than 16 on the ring schedule: one prescale launch for all 16-column passes
+// (tables: n_pass x table_floats), a ring launch per pass (partials: n_pass x partial_floats),
+// one combine launch writing whole rows (+ the epilogue)
+void launch_graphsum_ring_wide(const LdsSchedule &s, const float *in, int ld_in, float *out,
+                               int ld_out, int dim, float *tables, long long table_floats,
+                               float *partials, long long partial_floats, hipStream_t st,
+                               const int *col_map = nullptr, const GsEpilogue *epi = nullptr);
 void launch_gs_lds_combine(const LdsSchedule &s, const float *partial, float *out, int ld_out,
                            hipStream_t st, const GsEpilogue *epi = nullptr);
 void launch_graphsum_lds(const LdsSchedule &s, const float *in, int ld_in, float *out,

@@ -418,7 +418,7 @@ def _fused_run(pgcn, ds, fuse, epochs, prestage=1, **make):
     return out
 
 
-@pytest.mark.parametrize("case", ["cora", "cora_h4", "lds_dense"])
+@pytest.mark.parametrize("case", ["cora", "cora_h4", "lds_dense", "lds_deep"])
 def test_fused_epilogue_bit_identical(loaded, pgcn, case):
     """ReLU + hidden Dropout in the first GraphSum's final write, and the Dropout + ReLU
     backward in the output GraphSum's backward (reassociated order, cora_h4 / lds_dense) give
@@ -428,6 +428,9 @@ def test_fused_epilogue_bit_identical(loaded, pgcn, case):
     that GraphSum skips its prescale: compared with graphsum_prestage 0 too)."""
     if case == "lds_dense":
         ds, make, tails = pgcn.Dataset.synthetic(120000, 64, 41, 1500000, 21), {}, 2
+    elif case == "lds_deep":  # 128-wide rows: the tails ride the wide (all-pass) combine
+        ds = pgcn.Dataset.synthetic(70000, 32, 41, 600000, 23)
+        make, tails = dict(hidden_dims=(128, 128, 128), dropouts=(0.5,) * 4), 3
     else:
         ds = loaded["cora"]
         make, tails = ({"hidden_dims": (4,)}, 2) if case == "cora_h4" else ({}, 1)

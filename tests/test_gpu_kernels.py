@@ -150,7 +150,9 @@ def test_graphsum_lds_column_blocks(pgcn, blocks, window):
 @pytest.mark.parametrize("dim,ld", [(128, 128), (41, 44), (24, 24)])
 def test_graphsum_lds_wide_rows(pgcn, dim, ld):
     """Rows wider than 16 on a graph that takes the LDS GraphSum: one 16-column LDS pass per
-    chunk (the last one overlapping), against the oracle; padding columns stay zero."""
+    chunk (the last one overlapping), against the oracle; padding columns stay zero.  The
+    ring schedule's single prescale + combine launches for all passes (graphsum_ring_wide)
+    give the same bits as a prescale + combine per pass."""
     n = 120000
     indptr, indices = random_graph(n, 30, seed=dim, hubs=10, hub_deg=3000)
     x = np.zeros((n, ld), np.float32)
@@ -159,10 +161,18 @@ def test_graphsum_lds_wide_rows(pgcn, dim, ld):
     pgcn.check(pgcn.lib.pgcn_graph_create(n, helpers.ptr(indptr), helpers.ptr(indices),
                                           ctypes.byref(g)), "graph_create")
     xin = torch.from_numpy(x).to(DEV)
-    out = torch.full((n, ld), float("nan"), device=DEV)
-    pgcn.check(pgcn.lib.pgcn_graphsum(g, vp(xin), ld, vp(out), ld, dim, stream()), "gs")
+    outs = []
+    try:
+        for wide in (1, 0):  # one prescale + one combine for all passes, or per pass
+            pgcn.lib.pgcn_debug_set(b"graphsum_ring_wide", wide)
+            out = torch.full((n, ld), float("nan"), device=DEV)
+            pgcn.check(pgcn.lib.pgcn_graphsum(g, vp(xin), ld, vp(out), ld, dim, stream()), "gs")
+            outs.append(out)
+    finally:
+        pgcn.lib.pgcn_debug_set(b"graphsum_ring_wide", 0)
     torch.cuda.synchronize()
-    ours = out.cpu().numpy()
+    assert torch.equal(outs[0], outs[1])
+    ours = outs[0].cpu().numpy()
     ref = oracle_graphsum(indptr, indices, x, dim)
     bound = abs_bound(indptr, indices, x, dim)
     assert (np.abs(ours[:, :dim] - ref) <= 1e-5 * bound + 1e-30).all()

@@ -3,8 +3,9 @@ after scripts/profile.sh's fetch/write passes).
 
 usage: python3 tools/traffic.py gpurun_out/<dir> [epoch_calls]
 
-A GraphSum call is k_gs_prescale + k_graphsum_lds + k_gs_lds_combine (the three launches the
-bench's HIP events bracket).  Only the last `epoch_calls` calls (default 20: 4 epochs x 5) are
+A GraphSum call is its prescale (k_ring_prescale, or k_gs_prescale on the window-1 schedule;
+absent when a fused epilogue staged the table) + k_graphsum_ring / k_graphsum_lds +
+k_gs_lds_combine (the launches the bench's HIP events bracket).  Only the last `epoch_calls` calls (default 20: 4 epochs x 5) are
 counted, so the engine-build calls (Â X precompute) are left out.  Bytes follow
 MI355X_MICROARCH.md's HBM section: FETCH_SIZE x 2 (gfx950 tallies the 128-B requests of
 16-B/lane streams at 64 B) + WRITE_SIZE, both in KB.  Prints one JSON object.
@@ -32,7 +33,8 @@ def per_dispatch(counter):
 out = {}
 for counter in ("FETCH_SIZE", "WRITE_SIZE"):
     rows = [r for r in per_dispatch(counter)
-            if any(k in r[1] for k in ("k_gs_prescale", "k_graphsum_lds", "k_gs_lds_combine"))]
+            if any(k in r[1] for k in ("k_gs_prescale", "k_ring_prescale", "k_graphsum_lds",
+                                       "k_graphsum_ring", "k_gs_lds_combine"))]
     calls, cur = [], 0.0
     for _, name, v in rows:
         cur += v
