@@ -34,9 +34,11 @@ int g_split_cols = 1;
 // its final-write epilogue (gs_epilogue.hpp), bit-identical to separate launches
 int g_fuse_epilogue = 1;
 // "mm_side" (read at engine build): Matmul weight gradients on the side stream (ModuleContext)
-// on graphs of at least kMmSideRows rows; 2 = on every graph.  r02: reddit-114M 488.4 vs 484.8
-// epochs/s; cora 5,957 vs 7,136 (the stream hand-offs cost more than 7 us of kernels hide)
-int g_mm_side = 1;
+// on graphs of at least kMmSideRows rows; 2 = on every graph.  Off: r02 A/B on reddit-114M,
+// three runs each, 486.5 (on) vs 487.4 (off) epochs/s -- the LDS GraphSum holds every CU with
+// one workgroup, so the side kernels find no room to overlap; cora 5,957 vs 7,136 (the
+// stream hand-offs cost more than the ~7 us of kernels they hide)
+int g_mm_side = 0;
 constexpr int kMmSideRows = 65536;
 
 // ------------------------------------------------------------------------------------------
