@@ -10,9 +10,9 @@
  *  (2) Engine ABI -- the GCN object of include/gcn.cuh (ctor + train_epoch/eval/run),
  *      plus the edge-cut multi-GPU variant (new: the reference is single-GPU).
  *
- * A C++ host API mirroring the reference classes (Module, Variable, GCN, Parser) sits on
- * top of this ABI in parallel-gcn_amd/csrc/host/ (the .hpp files); INTEGRATION.md shows the bindings
- * a reference maintainer would add.
+ * The reference's C++ classes (Module and its subclasses, Variable, Adam, GCN, Parser) with
+ * their constructor shapes are published in include/pgcn.hpp (namespace pgcn::api, the same
+ * library); INTEGRATION.md shows the bindings a reference maintainer would add.
  */
 #ifndef PGCN_H
 #define PGCN_H
@@ -275,6 +275,12 @@ long long pgcn_partition_subgraph(int n, const int *indptr, const int *indices, 
                                   int rank, int *sub_indptr, int *sub_indices, float *sub_vals);
 
 /* --- diagnostics (profiling ablations; not for production use) ------------------------ */
+/* The edge-cut engine's GraphSum graph of rank `rank`, reduce-scatter chunk `chunk` of
+ * `chunks` at `world` ranks (rows world*maxrows/chunks, columns = the rank's nodes, global
+ * coefficients and scales), as GCN builds it: times the per-rank GraphSum of an N-GPU run on
+ * one GPU.  *rows / *cols give its shape. */
+int pgcn_debug_rank_graph(int n, const int *indptr, const int *indices, int world, int rank,
+                          int chunks, int chunk, pgcn_graph **out, int *rows, int *cols);
 /* "graphsum_variant": 0 normal, 1 skip the feature gather, 2 fold gathers into 4096 rows;
  * "graphsum_plain": 1 disables the XCD column blocking for schedules built afterwards. */
 int pgcn_debug_set(const char *key, int value);

@@ -15,7 +15,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libpgcn.so")
+# PGCN_LIB: another build of the library (A/B experiments); the default is the in-tree build
+LIB_PATH = os.environ.get("PGCN_LIB") or os.path.join(HERE, "libpgcn.so")
 
 PGCN_OK = 0
 PGCN_E_INVALID = -1
@@ -133,6 +134,8 @@ _sig("pgcn_debug_lds_check", c_int, c_int, c_int, c_void_p, c_void_p, c_int, P(c
 _sig("pgcn_debug_lds_counts", c_ll, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_ll,
      c_void_p)
 _sig("pgcn_partition_bounds", c_int, c_int, c_void_p, c_int, c_void_p, P(c_int))
+_sig("pgcn_debug_rank_graph", c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+     c_void_p, c_void_p, c_void_p)
 _sig("pgcn_partition_subgraph", c_ll, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p,
      c_void_p, c_void_p)
 
@@ -457,7 +460,7 @@ def csr_transpose(indptr, indices, n_cols):
 
 EXPORTED = [
     "pgcn_status_string", "pgcn_version", "pgcn_rng_seed", "pgcn_rng_seed_glibc", "pgcn_rng_jump",
-    "pgcn_graph_create",
+    "pgcn_graph_create", "pgcn_debug_rank_graph",
     "pgcn_graph_destroy", "pgcn_graph_nnz", "pgcn_graphsum", "pgcn_gemm", "pgcn_gemm_tn_workspace",
     "pgcn_gemm_tn", "pgcn_mask_nibbles", "pgcn_gemm_xstream", "pgcn_gemm_xstream_dual",
     "pgcn_gemm_tn_xstream",

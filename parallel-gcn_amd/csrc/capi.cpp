@@ -25,6 +25,8 @@ extern int g_split_cols;            // host/gcn.cpp
 extern int g_fuse_epilogue;         // host/gcn.cpp
 extern int g_mm_side;               // host/gcn.cpp
 extern int g_graphsum_ring_wide;    // host/graph.cpp
+extern long long g_lds_min_bytes;     // host/graph.cpp
+extern long long g_blocked_min_bytes; // host/graph.cpp
 extern int g_mask_side;             // host/gcn.cpp
 extern int g_xstream_tn_lds;        // k_gemm.hip
 extern int g_eval_ax;               // host/gcn.cpp
@@ -137,6 +139,42 @@ int pgcn_graph_create(int n, const int *indptr, const int *indices, pgcn_graph *
     *out = h.release();
   });
 }
+int pgcn_debug_rank_graph(int n, const int *indptr, const int *indices, int world, int rank,
+                          int chunks, int chunk, pgcn_graph **out, int *rows, int *cols) {
+  return guarded([&] {
+    PGCN_CHECK(n > 0 && indptr && indices && out && world >= 1 && rank >= 0 && rank < world &&
+                   chunks >= 1 && chunk >= 0 && chunk < chunks,
+               PGCN_E_INVALID, "rank_graph args");
+    check_device();
+    const Partition part = make_partition(n, indptr, world, rank, chunks);
+    const std::vector<float> sg = degree_scales(n, indptr);
+    const int h = part.chunk_rows();
+    std::vector<int> sp, si;
+    partition_subgraph_chunk(part, n, indptr, indices, chunk, &sp, &si);
+    // the same values and scales as GCN::build's chunk graphs
+    std::vector<float> rs((size_t)part.world * h, 0.0f), cs((size_t)part.local_rows()), sv(si.size());
+    for (int c = 0; c < part.local_rows(); c++) cs[(size_t)c] = sg[(size_t)part.first() + c];
+    for (int q = 0; q < part.world; q++)
+      for (int j = 0; j < h; j++) {
+        const int i = part.bounds[(size_t)q] + chunk * h + j;
+        if (i >= part.bounds[(size_t)q + 1]) continue;
+        const size_t r = (size_t)q * h + j;
+        rs[r] = sg[(size_t)i];
+        for (int t = sp[r]; t < sp[r + 1]; t++) {
+          const int gj = part.first() + si[(size_t)t];
+          sv[(size_t)t] = graph_coef(indptr[i + 1] - indptr[i], indptr[gj + 1] - indptr[gj]);
+        }
+      }
+    auto g = std::make_unique<pgcn_graph>();
+    g->g = std::make_unique<DevGraph>(part.world * h, part.local_rows(), sp.data(), si.data(),
+                                      sv.data());
+    g->g->set_scales(std::move(rs), cs);
+    if (rows) *rows = part.world * h;
+    if (cols) *cols = part.local_rows();
+    *out = g.release();
+  });
+}
+
 int pgcn_graph_destroy(pgcn_graph *g) {
   delete g;
   return PGCN_OK;
@@ -573,6 +611,10 @@ int pgcn_debug_set(const char *key, int value) {
   else if (!std::strcmp(key, "fuse_epilogue")) pgcn::g_fuse_epilogue = value;
   else if (!std::strcmp(key, "mm_side")) pgcn::g_mm_side = value;
   else if (!std::strcmp(key, "graphsum_ring_wide")) pgcn::g_graphsum_ring_wide = value;
+  else if (!std::strcmp(key, "lds_min_kb"))  // < 0: the default (one XCD's L2 budget)
+    pgcn::g_lds_min_bytes = value < 0 ? (long long)DevGraph::kL2Budget : 1024LL * value;
+  else if (!std::strcmp(key, "blocked_min_kb"))
+    pgcn::g_blocked_min_bytes = value < 0 ? (long long)DevGraph::kL2Budget : 1024LL * value;
   else if (!std::strcmp(key, "mask_side")) pgcn::g_mask_side = value;
   else if (!std::strcmp(key, "xstream_tn_lds")) pgcn::g_xstream_tn_lds = value;
   else if (!std::strcmp(key, "eval_ax")) pgcn::g_eval_ax = value;

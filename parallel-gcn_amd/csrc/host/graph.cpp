@@ -109,12 +109,17 @@ DevGraph::DevGraph(int n_rows, int n_cols, const int *indptr, const int *indices
 }
 
 int g_graphsum_force_plain = 0;  // diagnostics only (pgcn_debug_set)
+// d = 16 feature tables above these byte counts take the LDS GraphSum ("lds_min_bytes") and,
+// on the plain path, the XCD column blocking ("blocked_min_bytes"); below, one XCD's 4 MB L2
+// holds the whole table (DevGraph::kL2Budget)
+long long g_lds_min_bytes = (long long)DevGraph::kL2Budget;
+long long g_blocked_min_bytes = (long long)DevGraph::kL2Budget;
 
 int DevGraph::column_blocks(int dim) {
   const int vec = (dim + 3) / 4;
   const double table = (double)n_cols_ * vec * 16.0;
   if (g_graphsum_force_plain) return 1;
-  return (graphsum_group_lanes(vec) < 64 && table > kL2Budget) ? kBlocks : 1;
+  return (graphsum_group_lanes(vec) < 64 && table > g_blocked_min_bytes) ? kBlocks : 1;
 }
 
 // Cut the columns into kBlocks nnz-balanced ranges.
@@ -929,7 +934,8 @@ void DevGraph::prepare(int dim) {
 
 bool DevGraph::uses_lds(int dim) const {
   return (dim == 16 || (dim > 16 && g_graphsum_lds_wide)) && g_graphsum_lds &&
-         !h_row_scale_.empty() && !g_graphsum_force_plain && (double)n_cols_ * 64.0 > kL2Budget;
+         !h_row_scale_.empty() && !g_graphsum_force_plain &&
+         (double)n_cols_ * 64.0 > (double)g_lds_min_bytes;
 }
 
 // "graphsum_ring_wide": rows wider than 16 on the ring schedule take one prescale and one
