@@ -182,7 +182,18 @@ def main():
 
     def engine():
         if uid is not None:
-            return pgcn.GCN(params, ds, device=local_rank, rank=rank, world=world, unique_id=uid)
+            # RCCL prints a version banner on fd 1 at communicator init: keep stdout for the
+            # one JSON line (the banner goes to stderr)
+            sys.stdout.flush()
+            saved = os.dup(1)
+            os.dup2(2, 1)
+            try:
+                return pgcn.GCN(params, ds, device=local_rank, rank=rank, world=world,
+                                unique_id=uid)
+            finally:
+                sys.stdout.flush()
+                os.dup2(saved, 1)
+                os.close(saved)
         return pgcn.GCN(params, ds, device=local_rank)
 
     def barrier(g):

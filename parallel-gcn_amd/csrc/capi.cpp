@@ -612,7 +612,7 @@ int pgcn_debug_set(const char *key, int value) {
   else if (!std::strcmp(key, "mm_side")) pgcn::g_mm_side = value;
   else if (!std::strcmp(key, "graphsum_ring_wide")) pgcn::g_graphsum_ring_wide = value;
   else if (!std::strcmp(key, "lds_min_kb"))  // < 0: the default (one XCD's L2 budget)
-    pgcn::g_lds_min_bytes = value < 0 ? (long long)DevGraph::kL2Budget : 1024LL * value;
+    pgcn::g_lds_min_bytes = value < 0 ? DevGraph::kLdsMinBytes : 1024LL * value;
   else if (!std::strcmp(key, "blocked_min_kb"))
     pgcn::g_blocked_min_bytes = value < 0 ? (long long)DevGraph::kL2Budget : 1024LL * value;
   else if (!std::strcmp(key, "mask_side")) pgcn::g_mask_side = value;

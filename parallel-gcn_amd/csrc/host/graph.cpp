@@ -110,9 +110,12 @@ DevGraph::DevGraph(int n_rows, int n_cols, const int *indptr, const int *indices
 
 int g_graphsum_force_plain = 0;  // diagnostics only (pgcn_debug_set)
 // d = 16 feature tables above these byte counts take the LDS GraphSum ("lds_min_bytes") and,
-// on the plain path, the XCD column blocking ("blocked_min_bytes"); below, one XCD's 4 MB L2
-// holds the whole table (DevGraph::kL2Budget)
-long long g_lds_min_bytes = (long long)DevGraph::kL2Budget;
+// on the plain path, the XCD column blocking ("blocked_min_bytes", DevGraph::kL2Budget: below
+// it one XCD's 4 MB L2 holds the whole table).  The LDS path also wants rows to fill its
+// workgroups (kLdsMinRows).  r02, the edge-cut engine's per-rank graphs of reddit-114M
+// (tools/rank_graphsum.py, 118 k padded rows): 3.7 MB table (4 ranks) LDS 0.123 vs plain
+// 0.249 ms, 1.9 MB (8 ranks) 0.083 vs 0.114 ms; 15 MB (1 rank) 0.33 vs 1.04 ms
+long long g_lds_min_bytes = DevGraph::kLdsMinBytes;
 long long g_blocked_min_bytes = (long long)DevGraph::kL2Budget;
 
 int DevGraph::column_blocks(int dim) {
@@ -935,7 +938,7 @@ void DevGraph::prepare(int dim) {
 bool DevGraph::uses_lds(int dim) const {
   return (dim == 16 || (dim > 16 && g_graphsum_lds_wide)) && g_graphsum_lds &&
          !h_row_scale_.empty() && !g_graphsum_force_plain &&
-         (double)n_cols_ * 64.0 > (double)g_lds_min_bytes;
+         (double)n_cols_ * 64.0 > (double)g_lds_min_bytes && n_rows_ >= kLdsMinRows;
 }
 
 // "graphsum_ring_wide": rows wider than 16 on the ring schedule take one prescale and one

@@ -108,7 +108,9 @@ class DevGraph {
   std::unique_ptr<DevGraph> col_subset(const std::vector<int> &cols) const;
 
   static constexpr int kBlocks = kGraphBlocks;   // one column block per XCD
-  static constexpr double kL2Budget = 4.0e6;     // table bytes that stay plain
+  static constexpr double kL2Budget = 4.0e6;     // one XCD's L2: tables the plain kernel keeps whole
+  static constexpr long long kLdsMinBytes = 1 << 20;  // d = 16 tables above: LDS GraphSum ...
+  static constexpr int kLdsMinRows = 32768;           // ... when the rows fill its workgroups
 
  private:
   struct Sched {

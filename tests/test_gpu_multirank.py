@@ -63,8 +63,8 @@ def test_loopback_cora_matches_reference_lines(loaded, pgcn, world):
 
 @pytest.fixture(scope="module")
 def big_ds(pgcn):
-    # 140k nodes: at world 2 a rank's 70k columns take the LDS GraphSum, at world 4 (35k) the
-    # gather kernel
+    # 140k nodes: a rank's columns (70k / 35k / 17.5k at world 2 / 4 / 8) take the LDS GraphSum
+    # (tables above 1 MB); the gather kernel case forces the plain path
     return pgcn.Dataset.synthetic(140000, 64, 41, 1500000, 31)
 
 
@@ -75,12 +75,13 @@ def big_oracle(big_ds):
     return lines, ref.eval(3)
 
 
-@pytest.mark.parametrize("world,split_rows", [(2, 0), (2, 1), (4, 0)])
-def test_loopback_lds_graph_matches_oracle(pgcn, big_ds, big_oracle, world, split_rows):
-    with helpers.knobs(pgcn, split_rows=split_rows):
+@pytest.mark.parametrize("world,split_rows,lds", [(2, 0, 1), (2, 1, 1), (4, 0, 1), (8, 0, 1),
+                                                   (4, 0, 0)])
+def test_loopback_lds_graph_matches_oracle(pgcn, big_ds, big_oracle, world, split_rows, lds):
+    with helpers.knobs(pgcn, split_rows=split_rows, lds_min_kb=-1 if lds else 1 << 20):
         res = _run_world(pgcn, big_ds, world, 4)
     _check_ranks(res, world, big_ds.num_nodes)
-    assert res[0]["info"]["graphsum_lds"] == (1 if world == 2 else 0)
+    assert res[0]["info"]["graphsum_lds"] == lds
     assert res[0]["info"]["reassociated"] == 1
     cnt = helpers.split_counts(big_ds)
     lines, test = big_oracle

@@ -1,5 +1,5 @@
 """Parity of the MEASURED path: the default engine on graphs whose feature table takes the
-LDS GraphSum (n_cols * 64 B above the 4 MB L2 budget, graph.hpp kL2Budget), with dense
+LDS GraphSum (n_cols * 64 B above 1 MB and >= 32 k rows, graph.hpp kLdsMinBytes), with dense
 features (X-stream MFMA kernels + nibble dropout masks), 41 classes (the output layer runs
 reassociated as (Â H) W2 over every row, its backward over the training split's columns),
 eval's first layer from Â X, train-ahead -- against the oracle (the C restatement of
