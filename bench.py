@@ -114,6 +114,21 @@ def cpu_model():
     return "unknown"
 
 
+@contextlib.contextmanager
+def stdout_to_stderr():
+    """RCCL prints a version banner on fd 1 when it initialises: stdout stays reserved for the
+    bench's one JSON line, so native output inside the block goes to stderr."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def maybe_launch(args):
     """--gpus N > 1 without torch.distributed's environment: start the N ranks here (before
     anything touches a GPU) and exit with their status; a WORLD_SIZE that disagrees with
@@ -174,26 +189,19 @@ def main():
              else f"{len(hidden) + 1}-layer GCN, hidden={args.hidden}")
     uid = None
     if world > 1:
-        uid = [pgcn.comm_unique_id() if rank == 0 else None]
+        with stdout_to_stderr():
+            uid = [pgcn.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         uid = uid[0]
     elif args.edge_cut:
-        uid = pgcn.comm_unique_id()
+        with stdout_to_stderr():
+            uid = pgcn.comm_unique_id()
 
     def engine():
         if uid is not None:
-            # RCCL prints a version banner on fd 1 at communicator init: keep stdout for the
-            # one JSON line (the banner goes to stderr)
-            sys.stdout.flush()
-            saved = os.dup(1)
-            os.dup2(2, 1)
-            try:
+            with stdout_to_stderr():
                 return pgcn.GCN(params, ds, device=local_rank, rank=rank, world=world,
                                 unique_id=uid)
-            finally:
-                sys.stdout.flush()
-                os.dup2(saved, 1)
-                os.close(saved)
         return pgcn.GCN(params, ds, device=local_rank)
 
     def barrier(g):
