@@ -841,7 +841,16 @@ int g_lds_blocks_subset = 0;  // "lds_blocks_subset": override for large row sub
 
 int lds_blocks(int n_rows, int n_cols) {
   if (g_lds_blocks) return g_lds_blocks;
-  if ((double)n_rows >= 0.9 * (double)n_cols) return 4;
+  if ((double)n_rows >= 0.9 * (double)n_cols) {
+    // square-ish: 4 blocks, or 8 when the rowset batches fill the chip only then and every
+    // block keeps >= 20 slices of 512 columns (r02, edge-cut chunk graphs of reddit-114M,
+    // tools/rank_graphsum.py: 1 rank 0.336 vs 0.400 ms, 2 ranks 0.202 vs 0.223; 4 ranks
+    // (14 slices per block at 8) 0.130 vs 0.125)
+    const long long nrs = ((long long)n_rows + 15) / 16, cap = (long long)LDS_CW * LDS_SLOTS;
+    const long long nb = std::max(1LL, (nrs + cap - 1) / cap);
+    if (nb * 8 <= kCUs && n_cols / 8 >= 20 * RING_SR) return 8;
+    return 4;
+  }
   // row subsets: 8 blocks, or more when few batches of rowsets would leave each workgroup a
   // long sweep over its block's slices with little work per slice (the validation rows: 7
   // batches -> 32 blocks, a quarter of the slices per workgroup)

@@ -34,6 +34,11 @@ ix = np.ascontiguousarray(ds.graph_indices, np.int32)
 st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 PATHS = {"default": {}, "lds": {"lds_min_kb": 0}, "plain": {"lds_min_kb": 1 << 30},
          "plain_blocked": {"lds_min_kb": 1 << 30, "blocked_min_kb": 0}}
+if os.environ.get("RANK_GS_PATHS"):  # e.g. "lds_b8:lds_blocks=8,lds_min_kb=0;lds_b16:lds_blocks=16"
+    PATHS = {}
+    for item in os.environ["RANK_GS_PATHS"].split(";"):
+        name, _, kv = item.partition(":")
+        PATHS[name] = {k: int(v) for k, v in (x.split("=") for x in kv.split(",") if x)}
 
 
 def time_path(world, knobs, reps=20):
@@ -70,6 +75,7 @@ def time_path(world, knobs, reps=20):
             pg.lib.pgcn_graph_destroy(g)
         pg.lib.pgcn_debug_set(b"lds_min_kb", -1)  # the defaults
         pg.lib.pgcn_debug_set(b"blocked_min_kb", -1)
+        pg.lib.pgcn_debug_set(b"lds_blocks", 0)
 
 
 out = {"chunks": chunks}
