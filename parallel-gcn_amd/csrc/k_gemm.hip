@@ -741,6 +741,10 @@ void launch_mask_nibbles(const uint64_t *mask, long long mask_base, long long ma
                      mask_base, mask_ld, M, K, out);
 }
 
+// "xstream_nn_balance": 1 = grid sized so every wave gets the same number of row groups;
+// > 1 = that many workgroups (diagnostics)
+int g_xstream_nn_balance = 0;
+
 void launch_xstream_nn(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
                        int trans_b, float *C, int ldc, const uint64_t *maskT, float a_scale,
                        hipStream_t s, float *C2) {
@@ -750,7 +754,16 @@ void launch_xstream_nn(int M, int N, int K, const float *A, int lda, const float
   if (M <= 0) return;
   const int kc = (K + 63) / 64, S = xs_stride(K);
   const long long n_rg = ceil_div(M, 16);
-  const dim3 grid((unsigned)std::min<long long>(ceil_div(n_rg, 4), 2 * kCUs)), block(256);
+  long long wgs = std::min<long long>(ceil_div(n_rg, 4), 2 * kCUs);
+  if (g_xstream_nn_balance > 1) {  // diagnostics: exactly this many workgroups
+    wgs = g_xstream_nn_balance;
+  } else if (g_xstream_nn_balance) {
+    // every wave the same number of 16-row groups (+-1 over the grid): the last round of a
+    // grid-stride loop over n_rg groups no longer runs on a fraction of the waves
+    const long long per_wave = ceil_div(n_rg, 4 * wgs);
+    wgs = ceil_div(n_rg, 4 * per_wave);
+  }
+  const dim3 grid((unsigned)wgs), block(256);
   const size_t lds = (size_t)16 * S * sizeof(float);
 #define XNN_CASE(KC)                                                                          \
   case KC:                                                                                    \

@@ -28,16 +28,22 @@ constexpr int RING_PLANE_B = RING_P * 16;                   // 32,832 B per quar
 constexpr int RING_TABLE_B = 4 * RING_PLANE_B;              // 131,328 B
 constexpr int RING_CNT_USED = LDS_CW * LDS_SLOTS * 2;       // 480 B of counts per visit
 constexpr int RING_CNT_B = 512;
+// counts buffers: visit v's counts land with slice v + W - 1, up to K - W visits ahead of the
+// slowest wave's visit
+constexpr int RING_NCB = RING_K - RING_W + 1;
 constexpr int RING_CNT_OFF = RING_TABLE_B;
-constexpr int RING_FLAG_OFF = RING_CNT_OFF + RING_CNT_USED;  // loaded, done[4] (tail of buffer 0)
-constexpr int RING_ERING_OFF = RING_CNT_OFF + 2 * RING_CNT_B;
+// loaded, done[K], last (fused combine) in the tail of counts buffer 0
+constexpr int RING_FLAG_OFF = RING_CNT_OFF + RING_CNT_USED;
+constexpr int RING_LAST_FLAG = 1 + RING_K;
+constexpr int RING_ERING_OFF = RING_CNT_OFF + RING_NCB * RING_CNT_B;
 constexpr int RING_CHUNK = 512;                             // 4 entry blocks of 128 B
 constexpr int RING_ESLOTS = 4;                              // chunks: 3 in flight + 1 read
 constexpr int RING_ERING_B = RING_ESLOTS * RING_CHUNK;
 constexpr int RING_TOTAL_B = RING_ERING_OFF + LDS_CW * RING_ERING_B;  // 163,072 B
 static_assert(RING_TOTAL_B <= 160 * 1024, "LDS budget");
-static_assert(RING_FLAG_OFF + 6 * 4 <= RING_CNT_OFF + RING_CNT_B, "hand-off + arrival words fit");
-static_assert(RING_SR * 16 == 8192, "a slice's plane piece is 8 x 1-KB LDS-DMA pieces");
+static_assert(RING_FLAG_OFF + (RING_LAST_FLAG + 1) * 4 <= RING_CNT_OFF + RING_CNT_B,
+              "hand-off + arrival words fit");
+static_assert(RING_SR * 16 % 1024 == 0, "a slice's plane piece is whole 1-KB LDS-DMA pieces");
 static_assert(RING_K * RING_SR * 16 + 4 * 16 <= 65536, "ring rows addressable by 16 bits");
 
 // in'[r] = scale[r] * in[col_map ? col_map[r] : r], written to the slice-plane layout:
@@ -193,10 +199,10 @@ __device__ __forceinline__ void ring_combine_tail(int *__restrict__ arrive, int 
                                            __HIP_MEMORY_SCOPE_AGENT);
     const unsigned last = old == nb - 1;
     if (last) __hip_atomic_store(arrive + batch, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    flags[5] = last;
+    flags[RING_LAST_FLAG] = last;
   }
   __syncthreads();
-  if (!flags[5] || wave == LDS_CW) return;
+  if (!flags[RING_LAST_FLAG] || wave == LDS_CW) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // loads stay below the barrier
   const int *rw = rows + (((long long)batch * LDS_CW + wave) * LDS_SLOTS) * 16 + g;
   const unsigned bstride = (unsigned)part_stride * 64u;
@@ -271,7 +277,7 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
         make_float4(0.f, 0.f, 0.f, 0.f);
   unsigned *const flags = reinterpret_cast<unsigned *>(lb + RING_FLAG_OFF);
   unsigned *const loaded = flags, *const done = flags + 1;
-  if (threadIdx.x < 5) flags[threadIdx.x] = 0u;
+  if (threadIdx.x < RING_LAST_FLAG) flags[threadIdx.x] = 0u;
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();  // zero rows and hand-off words set (the only barrier)
   asm volatile("" ::: "memory");
@@ -297,16 +303,20 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
           glds16x4(src, dst);
         } else {
 #pragma unroll
-          for (int p = 0; p < 4; p++) {
-            glds16x4(src + p * (RING_SR * 16), dst + (unsigned)(p * RING_PLANE_B));
-            glds16x4(src + p * (RING_SR * 16) + 4096, dst + (unsigned)(p * RING_PLANE_B + 4096));
+          for (int p = 0; p < 4; p++) {  // plane p of the slice: RING_SR * 16 B
+#pragma unroll
+            for (int q = 0; q + 4096 <= RING_SR * 16; q += 4096)
+              glds16x4(src + p * (RING_SR * 16) + q, dst + (unsigned)(p * RING_PLANE_B + q));
+#pragma unroll
+            for (int q = RING_SR * 16 / 4096 * 4096; q < RING_SR * 16; q += 1024)
+              glds16(src + p * (RING_SR * 16) + q, dst + (unsigned)(p * RING_PLANE_B + q));
           }
         }
       }
       const int cv = s - (RING_W - 1);  // the visit whose last slice this is
       if (cv >= 0 && lane * 16 < RING_CNT_USED)
         glds16(cnt_src + (long long)cv * RING_CNT_USED + lane * 16,
-               lds_base + (unsigned)(RING_CNT_OFF + (cv & 1) * RING_CNT_B));
+               lds_base + (unsigned)(RING_CNT_OFF + (cv % RING_NCB) * RING_CNT_B));
       unsigned long long c1 = 0;
       if constexpr (DIAG == 4) c1 = ring_clk();
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // slice s and counts landed
@@ -380,7 +390,7 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
     if constexpr (DIAG == 4) hw0 = ring_clk();
     lds_wait_ge(loaded, (unsigned)(t + RING_W));  // slices t .. t+2 and visit t's counts
     if constexpr (DIAG == 4) st_wait += ring_clk() - hw0;
-    const uint4 *c4 = reinterpret_cast<const uint4 *>(lb + RING_CNT_OFF + (t & 1) * RING_CNT_B +
+    const uint4 *c4 = reinterpret_cast<const uint4 *>(lb + RING_CNT_OFF + (t % RING_NCB) * RING_CNT_B +
                                                       wave * 32);
     const uint4 cw0 = c4[0], cw1 = c4[1];
     const unsigned cw[8] = {

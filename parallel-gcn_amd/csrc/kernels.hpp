@@ -40,9 +40,21 @@ constexpr int LDS_SLOTS = 16;                        // rowsets (16 rows) per co
 constexpr int LDS_THREADS = 64 * (LDS_CW + 1);       // + one slice loader wave
 // Sliding-window ring schedule (k_graphsum_ring.hip, host/ring.cpp): slices of RING_SR rows,
 // a ring of RING_K slices in LDS as 4 quarter planes of RING_P rows, visits read RING_W slices
-constexpr int RING_SR = 512;
-constexpr int RING_K = 4;
-constexpr int RING_W = RING_K - 1;
+// (PGCN_RING_SR / _K / _W override them for schedule experiments; RING_W <= RING_K - 1: the
+// loader may run RING_K - RING_W slices ahead of a visit's last slice)
+#ifndef PGCN_RING_SR
+#define PGCN_RING_SR 512
+#endif
+#ifndef PGCN_RING_K
+#define PGCN_RING_K 4
+#endif
+#ifndef PGCN_RING_W
+#define PGCN_RING_W (PGCN_RING_K - 1)
+#endif
+constexpr int RING_SR = PGCN_RING_SR;
+constexpr int RING_K = PGCN_RING_K;
+constexpr int RING_W = PGCN_RING_W;
+static_assert(RING_W >= 1 && RING_W <= RING_K - 1 && RING_SR % 64 == 0, "ring shape");
 constexpr int RING_P = RING_K * RING_SR + 4;  // + 4 zero rows; = 4 mod 16 (bank quarters)
 constexpr int kRingWindow = 5;                // LdsSchedule::window of a ring schedule
 // ring schedule rows[]: row id | log2(spread) << 28; kRingEmpty = no row (spread kept)
