@@ -43,6 +43,7 @@ extern int g_ring_balance;          // host/ring.cpp
 extern int g_graphsum_ring_prio;    // k_graphsum_ring.hip
 extern int g_graphsum_ring_fused;   // k_graphsum_ring.hip
 extern int g_graphsum_prestage;     // host/module.cpp
+extern int g_xstream_epilogue;      // host/module.cpp
 extern int g_ring_spread;           // host/ring.cpp
 extern int g_parse_threads;         // host/data.cpp: pieces of the parallel text parse
 extern int g_graphsum_lds_sync;     // k_graphsum_lds.hip (diagnostics)
@@ -602,6 +603,7 @@ int pgcn_debug_set(const char *key, int value) {
   else if (!std::strcmp(key, "graphsum_ring_prio")) pgcn::g_graphsum_ring_prio = value;
   else if (!std::strcmp(key, "graphsum_ring_fused")) pgcn::g_graphsum_ring_fused = value;
   else if (!std::strcmp(key, "graphsum_prestage")) pgcn::g_graphsum_prestage = value;
+  else if (!std::strcmp(key, "xstream_epilogue")) pgcn::g_xstream_epilogue = value;
   else if (!std::strcmp(key, "ring_spread")) pgcn::g_ring_spread = value;
   else if (!std::strcmp(key, "graphsum_lds_sync")) pgcn::g_graphsum_lds_sync = value;
   else if (!std::strcmp(key, "graphsum_lds_opt")) pgcn::g_graphsum_lds_opt = value;

@@ -536,6 +536,7 @@ void GCN::insert_first_layer() {
   auto var2 = std::make_shared<Variable>(prow, h, true, round_up4(h));
   variables.push_back(var2);
   auto gs = std::make_unique<GraphSum>(var1, var2, graph.get(), h, &ctx);
+  smp->consumer = gs.get();
   if (feats.ax) {  // eval: (Â X) W1 -> var2 directly, the GraphSum is skipped
     smp->eval_out = var2;
     gs->first_layer = true;

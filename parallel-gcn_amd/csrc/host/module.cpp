@@ -134,16 +134,32 @@ SparseMatmul::SparseMatmul(const DevFeatures *x_, shared_ptr<Variable> b_,
                            shared_ptr<Variable> c_, const Dropout *drop_, ModuleContext *ctx_)
     : x(x_), b(std::move(b_)), c(std::move(c_)), drop(drop_), ctx(ctx_) {}
 
+// "xstream_epilogue": the first layer's X-stream product also applies the ReLU / writes the
+// ring table that the modules after it would launch for (bit-identical)
+int g_xstream_epilogue = 1;
+
 void SparseMatmul::forward(bool training, const Stream &s) const {
   last_training = training;
   const uint64_t *mask = training ? drop->state().mask.get() : nullptr;
   const long long base = drop->state().mask_base;
   const float scale = drop->scale();
   if (!training && x->ax && eval_out) {  // eval_ax: (Â X) W1 straight into the GraphSum's output
-    if (xstream_ok(b->cols, x->cols))
+    if (xstream_ok(b->cols, x->cols)) {
+      // eval: out = relu(Â X W1) (GraphSum, then its fused ReLU; the Dropout after it is the
+      // identity in eval), which the reassociated output layer's GraphSum reads next
+      XsEpilogue e;
+      if (g_xstream_epilogue && consumer && consumer->fwd_relu) {
+        e.relu = 1;
+        consumer->fwd_relu->skip_forward = true;
+        if (consumer->fwd_next)
+          e.next_table =
+              consumer->fwd_next->claim_forward_table(x->rows, eval_out->ld, &e.next_scale);
+        e.next_sr = RING_SR;
+      }
       launch_xstream_nn(x->rows, b->cols, x->cols, x->ax.get(), x->ldx, b->dev_data.get(), b->ld,
-                        0, eval_out->dev_data.get(), eval_out->ld, nullptr, 1.0f, s.get(), nullptr);
-    else
+                        0, eval_out->dev_data.get(), eval_out->ld, nullptr, 1.0f, s.get(), nullptr,
+                        &e);
+    } else
       launch_gemm_nn(x->rows, b->cols, x->cols, x->ax.get(), x->ldx, b->dev_data.get(), b->ld, 0,
                      eval_out->dev_data.get(), eval_out->ld, nullptr, 0, 0, 1.0f, s.get());
     return;
@@ -174,9 +190,14 @@ void SparseMatmul::forward(bool training, const Stream &s) const {
   MmProfile prof(ctx, s.get(), x->dense ? 2.0 * x->rows * b->cols * x->cols : 0.0);
   if (x->dense && x->maskT) {  // X-stream kernels (N <= 16, K <= 640)
     if (mask) launch_mask_nibbles(mask, base, x->cols, x->rows, x->cols, x->maskT.get(), s.get());
+    XsEpilogue e;  // the first GraphSum's prescaled input, written beside c
+    if (g_xstream_epilogue && consumer && (training || !eval_out)) {
+      e.next_table = consumer->claim_forward_table(x->rows, c->ld, &e.next_scale);
+      e.next_sr = RING_SR;
+    }
     launch_xstream_nn(x->rows, b->cols, x->cols, x->x.get(), x->ldx, b->dev_data.get(), b->ld, 0,
                       c->dev_data.get(), c->ld, mask ? x->maskT.get() : nullptr, scale, s.get(),
-                      nullptr);
+                      nullptr, &e);
   } else if (x->dense) {
     launch_gemm_nn(x->rows, b->cols, x->cols, x->x.get(), x->ldx, b->dev_data.get(), b->ld, 0,
                    c->dev_data.get(), c->ld, mask, base, x->cols, scale, s.get());
@@ -244,6 +265,16 @@ DevGraph *GraphSum::forward_graph() const {
 DevGraph *GraphSum::backward_graph() const {
   if (ctx->comm) return nullptr;
   return last_layer && ctx->split_colgraph ? ctx->split_colgraph : graph;
+}
+
+float4 *GraphSum::claim_forward_table(int rows, int ld, const float **scale) const {
+  DevGraph *g = forward_graph();
+  if (!g || !g_graphsum_prestage || dim != 16 || in->ld != 16 || ld != 16 || g->cols() != rows)
+    return nullptr;
+  float *t = g->ring_table(dim, scale);
+  if (!t) return nullptr;
+  prestaged_fwd = true;
+  return reinterpret_cast<float4 *>(t);
 }
 
 void GraphSum::stage_next(GsEpilogue &e, GraphSum *next, DevGraph *ng, bool fwd) const {

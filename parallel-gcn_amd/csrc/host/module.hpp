@@ -82,6 +82,7 @@ class Module {
 };
 
 class ReLU;
+class GraphSum;
 
 // Shared per-GCN state the modules read (current split, comm, profiling, RNG table).
 struct ModuleContext {
@@ -200,6 +201,10 @@ class SparseMatmul : public Module {
                const Dropout *drop_, ModuleContext *ctx_);
   // eval_ax: the first GraphSum's output, written by an eval forward from Â X
   shared_ptr<Variable> eval_out;
+  // the GraphSum reading c (training) / standing for eval_out (eval): the X-stream product's
+  // epilogue writes that GraphSum's ring table (training) or applies its fused ReLU and
+  // writes the next GraphSum's table (eval), when g_xstream_epilogue
+  const GraphSum *consumer = nullptr;
   void forward(bool training, const Stream &s) const override;
   void backward(const Stream &s) const override;
 };
@@ -242,6 +247,10 @@ class GraphSum : public Module {
   // the graph this module's next forward / backward sums over (single GPU)
   DevGraph *forward_graph() const;
   DevGraph *backward_graph() const;
+  // for a producer of this GraphSum's next forward input with `rows` rows and 16 columns:
+  // the ring table (and its scale) that call reads, marked as written by the producer
+  // (prestaged_fwd); null when that call has none
+  float4 *claim_forward_table(int rows, int ld, const float **scale) const;
 
  private:
   // mode (edge-cut output layer): 0 all rows, 1 forward over ctx->chunk_split_graphs (the

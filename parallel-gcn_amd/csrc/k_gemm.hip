@@ -189,7 +189,8 @@ __global__ __launch_bounds__(256, 2) void k_xstream_nn(int M, int N, int K, int 
                                                        const float *__restrict__ B, int ldb,
                                                        int trans_b, float *__restrict__ C,
                                                        int ldc, const uint64_t *__restrict__ maskT,
-                                                       float a_scale, float *__restrict__ C2 = nullptr) {
+                                                       float a_scale, float *__restrict__ C2,
+                                                       XsEpilogue epi) {
   static_assert(!DUAL || MASKED, "dual: the second product is the masked one");
   constexpr int NS = 4 * KC;  // 16-wide k-steps (the last ones may be past K)
   extern __shared__ float bt[];
@@ -255,7 +256,17 @@ __global__ __launch_bounds__(256, 2) void k_xstream_nn(int M, int N, int K, int 
       for (int r = 0; r < 4; r++) {
         const long long rr = rg * 16 + 4 * g + r;
         if (rr < M) {
-          C[rr * ldc + i] = acc[r];
+          float c = acc[r];
+          if constexpr (!DUAL) {
+            if (epi.relu && !(c > 0.0f)) c = 0.0f;  // k_relu_fwd's test (NaN -> 0)
+            if (epi.next_table) {  // k_ring_prescale of the stored value: s_r * C[r][i]
+              const long long sr = epi.next_sr;
+              float *t = reinterpret_cast<float *>(epi.next_table +
+                                                   (rr / sr) * 4 * sr + (i >> 2) * sr + rr % sr);
+              t[i & 3] = c * epi.next_scale[rr];
+            }
+          }
+          C[rr * ldc + i] = c;
           if constexpr (DUAL) C2[rr * ldc + i] = acc2[r];
         }
       }
@@ -747,7 +758,12 @@ int g_xstream_nn_balance = 0;
 
 void launch_xstream_nn(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
                        int trans_b, float *C, int ldc, const uint64_t *maskT, float a_scale,
-                       hipStream_t s, float *C2) {
+                       hipStream_t s, float *C2, const XsEpilogue *epi) {
+  const XsEpilogue none{};
+  const XsEpilogue &e = epi ? *epi : none;
+  PGCN_CHECK(!C2 || (!e.relu && !e.next_table), PGCN_E_INVALID, "xstream_nn: dual + epilogue");
+  PGCN_CHECK(!e.next_table || (N <= 16 && ldc == 16), PGCN_E_INVALID,
+             "xstream_nn: a staged table needs 16-column rows");
   PGCN_CHECK(xstream_ok(N, K), PGCN_E_INVALID, "xstream_nn: needs N <= 16, K <= 640");
   PGCN_CHECK(!C2 || maskT, PGCN_E_INVALID, "xstream_nn: the dual product needs the mask");
   PGCN_CHECK(lda % 4 == 0 && lda >= K, PGCN_E_INVALID, "gemm: lda must be a multiple of 4 >= K");
@@ -769,13 +785,13 @@ void launch_xstream_nn(int M, int N, int K, const float *A, int lda, const float
   case KC:                                                                                    \
     if (C2)                                                                                   \
       hipLaunchKernelGGL((k_xstream_nn<KC, true, true>), grid, block, lds, s, M, N, K, S, A,  \
-                         lda, B, ldb, trans_b, C, ldc, maskT, a_scale, C2);                   \
+                         lda, B, ldb, trans_b, C, ldc, maskT, a_scale, C2, e);                \
     else if (maskT)                                                                           \
       hipLaunchKernelGGL((k_xstream_nn<KC, true>), grid, block, lds, s, M, N, K, S, A, lda, B, \
-                         ldb, trans_b, C, ldc, maskT, a_scale, nullptr);                      \
+                         ldb, trans_b, C, ldc, maskT, a_scale, nullptr, e);                   \
     else                                                                                      \
       hipLaunchKernelGGL((k_xstream_nn<KC, false>), grid, block, lds, s, M, N, K, S, A, lda,   \
-                         B, ldb, trans_b, C, ldc, maskT, a_scale, nullptr);                   \
+                         B, ldb, trans_b, C, ldc, maskT, a_scale, nullptr, e);                \
     break;
   switch (kc) {
     XNN_CASE(1) XNN_CASE(2) XNN_CASE(3) XNN_CASE(4) XNN_CASE(5)

@@ -110,9 +110,20 @@ size_t gemm_tn_workspace(int M, int N, int K);
 bool xstream_ok(int N, int K);
 void launch_mask_nibbles(const uint64_t *mask, long long mask_base, long long mask_ld, int M,
                          int K, uint64_t *out, hipStream_t s);
+// What the first layer's X-stream product feeds (single C output, N <= 16): relu = the ReLU
+// of the GraphSum it stands for (eval from Â X; no mask: eval only), next_table = that
+// GraphSum's or the next one's prescaled ring table (next_scale[r] * value at the ring
+// layout of k_ring_prescale), so neither the ReLU nor the prescale needs a launch
+struct XsEpilogue {
+  int relu = 0;
+  float4 *next_table = nullptr;
+  const float *next_scale = nullptr;
+  int next_sr = 0;
+};
 void launch_xstream_nn(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
                        int trans_b, float *C, int ldc, const uint64_t *maskT, float a_scale,
-                       hipStream_t s, float *C2 = nullptr);  // C2: drop(X) W beside C = X W
+                       hipStream_t s, float *C2 = nullptr,  // C2: drop(X) W beside C = X W
+                       const XsEpilogue *epi = nullptr);
 // out[r][0:ld] = src[rows[r]][0:ld]  (ld % 4 == 0)
 void launch_gather_rows(const float *src, const int *rows, int n, int ld, float *out,
                         hipStream_t s);

@@ -196,7 +196,7 @@ def parse_line(line):
 # pgcn_debug_set defaults of the engine (parallel-gcn_amd/csrc/host/gcn.cpp)
 ENGINE_DEFAULTS = {"train_ahead": 1, "split_rows": 0, "split_cols": 1, "eval_ax": 1,
                    "epoch_graph": 0, "mask_side": 0, "fuse_epilogue": 1,
-                   "graphsum_ring_fused": 0, "graphsum_prestage": 1,
+                   "graphsum_ring_fused": 0, "graphsum_prestage": 1, "xstream_epilogue": 1,
                    "mm_side": 0, "graphsum_ring_wide": 0,
                    "lds_min_kb": -1, "blocked_min_kb": -1}
 

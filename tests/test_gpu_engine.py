@@ -407,8 +407,9 @@ def test_part2_configs_match_oracle(datasets, pgcn, name):
     g.close()
 
 
-def _fused_run(pgcn, ds, fuse, epochs, prestage=1, **make):
-    with helpers.knobs(pgcn, fuse_epilogue=fuse, graphsum_prestage=prestage):
+def _fused_run(pgcn, ds, fuse, epochs, prestage=1, xs=1, **make):
+    with helpers.knobs(pgcn, fuse_epilogue=fuse, graphsum_prestage=prestage,
+                       xstream_epilogue=xs):
         g = pgcn.GCN(pgcn.make_params(ds, **make), ds)
         lines = [g.train_epoch() + g.eval(2) for _ in range(epochs)]
         g.train_epoch()  # tensors of a training pass: relu/dropout forward and backward
@@ -425,7 +426,9 @@ def test_fused_epilogue_bit_identical(loaded, pgcn, case):
     the same bits as the separate kernels: epoch lines, weights, the hidden activations and
     their gradients (gs_epilogue.hpp; plain gather kernels on cora, LDS ring + combine on the
     dense graph, where the epilogue also writes the next GraphSum's prescaled input table and
-    that GraphSum skips its prescale: compared with graphsum_prestage 0 too)."""
+    that GraphSum skips its prescale: compared with graphsum_prestage 0 too; and the first
+    layer's X-stream product applying the eval ReLU / writing the ring tables, compared with
+    xstream_epilogue 0)."""
     if case == "lds_dense":
         ds, make, tails = pgcn.Dataset.synthetic(120000, 64, 41, 1500000, 21), {}, 2
     elif case == "lds_deep":  # 128-wide rows: the tails ride the wide (all-pass) combine
@@ -437,8 +440,9 @@ def test_fused_epilogue_bit_identical(loaded, pgcn, case):
     on = _fused_run(pgcn, ds, 1, 4, **make)
     off = _fused_run(pgcn, ds, 0, 4, **make)
     no_stage = _fused_run(pgcn, ds, 1, 4, prestage=0, **make)
+    no_xs = _fused_run(pgcn, ds, 1, 4, xs=0, **make)
     assert on["tails"] == tails and off["tails"] == 0
-    for other in (off, no_stage):
+    for other in (off, no_stage, no_xs):
         np.testing.assert_array_equal(on["lines"], other["lines"])
         for a, b in zip(on["vars"] + on["grads"], other["vars"] + other["grads"]):
             np.testing.assert_array_equal(a, b)
