@@ -29,6 +29,9 @@ extern long long g_lds_min_bytes;     // host/graph.cpp
 extern long long g_blocked_min_bytes; // host/graph.cpp
 extern int g_mask_side;             // host/gcn.cpp
 extern int g_xstream_tn_lds;        // k_gemm.hip
+extern int g_xstream_ring;          // k_xstream_lds.hip
+extern int g_xstream_ring_inflight; // k_xstream_lds.hip
+extern int g_xstream_ring_diag;     // k_xstream_lds.hip
 extern int g_xstream_nn_balance;    // k_gemm.hip
 extern int g_eval_ax;               // host/gcn.cpp
 extern int g_epoch_graph;           // host/gcn.cpp
@@ -620,6 +623,9 @@ int pgcn_debug_set(const char *key, int value) {
     pgcn::g_blocked_min_bytes = value < 0 ? (long long)DevGraph::kL2Budget : 1024LL * value;
   else if (!std::strcmp(key, "mask_side")) pgcn::g_mask_side = value;
   else if (!std::strcmp(key, "xstream_tn_lds")) pgcn::g_xstream_tn_lds = value;
+  else if (!std::strcmp(key, "xstream_ring")) pgcn::g_xstream_ring = value;
+  else if (!std::strcmp(key, "xstream_ring_inflight")) pgcn::g_xstream_ring_inflight = value;
+  else if (!std::strcmp(key, "xstream_ring_diag")) pgcn::g_xstream_ring_diag = value;
   else if (!std::strcmp(key, "xstream_nn_balance")) pgcn::g_xstream_nn_balance = value;
   else if (!std::strcmp(key, "eval_ax")) pgcn::g_eval_ax = value;
   else if (!std::strcmp(key, "epoch_graph")) pgcn::g_epoch_graph = value;

@@ -768,6 +768,10 @@ void launch_xstream_nn(int M, int N, int K, const float *A, int lda, const float
   PGCN_CHECK(!C2 || maskT, PGCN_E_INVALID, "xstream_nn: the dual product needs the mask");
   PGCN_CHECK(lda % 4 == 0 && lda >= K, PGCN_E_INVALID, "gemm: lda must be a multiple of 4 >= K");
   if (M <= 0) return;
+  if (xstream_ring_ok(K, lda)) {
+    launch_xstream_nn_ring(M, N, K, A, lda, B, ldb, trans_b, C, ldc, maskT, a_scale, s, C2, e);
+    return;
+  }
   const int kc = (K + 63) / 64, S = xs_stride(K);
   const long long n_rg = ceil_div(M, 16);
   long long wgs = std::min<long long>(ceil_div(n_rg, 4), 2 * kCUs);
@@ -911,7 +915,9 @@ void launch_xstream_tn(int M, int N, int K, const float *A, int lda, const float
   PGCN_CHECK(lda % 4 == 0 && lda >= K, PGCN_E_INVALID, "gemm_tn: lda must be a multiple of 4 >= K");
   const TnPlan p = xs_tn_plan(K);
   float *partial = static_cast<float *>(workspace);
-  if (M > 0 && g_xstream_tn_lds && ldg == 16 && lda <= 640 && p.nkc == 10) {
+  if (M > 0 && xstream_ring_ok(K, lda)) {
+    launch_xstream_tn_ring(M, N, K, A, lda, G, ldg, maskT, a_scale, partial, XS_TN_BLOCKS, s);
+  } else if (M > 0 && g_xstream_tn_lds && ldg == 16 && lda <= 640 && p.nkc == 10) {
     // the LDS-DMA ring (its waits are written for ten 64-column chunks: reddit's K = 602)
     if (maskT)
       hipLaunchKernelGGL((k_xstream_tn_lds<10, true>), dim3(XS_TN_BLOCKS), dim3(256), 0, s, M, N,

@@ -1,0 +1,504 @@
+// parallel-gcn_amd/csrc/k_xstream_lds.hip -- the X-stream GEMMs with loader and MFMA waves
+// split (the default form of k_xstream_nn / k_xstream_tn, csrc/k_gemm.hip, for reddit's
+// feature width).
+//
+// Same products as those kernels (Z = drop(X) W and W.grad = drop(X)^T dZ over the dense
+// feature matrix X [M][lda], N <= 16; src/module.cu:108-163 in the reference), same per-lane
+// MFMA feed.  What changes is who waits for memory.  In the register-streamed kernels every
+// wave both streams X and runs its MFMAs; on reddit (X = 563 MB) they move X at 3.4-4.1 TB/s
+// although a bare read of X with the same lane map reaches 6.1 TB/s here, because the
+// 0.05 ms of fp32 MFMA per pass (64 FLOP/clk/SIMD) does not overlap the stream
+// (tools/xs_micro.hip: read alone 91 us, read + MFMA in the same waves 122 us, MFMA alone
+// 50 us; loader + MFMA waves as below 90-98 us).
+//
+// One workgroup per CU, 5 waves (NN) or 4 (TN):
+//   wave 0 (loader)       copies whole 16-row groups of X (16 * lda contiguous floats) into an
+//                         LDS ring of up to 4 slots by LDS-DMA (global_load_lds_dwordx4,
+//                         nontemporal, 1 KB per instruction, no VGPRs, NI instructions per
+//                         group: a compile-time count, so hipcc sees a straight-line issue),
+//                         two groups in flight: wait for the slot to be handed back, issue,
+//                         s_waitcnt vmcnt(NI), publish the older group;
+//   waves 1..  (consumers) take the groups in turn, copy the group's MFMA operands from the
+//                         slot to registers (ds_read_b128), hand the slot back and run the
+//                         MFMAs, with their state (B of the NN product, the TN accumulators)
+//                         in registers.
+// The slot is the group's bytes as they lie in X (row stride lda / 4 chunks, lda = K rounded
+// up to 4), plus the bytes after it up to NI KB.  In the last group of X, lanes past the end
+// of X copy the group's first chunk instead, so every value in a slot is finite data except
+// the ld padding (k in [K, lda), possibly NaN): NN zeroes it in the slot before use (B is 0
+// for k >= K, so the finite values past K add exact zeros); in TN it reaches only output rows
+// k >= K, which are not written.
+// NN results are bit-identical to k_xstream_nn (same MFMA sequence per row group); TN sums
+// each workgroup's row groups in group order into one [K][16] partial per workgroup (the
+// ordered k_slab_reduce1 / k_gemm_tn_reduce pass follows): deterministic.
+#include <cmath>
+
+#include "common.hpp"
+#include "kernels.hpp"
+#include "lds_dma.hpp"
+
+namespace pgcn {
+
+// "xstream_ring": 1 = these kernels for the X-stream products where they apply (default),
+// 0 = the register-streamed k_xstream_nn / k_xstream_tn.  "xstream_ring_inflight": groups in
+// flight per loader wave (1 or 2)
+int g_xstream_ring = 1;
+int g_xstream_ring_inflight = 1;
+// "xstream_ring_diag" (timing only, wrong results): 1 = consumers skip their MFMAs (the
+// loaders' pace), 2 = loaders skip their DMAs (the consumers' pace)
+int g_xstream_ring_diag = 0;
+
+namespace {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+constexpr int XL_LOADERS = 1;
+constexpr int XL_NN_CONSUMERS = 4;  // NN: one per SIMD + a second on the loader's SIMD
+constexpr int XL_TN_CONSUMERS = 3;  // TN: its accumulators need a SIMD per consumer
+constexpr int XL_LDS = 159 * 1024;  // ring + hand-off words (one workgroup per CU)
+constexpr int XL_FLAGS = 64;        // ready[8], freed[8] at the end
+constexpr int XL_KC = 10;           // the instantiated width: K in (576, 640] (reddit: 602)
+constexpr int XL_BS = 648;          // B^T row stride in floats (== 8 mod 16: conflict-free)
+constexpr int XL_BT_BYTES = 16 * XL_BS * 4 / 1024 * 1024 + 1024;  // NN: B^T ahead of the ring
+
+struct XlRing {
+  int off;    // LDS byte offset of slot 0 (NN: past B^T)
+  int st;     // row stride in 16-B chunks (lda / 4 = ceil(K / 4))
+  int nslot;  // slots in the ring (<= 4)
+  int two;    // loaders keep two groups in flight
+  int diag;   // g_xstream_ring_diag
+};
+
+// DMA instructions (1 KB) per group for a row of lda floats: the group's 64 * lda bytes
+__host__ __device__ constexpr int xl_ni(int lda) { return (64 * lda + 1023) / 1024; }
+
+XlRing xl_ring(int lda, int ni, int off) {
+  XlRing r;
+  r.off = off;
+  r.st = lda / 4;
+  r.nslot = std::min(4, (XL_LDS - XL_FLAGS - off) / (ni * 1024));
+  r.two = g_xstream_ring_inflight > 1 && r.nslot == 4;
+  r.diag = g_xstream_ring_diag;
+  return r;
+}
+
+// keep bit t of `bits` (as 0 / all ones by a 1-bit signed field extract) masks element t, then
+// the scale: x * scale or +0 (k_gemm.hip's apply4 gives x * 0, a zero of x's sign: the sums
+// are the same).  FOLD: the scale is a power of two and is applied to the finished sums (NN)
+// or to dZ (TN) instead -- exact scalings, so the same bits with one multiply per product less.
+template <bool FOLD>
+__device__ __forceinline__ void xl_apply4(float4 &a, uint32_t bits, float scale) {
+  a.x = __uint_as_float(__float_as_uint(a.x) & (uint32_t)__builtin_amdgcn_sbfe((int)bits, 0, 1));
+  a.y = __uint_as_float(__float_as_uint(a.y) & (uint32_t)__builtin_amdgcn_sbfe((int)bits, 1, 1));
+  a.z = __uint_as_float(__float_as_uint(a.z) & (uint32_t)__builtin_amdgcn_sbfe((int)bits, 2, 1));
+  a.w = __uint_as_float(__float_as_uint(a.w) & (uint32_t)__builtin_amdgcn_sbfe((int)bits, 3, 1));
+  if constexpr (!FOLD) {
+    a.x *= scale;
+    a.y *= scale;
+    a.z *= scale;
+    a.w *= scale;
+  }
+}
+
+// groups of this workgroup: blockIdx.x + t * gridDim.x, t < T
+__device__ __forceinline__ int xl_groups(long long M) {
+  const long long n_rg = (M + 15) / 16;
+  return blockIdx.x < n_rg ? (int)((n_rg - blockIdx.x + gridDim.x - 1) / gridDim.x) : 0;
+}
+
+// nontemporal LDS-DMA of four consecutive 1-KB pieces (one address, offsets 0..3 KB)
+__device__ __forceinline__ void xl_dma4(const char *gsrc, unsigned lds_dst) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off nt\n\t"
+      "global_load_lds_dwordx4 %1, off offset:1024 nt\n\t"
+      "global_load_lds_dwordx4 %1, off offset:2048 nt\n\t"
+      "global_load_lds_dwordx4 %1, off offset:3072 nt\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_dst)
+      : "memory");
+}
+
+// Loader wave `wave`: groups wave, wave + XL_LOADERS, ... into slot t % nslot, NI pieces
+// each.  With two in flight a loader publishes group t - 2 once only group t's NI DMAs are
+// outstanding, or before it would block on a slot.
+template <int NI>
+__device__ __forceinline__ void xl_load(const float *__restrict__ A, int lda, long long M, int T,
+                                        int wave, int lane, const XlRing &rg, char *lds,
+                                        unsigned *ready, unsigned *freed) {
+  static_assert(NI < 64, "vmcnt counts at most 63");
+  __builtin_amdgcn_s_setprio(3);
+  const unsigned base = __builtin_amdgcn_readfirstlane(
+      (unsigned)reinterpret_cast<size_t>((__attribute__((address_space(3))) char *)lds));
+  const unsigned slot_bytes = NI * 1024;
+  const long long x_bytes = M * (long long)lda * 4;
+  int pend = -1;
+  auto publish = [&](int u) {
+    if (lane == 0) __atomic_store_n(ready + u % rg.nslot, (unsigned)(u + 1), __ATOMIC_RELAXED);
+    asm volatile("" ::: "memory");
+  };
+  for (int t = wave; t < T; t += XL_LOADERS) {
+    const int slot = t % rg.nslot;
+    if (t >= rg.nslot) {
+      const unsigned need = (unsigned)(t - rg.nslot + 1);
+      if ((unsigned)__builtin_amdgcn_readfirstlane(__atomic_load_n(freed + slot, __ATOMIC_RELAXED)) <
+          need) {
+        if (pend >= 0) {  // about to block: the group in flight goes out first
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          publish(pend);
+          pend = -1;
+        }
+        lds_wait_ge(freed + slot, need);
+      }
+    }
+    const long long b0 = (blockIdx.x + (long long)t * gridDim.x) * 16 * (long long)lda * 4;
+    const char *blk = reinterpret_cast<const char *>(A) + b0;
+    const unsigned dst = base + (unsigned)(rg.off + slot * slot_bytes);
+    if (rg.diag == 2) {
+      // timing only: no DMA
+    } else if (b0 + NI * 1024 <= x_bytes) {  // the whole NI KB lies inside X
+      const char *src = blk + lane * 16;
+#pragma unroll
+      for (int q = 0; q + 4 <= NI; q += 4) xl_dma4(src + q * 1024, dst + (unsigned)(q * 1024));
+#pragma unroll
+      for (int q = NI / 4 * 4; q < NI; q++) glds16_nt(src + q * 1024, dst + (unsigned)(q * 1024));
+    } else {  // the last group of X: lanes past its end copy the group's first chunk
+      const long long left = x_bytes - b0;
+#pragma unroll
+      for (int q = 0; q < NI; q++) {
+        const long long off = q * 1024 + lane * 16;
+        glds16_nt(blk + (off < left ? off : 0), dst + (unsigned)(q * 1024));
+      }
+    }
+    if (rg.two) {
+      if (pend >= 0) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");  // group pend landed
+        publish(pend);
+      }
+      pend = t;
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      publish(t);
+    }
+  }
+  if (pend >= 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    publish(pend);
+  }
+}
+
+// a consumer's release of a slot once every read of it returned
+__device__ __forceinline__ void xl_release(unsigned *freed, int slot, int t, int lane) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (lane == 0) __atomic_store_n(freed + slot, (unsigned)(t + 1), __ATOMIC_RELAXED);
+  asm volatile("" ::: "memory");
+}
+
+// NN: C[M][N<=16] = drop(X) W (DUAL: C = X W and C2 = drop(X) W); consumer lane (i, g) of a
+// group holds B[16 s + 4 g + t][i] for every step s (registers) and feeds MFMA t of step s with
+// X[row i][16 s + 4 g + t] -- k_xstream_nn's feed and order, so the same bits (up to the sign
+// of zero products: see xl_apply4).  B^T sits in LDS ahead of the ring (as in k_xstream_nn).
+template <int NI, bool MASKED, bool DUAL, bool FOLD>
+__global__ __launch_bounds__(64 * (XL_LOADERS + XL_NN_CONSUMERS), 1) void k_xs_nn_ring(
+    int M, int N, int K, const float *__restrict__ A, int lda, const float *__restrict__ B,
+    int ldb, int trans_b, float *__restrict__ C, int ldc, const uint64_t *__restrict__ maskT,
+    float a_scale, float *__restrict__ C2, XsEpilogue epi, XlRing rg) {
+  static_assert(!DUAL || MASKED, "dual: the second product is the masked one");
+  constexpr int NS = 4 * XL_KC;
+  __shared__ __attribute__((aligned(1024))) char lds[XL_LDS];
+  unsigned *const ready = reinterpret_cast<unsigned *>(lds + XL_LDS - XL_FLAGS);
+  unsigned *const freed = ready + 8;
+  if (threadIdx.x < 16) ready[threadIdx.x] = 0u;
+  {  // B^T [16][XL_BS] (zero outside [K, N]) ahead of the ring
+    float *bt = reinterpret_cast<float *>(lds);
+    for (int e = threadIdx.x; e < 16 * NS * 16; e += blockDim.x) {
+      const int k = e >> 4, j = e & 15;
+      float v = 0.0f;
+      if (k < K && j < N) v = trans_b ? B[(long long)j * ldb + k] : B[(long long)k * ldb + j];
+      bt[j * XL_BS + k] = v;
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int T = xl_groups(M);
+  if (wave < XL_LOADERS) {
+    xl_load<NI>(A, lda, M, T, wave, lane, rg, lds, ready, freed);
+    return;
+  }
+  const int cid = wave - XL_LOADERS, g = lane >> 4, i = lane & 15;
+  const float *bl = reinterpret_cast<const float *>(lds) + i * XL_BS + 4 * g;
+  auto load_mask = [&](int t, uint64_t(&m)[4]) {  // keep bits of the lane's row of group t
+    long long row = (blockIdx.x + (long long)t * gridDim.x) * 16 + i;
+    row = row < M ? row : M - 1;
+#pragma unroll
+    for (int q = 0; q < 4; q++) m[q] = maskT[row * 16 + 4 * q + g];
+  };
+  // group t with its keep bits in mw; the next group's go to mwn (two static buffers that
+  // alternate: a copy would wait for the prefetch)
+  auto group = [&](int t, const uint64_t(&mw)[4], uint64_t(&mwn)[4]) {
+    if (MASKED && t + XL_NN_CONSUMERS < T) load_mask(t + XL_NN_CONSUMERS, mwn);
+    const int slot = t % rg.nslot;
+    lds_wait_ge(ready + slot, (unsigned)(t + 1));
+    char *const sb = lds + rg.off + slot * (NI * 1024);
+    if (K & 3) {  // the ld padding k >= K of each row's last chunk (may be NaN)
+      if (lane < 16) {
+        float *pc = reinterpret_cast<float *>(sb + (lane * rg.st + rg.st - 1) * 16);
+        for (int e = K & 3; e < 4; e++) pc[e] = 0.0f;
+      }
+      asm volatile("" ::: "memory");
+    }
+    // the group's fragments into registers, then the slot goes back to the loader
+    const char *a = sb + i * rg.st * 16 + g * 16;
+    float4 xa[NS];
+#pragma unroll
+    for (int s = 0; s < NS; s++)
+      xa[s] = 16 * s < K ? *reinterpret_cast<const float4 *>(a + 64 * s) : make_float4(0.f, 0.f, 0.f, 0.f);
+    xl_release(freed, slot, t, lane);
+    floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f}, acc2 = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+      if (16 * s >= K || rg.diag == 1) break;  // steps wholly past K add nothing
+      float4 x = xa[s];
+      const float4 bb = *reinterpret_cast<const float4 *>(bl + 16 * s);
+      if constexpr (DUAL) {
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x.x, bb.x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x.y, bb.y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x.z, bb.z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x.w, bb.w, acc, 0, 0, 0);
+      }
+      if constexpr (MASKED)
+        xl_apply4<FOLD>(x, (uint32_t)(mw[s & 3] >> (4 * (s >> 2))) & 0xfu, a_scale);
+      floatx4 &am = DUAL ? acc2 : acc;
+      am = __builtin_amdgcn_mfma_f32_16x16x4f32(x.x, bb.x, am, 0, 0, 0);
+      am = __builtin_amdgcn_mfma_f32_16x16x4f32(x.y, bb.y, am, 0, 0, 0);
+      am = __builtin_amdgcn_mfma_f32_16x16x4f32(x.z, bb.z, am, 0, 0, 0);
+      am = __builtin_amdgcn_mfma_f32_16x16x4f32(x.w, bb.w, am, 0, 0, 0);
+    }
+    if constexpr (MASKED && FOLD) {  // the masked product's scale, on its sums
+      floatx4 &am = DUAL ? acc2 : acc;
+      am = am * a_scale;
+    }
+    // lane holds C[16 rg + 4 g + r][i] (k_xstream_nn's epilogue)
+    const long long rgi = blockIdx.x + (long long)t * gridDim.x;
+    if (i < ldc) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const long long rr = rgi * 16 + 4 * g + r;
+        if (rr < M) {
+          float c = acc[r];
+          if constexpr (!DUAL) {
+            if (epi.relu && !(c > 0.0f)) c = 0.0f;  // k_relu_fwd's test (NaN -> 0)
+            if (epi.next_table) {  // k_ring_prescale of the stored value: s_r * C[r][i]
+              const long long sr = epi.next_sr;
+              float *tb = reinterpret_cast<float *>(epi.next_table + (rr / sr) * 4 * sr +
+                                                    (i >> 2) * sr + rr % sr);
+              tb[i & 3] = c * epi.next_scale[rr];
+            }
+          }
+          C[rr * ldc + i] = c;
+          if constexpr (DUAL) C2[rr * ldc + i] = acc2[r];
+        }
+      }
+    }
+  };
+  uint64_t mwa[4] = {0, 0, 0, 0}, mwb[4] = {0, 0, 0, 0};
+  if (MASKED && cid < T) load_mask(cid, mwa);
+  for (int t = cid; t < T; t += 2 * XL_NN_CONSUMERS) {
+    group(t, mwa, mwb);
+    if (t + XL_NN_CONSUMERS < T) group(t + XL_NN_CONSUMERS, mwb, mwa);
+  }
+}
+
+// TN: partial[blockIdx.x][k][j] = sum over this workgroup's rows m of drop(X)[m][k] G[m][j].
+// A group is 4 steps of 4 rows; consumer lane (i, g) feeds MFMA (c, t) of step q with
+// X[row 4q + g][64 c + 4 i + t] and G[row 4q + g][i] (k_xstream_tn's feed); the two consumers'
+// accumulators (groups t = c mod 3 for consumer c) are added in consumer order at the end.
+template <int NI, bool MASKED, bool FOLD>
+__global__ __launch_bounds__(64 * (XL_LOADERS + XL_TN_CONSUMERS), 1) void k_xs_tn_ring(
+    int M, int N, int K, const float *__restrict__ A, int lda, const float *__restrict__ G,
+    int ldg, const uint64_t *__restrict__ maskT, float a_scale, float *__restrict__ partial,
+    XlRing rg) {
+  constexpr int KC = XL_KC;
+  __shared__ __attribute__((aligned(1024))) char lds[XL_LDS];
+  unsigned *const ready = reinterpret_cast<unsigned *>(lds + XL_LDS - XL_FLAGS);
+  unsigned *const freed = ready + 8;
+  if (threadIdx.x < 16) ready[threadIdx.x] = 0u;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, i = lane & 15;
+  const int T = xl_groups(M);
+  floatx4 acc[KC][4];
+#pragma unroll
+  for (int c = 0; c < KC; c++)
+#pragma unroll
+    for (int t = 0; t < 4; t++) acc[c][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  if (wave < XL_LOADERS) {
+    xl_load<NI>(A, lda, M, T, wave, lane, rg, lds, ready, freed);
+  } else {
+    const int cid = wave - XL_LOADERS;
+    auto load_rows = [&](int t, float(&bv)[4], uint64_t(&m)[4]) {  // dZ and keep bits, group t
+      const long long row0 = (blockIdx.x + (long long)t * gridDim.x) * 16;
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const long long mr = row0 + 4 * q + g;
+        const long long row = mr < M ? mr : M - 1;
+        const float v = G[row * ldg + (i < N ? i : 0)];
+        bv[q] = (mr < M && i < N) ? (MASKED && FOLD ? v * a_scale : v) : 0.0f;
+        if constexpr (MASKED) m[q] = maskT[row * 16 + i];
+      }
+    };
+    // group t with dZ / keep bits in bj / mw, the next group's into bjn / mwn (alternating
+    // static buffers)
+    auto group = [&](int t, const float(&bj)[4], const uint64_t(&mw)[4], float(&bjn)[4],
+                     uint64_t(&mwn)[4]) {
+      if (t + XL_TN_CONSUMERS < T) load_rows(t + XL_TN_CONSUMERS, bjn, mwn);
+      const int slot = t % rg.nslot;
+      lds_wait_ge(ready + slot, (unsigned)(t + 1));
+      // the group's fragments into registers, then the slot goes back to the loader
+      const char *sp = lds + rg.off + slot * (NI * 1024) + i * 16;
+      float4 xa[4][KC];
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int c = 0; c < KC; c++)
+          xa[q][c] = *reinterpret_cast<const float4 *>(sp + (4 * q + g) * rg.st * 16 + 256 * c);
+      xl_release(freed, slot, t, lane);
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        if (rg.diag == 1) break;
+#pragma unroll
+        for (int c = 0; c < KC; c++) {
+          float4 x = xa[q][c];
+          if constexpr (MASKED) xl_apply4<FOLD>(x, (uint32_t)(mw[q] >> (4 * c)) & 0xfu, a_scale);
+          acc[c][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(x.x, bj[q], acc[c][0], 0, 0, 0);
+          acc[c][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(x.y, bj[q], acc[c][1], 0, 0, 0);
+          acc[c][2] = __builtin_amdgcn_mfma_f32_16x16x4f32(x.z, bj[q], acc[c][2], 0, 0, 0);
+          acc[c][3] = __builtin_amdgcn_mfma_f32_16x16x4f32(x.w, bj[q], acc[c][3], 0, 0, 0);
+        }
+      }
+    };
+    float bja[4] = {0.f, 0.f, 0.f, 0.f}, bjb[4] = {0.f, 0.f, 0.f, 0.f};
+    uint64_t mwa[4] = {0, 0, 0, 0}, mwb[4] = {0, 0, 0, 0};
+    if (cid < T) load_rows(cid, bja, mwa);
+    for (int t = cid; t < T; t += 2 * XL_TN_CONSUMERS) {
+      group(t, bja, mwa, bjb, mwb);
+      if (t + XL_TN_CONSUMERS < T) group(t + XL_TN_CONSUMERS, bjb, mwb, bja, mwa);
+    }
+  }
+  // consumers 1, 2 hand their accumulators to consumer 0 through the (idle) ring; 0 adds them
+  // in consumer order and writes the partial
+  __syncthreads();
+  float *red = reinterpret_cast<float *>(lds);
+  constexpr int RED = KC * 4 * 4 * 64;  // floats per consumer
+  if (wave > XL_LOADERS) {
+    float *rw = red + (wave - XL_LOADERS - 1) * RED;
+#pragma unroll
+    for (int c = 0; c < KC; c++)
+#pragma unroll
+      for (int t = 0; t < 4; t++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) rw[((c * 4 + t) * 4 + r) * 64 + lane] = acc[c][t][r];
+  }
+  __syncthreads();
+  if (wave == XL_LOADERS) {
+    float *p = partial + (long long)blockIdx.x * K * 16;
+#pragma unroll
+    for (int c = 0; c < KC; c++)
+#pragma unroll
+      for (int t = 0; t < 4; t++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int k = 64 * c + 4 * (4 * g + r) + t;
+          float v = acc[c][t][r];
+#pragma unroll
+          for (int q = 0; q < XL_TN_CONSUMERS - 1; q++) v += red[q * RED + ((c * 4 + t) * 4 + r) * 64 + lane];
+          if (k < K) p[(long long)k * 16 + i] = v;
+        }
+  }
+}
+
+}  // namespace
+
+// a_scale = 2^n (dropout 1/2, 3/4, ...): scaling by it is exact, so it can move
+static bool xl_pow2(float v) {
+  int e;
+  return v > 0.0f && std::frexp(v, &e) == 0.5f && std::isnormal(v);
+}
+
+// the shapes these kernels take: ten 64-column chunks (K in 577..640), rows packed at lda =
+// K rounded up to 4 (the group is contiguous), N <= 16
+bool xstream_ring_ok(int K, int lda) {
+  return g_xstream_ring && K > 64 * (XL_KC - 1) && K <= 64 * XL_KC && lda == (K + 3) / 4 * 4;
+}
+
+void launch_xstream_nn_ring(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
+                            int trans_b, float *C, int ldc, const uint64_t *maskT, float a_scale,
+                            hipStream_t s, float *C2, const XsEpilogue &e) {
+  PGCN_CHECK(xstream_ring_ok(K, lda) && N <= 16 && ldc <= 16, PGCN_E_INVALID,
+             "xstream ring: K in 577..640, lda = K rounded to 4, N <= 16");
+  const int ni = xl_ni(lda);
+  const XlRing rg = xl_ring(lda, ni, XL_BT_BYTES);
+  PGCN_CHECK(rg.nslot >= 2, PGCN_E_INVALID, "xstream ring: LDS");
+  const long long n_rg = (M + 15) / 16;
+  const dim3 grid((unsigned)std::min<long long>(n_rg, kCUs)),
+      block(64 * (XL_LOADERS + XL_NN_CONSUMERS));
+  const bool fold = xl_pow2(a_scale);
+#define XNR_CASE(NI)                                                                           \
+  case NI:                                                                                     \
+    if (C2 && fold)                                                                            \
+      hipLaunchKernelGGL((k_xs_nn_ring<NI, true, true, true>), grid, block, 0, s, M, N, K, A,   \
+                         lda, B, ldb, trans_b, C, ldc, maskT, a_scale, C2, e, rg);             \
+    else if (C2)                                                                               \
+      hipLaunchKernelGGL((k_xs_nn_ring<NI, true, true, false>), grid, block, 0, s, M, N, K, A,  \
+                         lda, B, ldb, trans_b, C, ldc, maskT, a_scale, C2, e, rg);             \
+    else if (maskT && fold)                                                                    \
+      hipLaunchKernelGGL((k_xs_nn_ring<NI, true, false, true>), grid, block, 0, s, M, N, K, A,  \
+                         lda, B, ldb, trans_b, C, ldc, maskT, a_scale, nullptr, e, rg);        \
+    else if (maskT)                                                                            \
+      hipLaunchKernelGGL((k_xs_nn_ring<NI, true, false, false>), grid, block, 0, s, M, N, K, A, \
+                         lda, B, ldb, trans_b, C, ldc, maskT, a_scale, nullptr, e, rg);        \
+    else                                                                                       \
+      hipLaunchKernelGGL((k_xs_nn_ring<NI, false, false, false>), grid, block, 0, s, M, N, K,   \
+                         A, lda, B, ldb, trans_b, C, ldc, maskT, a_scale, nullptr, e, rg);     \
+    break;
+  switch (ni) {
+    XNR_CASE(37) XNR_CASE(38) XNR_CASE(39) XNR_CASE(40)
+    default: PGCN_CHECK(false, PGCN_E_INVALID, "xstream ring: no kernel for this row width");
+  }
+#undef XNR_CASE
+}
+
+void launch_xstream_tn_ring(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
+                            const uint64_t *maskT, float a_scale, float *partial, int n_blocks,
+                            hipStream_t s) {
+  PGCN_CHECK(xstream_ring_ok(K, lda) && N <= 16, PGCN_E_INVALID,
+             "xstream ring: K in 577..640, lda = K rounded to 4, N <= 16");
+  const int ni = xl_ni(lda);
+  const XlRing rg = xl_ring(lda, ni, 0);
+  const dim3 grid((unsigned)n_blocks),
+      block(64 * (XL_LOADERS + XL_TN_CONSUMERS));  // every block writes its partial
+  const bool fold = xl_pow2(a_scale);
+#define XTR_CASE(NI)                                                                           \
+  case NI:                                                                                     \
+    if (maskT && fold)                                                                         \
+      hipLaunchKernelGGL((k_xs_tn_ring<NI, true, true>), grid, block, 0, s, M, N, K, A, lda, G, \
+                         ldg, maskT, a_scale, partial, rg);                                    \
+    else if (maskT)                                                                            \
+      hipLaunchKernelGGL((k_xs_tn_ring<NI, true, false>), grid, block, 0, s, M, N, K, A, lda,   \
+                         G, ldg, maskT, a_scale, partial, rg);                                 \
+    else                                                                                       \
+      hipLaunchKernelGGL((k_xs_tn_ring<NI, false, false>), grid, block, 0, s, M, N, K, A, lda,  \
+                         G, ldg, maskT, a_scale, partial, rg);                                 \
+    break;
+  switch (ni) {
+    XTR_CASE(37) XTR_CASE(38) XTR_CASE(39) XTR_CASE(40)
+    default: PGCN_CHECK(false, PGCN_E_INVALID, "xstream ring: no kernel for this row width");
+  }
+#undef XTR_CASE
+}
+
+}  // namespace pgcn

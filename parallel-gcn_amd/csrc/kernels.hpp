@@ -124,6 +124,16 @@ void launch_xstream_nn(int M, int N, int K, const float *A, int lda, const float
                        int trans_b, float *C, int ldc, const uint64_t *maskT, float a_scale,
                        hipStream_t s, float *C2 = nullptr,  // C2: drop(X) W beside C = X W
                        const XsEpilogue *epi = nullptr);
+// k_xstream_lds.hip: the X-stream products with loader and MFMA waves split (the default
+// form, g_xstream_ring; the launchers above dispatch to them)
+bool xstream_ring_ok(int K, int lda);
+void launch_xstream_nn_ring(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
+                            int trans_b, float *C, int ldc, const uint64_t *maskT, float a_scale,
+                            hipStream_t s, float *C2, const XsEpilogue &e);
+// partial[n_blocks][K][16] (the workgroups' sums; reduced in block order by the caller)
+void launch_xstream_tn_ring(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
+                            const uint64_t *maskT, float a_scale, float *partial, int n_blocks,
+                            hipStream_t s);
 // out[r][0:ld] = src[rows[r]][0:ld]  (ld % 4 == 0)
 void launch_gather_rows(const float *src, const int *rows, int n, int ld, float *out,
                         hipStream_t s);

@@ -1,5 +1,5 @@
-// parallel-gcn_amd/csrc/lds_dma.hpp -- device helpers shared by the LDS-staged GraphSum
-// kernels (k_graphsum_lds.hip, k_graphsum_ring.hip): LDS-DMA pieces issued from inline asm,
+// parallel-gcn_amd/csrc/lds_dma.hpp -- device helpers shared by the LDS-staged kernels
+// (k_graphsum_lds.hip, k_graphsum_ring.hip, k_xstream_lds.hip): LDS-DMA pieces issued from inline asm,
 // LDS hand-off words, float4 accumulation.
 #pragma once
 #include "common.hpp"
@@ -20,6 +20,17 @@ __device__ __forceinline__ void glds16(const void *gsrc, unsigned lds_dst) {
   unsigned keep;
   asm volatile(
       "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_dst)
+      : "memory");
+}
+
+// The same piece with the nontemporal hint (a stream read once: X in the X-stream kernels)
+__device__ __forceinline__ void glds16_nt(const void *gsrc, unsigned lds_dst) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(gsrc), "s"(lds_dst)

@@ -448,6 +448,22 @@ def test_fused_epilogue_bit_identical(loaded, pgcn, case):
             np.testing.assert_array_equal(a, b)
 
 
+def test_xstream_ring_engine_matches_register_kernels(pgcn):
+    """The loader / MFMA-wave split of the first layer's X-stream products (k_xstream_lds.hip,
+    default) against the register-streamed kernels in a whole run (dense 64-feature graph,
+    LDS GraphSum): the forward products are bit-identical, W1.grad sums the same rows in
+    another order, so epoch lines agree to float rounding."""
+    ds = pgcn.Dataset.synthetic(120000, 64, 41, 1500000, 21)
+    lines = {}
+    for ring in (1, 0):
+        with helpers.knobs(pgcn, xstream_ring=ring):
+            g = pgcn.GCN(pgcn.make_params(ds), ds)
+            lines[ring] = np.array([g.train_epoch() + g.eval(2) for _ in range(4)], np.float64)
+            g.close()
+    np.testing.assert_allclose(lines[1], lines[0], rtol=2e-5, atol=1e-6)
+    np.testing.assert_array_equal(lines[1][0, :2], lines[0][0, :2])  # epoch 1 forward: NN only
+
+
 def test_early_stopping_matches_reference(datasets, pgcn):
     """GCN::run's early stopping (hpdga gcn.cpp:238-250, src/gcn.cu:377-395): after epoch e >=
     k, stop when val_loss(e) > the mean of the last k val losses (the current one included,

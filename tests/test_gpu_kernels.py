@@ -387,7 +387,8 @@ def nibble_mask_ref(mask, base, M, K):
 @pytest.mark.parametrize("M,N,K,base", [(3001, 16, 602, 0), (1000, 16, 602, 41), (77, 12, 100, 63),
                                         (129, 16, 640, 5), (20, 3, 7, 0)])
 def test_gemm_xstream(pgcn, M, N, K, base):
-    """X-stream NN/TN kernels with nibble-layout dropout bits vs fp64 references; the dual NN
+    """X-stream NN/TN kernels with nibble-layout dropout bits vs fp64 references (the loader /
+    MFMA-wave split of k_xstream_lds.hip and the register-streamed kernels); the dual NN
     kernel bit-identical to the plain and masked ones."""
     rng = np.random.default_rng(7 * M + K)
     lda = (K + 3) // 4 * 4
@@ -417,15 +418,25 @@ def test_gemm_xstream(pgcn, M, N, K, base):
         pgcn.check(pgcn.lib.pgcn_gemm_tn_xstream(M, N, K, vp(dA), lda, vp(dG), N, vp(W), N,
                                                  vp(nib) if drop else None, 2.0, vp(ws),
                                                  stream()), "xtn")
-        # the LDS-DMA ring variant of the TN kernel (option; taken for K in 577..640, N = 16)
+        # the register-streamed kernels (xstream_ring 0): NN bit-identical to the loader /
+        # MFMA-wave split (default), TN the same sums in another order; and the TN LDS-DMA
+        # ring option of those (taken for K in 577..640, N = 16)
+        C0 = torch.full((M, ldc), float("nan"), device=DEV)
+        W0 = torch.full((K, N), float("nan"), device=DEV)
         W2 = torch.full((K, N), float("nan"), device=DEV)
-        pgcn.lib.pgcn_debug_set(b"xstream_tn_lds", 1)
-        pgcn.check(pgcn.lib.pgcn_gemm_tn_xstream(M, N, K, vp(dA), lda, vp(dG), N, vp(W2), N,
-                                                 vp(nib) if drop else None, 2.0, vp(ws),
-                                                 stream()), "xtn lds")
-        pgcn.lib.pgcn_debug_set(b"xstream_tn_lds", 0)
+        with helpers.knobs(pgcn, xstream_ring=0):
+            pgcn.check(pgcn.lib.pgcn_gemm_xstream(M, N, K, vp(dA), lda, vp(dB), N, 0, vp(C0),
+                                                  ldc, vp(nib) if drop else None, 2.0, stream()),
+                       "xnn regs")
+            pgcn.check(pgcn.lib.pgcn_gemm_tn_xstream(M, N, K, vp(dA), lda, vp(dG), N, vp(W0), N,
+                                                     vp(nib) if drop else None, 2.0, vp(ws),
+                                                     stream()), "xtn regs")
+            with helpers.knobs(pgcn, xstream_tn_lds=1):
+                pgcn.check(pgcn.lib.pgcn_gemm_tn_xstream(M, N, K, vp(dA), lda, vp(dG), N, vp(W2),
+                                                         N, vp(nib) if drop else None, 2.0,
+                                                         vp(ws), stream()), "xtn lds")
         torch.cuda.synchronize()
-        np.testing.assert_allclose(W2.cpu().numpy(), W.cpu().numpy(), rtol=1e-5, atol=1e-5)
+        np.testing.assert_array_equal(C0.cpu().numpy(), C.cpu().numpy())
         ref = Ae @ B.astype(np.float64)
         bound = np.abs(Ae) @ np.abs(B.astype(np.float64))
         o = C.cpu().numpy()
@@ -433,7 +444,8 @@ def test_gemm_xstream(pgcn, M, N, K, base):
         np.testing.assert_array_equal(o[:, N:], 0.0)
         ref_t = Ae.T @ Gm.astype(np.float64)
         bound_t = np.abs(Ae).T @ np.abs(Gm.astype(np.float64))
-        assert (np.abs(W.cpu().numpy() - ref_t) <= 1e-5 * bound_t + 1e-30).all()
+        for tn in (W, W0, W2):  # the same products, rows summed in different orders
+            assert (np.abs(tn.cpu().numpy() - ref_t) <= 1e-5 * bound_t + 1e-30).all()
         outs[drop] = C
     # the dual kernel (eval + next training product in one pass) is bit-identical to both
     C1 = torch.full((M, ldc), float("nan"), device=DEV)
