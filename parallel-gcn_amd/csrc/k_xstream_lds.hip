@@ -11,14 +11,14 @@
 // (tools/xs_micro.hip: read alone 91 us, read + MFMA in the same waves 122 us, MFMA alone
 // 50 us; loader + MFMA waves as below 90-98 us).
 //
-// One workgroup per CU, 5 waves (NN) or 4 (TN):
-//   wave 0 (loader)       copies whole 16-row groups of X (16 * lda contiguous floats) into an
+// One workgroup per CU, 6 waves (NN: 2 loaders, 4 consumers) or 4 (TN: 1 loader, 3 consumers):
+//   loader waves          copy whole 16-row groups of X (16 * lda contiguous floats) into an
 //                         LDS ring of up to 4 slots by LDS-DMA (global_load_lds_dwordx4,
 //                         nontemporal, 1 KB per instruction, no VGPRs, NI instructions per
 //                         group: a compile-time count, so hipcc sees a straight-line issue),
-//                         two groups in flight: wait for the slot to be handed back, issue,
-//                         s_waitcnt vmcnt(NI), publish the older group;
-//   waves 1..  (consumers) take the groups in turn, copy the group's MFMA operands from the
+//                         one group in flight each (option: two): wait for the slot to be
+//                         handed back, issue, s_waitcnt, publish;
+//   consumer waves        take the groups in turn, copy the group's MFMA operands from the
 //                         slot to registers (ds_read_b128), hand the slot back and run the
 //                         MFMAs, with their state (B of the NN product, the TN accumulators)
 //                         in registers.
@@ -52,9 +52,10 @@ namespace {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
-constexpr int XL_LOADERS = 1;
-constexpr int XL_NN_CONSUMERS = 4;  // NN: one per SIMD + a second on the loader's SIMD
-constexpr int XL_TN_CONSUMERS = 3;  // TN: its accumulators need a SIMD per consumer
+// NN: 2 loaders + 4 consumers (two waves on two SIMDs: 2 x ~220 registers fit); TN: 1 loader +
+// 3 consumers (its accumulators need a SIMD per consumer)
+constexpr int XL_NN_LOADERS = 2, XL_NN_CONSUMERS = 4;
+constexpr int XL_TN_LOADERS = 1, XL_TN_CONSUMERS = 3;
 constexpr int XL_LDS = 159 * 1024;  // ring + hand-off words (one workgroup per CU)
 constexpr int XL_FLAGS = 64;        // ready[8], freed[8] at the end
 constexpr int XL_KC = 10;           // the instantiated width: K in (576, 640] (reddit: 602)
@@ -121,10 +122,10 @@ __device__ __forceinline__ void xl_dma4(const char *gsrc, unsigned lds_dst) {
       : "memory");
 }
 
-// Loader wave `wave`: groups wave, wave + XL_LOADERS, ... into slot t % nslot, NI pieces
+// Loader wave `wave` of NL: groups wave, wave + NL, ... into slot t % nslot, NI pieces
 // each.  With two in flight a loader publishes group t - 2 once only group t's NI DMAs are
 // outstanding, or before it would block on a slot.
-template <int NI>
+template <int NI, int NL>
 __device__ __forceinline__ void xl_load(const float *__restrict__ A, int lda, long long M, int T,
                                         int wave, int lane, const XlRing &rg, char *lds,
                                         unsigned *ready, unsigned *freed) {
@@ -139,7 +140,7 @@ __device__ __forceinline__ void xl_load(const float *__restrict__ A, int lda, lo
     if (lane == 0) __atomic_store_n(ready + u % rg.nslot, (unsigned)(u + 1), __ATOMIC_RELAXED);
     asm volatile("" ::: "memory");
   };
-  for (int t = wave; t < T; t += XL_LOADERS) {
+  for (int t = wave; t < T; t += NL) {
     const int slot = t % rg.nslot;
     if (t >= rg.nslot) {
       const unsigned need = (unsigned)(t - rg.nslot + 1);
@@ -201,7 +202,7 @@ __device__ __forceinline__ void xl_release(unsigned *freed, int slot, int t, int
 // X[row i][16 s + 4 g + t] -- k_xstream_nn's feed and order, so the same bits (up to the sign
 // of zero products: see xl_apply4).  B^T sits in LDS ahead of the ring (as in k_xstream_nn).
 template <int NI, bool MASKED, bool DUAL, bool FOLD>
-__global__ __launch_bounds__(64 * (XL_LOADERS + XL_NN_CONSUMERS), 1) void k_xs_nn_ring(
+__global__ __launch_bounds__(64 * (XL_NN_LOADERS + XL_NN_CONSUMERS), 1) void k_xs_nn_ring(
     int M, int N, int K, const float *__restrict__ A, int lda, const float *__restrict__ B,
     int ldb, int trans_b, float *__restrict__ C, int ldc, const uint64_t *__restrict__ maskT,
     float a_scale, float *__restrict__ C2, XsEpilogue epi, XlRing rg) {
@@ -224,11 +225,11 @@ __global__ __launch_bounds__(64 * (XL_LOADERS + XL_NN_CONSUMERS), 1) void k_xs_n
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int T = xl_groups(M);
-  if (wave < XL_LOADERS) {
-    xl_load<NI>(A, lda, M, T, wave, lane, rg, lds, ready, freed);
+  if (wave < XL_NN_LOADERS) {
+    xl_load<NI, XL_NN_LOADERS>(A, lda, M, T, wave, lane, rg, lds, ready, freed);
     return;
   }
-  const int cid = wave - XL_LOADERS, g = lane >> 4, i = lane & 15;
+  const int cid = wave - XL_NN_LOADERS, g = lane >> 4, i = lane & 15;
   const float *bl = reinterpret_cast<const float *>(lds) + i * XL_BS + 4 * g;
   auto load_mask = [&](int t, uint64_t(&m)[4]) {  // keep bits of the lane's row of group t
     long long row = (blockIdx.x + (long long)t * gridDim.x) * 16 + i;
@@ -317,7 +318,7 @@ __global__ __launch_bounds__(64 * (XL_LOADERS + XL_NN_CONSUMERS), 1) void k_xs_n
 // X[row 4q + g][64 c + 4 i + t] and G[row 4q + g][i] (k_xstream_tn's feed); the two consumers'
 // accumulators (groups t = c mod 3 for consumer c) are added in consumer order at the end.
 template <int NI, bool MASKED, bool FOLD>
-__global__ __launch_bounds__(64 * (XL_LOADERS + XL_TN_CONSUMERS), 1) void k_xs_tn_ring(
+__global__ __launch_bounds__(64 * (XL_TN_LOADERS + XL_TN_CONSUMERS), 1) void k_xs_tn_ring(
     int M, int N, int K, const float *__restrict__ A, int lda, const float *__restrict__ G,
     int ldg, const uint64_t *__restrict__ maskT, float a_scale, float *__restrict__ partial,
     XlRing rg) {
@@ -336,10 +337,10 @@ __global__ __launch_bounds__(64 * (XL_LOADERS + XL_TN_CONSUMERS), 1) void k_xs_t
   for (int c = 0; c < KC; c++)
 #pragma unroll
     for (int t = 0; t < 4; t++) acc[c][t] = floatx4{0.f, 0.f, 0.f, 0.f};
-  if (wave < XL_LOADERS) {
-    xl_load<NI>(A, lda, M, T, wave, lane, rg, lds, ready, freed);
+  if (wave < XL_TN_LOADERS) {
+    xl_load<NI, XL_TN_LOADERS>(A, lda, M, T, wave, lane, rg, lds, ready, freed);
   } else {
-    const int cid = wave - XL_LOADERS;
+    const int cid = wave - XL_TN_LOADERS;
     auto load_rows = [&](int t, float(&bv)[4], uint64_t(&m)[4]) {  // dZ and keep bits, group t
       const long long row0 = (blockIdx.x + (long long)t * gridDim.x) * 16;
 #pragma unroll
@@ -394,8 +395,8 @@ __global__ __launch_bounds__(64 * (XL_LOADERS + XL_TN_CONSUMERS), 1) void k_xs_t
   __syncthreads();
   float *red = reinterpret_cast<float *>(lds);
   constexpr int RED = KC * 4 * 4 * 64;  // floats per consumer
-  if (wave > XL_LOADERS) {
-    float *rw = red + (wave - XL_LOADERS - 1) * RED;
+  if (wave > XL_TN_LOADERS) {
+    float *rw = red + (wave - XL_TN_LOADERS - 1) * RED;
 #pragma unroll
     for (int c = 0; c < KC; c++)
 #pragma unroll
@@ -404,7 +405,7 @@ __global__ __launch_bounds__(64 * (XL_LOADERS + XL_TN_CONSUMERS), 1) void k_xs_t
         for (int r = 0; r < 4; r++) rw[((c * 4 + t) * 4 + r) * 64 + lane] = acc[c][t][r];
   }
   __syncthreads();
-  if (wave == XL_LOADERS) {
+  if (wave == XL_TN_LOADERS) {
     float *p = partial + (long long)blockIdx.x * K * 16;
 #pragma unroll
     for (int c = 0; c < KC; c++)
@@ -445,7 +446,7 @@ void launch_xstream_nn_ring(int M, int N, int K, const float *A, int lda, const 
   PGCN_CHECK(rg.nslot >= 2, PGCN_E_INVALID, "xstream ring: LDS");
   const long long n_rg = (M + 15) / 16;
   const dim3 grid((unsigned)std::min<long long>(n_rg, kCUs)),
-      block(64 * (XL_LOADERS + XL_NN_CONSUMERS));
+      block(64 * (XL_NN_LOADERS + XL_NN_CONSUMERS));
   const bool fold = xl_pow2(a_scale);
 #define XNR_CASE(NI)                                                                           \
   case NI:                                                                                     \
@@ -480,7 +481,7 @@ void launch_xstream_tn_ring(int M, int N, int K, const float *A, int lda, const 
   const int ni = xl_ni(lda);
   const XlRing rg = xl_ring(lda, ni, 0);
   const dim3 grid((unsigned)n_blocks),
-      block(64 * (XL_LOADERS + XL_TN_CONSUMERS));  // every block writes its partial
+      block(64 * (XL_TN_LOADERS + XL_TN_CONSUMERS));  // every block writes its partial
   const bool fold = xl_pow2(a_scale);
 #define XTR_CASE(NI)                                                                           \
   case NI:                                                                                     \
