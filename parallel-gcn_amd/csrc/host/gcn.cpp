@@ -460,7 +460,7 @@ void GCN::build(const GCNData &data) {
     ctx.side_join = Event::create();
   }
   ctx.train_ahead = g_train_ahead != 0;
-  ctx.mask_side = g_mask_side != 0;
+  ctx.mask_side = g_mask_side;
   ctx.xent_partials = xent_partials.get();
   ctx.xent_blocks = xent_blocks(prow);
   ctx.gemm_workspace = gemm_ws.get();

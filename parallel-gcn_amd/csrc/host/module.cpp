@@ -144,6 +144,13 @@ void SparseMatmul::forward(bool training, const Stream &s) const {
   const long long base = drop->state().mask_base;
   const float scale = drop->scale();
   if (!training && x->ax && eval_out) {  // eval_ax: (Â X) W1 straight into the GraphSum's output
+    if (ctx->train_ahead && ctx->mask_side == 2 && ctx->side_stream && x->maskT &&
+        !drop->drawn_ahead()) {
+      // the next training forward's input mask, drawn on the side stream beside this pass
+      ctx->tn_start.record(s.get());
+      ctx->tn_start.wait_on(ctx->side_stream);
+      drop->draw_ahead(ctx->side_stream, &ctx->mask_ready);
+    }
     if (xstream_ok(b->cols, x->cols)) {
       // eval: out = relu(Â X W1) (GraphSum, then its fused ReLU; the Dropout after it is the
       // identity in eval), which the reassociated output layer's GraphSum reads next
@@ -214,7 +221,7 @@ void SparseMatmul::backward(const Stream &s) const {
   const float scale = drop->scale();
   MmProfile prof(ctx, s.get(), x->dense ? 2.0 * x->rows * b->cols * x->cols : 0.0);
   if (x->dense && x->maskT) {  // the nibble mask of the last training forward
-    if (ctx->train_ahead && ctx->mask_side && ctx->side_stream && !drop->drawn_ahead()) {
+    if (ctx->train_ahead && ctx->mask_side == 1 && ctx->side_stream && !drop->drawn_ahead()) {
       // the next epoch's input mask, drawn on the side stream while this pass streams X
       // (maskT, which this pass reads, is rebuilt from it only by the next eval / training
       // forward on this stream)

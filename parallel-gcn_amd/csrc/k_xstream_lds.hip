@@ -44,6 +44,8 @@ namespace pgcn {
 // flight per loader wave (1 or 2)
 int g_xstream_ring = 1;
 int g_xstream_ring_inflight = 1;
+// "xstream_ring_slots": at most this many ring slots (0: as many as fit)
+int g_xstream_ring_slots = 0;
 // "xstream_ring_diag" (timing only, wrong results): 1 = consumers skip their MFMAs (the
 // loaders' pace), 2 = loaders skip their DMAs (the consumers' pace)
 int g_xstream_ring_diag = 0;
@@ -77,7 +79,8 @@ XlRing xl_ring(int lda, int ni, int off) {
   XlRing r;
   r.off = off;
   r.st = lda / 4;
-  r.nslot = std::min(4, (XL_LDS - XL_FLAGS - off) / (ni * 1024));
+  r.nslot = std::min(g_xstream_ring_slots > 1 ? std::min(4, g_xstream_ring_slots) : 4,
+                     (XL_LDS - XL_FLAGS - off) / (ni * 1024));
   r.two = g_xstream_ring_inflight > 1 && r.nslot == 4;
   r.diag = g_xstream_ring_diag;
   return r;
