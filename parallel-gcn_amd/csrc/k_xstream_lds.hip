@@ -46,6 +46,10 @@ int g_xstream_ring = 1;
 int g_xstream_ring_inflight = 1;
 // "xstream_ring_slots": at most this many ring slots (0: as many as fit)
 int g_xstream_ring_slots = 0;
+// "xstream_tn_split": TN with every consumer taking a share of K of every group (k_xs_tn_split;
+// r02: 173 vs 137 us on reddit -- every consumer now waits on every group and its dZ / keep-bit
+// prefetch runs only one group ahead)
+int g_xstream_tn_split = 0;
 // "xstream_ring_diag" (timing only, wrong results): 1 = consumers skip their MFMAs (the
 // loaders' pace), 2 = loaders skip their DMAs (the consumers' pace)
 int g_xstream_ring_diag = 0;
@@ -128,7 +132,9 @@ __device__ __forceinline__ void xl_dma4(const char *gsrc, unsigned lds_dst) {
 // Loader wave `wave` of NL: groups wave, wave + NL, ... into slot t % nslot, NI pieces
 // each.  With two in flight a loader publishes group t - 2 once only group t's NI DMAs are
 // outstanding, or before it would block on a slot.
-template <int NI, int NL>
+// REL: releases per slot use -- 1 (a consumer per group stores t + 1 into freed) or the
+// number of consumers that each read a share of every group (they add 1 each)
+template <int NI, int NL, int REL = 1>
 __device__ __forceinline__ void xl_load(const float *__restrict__ A, int lda, long long M, int T,
                                         int wave, int lane, const XlRing &rg, char *lds,
                                         unsigned *ready, unsigned *freed) {
@@ -146,7 +152,8 @@ __device__ __forceinline__ void xl_load(const float *__restrict__ A, int lda, lo
   for (int t = wave; t < T; t += NL) {
     const int slot = t % rg.nslot;
     if (t >= rg.nslot) {
-      const unsigned need = (unsigned)(t - rg.nslot + 1);
+      const unsigned need =
+          REL == 1 ? (unsigned)(t - rg.nslot + 1) : (unsigned)(REL * (t / rg.nslot));
       if ((unsigned)__builtin_amdgcn_readfirstlane(__atomic_load_n(freed + slot, __ATOMIC_RELAXED)) <
           need) {
         if (pend >= 0) {  // about to block: the group in flight goes out first
@@ -425,6 +432,104 @@ __global__ __launch_bounds__(64 * (XL_TN_LOADERS + XL_TN_CONSUMERS), 1) void k_x
   }
 }
 
+// TN, K-split form: every consumer reads every group, each its own 64-column chunks of K
+// (XL_KC chunks over XL_TS_CONSUMERS waves: 3, 3, 2, 2), so its accumulators are a few
+// registers and six waves fit (2 loaders + 4 consumers, all four SIMDs running MFMAs).  A
+// slot goes back when every consumer has added its release.  Each consumer sums its output
+// rows k over the workgroup's groups in order and writes them: no cross-wave reduction.
+constexpr int XL_TS_LOADERS = 2, XL_TS_CONSUMERS = 4, XL_TS_MAXC = 3;
+
+template <int NI, bool MASKED, bool FOLD>
+__global__ __launch_bounds__(64 * (XL_TS_LOADERS + XL_TS_CONSUMERS), 1) void k_xs_tn_split(
+    int M, int N, int K, const float *__restrict__ A, int lda, const float *__restrict__ G,
+    int ldg, const uint64_t *__restrict__ maskT, float a_scale, float *__restrict__ partial,
+    XlRing rg) {
+  __shared__ __attribute__((aligned(1024))) char lds[XL_LDS];
+  unsigned *const ready = reinterpret_cast<unsigned *>(lds + XL_LDS - XL_FLAGS);
+  unsigned *const freed = ready + 8;
+  if (threadIdx.x < 16) ready[threadIdx.x] = 0u;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, i = lane & 15;
+  const int T = xl_groups(M);
+  if (wave < XL_TS_LOADERS) {
+    xl_load<NI, XL_TS_LOADERS, XL_TS_CONSUMERS>(A, lda, M, T, wave, lane, rg, lds, ready, freed);
+    return;
+  }
+  const int cid = wave - XL_TS_LOADERS;
+  const int c0 = cid < 2 ? 3 * cid : 6 + 2 * (cid - 2);  // first chunk: 0, 3, 6, 8
+  const int nc = cid < 2 ? 3 : 2;                          // chunks: 3, 3, 2, 2
+  floatx4 acc[XL_TS_MAXC][4];
+#pragma unroll
+  for (int c = 0; c < XL_TS_MAXC; c++)
+#pragma unroll
+    for (int t = 0; t < 4; t++) acc[c][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  auto load_rows = [&](int t, float(&bv)[4], uint64_t(&m)[4]) {  // dZ and keep bits, group t
+    const long long row0 = (blockIdx.x + (long long)t * gridDim.x) * 16;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const long long mr = row0 + 4 * q + g;
+      const long long row = mr < M ? mr : M - 1;
+      const float v = G[row * ldg + (i < N ? i : 0)];
+      bv[q] = (mr < M && i < N) ? (MASKED && FOLD ? v * a_scale : v) : 0.0f;
+      if constexpr (MASKED) m[q] = maskT[row * 16 + i];
+    }
+  };
+  auto group = [&](int t, const float(&bj)[4], const uint64_t(&mw)[4], float(&bjn)[4],
+                   uint64_t(&mwn)[4]) {
+    if (t + 1 < T) load_rows(t + 1, bjn, mwn);
+    const int slot = t % rg.nslot;
+    lds_wait_ge(ready + slot, (unsigned)(t + 1));
+    const char *sp = lds + rg.off + slot * (NI * 1024) + (c0 * 16 + i) * 16;
+    float4 xa[4][XL_TS_MAXC];
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+#pragma unroll
+      for (int c = 0; c < XL_TS_MAXC; c++)
+        if (c < nc) xa[q][c] = *reinterpret_cast<const float4 *>(sp + (4 * q + g) * rg.st * 16 + 256 * c);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_fetch_add(freed + slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    asm volatile("" ::: "memory");
+    if (rg.diag == 1) return;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+#pragma unroll
+      for (int c = 0; c < XL_TS_MAXC; c++) {
+        if (c < nc) {
+          float4 x = xa[q][c];
+          if constexpr (MASKED)
+            xl_apply4<FOLD>(x, (uint32_t)(mw[q] >> (4 * (c0 + c))) & 0xfu, a_scale);
+          acc[c][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(x.x, bj[q], acc[c][0], 0, 0, 0);
+          acc[c][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(x.y, bj[q], acc[c][1], 0, 0, 0);
+          acc[c][2] = __builtin_amdgcn_mfma_f32_16x16x4f32(x.z, bj[q], acc[c][2], 0, 0, 0);
+          acc[c][3] = __builtin_amdgcn_mfma_f32_16x16x4f32(x.w, bj[q], acc[c][3], 0, 0, 0);
+        }
+      }
+    }
+  };
+  float bja[4] = {0.f, 0.f, 0.f, 0.f}, bjb[4] = {0.f, 0.f, 0.f, 0.f};
+  uint64_t mwa[4] = {0, 0, 0, 0}, mwb[4] = {0, 0, 0, 0};
+  if (T > 0) load_rows(0, bja, mwa);
+  for (int t = 0; t < T; t += 2) {
+    group(t, bja, mwa, bjb, mwb);
+    if (t + 1 < T) group(t + 1, bjb, mwb, bja, mwa);
+  }
+  float *p = partial + (long long)blockIdx.x * K * 16;
+#pragma unroll
+  for (int c = 0; c < XL_TS_MAXC; c++) {
+    if (c < nc) {
+#pragma unroll
+      for (int t = 0; t < 4; t++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int k = 64 * (c0 + c) + 4 * (4 * g + r) + t;
+          if (k < K) p[(long long)k * 16 + i] = acc[c][t][r];
+        }
+    }
+  }
+}
+
 }  // namespace
 
 // a_scale = 2^n (dropout 1/2, 3/4, ...): scaling by it is exact, so it can move
@@ -479,6 +584,32 @@ void launch_xstream_nn_ring(int M, int N, int K, const float *A, int lda, const 
 void launch_xstream_tn_ring(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
                             const uint64_t *maskT, float a_scale, float *partial, int n_blocks,
                             hipStream_t s) {
+  if (g_xstream_tn_split) {
+    PGCN_CHECK(xstream_ring_ok(K, lda) && N <= 16, PGCN_E_INVALID,
+               "xstream ring: K in 577..640, lda = K rounded to 4, N <= 16");
+    const int ni = xl_ni(lda);
+    const XlRing rg = xl_ring(lda, ni, 0);
+    const dim3 grid((unsigned)n_blocks), block(64 * (XL_TS_LOADERS + XL_TS_CONSUMERS));
+    const bool fold = xl_pow2(a_scale);
+#define XTS_CASE(NI)                                                                           \
+  case NI:                                                                                     \
+    if (maskT && fold)                                                                         \
+      hipLaunchKernelGGL((k_xs_tn_split<NI, true, true>), grid, block, 0, s, M, N, K, A, lda,   \
+                         G, ldg, maskT, a_scale, partial, rg);                                 \
+    else if (maskT)                                                                            \
+      hipLaunchKernelGGL((k_xs_tn_split<NI, true, false>), grid, block, 0, s, M, N, K, A, lda,  \
+                         G, ldg, maskT, a_scale, partial, rg);                                 \
+    else                                                                                       \
+      hipLaunchKernelGGL((k_xs_tn_split<NI, false, false>), grid, block, 0, s, M, N, K, A, lda, \
+                         G, ldg, maskT, a_scale, partial, rg);                                 \
+    break;
+    switch (ni) {
+      XTS_CASE(37) XTS_CASE(38) XTS_CASE(39) XTS_CASE(40)
+      default: PGCN_CHECK(false, PGCN_E_INVALID, "xstream ring: no kernel for this row width");
+    }
+#undef XTS_CASE
+    return;
+  }
   PGCN_CHECK(xstream_ring_ok(K, lda) && N <= 16, PGCN_E_INVALID,
              "xstream ring: K in 577..640, lda = K rounded to 4, N <= 16");
   const int ni = xl_ni(lda);

@@ -424,6 +424,7 @@ def test_gemm_xstream(pgcn, M, N, K, base):
         C0 = torch.full((M, ldc), float("nan"), device=DEV)
         W0 = torch.full((K, N), float("nan"), device=DEV)
         W2 = torch.full((K, N), float("nan"), device=DEV)
+        W3 = torch.full((K, N), float("nan"), device=DEV)
         with helpers.knobs(pgcn, xstream_ring=0):
             pgcn.check(pgcn.lib.pgcn_gemm_xstream(M, N, K, vp(dA), lda, vp(dB), N, 0, vp(C0),
                                                   ldc, vp(nib) if drop else None, 2.0, stream()),
@@ -435,6 +436,10 @@ def test_gemm_xstream(pgcn, M, N, K, base):
                 pgcn.check(pgcn.lib.pgcn_gemm_tn_xstream(M, N, K, vp(dA), lda, vp(dG), N, vp(W2),
                                                          N, vp(nib) if drop else None, 2.0,
                                                          vp(ws), stream()), "xtn lds")
+        with helpers.knobs(pgcn, xstream_tn_split=1):  # the K-split ring TN (option)
+            pgcn.check(pgcn.lib.pgcn_gemm_tn_xstream(M, N, K, vp(dA), lda, vp(dG), N, vp(W3), N,
+                                                     vp(nib) if drop else None, 2.0, vp(ws),
+                                                     stream()), "xtn split")
         torch.cuda.synchronize()
         np.testing.assert_array_equal(C0.cpu().numpy(), C.cpu().numpy())
         ref = Ae @ B.astype(np.float64)
@@ -444,7 +449,7 @@ def test_gemm_xstream(pgcn, M, N, K, base):
         np.testing.assert_array_equal(o[:, N:], 0.0)
         ref_t = Ae.T @ Gm.astype(np.float64)
         bound_t = np.abs(Ae).T @ np.abs(Gm.astype(np.float64))
-        for tn in (W, W0, W2):  # the same products, rows summed in different orders
+        for tn in (W, W0, W2, W3):  # the same products, rows summed in different orders
             assert (np.abs(tn.cpu().numpy() - ref_t) <= 1e-5 * bound_t + 1e-30).all()
         outs[drop] = C
     # the dual kernel (eval + next training product in one pass) is bit-identical to both

@@ -1,8 +1,7 @@
 """X-stream kernels on the reddit shape through the C ABI (run on the GPU box): ms per call of
 pgcn_gemm_xstream (Z = drop(X) W1, unmasked and with nibble keep bits) and pgcn_gemm_tn_xstream
 (W1.grad = drop(X)^T dZ) for each value of the "xstream_ring" knob (1: loader / MFMA-wave
-split, k_xstream_lds.hip, with 2 or 1 groups in flight per loader wave; 0: register-streamed
-kernels; diag 1 / 2: consumers without MFMAs / loaders without DMAs, timing only), with HIP
+split, k_xstream_lds.hip, TN in its K-split form or not; 0: register-streamed kernels; diag 1 / 2: consumers without MFMAs / loaders without DMAs, timing only), with HIP
 events on torch's stream.
 One JSON line.
 
@@ -61,10 +60,10 @@ def timeit(fn, reps=20):
 
 
 out = {"M": M, "K": K, "lda": LDA}
-for ring, infl, diag in ((1, 2, 0), (1, 1, 0), (0, 1, 0), (1, 2, 1), (1, 2, 2)):
-    with helpers.knobs(pg, xstream_ring=ring, xstream_ring_inflight=infl, xstream_ring_diag=diag):
+for ring, split, diag in ((1, 1, 0), (1, 0, 0), (0, 0, 0), (1, 1, 1), (1, 1, 2)):
+    with helpers.knobs(pg, xstream_ring=ring, xstream_tn_split=split, xstream_ring_diag=diag):
         for name, fn in (("nn", lambda: nn(False)), ("nn_masked", lambda: nn(True)),
                          ("tn_masked", lambda: tn(True))):
-            out[f"{name}_ring{ring}_{infl}" + (f"_diag{diag}" if diag else "") + "_ms"] = \
+            out[f"{name}_ring{ring}_split{split}" + (f"_diag{diag}" if diag else "") + "_ms"] = \
                 round(timeit(fn), 4)
 print(json.dumps(out))
