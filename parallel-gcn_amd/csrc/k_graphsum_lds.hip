@@ -642,8 +642,20 @@ __global__ __launch_bounds__(256) void k_gs_lds_combine(const float4 *__restrict
   const long long r = t >> 2;
   if (r >= n) return;
   const int v = (int)(t & 3);
-  float4 a = partial[r * 4 + v];
-  for (int b = 1; b < nb; b++) f4_acc(a, partial[((long long)b * part_stride + r) * 4 + v]);
+  float4 a;
+  if (nb <= 8) {  // every block's partial loaded before the (ordered) adds
+    float4 p[8];
+#pragma unroll
+    for (int b = 0; b < 8; b++)
+      if (b < nb) p[b] = partial[((long long)b * part_stride + r) * 4 + v];
+    a = p[0];
+#pragma unroll
+    for (int b = 1; b < 8; b++)
+      if (b < nb) f4_acc(a, p[b]);
+  } else {
+    a = partial[r * 4 + v];
+    for (int b = 1; b < nb; b++) f4_acc(a, partial[((long long)b * part_stride + r) * 4 + v]);
+  }
   const float s = scale[r];
   a.x *= s;
   a.y *= s;
