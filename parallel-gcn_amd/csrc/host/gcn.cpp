@@ -526,6 +526,7 @@ void GCN::insert_first_layer() {
   auto drop = std::make_unique<Dropout>(nullptr, params.dropouts.front(), rngs[0], &ctx);
   const Dropout *dptr = drop.get();
   dropouts_.push_back(dptr);
+  if (feats.dense && feats.maskT) ctx.input_drop = dptr;  // the X-stream path's input mask
   modules.push_back(std::move(drop));
   auto var1 = std::make_shared<Variable>(prow, h, true, round_up4(h));
   variables.push_back(var1);

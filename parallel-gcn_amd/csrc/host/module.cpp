@@ -500,7 +500,15 @@ Matmul::Matmul(shared_ptr<Variable> a_, shared_ptr<Variable> b_, shared_ptr<Vari
                int m_, int n_, int p_, ModuleContext *ctx_)
     : a(std::move(a_)), b(std::move(b_)), c(std::move(c_)), m(m_), n(n_), p(p_), ctx(ctx_) {}
 
-void Matmul::forward(bool, const Stream &s) const {
+void Matmul::forward(bool training, const Stream &s) const {
+  if (last_layer && !training && ctx->mask_side == 3 && ctx->train_ahead && ctx->side_stream &&
+      ctx->input_drop && !ctx->input_drop->drawn_ahead()) {
+    // the next training forward's input mask, drawn on the side stream beside this layer's
+    // product and the loss (short HBM-bound kernels with room beside them on every CU)
+    ctx->tn_start.record(s.get());
+    ctx->tn_start.wait_on(ctx->side_stream);
+    ctx->input_drop->draw_ahead(ctx->side_stream, &ctx->mask_ready);
+  }
   const bool cmp = last_layer && ctx->compact_n;  // compact output layer: the split's rows
   const Variable &A = cmp ? *ctx->compact_z : *a, &C = cmp ? *ctx->compact_out : *c;
   MmProfile prof(ctx, s.get(), 2.0 * (cmp ? ctx->compact_n : m) * p * n);

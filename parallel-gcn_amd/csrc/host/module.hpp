@@ -83,15 +83,18 @@ class Module {
 
 class ReLU;
 class GraphSum;
+class Dropout;
 
 // Shared per-GCN state the modules read (current split, comm, profiling, RNG table).
 struct ModuleContext {
   bool train_ahead = true;     // eval computes the next training forward's first product too
   // train-ahead option "mask_side": the next input mask is drawn on a side stream beside the
   // weight-gradient pass (1; r01: no gain -- the RNG kernel and the pass slow each other down
-  // and the reduce kernels after the pass starve) or beside the eval forward's X-stream
-  // product (2), else by the training forward on the main stream
+  // and the reduce kernels after the pass starve), beside the eval forward's X-stream product
+  // (2), or beside the eval forward's output layer and loss (3), else by the training forward
+  // on the main stream
   int mask_side = 0;
+  const Dropout *input_drop = nullptr;  // the first layer's Dropout (mask_side 3)
   hipStream_t side_stream = nullptr;  // ... drawn here ...
   Event tn_start, mask_ready;         // ... after tn_start (main), signalling mask_ready
   // "mm_side": a Matmul's weight gradient (b.grad = a^T c.grad, needed only by the optimizer)
