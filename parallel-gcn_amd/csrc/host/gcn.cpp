@@ -33,6 +33,10 @@ int g_split_cols = 1;
 // "fuse_epilogue" (read at engine build): the ReLU / Dropout modules next to a GraphSum run in
 // its final-write epilogue (gs_epilogue.hpp), bit-identical to separate launches
 int g_fuse_epilogue = 1;
+// "fuse_output": the output layer's Matmul forward runs inside the loss (launch_out_xent) when
+// the Matmul produces the logits (the reassociated order: GraphSum, then Matmul) from at most
+// 16 columns (bit-identical)
+int g_fuse_output = 1;
 // "mm_side" (read at engine build): Matmul weight gradients on the side stream (ModuleContext)
 // on graphs of at least kMmSideRows rows; 2 = on every graph.  Off: r02 A/B on reddit-114M,
 // three runs each, 486.5 (on) vs 487.4 (off) epochs/s -- the LDS GraphSum holds every CU with
@@ -477,8 +481,20 @@ void GCN::build(const GCNData &data) {
                  params.dropouts[(size_t)l], l);
   insert_last_layer();
   if (g_fuse_epilogue && !comm) fuse_epilogues();
+  if (g_fuse_output && !comm) fuse_output_layer();
   optimizer = Adam(weights, decays, adam_params);
   PGCN_HIP(hipDeviceSynchronize());
+}
+
+void GCN::fuse_output_layer() {
+  const size_t n = modules.size();
+  if (n < 2) return;
+  auto *ce = dynamic_cast<CrossEntropyLoss *>(modules[n - 1].get());
+  auto *mm = dynamic_cast<Matmul *>(modules[n - 2].get());
+  if (!ce || !mm || mm->output() != ce->input() || mm->inner() > 16 || mm->inner() < 1) return;
+  if (ce->input()->ld > 116 || mm->input()->rows != ce->input()->rows) return;
+  ce->fused = mm;
+  mm->fused_forward = true;
 }
 
 // GraphSum -> ReLU(out) [-> Dropout(out)] in the module list: the ReLU and the Dropout run in

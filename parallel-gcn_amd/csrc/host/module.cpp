@@ -501,6 +501,7 @@ Matmul::Matmul(shared_ptr<Variable> a_, shared_ptr<Variable> b_, shared_ptr<Vari
     : a(std::move(a_)), b(std::move(b_)), c(std::move(c_)), m(m_), n(n_), p(p_), ctx(ctx_) {}
 
 void Matmul::forward(bool training, const Stream &s) const {
+  if (fused_forward && !(last_layer && ctx->compact_n)) return;  // CrossEntropyLoss::forward
   if (last_layer && !training && ctx->mask_side == 3 && ctx->train_ahead && ctx->side_stream &&
       ctx->input_drop && !ctx->input_drop->drawn_ahead()) {
     // the next training forward's input mask, drawn on the side stream beside this layer's
@@ -548,6 +549,14 @@ CrossEntropyLoss::CrossEntropyLoss(shared_ptr<Variable> logits_, int num_classes
     : logits(std::move(logits_)), num_classes(num_classes_), ctx(ctx_) {}
 
 void CrossEntropyLoss::forward(bool training, const Stream &s) const {
+  if (fused && !ctx->compact_n) {
+    const Variable &Hv = *fused->input(), &Wv = *fused->weight();
+    launch_out_xent(Hv.dev_data.get(), Hv.ld, fused->inner(), Wv.dev_data.get(), Wv.ld,
+                    logits->dev_data.get(), logits->ld, training ? logits->dev_grad.get() : nullptr,
+                    ctx->truth, logits->rows, num_classes, ctx->count, training ? 1 : 0,
+                    ctx->xent_partials, s.get());
+    return;
+  }
   const Variable &L = ctx->compact_n ? *ctx->compact_out : *logits;
   launch_xent_fwd(L.dev_data.get(), L.ld, training ? L.dev_grad.get() : nullptr,
                   ctx->compact_n ? ctx->compact_truth : ctx->truth,

@@ -290,8 +290,13 @@ class Matmul : public Module {
 
  public:
   bool last_layer = false;  // the output layer's Matmul (compact rows apply)
+  bool fused_forward = false;  // its forward runs inside the loss's (CrossEntropyLoss::fused)
   Matmul(shared_ptr<Variable> a_, shared_ptr<Variable> b_, shared_ptr<Variable> c_, int m_,
          int n_, int p_, ModuleContext *ctx_);
+  const Variable *input() const { return a.get(); }
+  const Variable *weight() const { return b.get(); }
+  const Variable *output() const { return c.get(); }
+  int inner() const { return n; }
   void forward(bool training, const Stream &s) const override;
   void backward(const Stream &s) const override;
 };
@@ -305,6 +310,9 @@ class CrossEntropyLoss : public Module {
 
  public:
   CrossEntropyLoss(shared_ptr<Variable> logits_, int num_classes_, ModuleContext *ctx_);
+  // the output layer's Matmul whose forward this loss computes with its own (null: none)
+  const Matmul *fused = nullptr;
+  const Variable *input() const { return logits.get(); }
   void forward(bool training, const Stream &s) const override;
   void backward(const Stream &s) const override;
   void set_num_samples(int n) override { num_samples = n; }

@@ -248,11 +248,21 @@ __device__ __forceinline__ float block_sum(float v, float *smem) {
 // ------------------------------------------------------------------------------------------
 constexpr int XR = 256;  // rows per cross-entropy block (= threads)
 
+// FUSED: the logits are computed here from the output layer's input H [n][ldh] (kh <= 16
+// columns) and W [kh][ldw] -- each thread its row, z[j] = an fmaf chain over k in the order of
+// k_gemm_nn's v_mfma_f32_16x16x4_f32 sequence (MFMA t sums k = t, 4 + t, 8 + t, 12 + t as a
+// k-ordered fma chain), so the same bits as the separate Matmul -- and then go through the
+// same tile as the loaded ones (the output layer's Matmul forward + CrossEntropyLoss forward,
+// hpdga module.cpp:13-38, :122-153, in one pass: the logits are written once, not written
+// and read back).
+template <bool FUSED>
 __global__ __launch_bounds__(256) void k_xent_fwd(float *__restrict__ logits, int ld,
                                                   float *__restrict__ grad,
                                                   const int *__restrict__ truth, int n, int c,
                                                   int count, int training,
-                                                  float *__restrict__ partials, int write_back) {
+                                                  float *__restrict__ partials, int write_back,
+                                                  const float *__restrict__ H, int ldh, int kh,
+                                                  const float *__restrict__ W, int ldw) {
   // write_back 0: the shifted logits stay in LDS (the compact output layer's logits are read
   // by nobody after the loss; hpdga's in-place shift is kept where the variable is visible)
   extern __shared__ float smem[];
@@ -297,7 +307,31 @@ __global__ __launch_bounds__(256) void k_xent_fwd(float *__restrict__ logits, in
       reinterpret_cast<float4 *>(dst + base)[q] = make_float4(d[0], d[1], d[2], d[3]);
     }
   };
-  to_lds(logits);
+  if constexpr (FUSED) {
+    __shared__ float wt[16 * 128];  // W [k][j]
+    for (int e = threadIdx.x; e < 16 * ld; e += 256) {
+      const int k = e / ld, j = e - k * ld;
+      wt[e] = (k < kh && j < c) ? W[(long long)k * ldw + j] : 0.0f;
+    }
+    __syncthreads();
+    if (threadIdx.x < rows) {
+      float h[16];
+      const float *hr = H + (row0 + threadIdx.x) * (long long)ldh;
+#pragma unroll
+      for (int k = 0; k < 16; k++) h[k] = k < kh ? hr[k] : 0.0f;
+      float *lr = L + threadIdx.x * S;
+      for (int j = 0; j < ld; j++) {
+        float z = 0.0f;
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+#pragma unroll
+          for (int g = 0; g < 4; g++) z = fmaf(h[4 * g + t], wt[(4 * g + t) * ld + j], z);
+        lr[j] = z;
+      }
+    }
+  } else {
+    to_lds(logits);
+  }
   __syncthreads();
   float loss = 0.0f, wrong = 0.0f, se = 0.0f;
   const int t = threadIdx.x < rows ? truth[row0 + threadIdx.x] : -1;
@@ -317,7 +351,7 @@ __global__ __launch_bounds__(256) void k_xent_fwd(float *__restrict__ logits, in
     wrong = w ? 1.0f : 0.0f;
   }
   __syncthreads();
-  if (write_back) from_lds(logits);
+  if (write_back || FUSED) from_lds(logits);
   if (training) {
     __syncthreads();  // the shifted logits have left the tile
     if (threadIdx.x < rows) {
@@ -481,12 +515,29 @@ void launch_xent_fwd(float *logits, int ld, float *grad, const int *truth, int n
   const size_t lds = (size_t)XR * (ld + 1) * sizeof(float);  // <= 256*125*4 = 125 KB
   static bool attr = false;
   if (!attr) {
-    PGCN_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(k_xent_fwd),
+    PGCN_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(k_xent_fwd<false>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, 125 * 1024));
     attr = true;
   }
-  hipLaunchKernelGGL(k_xent_fwd, dim3(xent_blocks(n)), dim3(256), lds, s, logits, ld, grad,
-                     truth, n, c, count, training, partials, write_back);
+  hipLaunchKernelGGL(k_xent_fwd<false>, dim3(xent_blocks(n)), dim3(256), lds, s, logits, ld, grad,
+                     truth, n, c, count, training, partials, write_back, nullptr, 0, 0, nullptr, 0);
+}
+
+void launch_out_xent(const float *H, int ldh, int kh, const float *W, int ldw, float *logits,
+                     int ld, float *grad, const int *truth, int n, int c, int count, int training,
+                     float *partials, hipStream_t s) {
+  if (n <= 0) return;
+  PGCN_CHECK(ld <= 116 && c <= ld && ld % 4 == 0 && kh >= 1 && kh <= 16, PGCN_E_INVALID,
+             "out_xent: classes <= 116, hidden <= 16");
+  const size_t lds = (size_t)XR * (ld + 1) * sizeof(float);
+  static bool attr = false;
+  if (!attr) {
+    PGCN_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(k_xent_fwd<true>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, 117 * 1024));
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_xent_fwd<true>, dim3(xent_blocks(n)), dim3(256), lds, s, logits, ld, grad,
+                     truth, n, c, count, training, partials, 1, H, ldh, kh, W, ldw);
 }
 
 void launch_reduce_scalars(const float *partials, int n_blocks, const float *w, long long n_w,

@@ -170,6 +170,12 @@ void launch_dropout_apply_based(float *x, long long n, const uint64_t *mask, lon
 void launch_relu_fwd(float *x, long long n, uint8_t *mask, int training, hipStream_t s);
 void launch_relu_bwd(float *g, long long n, const uint8_t *mask, hipStream_t s);
 int xent_blocks(int n);
+// the output layer's product and the loss in one pass (k_xent_fwd<true>): logits = H W
+// (H [n][ldh], kh <= 16 columns; W [kh][ldw]) written max-shifted like launch_xent_fwd's
+// write_back, then its loss / grad / wrong count; bit-identical to launch_gemm_nn + xent
+void launch_out_xent(const float *H, int ldh, int kh, const float *W, int ldw, float *logits,
+                     int ld, float *grad, const int *truth, int n, int c, int count, int training,
+                     float *partials, hipStream_t s);
 void launch_xent_fwd(float *logits, int ld, float *grad, const int *truth, int n, int c,
                      int count, int training, float *partials, hipStream_t s, int write_back = 1);
 void launch_reduce_scalars(const float *partials, int n_blocks, const float *w, long long n_w,

@@ -448,6 +448,30 @@ def test_fused_epilogue_bit_identical(loaded, pgcn, case):
             np.testing.assert_array_equal(a, b)
 
 
+@pytest.mark.parametrize("case", ["cora_h4", "lds_dense"])
+def test_fused_output_layer_bit_identical(loaded, pgcn, case):
+    """The output layer's Matmul forward computed inside the loss kernel (launch_out_xent: an
+    fmaf chain in k_gemm_nn's MFMA order, then the same cross-entropy tile) gives the bits of
+    the separate Matmul + CrossEntropyLoss: epoch lines, weights, activations and gradients
+    (reassociated output layer: cora with hidden 4 < 7 classes; the LDS-path graph, 41
+    classes)."""
+    if case == "lds_dense":
+        ds, make = pgcn.Dataset.synthetic(120000, 64, 41, 1500000, 21), {}
+    else:
+        ds, make = loaded["cora"], {"hidden_dims": (4,)}
+    runs = {}
+    for fo in (1, 0):
+        with helpers.knobs(pgcn, fuse_output=fo):
+            g = pgcn.GCN(pgcn.make_params(ds, **make), ds)
+            lines = np.array([g.train_epoch() + g.eval(2) for _ in range(3)], np.float32)
+            g.train_epoch()
+            runs[fo] = (lines, [g.get_var(i) for i in (2, 3, 5)] + [g.get_var(i, 1) for i in (1, 3)])
+            g.close()
+    np.testing.assert_array_equal(runs[1][0], runs[0][0])
+    for a, b in zip(runs[1][1], runs[0][1]):
+        np.testing.assert_array_equal(a, b)
+
+
 def test_xstream_ring_engine_matches_register_kernels(pgcn):
     """The loader / MFMA-wave split of the first layer's X-stream products (k_xstream_lds.hip,
     default) against the register-streamed kernels in a whole run (dense 64-feature graph,
