@@ -519,6 +519,8 @@ void Matmul::forward(bool training, const Stream &s) const {
 
 void Matmul::backward(const Stream &s) const {
   const bool cmp = last_layer && ctx->compact_n;
+  const bool a_done = input_grad_done && !cmp;  // a.grad written by the loss kernel (forward)
+  input_grad_done = false;
   const Variable &A = cmp ? *ctx->compact_z : *a, &C = cmp ? *ctx->compact_out : *c;
   const int rows = cmp ? ctx->compact_n : m;
   const bool side = ctx->mm_side && ctx->side_stream && ctx->gemm_workspace_side && !ctx->profile;
@@ -533,8 +535,9 @@ void Matmul::backward(const Stream &s) const {
     ctx->side_pending = true;
   }
   // a.grad = c.grad * b^T   (b stored [n][p] => trans_b)
-  launch_gemm_nn(rows, n, p, C.dev_grad.get(), C.ld, b->dev_data.get(), b->ld, 1,
-                 A.dev_grad.get(), A.ld, nullptr, 0, 0, 1.0f, s.get());
+  if (!a_done)
+    launch_gemm_nn(rows, n, p, C.dev_grad.get(), C.ld, b->dev_data.get(), b->ld, 1,
+                   A.dev_grad.get(), A.ld, nullptr, 0, 0, 1.0f, s.get());
   // b.grad = a^T * c.grad (deterministic split-M reduction)
   if (!side)
     launch_gemm_tn(rows, p, n, A.dev_data.get(), A.ld, C.dev_grad.get(), C.ld, b->dev_grad.get(),
@@ -548,13 +551,18 @@ CrossEntropyLoss::CrossEntropyLoss(shared_ptr<Variable> logits_, int num_classes
                                    ModuleContext *ctx_)
     : logits(std::move(logits_)), num_classes(num_classes_), ctx(ctx_) {}
 
+// "fuse_output_bwd": the fused loss kernel also writes the output layer's input grad
+int g_fuse_output_bwd = 0;
+
 void CrossEntropyLoss::forward(bool training, const Stream &s) const {
   if (fused && !ctx->compact_n) {
     const Variable &Hv = *fused->input(), &Wv = *fused->weight();
+    float *dH = g_fuse_output_bwd && Hv.dev_grad ? Hv.dev_grad.get() : nullptr;
     launch_out_xent(Hv.dev_data.get(), Hv.ld, fused->inner(), Wv.dev_data.get(), Wv.ld,
                     logits->dev_data.get(), logits->ld, training ? logits->dev_grad.get() : nullptr,
                     ctx->truth, logits->rows, num_classes, ctx->count, training ? 1 : 0,
-                    ctx->xent_partials, s.get());
+                    ctx->xent_partials, s.get(), dH, Hv.ld);
+    fused->input_grad_done = training && dH;
     return;
   }
   const Variable &L = ctx->compact_n ? *ctx->compact_out : *logits;

@@ -291,6 +291,7 @@ class Matmul : public Module {
  public:
   bool last_layer = false;  // the output layer's Matmul (compact rows apply)
   bool fused_forward = false;  // its forward runs inside the loss's (CrossEntropyLoss::fused)
+  mutable bool input_grad_done = false;  // ... which also wrote a.grad (this training pass)
   Matmul(shared_ptr<Variable> a_, shared_ptr<Variable> b_, shared_ptr<Variable> c_, int m_,
          int n_, int p_, ModuleContext *ctx_);
   const Variable *input() const { return a.get(); }

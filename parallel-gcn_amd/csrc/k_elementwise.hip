@@ -262,7 +262,8 @@ __global__ __launch_bounds__(256) void k_xent_fwd(float *__restrict__ logits, in
                                                   int count, int training,
                                                   float *__restrict__ partials, int write_back,
                                                   const float *__restrict__ H, int ldh, int kh,
-                                                  const float *__restrict__ W, int ldw) {
+                                                  const float *__restrict__ W, int ldw,
+                                                  float *__restrict__ dH, int lddh) {
   // write_back 0: the shifted logits stay in LDS (the compact output layer's logits are read
   // by nobody after the loss; hpdga's in-place shift is kept where the variable is visible)
   extern __shared__ float smem[];
@@ -307,8 +308,8 @@ __global__ __launch_bounds__(256) void k_xent_fwd(float *__restrict__ logits, in
       reinterpret_cast<float4 *>(dst + base)[q] = make_float4(d[0], d[1], d[2], d[3]);
     }
   };
+  __shared__ float wt[FUSED ? 16 * 128 : 1];  // FUSED: W [k][j]
   if constexpr (FUSED) {
-    __shared__ float wt[16 * 128];  // W [k][j]
     for (int e = threadIdx.x; e < 16 * ld; e += 256) {
       const int k = e / ld, j = e - k * ld;
       wt[e] = (k < kh && j < c) ? W[(long long)k * ldw + j] : 0.0f;
@@ -364,6 +365,25 @@ __global__ __launch_bounds__(256) void k_xent_fwd(float *__restrict__ logits, in
         for (int j = c; j < ld; j++) l[j] = 0.0f;
       } else {
         for (int j = 0; j < ld; j++) l[j] = 0.0f;
+      }
+      if (FUSED && dH) {
+        // the output layer's input grad dH = grad W^T (Matmul::backward's a.grad), an fmaf
+        // chain over j in k_xstream_nn's order (step s, MFMA t, lane group g: j = 16 s + 4 g + t)
+        float *dr = dH + (row0 + threadIdx.x) * (long long)lddh;
+        for (int k = 0; k < lddh; k++) {
+          float z = 0.0f;
+          if (k < kh) {
+            for (int s0 = 0; s0 < c; s0 += 16)
+#pragma unroll
+              for (int tt = 0; tt < 4; tt++)
+#pragma unroll
+                for (int g = 0; g < 4; g++) {
+                  const int j = s0 + 4 * g + tt;
+                  if (j < c) z = fmaf(l[j], wt[k * ld + j], z);
+                }
+          }
+          dr[k] = z;
+        }
       }
     }
     __syncthreads();
@@ -520,12 +540,13 @@ void launch_xent_fwd(float *logits, int ld, float *grad, const int *truth, int n
     attr = true;
   }
   hipLaunchKernelGGL(k_xent_fwd<false>, dim3(xent_blocks(n)), dim3(256), lds, s, logits, ld, grad,
-                     truth, n, c, count, training, partials, write_back, nullptr, 0, 0, nullptr, 0);
+                     truth, n, c, count, training, partials, write_back, nullptr, 0, 0, nullptr, 0,
+                     nullptr, 0);
 }
 
 void launch_out_xent(const float *H, int ldh, int kh, const float *W, int ldw, float *logits,
                      int ld, float *grad, const int *truth, int n, int c, int count, int training,
-                     float *partials, hipStream_t s) {
+                     float *partials, hipStream_t s, float *dH, int lddh) {
   if (n <= 0) return;
   PGCN_CHECK(ld <= 116 && c <= ld && ld % 4 == 0 && kh >= 1 && kh <= 16, PGCN_E_INVALID,
              "out_xent: classes <= 116, hidden <= 16");
@@ -537,7 +558,8 @@ void launch_out_xent(const float *H, int ldh, int kh, const float *W, int ldw, f
     attr = true;
   }
   hipLaunchKernelGGL(k_xent_fwd<true>, dim3(xent_blocks(n)), dim3(256), lds, s, logits, ld, grad,
-                     truth, n, c, count, training, partials, 1, H, ldh, kh, W, ldw);
+                     truth, n, c, count, training, partials, 1, H, ldh, kh, W, ldw,
+                     training ? dH : nullptr, lddh);
 }
 
 void launch_reduce_scalars(const float *partials, int n_blocks, const float *w, long long n_w,

@@ -172,10 +172,12 @@ void launch_relu_bwd(float *g, long long n, const uint8_t *mask, hipStream_t s);
 int xent_blocks(int n);
 // the output layer's product and the loss in one pass (k_xent_fwd<true>): logits = H W
 // (H [n][ldh], kh <= 16 columns; W [kh][ldw]) written max-shifted like launch_xent_fwd's
-// write_back, then its loss / grad / wrong count; bit-identical to launch_gemm_nn + xent
+// write_back, then its loss / grad / wrong count; bit-identical to launch_gemm_nn + xent.
+// Training with dH: also dH [n][lddh] = grad W^T (columns >= kh zero), bit-identical to the
+// Matmul backward's launch_gemm_nn(trans_b)
 void launch_out_xent(const float *H, int ldh, int kh, const float *W, int ldw, float *logits,
                      int ld, float *grad, const int *truth, int n, int c, int count, int training,
-                     float *partials, hipStream_t s);
+                     float *partials, hipStream_t s, float *dH = nullptr, int lddh = 0);
 void launch_xent_fwd(float *logits, int ld, float *grad, const int *truth, int n, int c,
                      int count, int training, float *partials, hipStream_t s, int write_back = 1);
 void launch_reduce_scalars(const float *partials, int n_blocks, const float *w, long long n_w,
