@@ -65,8 +65,14 @@ class DeviceBuffer {
   void zero_async(hipStream_t s) const {
     if (size()) PGCN_HIP(hipMemsetAsync(get(), 0, size() * sizeof(T), s));
   }
+  // Complete on return: the engine's streams are non-blocking, so a memset left pending on the
+  // null stream is not ordered before their later kernels (a lazily allocated buffer -- the
+  // next input mask, the train-ahead product -- could be zeroed after a kernel wrote it)
   void zero() const {
-    if (size()) PGCN_HIP(hipMemset(get(), 0, size() * sizeof(T)));
+    if (size()) {
+      PGCN_HIP(hipMemsetAsync(get(), 0, size() * sizeof(T), nullptr));
+      PGCN_HIP(hipStreamSynchronize(nullptr));
+    }
   }
 };
 
