@@ -247,12 +247,11 @@ __device__ __forceinline__ float block_sum(float v, float *smem) {
 // partials[2*block].
 // ------------------------------------------------------------------------------------------
 constexpr int XR = 256;  // rows per cross-entropy block (= threads)
+typedef float floatx4e __attribute__((ext_vector_type(4)));
 
 // FUSED: the logits are computed here from the output layer's input H [n][ldh] (kh <= 16
-// columns) and W [kh][ldw] -- each thread its row, z[j] = an fmaf chain over k in the order of
-// k_gemm_nn's v_mfma_f32_16x16x4_f32 sequence (MFMA t sums k = t, 4 + t, 8 + t, 12 + t as a
-// k-ordered fma chain), so the same bits as the separate Matmul -- and then go through the
-// same tile as the loaded ones (the output layer's Matmul forward + CrossEntropyLoss forward,
+// columns) and W [kh][ldw] with k_gemm_nn's v_mfma_f32_16x16x4_f32 sequence, so the same bits
+// as the separate Matmul -- and then go through the same tile as the loaded ones (the output layer's Matmul forward + CrossEntropyLoss forward,
 // hpdga module.cpp:13-38, :122-153, in one pass: the logits are written once, not written
 // and read back).
 template <bool FUSED>
@@ -315,19 +314,29 @@ __global__ __launch_bounds__(256) void k_xent_fwd(float *__restrict__ logits, in
       wt[e] = (k < kh && j < c) ? W[(long long)k * ldw + j] : 0.0f;
     }
     __syncthreads();
-    if (threadIdx.x < rows) {
-      float h[16];
-      const float *hr = H + (row0 + threadIdx.x) * (long long)ldh;
+    // logits of the block's 256 rows on MFMA, as k_gemm_nn<3> computes them: wave w takes rows
+    // 64 w .. 64 w + 63 in groups of 16; lane (i, g) feeds MFMA t with H[row i][4 g + t] and
+    // W[4 g + t][16 tt + i]; lane holds logits[4 g + r][16 tt + i] -> the tile
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63, gi = ln >> 4, ii = ln & 15;
 #pragma unroll
-      for (int k = 0; k < 16; k++) h[k] = k < kh ? hr[k] : 0.0f;
-      float *lr = L + threadIdx.x * S;
-      for (int j = 0; j < ld; j++) {
-        float z = 0.0f;
+    for (int q = 0; q < 4; q++) {
+      long long grow = row0 + wv * 64 + q * 16 + ii;
+      grow = grow < n ? grow : n - 1;
+      const float *hr = H + grow * (long long)ldh;
+      float a[4];
 #pragma unroll
-        for (int t = 0; t < 4; t++)
+      for (int t4 = 0; t4 < 4; t4++) a[t4] = 4 * gi + t4 < kh ? hr[4 * gi + t4] : 0.0f;
+      for (int tt = 0; 16 * tt < ld; tt++) {
+        const int col = 16 * tt + ii;
+        floatx4e acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int g = 0; g < 4; g++) z = fmaf(h[4 * g + t], wt[(4 * g + t) * ld + j], z);
-        lr[j] = z;
+        for (int t4 = 0; t4 < 4; t4++)
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(
+              a[t4], col < ld ? wt[(4 * gi + t4) * ld + col] : 0.0f, acc, 0, 0, 0);
+        if (col < ld) {
+#pragma unroll
+          for (int r = 0; r < 4; r++) L[(wv * 64 + q * 16 + 4 * gi + r) * S + col] = acc[r];
+        }
       }
     }
   } else {
