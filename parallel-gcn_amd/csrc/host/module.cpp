@@ -551,10 +551,9 @@ CrossEntropyLoss::CrossEntropyLoss(shared_ptr<Variable> logits_, int num_classes
                                    ModuleContext *ctx_)
     : logits(std::move(logits_)), num_classes(num_classes_), ctx(ctx_) {}
 
-// "fuse_output_bwd": the fused loss kernel also writes the output layer's input grad (bit-
-// identical; measured slower on reddit, 507.8 vs 517.3 epochs/s: the per-row chain of 16 x 41
-// LDS-fed fmas costs more than the separate 16 us product)
-int g_fuse_output_bwd = 0;
+// "fuse_output_bwd": the fused loss kernel also writes the output layer's input grad (on MFMA
+// in k_xstream_nn's sequence: bit-identical; reddit A/B 517.7 -> 520.1 epochs/s)
+int g_fuse_output_bwd = 1;
 
 void CrossEntropyLoss::forward(bool training, const Stream &s) const {
   if (fused && !ctx->compact_n) {

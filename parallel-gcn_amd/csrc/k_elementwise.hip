@@ -375,23 +375,32 @@ __global__ __launch_bounds__(256) void k_xent_fwd(float *__restrict__ logits, in
       } else {
         for (int j = 0; j < ld; j++) l[j] = 0.0f;
       }
-      if (FUSED && dH) {
-        // the output layer's input grad dH = grad W^T (Matmul::backward's a.grad), an fmaf
-        // chain over j in k_xstream_nn's order (step s, MFMA t, lane group g: j = 16 s + 4 g + t)
-        float *dr = dH + (row0 + threadIdx.x) * (long long)lddh;
-        for (int k = 0; k < lddh; k++) {
-          float z = 0.0f;
-          if (k < kh) {
-            for (int s0 = 0; s0 < c; s0 += 16)
+    }
+    if (FUSED && dH) {
+      // the output layer's input grad dH = grad W^T (Matmul::backward's a.grad) on MFMA in
+      // k_xstream_nn's sequence (N = 16 outputs, K = c classes: step s, MFMA t, lane group g:
+      // class 16 s + 4 g + t), from the grad tile
+      __syncthreads();
+      const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63, gi = ln >> 4, ii = ln & 15;
 #pragma unroll
-              for (int tt = 0; tt < 4; tt++)
+      for (int q = 0; q < 4; q++) {
+        const int rl = wv * 64 + q * 16;  // local rows rl .. rl + 15
+        floatx4e acc = {0.f, 0.f, 0.f, 0.f};
+        for (int s0 = 0; s0 < c; s0 += 16) {
 #pragma unroll
-                for (int g = 0; g < 4; g++) {
-                  const int j = s0 + 4 * g + tt;
-                  if (j < c) z = fmaf(l[j], wt[k * ld + j], z);
-                }
+          for (int t4 = 0; t4 < 4; t4++) {
+            const int j = s0 + 4 * gi + t4;
+            const float av = j < c ? L[(rl + ii) * S + j] : 0.0f;
+            const float bv = (j < c && ii < kh) ? wt[ii * ld + j] : 0.0f;
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
           }
-          dr[k] = z;
+        }
+        if (ii < lddh) {
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            const int rr = rl + 4 * gi + r;
+            if (rr < rows) dH[(row0 + rr) * (long long)lddh + ii] = acc[r];
+          }
         }
       }
     }

@@ -460,7 +460,7 @@ def test_fused_output_layer_bit_identical(loaded, pgcn, case):
     else:
         ds, make = loaded["cora"], {"hidden_dims": (4,)}
     runs = {}
-    for fo in (1, 0):
+    for fo in (1, 0):  # 1: the logits and (fuse_output_bwd, default) the input grad fused
         with helpers.knobs(pgcn, fuse_output=fo):
             g = pgcn.GCN(pgcn.make_params(ds, **make), ds)
             lines = np.array([g.train_epoch() + g.eval(2) for _ in range(3)], np.float32)
