@@ -348,7 +348,9 @@ __global__ __launch_bounds__(256) void k_xent_fwd(float *__restrict__ logits, in
   float *l = L + threadIdx.x * S;
   if (t >= 0) {
     float mx = -1e30f;
+#pragma unroll 4
     for (int j = 0; j < c; j++) mx = fmaxf(mx, l[j]);
+#pragma unroll 4
     for (int j = 0; j < c; j++) {
       const float v = l[j] - mx;
       l[j] = v;
@@ -357,6 +359,7 @@ __global__ __launch_bounds__(256) void k_xent_fwd(float *__restrict__ logits, in
     const float lt = l[t];
     loss = logf(se) - lt;
     bool w = false;
+#pragma unroll 4
     for (int j = 0; j < c; j++) w |= l[j] > lt;
     wrong = w ? 1.0f : 0.0f;
   }
@@ -366,6 +369,7 @@ __global__ __launch_bounds__(256) void k_xent_fwd(float *__restrict__ logits, in
     __syncthreads();  // the shifted logits have left the tile
     if (threadIdx.x < rows) {
       if (t >= 0) {
+#pragma unroll 4
         for (int j = 0; j < c; j++) {
           float prob = expf(l[j]) / se;
           if (j == t) prob = (float)((double)prob - 1.0);  // hpdga module.cpp:145 (double temp)
