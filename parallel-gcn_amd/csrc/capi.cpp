@@ -36,6 +36,7 @@ extern int g_xstream_ring_slots;    // k_xstream_lds.hip
 extern int g_xstream_tn_split;      // k_xstream_lds.hip
 extern int g_fuse_output;           // host/gcn.cpp
 extern int g_fuse_output_bwd;       // host/module.cpp
+extern int g_fuse_output_wgrad;     // host/module.cpp
 extern int g_xstream_nn_balance;    // k_gemm.hip
 extern int g_eval_ax;               // host/gcn.cpp
 extern int g_epoch_graph;           // host/gcn.cpp
@@ -634,6 +635,7 @@ int pgcn_debug_set(const char *key, int value) {
   else if (!std::strcmp(key, "xstream_tn_split")) pgcn::g_xstream_tn_split = value;
   else if (!std::strcmp(key, "fuse_output")) pgcn::g_fuse_output = value;
   else if (!std::strcmp(key, "fuse_output_bwd")) pgcn::g_fuse_output_bwd = value;
+  else if (!std::strcmp(key, "fuse_output_wgrad")) pgcn::g_fuse_output_wgrad = value;
   else if (!std::strcmp(key, "xstream_nn_balance")) pgcn::g_xstream_nn_balance = value;
   else if (!std::strcmp(key, "eval_ax")) pgcn::g_eval_ax = value;
   else if (!std::strcmp(key, "epoch_graph")) pgcn::g_epoch_graph = value;

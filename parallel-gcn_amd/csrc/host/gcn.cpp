@@ -468,6 +468,7 @@ void GCN::build(const GCNData &data) {
   ctx.xent_partials = xent_partials.get();
   ctx.xent_blocks = xent_blocks(prow);
   ctx.gemm_workspace = gemm_ws.get();
+  ctx.gemm_workspace_bytes = gemm_ws.size() * sizeof(float);
   ctx.gs_events = &gs_events;
   ctx.gs_bytes = &gs_bytes;
   ctx.mm_events = &mm_events;

@@ -520,7 +520,8 @@ void Matmul::forward(bool training, const Stream &s) const {
 void Matmul::backward(const Stream &s) const {
   const bool cmp = last_layer && ctx->compact_n;
   const bool a_done = input_grad_done && !cmp;  // a.grad written by the loss kernel (forward)
-  input_grad_done = false;
+  const bool b_done = weight_grad_done && !cmp;  // b.grad too
+  input_grad_done = weight_grad_done = false;
   const Variable &A = cmp ? *ctx->compact_z : *a, &C = cmp ? *ctx->compact_out : *c;
   const int rows = cmp ? ctx->compact_n : m;
   const bool side = ctx->mm_side && ctx->side_stream && ctx->gemm_workspace_side && !ctx->profile;
@@ -539,7 +540,7 @@ void Matmul::backward(const Stream &s) const {
     launch_gemm_nn(rows, n, p, C.dev_grad.get(), C.ld, b->dev_data.get(), b->ld, 1,
                    A.dev_grad.get(), A.ld, nullptr, 0, 0, 1.0f, s.get());
   // b.grad = a^T * c.grad (deterministic split-M reduction)
-  if (!side)
+  if (!side && !b_done)
     launch_gemm_tn(rows, p, n, A.dev_data.get(), A.ld, C.dev_grad.get(), C.ld, b->dev_grad.get(),
                    b->ld, nullptr, 0, 0, 1.0f, ctx->gemm_workspace, s.get());
 }
@@ -554,16 +555,34 @@ CrossEntropyLoss::CrossEntropyLoss(shared_ptr<Variable> logits_, int num_classes
 // "fuse_output_bwd": the fused loss kernel also writes the output layer's input grad (on MFMA
 // in k_xstream_nn's sequence: bit-identical; reddit A/B 517.7 -> 520.1 epochs/s)
 int g_fuse_output_bwd = 1;
+// "fuse_output_wgrad": ... and per-block partials of the Matmul's weight grad, reduced in block
+// order right after it (deterministic; the same sums as k_gemm_tn's in another grouping): 1 on
+// graphs of >= 65,536 rows (small graphs keep k_gemm_tn's order: nothing to gain there), 2 on
+// any graph; hidden width 16 only (a narrower one -- cora at hidden 4 -- gave a W2.grad off in
+// its last rows in the r02 check, not yet understood, so it keeps k_gemm_tn)
+int g_fuse_output_wgrad = 1;
 
 void CrossEntropyLoss::forward(bool training, const Stream &s) const {
   if (fused && !ctx->compact_n) {
     const Variable &Hv = *fused->input(), &Wv = *fused->weight();
     float *dH = g_fuse_output_bwd && Hv.dev_grad ? Hv.dev_grad.get() : nullptr;
+    const int nb = xent_blocks(logits->rows);
+    float *dWp = nullptr;
+    if (training && g_fuse_output_wgrad &&
+        (g_fuse_output_wgrad == 2 || logits->rows >= 65536) && fused->inner() == 16 &&
+        Wv.dev_grad && logits->ld <= 48 &&
+        !ctx->mm_side &&
+        tn_reduce_blocks_workspace(nb, fused->inner(), 48) <= ctx->gemm_workspace_bytes)
+      dWp = static_cast<float *>(ctx->gemm_workspace);
     launch_out_xent(Hv.dev_data.get(), Hv.ld, fused->inner(), Wv.dev_data.get(), Wv.ld,
                     logits->dev_data.get(), logits->ld, training ? logits->dev_grad.get() : nullptr,
                     ctx->truth, logits->rows, num_classes, ctx->count, training ? 1 : 0,
-                    ctx->xent_partials, s.get(), dH, Hv.ld);
+                    ctx->xent_partials, s.get(), dH, Hv.ld, dWp);
+    if (dWp)
+      launch_tn_reduce_blocks(dWp, nb, fused->inner(), num_classes, 48, Wv.dev_grad.get(), Wv.ld,
+                              s.get());
     fused->input_grad_done = training && dH;
+    fused->weight_grad_done = dWp != nullptr;
     return;
   }
   const Variable &L = ctx->compact_n ? *ctx->compact_out : *logits;

@@ -136,6 +136,7 @@ struct ModuleContext {
   std::vector<DevGraph *> chunk_col_graphs;
   const void *jump_table = nullptr;  // M^period byte tables (device)
   void *gemm_workspace = nullptr;
+  size_t gemm_workspace_bytes = 0;
   // profiling of GraphSum calls
   bool profile = false;
   std::vector<std::pair<Event, Event>> *gs_events = nullptr;
@@ -292,6 +293,7 @@ class Matmul : public Module {
   bool last_layer = false;  // the output layer's Matmul (compact rows apply)
   bool fused_forward = false;  // its forward runs inside the loss's (CrossEntropyLoss::fused)
   mutable bool input_grad_done = false;  // ... which also wrote a.grad (this training pass)
+  mutable bool weight_grad_done = false;  // ... and b.grad
   Matmul(shared_ptr<Variable> a_, shared_ptr<Variable> b_, shared_ptr<Variable> c_, int m_,
          int n_, int p_, ModuleContext *ctx_);
   const Variable *input() const { return a.get(); }

@@ -262,7 +262,8 @@ __global__ __launch_bounds__(256) void k_xent_fwd(float *__restrict__ logits, in
                                                   float *__restrict__ partials, int write_back,
                                                   const float *__restrict__ H, int ldh, int kh,
                                                   const float *__restrict__ W, int ldw,
-                                                  float *__restrict__ dH, int lddh) {
+                                                  float *__restrict__ dH, int lddh,
+                                                  float *__restrict__ dWp) {
   // write_back 0: the shifted logits stay in LDS (the compact output layer's logits are read
   // by nobody after the loss; hpdga's in-place shift is kept where the variable is visible)
   extern __shared__ float smem[];
@@ -408,8 +409,49 @@ __global__ __launch_bounds__(256) void k_xent_fwd(float *__restrict__ logits, in
         }
       }
     }
+    // the output layer's weight grad, this block's share: partial [kh][48] = H^T grad
+    // over the block's rows (wave partials on MFMA, added in wave order), reduced over the
+    // blocks in block order by launch_tn_reduce_blocks
+    floatx4e pw[3] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    if (FUSED && dWp) {
+      if (!dH) __syncthreads();  // the grad tile is complete
+      const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63, gi = ln >> 4, ii = ln & 15;
+      for (int st = 0; st < 16; st++) {  // 4-row steps over the wave's 64 rows
+        const int rloc = wv * 64 + 4 * st + gi;
+        const bool ok = rloc < rows;
+        const float av = (ok && ii < kh) ? H[(row0 + rloc) * (long long)ldh + ii] : 0.0f;
+#pragma unroll
+        for (int tt = 0; tt < 3; tt++) {
+          const int col = 16 * tt + ii;
+          const float bv = (ok && col < ld) ? L[rloc * S + col] : 0.0f;
+          pw[tt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, pw[tt], 0, 0, 0);
+        }
+      }
+    }
     __syncthreads();
     from_lds(grad);
+    if (FUSED && dWp) {
+      __syncthreads();  // the tile is free: wave partials through it
+      const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63, gi = ln >> 4, ii = ln & 15;
+      float *rw = L + wv * (3 * 4 * 64);
+#pragma unroll
+      for (int tt = 0; tt < 3; tt++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) rw[(tt * 4 + r) * 64 + ln] = pw[tt][r];
+      __syncthreads();
+      if (wv == 0) {
+        float *pb = dWp + (long long)blockIdx.x * kh * 48;  // [kh][48] per block
+#pragma unroll
+        for (int tt = 0; tt < 3; tt++)
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            float v = pw[tt][r];
+#pragma unroll
+            for (int w2 = 1; w2 < 4; w2++) v += L[w2 * (3 * 4 * 64) + (tt * 4 + r) * 64 + ln];
+            if (4 * gi + r < kh) pb[(4 * gi + r) * 48 + 16 * tt + ii] = v;
+          }
+      }
+    }
   }
   const float ls = block_sum<256>(loss, red);
   const float ws = block_sum<256>(wrong, red);
@@ -563,15 +605,16 @@ void launch_xent_fwd(float *logits, int ld, float *grad, const int *truth, int n
   }
   hipLaunchKernelGGL(k_xent_fwd<false>, dim3(xent_blocks(n)), dim3(256), lds, s, logits, ld, grad,
                      truth, n, c, count, training, partials, write_back, nullptr, 0, 0, nullptr, 0,
-                     nullptr, 0);
+                     nullptr, 0, nullptr);
 }
 
 void launch_out_xent(const float *H, int ldh, int kh, const float *W, int ldw, float *logits,
                      int ld, float *grad, const int *truth, int n, int c, int count, int training,
-                     float *partials, hipStream_t s, float *dH, int lddh) {
+                     float *partials, hipStream_t s, float *dH, int lddh, float *dWp) {
   if (n <= 0) return;
   PGCN_CHECK(ld <= 116 && c <= ld && ld % 4 == 0 && kh >= 1 && kh <= 16, PGCN_E_INVALID,
              "out_xent: classes <= 116, hidden <= 16");
+  PGCN_CHECK(!dWp || ld <= 48, PGCN_E_INVALID, "out_xent: the weight-grad partial needs <= 48 classes");
   const size_t lds = (size_t)XR * (ld + 1) * sizeof(float);
   static bool attr = false;
   if (!attr) {
@@ -581,7 +624,7 @@ void launch_out_xent(const float *H, int ldh, int kh, const float *W, int ldw, f
   }
   hipLaunchKernelGGL(k_xent_fwd<true>, dim3(xent_blocks(n)), dim3(256), lds, s, logits, ld, grad,
                      truth, n, c, count, training, partials, 1, H, ldh, kh, W, ldw,
-                     training ? dH : nullptr, lddh);
+                     training ? dH : nullptr, lddh, training ? dWp : nullptr);
 }
 
 void launch_reduce_scalars(const float *partials, int n_blocks, const float *w, long long n_w,

@@ -908,6 +908,24 @@ static void tn_reduce(const TnPlan &p, int M, int N, int K, float *partial, floa
                      part2, M > 0 ? p.n_groups : 0, K, N, p.ldp, C, ldc, nst);
 }
 
+static TnPlan blocks_plan(int n_blocks, int ldp) {
+  TnPlan p{};
+  p.n_slabs = n_blocks;
+  p.ldp = ldp;
+  p.spg = 16;
+  p.n_groups = (n_blocks + p.spg - 1) / p.spg;
+  return p;
+}
+
+size_t tn_reduce_blocks_workspace(int n_blocks, int K, int ldp) {
+  return plan_bytes(blocks_plan(n_blocks, ldp), K);
+}
+
+void launch_tn_reduce_blocks(float *partial, int n_blocks, int K, int N, int ldp, float *C, int ldc,
+                             hipStream_t s) {
+  tn_reduce(blocks_plan(n_blocks, ldp), n_blocks, N, K, partial, C, ldc, s);
+}
+
 void launch_xstream_tn(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
                        float *C, int ldc, const uint64_t *maskT, float a_scale, void *workspace,
                        hipStream_t s) {

@@ -177,7 +177,13 @@ int xent_blocks(int n);
 // Matmul backward's launch_gemm_nn(trans_b)
 void launch_out_xent(const float *H, int ldh, int kh, const float *W, int ldw, float *logits,
                      int ld, float *grad, const int *truth, int n, int c, int count, int training,
-                     float *partials, hipStream_t s, float *dH = nullptr, int lddh = 0);
+                     float *partials, hipStream_t s, float *dH = nullptr, int lddh = 0,
+                     float *dWp = nullptr);
+// with dWp (training, <= 48 classes): per-block partials [xent_blocks(n)][kh][48] of W.grad =
+// H^T grad, reduced in block order into C [kh][ldc] (N = c columns) by:
+void launch_tn_reduce_blocks(float *partial, int n_blocks, int K, int N, int ldp, float *C, int ldc,
+                             hipStream_t s);
+size_t tn_reduce_blocks_workspace(int n_blocks, int K, int ldp);
 void launch_xent_fwd(float *logits, int ld, float *grad, const int *truth, int n, int c,
                      int count, int training, float *partials, hipStream_t s, int write_back = 1);
 void launch_reduce_scalars(const float *partials, int n_blocks, const float *w, long long n_w,

@@ -197,7 +197,7 @@ def parse_line(line):
 ENGINE_DEFAULTS = {"train_ahead": 1, "split_rows": 0, "split_cols": 1, "eval_ax": 1,
                    "epoch_graph": 0, "mask_side": 0, "fuse_epilogue": 1,
                    "graphsum_ring_fused": 0, "graphsum_prestage": 1, "xstream_epilogue": 1,
-                   "xstream_ring": 1, "xstream_ring_inflight": 1, "xstream_tn_split": 0, "fuse_output": 1, "fuse_output_bwd": 1,
+                   "xstream_ring": 1, "xstream_ring_inflight": 1, "xstream_tn_split": 0, "fuse_output": 1, "fuse_output_bwd": 1, "fuse_output_wgrad": 1,
                    "mm_side": 0, "graphsum_ring_wide": 0,
                    "lds_min_kb": -1, "blocked_min_kb": -1}
 
