@@ -558,8 +558,7 @@ int g_fuse_output_bwd = 1;
 // "fuse_output_wgrad": ... and per-block partials of the Matmul's weight grad, reduced in block
 // order right after it (deterministic; the same sums as k_gemm_tn's in another grouping): 1 on
 // graphs of >= 65,536 rows (small graphs keep k_gemm_tn's order: nothing to gain there), 2 on
-// any graph; hidden width 16 only (a narrower one -- cora at hidden 4 -- gave a W2.grad off in
-// its last rows in the r02 check, not yet understood, so it keeps k_gemm_tn)
+// any graph
 int g_fuse_output_wgrad = 1;
 
 void CrossEntropyLoss::forward(bool training, const Stream &s) const {
@@ -569,8 +568,7 @@ void CrossEntropyLoss::forward(bool training, const Stream &s) const {
     const int nb = xent_blocks(logits->rows);
     float *dWp = nullptr;
     if (training && g_fuse_output_wgrad &&
-        (g_fuse_output_wgrad == 2 || logits->rows >= 65536) && fused->inner() == 16 &&
-        Wv.dev_grad && logits->ld <= 48 &&
+        (g_fuse_output_wgrad == 2 || logits->rows >= 65536) && Wv.dev_grad && logits->ld <= 48 &&
         !ctx->mm_side &&
         tn_reduce_blocks_workspace(nb, fused->inner(), 48) <= ctx->gemm_workspace_bytes)
       dWp = static_cast<float *>(ctx->gemm_workspace);

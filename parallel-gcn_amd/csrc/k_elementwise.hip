@@ -246,7 +246,7 @@ __device__ __forceinline__ float block_sum(float v, float *smem) {
 // grad computed in place and copied out.  Per-block partial sums (loss, wrong) go to
 // partials[2*block].
 // ------------------------------------------------------------------------------------------
-constexpr int XR = 256;  // rows per cross-entropy block (= threads)
+constexpr int XR = 256;  // rows per cross-entropy block (= threads; 128 measured slower, r02)
 typedef float floatx4e __attribute__((ext_vector_type(4)));
 
 // FUSED: the logits are computed here from the output layer's input H [n][ldh] (kh <= 16
@@ -255,7 +255,7 @@ typedef float floatx4e __attribute__((ext_vector_type(4)));
 // hpdga module.cpp:13-38, :122-153, in one pass: the logits are written once, not written
 // and read back).
 template <bool FUSED>
-__global__ __launch_bounds__(256) void k_xent_fwd(float *__restrict__ logits, int ld,
+__global__ __launch_bounds__(XR) void k_xent_fwd(float *__restrict__ logits, int ld,
                                                   float *__restrict__ grad,
                                                   const int *__restrict__ truth, int n, int c,
                                                   int count, int training,
@@ -267,7 +267,7 @@ __global__ __launch_bounds__(256) void k_xent_fwd(float *__restrict__ logits, in
   // write_back 0: the shifted logits stay in LDS (the compact output layer's logits are read
   // by nobody after the loss; hpdga's in-place shift is kept where the variable is visible)
   extern __shared__ float smem[];
-  __shared__ float red[4];
+  __shared__ float red[XR / 64];
   const int S = ld + 1;
   float *L = smem;  // [XR][S]
   const long long row0 = (long long)blockIdx.x * XR;
@@ -280,16 +280,16 @@ __global__ __launch_bounds__(256) void k_xent_fwd(float *__restrict__ logits, in
   const int ld4 = ld >> 2, tile4 = tile >> 2;
   constexpr int XU = 8;
   auto to_lds = [&](const float *src) {
-    for (int q0 = threadIdx.x; q0 < tile4; q0 += 256 * XU) {
+    for (int q0 = threadIdx.x; q0 < tile4; q0 += XR * XU) {
       float4 v[XU];
 #pragma unroll
       for (int u = 0; u < XU; u++) {
-        const int q = q0 + 256 * u;
+        const int q = q0 + XR * u;
         if (q < tile4) v[u] = reinterpret_cast<const float4 *>(src + base)[q];
       }
 #pragma unroll
       for (int u = 0; u < XU; u++) {
-        const int q = q0 + 256 * u;
+        const int q = q0 + XR * u;
         if (q < tile4) {
           const int r = q / ld4, j = 4 * (q - r * ld4);
           float *d = L + r * S + j;
@@ -302,7 +302,7 @@ __global__ __launch_bounds__(256) void k_xent_fwd(float *__restrict__ logits, in
     }
   };
   auto from_lds = [&](float *dst) {
-    for (int q = threadIdx.x; q < tile4; q += 256) {
+    for (int q = threadIdx.x; q < tile4; q += XR) {
       const int r = q / ld4, j = 4 * (q - r * ld4);
       const float *d = L + r * S + j;
       reinterpret_cast<float4 *>(dst + base)[q] = make_float4(d[0], d[1], d[2], d[3]);
@@ -310,12 +310,12 @@ __global__ __launch_bounds__(256) void k_xent_fwd(float *__restrict__ logits, in
   };
   __shared__ float wt[FUSED ? 16 * 128 : 1];  // FUSED: W [k][j]
   if constexpr (FUSED) {
-    for (int e = threadIdx.x; e < 16 * ld; e += 256) {
+    for (int e = threadIdx.x; e < 16 * ld; e += XR) {
       const int k = e / ld, j = e - k * ld;
       wt[e] = (k < kh && j < c) ? W[(long long)k * ldw + j] : 0.0f;
     }
     __syncthreads();
-    // logits of the block's 256 rows on MFMA, as k_gemm_nn<3> computes them: wave w takes rows
+    // logits of the block's XR rows on MFMA, as k_gemm_nn<3> computes them: wave w takes rows
     // 64 w .. 64 w + 63 in groups of 16; lane (i, g) feeds MFMA t with H[row i][4 g + t] and
     // W[4 g + t][16 tt + i]; lane holds logits[4 g + r][16 tt + i] -> the tile
     const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63, gi = ln >> 4, ii = ln & 15;
@@ -447,14 +447,14 @@ __global__ __launch_bounds__(256) void k_xent_fwd(float *__restrict__ logits, in
           for (int r = 0; r < 4; r++) {
             float v = pw[tt][r];
 #pragma unroll
-            for (int w2 = 1; w2 < 4; w2++) v += L[w2 * (3 * 4 * 64) + (tt * 4 + r) * 64 + ln];
+            for (int w2 = 1; w2 < XR / 64; w2++) v += L[w2 * (3 * 4 * 64) + (tt * 4 + r) * 64 + ln];
             if (4 * gi + r < kh) pb[(4 * gi + r) * 48 + 16 * tt + ii] = v;
           }
       }
     }
   }
-  const float ls = block_sum<256>(loss, red);
-  const float ws = block_sum<256>(wrong, red);
+  const float ls = block_sum<XR>(loss, red);
+  const float ws = block_sum<XR>(wrong, red);
   if (threadIdx.x == 0) {
     partials[2 * blockIdx.x] = ls;
     partials[2 * blockIdx.x + 1] = ws;
@@ -603,7 +603,7 @@ void launch_xent_fwd(float *logits, int ld, float *grad, const int *truth, int n
                                  hipFuncAttributeMaxDynamicSharedMemorySize, 125 * 1024));
     attr = true;
   }
-  hipLaunchKernelGGL(k_xent_fwd<false>, dim3(xent_blocks(n)), dim3(256), lds, s, logits, ld, grad,
+  hipLaunchKernelGGL(k_xent_fwd<false>, dim3(xent_blocks(n)), dim3(XR), lds, s, logits, ld, grad,
                      truth, n, c, count, training, partials, write_back, nullptr, 0, 0, nullptr, 0,
                      nullptr, 0, nullptr);
 }
@@ -615,14 +615,16 @@ void launch_out_xent(const float *H, int ldh, int kh, const float *W, int ldw, f
   PGCN_CHECK(ld <= 116 && c <= ld && ld % 4 == 0 && kh >= 1 && kh <= 16, PGCN_E_INVALID,
              "out_xent: classes <= 116, hidden <= 16");
   PGCN_CHECK(!dWp || ld <= 48, PGCN_E_INVALID, "out_xent: the weight-grad partial needs <= 48 classes");
-  const size_t lds = (size_t)XR * (ld + 1) * sizeof(float);
+  // the tile, and (weight-grad partials) room for the waves' [3][4][64] partials in it
+  const size_t tile = (size_t)XR * (ld + 1), wparts = (size_t)(XR / 64) * 3 * 4 * 64;
+  const size_t lds = (training && dWp && wparts > tile ? wparts : tile) * sizeof(float);
   static bool attr = false;
   if (!attr) {
     PGCN_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(k_xent_fwd<true>),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, 117 * 1024));
     attr = true;
   }
-  hipLaunchKernelGGL(k_xent_fwd<true>, dim3(xent_blocks(n)), dim3(256), lds, s, logits, ld, grad,
+  hipLaunchKernelGGL(k_xent_fwd<true>, dim3(xent_blocks(n)), dim3(XR), lds, s, logits, ld, grad,
                      truth, n, c, count, training, partials, 1, H, ldh, kh, W, ldw,
                      training ? dH : nullptr, lddh, training ? dWp : nullptr);
 }

@@ -477,9 +477,8 @@ def test_fused_output_weight_grad_close(loaded, pgcn, case):
     """The loss kernel's per-block partials of W2.grad, reduced in block order
     (fuse_output_wgrad): the same sums as k_gemm_tn's in another grouping -- W2.grad of the
     first step within 2e-6 relative of the k_gemm_tn one, and the epoch lines after it within
-    float rounding (LDS-path graph, 41 classes, hidden 16). The fusion takes hidden 16 only:
-    cora at hidden 4 (output layer reassociated, fused loss kernel) keeps k_gemm_tn even
-    when forced, so its runs are bit-identical."""
+    float rounding (LDS-path graph, 41 classes, hidden 16; cora at hidden 4, 7 classes: a
+    grad tile narrower than the waves' partials, which the launch then sizes the LDS for)."""
     if case == "lds_dense":
         ds, make = pgcn.Dataset.synthetic(120000, 64, 41, 1500000, 21), {}
     else:
@@ -494,10 +493,6 @@ def test_fused_output_weight_grad_close(loaded, pgcn, case):
             runs[wg] = (np.array(lines[0]), np.array(lines[1:], np.float64), w2g)
             g.close()
     np.testing.assert_array_equal(runs[2][0], runs[0][0])  # the first forward: same bits
-    if case == "cora_h4":
-        np.testing.assert_array_equal(runs[2][2], runs[0][2])
-        np.testing.assert_array_equal(runs[2][1], runs[0][1])
-        return
     scale = np.abs(runs[0][2]).max()
     assert np.abs(runs[2][2] - runs[0][2]).max() <= 2e-6 * scale
     # the losses after it agree to float rounding (accuracies may flip a near-tied row)
