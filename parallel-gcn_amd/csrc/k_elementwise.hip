@@ -308,7 +308,9 @@ __global__ __launch_bounds__(XR) void k_xent_fwd(float *__restrict__ logits, int
       reinterpret_cast<float4 *>(dst + base)[q] = make_float4(d[0], d[1], d[2], d[3]);
     }
   };
-  __shared__ float wt[FUSED ? 16 * 128 : 1];  // FUSED: W [k][j]
+  // FUSED: W [k][j] (16 x ld) in the dynamic LDS past the tile (and past the waves' weight-grad
+  // partials, which reuse the tile): sized to the layer, not to the largest class count
+  float *wt = smem + (FUSED ? max(XR * S, (XR / 64) * 3 * 4 * 64) : 0);
   if constexpr (FUSED) {
     for (int e = threadIdx.x; e < 16 * ld; e += XR) {
       const int k = e / ld, j = e - k * ld;
@@ -617,11 +619,11 @@ void launch_out_xent(const float *H, int ldh, int kh, const float *W, int ldw, f
   PGCN_CHECK(!dWp || ld <= 48, PGCN_E_INVALID, "out_xent: the weight-grad partial needs <= 48 classes");
   // the tile, and (weight-grad partials) room for the waves' [3][4][64] partials in it
   const size_t tile = (size_t)XR * (ld + 1), wparts = (size_t)(XR / 64) * 3 * 4 * 64;
-  const size_t lds = (training && dWp && wparts > tile ? wparts : tile) * sizeof(float);
+  const size_t lds = ((wparts > tile ? wparts : tile) + (size_t)16 * ld) * sizeof(float);
   static bool attr = false;
   if (!attr) {
     PGCN_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(k_xent_fwd<true>),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, 117 * 1024));
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
     attr = true;
   }
   hipLaunchKernelGGL(k_xent_fwd<true>, dim3(xent_blocks(n)), dim3(XR), lds, s, logits, ld, grad,
