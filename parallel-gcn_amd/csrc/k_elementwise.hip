@@ -311,6 +311,20 @@ __global__ __launch_bounds__(XR) void k_xent_fwd(float *__restrict__ logits, int
   // FUSED: W [k][j] (16 x ld) in the dynamic LDS past the tile (and past the waves' weight-grad
   // partials, which reuse the tile): sized to the layer, not to the largest class count
   float *wt = smem + (FUSED ? max(XR * S, (XR / 64) * 3 * 4 * 64) : 0);
+  // FUSED: the lane's H operands of all four 16-row groups, loaded before W is staged (one
+  // HBM latency for the block instead of one per group)
+  float ha[4][4];
+  if constexpr (FUSED) {
+    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63, gi = ln >> 4, ii = ln & 15;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      long long grow = row0 + wv * 64 + q * 16 + ii;
+      grow = grow < n ? grow : n - 1;
+      const float *hr = H + grow * (long long)ldh;
+#pragma unroll
+      for (int t4 = 0; t4 < 4; t4++) ha[q][t4] = 4 * gi + t4 < kh ? hr[4 * gi + t4] : 0.0f;
+    }
+  }
   if constexpr (FUSED) {
     for (int e = threadIdx.x; e < 16 * ld; e += XR) {
       const int k = e / ld, j = e - k * ld;
@@ -323,12 +337,7 @@ __global__ __launch_bounds__(XR) void k_xent_fwd(float *__restrict__ logits, int
     const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63, gi = ln >> 4, ii = ln & 15;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-      long long grow = row0 + wv * 64 + q * 16 + ii;
-      grow = grow < n ? grow : n - 1;
-      const float *hr = H + grow * (long long)ldh;
-      float a[4];
-#pragma unroll
-      for (int t4 = 0; t4 < 4; t4++) a[t4] = 4 * gi + t4 < kh ? hr[4 * gi + t4] : 0.0f;
+      const float *a = ha[q];
       for (int tt = 0; 16 * tt < ld; tt++) {
         const int col = 16 * tt + ii;
         floatx4e acc = {0.f, 0.f, 0.f, 0.f};
@@ -369,6 +378,17 @@ __global__ __launch_bounds__(XR) void k_xent_fwd(float *__restrict__ logits, int
   __syncthreads();
   if (write_back || FUSED) from_lds(logits);
   if (training) {
+    // the weight-grad phase's H operands (row 4 st + gi of the wave, column ii), loaded now so
+    // their latency hides behind the grad computation
+    float hw[16];
+    if (FUSED && dWp) {
+      const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63, gi = ln >> 4, ii = ln & 15;
+#pragma unroll
+      for (int st = 0; st < 16; st++) {
+        const int rloc = wv * 64 + 4 * st + gi;
+        hw[st] = (rloc < rows && ii < kh) ? H[(row0 + rloc) * (long long)ldh + ii] : 0.0f;
+      }
+    }
     __syncthreads();  // the shifted logits have left the tile
     if (threadIdx.x < rows) {
       if (t >= 0) {
@@ -418,10 +438,11 @@ __global__ __launch_bounds__(XR) void k_xent_fwd(float *__restrict__ logits, int
     if (FUSED && dWp) {
       if (!dH) __syncthreads();  // the grad tile is complete
       const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63, gi = ln >> 4, ii = ln & 15;
+#pragma unroll
       for (int st = 0; st < 16; st++) {  // 4-row steps over the wave's 64 rows
         const int rloc = wv * 64 + 4 * st + gi;
         const bool ok = rloc < rows;
-        const float av = (ok && ii < kh) ? H[(row0 + rloc) * (long long)ldh + ii] : 0.0f;
+        const float av = hw[st];
 #pragma unroll
         for (int tt = 0; tt < 3; tt++) {
           const int col = 16 * tt + ii;
