@@ -281,14 +281,17 @@ long long pgcn_partition_subgraph(int n, const int *indptr, const int *indices, 
  * one GPU.  *rows / *cols give its shape. */
 int pgcn_debug_rank_graph(int n, const int *indptr, const int *indices, int world, int rank,
                           int chunks, int chunk, pgcn_graph **out, int *rows, int *cols);
-/* "graphsum_variant": 0 normal, 1 skip the feature gather, 2 fold gathers into 4096 rows;
- * "graphsum_plain": 1 disables the XCD column blocking for schedules built afterwards. */
+/* Engine options (process-wide; most are read when an engine is built).  Every option but the
+ * diagnostic ones selects between bit-identical or oracle-tested forms of the same epoch:
+ *   "train_ahead" 0/1, "eval_ax" 0/1, "split_cols" 0/1, "epoch_graph" 0/1, "mm_side" 0/1/2,
+ *   "fuse_epilogue" bits 1 tails | 2 prestaged tables | 4 X-stream epilogue (default 7),
+ *   "fuse_output" 0..3 (default 2), "xstream_ring" 0/1, "lds_min_kb" (< 0: default),
+ *   "lds_blocks" 0 (by shape) or 1..32, "parse_threads" (0: up to 16);
+ * diagnostics: "split_rows" 0/1 (stale logits outside the split), "gemm_variant" 0/1 (the
+ * general GEMM kernels only).  Returns PGCN_E_INVALID on an unknown key or value. */
 int pgcn_debug_set(const char *key, int value);
-/* copies up to max_elems of a diagnostic buffer ("graphsum_lds_stamps": per-wave cycle stamps
- * of the last graphsum_lds_diag=4 launch); returns the buffer's element count or a status */
-long long pgcn_debug_read(const char *key, void *dst, long long max_elems);
-/* Host-only check of the d = 16 LDS GraphSum schedule (window 1 or 2) of a CSR pattern: builds
- * it, walks it as k_graphsum_lds consumes it over a seeded input and returns the max relative
+/* Host-only check of the d = 16 LDS ring schedule (window must be 5) of a CSR pattern: builds
+ * it, walks it as k_graphsum_ring consumes it over a seeded input and returns the max relative
  * error of the row sums against a direct CSR sum, and the number of 4-step entry blocks. */
 int pgcn_debug_lds_check(int n_rows, int n_cols, const int *indptr, const int *indices,
                          int window, double *max_rel_err, long long *n_blocks);
@@ -296,6 +299,14 @@ int pgcn_debug_lds_check(int n_rows, int n_cols, const int *indptr, const int *i
  * cap) and its shape {n_batches, t_max, waves, slots, window}; returns the count or -1. */
 long long pgcn_debug_lds_counts(int n_rows, int n_cols, const int *indptr, const int *indices,
                                 int window, unsigned short *dst, long long cap, int *shape5);
+/* Launch counts of the engine's kernel families since the last reset (process-wide), so a test
+ * can assert which kernels a configuration took: "xs_nn_ring" / "xs_tn_ring" (loader + MFMA-wave
+ * X-stream kernels), "xs_nn" / "xs_tn" (register-streamed X-stream kernels), "gs_ring" (LDS ring
+ * GraphSum), "gs_gather" (gather GraphSum), "out_xent" (output layer fused into the loss),
+ * "gemm_nn" / "gemm_tn" (general MFMA GEMMs).  A non-null name returns its count (then zeroes it
+ * when reset != 0); a null name with reset != 0 zeroes every counter.  Status < 0 on an unknown
+ * name. */
+long long pgcn_debug_path_count(const char *name, int reset);
 
 #ifdef __cplusplus
 }

@@ -29,9 +29,19 @@
  *     k-th training forward of a Dropout draws stream positions
  *       glorot draws + (sizes of the Dropouts built before it) + (k - 1) * (sum of all sizes),
  *     i.e. exactly hpdga's sequence when every Dropout runs once per training pass;
- *   * the scheduling arguments of the reference constructors (smart_event / smart_stream
- *     references used for its S1-S4 stream overlap) are accepted and not needed: modules
- *     enqueue on the stream passed to forward/backward, in order;
+ *   * the scheduling arguments of the reference constructors are honoured as the reference
+ *     uses them (src/module.cu, src/optim.cu): SparseMatmul / Matmul forwards wait for their
+ *     weight's start_matmul_forward event, SparseMatmul's backward records start_set_input,
+ *     a GraphSum built with generate_event records start_matmul_backward after its backward,
+ *     Matmul's backward computes b.grad on its own stream after event_backward (through a
+ *     workspace of its own), CrossEntropyLoss records start_backward after a training forward
+ *     and its backward waits for it, and Adam::step() runs the first weight on
+ *     backward_streams[0] and the others on [1], each followed by its start_matmul_forward
+ *     event.  The constructors without those arguments enqueue everything in order on the
+ *     stream passed to forward/backward;
+ *   * a GraphSum reads dev_graph_value once, at construction (the reference reads it at every
+ *     launch); GCN takes Â's coefficients from the pattern and refuses a graph_value array
+ *     holding anything else;
  *   * CrossEntropyLoss::forward also counts the wrong predictions (accuracy());
  *   * a Dropout on the input features must exist before the SparseMatmul reading them.
  */
@@ -135,14 +145,14 @@ class DevSparseIndex {
   dev_ptr<natural> dev_indices, dev_indptr;
   natural indices_size = 0, indptr_size = 0;
   const SparseIndex &host() const { return host_; }
-  // the device adjacency of this pattern with these values (built once, shared by modules)
-  pgcn::DevGraph *graph(const std::vector<real> &values) const;
+  // the device adjacency of this pattern with these values (built once per distinct value
+  // array, shared by the modules that use it)
+  std::shared_ptr<pgcn::DevGraph> graph(const std::vector<real> &values) const;
 
  private:
   SparseIndex host_;
   std::shared_ptr<void> dev_;
-  mutable std::shared_ptr<pgcn::DevGraph> graph_;
-  mutable std::vector<real> graph_values_;
+  mutable std::vector<std::pair<std::vector<real>, std::shared_ptr<pgcn::DevGraph>>> graphs_;
 };
 
 // include/module.cuh:21-30
@@ -263,12 +273,17 @@ class Adam {
   Adam(const std::vector<shared_ptr<Variable>> &weights, const std::vector<bool> &decays,
        AdamParams const *params_, const std::vector<smart_stream> &backward_streams_,
        std::vector<smart_event> &start_matmul_forward_, smart_stream &forward_training_stream_);
-  void step(const smart_stream &stream);
-  void step();  // on the stream of the constructor (or the default API stream)
+  void step(const smart_stream &stream);  // every weight on `stream`
+  // the reference's schedule when built with its streams and events (src/optim.cu:57-95): the
+  // first weight on backward_streams[0], the others on [1], each followed by its
+  // start_matmul_forward event; else every weight on the default API stream
+  void step();
 
  private:
   shared_ptr<pgcn::Adam> impl_;
   smart_stream stream_;
+  std::vector<smart_stream> schedule_;
+  std::vector<smart_event> events_;
 };
 
 // include/gcn.cuh:40-58

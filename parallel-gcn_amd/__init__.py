@@ -128,7 +128,7 @@ _sig("pgcn_dataset_synthetic", c_int, c_int, c_int, c_int, c_ll, c_u64, P(c_void
 _sig("pgcn_dataset_view", c_int, c_void_p, P(PgcnData), P(c_int), P(c_int))
 _sig("pgcn_dataset_free", c_int, c_void_p)
 _sig("pgcn_debug_set", c_int, ctypes.c_char_p, c_int)
-_sig("pgcn_debug_read", c_ll, ctypes.c_char_p, c_void_p, c_ll)
+_sig("pgcn_debug_path_count", c_ll, ctypes.c_char_p, c_int)
 _sig("pgcn_debug_lds_check", c_int, c_int, c_int, c_void_p, c_void_p, c_int, P(ctypes.c_double),
      P(c_ll))
 _sig("pgcn_debug_lds_counts", c_ll, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_ll,
@@ -154,6 +154,27 @@ def check(status, where=""):
 
 def _ptr(a):
     return a.ctypes.data_as(c_void_p)
+
+
+KERNEL_PATHS = ("xs_nn_ring", "xs_tn_ring", "xs_nn", "xs_tn", "gs_ring", "gs_gather", "out_xent",
+                "gemm_nn", "gemm_tn")
+
+
+def path_counts(reset=False):
+    """Launch counts of the kernel families since the last reset (pgcn_debug_path_count)."""
+    out = {}
+    for k in KERNEL_PATHS:
+        n = lib.pgcn_debug_path_count(k.encode(), 0)
+        if n < 0:
+            raise PgcnError(int(n), "path_count " + k)
+        out[k] = int(n)
+    if reset:
+        lib.pgcn_debug_path_count(None, 1)
+    return out
+
+
+def reset_path_counts():
+    check(int(lib.pgcn_debug_path_count(None, 1)), "path_count reset")
 
 
 # --------------------------------------------------------------------------- data
@@ -477,5 +498,5 @@ EXPORTED = [
     "pgcn_dataset_load_binary", "pgcn_dataset_binarize", "pgcn_dataset_synthetic",
     "pgcn_dataset_view",
     "pgcn_dataset_free", "pgcn_partition_bounds", "pgcn_partition_subgraph", "pgcn_debug_set",
-    "pgcn_debug_read", "pgcn_debug_lds_check", "pgcn_debug_lds_counts",
+    "pgcn_debug_lds_check", "pgcn_debug_lds_counts", "pgcn_debug_path_count",
 ]

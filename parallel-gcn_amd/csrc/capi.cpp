@@ -1,4 +1,5 @@
 // parallel-gcn_amd/csrc/capi.cpp -- the extern "C" boundary declared in include/pgcn.h.
+#include <atomic>
 #include <cstring>
 #include <memory>
 
@@ -16,47 +17,27 @@
 using namespace pgcn;
 
 namespace pgcn {
-extern int g_graphsum_variant;      // k_graphsum.hip (diagnostics)
-extern int g_graphsum_force_plain;  // host/graph.cpp (diagnostics)
-extern int g_gemm_variant;          // k_gemm.hip (diagnostics)
+// engine knobs (pgcn_debug_set): defaults and meaning at their definitions
+extern int g_gemm_variant;          // k_gemm.hip
 extern int g_train_ahead;           // host/gcn.cpp
 extern int g_split_rows;            // host/gcn.cpp
 extern int g_split_cols;            // host/gcn.cpp
 extern int g_fuse_epilogue;         // host/gcn.cpp
-extern int g_mm_side;               // host/gcn.cpp
-extern int g_graphsum_ring_wide;    // host/graph.cpp
-extern long long g_lds_min_bytes;     // host/graph.cpp
-extern long long g_blocked_min_bytes; // host/graph.cpp
-extern int g_mask_side;             // host/gcn.cpp
-extern int g_xstream_tn_lds;        // k_gemm.hip
-extern int g_xstream_ring;          // k_xstream_lds.hip
-extern int g_xstream_ring_inflight; // k_xstream_lds.hip
-extern int g_xstream_ring_diag;     // k_xstream_lds.hip
-extern int g_xstream_ring_slots;    // k_xstream_lds.hip
-extern int g_xstream_tn_split;      // k_xstream_lds.hip
 extern int g_fuse_output;           // host/gcn.cpp
-extern int g_fuse_output_bwd;       // host/module.cpp
-extern int g_fuse_output_wgrad;     // host/module.cpp
-extern int g_xstream_nn_balance;    // k_gemm.hip
+extern int g_mm_side;               // host/gcn.cpp
 extern int g_eval_ax;               // host/gcn.cpp
 extern int g_epoch_graph;           // host/gcn.cpp
+extern long long g_lds_min_bytes;   // host/graph.cpp
 extern int g_lds_blocks;            // host/graph.cpp
-extern int g_lds_blocks_subset;     // host/graph.cpp (diagnostics)
-extern int g_graphsum_lds;          // host/graph.cpp (diagnostics)
-extern int g_graphsum_lds_wide;     // host/graph.cpp
-extern int g_graphsum_lds_order;    // host/graph.cpp (diagnostics)
-extern int g_graphsum_lds_diag;     // k_graphsum_lds.hip (diagnostics)
-extern int g_graphsum_lds_window;   // host/graph.cpp (diagnostics)
-extern int g_ring_balance;          // host/ring.cpp
-extern int g_graphsum_ring_prio;    // k_graphsum_ring.hip
-extern int g_graphsum_ring_fused;   // k_graphsum_ring.hip
-extern int g_graphsum_prestage;     // host/module.cpp
-extern int g_xstream_epilogue;      // host/module.cpp
-extern int g_ring_spread;           // host/ring.cpp
+extern int g_xstream_ring;          // k_xstream_lds.hip
 extern int g_parse_threads;         // host/data.cpp: pieces of the parallel text parse
-extern int g_graphsum_lds_sync;     // k_graphsum_lds.hip (diagnostics)
-extern int g_graphsum_lds_opt;      // k_graphsum_lds.hip (diagnostics)
-long long lds_stamps_read(void *dst, long long max_elems);
+
+namespace {
+std::atomic<long long> g_path_hits[KP_COUNT];
+const char *const kPathNames[KP_COUNT] = {"xs_nn_ring", "xs_tn_ring", "xs_nn",   "xs_tn",  "gs_ring",
+                                          "gs_gather",  "out_xent",   "gemm_nn", "gemm_tn"};
+}  // namespace
+void note_path(KernelPath p) { g_path_hits[p].fetch_add(1, std::memory_order_relaxed); }
 }  // namespace pgcn
 
 struct pgcn_graph {
@@ -599,72 +580,46 @@ int pgcn_dataset_free(pgcn_dataset *ds) {
 // ---------------------------------------------------------------- diagnostics
 int pgcn_debug_set(const char *key, int value) {
   if (!key) return PGCN_E_INVALID;
-  if (!std::strcmp(key, "graphsum_variant")) pgcn::g_graphsum_variant = value;
-  else if (!std::strcmp(key, "graphsum_plain")) pgcn::g_graphsum_force_plain = value;
-  else if (!std::strcmp(key, "graphsum_lds")) pgcn::g_graphsum_lds = value;
-  else if (!std::strcmp(key, "graphsum_lds_wide")) pgcn::g_graphsum_lds_wide = value;
-  else if (!std::strcmp(key, "graphsum_lds_order")) pgcn::g_graphsum_lds_order = value;
-  else if (!std::strcmp(key, "graphsum_lds_diag")) pgcn::g_graphsum_lds_diag = value;
-  else if (!std::strcmp(key, "graphsum_lds_window")) pgcn::g_graphsum_lds_window = value;
-  else if (!std::strcmp(key, "parse_threads")) pgcn::g_parse_threads = value;
-  else if (!std::strcmp(key, "ring_balance")) pgcn::g_ring_balance = value;
-  else if (!std::strcmp(key, "graphsum_ring_prio")) pgcn::g_graphsum_ring_prio = value;
-  else if (!std::strcmp(key, "graphsum_ring_fused")) pgcn::g_graphsum_ring_fused = value;
-  else if (!std::strcmp(key, "graphsum_prestage")) pgcn::g_graphsum_prestage = value;
-  else if (!std::strcmp(key, "xstream_epilogue")) pgcn::g_xstream_epilogue = value;
-  else if (!std::strcmp(key, "ring_spread")) pgcn::g_ring_spread = value;
-  else if (!std::strcmp(key, "graphsum_lds_sync")) pgcn::g_graphsum_lds_sync = value;
-  else if (!std::strcmp(key, "graphsum_lds_opt")) pgcn::g_graphsum_lds_opt = value;
-  else if (!std::strcmp(key, "gemm_variant")) pgcn::g_gemm_variant = value;
-  else if (!std::strcmp(key, "train_ahead")) pgcn::g_train_ahead = value;
+  if (!std::strcmp(key, "train_ahead")) pgcn::g_train_ahead = value;
   else if (!std::strcmp(key, "split_rows")) pgcn::g_split_rows = value;
   else if (!std::strcmp(key, "split_cols")) pgcn::g_split_cols = value;
-  else if (!std::strcmp(key, "fuse_epilogue")) pgcn::g_fuse_epilogue = value;
-  else if (!std::strcmp(key, "mm_side")) pgcn::g_mm_side = value;
-  else if (!std::strcmp(key, "graphsum_ring_wide")) pgcn::g_graphsum_ring_wide = value;
-  else if (!std::strcmp(key, "lds_min_kb"))  // < 0: the default (one XCD's L2 budget)
-    pgcn::g_lds_min_bytes = value < 0 ? DevGraph::kLdsMinBytes : 1024LL * value;
-  else if (!std::strcmp(key, "blocked_min_kb"))
-    pgcn::g_blocked_min_bytes = value < 0 ? (long long)DevGraph::kL2Budget : 1024LL * value;
-  else if (!std::strcmp(key, "mask_side")) pgcn::g_mask_side = value;
-  else if (!std::strcmp(key, "xstream_tn_lds")) pgcn::g_xstream_tn_lds = value;
-  else if (!std::strcmp(key, "xstream_ring")) pgcn::g_xstream_ring = value;
-  else if (!std::strcmp(key, "xstream_ring_inflight")) pgcn::g_xstream_ring_inflight = value;
-  else if (!std::strcmp(key, "xstream_ring_diag")) pgcn::g_xstream_ring_diag = value;
-  else if (!std::strcmp(key, "xstream_ring_slots")) pgcn::g_xstream_ring_slots = value;
-  else if (!std::strcmp(key, "xstream_tn_split")) pgcn::g_xstream_tn_split = value;
-  else if (!std::strcmp(key, "fuse_output")) pgcn::g_fuse_output = value;
-  else if (!std::strcmp(key, "fuse_output_bwd")) pgcn::g_fuse_output_bwd = value;
-  else if (!std::strcmp(key, "fuse_output_wgrad")) pgcn::g_fuse_output_wgrad = value;
-  else if (!std::strcmp(key, "xstream_nn_balance")) pgcn::g_xstream_nn_balance = value;
   else if (!std::strcmp(key, "eval_ax")) pgcn::g_eval_ax = value;
   else if (!std::strcmp(key, "epoch_graph")) pgcn::g_epoch_graph = value;
-  else if (!std::strcmp(key, "lds_blocks") || !std::strcmp(key, "lds_blocks_subset")) {
+  else if (!std::strcmp(key, "fuse_epilogue")) {
+    if (value < 0 || value > 7) return PGCN_E_INVALID;
+    pgcn::g_fuse_epilogue = value;
+  } else if (!std::strcmp(key, "fuse_output")) {
+    if (value < 0 || value > 3) return PGCN_E_INVALID;
+    pgcn::g_fuse_output = value;
+  } else if (!std::strcmp(key, "mm_side")) pgcn::g_mm_side = value;
+  else if (!std::strcmp(key, "xstream_ring")) pgcn::g_xstream_ring = value;
+  else if (!std::strcmp(key, "gemm_variant")) pgcn::g_gemm_variant = value;
+  else if (!std::strcmp(key, "lds_min_kb"))  // < 0: the default
+    pgcn::g_lds_min_bytes = value < 0 ? DevGraph::kLdsMinBytes : 1024LL * value;
+  else if (!std::strcmp(key, "lds_blocks")) {
     if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8 && value != 16 &&
         value != 32)
       return PGCN_E_INVALID;
-    (key[10] ? pgcn::g_lds_blocks_subset : pgcn::g_lds_blocks) = value;
-  }
+    pgcn::g_lds_blocks = value;
+  } else if (!std::strcmp(key, "parse_threads")) pgcn::g_parse_threads = value;
   else return PGCN_E_INVALID;
   return PGCN_OK;
 }
 
-// CPU check of the d = 16 LDS schedule of a CSR pattern: builds it (window 1 or 2), walks it
-// as the kernel does over a seeded input and reports the max relative error of the sums
-// against a direct CSR sum, and the number of entry blocks.  No device needed.
-// Diagnostics: the LDS schedule's step counts [wg][t_max][LDS_CW][LDS_SLOTS] (uint16) and its
-// shape {n_batches, t_max, LDS_CW, LDS_SLOTS, window} (schedule-balance analysis on the host).
+// CPU check of the d = 16 ring schedule of a CSR pattern: builds it, walks it as the kernel
+// does over a seeded input and reports the max relative error of the sums against a direct CSR
+// sum, and the number of entry blocks.  No device needed.  (window: kRingWindow, the only
+// schedule.)  Diagnostics: the schedule's step counts [wg][t_max][LDS_CW][LDS_SLOTS] (uint16)
+// and its shape {n_batches, t_max, LDS_CW, LDS_SLOTS, window} (balance analysis on the host).
 long long pgcn_debug_lds_counts(int n_rows, int n_cols, const int *indptr, const int *indices,
                                 int window, unsigned short *dst, long long cap, int *shape5) {
   long long n = -1;
   const int st = guarded([&] {
-    PGCN_CHECK(n_rows > 0 && n_cols > 0 && indptr && indices, PGCN_E_INVALID, "lds_counts args");
+    PGCN_CHECK(n_rows > 0 && n_cols > 0 && indptr && indices && window == kRingWindow,
+               PGCN_E_INVALID, "lds_counts args");
     std::vector<int> ip(indptr, indptr + n_rows + 1), ix(indices, indices + indptr[n_rows]);
-    const bool ring = window == kRingWindow;
-    const std::vector<int> cut = ring ? ring_cuts(n_cols, ix, lds_blocks(n_rows, n_cols))
-                                      : column_cuts(n_cols, ix, lds_blocks(n_rows, n_cols));
-    const LdsHost h = ring ? build_ring_host(n_rows, n_cols, ip, ix, cut)
-                           : build_lds_host(n_rows, n_cols, ip, ix, cut, window);
+    const std::vector<int> cut = ring_cuts(n_cols, ix, lds_blocks(n_rows, n_cols));
+    const LdsHost h = build_ring_host(n_rows, n_cols, ip, ix, cut);
     n = (long long)h.counts.size();
     if (dst) std::copy(h.counts.begin(), h.counts.begin() + std::min(n, cap), dst);
     if (shape5) {
@@ -672,7 +627,7 @@ long long pgcn_debug_lds_counts(int n_rows, int n_cols, const int *indptr, const
       shape5[1] = h.t_max;
       shape5[2] = LDS_CW;
       shape5[3] = LDS_SLOTS;
-      shape5[4] = h.window;
+      shape5[4] = kRingWindow;
     }
   });
   return st == PGCN_OK ? n : -1;
@@ -681,18 +636,16 @@ long long pgcn_debug_lds_counts(int n_rows, int n_cols, const int *indptr, const
 int pgcn_debug_lds_check(int n_rows, int n_cols, const int *indptr, const int *indices,
                          int window, double *max_rel_err, long long *n_blocks) {
   return guarded([&] {
-    PGCN_CHECK(n_rows > 0 && n_cols > 0 && indptr && indices, PGCN_E_INVALID, "lds_check args");
+    PGCN_CHECK(n_rows > 0 && n_cols > 0 && indptr && indices && window == kRingWindow,
+               PGCN_E_INVALID, "lds_check args");
     std::vector<int> ip(indptr, indptr + n_rows + 1), ix(indices, indices + indptr[n_rows]);
-    const bool ring = window == kRingWindow;
-    const std::vector<int> cut = ring ? ring_cuts(n_cols, ix, lds_blocks(n_rows, n_cols))
-                                      : column_cuts(n_cols, ix, lds_blocks(n_rows, n_cols));
-    const LdsHost h = ring ? build_ring_host(n_rows, n_cols, ip, ix, cut)
-                           : build_lds_host(n_rows, n_cols, ip, ix, cut, window);
+    const std::vector<int> cut = ring_cuts(n_cols, ix, lds_blocks(n_rows, n_cols));
+    const LdsHost h = build_ring_host(n_rows, n_cols, ip, ix, cut);
     std::vector<float> in((size_t)n_cols);
     uint64_t st[2] = {12345, 67890};
     for (auto &x : in) x = (float)((double)(xs_next(st) & 0xffffff) / (double)0x1000000 - 0.5);
     std::vector<double> out((size_t)n_rows, 0.0);
-    lds_emulate(h, n_rows, in.data(), out.data());
+    ring_emulate(h, n_rows, in.data(), out.data());
     double err = 0;
     for (int r = 0; r < n_rows; r++) {
       double ref = 0, mag = 0;
@@ -707,13 +660,16 @@ int pgcn_debug_lds_check(int n_rows, int n_cols, const int *indptr, const int *i
   });
 }
 
-long long pgcn_debug_read(const char *key, void *dst, long long max_elems) {
-  if (!key) return PGCN_E_INVALID;
-  long long r = PGCN_E_INVALID;
-  const int st = guarded([&] {
-    if (!std::strcmp(key, "graphsum_lds_stamps")) r = pgcn::lds_stamps_read(dst, max_elems);
-  });
-  return st != PGCN_OK ? st : r;
+long long pgcn_debug_path_count(const char *name, int reset) {
+  if (!name) {
+    if (!reset) return PGCN_E_INVALID;
+    for (auto &h : pgcn::g_path_hits) h.store(0);
+    return 0;
+  }
+  for (int p = 0; p < KP_COUNT; p++)
+    if (!std::strcmp(name, pgcn::kPathNames[p]))
+      return reset ? pgcn::g_path_hits[p].exchange(0) : pgcn::g_path_hits[p].load();
+  return PGCN_E_INVALID;
 }
 
 // ---------------------------------------------------------------- partition (host only)

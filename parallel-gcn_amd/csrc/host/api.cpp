@@ -229,21 +229,27 @@ DevSparseIndex::DevSparseIndex(const SparseIndex &sparse_index) : host_(sparse_i
   dev_ = b;
 }
 
-DevGraph *DevSparseIndex::graph(const std::vector<real> &values) const {
-  if (graph_ && values == graph_values_) return graph_.get();
+// One device graph per distinct value array (compared bit for bit, so NaNs compare equal to
+// themselves), all kept for as long as the index or a GraphSum built on them lives: two
+// GraphSums on one index with different values each keep their own graph.
+std::shared_ptr<DevGraph> DevSparseIndex::graph(const std::vector<real> &values) const {
+  for (const auto &gv : graphs_)
+    if (gv.first.size() == values.size() &&
+        std::memcmp(gv.first.data(), values.data(), values.size() * sizeof(real)) == 0)
+      return gv.second;
   const int n = (int)indptr_size - 1;
   PGCN_CHECK(n > 0 && values.size() == host_.indices.size(), PGCN_E_INVALID,
              "GraphSum: graph values must match the pattern");
   const std::vector<int> ip = to_int(host_.indptr), ix = to_int(host_.indices);
-  graph_ = std::make_shared<DevGraph>(n, n, ip.data(), ix.data(), values.data());
+  auto g = std::make_shared<DevGraph>(n, n, ip.data(), ix.data(), values.data());
   // Â = D^-1/2 A D^-1/2 exactly (the parser's coefficients): the LDS path's factorisation
   // s_i s_j applies; any other values keep the per-edge kernels
   if (values == graph_coefs(n, ip.data(), ix.data())) {
     const std::vector<float> s = degree_scales(n, ip.data());
-    graph_->set_scales(s, s);
+    g->set_scales(s, s);
   }
-  graph_values_ = values;
-  return graph_.get();
+  graphs_.emplace_back(values, g);
+  return g;
 }
 
 // ---------------------------------------------------------------------- modules
@@ -318,6 +324,10 @@ struct SparseMatmul::Impl {
   DevSparseIndex *sp;
   int m, n, p;
   Dropout::Impl *drop = nullptr;
+  // src/module.cu:124-160: the forward waits for the weight's optimizer step, the backward
+  // signals that the input may be reset (set_input)
+  bool events = false;
+  smart_event start_matmul_forward, start_set_input;
   DevFeatures feats;
   std::unique_ptr<pgcn::SparseMatmul> mod;
   pgcn::SparseMatmul *module() {
@@ -343,8 +353,13 @@ struct SparseMatmul::Impl {
 
 SparseMatmul::SparseMatmul(shared_ptr<Variable> a_, shared_ptr<Variable> b_,
                            shared_ptr<Variable> c_, DevSparseIndex *sp_, natural m_, natural n_,
-                           natural p_, smart_event &, smart_event &)
-    : SparseMatmul(std::move(a_), std::move(b_), std::move(c_), sp_, m_, n_, p_) {}
+                           natural p_, smart_event &start_matmul_forward_,
+                           smart_event &start_set_input_)
+    : SparseMatmul(std::move(a_), std::move(b_), std::move(c_), sp_, m_, n_, p_) {
+  impl_->events = true;
+  impl_->start_matmul_forward = start_matmul_forward_;
+  impl_->start_set_input = start_set_input_;
+}
 
 SparseMatmul::SparseMatmul(shared_ptr<Variable> a_, shared_ptr<Variable> b_,
                            shared_ptr<Variable> c_, DevSparseIndex *sp_, natural m_, natural n_,
@@ -368,19 +383,30 @@ SparseMatmul::SparseMatmul(shared_ptr<Variable> a_, shared_ptr<Variable> b_,
   cx.ensure_ws(gemm_tn_workspace(I.m, I.p, I.n));
 }
 void SparseMatmul::forward(bool training, const smart_stream &stream) const {
+  if (impl_->events) impl_->start_matmul_forward.wait(stream);
   impl_->module()->forward(training, Stream::wrap(stream.get()));
 }
 void SparseMatmul::backward(const smart_stream &stream) const {
   impl_->module()->backward(Stream::wrap(stream.get()));
+  if (impl_->events) impl_->start_set_input.record(stream);
 }
 
 struct GraphSum::Impl {
+  std::shared_ptr<pgcn::DevGraph> graph;  // kept alive as long as the module
   std::unique_ptr<pgcn::GraphSum> mod;
+  // src/module.cu:200-207: the backward signals that the Matmul before it may compute its
+  // weight gradient (its c.grad is complete)
+  bool generate_event = false;
+  smart_event start_matmul_backward;
 };
 
 GraphSum::GraphSum(shared_ptr<Variable> in_, shared_ptr<Variable> out_, DevSparseIndex *graph_,
-                   const real *dev_graph_value_, natural dim_, bool, smart_event &)
-    : GraphSum(std::move(in_), std::move(out_), graph_, dev_graph_value_, dim_) {}
+                   const real *dev_graph_value_, natural dim_, bool generate_event_,
+                   smart_event &start_matmul_backward_)
+    : GraphSum(std::move(in_), std::move(out_), graph_, dev_graph_value_, dim_) {
+  impl_->generate_event = generate_event_;
+  impl_->start_matmul_backward = start_matmul_backward_;
+}
 
 GraphSum::GraphSum(shared_ptr<Variable> in_, shared_ptr<Variable> out_, DevSparseIndex *graph_,
                    const real *dev_graph_value_, natural dim_)
@@ -392,7 +418,8 @@ GraphSum::GraphSum(shared_ptr<Variable> in_, shared_ptr<Variable> out_, DevSpars
   std::vector<real> vals(graph_->indices_size);
   PGCN_HIP(hipMemcpy(vals.data(), dev_graph_value_, vals.size() * sizeof(real),
                      hipMemcpyDeviceToHost));
-  impl_->mod = std::make_unique<pgcn::GraphSum>(in_->impl(), out_->impl(), graph_->graph(vals), d,
+  impl_->graph = graph_->graph(vals);
+  impl_->mod = std::make_unique<pgcn::GraphSum>(in_->impl(), out_->impl(), impl_->graph.get(), d,
                                                 &cx.ctx);
 }
 void GraphSum::forward(bool training, const smart_stream &stream) const {
@@ -400,6 +427,7 @@ void GraphSum::forward(bool training, const smart_stream &stream) const {
 }
 void GraphSum::backward(const smart_stream &stream) const {
   impl_->mod->backward(Stream::wrap(stream.get()));
+  if (impl_->generate_event) impl_->start_matmul_backward.record(stream);
 }
 
 struct ReLU::Impl {
@@ -419,11 +447,25 @@ void ReLU::backward(const smart_stream &stream) const {
 
 struct Matmul::Impl {
   std::unique_ptr<pgcn::Matmul> mod;
+  // src/module.cu:319-324, 431-472: the forward waits for the weight's optimizer step; the
+  // backward computes a.grad on the backward stream and b.grad on the module's own stream once
+  // event_backward (c.grad complete) has fired, through a workspace of its own
+  bool events = false;
+  smart_event event_forward, event_backward;
+  smart_stream my_stream;
+  DeviceBuffer<float> ws;
 };
 Matmul::Matmul(shared_ptr<Variable> a_, shared_ptr<Variable> b_, shared_ptr<Variable> c_,
-               natural m_, natural n_, natural p_, smart_event &, smart_event &,
-               const smart_stream &)
-    : Matmul(std::move(a_), std::move(b_), std::move(c_), m_, n_, p_) {}
+               natural m_, natural n_, natural p_, smart_event &event_forward_,
+               smart_event &event_backward_, const smart_stream &stream_)
+    : Matmul(std::move(a_), std::move(b_), std::move(c_), m_, n_, p_) {
+  Impl &I = *impl_;
+  I.events = true;
+  I.event_forward = event_forward_;
+  I.event_backward = event_backward_;
+  I.my_stream = stream_;
+  I.ws.allocate(gemm_tn_workspace((int)m_, (int)p_, (int)n_) / sizeof(float) + 64);
+}
 Matmul::Matmul(shared_ptr<Variable> a_, shared_ptr<Variable> b_, shared_ptr<Variable> c_,
                natural m_, natural n_, natural p_)
     : impl_(std::make_shared<Impl>()) {
@@ -436,10 +478,18 @@ Matmul::Matmul(shared_ptr<Variable> a_, shared_ptr<Variable> b_, shared_ptr<Vari
   impl_->mod = std::make_unique<pgcn::Matmul>(a_->impl(), b_->impl(), c_->impl(), m, n, p, &cx.ctx);
 }
 void Matmul::forward(bool training, const smart_stream &stream) const {
+  if (impl_->events) impl_->event_forward.wait(stream);
   impl_->mod->forward(training, Stream::wrap(stream.get()));
 }
 void Matmul::backward(const smart_stream &stream) const {
-  impl_->mod->backward(Stream::wrap(stream.get()));
+  Impl &I = *impl_;
+  if (!I.events) {
+    I.mod->backward(Stream::wrap(stream.get()));
+    return;
+  }
+  I.mod->backward_input(Stream::wrap(stream.get()));
+  I.event_backward.wait(I.my_stream);
+  I.mod->backward_weight(I.my_stream.get(), I.ws.get());
 }
 
 struct CrossEntropyLoss::Impl {
@@ -449,10 +499,17 @@ struct CrossEntropyLoss::Impl {
   int classes;
   std::unique_ptr<pgcn::CrossEntropyLoss> mod;
   PinnedBuffer<float> res{2};
+  // src/module.cu:526-548: a training forward signals start_backward once the loss gradient is
+  // written; the backward stream waits for it
+  bool events = false;
+  smart_event start_backward;
 };
 CrossEntropyLoss::CrossEntropyLoss(shared_ptr<Variable> logits_, const integer *dev_truth_,
-                                   real *loss_, natural num_classes_, smart_event &)
-    : CrossEntropyLoss(std::move(logits_), dev_truth_, loss_, num_classes_) {}
+                                   real *loss_, natural num_classes_, smart_event &event)
+    : CrossEntropyLoss(std::move(logits_), dev_truth_, loss_, num_classes_) {
+  impl_->events = true;
+  impl_->start_backward = event;
+}
 CrossEntropyLoss::CrossEntropyLoss(shared_ptr<Variable> logits_, const integer *dev_truth_,
                                    real *loss_, natural num_classes_)
     : impl_(std::make_shared<Impl>()) {
@@ -488,6 +545,7 @@ void CrossEntropyLoss::forward(bool training, const smart_stream &stream) const 
   m.xent_blocks = xent_blocks(rows);
   m.compact_n = 0;
   impl_->mod->forward(training, Stream::wrap(stream.get()));
+  if (training && impl_->events) impl_->start_backward.record(stream);
   // mean loss and accuracy of the labelled rows (no weight decay term: GCN adds it)
   launch_reduce_scalars(cx.xent_partials.get(), m.xent_blocks, nullptr, 0, cx.sums.get(),
                         stream.get(), count, 0.0f, cx.out2.get());
@@ -497,7 +555,10 @@ void CrossEntropyLoss::forward(bool training, const smart_stream &stream) const 
     PGCN_HIP(hipMemcpyAsync(impl_->loss, cx.out2.get(), sizeof(float), hipMemcpyDeviceToHost,
                             stream.get()));
 }
-void CrossEntropyLoss::backward(const smart_stream &) const {}  // module.cpp:155-156
+void CrossEntropyLoss::backward(const smart_stream &stream) const {
+  // the gradient itself was written by the forward (hpdga module.cpp:155-156)
+  if (impl_->events) impl_->start_backward.wait(stream);
+}
 real CrossEntropyLoss::accuracy() const { return impl_->res.get()[1]; }
 
 // ---------------------------------------------------------------------- Adam
@@ -518,13 +579,33 @@ Adam::Adam(const std::vector<shared_ptr<Variable>> &weights, const std::vector<b
   impl_ = std::make_shared<pgcn::Adam>(w, decays, a);
 }
 Adam::Adam(const std::vector<shared_ptr<Variable>> &weights, const std::vector<bool> &decays,
-           AdamParams const *params_, const std::vector<smart_stream> &,
-           std::vector<smart_event> &, smart_stream &forward_training_stream_)
+           AdamParams const *params_, const std::vector<smart_stream> &backward_streams_,
+           std::vector<smart_event> &start_matmul_forward_, smart_stream &forward_training_stream_)
     : Adam(weights, decays, params_) {
+  PGCN_CHECK(backward_streams_.size() >= 2 && start_matmul_forward_.size() == weights.size(),
+             PGCN_E_INVALID, "Adam: two backward streams and one event per weight");
   stream_ = forward_training_stream_;
+  // src/optim.cu:57-95: the first weight on backward_streams[0], the others on [1], each
+  // followed by its start_matmul_forward event
+  for (size_t i = 0; i < weights.size(); i++) {
+    schedule_.push_back(backward_streams_[i == 0 ? 0 : 1]);
+    events_.push_back(start_matmul_forward_[i]);
+  }
 }
 void Adam::step(const smart_stream &stream) { impl_->step(Stream::wrap(stream.get())); }
-void Adam::step() { step(stream_); }
+void Adam::step() {
+  if (schedule_.empty()) {
+    step(stream_);
+    return;
+  }
+  std::vector<hipStream_t> st;
+  std::vector<hipEvent_t> ev;
+  for (size_t i = 0; i < schedule_.size(); i++) {
+    st.push_back(schedule_[i].get());
+    ev.push_back(events_[i].get());
+  }
+  impl_->step_each(st, ev);
+}
 
 // ---------------------------------------------------------------------- Parser
 Parser::Parser(GCNParams *gcnParams, GCNData *gcnData, const std::string &graph_name,
@@ -587,6 +668,18 @@ GCN::GCN(GCNParams const *params_, AdamParams const *adam_params_, GCNData const
   d.feature_value = data_->feature_value;
   d.split = to_int(data_->split);
   d.label = data_->label;
+  // the engine computes Â's coefficients itself (bit-exact with the parser's, hpdga
+  // module.cpp:88-90); a graph_value array holding anything else is refused, not ignored
+  if (!data_->graph_value.empty()) {
+    const std::vector<float> want =
+        graph_coefs(d.num_nodes, d.graph.indptr.data(), d.graph.indices.data());
+    PGCN_CHECK(data_->graph_value.size() == want.size() &&
+                   std::memcmp(data_->graph_value.data(), want.data(),
+                               want.size() * sizeof(float)) == 0,
+               PGCN_E_INVALID,
+               "GCN: graph_value must be empty or Â's coefficients 1/sqrtf(deg_i deg_j) (the "
+               "engine's GraphSum computes them; other values need the Module API)");
+  }
   int dev = 0;
   PGCN_HIP(hipGetDevice(&dev));
   impl_ = std::make_unique<pgcn::GCN>(q, a, d, dev);

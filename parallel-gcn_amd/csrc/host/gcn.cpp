@@ -15,7 +15,6 @@ namespace pgcn {
 // "train_ahead" (pgcn_debug_set, read at engine build): eval's first-layer forward also
 // computes the next training forward's product (SparseMatmul, one pass over dense X)
 int g_train_ahead = 1;
-int g_mask_side = 0;  // "mask_side" (read at engine build): see ModuleContext::mask_side
 // "eval_ax" (read at engine build): eval's first layer as (Â X) W1 from Â X computed once
 // (Â and X are constants: exact algebra, fp32 rounding order differs)
 int g_eval_ax = 1;
@@ -30,13 +29,20 @@ int g_split_rows = 0;
 // edges from the training split's columns.  The loss gradient is exactly zero on every other
 // row, so the skipped terms are exact zeros: in.grad is the full gradient of every row
 int g_split_cols = 1;
-// "fuse_epilogue" (read at engine build): the ReLU / Dropout modules next to a GraphSum run in
-// its final-write epilogue (gs_epilogue.hpp), bit-identical to separate launches
-int g_fuse_epilogue = 1;
-// "fuse_output": the output layer's Matmul forward runs inside the loss (launch_out_xent) when
-// the Matmul produces the logits (the reassociated order: GraphSum, then Matmul) from at most
-// 16 columns (bit-identical)
-int g_fuse_output = 1;
+// "fuse_epilogue" (read at engine build), bits, all bit-identical to separate launches:
+//   1 (kFuseTails)    the ReLU / Dropout modules next to a GraphSum run in its final-write
+//                     epilogue (gs_epilogue.hpp);
+//   2 (kFusePrestage) ... and that epilogue also writes the next GraphSum's prescaled input
+//                     table, which then skips its prescale launch;
+//   4 (kFuseXstream)  the first layer's X-stream product applies the eval ReLU / writes the
+//                     first GraphSum's table.
+int g_fuse_epilogue = kFuseTails | kFusePrestage | kFuseXstream;
+// "fuse_output" (read at engine build): 0 = separate Matmul + loss; 1 = the output layer's
+// Matmul forward and input grad run inside the loss (launch_out_xent) when the Matmul produces
+// the logits (the reassociated order: GraphSum, then Matmul) from at most 16 columns
+// (bit-identical); 2 (default) = ... and its weight grad's block partials on graphs of >=
+// 65,536 rows (the same sums in another grouping); 3 = ... on any graph
+int g_fuse_output = 2;
 // "mm_side" (read at engine build): Matmul weight gradients on the side stream (ModuleContext)
 // on graphs of at least kMmSideRows rows; 2 = on every graph.  Off: r02 A/B on reddit-114M,
 // three runs each, 486.5 (on) vs 487.4 (off) epochs/s -- the LDS GraphSum holds every CU with
@@ -74,6 +80,21 @@ float Adam::step_size(int t) const {
 void Adam::step(const Stream &s) {
   step_count++;
   launch(s, step_size(step_count), nullptr, nullptr, 1);
+}
+
+void Adam::step_each(const std::vector<hipStream_t> &streams,
+                     const std::vector<hipEvent_t> &events) {
+  PGCN_CHECK(streams.size() == vars.size() && events.size() == vars.size(), PGCN_E_INVALID,
+             "Adam: one stream and one event per weight");
+  step_count++;
+  const float st = step_size(step_count);
+  for (size_t i = 0; i < vars.size(); i++) {
+    const Var &v = vars[i];
+    launch_adam(v.w->dev_data.get(), v.w->dev_grad.get(), v.m.get(), v.v.get(), v.w->size, st,
+                params.beta1, params.beta2, params.eps, params.weight_decay, v.decay ? 1 : 0,
+                streams[i]);
+    if (events[i]) PGCN_HIP(hipEventRecord(events[i], streams[i]));
+  }
 }
 
 void Adam::step_graph(const Stream &s, const float *table, const int *ctr, int cap) const {
@@ -231,12 +252,9 @@ GCN::GCN(const GCNParams &params_, const AdamParams &adam, const GCNData &data, 
   int lo_prio = 0, hi_prio = 0;
   PGCN_HIP(hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
   stream = Stream::create(hi_prio);  // the reference uses High priority streams
-  // side stream: the next epoch's input-dropout mask is drawn here while the weight-gradient
-  // pass streams X (compute-bound RNG beside an HBM-bound GEMM)
+  // side stream: weight gradients beside the rest of the backward pass (mm_side)
   side_stream = Stream::create(lo_prio);
   ctx.side_stream = side_stream.get();
-  ctx.mask_ready = Event::create();
-  ctx.tn_start = Event::create();
   const int world = dist ? dist->world : 1, rank = dist ? dist->rank : 0;
   part = make_partition(params.num_nodes, data.graph.indptr.data(), world, rank,
                         dist ? kRsChunks : 1);
@@ -464,7 +482,6 @@ void GCN::build(const GCNData &data) {
     ctx.side_join = Event::create();
   }
   ctx.train_ahead = g_train_ahead != 0;
-  ctx.mask_side = g_mask_side;
   ctx.xent_partials = xent_partials.get();
   ctx.xent_blocks = xent_blocks(prow);
   ctx.gemm_workspace = gemm_ws.get();
@@ -481,7 +498,7 @@ void GCN::build(const GCNData &data) {
     insert_layer(params.hidden_dims[(size_t)l - 1], params.hidden_dims[(size_t)l],
                  params.dropouts[(size_t)l], l);
   insert_last_layer();
-  if (g_fuse_epilogue && !comm) fuse_epilogues();
+  if ((g_fuse_epilogue & kFuseTails) && !comm) fuse_epilogues();
   if (g_fuse_output && !comm) fuse_output_layer();
   optimizer = Adam(weights, decays, adam_params);
   PGCN_HIP(hipDeviceSynchronize());
@@ -543,7 +560,6 @@ void GCN::insert_first_layer() {
   auto drop = std::make_unique<Dropout>(nullptr, params.dropouts.front(), rngs[0], &ctx);
   const Dropout *dptr = drop.get();
   dropouts_.push_back(dptr);
-  if (feats.dense && feats.maskT) ctx.input_drop = dptr;  // the X-stream path's input mask
   modules.push_back(std::move(drop));
   auto var1 = std::make_shared<Variable>(prow, h, true, round_up4(h));
   variables.push_back(var1);
@@ -751,9 +767,9 @@ void GCN::enqueue_epoch(bool graph) {
 // A replayed epoch must launch exactly what an eager one would: no host-side state may change
 // between epochs.  Excluded: the edge-cut engine (RCCL calls), GraphSum profiling (host
 // events), and train-ahead over dense X without eval_ax (it swaps buffers on the host between
-// eval and the next training forward), mask_side (side stream).
+// eval and the next training forward).
 bool GCN::graph_eligible() const {
-  if (!g_epoch_graph || !warm || comm || ctx.profile || ctx.mask_side) return false;
+  if (!g_epoch_graph || !warm || comm || ctx.profile) return false;
   if (ctx.train_ahead && feats.dense && feats.maskT && !feats.ax) return false;
   return true;
 }

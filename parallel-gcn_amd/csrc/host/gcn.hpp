@@ -56,6 +56,10 @@ class Adam {
   Adam(const std::vector<shared_ptr<Variable>> &weights, const std::vector<bool> &decays,
        const AdamParams &p);
   void step(const Stream &s);
+  // the reference's per-tensor schedule (src/optim.cu:57-95): one step, tensor i on
+  // streams[i], then events[i] recorded there (null: none); the same arithmetic as step()
+  void step_each(const std::vector<hipStream_t> &streams, const std::vector<hipEvent_t> &events);
+  size_t size() const { return vars.size(); }
   // epoch graphs: the same launches reading the step size from table[ctr[0] % cap] on the
   // device (the host counts the step with advance() at every replay)
   void step_graph(const Stream &s, const float *table, const int *ctr, int cap) const;

@@ -108,21 +108,18 @@ DevGraph::DevGraph(int n_rows, int n_cols, const int *indptr, const int *indices
   PGCN_HIP(hipMemset(vals_.get() + nnz_, 0, 64 * sizeof(float)));
 }
 
-int g_graphsum_force_plain = 0;  // diagnostics only (pgcn_debug_set)
-// d = 16 feature tables above these byte counts take the LDS GraphSum ("lds_min_bytes") and,
-// on the plain path, the XCD column blocking ("blocked_min_bytes", DevGraph::kL2Budget: below
-// it one XCD's 4 MB L2 holds the whole table).  The LDS path also wants rows to fill its
-// workgroups (kLdsMinRows).  r02, the edge-cut engine's per-rank graphs of reddit-114M
-// (tools/rank_graphsum.py, 118 k padded rows): 3.7 MB table (4 ranks) LDS 0.123 vs plain
-// 0.249 ms, 1.9 MB (8 ranks) 0.083 vs 0.114 ms; 15 MB (1 rank) 0.33 vs 1.04 ms
+// d = 16 feature tables above this byte count take the LDS GraphSum ("lds_min_kb"; the
+// plain path blocks its columns per XCD above DevGraph::kL2Budget: below it one XCD's 4 MB L2
+// holds the whole table).  The LDS path also wants rows to fill its workgroups (kLdsMinRows).
+// r02, the edge-cut engine's per-rank graphs of reddit-114M (tools/rank_graphsum.py, 118 k
+// padded rows): 3.7 MB table (4 ranks) LDS 0.123 vs plain 0.249 ms, 1.9 MB (8 ranks) 0.083 vs
+// 0.114 ms; 15 MB (1 rank) 0.33 vs 1.04 ms
 long long g_lds_min_bytes = DevGraph::kLdsMinBytes;
-long long g_blocked_min_bytes = (long long)DevGraph::kL2Budget;
 
 int DevGraph::column_blocks(int dim) {
   const int vec = (dim + 3) / 4;
   const double table = (double)n_cols_ * vec * 16.0;
-  if (g_graphsum_force_plain) return 1;
-  return (graphsum_group_lanes(vec) < 64 && table > g_blocked_min_bytes) ? kBlocks : 1;
+  return (graphsum_group_lanes(vec) < 64 && table > kL2Budget) ? kBlocks : 1;
 }
 
 // Cut the columns into kBlocks nnz-balanced ranges.
@@ -343,501 +340,11 @@ void DevGraph::set_scales(std::vector<float> row_scale, std::vector<float> col_s
   lds_.reset();
 }
 
-// rows g (lanes 4g..4g+3) that one ds_read_b128 lane group serves (MI355X_MICROARCH.md §LDS:
-// lanes {0-3,12-15,20-27}, {4-11,16-19,28-31}, {32-35,44-47,52-59}, {36-43,48-51,60-63})
-static const int kLdsLaneGroups[4][4] = {{0, 3, 5, 6}, {1, 2, 4, 7}, {8, 11, 13, 14}, {9, 10, 12, 15}};
-
-int g_graphsum_lds = 1;
-int g_graphsum_lds_wide = 1;  // "graphsum_lds_wide": rows wider than 16 as 16-column LDS passes
-// "graphsum_lds_window": 1 = slots one after another; 2 = two-slot runs (exec-masked; slower on
-// gfx950); 3 = slot pairs interleaved block by block (two blocks of LDS reads in flight; r01:
-// same time as 1 -- the kernel is not bound by per-wave LDS latency);
-// 4 = 8-step blocks; 5 (default) = the sliding-window ring schedule (host/ring.cpp)
-int g_graphsum_lds_window = 5;
-int g_graphsum_lds_order = 1;  // diagnostics ("graphsum_lds_order"): 0 = runs in column order  // diagnostics (pgcn_debug_set "graphsum_lds"): 0 disables the LDS path
-
-// LDS-staged d = 16 schedule (see k_graphsum_lds.hip for the layout it feeds), host side:
-// a pure function of the CSR pattern and the column cuts (tested on the CPU by
-// lds_emulate, which walks it the way the kernel does).
-LdsHost build_lds_host(int n_rows, int n_cols, const std::vector<int> &h_indptr_,
-                       const std::vector<int> &h_indices_, const std::vector<int> &bcut_,
-                       int window) {
-  (void)n_cols;
-  const int n_rows_ = n_rows;
-  const int B = (int)bcut_.size() - 1, SR = LDS_SR, CW = LDS_CW, NS = LDS_SLOTS;
-  PGCN_CHECK(B >= 1 && kCUs % B == 0, PGCN_E_INVALID, "graphsum_lds: column blocks");
-  // slices of each column block
-  std::vector<int> nsl((size_t)B);
-  int t_max = 1;
-  for (int b = 0; b < B; b++) {
-    nsl[(size_t)b] = (bcut_[(size_t)b + 1] - bcut_[(size_t)b] + SR - 1) / SR;
-    t_max = std::max(t_max, nsl[(size_t)b]);
-  }
-  std::vector<int2> slices((size_t)B * t_max, make_int2(0, 0));
-  for (int b = 0; b < B; b++)
-    for (int t = 0; t < nsl[(size_t)b]; t++) {
-      const int c0 = bcut_[(size_t)b] + t * SR;
-      slices[(size_t)b * t_max + t] = make_int2(c0, std::min(SR, bcut_[(size_t)b + 1] - c0));
-    }
-  // rowsets: rows by degree (descending), 16 per rowset, dealt round-robin to batches
-  std::vector<int> order((size_t)n_rows_);
-  std::iota(order.begin(), order.end(), 0);
-  std::stable_sort(order.begin(), order.end(), [&](int a, int c) {
-    return h_indptr_[(size_t)a + 1] - h_indptr_[(size_t)a] > h_indptr_[(size_t)c + 1] - h_indptr_[(size_t)c];
-  });
-  const long long nrs = ((long long)n_rows_ + 15) / 16;
-  const long long cap = (long long)CW * NS;
-  // batches in multiples of kCUs / B: the B x batches workgroups then fill whole rounds of the
-  // 256 CUs (one 156-KB-LDS workgroup per CU)
-  const int per_round = kCUs / B;
-  const int nbat = (int)(((nrs + cap - 1) / cap + per_round - 1) / per_round * per_round);
-  const long long n_wg = (long long)nbat * B;
-  // column-sorted copy of every row (a row's edges inside a slice are then one run)
-  std::vector<int> sidx(h_indices_);
-  parallel_for(n_rows_, [&](long long b0, long long b1) {
-    for (long long i = b0; i < b1; i++)
-      std::sort(sidx.begin() + h_indptr_[(size_t)i], sidx.begin() + h_indptr_[(size_t)i + 1]);
-  });
-  // entry blocks of every (rowset, slice): ceil(max over the rowset's rows of the run / 4)
-  int n_sl = 0;
-  std::vector<int> sl_first((size_t)B + 1, 0);  // global slice ids of block b
-  for (int b = 0; b < B; b++) sl_first[(size_t)b + 1] = sl_first[(size_t)b] + nsl[(size_t)b];
-  n_sl = sl_first[(size_t)B];
-  std::vector<int> sl_start((size_t)n_sl);
-  for (int b = 0; b < B; b++)
-    for (int t = 0; t < nsl[(size_t)b]; t++)
-      sl_start[(size_t)(sl_first[(size_t)b] + t)] = slices[(size_t)b * t_max + t].x;
-  std::vector<unsigned short> rs_blocks((size_t)nrs * n_sl, 0);
-  parallel_for(nrs, [&](long long r0, long long r1) {
-    std::vector<int> mx((size_t)n_sl);
-    for (long long r = r0; r < r1; r++) {
-      std::fill(mx.begin(), mx.end(), 0);
-      for (int g = 0; g < 16; g++) {
-        const long long i = 16 * r + g;
-        if (i >= n_rows_) break;
-        const int row = order[(size_t)i];
-        int s = 0, run = 0;
-        for (int k = h_indptr_[(size_t)row]; k < h_indptr_[(size_t)row + 1]; k++) {
-          const int c = sidx[(size_t)k];
-          int s2 = s;
-          while (s2 + 1 < n_sl && sl_start[(size_t)s2 + 1] <= c) s2++;
-          if (s2 != s) {
-            mx[(size_t)s] = std::max(mx[(size_t)s], run);
-            s = s2;
-            run = 0;
-          }
-          run++;
-        }
-        mx[(size_t)s] = std::max(mx[(size_t)s], run);
-      }
-      for (int s = 0; s < n_sl; s++) rs_blocks[(size_t)r * n_sl + s] = (unsigned short)std::min(65535, (mx[(size_t)s] + 3) / 4);
-    }
-  }, 0, 64);
-  // rowsets dealt round-robin (degree order) to batches; inside a batch each rowset goes to the
-  // wave (with a free slot) whose per-slice loads grow the sum over slices of the per-slice
-  // maximum least -- every slice ends in a workgroup barrier, so the slowest wave of each
-  // slice sets the pace.  Heaviest rowsets first.
-  std::vector<int> rows((size_t)nbat * CW * NS * 16, -1);
-  parallel_for(nbat, [&](long long b0, long long b1) {
-    std::vector<int> load((size_t)CW * n_sl), cur_max((size_t)n_sl);
-    for (long long bat = b0; bat < b1; bat++) {
-      std::vector<long long> mine;
-      for (long long r = bat; r < nrs; r += nbat) mine.push_back(r);
-      std::vector<long long> tot(mine.size(), 0);
-      for (size_t a = 0; a < mine.size(); a++)
-        for (int s = 0; s < n_sl; s++) tot[a] += rs_blocks[(size_t)mine[a] * n_sl + s];
-      std::vector<size_t> idx(mine.size());
-      std::iota(idx.begin(), idx.end(), 0);
-      std::stable_sort(idx.begin(), idx.end(), [&](size_t x, size_t y) { return tot[x] > tot[y]; });
-      std::fill(load.begin(), load.end(), 0);
-      std::fill(cur_max.begin(), cur_max.end(), 0);
-      std::vector<int> used((size_t)CW, 0);
-      for (size_t a : idx) {
-        const unsigned short *x = &rs_blocks[(size_t)mine[a] * n_sl];
-        long long best = -1;
-        int bw = -1;
-        for (int w = 0; w < CW; w++) {
-          if (used[(size_t)w] >= NS) continue;
-          long long inc = 0;
-          const int *lw = &load[(size_t)w * n_sl];
-          for (int s = 0; s < n_sl; s++) {
-            const int nl = lw[s] + x[s];
-            if (nl > cur_max[(size_t)s]) inc += nl - cur_max[(size_t)s];
-          }
-          if (bw < 0 || inc < best || (inc == best && used[(size_t)w] < used[(size_t)bw])) {
-            best = inc;
-            bw = w;
-          }
-        }
-        PGCN_CHECK(bw >= 0, PGCN_E_INVALID, "graphsum_lds: batch over capacity");
-        int *lw = &load[(size_t)bw * n_sl];
-        for (int s = 0; s < n_sl; s++) {
-          lw[s] += x[s];
-          cur_max[(size_t)s] = std::max(cur_max[(size_t)s], lw[s]);
-        }
-        const int j = used[(size_t)bw]++;
-        for (int g = 0; g < 16; g++) {
-          const long long i = 16 * mine[a] + g;
-          rows[(size_t)(((bat * CW + bw) * NS + j) * 16 + g)] = i < n_rows_ ? order[(size_t)i] : -1;
-        }
-      }
-    }
-  }, 0, 1);
-  std::vector<unsigned short> counts((size_t)n_wg * t_max * CW * NS, 0);
-  std::vector<long long> kbs((size_t)n_wg * CW, 0);
-  const bool win2 = window == 2, pair = window == 3;
-  // steps per entry block: 4 (128-B blocks), window 4: 8 (256-B blocks, the kernel runs exact
-  // step counts: the last block of a run takes 1..8 steps)
-  const int SPB = window == 4 ? 8 : 4, BLK = 16 * SPB;
-  // walks (wg, wave): for each slice, each rowset slot, the 16 rows' runs in that slice
-  auto walk = [&](long long wg, int w, unsigned short *out_entries) {
-    const int b = (int)(wg % B), bat = (int)(wg / B);
-    const int *rw = &rows[(size_t)(((long long)bat * CW + w) * NS) * 16];
-    int cur[LDS_SLOTS * 16], end[LDS_SLOTS * 16];
-    for (int k = 0; k < NS * 16; k++) {
-      const int r = rw[k];
-      if (r < 0) {
-        cur[k] = end[k] = 0;
-        continue;
-      }
-      const int *rb = &sidx[(size_t)h_indptr_[(size_t)r]], *re = &sidx[(size_t)h_indptr_[(size_t)r + 1]];
-      cur[k] = (int)(std::lower_bound(rb, re, bcut_[(size_t)b]) - sidx.data());
-      end[k] = h_indptr_[(size_t)r + 1];
-    }
-    long long kb_total = 0;
-    // window 3: a slice's blocks are built per slot, then emitted in slot-pair order
-    std::vector<unsigned short> sb[LDS_SLOTS];
-    int sb_n[LDS_SLOTS];
-    for (int t = 0; t < nsl[(size_t)b]; t++) {
-      const int2 sc = slices[(size_t)b * t_max + t];
-      const int c1 = sc.x + sc.y;
-      const long long kb_slice = kb_total;
-      for (int j = 0; j < NS; j++) {
-        int n[16], m = 0;
-        for (int g = 0; g < 16; g++) {
-          const int k = j * 16 + g;
-          int e = cur[k];
-          while (e < end[k] && sidx[(size_t)e] < c1) e++;
-          n[g] = e - cur[k];
-          m = std::max(m, n[g]);
-        }
-        PGCN_CHECK(m < 65536, PGCN_E_INVALID, "graphsum_lds: slice run too long");
-        counts[(size_t)(((wg * t_max + t) * CW + w) * NS + j)] = (unsigned short)m;
-        const int nkb = (m + SPB - 1) / SPB;
-        unsigned short *slot_out = nullptr;  // this slot's nkb blocks
-        if (out_entries && pair) {
-          sb[j].assign((size_t)nkb * 64, 0);
-          sb_n[j] = nkb;
-          slot_out = sb[j].data();
-        } else if (out_entries) {
-          slot_out = out_entries + kb_total * BLK;
-        }
-        if (slot_out && nkb > 0 && !g_graphsum_lds_order) {
-          for (int kb = 0; kb < nkb; kb++)
-            for (int g = 0; g < 16; g++)
-              for (int u = 0; u < SPB; u++) {
-                const int st = SPB * kb + u, k = j * 16 + g;
-                slot_out[kb * BLK + g * SPB + u] =
-                    (unsigned short)(st < n[g] ? (sidx[(size_t)cur[k] + st] - sc.x) * 64 : SR * 64);
-              }
-        } else if (slot_out && nkb > 0) {
-          // Order each row's run (any fixed order sums the same terms) so that at every step
-          // the 4 rows served by one ds_read_b128 lane group read 4 different bank quarters
-          // (64-B row r occupies quarter r % 4); padding takes a zero row of a free quarter.
-          unsigned short *dst = slot_out;
-          for (int q = 0; q < 4; q++) {
-            const int *grp = kLdsLaneGroups[q];
-            std::vector<int> byres[4][4];  // [member][residue] -> local columns
-            int rem[4];
-            for (int a = 0; a < 4; a++) {
-              const int g = grp[a], k = j * 16 + g;
-              for (int e = 0; e < n[g]; e++) {
-                const int lc = sidx[(size_t)cur[k] + e] - sc.x;
-                byres[a][lc & 3].push_back(lc);
-              }
-              rem[a] = n[g];
-            }
-            for (int st = 0; st < SPB * nkb; st++) {
-              int used = 0, ord[4] = {0, 1, 2, 3};
-              // rows with no slack left choose first, then rows with more edges left
-              std::sort(ord, ord + 4, [&](int x, int y) {
-                const bool fx = rem[x] >= m - st, fy = rem[y] >= m - st;
-                if (fx != fy) return fx;
-                return rem[x] > rem[y];
-              });
-              for (int oi = 0; oi < 4; oi++) {
-                const int a = ord[oi];
-                int pick = -1;
-                for (int r = 0; r < 4; r++)
-                  if (!(used >> r & 1) && !byres[a][r].empty() &&
-                      (pick < 0 || byres[a][r].size() > byres[a][pick].size()))
-                    pick = r;
-                const bool must = rem[a] > 0 && rem[a] >= m - st;
-                if (pick < 0 && must)  // forced conflict: largest residue list
-                  for (int r = 0; r < 4; r++)
-                    if (!byres[a][r].empty() && (pick < 0 || byres[a][r].size() > byres[a][pick].size()))
-                      pick = r;
-                int val;
-                if (pick >= 0 && st < m) {
-                  val = byres[a][pick].back() * 64;
-                  byres[a][pick].pop_back();
-                  rem[a]--;
-                  used |= 1 << pick;
-                } else {
-                  int r = 0;
-                  while (used >> r & 1) r++;
-                  val = (SR + r) * 64;
-                  used |= 1 << r;
-                }
-                dst[(st / SPB) * BLK + grp[a] * SPB + (st % SPB)] = (unsigned short)val;
-              }
-            }
-          }
-        }
-        for (int g = 0; g < 16; g++) cur[j * 16 + g] += n[g];
-        kb_total += nkb;
-      }
-      if (out_entries && pair) {  // slots 2p, 2p+1: A0 B0 A1 B1 ..., then the longer's rest
-        unsigned short *o = out_entries + kb_slice * 64;
-        auto put = [&](int j, int i) {
-          std::copy(sb[j].begin() + (size_t)i * 64, sb[j].begin() + (size_t)(i + 1) * 64, o);
-          o += 64;
-        };
-        for (int p = 0; p < NS / 2; p++) {
-          const int a = 2 * p, c = 2 * p + 1, both = std::min(sb_n[a], sb_n[c]);
-          for (int i = 0; i < both; i++) {
-            put(a, i);
-            put(c, i);
-          }
-          for (int i = both; i < sb_n[a]; i++) put(a, i);
-          for (int i = both; i < sb_n[c]; i++) put(c, i);
-        }
-        PGCN_CHECK(o == out_entries + kb_total * 64, PGCN_E_INVALID, "graphsum_lds: pair order");
-      }
-    }
-    return kb_total;
-  };
-  // Window 2: per slice the wave runs its 16 slots as runs J = 0..15 in which every lane
-  // group takes an edge of slot J or, once its slot-J edges are done, of slot J+1 (exec
-  // masks pick the accumulator); run J ends when slot J is drained everywhere.  The cost per
-  // slot is then about the max over groups of the per-group total instead of the sum over
-  // slots of per-slot maxima (the lockstep padding of window 1).
-  auto walk2 = [&](long long wg, int w, unsigned short *out_entries, uint64_t *out_masks) {
-    const int b = (int)(wg % B), bat = (int)(wg / B);
-    const int *rw = &rows[(size_t)(((long long)bat * CW + w) * NS) * 16];
-    int cur[LDS_SLOTS * 16], end[LDS_SLOTS * 16];
-    for (int k = 0; k < NS * 16; k++) {
-      const int r = rw[k];
-      if (r < 0) {
-        cur[k] = end[k] = 0;
-        continue;
-      }
-      const int *rb = &sidx[(size_t)h_indptr_[(size_t)r]], *re = &sidx[(size_t)h_indptr_[(size_t)r + 1]];
-      cur[k] = (int)(std::lower_bound(rb, re, bcut_[(size_t)b]) - sidx.data());
-      end[k] = h_indptr_[(size_t)r + 1];
-    }
-    // byres[j][g][res]: slice-local rows of slot j, group g with row % 4 == res
-    std::vector<std::vector<int>> byres((size_t)NS * 16 * 4);
-    std::vector<int> cnt((size_t)NS * 16);
-    auto lst = [&](int j, int g, int r) -> std::vector<int> & { return byres[((size_t)j * 16 + g) * 4 + r]; };
-    long long kb_total = 0;
-    for (int t = 0; t < nsl[(size_t)b]; t++) {
-      const int2 sc = slices[(size_t)b * t_max + t];
-      const int c1 = sc.x + sc.y;
-      for (int j = 0; j < NS; j++)
-        for (int g = 0; g < 16; g++) {
-          const int k = j * 16 + g;
-          int e = cur[k];
-          for (int r = 0; r < 4; r++) lst(j, g, r).clear();
-          while (e < end[k] && sidx[(size_t)e] < c1) {
-            const int lr = sidx[(size_t)e] - sc.x;
-            lst(j, g, lr & 3).push_back(lr);
-            e++;
-          }
-          cnt[(size_t)k] = e - cur[k];
-          cur[k] = e;
-        }
-      auto drained = [&](int j) {
-        for (int g = 0; g < 16; g++)
-          if (cnt[(size_t)j * 16 + g]) return false;
-        return true;
-      };
-      int nblk[LDS_SLOTS] = {0};
-      int J = 0;
-      while (J < NS && drained(J)) J++;
-      while (J < NS) {
-        for (int st = 0; st < 4; st++) {
-          uint64_t m = 0;
-          for (int q = 0; q < 4; q++) {
-            const int *grp = kLdsLaneGroups[q];
-            int ord[4] = {0, 1, 2, 3};
-            std::sort(ord, ord + 4, [&](int x, int y) {
-              return cnt[(size_t)J * 16 + grp[x]] > cnt[(size_t)J * 16 + grp[y]];
-            });
-            int used = 0;
-            for (int oi = 0; oi < 4; oi++) {
-              const int g = grp[ord[oi]];
-              int slot = -1, res = -1;
-              for (int jj = J; jj <= std::min(J + 1, NS - 1) && slot < 0; jj++) {
-                if (!cnt[(size_t)jj * 16 + g]) continue;
-                for (int r = 0; r < 4; r++)  // a free bank quarter, the fullest list
-                  if (!(used >> r & 1) && !lst(jj, g, r).empty() &&
-                      (res < 0 || lst(jj, g, r).size() > lst(jj, g, res).size()))
-                    res = r;
-                if (res < 0)  // forced conflict: the fullest list
-                  for (int r = 0; r < 4; r++)
-                    if (!lst(jj, g, r).empty() && (res < 0 || lst(jj, g, r).size() > lst(jj, g, res).size()))
-                      res = r;
-                slot = jj;
-              }
-              int val;
-              if (slot >= 0) {
-                val = lst(slot, g, res).back() * 64;
-                lst(slot, g, res).pop_back();
-                cnt[(size_t)slot * 16 + g]--;
-                if (slot != J) m |= 0xfull << (4 * g);
-              } else {  // padding: a zero row of a free quarter
-                res = 0;
-                while (used >> res & 1) res++;
-                val = (SR + res) * 64;
-              }
-              used |= 1 << res;
-              if (out_entries) out_entries[(size_t)kb_total * 64 + g * 4 + st] = (unsigned short)val;
-            }
-          }
-          if (out_masks) out_masks[(size_t)kb_total * 4 + st] = m;
-        }
-        nblk[J]++;
-        kb_total++;
-        while (J < NS && drained(J)) J++;
-      }
-      for (int j = 0; j < NS; j++) {
-        PGCN_CHECK(nblk[j] < 65536, PGCN_E_INVALID, "graphsum_lds: run too long");
-        counts[(size_t)(((wg * t_max + t) * CW + w) * NS + j)] = (unsigned short)nblk[j];
-      }
-    }
-    return kb_total;
-  };
-  parallel_for(n_wg * CW, [&](long long a, long long e) {
-    for (long long x = a; x < e; x++)
-      kbs[(size_t)x] = win2 ? walk2(x / CW, (int)(x % CW), nullptr, nullptr)
-                            : walk(x / CW, (int)(x % CW), nullptr);
-  }, 0, 64);
-  std::vector<long long> off((size_t)n_wg * CW + 1, 0);
-  for (size_t x = 0; x < kbs.size(); x++) off[x + 1] = off[x] + kbs[x];
-  const long long total_kb = off.back();
-  std::vector<unsigned short> ent((size_t)std::max<long long>(total_kb, 1) * BLK, 0);
-  std::vector<uint64_t> msk(win2 ? (size_t)std::max<long long>(total_kb, 1) * 4 : 0, 0);
-  parallel_for(n_wg * CW, [&](long long a, long long e) {
-    for (long long x = a; x < e; x++) {
-      if (win2)
-        walk2(x / CW, (int)(x % CW), &ent[(size_t)off[(size_t)x] * 64], &msk[(size_t)off[(size_t)x] * 4]);
-      else
-        walk(x / CW, (int)(x % CW), &ent[(size_t)off[(size_t)x] * BLK]);
-    }
-  }, 0, 64);
-  LdsHost h;
-  h.n_blocks = B;
-  h.window = win2 ? 2 : pair ? 3 : window == 4 ? 4 : 1;
-  h.n_batches = nbat;
-  h.t_max = t_max;
-  h.nsl = std::move(nsl);
-  h.slices = std::move(slices);
-  h.rows = std::move(rows);
-  h.counts = std::move(counts);
-  h.wave_off = std::move(off);
-  h.entries = std::move(ent);
-  h.masks = std::move(msk);
-  return h;
-}
-
-
-// Walks a schedule exactly as k_graphsum_lds consumes it (entry blocks in wave order, runs
-// per slice and slot, window-2 masks, zero rows) and adds each row's sum of in[col] into
-// out[row]; throws on any inconsistency the kernel would turn into a wrong sum.
-void lds_emulate(const LdsHost &h, int n_rows, const float *in, double *out) {
-  if (h.window == kRingWindow) {
-    ring_emulate(h, n_rows, in, out);
-    return;
-  }
-  const int B = h.n_blocks, CW = LDS_CW, NS = LDS_SLOTS;
-  const int SPB = h.window == 4 ? 8 : 4, BLK = 16 * SPB;
-  const long long n_wg = (long long)h.n_batches * B;
-  std::vector<double> acc((size_t)NS * 16);
-  for (long long wg = 0; wg < n_wg; wg++) {
-    const int b = (int)(wg % B), bat = (int)(wg / B);
-    for (int w = 0; w < CW; w++) {
-      long long kb = h.wave_off[(size_t)(wg * CW + w)];
-      std::fill(acc.begin(), acc.end(), 0.0);
-      for (int t = 0; t < h.nsl[(size_t)b]; t++) {
-        const int2 sc = h.slices[(size_t)b * h.t_max + t];
-        // the order the kernel takes blocks in: (slot, block index within the slot)
-        std::vector<std::pair<int, int>> seq;
-        const unsigned short *cn = &h.counts[(size_t)(((wg * h.t_max + t) * CW + w) * NS)];
-        if (h.window == 3) {
-          for (int p = 0; p < NS / 2; p++) {
-            const int na = (cn[2 * p] + 3) / 4, nc = (cn[2 * p + 1] + 3) / 4;
-            for (int i = 0; i < std::min(na, nc); i++) {
-              seq.push_back({2 * p, i});
-              seq.push_back({2 * p + 1, i});
-            }
-            for (int i = std::min(na, nc); i < na; i++) seq.push_back({2 * p, i});
-            for (int i = std::min(na, nc); i < nc; i++) seq.push_back({2 * p + 1, i});
-          }
-        } else {
-          for (int j = 0; j < NS; j++) {
-            const int nblk = h.window == 2 ? cn[j] : (cn[j] + SPB - 1) / SPB;
-            for (int k = 0; k < nblk; k++) seq.push_back({j, k});
-          }
-        }
-        for (const auto &jk : seq) {
-          const int j = jk.first, k = jk.second, n = cn[j];
-          {
-            for (int st = 0; st < SPB; st++) {
-              const uint64_t m = h.window == 2 ? h.masks[(size_t)kb * 4 + st] : 0;
-              for (int g = 0; g < 16; g++) {
-                const int e = h.entries[(size_t)kb * BLK + g * SPB + st];
-                PGCN_CHECK(e % 64 == 0, PGCN_E_INVALID, "lds schedule: entry not a row offset");
-                const int row = e / 64;
-                // steps past the run's count are padding (zero rows) in every window
-                PGCN_CHECK(h.window == 2 || SPB * k + st < n || row >= LDS_SR, PGCN_E_INVALID,
-                           "lds schedule: edge past the run's step count");
-                PGCN_CHECK(row >= LDS_SR || row < sc.y, PGCN_E_INVALID,
-                           "lds schedule: entry past the slice");
-                const unsigned q = (unsigned)(m >> (4 * g)) & 0xfu;
-                PGCN_CHECK(q == 0 || q == 0xfu, PGCN_E_INVALID, "lds schedule: split lane group");
-                const int slot = q ? j + 1 : j;
-                PGCN_CHECK(slot < NS, PGCN_E_INVALID, "lds schedule: mask past the last slot");
-                if (row < LDS_SR) acc[(size_t)slot * 16 + g] += (double)in[sc.x + row];
-              }
-            }
-          }
-          kb++;
-        }
-      }
-      PGCN_CHECK(kb == h.wave_off[(size_t)(wg * CW + w) + 1], PGCN_E_INVALID,
-                 "lds schedule: wave stream length");
-      for (int j = 0; j < NS; j++)
-        for (int g = 0; g < 16; g++) {
-          const int r = h.rows[(size_t)(((long long)bat * CW + w) * NS + j) * 16 + g];
-          if (r >= 0) {
-            PGCN_CHECK(r < n_rows, PGCN_E_INVALID, "lds schedule: row id");
-            out[r] += acc[(size_t)j * 16 + g];
-          } else {
-            PGCN_CHECK(acc[(size_t)j * 16 + g] == 0.0, PGCN_E_INVALID,
-                       "lds schedule: edges on an empty slot");
-          }
-        }
-    }
-  }
-}
-
 // "lds_blocks": column blocks of the LDS schedule; 0 = by shape (r01, reddit): 4 blocks when the
 // graph has about as many rows as columns (the full graph and its column subsets: one round of
 // 256 workgroups, half the partials; the same kernel time, combine 18 -> 11 us), 8 for a small
 // row subset (its 256 workgroups then stream half the table each: val rows 0.11 vs 0.22 ms)
 int g_lds_blocks = 0;
-int g_lds_blocks_subset = 0;  // "lds_blocks_subset": override for large row subsets (diagnostics)
 
 int lds_blocks(int n_rows, int n_cols) {
   if (g_lds_blocks) return g_lds_blocks;
@@ -858,7 +365,6 @@ int lds_blocks(int n_rows, int n_cols) {
   const long long nb = std::max(1LL, (nrs + cap - 1) / cap);
   int B = 8;
   while (B < 32 && nb * B * 2 <= kCUs) B *= 2;
-  if (B == 8 && g_lds_blocks_subset) return g_lds_blocks_subset;  // diagnostics
   return B;
 }
 
@@ -880,24 +386,12 @@ std::vector<int> column_cuts(int n_cols, const std::vector<int> &indices, int n_
 }
 
 void DevGraph::build_lds() {
-  const bool ring = g_graphsum_lds_window == kRingWindow;
-  if (lds_cut_.empty() || ring != lds_ring_cut_) {
-    lds_cut_ = ring ? ring_cuts(n_cols_, h_indices_, lds_blocks(n_rows_, n_cols_))
-                    : column_cuts(n_cols_, h_indices_, lds_blocks(n_rows_, n_cols_));
-    lds_ring_cut_ = ring;
-  }
+  if (lds_cut_.empty()) lds_cut_ = ring_cuts(n_cols_, h_indices_, lds_blocks(n_rows_, n_cols_));
   auto L = std::make_unique<LdsSched>();
-  LdsHost h = ring ? build_ring_host(n_rows_, n_cols_, h_indptr_, h_indices_, lds_cut_)
-                   : build_lds_host(n_rows_, n_cols_, h_indptr_, h_indices_, lds_cut_,
-                                    g_graphsum_lds_window);
-  const bool win2 = h.window == 2;
+  LdsHost h = build_ring_host(n_rows_, n_cols_, h_indptr_, h_indices_, lds_cut_);
   // + 2 KB slack: ring refills read whole 512-B chunks (up to 3) past a wave's last block
-  L->entries.allocate(h.entries.size() / 4 + 256);  // 2 KB: ring refills run 3 chunks past
+  L->entries.allocate(h.entries.size() / 4 + 256);
   L->entries.upload(reinterpret_cast<const uint2 *>(h.entries.data()), h.entries.size() / 4);
-  if (win2) {  // + 64 B of slack: the mask loads touch the line after the last block's
-    L->masks.allocate(h.masks.size() + 8);
-    L->masks.upload(h.masks);
-  }
   L->wave_off.allocate(h.wave_off.size());
   L->wave_off.upload(h.wave_off);
   L->counts.allocate(h.counts.size());
@@ -908,19 +402,12 @@ void DevGraph::build_lds() {
   L->n_slices.upload(h.nsl);
   L->rows.allocate(h.rows.size());
   L->rows.upload(h.rows);
-  if (ring) {
-    L->arrive.allocate((size_t)h.n_batches);
-    L->arrive.zero();
-    L->s.arrive = L->arrive.get();
-  }
   L->row_scale.allocate(h_row_scale_.size());
   L->row_scale.upload(h_row_scale_);
   L->col_scale.allocate(h_col_scale_.size());
   L->col_scale.upload(h_col_scale_);
-  // + LDS_ROWS rows: slice copies run whole pieces past the last column (never read)
-  // ring: whole slices of RING_SR rows (the loader copies 8-KB plane pieces)
-  L->scratch.allocate(ring ? (size_t)ceil_div(n_cols_, RING_SR) * RING_SR * 16
-                           : ((size_t)n_cols_ + LDS_ROWS) * 16 + 64);
+  // whole slices of RING_SR rows (the loader copies 8-KB plane pieces)
+  L->scratch.allocate((size_t)ceil_div(n_cols_, RING_SR) * RING_SR * 16);
   L->partial.allocate((size_t)h.n_blocks * n_rows_ * 16);
   L->s.n_blocks = h.n_blocks;
   L->s.n_rows = n_rows_;
@@ -935,8 +422,6 @@ void DevGraph::build_lds() {
   L->s.rows = L->rows.get();
   L->s.row_scale = L->row_scale.get();
   L->s.col_scale = L->col_scale.get();
-  L->s.window = h.window;
-  L->s.masks = win2 ? L->masks.get() : nullptr;
   lds_ = std::move(L);
 }
 
@@ -945,17 +430,9 @@ void DevGraph::prepare(int dim) {
 }
 
 bool DevGraph::uses_lds(int dim) const {
-  return (dim == 16 || (dim > 16 && g_graphsum_lds_wide)) && g_graphsum_lds &&
-         !h_row_scale_.empty() && !g_graphsum_force_plain &&
-         (double)n_cols_ * 64.0 > (double)g_lds_min_bytes && n_rows_ >= kLdsMinRows;
+  return dim >= 16 && !h_row_scale_.empty() && (double)n_cols_ * 64.0 > (double)g_lds_min_bytes &&
+         n_rows_ >= kLdsMinRows;
 }
-
-// "graphsum_ring_wide": rows wider than 16 on the ring schedule take one prescale and one
-// combine launch for all their 16-column passes (0: a prescale + ring + combine per pass)
-// r02: correct and slower on the 4-layer hidden-128 reddit model (1.677 vs 1.594 ms per call:
-// the 8 passes' partials, 480 MB, no longer stay in the Infinity Cache between a pass's ring
-// launch and its combine), so off; the per-pass combine carries the epilogue instead
-int g_graphsum_ring_wide = 0;
 
 bool DevGraph::epilogue_ok(int dim, int ld_in, int ld_out) const {
   (void)ld_in;
@@ -967,9 +444,8 @@ bool DevGraph::epilogue_ok(int dim, int ld_in, int ld_out) const {
 }
 
 float *DevGraph::ring_table(int dim, const float **next_scale) {
-  if (dim > 16 || !uses_lds(dim) || col_map_ || g_graphsum_lds_window != kRingWindow) return nullptr;
+  if (dim > 16 || !uses_lds(dim) || col_map_) return nullptr;
   if (!lds_) build_lds();
-  if (lds_->s.window != kRingWindow) return nullptr;
   *next_scale = lds_->s.col_scale;
   return lds_->scratch.get();
 }
@@ -989,29 +465,14 @@ void DevGraph::graphsum(const float *in, int ld_in, float *out, int ld_out, int 
     // d = 128 on reddit: 8 passes ~2.7 ms against ~7 ms for the gather kernel, whose 512-B
     // rows come from the Infinity Cache at ~7.7 TB/s
     const int ldm = std::min(ld_in, ld_out);
-    PGCN_CHECK(!prestaged || (dim <= 16 && lds_->s.window == kRingWindow && !col_map),
-               PGCN_E_INVALID, "graphsum: prestaged input on a path without a ring table");
-    if (dim > 16 && lds_->s.window == kRingWindow && g_graphsum_ring_wide) {
-      const int n_pass = (dim + 15) / 16;
-      const long long tf = (long long)lds_->scratch.size(), pf = (long long)lds_->partial.size();
-      if ((long long)lds_->wide_tables.size() < n_pass * tf) {
-        lds_->wide_tables.allocate((size_t)(n_pass * tf));
-        lds_->wide_partials.allocate((size_t)(n_pass * pf));
-      }
-      launch_graphsum_ring_wide(lds_->s, in, ld_in, out, ld_out, dim, lds_->wide_tables.get(), tf,
-                                lds_->wide_partials.get(), pf, s, col_map, epi);
-      return;
-    }
+    PGCN_CHECK(!prestaged || (dim <= 16 && !col_map), PGCN_E_INVALID,
+               "graphsum: prestaged input on a path without a ring table");
     for (int c0 = 0; c0 < dim; c0 += 16) {
       const int c = std::min(c0, ldm - 16);
       GsEpilogue ep = epi ? *epi : GsEpilogue{};
       ep.col0 = c;
-      if (lds_->s.window == kRingWindow)
-        launch_graphsum_ring(lds_->s, in + c, ld_in, out + c, ld_out, lds_->scratch.get(),
-                             lds_->partial.get(), s, col_map, &ep, prestaged);
-      else
-        launch_graphsum_lds(lds_->s, in + c, ld_in, out + c, ld_out, lds_->scratch.get(),
-                            lds_->partial.get(), s, col_map, &ep);
+      launch_graphsum_ring(lds_->s, in + c, ld_in, out + c, ld_out, lds_->scratch.get(),
+                           lds_->partial.get(), s, col_map, &ep, prestaged);
     }
     return;
   }

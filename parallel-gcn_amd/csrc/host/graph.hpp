@@ -40,28 +40,24 @@ bool csr_symmetric(int n, const int *indptr, const int *indices);
 // s[i] = 1/sqrt(deg_i) with deg = row length of the (symmetric) CSR: Â = D^-1/2 A D^-1/2.
 std::vector<float> degree_scales(int n, const int *indptr);
 
-// Host image of the d = 16 LDS schedule (k_graphsum_lds.hip), before upload.
+// Host image of the d = 16 LDS ring schedule (k_graphsum_ring.hip), before upload.
 struct LdsHost {
-  int window = 1, n_batches = 0, t_max = 0, n_blocks = kGraphBlocks;
+  int n_batches = 0, t_max = 0, n_blocks = 4;
   std::vector<int> nsl;                 // slices per column block
   std::vector<int2> slices;             // [block][t_max] {first column, rows}
-  std::vector<int> rows;                // [batch][LDS_CW][LDS_SLOTS][16]
+  std::vector<int> rows;                // [batch][LDS_CW][LDS_SLOTS][16] row | spread
   std::vector<unsigned short> counts;   // [wg][t_max][LDS_CW][LDS_SLOTS]
   std::vector<long long> wave_off;      // [wg*LDS_CW + 1] entry-block offsets
-  std::vector<unsigned short> entries;  // [kb][16 groups][4 steps] byte offsets
-  std::vector<uint64_t> masks;          // window 2: [kb][4 steps] lane masks
+  std::vector<unsigned short> entries;  // [kb][16 groups][4 steps] ring-row byte offsets
 };
 // nnz-balanced column cuts (kGraphBlocks + 1 boundaries)
 std::vector<int> column_cuts(int n_cols, const std::vector<int> &indices,
                              int n_blocks = kGraphBlocks);
-// column blocks of the LDS GraphSum schedule of an n_rows x n_cols graph (XCD-affine: 4 or 8)
+// column blocks of the LDS GraphSum schedule of an n_rows x n_cols graph (XCD-affine)
 int lds_blocks(int n_rows, int n_cols);
-LdsHost build_lds_host(int n_rows, int n_cols, const std::vector<int> &indptr,
-                       const std::vector<int> &indices, const std::vector<int> &bcut, int window);
-// CPU walk of the schedule as the kernel consumes it: out[row] += sum of in[col] (throws on
-// an inconsistent schedule)
-void lds_emulate(const LdsHost &h, int n_rows, const float *in, double *out);
-// ring schedule (host/ring.cpp): block cuts on RING_SR multiples, the schedule, its emulation
+// ring schedule (host/ring.cpp): block cuts on RING_SR multiples, the schedule, and its CPU
+// walk as the kernel consumes it: out[row] += sum of in[col] (throws on an inconsistent
+// schedule)
 std::vector<int> ring_cuts(int n_cols, const std::vector<int> &indices, int n_blocks);
 LdsHost build_ring_host(int n_rows, int n_cols, const std::vector<int> &indptr,
                         const std::vector<int> &indices, const std::vector<int> &bcut);
@@ -86,7 +82,7 @@ class DevGraph {
   float *ring_table(int dim, const float **next_scale);
   // graphsum() of this width can take an epilogue (one pass over the columns)
   bool epilogue_ok(int dim, int ld_in, int ld_out) const;
-  // graphsum() of this width runs the LDS-staged kernel (k_graphsum_lds)
+  // graphsum() of this width runs the LDS ring kernel (k_graphsum_ring)
   bool uses_lds(int dim) const;
   // builds the schedule a graphsum() of this width will use now (host work, kept out of timed
   // device regions)
@@ -96,7 +92,7 @@ class DevGraph {
   // schedule statistics (for tests / reports)
   int column_blocks(int dim);
 
-  // Enables the d = 16 LDS path (k_graphsum_lds): out_i = row_scale_i * sum_j col_scale_j
+  // Enables the d = 16 LDS path (k_graphsum_ring): out_i = row_scale_i * sum_j col_scale_j
   // in_j over the CSR pattern, i.e. vals_ij = row_scale_i * col_scale_j.
   void set_scales(std::vector<float> row_scale, std::vector<float> col_scale);
   // The rows `rows` (ascending) of this CSR as a graph of its own: same columns, values and
@@ -126,13 +122,11 @@ class DevGraph {
   struct LdsSched {
     LdsSchedule s;
     DeviceBuffer<uint2> entries;
-    DeviceBuffer<uint64_t> masks;
     DeviceBuffer<long long> wave_off;
     DeviceBuffer<unsigned short> counts;
     DeviceBuffer<int2> slices;
-    DeviceBuffer<int> n_slices, rows, arrive;
+    DeviceBuffer<int> n_slices, rows;
     DeviceBuffer<float> row_scale, col_scale, scratch, partial;
-    DeviceBuffer<float> wide_tables, wide_partials;  // rows wider than 16: one per pass
   };
   std::unique_ptr<LdsSched> lds_;
   std::vector<float> h_row_scale_, h_col_scale_;
@@ -149,7 +143,6 @@ class DevGraph {
   bool blocked_built_ = false;
   std::vector<int> bcut_;                 // kBlocks + 1 column boundaries
   std::vector<int> lds_cut_;              // LDS schedule: lds_blocks() + 1 boundaries
-  bool lds_ring_cut_ = false;             // lds_cut_ on RING_SR multiples (ring schedule)
   std::vector<long long> bseg_;           // (kBlocks) x (n_rows + 1) segment offsets
   long long bnnz_ = 0;                    // blocked slots incl. padding
   DeviceBuffer<int> bindices_;

@@ -134,28 +134,17 @@ SparseMatmul::SparseMatmul(const DevFeatures *x_, shared_ptr<Variable> b_,
                            shared_ptr<Variable> c_, const Dropout *drop_, ModuleContext *ctx_)
     : x(x_), b(std::move(b_)), c(std::move(c_)), drop(drop_), ctx(ctx_) {}
 
-// "xstream_epilogue": the first layer's X-stream product also applies the ReLU / writes the
-// ring table that the modules after it would launch for (bit-identical)
-int g_xstream_epilogue = 1;
-
 void SparseMatmul::forward(bool training, const Stream &s) const {
   last_training = training;
   const uint64_t *mask = training ? drop->state().mask.get() : nullptr;
   const long long base = drop->state().mask_base;
   const float scale = drop->scale();
   if (!training && x->ax && eval_out) {  // eval_ax: (Â X) W1 straight into the GraphSum's output
-    if (ctx->train_ahead && ctx->mask_side == 2 && ctx->side_stream && x->maskT &&
-        !drop->drawn_ahead()) {
-      // the next training forward's input mask, drawn on the side stream beside this pass
-      ctx->tn_start.record(s.get());
-      ctx->tn_start.wait_on(ctx->side_stream);
-      drop->draw_ahead(ctx->side_stream, &ctx->mask_ready);
-    }
     if (xstream_ok(b->cols, x->cols)) {
       // eval: out = relu(Â X W1) (GraphSum, then its fused ReLU; the Dropout after it is the
       // identity in eval), which the reassociated output layer's GraphSum reads next
       XsEpilogue e;
-      if (g_xstream_epilogue && consumer && consumer->fwd_relu) {
+      if ((g_fuse_epilogue & kFuseXstream) && consumer && consumer->fwd_relu) {
         e.relu = 1;
         consumer->fwd_relu->skip_forward = true;
         if (consumer->fwd_next)
@@ -198,7 +187,7 @@ void SparseMatmul::forward(bool training, const Stream &s) const {
   if (x->dense && x->maskT) {  // X-stream kernels (N <= 16, K <= 640)
     if (mask) launch_mask_nibbles(mask, base, x->cols, x->rows, x->cols, x->maskT.get(), s.get());
     XsEpilogue e;  // the first GraphSum's prescaled input, written beside c
-    if (g_xstream_epilogue && consumer && (training || !eval_out)) {
+    if ((g_fuse_epilogue & kFuseXstream) && consumer && (training || !eval_out)) {
       e.next_table = consumer->claim_forward_table(x->rows, c->ld, &e.next_scale);
       e.next_sr = RING_SR;
     }
@@ -221,14 +210,6 @@ void SparseMatmul::backward(const Stream &s) const {
   const float scale = drop->scale();
   MmProfile prof(ctx, s.get(), x->dense ? 2.0 * x->rows * b->cols * x->cols : 0.0);
   if (x->dense && x->maskT) {  // the nibble mask of the last training forward
-    if (ctx->train_ahead && ctx->mask_side == 1 && ctx->side_stream && !drop->drawn_ahead()) {
-      // the next epoch's input mask, drawn on the side stream while this pass streams X
-      // (maskT, which this pass reads, is rebuilt from it only by the next eval / training
-      // forward on this stream)
-      ctx->tn_start.record(s.get());
-      ctx->tn_start.wait_on(ctx->side_stream);
-      drop->draw_ahead(ctx->side_stream, &ctx->mask_ready);
-    }
     launch_xstream_tn(x->rows, b->cols, x->cols, x->x.get(), x->ldx, c->dev_grad.get(), c->ld,
                       b->dev_grad.get(), b->ld, mask ? x->maskT.get() : nullptr, scale,
                       ctx->gemm_workspace, s.get());
@@ -261,9 +242,6 @@ GraphSum::GraphSum(shared_ptr<Variable> in_, shared_ptr<Variable> out_, DevGraph
   }
 }
 
-// "graphsum_prestage": a fused epilogue also writes the next GraphSum's prescaled input
-int g_graphsum_prestage = 1;
-
 DevGraph *GraphSum::forward_graph() const {
   if (ctx->comm) return nullptr;
   return last_layer && ctx->split_graph ? ctx->split_graph : graph;
@@ -276,7 +254,7 @@ DevGraph *GraphSum::backward_graph() const {
 
 float4 *GraphSum::claim_forward_table(int rows, int ld, const float **scale) const {
   DevGraph *g = forward_graph();
-  if (!g || !g_graphsum_prestage || dim != 16 || in->ld != 16 || ld != 16 || g->cols() != rows)
+  if (!g || !(g_fuse_epilogue & kFusePrestage) || dim != 16 || in->ld != 16 || ld != 16 || g->cols() != rows)
     return nullptr;
   float *t = g->ring_table(dim, scale);
   if (!t) return nullptr;
@@ -285,7 +263,7 @@ float4 *GraphSum::claim_forward_table(int rows, int ld, const float **scale) con
 }
 
 void GraphSum::stage_next(GsEpilogue &e, GraphSum *next, DevGraph *ng, bool fwd) const {
-  if (!next || !ng || !g_graphsum_prestage) return;
+  if (!next || !ng || !(g_fuse_epilogue & kFusePrestage)) return;
   const float *sc = nullptr;
   float *t = ng->ring_table(next->dim, &sc);
   if (!t) return;
@@ -502,19 +480,21 @@ Matmul::Matmul(shared_ptr<Variable> a_, shared_ptr<Variable> b_, shared_ptr<Vari
 
 void Matmul::forward(bool training, const Stream &s) const {
   if (fused_forward && !(last_layer && ctx->compact_n)) return;  // CrossEntropyLoss::forward
-  if (last_layer && !training && ctx->mask_side == 3 && ctx->train_ahead && ctx->side_stream &&
-      ctx->input_drop && !ctx->input_drop->drawn_ahead()) {
-    // the next training forward's input mask, drawn on the side stream beside this layer's
-    // product and the loss (short HBM-bound kernels with room beside them on every CU)
-    ctx->tn_start.record(s.get());
-    ctx->tn_start.wait_on(ctx->side_stream);
-    ctx->input_drop->draw_ahead(ctx->side_stream, &ctx->mask_ready);
-  }
   const bool cmp = last_layer && ctx->compact_n;  // compact output layer: the split's rows
   const Variable &A = cmp ? *ctx->compact_z : *a, &C = cmp ? *ctx->compact_out : *c;
   MmProfile prof(ctx, s.get(), 2.0 * (cmp ? ctx->compact_n : m) * p * n);
   launch_gemm_nn(cmp ? ctx->compact_n : m, p, n, A.dev_data.get(), A.ld, b->dev_data.get(), b->ld,
                  0, C.dev_data.get(), C.ld, nullptr, 0, 0, 1.0f, s.get());
+}
+
+void Matmul::backward_input(const Stream &s) const {
+  launch_gemm_nn(m, n, p, c->dev_grad.get(), c->ld, b->dev_data.get(), b->ld, 1, a->dev_grad.get(),
+                 a->ld, nullptr, 0, 0, 1.0f, s.get());
+}
+
+void Matmul::backward_weight(hipStream_t s, void *ws) const {
+  launch_gemm_tn(m, p, n, a->dev_data.get(), a->ld, c->dev_grad.get(), c->ld, b->dev_grad.get(),
+                 b->ld, nullptr, 0, 0, 1.0f, ws, s);
 }
 
 void Matmul::backward(const Stream &s) const {
@@ -525,7 +505,8 @@ void Matmul::backward(const Stream &s) const {
   const Variable &A = cmp ? *ctx->compact_z : *a, &C = cmp ? *ctx->compact_out : *c;
   const int rows = cmp ? ctx->compact_n : m;
   const bool side = ctx->mm_side && ctx->side_stream && ctx->gemm_workspace_side && !ctx->profile;
-  MmProfile prof(ctx, s.get(), 2.0 * 2.0 * rows * p * n);
+  // (the contractions the loss kernel did are profiled there; a side-stream b.grad is not)
+  MmProfile prof(ctx, s.get(), 2.0 * rows * p * n * ((a_done ? 0 : 1) + (side || b_done ? 0 : 1)));
   if (side) {
     // b.grad = a^T * c.grad on the side stream, from here (a.data and c.grad are final; nothing
     // later in the backward pass writes them), joined before the optimizer (GCN)
@@ -552,23 +533,24 @@ CrossEntropyLoss::CrossEntropyLoss(shared_ptr<Variable> logits_, int num_classes
                                    ModuleContext *ctx_)
     : logits(std::move(logits_)), num_classes(num_classes_), ctx(ctx_) {}
 
-// "fuse_output_bwd": the fused loss kernel also writes the output layer's input grad (on MFMA
-// in k_xstream_nn's sequence: bit-identical; reddit A/B 517.7 -> 520.1 epochs/s)
-int g_fuse_output_bwd = 1;
-// "fuse_output_wgrad": ... and per-block partials of the Matmul's weight grad, reduced in block
-// order right after it (deterministic; the same sums as k_gemm_tn's in another grouping): 1 on
-// graphs of >= 65,536 rows (small graphs keep k_gemm_tn's order: nothing to gain there), 2 on
-// any graph
-int g_fuse_output_wgrad = 1;
+// The fused loss kernel also writes the output layer's input grad (on MFMA in k_xstream_nn's
+// sequence: bit-identical; reddit A/B 517.7 -> 520.1 epochs/s) and, at fuse_output >= 2,
+// per-block partials of the Matmul's weight grad, reduced in block order right after it
+// (deterministic; the same sums as k_gemm_tn's in another grouping): 2 on graphs of >= 65,536
+// rows (small graphs keep k_gemm_tn's order: nothing to gain there), 3 on any graph
 
 void CrossEntropyLoss::forward(bool training, const Stream &s) const {
   if (fused && !ctx->compact_n) {
     const Variable &Hv = *fused->input(), &Wv = *fused->weight();
-    float *dH = g_fuse_output_bwd && Hv.dev_grad ? Hv.dev_grad.get() : nullptr;
+    // the fused output layer's contractions (logits = H W; training: dH = dOut W^T and the
+    // W.grad partials) over the fused kernel's time, which includes the loss itself
+    const double mm = 2.0 * logits->rows * num_classes * fused->inner();
+    MmProfile prof(ctx, s.get(), training ? 3.0 * mm : mm);
+    float *dH = Hv.dev_grad ? Hv.dev_grad.get() : nullptr;
     const int nb = xent_blocks(logits->rows);
     float *dWp = nullptr;
-    if (training && g_fuse_output_wgrad &&
-        (g_fuse_output_wgrad == 2 || logits->rows >= 65536) && Wv.dev_grad && logits->ld <= 48 &&
+    if (training && g_fuse_output >= 2 && (g_fuse_output == 3 || logits->rows >= 65536) &&
+        Wv.dev_grad && logits->ld <= 48 &&
         !ctx->mm_side &&
         tn_reduce_blocks_workspace(nb, fused->inner(), 48) <= ctx->gemm_workspace_bytes)
       dWp = static_cast<float *>(ctx->gemm_workspace);

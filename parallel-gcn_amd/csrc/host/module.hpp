@@ -85,18 +85,18 @@ class ReLU;
 class GraphSum;
 class Dropout;
 
+// "fuse_epilogue" bits (host/gcn.cpp g_fuse_epilogue) and "fuse_output" (g_fuse_output)
+constexpr int kFuseTails = 1, kFusePrestage = 2, kFuseXstream = 4;
+extern int g_fuse_epilogue;
+extern int g_fuse_output;
+
 // Shared per-GCN state the modules read (current split, comm, profiling, RNG table).
 struct ModuleContext {
   bool train_ahead = true;     // eval computes the next training forward's first product too
-  // train-ahead option "mask_side": the next input mask is drawn on a side stream beside the
-  // weight-gradient pass (1; r01: no gain -- the RNG kernel and the pass slow each other down
-  // and the reduce kernels after the pass starve), beside the eval forward's X-stream product
-  // (2), or beside the eval forward's output layer and loss (3), else by the training forward
-  // on the main stream
-  int mask_side = 0;
-  const Dropout *input_drop = nullptr;  // the first layer's Dropout (mask_side 3)
-  hipStream_t side_stream = nullptr;  // ... drawn here ...
-  Event tn_start, mask_ready;         // ... after tn_start (main), signalling mask_ready
+  // (measured and removed, r01/r02: drawing the next input mask on a side stream beside the
+  // weight-gradient pass, the eval forward's X-stream product or its output layer -- the RNG
+  // kernel and the pass beside it slow each other down, DESIGN.md §3 "Streams")
+  hipStream_t side_stream = nullptr;  // mm_side's stream
   // "mm_side": a Matmul's weight gradient (b.grad = a^T c.grad, needed only by the optimizer)
   // runs on side_stream beside the rest of the backward pass (the reference's S2/S3 streams,
   // src/module.cu:445-472); GCN joins it (side_join) before the all-reduce / optimizer
@@ -208,7 +208,7 @@ class SparseMatmul : public Module {
   shared_ptr<Variable> eval_out;
   // the GraphSum reading c (training) / standing for eval_out (eval): the X-stream product's
   // epilogue writes that GraphSum's ring table (training) or applies its fused ReLU and
-  // writes the next GraphSum's table (eval), when g_xstream_epilogue
+  // writes the next GraphSum's table (eval), when g_fuse_epilogue & kFuseXstream
   const GraphSum *consumer = nullptr;
   void forward(bool training, const Stream &s) const override;
   void backward(const Stream &s) const override;
@@ -302,6 +302,12 @@ class Matmul : public Module {
   int inner() const { return n; }
   void forward(bool training, const Stream &s) const override;
   void backward(const Stream &s) const override;
+  // the two halves of backward(), for callers that schedule them on their own streams (the
+  // C++ API's reference schedule, src/module.cu:431-472): a.grad = c.grad b^T on s, and
+  // b.grad = a^T c.grad on `ws` (a workspace of gemm_tn_workspace(m, p, n) bytes owned by the
+  // caller when the stream is not the module's usual one)
+  void backward_input(const Stream &s) const;
+  void backward_weight(hipStream_t s, void *ws) const;
 };
 
 // include/module.cuh:128-145

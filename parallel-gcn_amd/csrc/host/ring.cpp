@@ -63,12 +63,10 @@ struct Lane {
 };
 }  // namespace
 
-// "ring_balance": 0 = off; g > 0 = a wave below its visit's slowest takes extra blocks on
-// rowsets where some lane has at least g more edges pending than its current steps
-int g_ring_balance = 0;
-// "ring_spread": x10 mean edges per slice above which a row is spread over 2, 4, 8 or 16 lane
-// groups (0 = never)
-int g_ring_spread = 60;
+// x10 mean edges per slice above which a row is spread over 2, 4, 8 or 16 lane groups (r02
+// sweep on reddit-114M: 60 best; pulling extra blocks into waves below a visit's slowest
+// measured no faster and was removed)
+constexpr int kRingSpread = 60;
 
 std::vector<int> ring_cuts(int n_cols, const std::vector<int> &indices, int n_blocks) {
   std::vector<int> cut = column_cuts(n_cols, indices, n_blocks);
@@ -107,7 +105,7 @@ LdsHost build_ring_host(int n_rows, int n_cols, const std::vector<int> &indptr,
   // Units: a row takes m = 2^s lane groups ("spread"), each summing every m-th of its edges
   // in this column block; the wave adds the m partial sums at the end (k_graphsum_ring's
   // partial write).  m doubles while the row's mean edges per slice over m exceed
-  // g_ring_spread / 10 (hub rows would otherwise pace their rowset, their wave and, through
+  // kRingSpread / 10 (hub rows would otherwise pace their rowset, their wave and, through
   // the visits' hand-offs, their workgroup).  Rowsets hold 16 units of one m, rows by m, then
   // degree, descending; rowsets are dealt round-robin to batches.
   std::vector<int> order((size_t)n_rows);
@@ -116,7 +114,7 @@ LdsHost build_ring_host(int n_rows, int n_cols, const std::vector<int> &indptr,
   auto spread_of = [&](int row) {
     const double lam = (indptr[(size_t)row + 1] - indptr[(size_t)row]) * per_slice;
     int s = 0;
-    while (s < 4 && g_ring_spread > 0 && lam / (1 << s) > g_ring_spread / 10.0) s++;
+    while (s < 4 && lam / (1 << s) > kRingSpread / 10.0) s++;
     return s;
   };
   std::vector<int> spread((size_t)n_rows);
@@ -230,10 +228,7 @@ LdsHost build_ring_host(int n_rows, int n_cols, const std::vector<int> &indptr,
   // appends each wave's entry blocks to out[wave].
   //
   // Visits end in hand-offs (a slice leaves the ring once every wave is done with it), so
-  // the slowest wave of a visit paces the workgroup.  A wave with fewer forced blocks than the
-  // visit's slowest (forced: the most edges a lane of the rowset still has in slice v) takes
-  // extra blocks on the rowsets with the most edges pending in the window (g_ring_balance),
-  // pulling work ahead instead of waiting.
+  // the slowest wave of a visit paces the workgroup.
   auto walk_wg = [&](long long wg, std::vector<std::vector<unsigned short>> &out) {
     const int b = (int)(wg % B), bat = (int)(wg / B), T = nsl[(size_t)b];
     const int base_col = bcut[(size_t)b];
@@ -262,9 +257,7 @@ LdsHost build_ring_host(int n_rows, int n_cols, const std::vector<int> &indptr,
     std::vector<int> nb((size_t)CW * NS);
     for (int v = 0; v < T; v++) {
       // forced blocks per (wave, rowset)
-      int top = 0;
       for (int w = 0; w < CW; w++) {
-        int load = 0;
         for (int j = 0; j < NS; j++) {
           int n = 0;
           for (int g = 0; g < 16; g++) {
@@ -276,31 +269,8 @@ LdsHost build_ring_host(int n_rows, int n_cols, const std::vector<int> &indptr,
             n = std::max(n, L.due);
           }
           nb[(size_t)w * NS + j] = (n + 3) / 4;
-          load += (n + 3) / 4;
         }
-        top = std::max(top, load);
       }
-      if (g_ring_balance)
-        for (int w = 0; w < CW; w++) {
-          int load = 0;
-          for (int j = 0; j < NS; j++) load += nb[(size_t)w * NS + j];
-          while (load < top) {
-            int best = -1, gain = g_ring_balance - 1;
-            for (int j = 0; j < NS; j++) {
-              int gj = 0;
-              for (int g = 0; g < 16; g++)
-                gj = std::max(gj, lanes[((size_t)w * NS + j) * 16 + g].pending() -
-                                      4 * nb[(size_t)w * NS + j]);
-              if (gj > gain) {
-                gain = gj;
-                best = j;
-              }
-            }
-            if (best < 0) break;
-            nb[(size_t)w * NS + best]++;
-            load++;
-          }
-        }
       for (int w = 0; w < CW; w++) {
         for (int j = 0; j < NS; j++) {
           const int S = 4 * nb[(size_t)w * NS + j];
@@ -397,7 +367,6 @@ LdsHost build_ring_host(int n_rows, int n_cols, const std::vector<int> &indptr,
   }, 0, 2);
   LdsHost h;
   h.n_blocks = B;
-  h.window = kRingWindow;
   h.n_batches = nbat;
   h.t_max = t_max;
   h.nsl = std::move(nsl);

@@ -634,6 +634,7 @@ void launch_xent_fwd(float *logits, int ld, float *grad, const int *truth, int n
 void launch_out_xent(const float *H, int ldh, int kh, const float *W, int ldw, float *logits,
                      int ld, float *grad, const int *truth, int n, int c, int count, int training,
                      float *partials, hipStream_t s, float *dH, int lddh, float *dWp) {
+  note_path(KP_OUT_XENT);
   if (n <= 0) return;
   PGCN_CHECK(ld <= 116 && c <= ld && ld % 4 == 0 && kh >= 1 && kh <= 16, PGCN_E_INVALID,
              "out_xent: classes <= 116, hidden <= 16");

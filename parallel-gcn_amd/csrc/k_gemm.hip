@@ -417,163 +417,6 @@ __global__ __launch_bounds__(256, 1) void k_xstream_tn(int M, int N, int K,
   }
 }
 
-// ------------------------------------------------------------------------------------------
-// TN through an LDS-DMA ring: the same product and per-lane MFMA feed as k_xstream_tn, but a
-// step's 4 rows of X (contiguous, 16*lda bytes), its 4 rows of G and of the nibble mask reach
-// LDS by global_load_lds_dwordx4 (1 KB per wave instruction, no VGPRs), XT_SLOTS - 1 steps
-// ahead.  Slots are wave-private: no barrier, each wave counts its own DMAs (12 per step:
-// <= 10 X pieces, 1 G, 1 mask; a step past the wave's last still issues its DMAs, clamped to
-// row M - 1, so every wait is the same constant vmcnt).  Rows >= M read row M - 1 with b = 0.
-// ------------------------------------------------------------------------------------------
-constexpr int XT_SLOTS = 3;
-constexpr int XT_SLOT_BYTES = 16 * 640 + 256 + 512;  // X (lda <= 640), G (16 floats), mask
-
-__device__ __forceinline__ void xt_glds16(const void *gsrc, unsigned lds_dst) {
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(gsrc), "s"(lds_dst)
-      : "memory");
-}
-
-template <int KC, bool MASKED>
-__global__ __launch_bounds__(256, 1) void k_xstream_tn_lds(int M, int N, int K,
-                                                           const float *__restrict__ A, int lda,
-                                                           const float *__restrict__ G, int ldg,
-                                                           const uint64_t *__restrict__ maskT,
-                                                           float a_scale,
-                                                           float *__restrict__ partial) {
-  __shared__ __attribute__((aligned(16))) char ring[4 * XT_SLOTS * XT_SLOT_BYTES];
-  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int g = lane >> 4, i = lane & 15;
-  const unsigned lds_base = __builtin_amdgcn_readfirstlane(
-      (unsigned)reinterpret_cast<size_t>((__attribute__((address_space(3))) char *)ring));
-  const unsigned my_ring = lds_base + (unsigned)(w * XT_SLOTS * XT_SLOT_BYTES);
-  const char *my_ring_p = ring + w * XT_SLOTS * XT_SLOT_BYTES;
-  const int xbytes = 16 * lda;  // one step: 4 rows
-  const int npieces = (xbytes + 1023) >> 10;
-  const long long n_steps = (M + 3) / 4;
-  const long long wid = (long long)blockIdx.x * 4 + w, nw = (long long)gridDim.x * 4;
-  const long long my_steps = wid < n_steps ? (n_steps - wid + nw - 1) / nw : 0;
-  // per-lane placement of the X pieces inside a step (the same for every step)
-  int prow[KC], pcol[KC];  // row 0..3 of the step, byte inside the row (-1: lane idle)
-#pragma unroll
-  for (int q = 0; q < KC; q++) {
-    const int o = 1024 * q + 16 * lane;
-    prow[q] = o < xbytes ? o / (4 * lda) : -1;
-    pcol[q] = o < xbytes ? o - prow[q] * 4 * lda : 0;
-  }
-  auto issue = [&](long long n, int slot) {  // DMAs of this wave's n-th step into a slot
-    const long long m0 = (wid + n * nw) * 4;  // first row of the step
-    const unsigned dst = my_ring + (unsigned)(slot * XT_SLOT_BYTES);
-#pragma unroll
-    for (int q = 0; q < KC; q++) {
-      if (q < npieces && prow[q] >= 0) {
-        long long r = m0 + prow[q];
-        r = r < M ? r : M - 1;
-        xt_glds16(reinterpret_cast<const char *>(A + r * lda) + pcol[q], dst + (unsigned)(1024 * q));
-      }
-    }
-    if (lane < 16) {  // G: 4 rows x 64 B
-      long long r = m0 + (lane >> 2);
-      r = r < M ? r : M - 1;
-      xt_glds16(reinterpret_cast<const char *>(G + r * ldg) + 16 * (lane & 3), dst + (unsigned)xbytes);
-    }
-    if (lane < 32) {  // mask: 4 rows x 128 B
-      long long r = m0 + (lane >> 3);
-      r = r < M ? r : M - 1;
-      const uint64_t *src = MASKED ? maskT + r * 16 : maskT;
-      if (MASKED)
-        xt_glds16(reinterpret_cast<const char *>(src) + 16 * (lane & 7),
-                  dst + (unsigned)(xbytes + 256));
-    }
-  };
-  floatx4 acc[KC][4];
-#pragma unroll
-  for (int c = 0; c < KC; c++)
-#pragma unroll
-    for (int t = 0; t < 4; t++) acc[c][t] = floatx4{0.f, 0.f, 0.f, 0.f};
-  // DMA instructions one step issues for this wave: the waits count them
-  static_assert(XT_SLOTS == 3, "waits below assume two steps in flight");
-  issue(0, 0);
-  issue(1, 1);
-  int slot = 0;
-  for (long long n = 0; n < my_steps; n++) {
-    issue(n + 2, (slot + 2) % XT_SLOTS);
-    // step n's DMAs have landed once only the two younger steps' are outstanding
-    if constexpr (MASKED) {
-      if (npieces == KC) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (KC + 2)) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-      if (npieces == KC) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (KC + 1)) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    const char *sp = my_ring_p + slot * XT_SLOT_BYTES;
-    const long long m0 = (wid + n * nw) * 4;
-    const float gv = *reinterpret_cast<const float *>(sp + xbytes + 64 * g + 4 * (i < N ? i : 0));
-    const float bj = (m0 + g < M && i < N) ? gv : 0.0f;
-    uint64_t mw = 0;
-    if constexpr (MASKED) mw = *reinterpret_cast<const uint64_t *>(sp + xbytes + 256 + 128 * g + 8 * i);
-    const char *xr = sp + g * 4 * lda;
-#pragma unroll
-    for (int c = 0; c < KC; c++) {
-      const int kb = 64 * c + 4 * i;
-      float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (kb < lda) x = *reinterpret_cast<const float4 *>(xr + 4 * kb);
-      if (64 * c + 64 > K) {
-        if (kb + 1 > K) x.x = 0.f;
-        if (kb + 2 > K) x.y = 0.f;
-        if (kb + 3 > K) x.z = 0.f;
-        if (kb + 4 > K) x.w = 0.f;
-      }
-      if constexpr (MASKED) apply4(x, (uint32_t)(mw >> (4 * c)) & 0xfu, a_scale);
-      acc[c][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(x.x, bj, acc[c][0], 0, 0, 0);
-      acc[c][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(x.y, bj, acc[c][1], 0, 0, 0);
-      acc[c][2] = __builtin_amdgcn_mfma_f32_16x16x4f32(x.z, bj, acc[c][2], 0, 0, 0);
-      acc[c][3] = __builtin_amdgcn_mfma_f32_16x16x4f32(x.w, bj, acc[c][3], 0, 0, 0);
-    }
-    slot = slot + 1 == XT_SLOTS ? 0 : slot + 1;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dummy DMAs past the last step
-  __syncthreads();
-  // waves 1..3 hand their chunk tiles to wave 0 through LDS (fixed order; the ring is free)
-  float *red = reinterpret_cast<float *>(ring);
-  float *p = partial + (long long)blockIdx.x * K * 16;
-#pragma unroll
-  for (int c = 0; c < KC; c++) {
-    if (w > 0) {
-#pragma unroll
-      for (int t = 0; t < 4; t++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) red[((w - 1) * 64 + lane) * 16 + t * 4 + r] = acc[c][t][r];
-    }
-    __syncthreads();
-    if (w == 0) {
-#pragma unroll
-      for (int t = 0; t < 4; t++) {
-        floatx4 v = acc[c][t];
-#pragma unroll
-        for (int q = 0; q < 3; q++)
-#pragma unroll
-          for (int r = 0; r < 4; r++) v[r] += red[(q * 64 + lane) * 16 + t * 4 + r];
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int k = 64 * c + 4 * (4 * g + r) + t;
-          if (k < K) p[(long long)k * 16 + i] = v[r];
-        }
-      }
-    }
-    __syncthreads();
-  }
-}
-
-// "xstream_tn_lds": 1 = the LDS-DMA ring (r01: 179 us vs 165-169 us for the register-streamed
-// kernel on reddit: X streams at ~3.4 TB/s either way, about what torch's own reductions get
-// from this 563-MB array here, so the ring is kept as an option, off)
-int g_xstream_tn_lds = 0;
-
 int g_gemm_variant = 0;  // diagnostics ("gemm_variant"): 1 = the general kernels only
 
 // ------------------------------------------------------------------------------------------
@@ -752,10 +595,6 @@ void launch_mask_nibbles(const uint64_t *mask, long long mask_base, long long ma
                      mask_base, mask_ld, M, K, out);
 }
 
-// "xstream_nn_balance": 1 = grid sized so every wave gets the same number of row groups;
-// > 1 = that many workgroups (diagnostics)
-int g_xstream_nn_balance = 0;
-
 void launch_xstream_nn(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
                        int trans_b, float *C, int ldc, const uint64_t *maskT, float a_scale,
                        hipStream_t s, float *C2, const XsEpilogue *epi) {
@@ -772,17 +611,10 @@ void launch_xstream_nn(int M, int N, int K, const float *A, int lda, const float
     launch_xstream_nn_ring(M, N, K, A, lda, B, ldb, trans_b, C, ldc, maskT, a_scale, s, C2, e);
     return;
   }
+  note_path(KP_XS_NN);
   const int kc = (K + 63) / 64, S = xs_stride(K);
   const long long n_rg = ceil_div(M, 16);
-  long long wgs = std::min<long long>(ceil_div(n_rg, 4), 2 * kCUs);
-  if (g_xstream_nn_balance > 1) {  // diagnostics: exactly this many workgroups
-    wgs = g_xstream_nn_balance;
-  } else if (g_xstream_nn_balance) {
-    // every wave the same number of 16-row groups (+-1 over the grid): the last round of a
-    // grid-stride loop over n_rg groups no longer runs on a fraction of the waves
-    const long long per_wave = ceil_div(n_rg, 4 * wgs);
-    wgs = ceil_div(n_rg, 4 * per_wave);
-  }
+  const long long wgs = std::min<long long>(ceil_div(n_rg, 4), 2 * kCUs);
   const dim3 grid((unsigned)wgs), block(256);
   const size_t lds = (size_t)16 * S * sizeof(float);
 #define XNN_CASE(KC)                                                                          \
@@ -835,6 +667,7 @@ static void gemm_nn_slab(int M, int N, int K, const float *A, int lda, const flo
     launch_xstream_nn(M, N, K, A, lda, B, ldb, trans_b, C, ldc, nullptr, 1.0f, s, nullptr);
     return;
   }
+  note_path(KP_GEMM_NN);
   const int nt = (N + 15) / 16;
   const dim3 grid((unsigned)ceil_div(M, 64)), block(256);
 #define NN_CASE(T)                                                                            \
@@ -935,15 +768,8 @@ void launch_xstream_tn(int M, int N, int K, const float *A, int lda, const float
   float *partial = static_cast<float *>(workspace);
   if (M > 0 && xstream_ring_ok(K, lda)) {
     launch_xstream_tn_ring(M, N, K, A, lda, G, ldg, maskT, a_scale, partial, XS_TN_BLOCKS, s);
-  } else if (M > 0 && g_xstream_tn_lds && ldg == 16 && lda <= 640 && p.nkc == 10) {
-    // the LDS-DMA ring (its waits are written for ten 64-column chunks: reddit's K = 602)
-    if (maskT)
-      hipLaunchKernelGGL((k_xstream_tn_lds<10, true>), dim3(XS_TN_BLOCKS), dim3(256), 0, s, M, N,
-                         K, A, lda, G, ldg, maskT, a_scale, partial);
-    else
-      hipLaunchKernelGGL((k_xstream_tn_lds<10, false>), dim3(XS_TN_BLOCKS), dim3(256), 0, s, M, N,
-                         K, A, lda, G, ldg, maskT, a_scale, partial);
   } else if (M > 0) {
+    note_path(KP_XS_TN);
 #define XTN_CASE(KC)                                                                           \
   case KC:                                                                                     \
     if (maskT)                                                                                 \
@@ -994,6 +820,7 @@ static void gemm_tn_slab(int M, int N, int K, const float *A, int lda, const flo
   const TnPlan p = tn_plan(M, N, K);
   float *partial = static_cast<float *>(workspace);
   if (M > 0) {
+    note_path(KP_GEMM_TN);
     const dim3 grid((unsigned)p.n_slabs, (unsigned)p.kgroups), block(256);
     bool done = false;
 #define TN_CASE(NJ, KCW, WK)                                                                   \

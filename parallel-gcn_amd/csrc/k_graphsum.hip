@@ -39,9 +39,8 @@ __device__ __forceinline__ float4 f4_shfl_xor(float4 v, int m) {
                      __shfl_xor(v.w, m, 64));
 }
 
-// G lanes per item (G | 64); VEC float4 per row.  VAR != 0 only in diagnostic builds of
-// the launch (pgcn_debug_set): 1 = no feature gather, 2 = gathers folded into 4096 rows.
-template <int VEC, int G, int VAR = 0>
+// G lanes per item (G | 64); VEC float4 per row.
+template <int VEC, int G>
 __global__ __launch_bounds__(256) void k_graphsum(const int4 *__restrict__ items,
                                                   const int *__restrict__ block_items,
                                                   int nbc, const int *__restrict__ indices,
@@ -68,20 +67,9 @@ __global__ __launch_bounds__(256) void k_graphsum(const int4 *__restrict__ items
       for (; j + 3 * NB < end; j += 4 * NB) {
         int c0 = indices[j], c1 = indices[j + NB], c2 = indices[j + 2 * NB],
             c3 = indices[j + 3 * NB];
-        if constexpr (VAR == 2) { c0 &= 4095; c1 &= 4095; c2 &= 4095; c3 &= 4095; }
         const float w0 = vals[j], w1 = vals[j + NB], w2 = vals[j + 2 * NB], w3 = vals[j + 3 * NB];
-        float4 x0, x1, x2, x3;
-        if constexpr (VAR == 1) {
-          x0 = make_float4(__int_as_float(c0), 1.f, 1.f, 1.f);
-          x1 = make_float4(__int_as_float(c1), 1.f, 1.f, 1.f);
-          x2 = make_float4(__int_as_float(c2), 1.f, 1.f, 1.f);
-          x3 = make_float4(__int_as_float(c3), 1.f, 1.f, 1.f);
-        } else {
-          x0 = in[(long long)c0 * ld4_in + v];
-          x1 = in[(long long)c1 * ld4_in + v];
-          x2 = in[(long long)c2 * ld4_in + v];
-          x3 = in[(long long)c3 * ld4_in + v];
-        }
+        const float4 x0 = in[(long long)c0 * ld4_in + v], x1 = in[(long long)c1 * ld4_in + v],
+                     x2 = in[(long long)c2 * ld4_in + v], x3 = in[(long long)c3 * ld4_in + v];
         acc = f4_fma(w0, x0, acc);
         acc = f4_fma(w1, x1, acc);
         acc = f4_fma(w2, x2, acc);
@@ -136,7 +124,6 @@ __device__ __forceinline__ float float4_comp(const float4 &v, int c) {
   return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
 }
 
-template <int VAR>
 __global__ __launch_bounds__(256) void k_graphsum16(const int4 *__restrict__ items,
                                                     const int *__restrict__ block_items, int nbc,
                                                     const int *__restrict__ indices,
@@ -160,14 +147,8 @@ __global__ __launch_bounds__(256) void k_graphsum16(const int4 *__restrict__ ite
       int4 ci = make_int4(0, 0, 0, 0);
       float4 cw = make_float4(0.f, 0.f, 0.f, 0.f);
       if (e < item.z) {
-        if constexpr (VAR == 4) {  // diagnostics: synthetic in-slice columns, no index stream
-          const unsigned hh = (unsigned)e * 2654435761u;
-          ci = make_int4((hh >> 9) & 0x3fff, (hh >> 7) & 0x3fff, (hh >> 5) & 0x3fff, (hh >> 3) & 0x3fff);
-          cw = make_float4(1.f, 1.f, 1.f, 1.f);
-        } else {
-          ci = *reinterpret_cast<const int4 *>(indices + e);
-          cw = *reinterpret_cast<const float4 *>(vals + e);
-        }
+        ci = *reinterpret_cast<const int4 *>(indices + e);
+        cw = *reinterpret_cast<const float4 *>(vals + e);
       }
       const int lim = item.z - base - 16 * nb;  // slots of this sub-group in the sub-chunk
 #pragma unroll
@@ -180,10 +161,7 @@ __global__ __launch_bounds__(256) void k_graphsum16(const int4 *__restrict__ ite
           const int src = gbase + 4 * nb + (s >> 2);
           const int c = __shfl(int4_comp(ci, s & 3), src, 64);
           w[t] = __shfl(float4_comp(cw, s & 3), src, 64);
-          if constexpr (VAR == 1)  // diagnostics: no feature gather
-            x[t] = make_float4(__int_as_float(c), 1.f, 1.f, 1.f);
-          else
-            x[t] = s < lim ? in[(long long)c * ld4_in + v] : make_float4(0.f, 0.f, 0.f, 0.f);
+          x[t] = s < lim ? in[(long long)c * ld4_in + v] : make_float4(0.f, 0.f, 0.f, 0.f);
         }
 #pragma unroll
         for (int t = 0; t < 8; t++) acc = f4_fma(w[t], x[t], acc);
@@ -202,91 +180,6 @@ __global__ __launch_bounds__(256) void k_graphsum16(const int4 *__restrict__ ite
   }
 }
 
-// Software-pipelined form of k_graphsum16: the edge list of the NEXT sub-chunk (and the
-// next item's header) is loaded after the current sub-chunk's 16 gathers are issued, so the
-// waits on the gathers (in-order vmcnt) never wait for the HBM-latency index stream.
-__global__ __launch_bounds__(256) void k_graphsum16p(const int4 *__restrict__ items,
-                                                     const int *__restrict__ block_items, int nbc,
-                                                     const int *__restrict__ indices,
-                                                     const float *__restrict__ vals,
-                                                     const float4 *__restrict__ in, int ld4_in,
-                                                     float4 *__restrict__ out, int ld4_out,
-                                                     float4 *__restrict__ partial,
-                                                     GsEpilogue epi) {
-  const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
-  const int q = lane >> 4, r = lane & 15;
-  const int nb = r >> 2, v = r & 3;
-  const int gbase = lane & ~15;
-  const int b = blockIdx.x % nbc;
-  const int wg = blockIdx.x / nbc, nwg = gridDim.x / nbc;
-  const int first = block_items[b], last = block_items[b + 1];
-  const int stride = nwg * 16;
-  int it = first + (wg * 4 + wib) * 4 + q;
-  if (it >= last) return;  // uniform per 16-lane group; groups only talk inside themselves
-  int4 item = items[it];
-  int4 item_next = it + stride < last ? items[it + stride] : make_int4(0, 0, 0, -2);
-  int base = item.y;
-  int4 ci;
-  float4 cw;
-  {
-    const int e = base + 4 * r;
-    ci = e < item.z ? *reinterpret_cast<const int4 *>(indices + e) : make_int4(0, 0, 0, 0);
-    cw = e < item.z ? *reinterpret_cast<const float4 *>(vals + e) : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  while (true) {
-    // 1. issue the 16 independent gathers of the current sub-chunk
-    const int lim = item.z - base - 16 * nb;
-    float4 x[16];
-    float w[16];
-#pragma unroll
-    for (int s = 0; s < 16; s++) {
-      const int src = gbase + 4 * nb + (s >> 2);
-      const int c = __shfl(int4_comp(ci, s & 3), src, 64);
-      w[s] = __shfl(float4_comp(cw, s & 3), src, 64);
-      x[s] = s < lim ? in[(long long)c * ld4_in + v] : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    // 2. where does the next sub-chunk come from?
-    const bool item_done = base + 64 >= item.z;
-    int nbase = base + 64;
-    int4 nitem = item;
-    if (item_done) {
-      nitem = item_next;
-      nbase = nitem.y;
-    }
-    const bool more = !item_done || nitem.w != -2;
-    // 3. prefetch its edge list (younger than the gathers)
-    if (more) {
-      const int e = nbase + 4 * r;
-      ci = e < nitem.z ? *reinterpret_cast<const int4 *>(indices + e) : make_int4(0, 0, 0, 0);
-      cw = e < nitem.z ? *reinterpret_cast<const float4 *>(vals + e)
-                       : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    // 4. accumulate
-#pragma unroll
-    for (int s = 0; s < 16; s++) acc = f4_fma(w[s], x[s], acc);
-    if (item_done) {
-      float4 t = f4_add(acc, f4_shfl_xor(acc, 4));
-      t = f4_add(t, f4_shfl_xor(t, 8));
-      if (nb == 0) {
-        if (item.w < 0) {
-          gs_epilogue(t, item.x, 4 * v, epi);
-          out[(long long)item.x * ld4_out + v] = t;
-        } else {
-          partial[(long long)item.w * 4 + v] = t;
-        }
-      }
-      acc = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (!more) break;
-      it += stride;
-      item = nitem;
-      item_next = it + stride < last ? items[it + stride] : make_int4(0, 0, 0, -2);
-    }
-    base = nbase;
-  }
-}
-
-// out[row] = sum of partial slots [first, first+count) in slot order (count may be 0)
 template <int VEC>
 __global__ __launch_bounds__(256) void k_graphsum_combine(const int4 *__restrict__ comb,
                                                           int n_comb,
@@ -304,8 +197,6 @@ __global__ __launch_bounds__(256) void k_graphsum_combine(const int4 *__restrict
   out[(long long)c.x * ld4_out + v] = acc;
 }
 
-int g_graphsum_variant = 0;  // diagnostics only (pgcn_debug_set)
-
 template <int VEC, int G>
 static void launch_vec(const GraphSchedule &s, const int *indices, const float *vals,
                        const float *in, int ld_in, float *out, int ld_out, float *partial,
@@ -317,34 +208,19 @@ static void launch_vec(const GraphSchedule &s, const int *indices, const float *
     const long long cap = 4096 / s.nbc;
     if (per_block > cap) per_block = cap;
     if (per_block < 1) per_block = 1;
-#define GS_LAUNCH(VAR)                                                                    \
-  hipLaunchKernelGGL((k_graphsum<VEC, G, VAR>), dim3((unsigned)(per_block * s.nbc)), dim3(256), \
-                     0, st, s.items, s.block_items, s.nbc, indices, vals,                   \
-                     reinterpret_cast<const float4 *>(in), ld_in / 4,                       \
-                     reinterpret_cast<float4 *>(out), ld_out / 4,                           \
-                     reinterpret_cast<float4 *>(partial), epi)
-    if (g_graphsum_variant == 1 && VEC == 4) GS_LAUNCH(1);
-    else if (g_graphsum_variant == 2 && VEC == 4) GS_LAUNCH(2);
-    else if (VEC == 4 && s.nbc > 1 && g_graphsum_variant != 3) {
-#define GS16(VAR)                                                                          \
-  hipLaunchKernelGGL(k_graphsum16<VAR>, dim3((unsigned)(per_block * s.nbc)), dim3(256), 0, st, \
-                     s.items, s.block_items, s.nbc, indices, vals,                        \
-                     reinterpret_cast<const float4 *>(in), ld_in / 4,                     \
-                     reinterpret_cast<float4 *>(out), ld_out / 4,                         \
-                     reinterpret_cast<float4 *>(partial), epi)
-      if (g_graphsum_variant == 11) GS16(1);
-      else if (g_graphsum_variant == 14) GS16(4);
-      else if (g_graphsum_variant != 6) GS16(0);
-      else  // diagnostic: software-pipelined form (slower: 132 VGPRs, 3 waves/SIMD)
-        hipLaunchKernelGGL(k_graphsum16p, dim3((unsigned)(per_block * s.nbc)), dim3(256), 0, st,
-                           s.items, s.block_items, s.nbc, indices, vals,
-                           reinterpret_cast<const float4 *>(in), ld_in / 4,
-                           reinterpret_cast<float4 *>(out), ld_out / 4,
-                           reinterpret_cast<float4 *>(partial), epi);
-#undef GS16
-    }
-    else GS_LAUNCH(0);
-#undef GS_LAUNCH
+    const dim3 grid((unsigned)(per_block * s.nbc)), block(256);
+    // (measured and removed, r01: a software-pipelined k_graphsum16, 132 VGPRs at 3 waves per
+    // SIMD, slower)
+    if (VEC == 4 && s.nbc > 1)
+      hipLaunchKernelGGL(k_graphsum16, grid, block, 0, st, s.items, s.block_items, s.nbc, indices,
+                         vals, reinterpret_cast<const float4 *>(in), ld_in / 4,
+                         reinterpret_cast<float4 *>(out), ld_out / 4,
+                         reinterpret_cast<float4 *>(partial), epi);
+    else
+      hipLaunchKernelGGL((k_graphsum<VEC, G>), grid, block, 0, st, s.items, s.block_items, s.nbc,
+                         indices, vals, reinterpret_cast<const float4 *>(in), ld_in / 4,
+                         reinterpret_cast<float4 *>(out), ld_out / 4,
+                         reinterpret_cast<float4 *>(partial), epi);
   }
   if (s.n_comb > 0) {
     const long long threads = (long long)s.n_comb * VEC;
@@ -364,6 +240,7 @@ int graphsum_group_lanes(int vec) {
 void launch_graphsum(const GraphSchedule &s, const int *indices, const float *vals,
                      const float *in, int ld_in, float *out, int ld_out, float *partial,
                      hipStream_t st, const GsEpilogue *epi) {
+  note_path(KP_GS_GATHER);
   const GsEpilogue none{};
   const GsEpilogue &e = epi ? *epi : none;
   switch (s.vec) {

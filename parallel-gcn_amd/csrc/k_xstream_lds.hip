@@ -40,19 +40,11 @@
 namespace pgcn {
 
 // "xstream_ring": 1 = these kernels for the X-stream products where they apply (default),
-// 0 = the register-streamed k_xstream_nn / k_xstream_tn.  "xstream_ring_inflight": groups in
-// flight per loader wave (1 or 2)
+// 0 = the register-streamed k_xstream_nn / k_xstream_tn (the oracle-tested fallback of every
+// other width).  Measured and removed (r02): two groups in flight per loader wave, fewer
+// slots, and a TN split in which every consumer takes a share of K of every group (173 vs 137
+// us on reddit: every consumer then waits on every group).
 int g_xstream_ring = 1;
-int g_xstream_ring_inflight = 1;
-// "xstream_ring_slots": at most this many ring slots (0: as many as fit)
-int g_xstream_ring_slots = 0;
-// "xstream_tn_split": TN with every consumer taking a share of K of every group (k_xs_tn_split;
-// r02: 173 vs 137 us on reddit -- every consumer now waits on every group and its dZ / keep-bit
-// prefetch runs only one group ahead)
-int g_xstream_tn_split = 0;
-// "xstream_ring_diag" (timing only, wrong results): 1 = consumers skip their MFMAs (the
-// loaders' pace), 2 = loaders skip their DMAs (the consumers' pace)
-int g_xstream_ring_diag = 0;
 
 namespace {
 
@@ -72,8 +64,6 @@ struct XlRing {
   int off;    // LDS byte offset of slot 0 (NN: past B^T)
   int st;     // row stride in 16-B chunks (lda / 4 = ceil(K / 4))
   int nslot;  // slots in the ring (<= 4)
-  int two;    // loaders keep two groups in flight
-  int diag;   // g_xstream_ring_diag
 };
 
 // DMA instructions (1 KB) per group for a row of lda floats: the group's 64 * lda bytes
@@ -83,10 +73,7 @@ XlRing xl_ring(int lda, int ni, int off) {
   XlRing r;
   r.off = off;
   r.st = lda / 4;
-  r.nslot = std::min(g_xstream_ring_slots > 1 ? std::min(4, g_xstream_ring_slots) : 4,
-                     (XL_LDS - XL_FLAGS - off) / (ni * 1024));
-  r.two = g_xstream_ring_inflight > 1 && r.nslot == 4;
-  r.diag = g_xstream_ring_diag;
+  r.nslot = std::min(4, (XL_LDS - XL_FLAGS - off) / (ni * 1024));
   return r;
 }
 
@@ -130,46 +117,29 @@ __device__ __forceinline__ void xl_dma4(const char *gsrc, unsigned lds_dst) {
 }
 
 // Loader wave `wave` of NL: groups wave, wave + NL, ... into slot t % nslot, NI pieces
-// each.  With two in flight a loader publishes group t - 2 once only group t's NI DMAs are
-// outstanding, or before it would block on a slot.
-// REL: releases per slot use -- 1 (a consumer per group stores t + 1 into freed) or the
-// number of consumers that each read a share of every group (they add 1 each)
-template <int NI, int NL, int REL = 1>
+// each; a consumer per group releases the slot by storing t + 1 into freed.
+template <int NI, int NL>
 __device__ __forceinline__ void xl_load(const float *__restrict__ A, int lda, long long M, int T,
                                         int wave, int lane, const XlRing &rg, char *lds,
                                         unsigned *ready, unsigned *freed) {
   static_assert(NI < 64, "vmcnt counts at most 63");
   __builtin_amdgcn_s_setprio(3);
+  wave = __builtin_amdgcn_readfirstlane(wave);  // uniform (the LDS-DMA destination is an SGPR)
   const unsigned base = __builtin_amdgcn_readfirstlane(
       (unsigned)reinterpret_cast<size_t>((__attribute__((address_space(3))) char *)lds));
   const unsigned slot_bytes = NI * 1024;
   const long long x_bytes = M * (long long)lda * 4;
-  int pend = -1;
   auto publish = [&](int u) {
     if (lane == 0) __atomic_store_n(ready + u % rg.nslot, (unsigned)(u + 1), __ATOMIC_RELAXED);
     asm volatile("" ::: "memory");
   };
   for (int t = wave; t < T; t += NL) {
     const int slot = t % rg.nslot;
-    if (t >= rg.nslot) {
-      const unsigned need =
-          REL == 1 ? (unsigned)(t - rg.nslot + 1) : (unsigned)(REL * (t / rg.nslot));
-      if ((unsigned)__builtin_amdgcn_readfirstlane(__atomic_load_n(freed + slot, __ATOMIC_RELAXED)) <
-          need) {
-        if (pend >= 0) {  // about to block: the group in flight goes out first
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          publish(pend);
-          pend = -1;
-        }
-        lds_wait_ge(freed + slot, need);
-      }
-    }
+    if (t >= rg.nslot) lds_wait_ge(freed + slot, (unsigned)(t - rg.nslot + 1));
     const long long b0 = (blockIdx.x + (long long)t * gridDim.x) * 16 * (long long)lda * 4;
     const char *blk = reinterpret_cast<const char *>(A) + b0;
-    const unsigned dst = base + (unsigned)(rg.off + slot * slot_bytes);
-    if (rg.diag == 2) {
-      // timing only: no DMA
-    } else if (b0 + NI * 1024 <= x_bytes) {  // the whole NI KB lies inside X
+    const unsigned dst = __builtin_amdgcn_readfirstlane(base + (unsigned)(rg.off + slot * slot_bytes));
+    if (b0 + NI * 1024 <= x_bytes) {  // the whole NI KB lies inside X
       const char *src = blk + lane * 16;
 #pragma unroll
       for (int q = 0; q + 4 <= NI; q += 4) xl_dma4(src + q * 1024, dst + (unsigned)(q * 1024));
@@ -183,20 +153,8 @@ __device__ __forceinline__ void xl_load(const float *__restrict__ A, int lda, lo
         glds16_nt(blk + (off < left ? off : 0), dst + (unsigned)(q * 1024));
       }
     }
-    if (rg.two) {
-      if (pend >= 0) {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");  // group pend landed
-        publish(pend);
-      }
-      pend = t;
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      publish(t);
-    }
-  }
-  if (pend >= 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    publish(pend);
+    publish(t);
   }
 }
 
@@ -271,7 +229,7 @@ __global__ __launch_bounds__(64 * (XL_NN_LOADERS + XL_NN_CONSUMERS), 1) void k_x
     floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f}, acc2 = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < NS; s++) {
-      if (16 * s >= K || rg.diag == 1) break;  // steps wholly past K add nothing
+      if (16 * s >= K) break;  // steps wholly past K add nothing
       float4 x = xa[s];
       const float4 bb = *reinterpret_cast<const float4 *>(bl + 16 * s);
       if constexpr (DUAL) {
@@ -380,7 +338,6 @@ __global__ __launch_bounds__(64 * (XL_TN_LOADERS + XL_TN_CONSUMERS), 1) void k_x
       xl_release(freed, slot, t, lane);
 #pragma unroll
       for (int q = 0; q < 4; q++) {
-        if (rg.diag == 1) break;
 #pragma unroll
         for (int c = 0; c < KC; c++) {
           float4 x = xa[q][c];
@@ -432,104 +389,6 @@ __global__ __launch_bounds__(64 * (XL_TN_LOADERS + XL_TN_CONSUMERS), 1) void k_x
   }
 }
 
-// TN, K-split form: every consumer reads every group, each its own 64-column chunks of K
-// (XL_KC chunks over XL_TS_CONSUMERS waves: 3, 3, 2, 2), so its accumulators are a few
-// registers and six waves fit (2 loaders + 4 consumers, all four SIMDs running MFMAs).  A
-// slot goes back when every consumer has added its release.  Each consumer sums its output
-// rows k over the workgroup's groups in order and writes them: no cross-wave reduction.
-constexpr int XL_TS_LOADERS = 2, XL_TS_CONSUMERS = 4, XL_TS_MAXC = 3;
-
-template <int NI, bool MASKED, bool FOLD>
-__global__ __launch_bounds__(64 * (XL_TS_LOADERS + XL_TS_CONSUMERS), 1) void k_xs_tn_split(
-    int M, int N, int K, const float *__restrict__ A, int lda, const float *__restrict__ G,
-    int ldg, const uint64_t *__restrict__ maskT, float a_scale, float *__restrict__ partial,
-    XlRing rg) {
-  __shared__ __attribute__((aligned(1024))) char lds[XL_LDS];
-  unsigned *const ready = reinterpret_cast<unsigned *>(lds + XL_LDS - XL_FLAGS);
-  unsigned *const freed = ready + 8;
-  if (threadIdx.x < 16) ready[threadIdx.x] = 0u;
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int g = lane >> 4, i = lane & 15;
-  const int T = xl_groups(M);
-  if (wave < XL_TS_LOADERS) {
-    xl_load<NI, XL_TS_LOADERS, XL_TS_CONSUMERS>(A, lda, M, T, wave, lane, rg, lds, ready, freed);
-    return;
-  }
-  const int cid = wave - XL_TS_LOADERS;
-  const int c0 = cid < 2 ? 3 * cid : 6 + 2 * (cid - 2);  // first chunk: 0, 3, 6, 8
-  const int nc = cid < 2 ? 3 : 2;                          // chunks: 3, 3, 2, 2
-  floatx4 acc[XL_TS_MAXC][4];
-#pragma unroll
-  for (int c = 0; c < XL_TS_MAXC; c++)
-#pragma unroll
-    for (int t = 0; t < 4; t++) acc[c][t] = floatx4{0.f, 0.f, 0.f, 0.f};
-  auto load_rows = [&](int t, float(&bv)[4], uint64_t(&m)[4]) {  // dZ and keep bits, group t
-    const long long row0 = (blockIdx.x + (long long)t * gridDim.x) * 16;
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const long long mr = row0 + 4 * q + g;
-      const long long row = mr < M ? mr : M - 1;
-      const float v = G[row * ldg + (i < N ? i : 0)];
-      bv[q] = (mr < M && i < N) ? (MASKED && FOLD ? v * a_scale : v) : 0.0f;
-      if constexpr (MASKED) m[q] = maskT[row * 16 + i];
-    }
-  };
-  auto group = [&](int t, const float(&bj)[4], const uint64_t(&mw)[4], float(&bjn)[4],
-                   uint64_t(&mwn)[4]) {
-    if (t + 1 < T) load_rows(t + 1, bjn, mwn);
-    const int slot = t % rg.nslot;
-    lds_wait_ge(ready + slot, (unsigned)(t + 1));
-    const char *sp = lds + rg.off + slot * (NI * 1024) + (c0 * 16 + i) * 16;
-    float4 xa[4][XL_TS_MAXC];
-#pragma unroll
-    for (int q = 0; q < 4; q++)
-#pragma unroll
-      for (int c = 0; c < XL_TS_MAXC; c++)
-        if (c < nc) xa[q][c] = *reinterpret_cast<const float4 *>(sp + (4 * q + g) * rg.st * 16 + 256 * c);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_fetch_add(freed + slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    asm volatile("" ::: "memory");
-    if (rg.diag == 1) return;
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-#pragma unroll
-      for (int c = 0; c < XL_TS_MAXC; c++) {
-        if (c < nc) {
-          float4 x = xa[q][c];
-          if constexpr (MASKED)
-            xl_apply4<FOLD>(x, (uint32_t)(mw[q] >> (4 * (c0 + c))) & 0xfu, a_scale);
-          acc[c][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(x.x, bj[q], acc[c][0], 0, 0, 0);
-          acc[c][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(x.y, bj[q], acc[c][1], 0, 0, 0);
-          acc[c][2] = __builtin_amdgcn_mfma_f32_16x16x4f32(x.z, bj[q], acc[c][2], 0, 0, 0);
-          acc[c][3] = __builtin_amdgcn_mfma_f32_16x16x4f32(x.w, bj[q], acc[c][3], 0, 0, 0);
-        }
-      }
-    }
-  };
-  float bja[4] = {0.f, 0.f, 0.f, 0.f}, bjb[4] = {0.f, 0.f, 0.f, 0.f};
-  uint64_t mwa[4] = {0, 0, 0, 0}, mwb[4] = {0, 0, 0, 0};
-  if (T > 0) load_rows(0, bja, mwa);
-  for (int t = 0; t < T; t += 2) {
-    group(t, bja, mwa, bjb, mwb);
-    if (t + 1 < T) group(t + 1, bjb, mwb, bja, mwa);
-  }
-  float *p = partial + (long long)blockIdx.x * K * 16;
-#pragma unroll
-  for (int c = 0; c < XL_TS_MAXC; c++) {
-    if (c < nc) {
-#pragma unroll
-      for (int t = 0; t < 4; t++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int k = 64 * (c0 + c) + 4 * (4 * g + r) + t;
-          if (k < K) p[(long long)k * 16 + i] = acc[c][t][r];
-        }
-    }
-  }
-}
-
 }  // namespace
 
 // a_scale = 2^n (dropout 1/2, 3/4, ...): scaling by it is exact, so it can move
@@ -547,6 +406,7 @@ bool xstream_ring_ok(int K, int lda) {
 void launch_xstream_nn_ring(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
                             int trans_b, float *C, int ldc, const uint64_t *maskT, float a_scale,
                             hipStream_t s, float *C2, const XsEpilogue &e) {
+  note_path(KP_XS_NN_RING);
   PGCN_CHECK(xstream_ring_ok(K, lda) && N <= 16 && ldc <= 16, PGCN_E_INVALID,
              "xstream ring: K in 577..640, lda = K rounded to 4, N <= 16");
   const int ni = xl_ni(lda);
@@ -584,32 +444,7 @@ void launch_xstream_nn_ring(int M, int N, int K, const float *A, int lda, const 
 void launch_xstream_tn_ring(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
                             const uint64_t *maskT, float a_scale, float *partial, int n_blocks,
                             hipStream_t s) {
-  if (g_xstream_tn_split) {
-    PGCN_CHECK(xstream_ring_ok(K, lda) && N <= 16, PGCN_E_INVALID,
-               "xstream ring: K in 577..640, lda = K rounded to 4, N <= 16");
-    const int ni = xl_ni(lda);
-    const XlRing rg = xl_ring(lda, ni, 0);
-    const dim3 grid((unsigned)n_blocks), block(64 * (XL_TS_LOADERS + XL_TS_CONSUMERS));
-    const bool fold = xl_pow2(a_scale);
-#define XTS_CASE(NI)                                                                           \
-  case NI:                                                                                     \
-    if (maskT && fold)                                                                         \
-      hipLaunchKernelGGL((k_xs_tn_split<NI, true, true>), grid, block, 0, s, M, N, K, A, lda,   \
-                         G, ldg, maskT, a_scale, partial, rg);                                 \
-    else if (maskT)                                                                            \
-      hipLaunchKernelGGL((k_xs_tn_split<NI, true, false>), grid, block, 0, s, M, N, K, A, lda,  \
-                         G, ldg, maskT, a_scale, partial, rg);                                 \
-    else                                                                                       \
-      hipLaunchKernelGGL((k_xs_tn_split<NI, false, false>), grid, block, 0, s, M, N, K, A, lda, \
-                         G, ldg, maskT, a_scale, partial, rg);                                 \
-    break;
-    switch (ni) {
-      XTS_CASE(37) XTS_CASE(38) XTS_CASE(39) XTS_CASE(40)
-      default: PGCN_CHECK(false, PGCN_E_INVALID, "xstream ring: no kernel for this row width");
-    }
-#undef XTS_CASE
-    return;
-  }
+  note_path(KP_XS_TN_RING);
   PGCN_CHECK(xstream_ring_ok(K, lda) && N <= 16, PGCN_E_INVALID,
              "xstream ring: K in 577..640, lda = K rounded to 4, N <= 16");
   const int ni = xl_ni(lda);

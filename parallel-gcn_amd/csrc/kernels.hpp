@@ -10,6 +10,14 @@
 
 namespace pgcn {
 
+// Launch counts of the kernel families (process-wide; pgcn_debug_path_count): tests assert
+// which kernels a configuration took
+enum KernelPath {
+  KP_XS_NN_RING, KP_XS_TN_RING, KP_XS_NN, KP_XS_TN, KP_GS_RING, KP_GS_GATHER, KP_OUT_XENT,
+  KP_GEMM_NN, KP_GEMM_TN, KP_COUNT
+};
+void note_path(KernelPath p);
+
 // GraphSum work schedule for one row width (VEC float4 per row); device arrays.
 struct GraphSchedule {
   int vec = 0;
@@ -30,13 +38,10 @@ void launch_graphsum(const GraphSchedule &s, const int *indices, const float *va
                      hipStream_t st, const GsEpilogue *epi = nullptr);
 bool graphsum_vec_supported(int vec);
 
-// ---- d = 16 GraphSum with LDS-staged feature slices (k_graphsum_lds.hip) ----------------
-constexpr int kGraphBlocks = 8;                      // column blocks (one per XCD)
-constexpr int LDS_SR = 1020;                         // feature rows per LDS slice
-constexpr int LDS_ROWS = LDS_SR + 4;                 // + 4 zero rows = 1024 rows = 64 KB, so a
-                                                     //   row's byte offset fits an edge's 16 bits
+// ---- d = 16 GraphSum with LDS-staged feature slices (k_graphsum_ring.hip) -----------------
+constexpr int kGraphBlocks = 8;                      // plain kernel: column blocks (one per XCD)
 constexpr int LDS_CW = 15;                           // summing waves per workgroup
-constexpr int LDS_SLOTS = 16;                        // rowsets (16 rows) per compute wave
+constexpr int LDS_SLOTS = 16;                        // rowsets (16 rows) per summing wave
 constexpr int LDS_THREADS = 64 * (LDS_CW + 1);       // + one slice loader wave
 // Sliding-window ring schedule (k_graphsum_ring.hip, host/ring.cpp): slices of RING_SR rows,
 // a ring of RING_K slices in LDS as 4 quarter planes of RING_P rows, visits read RING_W slices
@@ -56,7 +61,7 @@ constexpr int RING_K = PGCN_RING_K;
 constexpr int RING_W = PGCN_RING_W;
 static_assert(RING_W >= 1 && RING_W <= RING_K - 1 && RING_SR % 64 == 0, "ring shape");
 constexpr int RING_P = RING_K * RING_SR + 4;  // + 4 zero rows; = 4 mod 16 (bank quarters)
-constexpr int kRingWindow = 5;                // LdsSchedule::window of a ring schedule
+constexpr int kRingWindow = 5;                // the schedule kind reported by pgcn_debug_lds_counts
 // ring schedule rows[]: row id | log2(spread) << 28; kRingEmpty = no row (spread kept)
 constexpr int kRingRowMask = 0x0fffffff;
 constexpr int kRingEmpty = 0x0fffffff;
@@ -64,43 +69,24 @@ static_assert(RING_P % 16 == 4, "plane stride: lane v's chunk = 4v + row (mod 16
 struct LdsSchedule {
   int n_rows = 0, n_cols = 0;
   int n_batches = 0;  // workgroups = n_batches * n_blocks
-  int n_blocks = kGraphBlocks;  // column blocks (workgroup w serves block w % n_blocks)
+  int n_blocks = 4;   // column blocks (workgroup w serves block w % n_blocks)
   int t_max = 0;      // max slices per column block
   const uint2 *entries = nullptr;            // [kb][16 lane groups] x 4 uint16 row offsets
   const long long *wave_off = nullptr;       // [wg][LDS_CW] first kb of each wave's stream
   const unsigned short *counts = nullptr;    // [wg][t_max][LDS_CW][LDS_SLOTS] steps
   const int2 *slices = nullptr;              // [block][t_max] {first column, rows}
   const int *n_slices = nullptr;             // [block]
-  const int *rows = nullptr;                 // [batch][LDS_CW][LDS_SLOTS][16] row or -1
+  const int *rows = nullptr;                 // [batch][LDS_CW][LDS_SLOTS][16] row | spread
   const float *row_scale = nullptr;          // 1/sqrt(deg) of output rows
   const float *col_scale = nullptr;          // 1/sqrt(deg) of input rows
-  // window 2: counts are per window base J; per entry block 4 lane masks (one per step) of
-  // the lanes whose edge belongs to slot J+1 (the others add into slot J)
-  int window = 1;
-  const uint64_t *masks = nullptr;           // [kb][4]
-  // ring schedule: per batch, the arrivals of its column blocks' workgroups (zeroed; the
-  // fused combine of k_graphsum_ring leaves it zeroed)
-  int *arrive = nullptr;
 };
-// ring schedule (window == kRingWindow): scratch_in holds ceil(n_cols / RING_SR) slices
-// prestaged: scratch_in already holds this call's prescaled input (written by the epilogue of
-// the GraphSum that produced `in`), the prescale launch is skipped
+// prescale (skipped when `prestaged`: scratch_in already holds this call's prescaled input,
+// written by the epilogue of the kernel that produced `in`) + ring kernel + combine (+ epi);
+// scratch_in holds ceil(n_cols / RING_SR) slices
 void launch_graphsum_ring(const LdsSchedule &s, const float *in, int ld_in, float *out,
                           int ld_out, float *scratch_in, float *partial, hipStream_t st,
                           const int *col_map = nullptr, const GsEpilogue *epi = nullptr,
-                          bool prestaged = false, bool combine = true);
-// rows wider than 16 on the ring schedule: one prescale launch for all 16-column passes
-// (tables: n_pass x table_floats), a ring launch per pass (partials: n_pass x partial_floats),
-// one combine launch writing whole rows (+ the epilogue)
-void launch_graphsum_ring_wide(const LdsSchedule &s, const float *in, int ld_in, float *out,
-                               int ld_out, int dim, float *tables, long long table_floats,
-                               float *partials, long long partial_floats, hipStream_t st,
-                               const int *col_map = nullptr, const GsEpilogue *epi = nullptr);
-void launch_gs_lds_combine(const LdsSchedule &s, const float *partial, float *out, int ld_out,
-                           hipStream_t st, const GsEpilogue *epi = nullptr);
-void launch_graphsum_lds(const LdsSchedule &s, const float *in, int ld_in, float *out,
-                         int ld_out, float *scratch_in, float *partial, hipStream_t st,
-                         const int *col_map = nullptr, const GsEpilogue *epi = nullptr);
+                          bool prestaged = false);
 
 void launch_gemm_nn(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
                     int trans_b, float *C, int ldc, const uint64_t *a_mask, long long mask_base,

@@ -1,15 +1,15 @@
 #!/bin/bash
-# SQ counter passes over the ring GraphSum (tools/gs_ring_sweep.py, one setting), one pass per
-# counter group.  usage: scripts/pmc_ring.sh <outdir-under-gpurun_out> <spread,balance,prio>
+# SQ counter passes over the ring GraphSum (tools/gs_call.py: d = 16 calls on reddit-114M), one
+# pass per counter group.  usage: scripts/pmc_ring.sh <outdir-under-gpurun_out> [calls]
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out/${1:-pmc_ring}; CFG=${2:-60,0,1}
+OUT=gpurun_out/${1:-pmc_ring}; CFG=${2:-5}
 mkdir -p "$OUT"
 ROOT=$(pwd)
 cd /tmp && export TMPDIR=/tmp && cd "$ROOT"
 pass() {  # name, counters...
   local name=$1; shift
-  timeout -s KILL 120 rocprofv3 --pmc "$@" -d "$OUT/$name" -o run -f csv -- python3 tools/gs_ring_sweep.py $CFG \
+  timeout -s KILL 120 rocprofv3 --pmc "$@" -d "$OUT/$name" -o run -f csv -- python3 tools/gs_call.py $CFG \
       > "$OUT/$name.log" 2>&1
   local rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || tail -5 "$OUT/$name.log"; return $rc
 }

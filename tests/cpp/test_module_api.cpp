@@ -5,12 +5,23 @@
 //     GCN constructor does (src/gcn.cpp:64-128: Dropout, SparseMatmul, GraphSum, ReLU,
 //     Dropout, Matmul, GraphSum, CrossEntropyLoss, Adam over {W1 decayed, W2}) and runs its
 //     train_epoch / eval(2) (src/gcn.cpp:179-212: loss + l2 penalty of W1, accuracy);
+//   test_module_api streams <root> <name> <epochs>
+//     the same modules wired to the CUDA reference's streams and events (src/gcn.cu:5-11,
+//     47-143, 293-343; src/module.cu; src/optim.cu:57-95): training forward on
+//     forward_training_stream, backward on backward_streams[0], Matmul's weight gradient on
+//     backward_streams[1] after start_matmul_backward, Adam's first weight on [0] and the other
+//     on [1] recording start_matmul_forward, eval on forward_evaluation_stream waiting for them;
 //   test_module_api gcn <root> <name> <epochs>
-//     the same epochs through pgcn::api::GCN (the fused engine).
+//     the same epochs through pgcn::api::GCN (the fused engine);
+//   test_module_api twographs <root> <name> 0
+//     two GraphSums on one DevSparseIndex with different values (Â and 2 Â): each keeps its own
+//     device graph; prints "twographs ok" when the second's output is twice the first's.
 // Prints one line per epoch: "epoch=<e> <train_loss> <train_acc> <val_loss> <val_acc>" (%.9g);
 // tests/test_gpu_engine.py compares them with the reference's golden epoch lines.
 #include <pgcn.hpp>
 
+#include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <exception>
@@ -38,7 +49,7 @@ int main(int argc, char **argv) {
 
 static int run(int argc, char **argv) {
   if (argc < 5) {
-    fprintf(stderr, "usage: %s modules|gcn <root> <name> <epochs>\n", argv[0]);
+    fprintf(stderr, "usage: %s modules|streams|gcn|twographs <root> <name> <epochs>\n", argv[0]);
     return 2;
   }
   const std::string mode = argv[1];
@@ -64,9 +75,44 @@ static int run(int argc, char **argv) {
     return 0;
   }
 
+  if (mode == "twographs") {
+    DevSparseIndex graph(data.graph);
+    std::vector<real> v1 = data.graph_value, v2 = data.graph_value;
+    for (auto &x : v2) x *= 2.0f;
+    real *d1 = nullptr, *d2 = nullptr;
+    (void)hipMalloc(&d1, sizeof(real) * v1.size());
+    (void)hipMalloc(&d2, sizeof(real) * v2.size());
+    (void)hipMemcpy(d1, v1.data(), sizeof(real) * v1.size(), hipMemcpyHostToDevice);
+    (void)hipMemcpy(d2, v2.data(), sizeof(real) * v2.size(), hipMemcpyHostToDevice);
+    auto in = std::make_shared<Variable>(N * H), o1 = std::make_shared<Variable>(N * H),
+         o2 = std::make_shared<Variable>(N * H);
+    GraphSum gs1(in, o1, &graph, d1, H);
+    GraphSum gs2(in, o2, &graph, d2, H);  // a second graph on the same index
+    std::vector<real> x((size_t)N * H);
+    for (size_t i = 0; i < x.size(); i++) x[i] = (real)((i * 2654435761u) % 1000) / 500.0f - 1.0f;
+    in->from_host(x);
+    smart_stream st;
+    gs1.forward(false, st);
+    gs2.forward(false, st);
+    st.sync();
+    const std::vector<real> a = o1->to_host(), b = o2->to_host();
+    double worst = 0;
+    for (size_t i = 0; i < a.size(); i++)
+      worst = std::max(worst, std::fabs((double)b[i] - 2.0 * a[i]) / (std::fabs(2.0 * a[i]) + 1e-6));
+    (void)hipFree(d1);
+    (void)hipFree(d2);
+    printf("twographs %s max_rel=%.3g\n", worst <= 1e-5 ? "ok" : "BAD", worst);
+    return worst <= 1e-5 ? 0 : 1;
+  }
+
   Variable::initialize_random();
+  const bool streams = mode == "streams";
   smart_stream stream;
-  smart_event ev_fwd, ev_input, ev_bwd, ev_mm_f, ev_mm_b, ev_ce;
+  smart_event ev_fwd, ev_input, ev_bwd, ev_mm_f, ev_mm_b, ev_ce, trash;
+  // the CUDA reference's GCNSmartObjects (src/gcn.cu:5-11) for the streams mode
+  smart_stream forward_training, forward_evaluation;
+  std::vector<smart_stream> backward_streams(2);
+  std::vector<smart_event> start_matmul_forward(2);
   DevSparseIndex feat_index(data.feature_index), graph(data.graph);
   integer *dev_truth = nullptr;
   (void)hipMalloc(&dev_truth, sizeof(integer) * N);
@@ -86,24 +132,33 @@ static int run(int argc, char **argv) {
   auto W1 = std::make_shared<Variable>(F * H, true, true, F, H);
   W1->glorot();
   modules.push_back(std::make_unique<SparseMatmul>(input, W1, l1_var1, &feat_index, N, F, H,
-                                                   ev_fwd, ev_input));
+                                                   streams ? start_matmul_forward[0] : ev_fwd,
+                                                   ev_input));
   auto l1_var2 = std::make_shared<Variable>(N * H);
   modules.push_back(std::make_unique<GraphSum>(l1_var1, l1_var2, &graph, dev_graph_value, H,
-                                               false, ev_bwd));
+                                               false, trash));
   modules.push_back(std::make_unique<ReLU>(l1_var2));
   modules.push_back(std::make_unique<Dropout>(l1_var2, p));
   auto l2_var1 = std::make_shared<Variable>(N * C);
   auto W2 = std::make_shared<Variable>(H * C, true, true, H, C);
   W2->glorot();
-  modules.push_back(std::make_unique<Matmul>(l1_var2, W2, l2_var1, N, H, C, ev_mm_f, ev_mm_b,
-                                             stream));
+  modules.push_back(std::make_unique<Matmul>(l1_var2, W2, l2_var1, N, H, C,
+                                             streams ? start_matmul_forward[1] : ev_mm_f,
+                                             ev_mm_b, streams ? backward_streams[1] : stream));
   auto output = std::make_shared<Variable>(N * C);
+  // the output GraphSum's backward fires the Matmul's weight gradient (generate_event)
   modules.push_back(std::make_unique<GraphSum>(l2_var1, output, &graph, dev_graph_value, C,
-                                               false, ev_bwd));
+                                               streams, streams ? ev_mm_b : ev_bwd));
   auto ce = std::make_unique<CrossEntropyLoss>(output, dev_truth, &loss, C, ev_ce);
   CrossEntropyLoss *cep = ce.get();
   modules.push_back(std::move(ce));
-  Adam optimizer({W1, W2}, {true, false}, &adam);
+  std::unique_ptr<Adam> opt_holder =
+      streams ? std::make_unique<Adam>(std::vector<shared_ptr<Variable>>{W1, W2},
+                                       std::vector<bool>{true, false}, &adam, backward_streams,
+                                       start_matmul_forward, forward_training)
+              : std::make_unique<Adam>(std::vector<shared_ptr<Variable>>{W1, W2},
+                                       std::vector<bool>{true, false}, &adam);
+  Adam &optimizer = *opt_holder;
 
   auto l2_penalty = [&]() {  // hpdga gcn.cpp:166-173 (float, element order)
     const std::vector<real> w = W1->to_host();
@@ -113,6 +168,27 @@ static int run(int argc, char **argv) {
   };
   auto pass = [&](natural split, bool training) {
     const std::vector<integer> t = truth_of(data, split);  // set_truth (src/gcn.cpp:136-147)
+    if (streams) {
+      const smart_stream &fs = training ? forward_training : forward_evaluation;
+      fs.sync();
+      (void)hipMemcpy(dev_truth, t.data(), sizeof(integer) * N, hipMemcpyHostToDevice);
+      natural labelled = 0;
+      for (integer x : t) labelled += x >= 0;
+      cep->set_num_samples(labelled);
+      // eval's first GraphSum rewrites layer1_var2, which the last W2.grad (on
+      // backward_streams[1]) reads: the reference leaves that open until eval's Matmul waits
+      // for W2's step; the harness closes it up front (same event)
+      if (!training) start_matmul_forward[1].wait(fs);
+      for (auto &m : modules) m->forward(training, fs);
+      fs.sync();  // finalize (src/gcn.cu:453-471)
+      const float l = loss + l2_penalty(), acc = cep->accuracy();
+      if (training) {
+        for (int i = (int)modules.size() - 1; i >= 0; i--)
+          modules[(size_t)i]->backward(backward_streams[0]);
+        optimizer.step();
+      }
+      return std::make_pair(l, acc);
+    }
     stream.sync();
     (void)hipMemcpy(dev_truth, t.data(), sizeof(integer) * N, hipMemcpyHostToDevice);
     natural labelled = 0;

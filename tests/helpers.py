@@ -111,6 +111,24 @@ class OracleGCN:
         self.lib.or_gcn_eval(self.h, split, ptr(out))
         return float(out[0]), float(out[1])
 
+    def logits(self):
+        """The output variable (the logits of the last forward, max-shifted on labelled rows)."""
+        return self.var(self.lib.or_gcn_num_vars(self.h) - 1)
+
+    def epoch_with_ties(self, label, split, c, tol=1e-5):
+        """train_epoch() + eval(2), and the near-tied rows of each pass's logits (near_ties):
+        the accuracy tolerance of assert_line_close."""
+        tr = self.train_epoch()
+        t1 = near_ties(self.logits(), label, split, 1, c, tol)
+        ev = self.eval(2)
+        t2 = near_ties(self.logits(), label, split, 2, c, tol)
+        return tr + ev, {1: t1, 2: t2}
+
+    def eval_with_ties(self, split_id, label, split, c, tol=1e-5):
+        """eval(split_id) and the near-tied rows of its logits."""
+        r = self.eval(split_id)
+        return r, near_ties(self.logits(), label, split, split_id, c, tol)
+
     def var(self, idx, which=0):
         n = self.lib.or_gcn_get_var(self.h, idx, which, None)
         out = np.zeros(max(n, 0), np.float32)
@@ -193,13 +211,11 @@ def parse_line(line):
 
 
 # --------------------------------------------------------------------------- engine knobs
-# pgcn_debug_set defaults of the engine (parallel-gcn_amd/csrc/host/gcn.cpp)
+# pgcn_debug_set defaults of the engine (include/pgcn.h; parallel-gcn_amd/csrc/host/gcn.cpp)
 ENGINE_DEFAULTS = {"train_ahead": 1, "split_rows": 0, "split_cols": 1, "eval_ax": 1,
-                   "epoch_graph": 0, "mask_side": 0, "fuse_epilogue": 1,
-                   "graphsum_ring_fused": 0, "graphsum_prestage": 1, "xstream_epilogue": 1,
-                   "xstream_ring": 1, "xstream_ring_inflight": 1, "xstream_tn_split": 0, "fuse_output": 1, "fuse_output_bwd": 1, "fuse_output_wgrad": 1,
-                   "mm_side": 0, "graphsum_ring_wide": 0,
-                   "lds_min_kb": -1, "blocked_min_kb": -1}
+                   "epoch_graph": 0, "fuse_epilogue": 7, "fuse_output": 2, "mm_side": 0,
+                   "xstream_ring": 1, "gemm_variant": 0, "lds_min_kb": -1, "lds_blocks": 0,
+                   "parse_threads": 0}
 
 
 @contextlib.contextmanager
@@ -219,11 +235,31 @@ def split_counts(ds):
     return {s: int(((sp == s) & (lab >= 0)).sum()) for s in (1, 2, 3)}
 
 
-def assert_line_close(ours, want, counts, rtol=1e-4, what=""):
+def near_ties(logits, label, split, sp, c, tol=1e-5):
+    """Labelled rows of split `sp` whose true-class logit is within tol (relative to the row's
+    largest |logit|, at least tol absolute) of the largest other logit in the oracle's logits:
+    the only rows whose correct/wrong verdict a last-bits difference of the logits can flip."""
+    z = np.asarray(logits, np.float64).reshape(-1, c)
+    lab, spl = np.asarray(label), np.asarray(split)
+    rows = np.nonzero((spl[:len(z)] == sp) & (lab[:len(z)] >= 0))[0]
+    if len(rows) == 0:
+        return 0
+    zr, lr = z[rows], lab[rows]
+    idx = np.arange(len(rows))
+    zl = zr[idx, lr].copy()
+    zr[idx, lr] = -np.inf
+    gap = np.abs(zl - zr.max(axis=1))
+    zr[idx, lr] = zl
+    return int((gap <= tol * np.maximum(1.0, np.abs(zr).max(axis=1))).sum())
+
+
+def assert_line_close(ours, want, counts, rtol=1e-4, what="", ties=None):
     """One epoch line (train_loss, train_acc, val_loss, val_acc) against the oracle's: losses
-    within rtol (the north star's 1e-4), accuracies within max(2 rows, 0.5 %) of the split."""
+    within rtol (the north star's 1e-4); accuracies within `ties[split]` rows (the oracle's
+    near-tied rows of that pass, near_ties) when given, else within 2 rows."""
     for k in (0, 2):
         assert abs(ours[k] - want[k]) <= rtol * abs(want[k]), (what, k, ours, want)
     for k, sp in ((1, 1), (3, 2)):
-        assert abs(ours[k] - want[k]) * counts[sp] <= max(2.0, 0.005 * counts[sp]) + 1e-3, \
-            (what, k, ours, want)
+        allowed = 2 if ties is None else ties[sp]
+        assert abs(ours[k] - want[k]) * counts[sp] <= allowed + 1e-3, \
+            (what, k, ours, want, f"allowed {allowed} rows")

@@ -2,8 +2,9 @@
 
 Tolerances (north star: "within 1e-4 relative on loss/logits, integer indexing bit-exact"):
   * loss values: |ours - ref| <= 1e-4 * |ref| per epoch line, all 100 epochs;
-  * accuracies: a count difference of at most max(2, 0.5 %) of the labelled rows (ties and
-    near-ties of logits may flip a row when fp32 summation orders differ);
+  * accuracies: a count difference of at most 2 labelled rows per split (near-ties of logits
+    may flip a row when fp32 summation orders differ; the large-graph tests count the oracle's
+    near-tied rows instead, tests/test_gpu_parity_large.py);
   * integer/bit work bit-exact: dropout masks (compared through the dropped input and the
     hidden activations' zero pattern), the parsed CSR, labels/splits;
   * tensors after epoch 1: rtol 1e-4 / atol 1e-6 (SpMM over sparse X is bit-exact).
@@ -58,8 +59,24 @@ def engine_runs(loaded, pgcn):
     return _run_all(loaded, pgcn)
 
 
+@pytest.fixture(scope="module")
+def oracle_ties(loaded):
+    """Per dataset, the oracle's near-tied rows (within 1e-4 of a tie, the north star's logit
+    tolerance: after 100 Adam epochs the logits carry that much drift) of every pass of the
+    100 epochs and of eval(3): the accuracy tolerance of test_epoch_lines (the oracle is
+    bit-exact with the reference build, tests/test_oracle_pinned.py)."""
+    out = {}
+    for name in DATASETS:
+        ds = loaded[name]
+        ref = helpers.OracleGCN(helpers.ds_dict(ds))
+        ties = [ref.epoch_with_ties(ds.label, ds.split, ds.output_dim, tol=1e-4)[1]
+                for _ in range(100)]
+        out[name] = (ties, ref.eval_with_ties(3, ds.label, ds.split, ds.output_dim, tol=1e-4)[1])
+    return out
+
+
 @pytest.mark.parametrize("name", DATASETS)
-def test_epoch_lines(engine_runs, name):
+def test_epoch_lines(engine_runs, oracle_ties, name):
     runs = engine_runs
     gold = helpers.golden(name)["epoch_lines"].reshape(-1, 4)
     ours = runs[name]["lines"]
@@ -67,14 +84,17 @@ def test_epoch_lines(engine_runs, name):
     for col in (0, 2):  # losses
         rel = np.abs(ours[:, col] - gold[:, col]) / np.abs(gold[:, col])
         assert rel.max() <= 1e-4, f"{name} loss col {col}: max rel {rel.max():.3g}"
-    for col, split in ((1, 1), (3, 2)):  # accuracies
+    ties, test_ties = oracle_ties[name]
+    for col, split in ((1, 1), (3, 2)):  # accuracies: only near-tied rows may differ
         dcount = np.abs(ours[:, col] - gold[:, col]) * cnt[split]
-        assert dcount.max() <= max(2.0, 0.005 * cnt[split]) + 1e-3, \
-            f"{name} acc col {col}: max row diff {dcount.max():.2f}"
+        allowed = np.array([t[split] for t in ties], np.float64)
+        bad = np.nonzero(dcount > allowed + 1e-3)[0]
+        assert len(bad) == 0, (f"{name} acc col {col}: epochs {bad + 1} differ by "
+                               f"{dcount[bad]} rows, near-ties {allowed[bad]}")
     tl, ta = runs[name]["test"]
     gt = helpers.golden(name)["test_scalars"]
     assert abs(tl - gt[0]) <= 1e-4 * abs(gt[0])
-    assert abs(ta - gt[1]) * cnt[3] <= max(2.0, 0.005 * cnt[3]) + 1e-3
+    assert abs(ta - gt[1]) * cnt[3] <= test_ties + 1e-3
 
 
 @pytest.mark.parametrize("split_rows", [0, 1])
@@ -258,9 +278,8 @@ def test_train_ahead_bit_identical(pgcn):
     p = pgcn.make_params(ds)
     runs = []
     pgcn.lib.pgcn_debug_set(b"eval_ax", 0)  # eval streams X (else it reads Â X instead)
-    for ahead, side in ((1, 0), (1, 1), (0, 0)):
+    for ahead in (1, 0):
         pgcn.lib.pgcn_debug_set(b"train_ahead", ahead)
-        pgcn.lib.pgcn_debug_set(b"mask_side", side)  # next mask drawn beside the W1-grad pass
         g = pgcn.GCN(p, ds, device=0)
         lines = []
         for e in range(6):
@@ -276,7 +295,6 @@ def test_train_ahead_bit_identical(pgcn):
         runs.append(lines)
         g.close()
     pgcn.lib.pgcn_debug_set(b"train_ahead", 1)
-    pgcn.lib.pgcn_debug_set(b"mask_side", 0)
     pgcn.lib.pgcn_debug_set(b"eval_ax", 1)
     for other in runs[1:]:
         for a, b in zip(runs[0], other):
@@ -397,19 +415,14 @@ def test_part2_configs_match_oracle(datasets, pgcn, name):
     ref = helpers.OracleGCN(helpers.ds_dict(ds), hidden_dims=cfg["hidden"],
                             dropouts=cfg["dropouts"], wd=cfg["wd"], seed=cfg["seed"])
     cnt = _counts(ds)
-    for _ in range(15):
-        ours = g.train_epoch() + g.eval(2)
-        want = ref.train_epoch() + ref.eval(2)
-        for k in (0, 2):
-            assert abs(ours[k] - want[k]) <= 1e-4 * abs(want[k]), (ours, want)
-        for k, sp in ((1, 1), (3, 2)):
-            assert abs(ours[k] - want[k]) * cnt[sp] <= max(2, 0.005 * cnt[sp]), (ours, want)
+    for e in range(15):
+        helpers.assert_line_close(g.train_epoch() + g.eval(2), ref.train_epoch() + ref.eval(2),
+                                  cnt, what=f"epoch {e + 1}")
     g.close()
 
 
-def _fused_run(pgcn, ds, fuse, epochs, prestage=1, xs=1, **make):
-    with helpers.knobs(pgcn, fuse_epilogue=fuse, graphsum_prestage=prestage,
-                       xstream_epilogue=xs):
+def _fused_run(pgcn, ds, fuse, epochs, **make):
+    with helpers.knobs(pgcn, fuse_epilogue=fuse):
         g = pgcn.GCN(pgcn.make_params(ds, **make), ds)
         lines = [g.train_epoch() + g.eval(2) for _ in range(epochs)]
         g.train_epoch()  # tensors of a training pass: relu/dropout forward and backward
@@ -426,9 +439,9 @@ def test_fused_epilogue_bit_identical(loaded, pgcn, case):
     the same bits as the separate kernels: epoch lines, weights, the hidden activations and
     their gradients (gs_epilogue.hpp; plain gather kernels on cora, LDS ring + combine on the
     dense graph, where the epilogue also writes the next GraphSum's prescaled input table and
-    that GraphSum skips its prescale: compared with graphsum_prestage 0 too; and the first
-    layer's X-stream product applying the eval ReLU / writing the ring tables, compared with
-    xstream_epilogue 0)."""
+    that GraphSum skips its prescale: compared without that bit too; and the first layer's
+    X-stream product applying the eval ReLU / writing the ring tables, compared without it:
+    fuse_epilogue 7 = all, 0 = none, 5 = no prestaged tables, 3 = no X-stream epilogue)."""
     if case == "lds_dense":
         ds, make, tails = pgcn.Dataset.synthetic(120000, 64, 41, 1500000, 21), {}, 2
     elif case == "lds_deep":  # 128-wide rows: the tails ride the wide (all-pass) combine
@@ -437,10 +450,10 @@ def test_fused_epilogue_bit_identical(loaded, pgcn, case):
     else:
         ds = loaded["cora"]
         make, tails = ({"hidden_dims": (4,)}, 2) if case == "cora_h4" else ({}, 1)
-    on = _fused_run(pgcn, ds, 1, 4, **make)
+    on = _fused_run(pgcn, ds, 7, 4, **make)
     off = _fused_run(pgcn, ds, 0, 4, **make)
-    no_stage = _fused_run(pgcn, ds, 1, 4, prestage=0, **make)
-    no_xs = _fused_run(pgcn, ds, 1, 4, xs=0, **make)
+    no_stage = _fused_run(pgcn, ds, 5, 4, **make)
+    no_xs = _fused_run(pgcn, ds, 3, 4, **make)
     assert on["tails"] == tails and off["tails"] == 0
     for other in (off, no_stage, no_xs):
         np.testing.assert_array_equal(on["lines"], other["lines"])
@@ -460,8 +473,8 @@ def test_fused_output_layer_bit_identical(loaded, pgcn, case):
     else:
         ds, make = loaded["cora"], {"hidden_dims": (4,)}
     runs = {}
-    for fo in (1, 0):  # 1: the logits and (fuse_output_bwd, default) the input grad fused
-        with helpers.knobs(pgcn, fuse_output=fo, fuse_output_wgrad=0):
+    for fo in (1, 0):  # 1: the logits and the input grad fused (no weight-grad partials)
+        with helpers.knobs(pgcn, fuse_output=fo):
             g = pgcn.GCN(pgcn.make_params(ds, **make), ds)
             lines = np.array([g.train_epoch() + g.eval(2) for _ in range(3)], np.float32)
             g.train_epoch()
@@ -475,7 +488,7 @@ def test_fused_output_layer_bit_identical(loaded, pgcn, case):
 @pytest.mark.parametrize("case", ["lds_dense", "cora_h4"])
 def test_fused_output_weight_grad_close(loaded, pgcn, case):
     """The loss kernel's per-block partials of W2.grad, reduced in block order
-    (fuse_output_wgrad): the same sums as k_gemm_tn's in another grouping -- W2.grad of the
+    (fuse_output 2 / 3): the same sums as k_gemm_tn's in another grouping -- W2.grad of the
     first step within 2e-6 relative of the k_gemm_tn one, and the epoch lines after it within
     float rounding (LDS-path graph, 41 classes, hidden 16; cora at hidden 4, 7 classes: a
     grad tile narrower than the waves' partials, which the launch then sizes the LDS for)."""
@@ -484,35 +497,19 @@ def test_fused_output_weight_grad_close(loaded, pgcn, case):
     else:
         ds, make = loaded["cora"], {"hidden_dims": (4,)}
     runs = {}
-    for wg in (2, 0):  # 2: fused on any graph size (1, the default, from 65,536 rows)
-        with helpers.knobs(pgcn, fuse_output_wgrad=wg):
+    for wg in (3, 1):  # 3: the partials on any graph size (2, the default, from 65,536 rows)
+        with helpers.knobs(pgcn, fuse_output=wg):
             g = pgcn.GCN(pgcn.make_params(ds, **make), ds)
             first = g.train_epoch()
             w2g = g.get_var(5, 1).copy()
             lines = [first] + [g.train_epoch() + g.eval(2) for _ in range(3)]
             runs[wg] = (np.array(lines[0]), np.array(lines[1:], np.float64), w2g)
             g.close()
-    np.testing.assert_array_equal(runs[2][0], runs[0][0])  # the first forward: same bits
-    scale = np.abs(runs[0][2]).max()
-    assert np.abs(runs[2][2] - runs[0][2]).max() <= 2e-6 * scale
+    np.testing.assert_array_equal(runs[3][0], runs[1][0])  # the first forward: same bits
+    scale = np.abs(runs[1][2]).max()
+    assert np.abs(runs[3][2] - runs[1][2]).max() <= 2e-6 * scale
     # the losses after it agree to float rounding (accuracies may flip a near-tied row)
-    np.testing.assert_allclose(runs[2][1][:, [0, 2]], runs[0][1][:, [0, 2]], rtol=2e-5)
-
-
-def test_xstream_ring_engine_matches_register_kernels(pgcn):
-    """The loader / MFMA-wave split of the first layer's X-stream products (k_xstream_lds.hip,
-    default) against the register-streamed kernels in a whole run (dense 64-feature graph,
-    LDS GraphSum): the forward products are bit-identical, W1.grad sums the same rows in
-    another order, so epoch lines agree to float rounding."""
-    ds = pgcn.Dataset.synthetic(120000, 64, 41, 1500000, 21)
-    lines = {}
-    for ring in (1, 0):
-        with helpers.knobs(pgcn, xstream_ring=ring):
-            g = pgcn.GCN(pgcn.make_params(ds), ds)
-            lines[ring] = np.array([g.train_epoch() + g.eval(2) for _ in range(4)], np.float64)
-            g.close()
-    np.testing.assert_allclose(lines[1], lines[0], rtol=2e-5, atol=1e-6)
-    np.testing.assert_array_equal(lines[1][0, :2], lines[0][0, :2])  # epoch 1 forward: NN only
+    np.testing.assert_allclose(runs[3][1][:, [0, 2]], runs[1][1][:, [0, 2]], rtol=2e-5)
 
 
 def test_early_stopping_matches_reference(datasets, pgcn):
@@ -550,21 +547,29 @@ def test_early_stopping_matches_reference(datasets, pgcn):
     g.close()
 
 
-@pytest.mark.parametrize("mode", ["modules", "gcn"])
-def test_cpp_module_api_matches_reference(datasets, pgcn, mode):
-    """The reference-shaped C++ API (include/pgcn.hpp) from a C++ program
-    (tests/cpp/test_module_api.cpp): "modules" assembles the 2-layer GCN from Variable,
-    Dropout, SparseMatmul, GraphSum, ReLU, Matmul, CrossEntropyLoss and Adam objects exactly
-    as hpdga-spring23's GCN constructor does and runs its train_epoch / eval(2); "gcn" runs
-    pgcn::api::GCN.  All 100 cora epoch lines against the reference's golden lines (losses
-    1e-4 relative, accuracies within the usual row tolerance)."""
+def _cpp_api(datasets, mode, epochs):
     import os
     import subprocess
     root, names = datasets
     exe = os.path.join(os.path.dirname(helpers.__file__), "..", "parallel-gcn_amd", "bin",
                        "test_module_api")
-    out = subprocess.run([exe, mode, root, names["cora"], "100"], capture_output=True, text=True,
-                         timeout=300)
+    return subprocess.run([exe, mode, root, names["cora"], str(epochs)], capture_output=True,
+                          text=True, timeout=300)
+
+
+@pytest.mark.parametrize("mode", ["modules", "streams", "gcn"])
+def test_cpp_module_api_matches_reference(datasets, pgcn, mode):
+    """The reference-shaped C++ API (include/pgcn.hpp) from a C++ program
+    (tests/cpp/test_module_api.cpp): "modules" assembles the 2-layer GCN from Variable,
+    Dropout, SparseMatmul, GraphSum, ReLU, Matmul, CrossEntropyLoss and Adam objects exactly
+    as hpdga-spring23's GCN constructor does and runs its train_epoch / eval(2); "streams"
+    wires the same modules to the CUDA reference's streams and events (training forward,
+    backward, Matmul weight gradient + Adam on a second backward stream, eval on its own
+    stream; src/gcn.cu:5-11, src/module.cu, src/optim.cu:57-95), which the API honours; "gcn"
+    runs pgcn::api::GCN.  All 100 cora epoch lines against the reference's golden lines
+    (losses 1e-4 relative, accuracies within 2 rows)."""
+    root, names = datasets
+    out = _cpp_api(datasets, mode, 100)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = np.array([[float(x) for x in ln.split()[1:]] for ln in out.stdout.splitlines()
                       if ln.startswith("epoch=")], np.float64)
@@ -575,18 +580,26 @@ def test_cpp_module_api_matches_reference(datasets, pgcn, mode):
         helpers.assert_line_close(lines[e], gold[e], cnt, what=f"{mode} epoch {e + 1}")
 
 
+def test_cpp_two_graphsums_on_one_index(datasets):
+    """Two GraphSums on one DevSparseIndex with different values (Â and 2 Â) each keep their
+    own device graph (the first one's graph is not freed when the second is built): the second
+    output is twice the first (include/pgcn.hpp DevSparseIndex::graph)."""
+    out = _cpp_api(datasets, "twographs", 0)
+    assert out.returncode == 0 and "twographs ok" in out.stdout, out.stdout + out.stderr[-2000:]
+
+
 @pytest.mark.parametrize("case", ["cora", "lds_dense"])
 def test_matmul_side_stream_bit_identical(loaded, pgcn, case):
     """Matmul weight gradients on the side stream (mm_side, joined before the optimizer) give
     the same bits as the in-order launches: epoch lines and weights after 4 epochs (cora: the
     reference module order, W2.grad beside Dropout/ReLU/GraphSum backward; the dense LDS
     graph: the reassociated output layer, W2.grad beside both backward GraphSums; both with
-    k_gemm_tn for W2.grad, as the loss kernel's partials (fuse_output_wgrad) are off beside
+    k_gemm_tn for W2.grad, as the loss kernel's partials (fuse_output 2) are off beside
     mm_side)."""
     ds = loaded["cora"] if case == "cora" else pgcn.Dataset.synthetic(120000, 64, 41, 1500000, 21)
     runs = []
     for side in (2, 0):  # 2: on whatever the graph size
-        with helpers.knobs(pgcn, mm_side=side, fuse_output_wgrad=0):
+        with helpers.knobs(pgcn, mm_side=side, fuse_output=1):
             g = pgcn.GCN(pgcn.make_params(ds), ds)
             lines = np.array([g.train_epoch() + g.eval(2) for _ in range(4)], np.float32)
             runs.append((lines, g.get_var(2), g.get_var(5)))

@@ -16,7 +16,6 @@ import helpers
 pytestmark = pytest.mark.gpu
 
 DEV = "cuda"
-LDS_WINDOW_DEFAULT = 5  # host/graph.cpp g_graphsum_lds_window (the ring schedule)
 
 
 def vp(t):
@@ -78,18 +77,10 @@ def abs_bound(indptr, indices, x, dim):
     (5000, 8, 3, 2),         # pubmed-like C = 3
     (5000, 8, 7, 2),         # cora C = 7
     (20000, 10, 128, 3),     # 4-layer hidden 128
-    (120000, 40, 16, -2),    # LDS path, window-2 schedule (two-slot runs, exec-masked adds)
-    (120000, 40, 16, -3),    # LDS path, window-3 schedule (slot pairs interleaved)
-    (120000, 40, 16, -4),    # LDS path, window-4 schedule (8-step blocks, exact step counts)
-    (120000, 40, 16, -1),    # LDS path, window-1 schedule (4-step blocks)
-    (120000, 40, 16, -5),    # LDS path, ring schedule (visits over 3 resident slices)
+    (120000, 40, 16, 20),    # the same graph, LDS ring path (the table exceeds 1 MB)
+    (150000, 60, 16, 40),    # LDS ring path, more hubs (spread rows over 2..16 lane groups)
 ])
 def test_graphsum_vs_oracle(pgcn, n, deg, dim, hubs):
-    # LDS path (d = 16, table > L2): default window 1 (slots one after another); hubs < 0
-    # selects window -hubs (with 20 hubs)
-    window = -hubs if hubs < 0 else LDS_WINDOW_DEFAULT
-    hubs = 20 if hubs < 0 else hubs
-    pgcn.lib.pgcn_debug_set(b"graphsum_lds_window", window)  # schedules built from here on
     indptr, indices = random_graph(n, deg, seed=n + dim, hubs=hubs, hub_deg=3000)
     ld = (dim + 3) // 4 * 4
     rng = np.random.default_rng(7)
@@ -115,17 +106,15 @@ def test_graphsum_vs_oracle(pgcn, n, deg, dim, hubs):
     torch.cuda.synchronize()
     assert torch.equal(out, out2)
     pgcn.lib.pgcn_graph_destroy(g)
-    pgcn.lib.pgcn_debug_set(b"graphsum_lds_window", LDS_WINDOW_DEFAULT)
 
 
-@pytest.mark.parametrize("blocks,window", [(2, 1), (8, 1), (16, 1), (32, 1), (8, 5), (32, 5)])
-def test_graphsum_lds_column_blocks(pgcn, blocks, window):
-    """The LDS schedule with other column-block counts than the shape rule picks (4 for square
-    graphs, 8 for row subsets): the same sums (XCD mapping: workgroup w serves block w % B).
-    Ring schedule (window 5) at 32 blocks: 7-8 slices per block, so the ring's prologue and
-    drain (the loader's last W - 1 iterations) make up much of each sweep."""
+@pytest.mark.parametrize("blocks", [2, 8, 16, 32])
+def test_graphsum_lds_column_blocks(pgcn, blocks):
+    """The LDS ring schedule with other column-block counts than the shape rule picks (4 for
+    square graphs, 8 for row subsets): the same sums (XCD mapping: workgroup w serves block
+    w % B).  At 32 blocks: 7-8 slices per block, so the ring's prologue and drain (the loader's
+    last W - 1 iterations) make up much of each sweep."""
     assert pgcn.lib.pgcn_debug_set(b"lds_blocks", blocks) == 0
-    pgcn.lib.pgcn_debug_set(b"graphsum_lds_window", window)
     try:
         n, dim = 120000, 16
         indptr, indices = random_graph(n, 40, seed=blocks, hubs=20, hub_deg=3000)
@@ -144,15 +133,13 @@ def test_graphsum_lds_column_blocks(pgcn, blocks, window):
         pgcn.lib.pgcn_graph_destroy(g)
     finally:
         pgcn.lib.pgcn_debug_set(b"lds_blocks", 0)
-        pgcn.lib.pgcn_debug_set(b"graphsum_lds_window", LDS_WINDOW_DEFAULT)
 
 
 @pytest.mark.parametrize("dim,ld", [(128, 128), (41, 44), (24, 24)])
 def test_graphsum_lds_wide_rows(pgcn, dim, ld):
     """Rows wider than 16 on a graph that takes the LDS GraphSum: one 16-column LDS pass per
-    chunk (the last one overlapping), against the oracle; padding columns stay zero.  The
-    ring schedule's single prescale + combine launches for all passes (graphsum_ring_wide)
-    give the same bits as a prescale + combine per pass."""
+    chunk (the last one overlapping), against the oracle; padding columns stay zero;
+    deterministic (the same bits on a rerun)."""
     n = 120000
     indptr, indices = random_graph(n, 30, seed=dim, hubs=10, hub_deg=3000)
     x = np.zeros((n, ld), np.float32)
@@ -162,14 +149,10 @@ def test_graphsum_lds_wide_rows(pgcn, dim, ld):
                                           ctypes.byref(g)), "graph_create")
     xin = torch.from_numpy(x).to(DEV)
     outs = []
-    try:
-        for wide in (1, 0):  # one prescale + one combine for all passes, or per pass
-            pgcn.lib.pgcn_debug_set(b"graphsum_ring_wide", wide)
-            out = torch.full((n, ld), float("nan"), device=DEV)
-            pgcn.check(pgcn.lib.pgcn_graphsum(g, vp(xin), ld, vp(out), ld, dim, stream()), "gs")
-            outs.append(out)
-    finally:
-        pgcn.lib.pgcn_debug_set(b"graphsum_ring_wide", 0)
+    for _ in range(2):
+        out = torch.full((n, ld), float("nan"), device=DEV)
+        pgcn.check(pgcn.lib.pgcn_graphsum(g, vp(xin), ld, vp(out), ld, dim, stream()), "gs")
+        outs.append(out)
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])
     ours = outs[0].cpu().numpy()
@@ -178,40 +161,6 @@ def test_graphsum_lds_wide_rows(pgcn, dim, ld):
     assert (np.abs(ours[:, :dim] - ref) <= 1e-5 * bound + 1e-30).all()
     np.testing.assert_array_equal(ours[:, dim:], 0.0)
     pgcn.lib.pgcn_graph_destroy(g)
-
-
-@pytest.mark.parametrize("blocks", [0, 8, 32])
-def test_graphsum_ring_fused_combine(pgcn, blocks):
-    """Ring schedule with the combine fused into the kernel (the batch's last workgroup adds
-    the column blocks' partials, graphsum_ring_fused 1) against the separate k_gs_lds_combine
-    launch (0): identical bits, over back-to-back calls (the arrival counters reset
-    themselves), at the default 4 blocks and at 8 / 32 blocks (more workgroups per batch)."""
-    assert pgcn.lib.pgcn_debug_set(b"lds_blocks", blocks) == 0
-    try:
-        n, dim = 120000, 16
-        indptr, indices = random_graph(n, 40, seed=11 + blocks, hubs=20, hub_deg=3000)
-        x = torch.randn(n, dim, device=DEV)
-        g = ctypes.c_void_p()
-        pgcn.check(pgcn.lib.pgcn_graph_create(n, helpers.ptr(indptr), helpers.ptr(indices),
-                                              ctypes.byref(g)), "graph_create")
-        outs = {}
-        for fused in (0, 1):
-            pgcn.lib.pgcn_debug_set(b"graphsum_ring_fused", fused)
-            outs[fused] = []
-            for k in range(4):
-                o = torch.full((n, dim), float("nan"), device=DEV)
-                pgcn.check(pgcn.lib.pgcn_graphsum(g, vp(x), dim, vp(o), dim, dim, stream()), "gs")
-                outs[fused].append(o)
-        torch.cuda.synchronize()
-        for o in outs[1] + outs[0][1:]:
-            assert torch.equal(o, outs[0][0])
-        ref = oracle_graphsum(indptr, indices, x.cpu().numpy(), dim)
-        bound = abs_bound(indptr, indices, x.cpu().numpy(), dim)
-        assert (np.abs(outs[1][0].cpu().numpy() - ref) <= 1e-5 * bound + 1e-30).all()
-        pgcn.lib.pgcn_graph_destroy(g)
-    finally:
-        pgcn.lib.pgcn_debug_set(b"graphsum_ring_fused", 0)
-        pgcn.lib.pgcn_debug_set(b"lds_blocks", 0)
 
 
 def test_graphsum_linearity_large(pgcn):
@@ -419,12 +368,9 @@ def test_gemm_xstream(pgcn, M, N, K, base):
                                                  vp(nib) if drop else None, 2.0, vp(ws),
                                                  stream()), "xtn")
         # the register-streamed kernels (xstream_ring 0): NN bit-identical to the loader /
-        # MFMA-wave split (default), TN the same sums in another order; and the TN LDS-DMA
-        # ring option of those (taken for K in 577..640, N = 16)
+        # MFMA-wave split (default), TN the same sums in another order
         C0 = torch.full((M, ldc), float("nan"), device=DEV)
         W0 = torch.full((K, N), float("nan"), device=DEV)
-        W2 = torch.full((K, N), float("nan"), device=DEV)
-        W3 = torch.full((K, N), float("nan"), device=DEV)
         with helpers.knobs(pgcn, xstream_ring=0):
             pgcn.check(pgcn.lib.pgcn_gemm_xstream(M, N, K, vp(dA), lda, vp(dB), N, 0, vp(C0),
                                                   ldc, vp(nib) if drop else None, 2.0, stream()),
@@ -432,14 +378,6 @@ def test_gemm_xstream(pgcn, M, N, K, base):
             pgcn.check(pgcn.lib.pgcn_gemm_tn_xstream(M, N, K, vp(dA), lda, vp(dG), N, vp(W0), N,
                                                      vp(nib) if drop else None, 2.0, vp(ws),
                                                      stream()), "xtn regs")
-            with helpers.knobs(pgcn, xstream_tn_lds=1):
-                pgcn.check(pgcn.lib.pgcn_gemm_tn_xstream(M, N, K, vp(dA), lda, vp(dG), N, vp(W2),
-                                                         N, vp(nib) if drop else None, 2.0,
-                                                         vp(ws), stream()), "xtn lds")
-        with helpers.knobs(pgcn, xstream_tn_split=1):  # the K-split ring TN (option)
-            pgcn.check(pgcn.lib.pgcn_gemm_tn_xstream(M, N, K, vp(dA), lda, vp(dG), N, vp(W3), N,
-                                                     vp(nib) if drop else None, 2.0, vp(ws),
-                                                     stream()), "xtn split")
         torch.cuda.synchronize()
         np.testing.assert_array_equal(C0.cpu().numpy(), C.cpu().numpy())
         ref = Ae @ B.astype(np.float64)
@@ -449,7 +387,7 @@ def test_gemm_xstream(pgcn, M, N, K, base):
         np.testing.assert_array_equal(o[:, N:], 0.0)
         ref_t = Ae.T @ Gm.astype(np.float64)
         bound_t = np.abs(Ae).T @ np.abs(Gm.astype(np.float64))
-        for tn in (W, W0, W2, W3):  # the same products, rows summed in different orders
+        for tn in (W, W0):  # the same products, rows summed in different orders
             assert (np.abs(tn.cpu().numpy() - ref_t) <= 1e-5 * bound_t + 1e-30).all()
         outs[drop] = C
     # the dual kernel (eval + next training product in one pass) is bit-identical to both

@@ -70,9 +70,13 @@ def big_ds(pgcn):
 
 @pytest.fixture(scope="module")
 def big_oracle(big_ds):
+    """4 epoch lines, eval(3), and the oracle's near-tied rows of every pass (the accuracy
+    tolerance, helpers.near_ties)."""
     ref = helpers.OracleGCN(helpers.ds_dict(big_ds))
-    lines = [ref.train_epoch() + ref.eval(2) for _ in range(4)]
-    return lines, ref.eval(3)
+    c = big_ds.output_dim
+    runs = [ref.epoch_with_ties(big_ds.label, big_ds.split, c) for _ in range(4)]
+    test, tt = ref.eval_with_ties(3, big_ds.label, big_ds.split, c)
+    return [r[0] for r in runs], [r[1] for r in runs], test, {1: tt, 2: tt}
 
 
 @pytest.mark.parametrize("world,split_rows,lds", [(2, 0, 1), (2, 1, 1), (4, 0, 1), (8, 0, 1),
@@ -84,8 +88,9 @@ def test_loopback_lds_graph_matches_oracle(pgcn, big_ds, big_oracle, world, spli
     assert res[0]["info"]["graphsum_lds"] == lds
     assert res[0]["info"]["reassociated"] == 1
     cnt = helpers.split_counts(big_ds)
-    lines, test = big_oracle
-    for e, (ours, want) in enumerate(zip(res[0]["lines"], lines)):
-        helpers.assert_line_close(ours, want, cnt, what=f"world {world} epoch {e + 1}")
+    lines, ties, test, test_ties = big_oracle
+    for e, (ours, want, tie) in enumerate(zip(res[0]["lines"], lines, ties)):
+        helpers.assert_line_close(ours, want, cnt, what=f"world {world} epoch {e + 1}", ties=tie)
     t = res[0]["test"]
-    helpers.assert_line_close(t + t, test * 2, {1: cnt[3], 2: cnt[3]}, what="test")
+    helpers.assert_line_close(t + t, test * 2, {1: cnt[3], 2: cnt[3]}, what="test",
+                              ties=test_ties)

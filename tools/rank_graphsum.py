@@ -6,8 +6,7 @@ times one d = 16 GraphSum call (every chunk) on each kernel path the shape admit
   * "default"  -- the engine's choice (LDS ring schedule when the rank's table exceeds 4 MB,
                   else the plain gather kernel);
   * "lds"      -- the LDS ring schedule forced (lds_min_kb 0);
-  * "plain"    -- the plain gather kernel (lds_min_kb huge), without / with the XCD column
-                  blocking ("plain_blocked": blocked_min_kb 0).
+  * "plain"    -- the plain gather kernel (lds_min_kb huge).
 Prints one JSON object: ms per GraphSum call (all chunks) per (world, path).
 
 usage: python3 tools/rank_graphsum.py [worlds=2,4,8] [chunks=2]
@@ -32,8 +31,7 @@ n = ds.num_nodes
 ip = np.ascontiguousarray(ds.graph_indptr, np.int32)
 ix = np.ascontiguousarray(ds.graph_indices, np.int32)
 st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-PATHS = {"default": {}, "lds": {"lds_min_kb": 0}, "plain": {"lds_min_kb": 1 << 30},
-         "plain_blocked": {"lds_min_kb": 1 << 30, "blocked_min_kb": 0}}
+PATHS = {"default": {}, "lds": {"lds_min_kb": 0}, "plain": {"lds_min_kb": 1 << 30}}
 if os.environ.get("RANK_GS_PATHS"):  # e.g. "lds_b8:lds_blocks=8,lds_min_kb=0;lds_b16:lds_blocks=16"
     PATHS = {}
     for item in os.environ["RANK_GS_PATHS"].split(";"):
@@ -74,7 +72,6 @@ def time_path(world, knobs, reps=20):
         for g in graphs:
             pg.lib.pgcn_graph_destroy(g)
         pg.lib.pgcn_debug_set(b"lds_min_kb", -1)  # the defaults
-        pg.lib.pgcn_debug_set(b"blocked_min_kb", -1)
         pg.lib.pgcn_debug_set(b"lds_blocks", 0)
 
 
