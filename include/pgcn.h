@@ -303,10 +303,14 @@ long long pgcn_debug_lds_counts(int n_rows, int n_cols, const int *indptr, const
  * can assert which kernels a configuration took: "xs_nn_ring" / "xs_tn_ring" (loader + MFMA-wave
  * X-stream kernels), "xs_nn" / "xs_tn" (register-streamed X-stream kernels), "gs_ring" (LDS ring
  * GraphSum), "gs_gather" (gather GraphSum), "out_xent" (output layer fused into the loss),
- * "gemm_nn" / "gemm_tn" (general MFMA GEMMs).  A non-null name returns its count (then zeroes it
+ * "gemm_nn" / "gemm_tn" (general MFMA GEMMs), "launches" (every kernel launch of the library).
+ * A non-null name returns its count (then zeroes it
  * when reset != 0); a null name with reset != 0 zeroes every counter.  Status < 0 on an unknown
  * name. */
 long long pgcn_debug_path_count(const char *name, int reset);
+/* n empty kernels back to back on `stream` (the per-launch floor the small graphs' epochs are
+ * compared with: launches per epoch x the time of one empty launch). */
+int pgcn_debug_empty_launches(int n, void *stream);
 
 #ifdef __cplusplus
 }

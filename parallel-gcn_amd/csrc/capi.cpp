@@ -34,8 +34,9 @@ extern int g_parse_threads;         // host/data.cpp: pieces of the parallel tex
 
 namespace {
 std::atomic<long long> g_path_hits[KP_COUNT];
-const char *const kPathNames[KP_COUNT] = {"xs_nn_ring", "xs_tn_ring", "xs_nn",   "xs_tn",  "gs_ring",
-                                          "gs_gather",  "out_xent",   "gemm_nn", "gemm_tn"};
+const char *const kPathNames[KP_COUNT] = {"xs_nn_ring", "xs_tn_ring", "xs_nn",   "xs_tn",
+                                          "gs_ring",    "gs_gather",  "out_xent", "gemm_nn",
+                                          "gemm_tn",    "launches"};
 }  // namespace
 void note_path(KernelPath p) { g_path_hits[p].fetch_add(1, std::memory_order_relaxed); }
 }  // namespace pgcn
@@ -657,6 +658,14 @@ int pgcn_debug_lds_check(int n_rows, int n_cols, const int *indptr, const int *i
     }
     if (max_rel_err) *max_rel_err = err;
     if (n_blocks) *n_blocks = h.wave_off.back();
+  });
+}
+
+int pgcn_debug_empty_launches(int n, void *stream) {
+  return guarded([&] {
+    PGCN_CHECK(n >= 0, PGCN_E_INVALID, "empty_launches: n >= 0");
+    launch_empty(n, as_stream(stream));
+    PGCN_HIP(hipGetLastError());
   });
 }
 

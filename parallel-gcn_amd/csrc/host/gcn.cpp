@@ -472,6 +472,8 @@ void GCN::build(const GCNData &data) {
   size_t ws = 0;
   for (int l = 0; l < L; l++)
     ws = std::max(ws, gemm_tn_workspace(rows, dims[(size_t)l + 1], dims[(size_t)l]));
+  // the fused loss kernel's per-block W.grad partials of the output layer (fuse_output >= 2)
+  ws = std::max(ws, tn_reduce_blocks_workspace(xent_blocks(prow), 16, 48));
   gemm_ws.allocate(ws / sizeof(float) + 64);
   if (g_mm_side == 2 || (g_mm_side == 1 && rows >= kMmSideRows)) {
     // the side stream's Matmul weight gradients have a workspace of their own

@@ -150,7 +150,7 @@ void launch_scatter_rows(const float *src, const int *rows, int n, int ld, float
   PGCN_CHECK(ld % 4 == 0, PGCN_E_INVALID, "scatter_rows: ld % 4");
   if (n <= 0) return;
   const long long tot = (long long)n * (ld / 4);
-  hipLaunchKernelGGL(k_scatter_rows, dim3((unsigned)ceil_div(tot, 256)), dim3(256), 0, s,
+  PGCN_LAUNCH(k_scatter_rows, dim3((unsigned)ceil_div(tot, 256)), dim3(256), 0, s,
                      reinterpret_cast<const float4 *>(src), rows, n, ld / 4,
                      reinterpret_cast<float4 *>(out));
 }
@@ -169,7 +169,7 @@ __global__ __launch_bounds__(256) void k_loopback_sum(LoopbackSrcs srcs, float *
 void launch_loopback_sum(const LoopbackSrcs &srcs, float *dst, size_t count, hipStream_t s) {
   PGCN_CHECK(srcs.n >= 1 && srcs.n <= kLoopbackMaxRanks, PGCN_E_INVALID, "loopback_sum: ranks");
   if (count == 0) return;
-  hipLaunchKernelGGL(k_loopback_sum, dim3((unsigned)ceil_div((long long)count, 256)), dim3(256), 0,
+  PGCN_LAUNCH(k_loopback_sum, dim3((unsigned)ceil_div((long long)count, 256)), dim3(256), 0,
                      s, srcs, dst, count);
 }
 
@@ -189,7 +189,7 @@ void launch_gather_rows(const float *src, const int *rows, int n, int ld, float 
   PGCN_CHECK(ld % 4 == 0, PGCN_E_INVALID, "gather_rows: ld % 4");
   if (n <= 0) return;
   const long long tot = (long long)n * (ld / 4);
-  hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)ceil_div(tot, 256)), dim3(256), 0, s,
+  PGCN_LAUNCH(k_gather_rows, dim3((unsigned)ceil_div(tot, 256)), dim3(256), 0, s,
                      reinterpret_cast<const float4 *>(src), rows, n, ld / 4,
                      reinterpret_cast<float4 *>(out));
 }
@@ -238,24 +238,41 @@ __device__ __forceinline__ float block_sum(float v, float *smem) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Cross entropy (hpdga module.cpp:122-153) + accuracy (hpdga gcn.cpp:150-164), one thread
-// per row, every thread of the block computing (XR = 256 rows).  Labelled rows are
-// max-shifted in place like the reference; the grad is written divided by the labelled count
-// (known per split on the host).  Rows go through ONE LDS tile [XR][ld+1] (row stride ld+1:
-// conflict-free per-row reads) with coalesced copies: logits in, shifted logits out, then the
-// grad computed in place and copied out.  Per-block partial sums (loss, wrong) go to
-// partials[2*block].
+// Cross entropy (hpdga module.cpp:122-153) + accuracy (hpdga gcn.cpp:150-164).  A block of XR
+// = 64 rows, 4 waves, each wave working alone on its 16 rows (no block barrier between the
+// phases): a row's classes are split over a lane quad (lane q takes classes q, q + 4, ...;
+// C = 41: 11 per lane), max and exp-sum combined across the quad by xor shuffles in a fixed
+// order ((s0 + s1) + (s2 + s3): commutative adds, every lane holds the same bits), so a row's
+// serial chain is 11 steps instead of 41 (r02: one thread per row, 256-row blocks at 3 per CU
+// with a block barrier per phase, 73 us per training call).  Labelled rows are max-shifted in
+// place like the reference; the grad is written divided by the labelled count (known per split
+// on the host).  A wave's rows go through its part of ONE LDS tile [XR][ld+1] with coalesced
+// copies: logits in (or computed, FUSED), shifted logits out, then the grad computed in place
+// and copied out.  Per-block partial sums (loss, wrong) go to partials[2*block].
 // ------------------------------------------------------------------------------------------
-constexpr int XR = 256;  // rows per cross-entropy block (= threads; 128 measured slower, r02)
+#ifndef PGCN_XENT_ROWS
+#define PGCN_XENT_ROWS 64
+#endif
+constexpr int XR = PGCN_XENT_ROWS;  // rows per cross-entropy block
+constexpr int XT = 4 * XR;    // threads: a lane quad per row; wave w holds rows 16 w .. 16 w + 15
+__host__ __device__ inline int xent_stride(int ld) { return ld + 1 > 49 ? (ld + 1) | 1 : 49; }
 typedef float floatx4e __attribute__((ext_vector_type(4)));
+
+// a wave's LDS writes are visible to its own later LDS reads (one wave: in-order LDS pipe);
+// this keeps the compiler from moving the reads above the writes
+__device__ __forceinline__ void wave_lds_fence() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
 
 // FUSED: the logits are computed here from the output layer's input H [n][ldh] (kh <= 16
 // columns) and W [kh][ldw] with k_gemm_nn's v_mfma_f32_16x16x4_f32 sequence, so the same bits
-// as the separate Matmul -- and then go through the same tile as the loaded ones (the output layer's Matmul forward + CrossEntropyLoss forward,
-// hpdga module.cpp:13-38, :122-153, in one pass: the logits are written once, not written
-// and read back).
+// as the separate Matmul -- and then go through the same tile as the loaded ones (the output
+// layer's Matmul forward + CrossEntropyLoss forward, hpdga module.cpp:13-38, :122-153, in one
+// pass: the logits are written once, not written and read back).  Training: also the output
+// layer's input grad dH = grad W^T and (dWp) this block's partial of W.grad = H^T grad.
 template <bool FUSED>
-__global__ __launch_bounds__(XR) void k_xent_fwd(float *__restrict__ logits, int ld,
+__global__ __launch_bounds__(XT) void k_xent_fwd(float *__restrict__ logits, int ld,
                                                   float *__restrict__ grad,
                                                   const int *__restrict__ truth, int n, int c,
                                                   int count, int training,
@@ -267,201 +284,233 @@ __global__ __launch_bounds__(XR) void k_xent_fwd(float *__restrict__ logits, int
   // write_back 0: the shifted logits stay in LDS (the compact output layer's logits are read
   // by nobody after the loss; hpdga's in-place shift is kept where the variable is visible)
   extern __shared__ float smem[];
-  __shared__ float red[XR / 64];
-  const int S = ld + 1;
-  float *L = smem;  // [XR][S]
-  const long long row0 = (long long)blockIdx.x * XR;
+  __shared__ float red[XT / 64];
+  // tile row stride: odd (conflict-free row walks) and >= 48, so a wave's 16 rows can take its
+  // [3][4][64] weight-grad partial once the grad has left the tile (no extra LDS: 8 blocks per CU)
+  const int S = xent_stride(ld);
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63, gi = ln >> 4, ii = ln & 15;
+  const long long row0 = (long long)blockIdx.x * XR, wrow0 = row0 + 16 * wv;
   const int rows = (int)min((long long)XR, (long long)n - row0);
-  const long long base = row0 * ld;
-  const int tile = rows * ld;
-  // The tile is rows*ld contiguous floats (ld % 4 == 0, 16-B aligned): float4 copies,
-  // XU per thread in flight (all loads of a batch before its LDS stores); float4 q = row
-  // q / (ld/4), column 4 (q % (ld/4)) -- one division per float4, not per float.
-  const int ld4 = ld >> 2, tile4 = tile >> 2;
-  constexpr int XU = 8;
+  const int wrows = max(0, min(16, rows - 16 * wv));  // this wave's rows
+  float *L = smem + wv * 16 * S;  // the wave's part of the tile [16][S]
+  // the wave's rows: wrows*ld contiguous floats (ld % 4 == 0, 16-B aligned), copied as float4
+  // q = lane + 64 u (1 KB contiguous per wave instruction; r03: a quad per row, 176-B strided
+  // pieces, made the kernel 20 % slower); row q / (ld/4) by a 24-bit multiply-shift (exact for
+  // q < 2^20 / (ld/4); here q < 512)
+  const int ld4 = ld >> 2, tile4 = (wrows * ld) >> 2;
+  const unsigned magic = (1u << 20) / (unsigned)ld4 + 1u;
+  const long long base = wrow0 * ld;
   auto to_lds = [&](const float *src) {
-    for (int q0 = threadIdx.x; q0 < tile4; q0 += XR * XU) {
-      float4 v[XU];
+    float4 v[8];  // ld <= 124: 16 * 31 float4 <= 64 * 8
 #pragma unroll
-      for (int u = 0; u < XU; u++) {
-        const int q = q0 + XR * u;
-        if (q < tile4) v[u] = reinterpret_cast<const float4 *>(src + base)[q];
-      }
+    for (int u = 0; u < 8; u++) {
+      const int q = ln + 64 * u;
+      if (q < tile4) v[u] = reinterpret_cast<const float4 *>(src + base)[q];
+    }
 #pragma unroll
-      for (int u = 0; u < XU; u++) {
-        const int q = q0 + XR * u;
-        if (q < tile4) {
-          const int r = q / ld4, j = 4 * (q - r * ld4);
-          float *d = L + r * S + j;
-          d[0] = v[u].x;
-          d[1] = v[u].y;
-          d[2] = v[u].z;
-          d[3] = v[u].w;
-        }
+    for (int u = 0; u < 8; u++) {
+      const int q = ln + 64 * u;
+      if (q < tile4) {
+        const int r = (int)(__umul24((unsigned)q, magic) >> 20), j = 4 * (q - r * ld4);
+        float *d = L + r * S + j;
+        d[0] = v[u].x;
+        d[1] = v[u].y;
+        d[2] = v[u].z;
+        d[3] = v[u].w;
       }
     }
   };
   auto from_lds = [&](float *dst) {
-    for (int q = threadIdx.x; q < tile4; q += XR) {
-      const int r = q / ld4, j = 4 * (q - r * ld4);
+    for (int q = ln; q < tile4; q += 64) {
+      const int r = (int)(__umul24((unsigned)q, magic) >> 20), j = 4 * (q - r * ld4);
       const float *d = L + r * S + j;
       reinterpret_cast<float4 *>(dst + base)[q] = make_float4(d[0], d[1], d[2], d[3]);
     }
   };
-  // FUSED: W [k][j] (16 x ld) in the dynamic LDS past the tile (and past the waves' weight-grad
-  // partials, which reuse the tile): sized to the layer, not to the largest class count
-  float *wt = smem + (FUSED ? max(XR * S, (XR / 64) * 3 * 4 * 64) : 0);
-  // FUSED: the lane's H operands of all four 16-row groups, loaded before W is staged (one
-  // HBM latency for the block instead of one per group)
-  float ha[4][4];
+  // FUSED: W [k][j] (16 x ld) past the tile
+  float *wt = smem + XR * S;
+  // FUSED: the lane's H operands of its wave's 16-row group (MFMA t of lane (gi, ii):
+  // H[row ii][4 gi + t]) and, training with dWp, of the weight-grad steps (row 4 st + gi,
+  // column ii), both loaded before W is staged (one HBM latency for the block)
+  float ha[4], hw[4];
+  // the quad of the wave's row rq (lane q takes classes q + 4 k); its truth label, loaded
+  // with the block's first loads
+  const int rq = ln >> 2, q = ln & 3;
+  const int t = rq < wrows ? truth[wrow0 + rq] : -1;
   if constexpr (FUSED) {
-    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63, gi = ln >> 4, ii = ln & 15;
+    const long long grow = wrow0 + ii < n ? wrow0 + ii : n - 1;
+    const float *hr = H + grow * (long long)ldh;
+    if (4 * gi + 3 < kh && ldh % 4 == 0) {
+      const float4 h4 = *reinterpret_cast<const float4 *>(hr + 4 * gi);
+      ha[0] = h4.x;
+      ha[1] = h4.y;
+      ha[2] = h4.z;
+      ha[3] = h4.w;
+    } else {
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-      long long grow = row0 + wv * 64 + q * 16 + ii;
-      grow = grow < n ? grow : n - 1;
-      const float *hr = H + grow * (long long)ldh;
-#pragma unroll
-      for (int t4 = 0; t4 < 4; t4++) ha[q][t4] = 4 * gi + t4 < kh ? hr[4 * gi + t4] : 0.0f;
+      for (int t4 = 0; t4 < 4; t4++) ha[t4] = 4 * gi + t4 < kh ? hr[4 * gi + t4] : 0.0f;
     }
-  }
-  if constexpr (FUSED) {
-    for (int e = threadIdx.x; e < 16 * ld; e += XR) {
-      const int k = e / ld, j = e - k * ld;
-      wt[e] = (k < kh && j < c) ? W[(long long)k * ldw + j] : 0.0f;
+    if (training && dWp) {
+#pragma unroll
+      for (int st = 0; st < 4; st++) {
+        const int rloc = 4 * st + gi;
+        hw[st] = (rloc < wrows && ii < kh) ? H[(wrow0 + rloc) * (long long)ldh + ii] : 0.0f;
+      }
     }
-    __syncthreads();
-    // logits of the block's XR rows on MFMA, as k_gemm_nn<3> computes them: wave w takes rows
-    // 64 w .. 64 w + 63 in groups of 16; lane (i, g) feeds MFMA t with H[row i][4 g + t] and
-    // W[4 g + t][16 tt + i]; lane holds logits[4 g + r][16 tt + i] -> the tile
-    const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63, gi = ln >> 4, ii = ln & 15;
+    // W's 16 rows staged by the waves in turn (rows wv, wv + XT/64, ...), a lane per column
+    for (int k = wv; k < 16; k += XT / 64)
+      for (int j = ln; j < ld; j += 64) wt[k * ld + j] = (k < kh && j < c) ? W[(long long)k * ldw + j] : 0.0f;
+    __syncthreads();  // W staged (the only barrier before the block's final sums)
+    // logits of the wave's 16 rows on MFMA, as k_gemm_nn<3> computes them; lane holds
+    // logits[4 gi + r][16 tt + ii] -> the tile
+    for (int tt = 0; 16 * tt < ld; tt++) {
+      const int col = 16 * tt + ii;
+      floatx4e acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const float *a = ha[q];
-      for (int tt = 0; 16 * tt < ld; tt++) {
-        const int col = 16 * tt + ii;
-        floatx4e acc = {0.f, 0.f, 0.f, 0.f};
+      for (int t4 = 0; t4 < 4; t4++)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(
+            ha[t4], col < ld ? wt[(4 * gi + t4) * ld + col] : 0.0f, acc, 0, 0, 0);
+      if (col < ld) {
 #pragma unroll
-        for (int t4 = 0; t4 < 4; t4++)
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(
-              a[t4], col < ld ? wt[(4 * gi + t4) * ld + col] : 0.0f, acc, 0, 0, 0);
-        if (col < ld) {
-#pragma unroll
-          for (int r = 0; r < 4; r++) L[(wv * 64 + q * 16 + 4 * gi + r) * S + col] = acc[r];
-        }
+        for (int r = 0; r < 4; r++) L[(4 * gi + r) * S + col] = acc[r];
       }
     }
   } else {
     to_lds(logits);
   }
-  __syncthreads();
+  wave_lds_fence();
   float loss = 0.0f, wrong = 0.0f, se = 0.0f;
-  const int t = threadIdx.x < rows ? truth[row0 + threadIdx.x] : -1;
-  float *l = L + threadIdx.x * S;
-  if (t >= 0) {
-    float mx = -1e30f;
-#pragma unroll 4
-    for (int j = 0; j < c; j++) mx = fmaxf(mx, l[j]);
-#pragma unroll 4
-    for (int j = 0; j < c; j++) {
-      const float v = l[j] - mx;
-      l[j] = v;
-      se += expf(v);
-    }
-    const float lt = l[t];
-    loss = logf(se) - lt;
-    bool w = false;
-#pragma unroll 4
-    for (int j = 0; j < c; j++) w |= l[j] > lt;
-    wrong = w ? 1.0f : 0.0f;
+  float *l = L + rq * S;
+  // up to 48 classes (reddit: 41) the lane's classes live in registers: every LDS read of the
+  // row issued at once, the exps independent (the loops' LDS round trips were the kernel's
+  // serial chain); wider rows take the same steps through the tile
+  constexpr int NV = 12;
+  const bool regs = c <= 4 * NV;
+  float v[NV];
+  if (regs) {
+#pragma unroll
+    for (int k = 0; k < NV; k++) v[k] = q + 4 * k < c ? l[q + 4 * k] : -1e30f;
   }
-  __syncthreads();
+  if (t >= 0) {  // uniform over the quad
+    float mx = -1e30f;
+    if (regs) {
+#pragma unroll
+      for (int k = 0; k < NV; k++) mx = fmaxf(mx, v[k]);
+    } else {
+      for (int j = q; j < c; j += 4) mx = fmaxf(mx, l[j]);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 2, 64));
+    float s = 0.0f;
+    if (regs) {
+#pragma unroll
+      for (int k = 0; k < NV; k++) {
+        if (q + 4 * k < c) {
+          v[k] -= mx;
+          l[q + 4 * k] = v[k];
+          s += expf(v[k]);
+        }
+      }
+    } else {
+      for (int j = q; j < c; j += 4) {
+        const float x = l[j] - mx;
+        l[j] = x;
+        s += expf(x);
+      }
+    }
+    s += __shfl_xor(s, 1, 64);      // lanes 0, 1: s0 + s1; lanes 2, 3: s2 + s3
+    se = s + __shfl_xor(s, 2, 64);  // (s0 + s1) + (s2 + s3) on every lane
+    wave_lds_fence();               // the quad's shifted logits are all in the tile
+    const float lt = l[t];
+    bool w = false;
+    if (regs) {
+#pragma unroll
+      for (int k = 0; k < NV; k++) w |= q + 4 * k < c && v[k] > lt;
+    } else {
+      for (int j = q; j < c; j += 4) w |= l[j] > lt;
+    }
+    const int wq = (int)w | __shfl_xor((int)w, 1, 64);
+    const int wall = wq | __shfl_xor(wq, 2, 64);
+    if (q == 0) {
+      loss = logf(se) - lt;
+      wrong = wall ? 1.0f : 0.0f;
+    }
+  }
+  wave_lds_fence();
   if (write_back || FUSED) from_lds(logits);
   if (training) {
-    // the weight-grad phase's H operands (row 4 st + gi of the wave, column ii), loaded now so
-    // their latency hides behind the grad computation
-    float hw[16];
-    if (FUSED && dWp) {
-      const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63, gi = ln >> 4, ii = ln & 15;
-#pragma unroll
-      for (int st = 0; st < 16; st++) {
-        const int rloc = wv * 64 + 4 * st + gi;
-        hw[st] = (rloc < rows && ii < kh) ? H[(row0 + rloc) * (long long)ldh + ii] : 0.0f;
-      }
-    }
-    __syncthreads();  // the shifted logits have left the tile
-    if (threadIdx.x < rows) {
+    wave_lds_fence();  // the shifted logits have been read out
+    if (rq < wrows) {
       if (t >= 0) {
-#pragma unroll 4
-        for (int j = 0; j < c; j++) {
-          float prob = expf(l[j]) / se;
-          if (j == t) prob = (float)((double)prob - 1.0);  // hpdga module.cpp:145 (double temp)
-          l[j] = prob / (float)count;
+        if (regs) {
+          // (reciprocal multiplies instead of the two divisions measured no faster, r03)
+#pragma unroll
+          for (int k = 0; k < NV; k++) {
+            const int j = q + 4 * k;
+            if (j < c) {
+              float prob = expf(v[k]) / se;
+              if (j == t) prob = (float)((double)prob - 1.0);  // hpdga module.cpp:145
+              l[j] = prob / (float)count;
+            }
+          }
+        } else {
+          for (int j = q; j < c; j += 4) {
+            float prob = expf(l[j]) / se;
+            if (j == t) prob = (float)((double)prob - 1.0);  // hpdga module.cpp:145 (double temp)
+            l[j] = prob / (float)count;
+          }
         }
-        for (int j = c; j < ld; j++) l[j] = 0.0f;
+        for (int j = c + q; j < ld; j += 4) l[j] = 0.0f;
       } else {
-        for (int j = 0; j < ld; j++) l[j] = 0.0f;
+        for (int j = q; j < ld; j += 4) l[j] = 0.0f;
       }
     }
+    wave_lds_fence();  // the wave's grad rows are complete
     if (FUSED && dH) {
       // the output layer's input grad dH = grad W^T (Matmul::backward's a.grad) on MFMA in
       // k_xstream_nn's sequence (N = 16 outputs, K = c classes: step s, MFMA t, lane group g:
       // class 16 s + 4 g + t), from the grad tile
-      __syncthreads();
-      const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63, gi = ln >> 4, ii = ln & 15;
+      floatx4e acc = {0.f, 0.f, 0.f, 0.f};
+      for (int s0 = 0; s0 < c; s0 += 16) {
 #pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const int rl = wv * 64 + q * 16;  // local rows rl .. rl + 15
-        floatx4e acc = {0.f, 0.f, 0.f, 0.f};
-        for (int s0 = 0; s0 < c; s0 += 16) {
-#pragma unroll
-          for (int t4 = 0; t4 < 4; t4++) {
-            const int j = s0 + 4 * gi + t4;
-            const float av = j < c ? L[(rl + ii) * S + j] : 0.0f;
-            const float bv = (j < c && ii < kh) ? wt[ii * ld + j] : 0.0f;
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
-          }
+        for (int t4 = 0; t4 < 4; t4++) {
+          const int j = s0 + 4 * gi + t4;
+          const float av = j < c ? L[ii * S + j] : 0.0f;
+          const float bv = (j < c && ii < kh) ? wt[ii * ld + j] : 0.0f;
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
         }
-        if (ii < lddh) {
+      }
+      if (ii < lddh) {
 #pragma unroll
-          for (int r = 0; r < 4; r++) {
-            const int rr = rl + 4 * gi + r;
-            if (rr < rows) dH[(row0 + rr) * (long long)lddh + ii] = acc[r];
-          }
+        for (int r = 0; r < 4; r++) {
+          const int rr = 4 * gi + r;
+          if (rr < wrows) dH[(wrow0 + rr) * (long long)lddh + ii] = acc[r];
         }
       }
     }
-    // the output layer's weight grad, this block's share: partial [kh][48] = H^T grad
-    // over the block's rows (wave partials on MFMA, added in wave order), reduced over the
-    // blocks in block order by launch_tn_reduce_blocks
-    floatx4e pw[3] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    // the output layer's weight grad, this block's share: partial [kh][48] = H^T grad over
+    // the block's rows (wave partials over their 16 rows on MFMA, added in wave order),
+    // reduced over the blocks in block order by launch_tn_reduce_blocks
     if (FUSED && dWp) {
-      if (!dH) __syncthreads();  // the grad tile is complete
-      const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63, gi = ln >> 4, ii = ln & 15;
+      floatx4e pw[3] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-      for (int st = 0; st < 16; st++) {  // 4-row steps over the wave's 64 rows
-        const int rloc = wv * 64 + 4 * st + gi;
-        const bool ok = rloc < rows;
-        const float av = hw[st];
+      for (int st = 0; st < 4; st++) {  // 4-row steps over the wave's 16 rows
+        const int rloc = 4 * st + gi;
+        const bool ok = rloc < wrows;
 #pragma unroll
         for (int tt = 0; tt < 3; tt++) {
           const int col = 16 * tt + ii;
           const float bv = (ok && col < ld) ? L[rloc * S + col] : 0.0f;
-          pw[tt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, pw[tt], 0, 0, 0);
+          pw[tt] = __builtin_amdgcn_mfma_f32_16x16x4f32(hw[st], bv, pw[tt], 0, 0, 0);
         }
       }
-    }
-    __syncthreads();
-    from_lds(grad);
-    if (FUSED && dWp) {
-      __syncthreads();  // the tile is free: wave partials through it
-      const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63, gi = ln >> 4, ii = ln & 15;
-      float *rw = L + wv * (3 * 4 * 64);
+      from_lds(grad);
+      wave_lds_fence();  // the grad has been read out: the wave's tile takes its partial
 #pragma unroll
       for (int tt = 0; tt < 3; tt++)
 #pragma unroll
-        for (int r = 0; r < 4; r++) rw[(tt * 4 + r) * 64 + ln] = pw[tt][r];
-      __syncthreads();
+        for (int r = 0; r < 4; r++) L[(tt * 4 + r) * 64 + ln] = pw[tt][r];
+      __syncthreads();  // every wave's partial is in LDS
       if (wv == 0) {
         float *pb = dWp + (long long)blockIdx.x * kh * 48;  // [kh][48] per block
 #pragma unroll
@@ -470,14 +519,16 @@ __global__ __launch_bounds__(XR) void k_xent_fwd(float *__restrict__ logits, int
           for (int r = 0; r < 4; r++) {
             float v = pw[tt][r];
 #pragma unroll
-            for (int w2 = 1; w2 < XR / 64; w2++) v += L[w2 * (3 * 4 * 64) + (tt * 4 + r) * 64 + ln];
+            for (int w2 = 1; w2 < XT / 64; w2++) v += smem[w2 * 16 * S + (tt * 4 + r) * 64 + ln];
             if (4 * gi + r < kh) pb[(4 * gi + r) * 48 + 16 * tt + ii] = v;
           }
       }
+    } else {
+      from_lds(grad);
     }
   }
-  const float ls = block_sum<XR>(loss, red);
-  const float ws = block_sum<XR>(wrong, red);
+  const float ls = block_sum<XT>(loss, red);
+  const float ws = block_sum<XT>(wrong, red);
   if (threadIdx.x == 0) {
     partials[2 * blockIdx.x] = ls;
     partials[2 * blockIdx.x + 1] = ws;
@@ -591,42 +642,42 @@ void launch_dropout_mask(uint64_t *states, long long n_chunks, long long elem0,
   const int threshold = (int)(p * (float)0x7fffffff);
   // 8 KB LDS: up to 8 workgroups per CU (a side-stream draw takes fewer: max_blocks)
   const int grid = grid_for(ceil_div(n_chunks, 2), 256, max_blocks > 0 ? max_blocks : 8 * kCUs);
-  hipLaunchKernelGGL(k_dropout_mask, dim3(grid), dim3(256), 0, s, states, n_chunks, elem0,
+  PGCN_LAUNCH(k_dropout_mask, dim3(grid), dim3(256), 0, s, states, n_chunks, elem0,
                      elem_end, threshold, mask, static_cast<const uint4 *>(table));
 }
 
 void launch_dropout_apply_based(float *x, long long n, const uint64_t *mask, long long base,
                                 float scale, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_dropout_apply, dim3(grid_for(ceil_div(n, 4))), dim3(256), 0, s, x, n,
+  PGCN_LAUNCH(k_dropout_apply, dim3(grid_for(ceil_div(n, 4))), dim3(256), 0, s, x, n,
                      mask, base, scale);
 }
 
 void launch_relu_fwd(float *x, long long n, uint8_t *mask, int training, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_relu_fwd, dim3(grid_for(n)), dim3(256), 0, s, x, n, mask, training);
+  PGCN_LAUNCH(k_relu_fwd, dim3(grid_for(n)), dim3(256), 0, s, x, n, mask, training);
 }
 
 void launch_relu_bwd(float *g, long long n, const uint8_t *mask, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_relu_bwd, dim3(grid_for(n)), dim3(256), 0, s, g, n, mask);
+  PGCN_LAUNCH(k_relu_bwd, dim3(grid_for(n)), dim3(256), 0, s, g, n, mask);
 }
 
 int xent_blocks(int n) { return (int)ceil_div(n, XR); }
+
+__global__ void k_empty() {}
+
+void launch_empty(int n, hipStream_t s) {
+  for (int i = 0; i < n; i++) hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, s);
+}
 
 void launch_xent_fwd(float *logits, int ld, float *grad, const int *truth, int n, int c,
                      int count, int training, float *partials, hipStream_t s, int write_back) {
   if (n <= 0) return;
   PGCN_CHECK(ld <= 124 && c <= ld && ld % 4 == 0, PGCN_E_INVALID,
              "xent: classes must be <= 124 (ld a multiple of 4)");
-  const size_t lds = (size_t)XR * (ld + 1) * sizeof(float);  // <= 256*125*4 = 125 KB
-  static bool attr = false;
-  if (!attr) {
-    PGCN_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(k_xent_fwd<false>),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, 125 * 1024));
-    attr = true;
-  }
-  hipLaunchKernelGGL(k_xent_fwd<false>, dim3(xent_blocks(n)), dim3(XR), lds, s, logits, ld, grad,
+  const size_t lds = (size_t)XR * xent_stride(ld) * sizeof(float);  // <= 64*125*4 = 31 KB
+  PGCN_LAUNCH(k_xent_fwd<false>, dim3(xent_blocks(n)), dim3(XT), lds, s, logits, ld, grad,
                      truth, n, c, count, training, partials, write_back, nullptr, 0, 0, nullptr, 0,
                      nullptr, 0, nullptr);
 }
@@ -640,15 +691,9 @@ void launch_out_xent(const float *H, int ldh, int kh, const float *W, int ldw, f
              "out_xent: classes <= 116, hidden <= 16");
   PGCN_CHECK(!dWp || ld <= 48, PGCN_E_INVALID, "out_xent: the weight-grad partial needs <= 48 classes");
   // the tile, and (weight-grad partials) room for the waves' [3][4][64] partials in it
-  const size_t tile = (size_t)XR * (ld + 1), wparts = (size_t)(XR / 64) * 3 * 4 * 64;
-  const size_t lds = ((wparts > tile ? wparts : tile) + (size_t)16 * ld) * sizeof(float);
-  static bool attr = false;
-  if (!attr) {
-    PGCN_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(k_xent_fwd<true>),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
-    attr = true;
-  }
-  hipLaunchKernelGGL(k_xent_fwd<true>, dim3(xent_blocks(n)), dim3(XR), lds, s, logits, ld, grad,
+  // the tile (which also takes the waves' weight-grad partials) and W
+  const size_t lds = ((size_t)XR * xent_stride(ld) + (size_t)16 * ld) * sizeof(float);
+  PGCN_LAUNCH(k_xent_fwd<true>, dim3(xent_blocks(n)), dim3(XT), lds, s, logits, ld, grad,
                      truth, n, c, count, training, partials, 1, H, ldh, kh, W, ldw,
                      training ? dH : nullptr, lddh, training ? dWp : nullptr);
 }
@@ -656,13 +701,13 @@ void launch_out_xent(const float *H, int ldh, int kh, const float *W, int ldw, f
 void launch_reduce_scalars(const float *partials, int n_blocks, const float *w, long long n_w,
                            float *sums, hipStream_t s, int count, float wd, float *out2,
                            const int *ctr, int ring_cap) {
-  hipLaunchKernelGGL(k_reduce_scalars, dim3(1), dim3(1024), 0, s, partials, n_blocks, w, n_w,
+  PGCN_LAUNCH(k_reduce_scalars, dim3(1), dim3(1024), 0, s, partials, n_blocks, w, n_w,
                      sums, count, wd, out2, ctr, ring_cap);
 }
 
 void launch_compose(const float *sums, int count, float wd, float *out2, hipStream_t s,
                     const int *ctr, int ring_cap) {
-  hipLaunchKernelGGL(k_compose, dim3(1), dim3(64), 0, s, sums, count, wd, out2, ctr, ring_cap);
+  PGCN_LAUNCH(k_compose, dim3(1), dim3(64), 0, s, sums, count, wd, out2, ctr, ring_cap);
 }
 
 // epoch graphs: the device copy of the host's (Adam step, epoch) counters
@@ -679,7 +724,7 @@ __global__ void k_counters(int *ctr, int set, int step, int epoch) {
 }
 
 void launch_counters(int *ctr, int set, int step, int epoch, hipStream_t s) {
-  hipLaunchKernelGGL(k_counters, dim3(1), dim3(64), 0, s, ctr, set, step, epoch);
+  PGCN_LAUNCH(k_counters, dim3(1), dim3(64), 0, s, ctr, set, step, epoch);
 }
 
 void launch_adam_multi(const AdamBatch &b, float step_size, float beta1, float beta2, float eps,
@@ -688,7 +733,7 @@ void launch_adam_multi(const AdamBatch &b, float step_size, float beta1, float b
   if (b.count <= 0) return;
   long long nmax = 0;
   for (int t = 0; t < b.count; t++) nmax = std::max(nmax, b.n[t]);
-  hipLaunchKernelGGL(k_adam_multi, dim3(grid_for(nmax), b.count), dim3(256), 0, s, b, step_size,
+  PGCN_LAUNCH(k_adam_multi, dim3(grid_for(nmax), b.count), dim3(256), 0, s, b, step_size,
                      beta1, beta2, eps, wd, step_table, ctr, table_cap);
 }
 
@@ -696,7 +741,7 @@ void launch_adam(float *w, const float *g, float *m, float *v, long long n, floa
                  float beta1, float beta2, float eps, float wd, int decay, hipStream_t s,
                  const float *step_table, const int *ctr, int table_cap) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_adam, dim3(grid_for(n)), dim3(256), 0, s, w, g, m, v, n, step_size,
+  PGCN_LAUNCH(k_adam, dim3(grid_for(n)), dim3(256), 0, s, w, g, m, v, n, step_size,
                      beta1, beta2, eps, wd, decay, step_table, ctr, table_cap);
 }
 

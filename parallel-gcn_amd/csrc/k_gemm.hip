@@ -591,7 +591,7 @@ void launch_mask_nibbles(const uint64_t *mask, long long mask_base, long long ma
   PGCN_CHECK(K >= 1 && K <= 1024, PGCN_E_INVALID, "mask_nibbles: K must be in [1,1024]");
   if (M <= 0) return;
   PGCN_CHECK(mask_ld >= K && mask_ld <= 1024, PGCN_E_INVALID, "mask_nibbles: K <= mask_ld <= 1024");
-  hipLaunchKernelGGL(k_mask_nibbles, dim3((unsigned)ceil_div(M, NIB_ROWS)), dim3(256), 0, s, mask,
+  PGCN_LAUNCH(k_mask_nibbles, dim3((unsigned)ceil_div(M, NIB_ROWS)), dim3(256), 0, s, mask,
                      mask_base, mask_ld, M, K, out);
 }
 
@@ -620,13 +620,13 @@ void launch_xstream_nn(int M, int N, int K, const float *A, int lda, const float
 #define XNN_CASE(KC)                                                                          \
   case KC:                                                                                    \
     if (C2)                                                                                   \
-      hipLaunchKernelGGL((k_xstream_nn<KC, true, true>), grid, block, lds, s, M, N, K, S, A,  \
+      PGCN_LAUNCH((k_xstream_nn<KC, true, true>), grid, block, lds, s, M, N, K, S, A,  \
                          lda, B, ldb, trans_b, C, ldc, maskT, a_scale, C2, e);                \
     else if (maskT)                                                                           \
-      hipLaunchKernelGGL((k_xstream_nn<KC, true>), grid, block, lds, s, M, N, K, S, A, lda, B, \
+      PGCN_LAUNCH((k_xstream_nn<KC, true>), grid, block, lds, s, M, N, K, S, A, lda, B, \
                          ldb, trans_b, C, ldc, maskT, a_scale, nullptr, e);                   \
     else                                                                                      \
-      hipLaunchKernelGGL((k_xstream_nn<KC, false>), grid, block, lds, s, M, N, K, S, A, lda,   \
+      PGCN_LAUNCH((k_xstream_nn<KC, false>), grid, block, lds, s, M, N, K, S, A, lda,   \
                          B, ldb, trans_b, C, ldc, maskT, a_scale, nullptr, e);                \
     break;
   switch (kc) {
@@ -672,7 +672,7 @@ static void gemm_nn_slab(int M, int N, int K, const float *A, int lda, const flo
   const dim3 grid((unsigned)ceil_div(M, 64)), block(256);
 #define NN_CASE(T)                                                                            \
   case T:                                                                                     \
-    hipLaunchKernelGGL(k_gemm_nn<T>, grid, block, 0, s, M, N, K, A, lda, B, ldb, trans_b, C, \
+    PGCN_LAUNCH(k_gemm_nn<T>, grid, block, 0, s, M, N, K, A, lda, B, ldb, trans_b, C, \
                        ldc, a_mask, mask_base, mask_ld, a_scale, nst);                        \
     break;
   switch (nt) {
@@ -735,9 +735,9 @@ static void tn_reduce(const TnPlan &p, int M, int N, int K, float *partial, floa
   float *part2 = partial + (size_t)p.n_slabs * K * p.ldp;
   const long long elems = (long long)K * p.ldp;
   if (M > 0)
-    hipLaunchKernelGGL(k_slab_reduce1, dim3((unsigned)ceil_div(elems, 256), (unsigned)p.n_groups),
+    PGCN_LAUNCH(k_slab_reduce1, dim3((unsigned)ceil_div(elems, 256), (unsigned)p.n_groups),
                        dim3(256), 0, s, partial, p.n_slabs, elems, p.spg, part2);
-  hipLaunchKernelGGL(k_gemm_tn_reduce, dim3((unsigned)ceil_div(elems, 256)), dim3(256), 0, s,
+  PGCN_LAUNCH(k_gemm_tn_reduce, dim3((unsigned)ceil_div(elems, 256)), dim3(256), 0, s,
                      part2, M > 0 ? p.n_groups : 0, K, N, p.ldp, C, ldc, nst);
 }
 
@@ -773,10 +773,10 @@ void launch_xstream_tn(int M, int N, int K, const float *A, int lda, const float
 #define XTN_CASE(KC)                                                                           \
   case KC:                                                                                     \
     if (maskT)                                                                                 \
-      hipLaunchKernelGGL((k_xstream_tn<KC, true>), dim3(XS_TN_BLOCKS), dim3(256), 0, s, M, N, K, \
+      PGCN_LAUNCH((k_xstream_tn<KC, true>), dim3(XS_TN_BLOCKS), dim3(256), 0, s, M, N, K, \
                          A, lda, G, ldg, maskT, a_scale, partial);                             \
     else                                                                                       \
-      hipLaunchKernelGGL((k_xstream_tn<KC, false>), dim3(XS_TN_BLOCKS), dim3(256), 0, s, M, N,  \
+      PGCN_LAUNCH((k_xstream_tn<KC, false>), dim3(XS_TN_BLOCKS), dim3(256), 0, s, M, N,  \
                          K, A, lda, G, ldg, maskT, a_scale, partial);                          \
     break;
     switch (p.nkc) {
@@ -825,7 +825,7 @@ static void gemm_tn_slab(int M, int N, int K, const float *A, int lda, const flo
     bool done = false;
 #define TN_CASE(NJ, KCW, WK)                                                                   \
   if (!done && p.nj == NJ && p.kcw == KCW && p.wk == WK) {                                    \
-    hipLaunchKernelGGL((k_gemm_tn<NJ, KCW, WK>), grid, block, 0, s, M, N, K, p.slab, A, lda, G, \
+    PGCN_LAUNCH((k_gemm_tn<NJ, KCW, WK>), grid, block, 0, s, M, N, K, p.slab, A, lda, G, \
                        ldg, a_mask, mask_base, mask_ld, a_scale, partial, p.ldp);              \
     done = true;                                                                               \
   }

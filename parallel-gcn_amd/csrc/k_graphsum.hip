@@ -212,19 +212,19 @@ static void launch_vec(const GraphSchedule &s, const int *indices, const float *
     // (measured and removed, r01: a software-pipelined k_graphsum16, 132 VGPRs at 3 waves per
     // SIMD, slower)
     if (VEC == 4 && s.nbc > 1)
-      hipLaunchKernelGGL(k_graphsum16, grid, block, 0, st, s.items, s.block_items, s.nbc, indices,
+      PGCN_LAUNCH(k_graphsum16, grid, block, 0, st, s.items, s.block_items, s.nbc, indices,
                          vals, reinterpret_cast<const float4 *>(in), ld_in / 4,
                          reinterpret_cast<float4 *>(out), ld_out / 4,
                          reinterpret_cast<float4 *>(partial), epi);
     else
-      hipLaunchKernelGGL((k_graphsum<VEC, G>), grid, block, 0, st, s.items, s.block_items, s.nbc,
+      PGCN_LAUNCH((k_graphsum<VEC, G>), grid, block, 0, st, s.items, s.block_items, s.nbc,
                          indices, vals, reinterpret_cast<const float4 *>(in), ld_in / 4,
                          reinterpret_cast<float4 *>(out), ld_out / 4,
                          reinterpret_cast<float4 *>(partial), epi);
   }
   if (s.n_comb > 0) {
     const long long threads = (long long)s.n_comb * VEC;
-    hipLaunchKernelGGL(k_graphsum_combine<VEC>, dim3((unsigned)ceil_div(threads, 256)),
+    PGCN_LAUNCH(k_graphsum_combine<VEC>, dim3((unsigned)ceil_div(threads, 256)),
                        dim3(256), 0, st, s.comb, s.n_comb,
                        reinterpret_cast<const float4 *>(partial), reinterpret_cast<float4 *>(out),
                        ld_out / 4, epi);

@@ -283,17 +283,17 @@ void launch_graphsum_ring(const LdsSchedule &s, const float *in, int ld_in, floa
   PGCN_CHECK(ld_in % 4 == 0 && ld_out % 4 == 0, PGCN_E_INVALID, "graphsum_ring: ld % 4");
   const long long pre = (long long)s.n_cols * 4;
   if (!prestaged)
-    hipLaunchKernelGGL(k_ring_prescale, dim3((unsigned)ceil_div(pre, 256)), dim3(256), 0, st,
+    PGCN_LAUNCH(k_ring_prescale, dim3((unsigned)ceil_div(pre, 256)), dim3(256), 0, st,
                        reinterpret_cast<const float4 *>(in), ld_in / 4, s.col_scale, s.n_cols,
                        reinterpret_cast<float4 *>(scratch_in), col_map);
   const long long n_wg = (long long)s.n_batches * s.n_blocks;
-  hipLaunchKernelGGL(k_graphsum_ring, dim3((unsigned)n_wg), dim3(LDS_THREADS), 0, st, s.entries,
+  PGCN_LAUNCH(k_graphsum_ring, dim3((unsigned)n_wg), dim3(LDS_THREADS), 0, st, s.entries,
                      s.wave_off, s.counts, s.t_max, s.slices, s.n_slices, s.rows,
                      reinterpret_cast<const char *>(scratch_in), reinterpret_cast<float4 *>(partial),
                      (long long)s.n_rows, s.n_blocks);
   const GsEpilogue none{};
   const long long post = (long long)s.n_rows * 4;
-  hipLaunchKernelGGL(k_gs_lds_combine, dim3((unsigned)ceil_div(post, 256)), dim3(256), 0, st,
+  PGCN_LAUNCH(k_gs_lds_combine, dim3((unsigned)ceil_div(post, 256)), dim3(256), 0, st,
                      reinterpret_cast<const float4 *>(partial), (long long)s.n_rows, s.n_blocks,
                      s.row_scale, s.n_rows, reinterpret_cast<float4 *>(out), ld_out / 4,
                      epi ? *epi : none);

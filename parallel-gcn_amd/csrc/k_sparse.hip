@@ -107,7 +107,7 @@ void launch_spmm_csr(int m, int p, int ldc, const int *indptr, const int *indice
                      const float *b, float *c, hipStream_t s) {
   if (m <= 0) return;
   const long long threads = (long long)m * p;
-  hipLaunchKernelGGL(k_spmm_csr, dim3((unsigned)ceil_div(threads, 256)), dim3(256), 0, s, m, p,
+  PGCN_LAUNCH(k_spmm_csr, dim3((unsigned)ceil_div(threads, 256)), dim3(256), 0, s, m, p,
                      ldc, indptr, indices, a, mask, mask_base, scale, b, c);
 }
 
@@ -116,7 +116,7 @@ void launch_spmm_csc_bwd(int nf, int p, int ldg, const int *csc_ptr, const int *
                          long long mask_base, float scale, const float *cgrad, float *bgrad,
                          hipStream_t s) {
   if (nf <= 0 || p <= 0) return;
-  hipLaunchKernelGGL(k_spmm_csc_bwd, dim3((unsigned)nf, (unsigned)ceil_div(p, 16)),
+  PGCN_LAUNCH(k_spmm_csc_bwd, dim3((unsigned)nf, (unsigned)ceil_div(p, 16)),
                      dim3(kCscChunk), 0, s, nf, p, ldg, csc_ptr, csc_row, csc_pos, a, mask,
                      mask_base, scale, cgrad, bgrad);
 }

@@ -338,6 +338,10 @@ __global__ __launch_bounds__(64 * (XL_TN_LOADERS + XL_TN_CONSUMERS), 1) void k_x
       xl_release(freed, slot, t, lane);
 #pragma unroll
       for (int q = 0; q < 4; q++) {
+        // a uniform exit per row step (never taken: nslot >= 2) keeps hipcc from scheduling
+        // the four steps as one block, which holds every step's masked operands live at once
+        // and spills (r03: 512 VGPRs + scratch, 202 vs 144 us; with it 360 VGPRs, none)
+        if (rg.nslot <= 0) break;
 #pragma unroll
         for (int c = 0; c < KC; c++) {
           float4 x = xa[q][c];
@@ -419,19 +423,19 @@ void launch_xstream_nn_ring(int M, int N, int K, const float *A, int lda, const 
 #define XNR_CASE(NI)                                                                           \
   case NI:                                                                                     \
     if (C2 && fold)                                                                            \
-      hipLaunchKernelGGL((k_xs_nn_ring<NI, true, true, true>), grid, block, 0, s, M, N, K, A,   \
+      PGCN_LAUNCH((k_xs_nn_ring<NI, true, true, true>), grid, block, 0, s, M, N, K, A,   \
                          lda, B, ldb, trans_b, C, ldc, maskT, a_scale, C2, e, rg);             \
     else if (C2)                                                                               \
-      hipLaunchKernelGGL((k_xs_nn_ring<NI, true, true, false>), grid, block, 0, s, M, N, K, A,  \
+      PGCN_LAUNCH((k_xs_nn_ring<NI, true, true, false>), grid, block, 0, s, M, N, K, A,  \
                          lda, B, ldb, trans_b, C, ldc, maskT, a_scale, C2, e, rg);             \
     else if (maskT && fold)                                                                    \
-      hipLaunchKernelGGL((k_xs_nn_ring<NI, true, false, true>), grid, block, 0, s, M, N, K, A,  \
+      PGCN_LAUNCH((k_xs_nn_ring<NI, true, false, true>), grid, block, 0, s, M, N, K, A,  \
                          lda, B, ldb, trans_b, C, ldc, maskT, a_scale, nullptr, e, rg);        \
     else if (maskT)                                                                            \
-      hipLaunchKernelGGL((k_xs_nn_ring<NI, true, false, false>), grid, block, 0, s, M, N, K, A, \
+      PGCN_LAUNCH((k_xs_nn_ring<NI, true, false, false>), grid, block, 0, s, M, N, K, A, \
                          lda, B, ldb, trans_b, C, ldc, maskT, a_scale, nullptr, e, rg);        \
     else                                                                                       \
-      hipLaunchKernelGGL((k_xs_nn_ring<NI, false, false, false>), grid, block, 0, s, M, N, K,   \
+      PGCN_LAUNCH((k_xs_nn_ring<NI, false, false, false>), grid, block, 0, s, M, N, K,   \
                          A, lda, B, ldb, trans_b, C, ldc, maskT, a_scale, nullptr, e, rg);     \
     break;
   switch (ni) {
@@ -455,13 +459,13 @@ void launch_xstream_tn_ring(int M, int N, int K, const float *A, int lda, const 
 #define XTR_CASE(NI)                                                                           \
   case NI:                                                                                     \
     if (maskT && fold)                                                                         \
-      hipLaunchKernelGGL((k_xs_tn_ring<NI, true, true>), grid, block, 0, s, M, N, K, A, lda, G, \
+      PGCN_LAUNCH((k_xs_tn_ring<NI, true, true>), grid, block, 0, s, M, N, K, A, lda, G, \
                          ldg, maskT, a_scale, partial, rg);                                    \
     else if (maskT)                                                                            \
-      hipLaunchKernelGGL((k_xs_tn_ring<NI, true, false>), grid, block, 0, s, M, N, K, A, lda,   \
+      PGCN_LAUNCH((k_xs_tn_ring<NI, true, false>), grid, block, 0, s, M, N, K, A, lda,   \
                          G, ldg, maskT, a_scale, partial, rg);                                 \
     else                                                                                       \
-      hipLaunchKernelGGL((k_xs_tn_ring<NI, false, false>), grid, block, 0, s, M, N, K, A, lda,  \
+      PGCN_LAUNCH((k_xs_tn_ring<NI, false, false>), grid, block, 0, s, M, N, K, A, lda,  \
                          G, ldg, maskT, a_scale, partial, rg);                                 \
     break;
   switch (ni) {

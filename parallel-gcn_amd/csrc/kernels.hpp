@@ -14,9 +14,17 @@ namespace pgcn {
 // which kernels a configuration took
 enum KernelPath {
   KP_XS_NN_RING, KP_XS_TN_RING, KP_XS_NN, KP_XS_TN, KP_GS_RING, KP_GS_GATHER, KP_OUT_XENT,
-  KP_GEMM_NN, KP_GEMM_TN, KP_COUNT
+  KP_GEMM_NN, KP_GEMM_TN, KP_LAUNCHES, KP_COUNT
 };
 void note_path(KernelPath p);
+// every kernel launch of the library goes through this (counted: "launches")
+#define PGCN_LAUNCH(...)                     \
+  do {                                       \
+    ::pgcn::note_path(::pgcn::KP_LAUNCHES);  \
+    hipLaunchKernelGGL(__VA_ARGS__);         \
+  } while (0)
+// n empty kernels back to back on s (the per-launch floor of the small graphs' epochs)
+void launch_empty(int n, hipStream_t s);
 
 // GraphSum work schedule for one row width (VEC float4 per row); device arrays.
 struct GraphSchedule {

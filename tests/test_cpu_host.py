@@ -407,3 +407,33 @@ def test_cpp_api_header_and_driver_without_device(datasets):
     r = subprocess.run([exe, "modules", root, names["cora"], "1"], capture_output=True, text=True,
                        timeout=120)
     assert r.returncode != 0 and "no HIP device" in r.stderr, (r.returncode, r.stderr[-500:])
+
+
+def test_no_kernel_spills_to_scratch(tmp_path):
+    """Every HIP kernel of libpgcn.so runs without scratch (private segment 0): a spill is a
+    silent slowdown (r03: the X-stream TN kernel lost 40 % to 348 B of spills after an
+    unrelated edit).  Reads the gfx950 code objects' metadata of the built objects."""
+    import glob
+    import re
+    import shutil
+    import subprocess
+    llvm = "/opt/rocm/lib/llvm/bin"
+    objs = sorted(glob.glob(os.path.join(helpers.REPO, "parallel-gcn_amd", "build", "k_*.o")))
+    assert objs, "libpgcn.so not built"
+    seen = 0
+    for o in objs:
+        local = tmp_path / os.path.basename(o)
+        shutil.copy(o, local)
+        subprocess.run([f"{llvm}/llvm-objdump", "--offloading", str(local)], check=True,
+                       capture_output=True, cwd=tmp_path)
+        dev = glob.glob(str(local) + ".*gfx950")
+        assert dev, o
+        notes = subprocess.run([f"{llvm}/llvm-readelf", "--notes", dev[0]], check=True,
+                               capture_output=True, text=True).stdout
+        names = re.findall(r"^\s+\.name:\s+(\S+)", notes, re.M)
+        scratch = [int(x) for x in re.findall(r"\.private_segment_fixed_size:\s+(\d+)", notes)]
+        assert len(names) == len(scratch) and names, o
+        bad = [(n, b) for n, b in zip(names, scratch) if b]
+        assert not bad, bad
+        seen += len(names)
+    assert seen >= 20

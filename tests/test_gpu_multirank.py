@@ -94,3 +94,43 @@ def test_loopback_lds_graph_matches_oracle(pgcn, big_ds, big_oracle, world, spli
     t = res[0]["test"]
     helpers.assert_line_close(t + t, test * 2, {1: cnt[3], 2: cnt[3]}, what="test",
                               ties=test_ties)
+
+
+# BASELINE configs[4] (4 layers, hidden 128) on the edge-cut path: 140k nodes, so a rank's
+# column block takes the LDS GraphSum at world 8 too (17.5k columns x 64 B > 1 MB); every
+# d = 128 GraphSum then runs as 16-column LDS passes over the rank's chunk graphs, each chunk
+# reduce-scattered on the comm stream
+DEEP = dict(n=140000, f=32, c=41, edges=1500000, seed=33)
+DEEP_DIMS, DEEP_DROPS = (128, 128, 128), (0.5, 0.5, 0.5, 0.5)
+
+
+@pytest.fixture(scope="module")
+def deep_ds(pgcn):
+    return pgcn.Dataset.synthetic(DEEP["n"], DEEP["f"], DEEP["c"], DEEP["edges"], DEEP["seed"])
+
+
+@pytest.fixture(scope="module")
+def deep_oracle(deep_ds):
+    ref = helpers.OracleGCN(helpers.ds_dict(deep_ds), hidden_dims=DEEP_DIMS, dropouts=DEEP_DROPS)
+    c = deep_ds.output_dim
+    runs = [ref.epoch_with_ties(deep_ds.label, deep_ds.split, c) for _ in range(2)]
+    test, tt = ref.eval_with_ties(3, deep_ds.label, deep_ds.split, c)
+    return [r[0] for r in runs], [r[1] for r in runs], test, {1: tt, 2: tt}
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_loopback_deep_wide_matches_oracle(pgcn, deep_ds, deep_oracle, world):
+    """4-layer hidden-128 model (BASELINE configs[4]) on the edge-cut engine at worlds 2 and 8
+    (loopback communicator): 128-wide GraphSums on the ranks' chunk graphs with their
+    reduce-scatters, the hidden layers' Matmul weight gradients all-reduced, against the
+    oracle's L-layer restatement (hpdga's algorithm, src/gcn.cu:85-112's layer builder)."""
+    p = pgcn.make_params(deep_ds, hidden_dims=DEEP_DIMS, dropouts=DEEP_DROPS)
+    res = _run_world(pgcn, deep_ds, world, 2, params=p)
+    _check_ranks(res, world, deep_ds.num_nodes)
+    assert res[0]["info"]["graphsum_lds"] == 1
+    cnt = helpers.split_counts(deep_ds)
+    lines, ties, test, test_ties = deep_oracle
+    for e, (ours, want, tie) in enumerate(zip(res[0]["lines"], lines, ties)):
+        helpers.assert_line_close(ours, want, cnt, what=f"world {world} epoch {e + 1}", ties=tie)
+    t = res[0]["test"]
+    helpers.assert_line_close(t + t, test * 2, {1: cnt[3], 2: cnt[3]}, what="test", ties=test_ties)

@@ -12,6 +12,12 @@ Two GPU numbers per dataset:
     reported as 100 / sum of epoch times like TMR_TRAIN.
 The CPU leg is oracle/_ref (the reference's hpdga sources, 1 thread) when built, else the C
 restatement.  Inputs come from the committed fixtures (tests/golden/data).
+
+Launch floor: these epochs are a few dozen short kernels each, so next to epochs/s the tool
+reports the kernel launches per epoch (the library's launch counter, pgcn_debug_path_count
+"launches") times the time of one empty kernel launched back to back the same way
+(pgcn_debug_empty_launches), i.e. the epochs/s an epoch of empty kernels would reach, and
+the measured rate as a fraction of it.
 """
 import argparse
 import json
@@ -51,6 +57,37 @@ def gpu_rates(pg, ds, epochs, graph):
     return async_rate, min(epochs, 100) / total, res
 
 
+def launch_floor_us(pg, n=2000):
+    """microseconds per empty kernel launched back to back from the host (best of 3)."""
+    import ctypes
+    st = torch.cuda.current_stream()
+    sp = ctypes.c_void_p(st.cuda_stream)
+    pg.check(pg.lib.pgcn_debug_empty_launches(100, sp), "empty")
+    torch.cuda.synchronize()
+    best = None
+    for _ in range(3):
+        t0 = time.perf_counter()
+        pg.check(pg.lib.pgcn_debug_empty_launches(n, sp), "empty")
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / n * 1e6
+        best = dt if best is None else min(best, dt)
+    return best
+
+
+def launches_per_epoch(pg, ds, epochs=20):
+    g = pg.GCN(pg.make_params(ds), ds, device=0)
+    for _ in range(3):
+        g.epoch_async()
+    g.sync()
+    pg.reset_path_counts()
+    for _ in range(epochs):
+        g.epoch_async()
+    g.sync()
+    n = pg.path_counts()["launches"] / epochs
+    g.close()
+    return n
+
+
 def cpu_rate(ds, reps):
     import bench
     kind, times, _ = bench.cpu_baseline(ds, reps)
@@ -70,6 +107,9 @@ def main():
     pg = helpers.pgcn()
     modes = [0, 1] if args.graph == "both" else [int(args.graph)]
     out = {}
+    floor_us = launch_floor_us(pg)
+    out["empty_launch_us"] = floor_us
+    print("empty launch", round(floor_us, 3), "us", flush=True)
     with tempfile.TemporaryDirectory() as root:
         for name in ((args.only,) if args.only else ("cora", "citeseer", "pubmed_synth")):
             dname = helpers.materialize_dataset(name, root)
@@ -81,6 +121,11 @@ def main():
                 row[f"{key}_async_epochs_s"] = a
                 row[f"{key}_reference_loop_epochs_s"] = r
                 row[f"{key}_last"] = [float(v) for v in np.asarray(res).ravel()]
+            lpe = launches_per_epoch(pg, ds)
+            row["launches_per_epoch"] = lpe
+            row["launch_floor_epochs_s"] = 1e6 / (lpe * floor_us)
+            if "eager_async_epochs_s" in row:
+                row["eager_frac_of_launch_floor"] = row["eager_async_epochs_s"] / row["launch_floor_epochs_s"]
             if not args.no_cpu:
                 kind, c = cpu_rate(ds, args.cpu_reps)
                 row["cpu_epochs_s"] = c
