@@ -158,7 +158,7 @@ def _ptr(a):
 
 
 KERNEL_PATHS = ("xs_nn_ring", "xs_tn_ring", "xs_nn", "xs_tn", "gs_ring", "gs_gather", "out_xent",
-                "gemm_nn", "gemm_tn", "launches")
+                "gemm_nn", "gemm_tn", "gemm_nn_w", "gemm_tn_w", "launches")
 
 
 def path_counts(reset=False):

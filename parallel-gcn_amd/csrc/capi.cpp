@@ -36,7 +36,7 @@ namespace {
 std::atomic<long long> g_path_hits[KP_COUNT];
 const char *const kPathNames[KP_COUNT] = {"xs_nn_ring", "xs_tn_ring", "xs_nn",   "xs_tn",
                                           "gs_ring",    "gs_gather",  "out_xent", "gemm_nn",
-                                          "gemm_tn",    "launches"};
+                                          "gemm_tn",    "gemm_nn_w",  "gemm_tn_w", "launches"};
 }  // namespace
 void note_path(KernelPath p) { g_path_hits[p].fetch_add(1, std::memory_order_relaxed); }
 }  // namespace pgcn

@@ -667,6 +667,11 @@ static void gemm_nn_slab(int M, int N, int K, const float *A, int lda, const flo
     launch_xstream_nn(M, N, K, A, lda, B, ldb, trans_b, C, ldc, nullptr, 1.0f, s, nullptr);
     return;
   }
+  if (g_gemm_variant != 1 && gemm_wide_ok(N)) {
+    launch_gemm_nn_wide(M, N, K, A, lda, B, ldb, trans_b, C, ldc, a_mask, mask_base, mask_ld,
+                        a_scale, s, nst);
+    return;
+  }
   note_path(KP_GEMM_NN);
   const int nt = (N + 15) / 16;
   const dim3 grid((unsigned)ceil_div(M, 64)), block(256);
@@ -724,6 +729,7 @@ static size_t plan_bytes(const TnPlan &p, int K) {
 size_t gemm_tn_workspace(int M, int N, int K) {
   N = std::min(N, 128);  // wider outputs run in 128-column slabs
   size_t ws = plan_bytes(tn_plan(M, N, K), K);  // either kernel family may run
+  if (gemm_wide_ok(N)) ws = std::max(ws, gemm_tn_wide_workspace(M, N, K));
   if (N <= 16) ws = std::max(ws, plan_bytes(xs_tn_plan(K), K));
   return ws;
 }
@@ -739,6 +745,16 @@ static void tn_reduce(const TnPlan &p, int M, int N, int K, float *partial, floa
                        dim3(256), 0, s, partial, p.n_slabs, elems, p.spg, part2);
   PGCN_LAUNCH(k_gemm_tn_reduce, dim3((unsigned)ceil_div(elems, 256)), dim3(256), 0, s,
                      part2, M > 0 ? p.n_groups : 0, K, N, p.ldp, C, ldc, nst);
+}
+
+void launch_slab_reduce(float *partial, int n_slabs, int K, int N, int ldp, float *C, int ldc,
+                        int nst, hipStream_t s) {
+  TnPlan p{};
+  p.n_slabs = n_slabs;
+  p.ldp = ldp;
+  p.spg = 16;
+  p.n_groups = (n_slabs + p.spg - 1) / p.spg;
+  tn_reduce(p, n_slabs, N, K, partial, C, ldc, s, nst);
 }
 
 static TnPlan blocks_plan(int n_blocks, int ldp) {
@@ -815,6 +831,12 @@ static void gemm_tn_slab(int M, int N, int K, const float *A, int lda, const flo
                          int nst) {
   if (!a_mask && xstream_ok(N, K) && nst == ldc) {
     launch_xstream_tn(M, N, K, A, lda, G, ldg, C, ldc, nullptr, 1.0f, workspace, s);
+    return;
+  }
+  if (g_gemm_variant != 1 && gemm_wide_ok(N) && ldg % 4 == 0 &&
+      (reinterpret_cast<size_t>(G) & 15) == 0) {
+    launch_gemm_tn_wide(M, N, K, A, lda, G, ldg, C, ldc, a_mask, mask_base, mask_ld, a_scale,
+                        workspace, s, nst);
     return;
   }
   const TnPlan p = tn_plan(M, N, K);

@@ -14,7 +14,7 @@ namespace pgcn {
 // which kernels a configuration took
 enum KernelPath {
   KP_XS_NN_RING, KP_XS_TN_RING, KP_XS_NN, KP_XS_TN, KP_GS_RING, KP_GS_GATHER, KP_OUT_XENT,
-  KP_GEMM_NN, KP_GEMM_TN, KP_LAUNCHES, KP_COUNT
+  KP_GEMM_NN, KP_GEMM_TN, KP_GEMM_NN_W, KP_GEMM_TN_W, KP_LAUNCHES, KP_COUNT
 };
 void note_path(KernelPath p);
 // every kernel launch of the library goes through this (counted: "launches")
@@ -100,6 +100,20 @@ void launch_gemm_nn(int M, int N, int K, const float *A, int lda, const float *B
                     int trans_b, float *C, int ldc, const uint64_t *a_mask, long long mask_base,
                     long long mask_ld, float a_scale, hipStream_t s);
 size_t gemm_tn_workspace(int M, int N, int K);
+// wide outputs (k_gemm_wide.hip): N in 65..128 (the hidden-128 layers), register-blocked MFMA
+bool gemm_wide_ok(int N);
+void launch_gemm_nn_wide(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
+                         int trans_b, float *C, int ldc, const uint64_t *a_mask,
+                         long long mask_base, long long mask_ld, float a_scale, hipStream_t s,
+                         int nst);
+size_t gemm_tn_wide_workspace(int M, int N, int K);
+void launch_gemm_tn_wide(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
+                         float *C, int ldc, const uint64_t *a_mask, long long mask_base,
+                         long long mask_ld, float a_scale, void *workspace, hipStream_t s,
+                         int nst);
+// ordered reduce of n_slabs partials [K][ldp] (k_gemm.hip): slab order, deterministic
+void launch_slab_reduce(float *partial, int n_slabs, int K, int N, int ldp, float *C, int ldc,
+                        int nst, hipStream_t s);
 // X-stream kernels (k_gemm.hip): N <= 16, K <= 640, dropout bits in the nibble layout
 bool xstream_ok(int N, int K);
 void launch_mask_nibbles(const uint64_t *mask, long long mask_base, long long mask_ld, int M,
