@@ -166,6 +166,9 @@ void build_dev_features(DevFeatures &feats, const int *fptr, const int *indices,
     if (xstream_ok(hidden0, F)) {
       feats.maskT.allocate((size_t)std::max(rows, 1) * 16);
       feats.maskT.zero();
+    } else if (gemm_wide_ok(std::min(hidden0, 128)) && F <= 1024) {
+      feats.maskW.allocate((size_t)std::max(rows, 1) * 16);
+      feats.maskW.zero();
     }
   } else {
     std::vector<int> ip((size_t)rows + 1);

@@ -195,8 +195,12 @@ void SparseMatmul::forward(bool training, const Stream &s) const {
                       c->dev_data.get(), c->ld, mask ? x->maskT.get() : nullptr, scale, s.get(),
                       nullptr, &e);
   } else if (x->dense) {
+    // wide outputs: the mask in the nibble layout too (one pass over the bitmap; the wide
+    // kernels then read one word per row and 4 steps, and the backward reuses it)
+    const uint64_t *mw = mask && x->maskW ? x->maskW.get() : nullptr;
+    if (mw) launch_mask_nibbles(mask, base, x->cols, x->rows, x->cols, x->maskW.get(), s.get());
     launch_gemm_nn(x->rows, b->cols, x->cols, x->x.get(), x->ldx, b->dev_data.get(), b->ld, 0,
-                   c->dev_data.get(), c->ld, mask, base, x->cols, scale, s.get());
+                   c->dev_data.get(), c->ld, mask, base, x->cols, scale, s.get(), mw);
   } else {
     launch_spmm_csr(x->rows, b->cols, c->ld, x->indptr.get(), x->indices.get(), x->values.get(),
                     mask, base, scale, b->dev_data.get(), c->dev_data.get(), s.get());
@@ -216,7 +220,7 @@ void SparseMatmul::backward(const Stream &s) const {
   } else if (x->dense) {
     launch_gemm_tn(x->rows, b->cols, x->cols, x->x.get(), x->ldx, c->dev_grad.get(), c->ld,
                    b->dev_grad.get(), b->ld, mask, base, x->cols, scale, ctx->gemm_workspace,
-                   s.get());
+                   s.get(), mask && x->maskW ? x->maskW.get() : nullptr);
   } else {
     launch_spmm_csc_bwd(x->cols, b->cols, c->ld, x->csc_ptr.get(), x->csc_row.get(),
                         x->csc_pos.get(), x->values.get(), mask, base, scale, c->dev_grad.get(),

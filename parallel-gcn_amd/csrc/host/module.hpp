@@ -56,6 +56,9 @@ struct DevFeatures {
   // dense + X-stream kernels: the input dropout's keep bits in the nibble layout
   // (k_mask_nibbles, [rows][16] words), rebuilt by every training forward
   DeviceBuffer<uint64_t> maskT;
+  // dense + wide first layer (k_gemm_wide.hip, 33..128 outputs, F <= 1024): the same nibble
+  // layout for the wide kernels' dropout bits, rebuilt by every training forward
+  DeviceBuffer<uint64_t> maskW;
   // sparse: CSR (+ transposed index for the weight gradient)
   DeviceBuffer<int> indptr, indices, csc_ptr, csc_row, csc_pos;
   DeviceBuffer<float> values;

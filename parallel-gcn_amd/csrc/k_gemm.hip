@@ -639,11 +639,11 @@ void launch_xstream_nn(int M, int N, int K, const float *A, int lda, const float
 static void gemm_nn_slab(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
                          int trans_b, float *C, int ldc, const uint64_t *a_mask,
                          long long mask_base, long long mask_ld, float a_scale, hipStream_t s,
-                         int nst);
+                         int nst, const uint64_t *maskT);
 
 void launch_gemm_nn(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
                     int trans_b, float *C, int ldc, const uint64_t *a_mask, long long mask_base,
-                    long long mask_ld, float a_scale, hipStream_t s) {
+                    long long mask_ld, float a_scale, hipStream_t s, const uint64_t *maskT) {
   PGCN_CHECK(lda % 4 == 0 && lda >= K, PGCN_E_INVALID, "gemm: lda must be a multiple of 4 >= K");
   PGCN_CHECK(N >= 1, PGCN_E_INVALID, "gemm: N must be >= 1");
   if (M <= 0) return;
@@ -652,24 +652,24 @@ void launch_gemm_nn(int M, int N, int K, const float *A, int lda, const float *B
     for (int j0 = 0; j0 < N; j0 += 128)
       gemm_nn_slab(M, std::min(128, N - j0), K, A, lda,
                    trans_b ? B + (long long)j0 * ldb : B + j0, ldb, trans_b, C + j0, ldc, a_mask,
-                   mask_base, mask_ld, a_scale, s, j0 + 128 >= N ? ldc - j0 : 128);
+                   mask_base, mask_ld, a_scale, s, j0 + 128 >= N ? ldc - j0 : 128, maskT);
     return;
   }
   gemm_nn_slab(M, N, K, A, lda, B, ldb, trans_b, C, ldc, a_mask, mask_base, mask_ld, a_scale, s,
-               ldc);
+               ldc, maskT);
 }
 
 static void gemm_nn_slab(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
                          int trans_b, float *C, int ldc, const uint64_t *a_mask,
                          long long mask_base, long long mask_ld, float a_scale, hipStream_t s,
-                         int nst) {
+                         int nst, const uint64_t *maskT) {
   if (!a_mask && xstream_ok(N, K) && nst == ldc) {
     launch_xstream_nn(M, N, K, A, lda, B, ldb, trans_b, C, ldc, nullptr, 1.0f, s, nullptr);
     return;
   }
   if (g_gemm_variant != 1 && gemm_wide_ok(N)) {
     launch_gemm_nn_wide(M, N, K, A, lda, B, ldb, trans_b, C, ldc, a_mask, mask_base, mask_ld,
-                        a_scale, s, nst);
+                        a_scale, s, nst, a_mask && K <= 1024 ? maskT : nullptr);
     return;
   }
   note_path(KP_GEMM_NN);
@@ -807,28 +807,30 @@ void launch_xstream_tn(int M, int N, int K, const float *A, int lda, const float
 static void gemm_tn_slab(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
                          float *C, int ldc, const uint64_t *a_mask, long long mask_base,
                          long long mask_ld, float a_scale, void *workspace, hipStream_t s,
-                         int nst);
+                         int nst, const uint64_t *maskT);
 
 void launch_gemm_tn(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
                     float *C, int ldc, const uint64_t *a_mask, long long mask_base,
-                    long long mask_ld, float a_scale, void *workspace, hipStream_t s) {
+                    long long mask_ld, float a_scale, void *workspace, hipStream_t s,
+                    const uint64_t *maskT) {
   PGCN_CHECK(N >= 1, PGCN_E_INVALID, "gemm_tn: N must be >= 1");
   PGCN_CHECK(lda % 4 == 0 && lda >= K, PGCN_E_INVALID, "gemm_tn: lda must be a multiple of 4 >= K");
   if (N > 128) {  // 128-column slabs of G and C, one after another through the workspace,
     // each writing its own columns only (the last one also C's padding columns)
     for (int j0 = 0; j0 < N; j0 += 128)
       gemm_tn_slab(M, std::min(128, N - j0), K, A, lda, G + j0, ldg, C + j0, ldc, a_mask,
-                   mask_base, mask_ld, a_scale, workspace, s, j0 + 128 >= N ? ldc - j0 : 128);
+                   mask_base, mask_ld, a_scale, workspace, s, j0 + 128 >= N ? ldc - j0 : 128,
+                   maskT);
     return;
   }
   gemm_tn_slab(M, N, K, A, lda, G, ldg, C, ldc, a_mask, mask_base, mask_ld, a_scale, workspace, s,
-               ldc);
+               ldc, maskT);
 }
 
 static void gemm_tn_slab(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
                          float *C, int ldc, const uint64_t *a_mask, long long mask_base,
                          long long mask_ld, float a_scale, void *workspace, hipStream_t s,
-                         int nst) {
+                         int nst, const uint64_t *maskT) {
   if (!a_mask && xstream_ok(N, K) && nst == ldc) {
     launch_xstream_tn(M, N, K, A, lda, G, ldg, C, ldc, nullptr, 1.0f, workspace, s);
     return;
@@ -836,7 +838,7 @@ static void gemm_tn_slab(int M, int N, int K, const float *A, int lda, const flo
   if (g_gemm_variant != 1 && gemm_wide_ok(N) && ldg % 4 == 0 &&
       (reinterpret_cast<size_t>(G) & 15) == 0) {
     launch_gemm_tn_wide(M, N, K, A, lda, G, ldg, C, ldc, a_mask, mask_base, mask_ld, a_scale,
-                        workspace, s, nst);
+                        workspace, s, nst, a_mask && K <= 1024 ? maskT : nullptr);
     return;
   }
   const TnPlan p = tn_plan(M, N, K);

@@ -70,7 +70,10 @@ constexpr int WNN_KC = 64;             // k per LDS chunk of B^T
 constexpr int WNN_S = WNN_KC + 4;      // B^T row stride in floats (== 4 mod 64: 2-way at most)
 constexpr int WNN_ROWS = 128;          // rows per workgroup (4 waves x 2 tiles x 16)
 
-template <bool TRANS_B, bool MASKED>
+// Dropout bits of A (MK): 0 none, 1 the flat element-order bitmap (bit mask_base + row *
+// mask_ld + k), 2 the nibble layout of k_mask_nibbles (maskT[row][j] nibble c = bits of
+// k = 64c + 4j .. +3; K <= 1024).
+template <int NT, bool TRANS_B, int MK>
 __global__ __launch_bounds__(256, 2) void k_gemm_nn_w(int M, int N, int K,
                                                       const float *__restrict__ A, int lda,
                                                       const float *__restrict__ B, int ldb,
@@ -78,10 +81,12 @@ __global__ __launch_bounds__(256, 2) void k_gemm_nn_w(int M, int N, int K,
                                                       const uint64_t *__restrict__ a_mask,
                                                       long long mask_base, long long mask_ld,
                                                       float a_scale, int nst) {
-  constexpr int NT = 8;                        // 128 columns (past N: zero B columns)
-  constexpr int NC = 16 * NT;
-  constexpr int PER = NC * WNN_KC / 256;       // B elements per thread per chunk (32)
-  __shared__ float bt[2][NC * WNN_S];
+  constexpr bool MASKED = MK != 0;
+  constexpr int NC = 16 * NT;                  // columns of the tile (past N: zero B columns)
+  constexpr int NCP = NT <= 4 ? 64 : 128;      // staging width (columns past NC stay unused)
+  constexpr int PER = NCP * WNN_KC / 256;      // B elements per thread per chunk
+  static_assert(NC <= NCP, "staging covers the tile");
+  __shared__ float bt[2][NCP * WNN_S];
   const int tid = threadIdx.x;
   const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, i = lane & 15;
@@ -102,10 +107,10 @@ __global__ __launch_bounds__(256, 2) void k_gemm_nn_w(int M, int N, int K,
     for (int t = 0; t < NT; t++) acc[r][t] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   // B chunk c -> registers, element q of this thread: (j, kk) coalesced along B's rows
-  //   B [K][ldb]   : j = tid % 128, kk = tid / 128 + 2 q
+  //   B [K][ldb]   : j = tid % NCP, kk = tid / NCP + (256 / NCP) q
   //   B^T [N][ldb] : j = tid / 64 + 4 q, kk = tid % 64
-  const int sj = TRANS_B ? tid / 64 : tid % NC, skk = TRANS_B ? tid % WNN_KC : tid / NC;
-  constexpr int DJ = TRANS_B ? 4 : 0, DK = TRANS_B ? 0 : 2;
+  const int sj = TRANS_B ? tid / 64 : tid % NCP, skk = TRANS_B ? tid % WNN_KC : tid / NCP;
+  constexpr int DJ = TRANS_B ? 4 : 0, DK = TRANS_B ? 0 : 256 / NCP;
   // buffer loads: one 32-bit voffset per thread, the q stride in the scalar offset, rows past
   // B's (K rows of B, N rows of B^T) read as 0 by the descriptor's range check
   const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
@@ -168,18 +173,24 @@ __global__ __launch_bounds__(256, 2) void k_gemm_nn_w(int M, int N, int K,
       wc[r] = sh ? (wn0[r] >> sh) | (w1 << (64 - sh)) : wn0[r];
     }
   };
-  load_raw(0, 0, ar[0]);
-  if (nchunks > 0) {
-    load_raw(0, 1, ar[1]);
-    load_raw(0, 2, ar[2]);
+  // nibble masks: the lane's words of its two rows, j = 4 s + g (every chunk takes nibble c)
+  uint64_t nw[2][4];
+  if constexpr (MK == 2) {
+#pragma unroll
+    for (int r = 0; r < 2; r++)
+#pragma unroll
+      for (int s = 0; s < 4; s++) nw[r][s] = a_mask[row[r] * 16 + 4 * s + g];
   }
-  if constexpr (MASKED) load_win(0);
+  load_raw(0, 0, ar[0]);
+  load_raw(0, 1, ar[1]);
+  load_raw(0, 2, ar[2]);
+  if constexpr (MK == 1) load_win(0);
   for (int c = 0; c < nchunks; c++) {
     const int buf = c & 1;
-    if constexpr (MASKED) make_win(c);
+    if constexpr (MK == 1) make_win(c);
     if (c + 1 < nchunks) {
       load_chunk(c + 1);  // in flight during this chunk's MFMAs
-      if constexpr (MASKED) load_win(c + 1);
+      if constexpr (MK == 1) load_win(c + 1);
     }
     const bool tail = c * WNN_KC + WNN_KC > K;
     const float *bl = &bt[buf][i * WNN_S + 4 * g];
@@ -204,7 +215,8 @@ __global__ __launch_bounds__(256, 2) void k_gemm_nn_w(int M, int N, int K,
       if constexpr (MASKED) {
 #pragma unroll
         for (int r = 0; r < 2; r++) {
-          const uint32_t bits = (uint32_t)(wc[r] >> (16 * s + 4 * g)) & 0xfu;
+          const uint32_t bits = MK == 1 ? (uint32_t)(wc[r] >> (16 * s + 4 * g)) & 0xfu
+                                        : (uint32_t)(nw[r][s] >> (4 * c)) & 0xfu;
           av[r].x *= (bits & 1) ? a_scale : 0.0f;
           av[r].y *= (bits & 2) ? a_scale : 0.0f;
           av[r].z *= (bits & 4) ? a_scale : 0.0f;
@@ -212,6 +224,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_nn_w(int M, int N, int K,
         }
       }
       const float4 a0 = av[0], a1 = av[1];
+      if (c * WNN_KC + 16 * s >= K) continue;  // a step wholly past K adds zeros: skipped
       float4 b[NT];
 #pragma unroll
       for (int t = 0; t < NT; t++) b[t] = *reinterpret_cast<const float4 *>(bl + 16 * t * WNN_S + 16 * s);
@@ -255,26 +268,177 @@ __global__ __launch_bounds__(256, 2) void k_gemm_nn_w(int M, int N, int K,
     }
 }
 
-bool gemm_wide_ok(int N) { return N > 64 && N <= 128; }
+// Persistent NN for K <= 128 (the hidden layers' products and input grads, the output layer):
+// all of B^T stays in LDS (one or two 64-k chunks, staged once) and a workgroup walks row
+// tiles blockIdx.x, blockIdx.x + gridDim.x, ..; the A ring runs on across tiles, so the next
+// tile's first steps load while this tile's last ones compute.  Same MFMA sequence per tile.
+template <int NT, bool TRANS_B, int NCH>
+__global__ __launch_bounds__(256, 2) void k_gemm_nn_wp(int M, int N, int K,
+                                                       const float *__restrict__ A, int lda,
+                                                       const float *__restrict__ B, int ldb,
+                                                       float *__restrict__ C, int ldc, int nst) {
+  constexpr int NCP = NT <= 4 ? 64 : 128;
+  constexpr int PER = NCP * WNN_KC / 256;
+  constexpr int US = 4 * NCH;  // steps per tile
+  __shared__ float bt[NCH][NCP * WNN_S];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, i = lane & 15;
+  {  // B^T, every chunk, once
+    const int sj = TRANS_B ? tid / 64 : tid % NCP, skk = TRANS_B ? tid % WNN_KC : tid / NCP;
+    constexpr int DJ = TRANS_B ? 4 : 0, DK = TRANS_B ? 0 : 256 / NCP;
+    const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float *>(B), 0, (int)((long long)(TRANS_B ? N : K) * ldb * 4), 0x00020000);
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+      const int k = c * WNN_KC + skk;
+      const bool ok = TRANS_B ? k < K : sj < N;
+      const int voff = 4 * (TRANS_B ? sj * ldb + k : k * ldb + sj);
+      const int sq = 4 * (TRANS_B ? DJ * ldb : DK * ldb);
+      float *d = &bt[c][sj * WNN_S + skk];
+#pragma unroll
+      for (int q = 0; q < PER; q++) {
+        const float v = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(brs, voff, sq * q, 0));
+        d[(DJ * WNN_S + DK) * q] = ok ? v : 0.0f;
+      }
+    }
+  }
+  const long long ntiles = ((long long)M + WNN_ROWS - 1) / WNN_ROWS;
+  auto row_of = [&](long long tile, int r) {
+    const long long rr = tile * WNN_ROWS + 32 * w + 16 * r + i;
+    return rr < M ? rr : (long long)M - 1;
+  };
+  float4 ar[4][2];
+  // step u of tile `tile` (u < US) into dst
+  auto load_step = [&](long long tile, int u, float4 (&dst)[2]) {
+    const int k = (u / 4) * WNN_KC + 16 * (u % 4) + 4 * g;
+#pragma unroll
+    for (int r = 0; r < 2; r++)
+      dst[r] = *reinterpret_cast<const float4 *>(A + row_of(tile, r) * (long long)lda +
+                                                 (k < K ? k : 0));  // k >= K: zeroed at use
+  };
+  long long tile = blockIdx.x;
+  if (tile < ntiles) {
+    load_step(tile, 0, ar[0]);
+    load_step(tile, 1, ar[1]);
+    load_step(tile, 2, ar[2]);
+  }
+  __syncthreads();
+  for (; tile < ntiles; tile += gridDim.x) {
+    floatx4 acc[2][NT];
+#pragma unroll
+    for (int r = 0; r < 2; r++)
+#pragma unroll
+      for (int t = 0; t < NT; t++) acc[r][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < US; u++) {
+      const int c = u / 4, s = u % 4;
+      {  // step u + 3 of the stream (this tile or the next one) into the slot u - 1 left
+        const int un = u + 3;
+        if (un < US) load_step(tile, un, ar[un & 3]);
+        else if (tile + gridDim.x < ntiles) load_step(tile + gridDim.x, un - US, ar[un & 3]);
+      }
+      float4 av[2] = {ar[u & 3][0], ar[u & 3][1]};
+      if (c * WNN_KC + WNN_KC > K) {
+        const int k = c * WNN_KC + 16 * s + 4 * g;
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+          av[r].x = k + 1 > K ? 0.f : av[r].x;
+          av[r].y = k + 2 > K ? 0.f : av[r].y;
+          av[r].z = k + 3 > K ? 0.f : av[r].z;
+          av[r].w = k + 4 > K ? 0.f : av[r].w;
+        }
+      }
+      const float4 a0 = av[0], a1 = av[1];
+      const float *bl = &bt[c][i * WNN_S + 4 * g];
+      if (c * WNN_KC + 16 * s >= K) continue;  // a step wholly past K adds zeros: skipped
+      float4 b[NT];
+#pragma unroll
+      for (int t = 0; t < NT; t++) b[t] = *reinterpret_cast<const float4 *>(bl + 16 * t * WNN_S + 16 * s);
+#pragma unroll
+      for (int t = 0; t < NT; t++) {
+        acc[0][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, b[t].x, acc[0][t], 0, 0, 0);
+        acc[1][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, b[t].x, acc[1][t], 0, 0, 0);
+      }
+#pragma unroll
+      for (int t = 0; t < NT; t++) {
+        acc[0][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, b[t].y, acc[0][t], 0, 0, 0);
+        acc[1][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, b[t].y, acc[1][t], 0, 0, 0);
+      }
+#pragma unroll
+      for (int t = 0; t < NT; t++) {
+        acc[0][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, b[t].z, acc[0][t], 0, 0, 0);
+        acc[1][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, b[t].z, acc[1][t], 0, 0, 0);
+      }
+#pragma unroll
+      for (int t = 0; t < NT; t++) {
+        acc[0][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, b[t].w, acc[0][t], 0, 0, 0);
+        acc[1][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, b[t].w, acc[1][t], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const long long rbase = tile * WNN_ROWS + 32 * w;
+#pragma unroll
+    for (int r = 0; r < 2; r++)
+#pragma unroll
+      for (int t = 0; t < NT; t++) {
+        const int col = 16 * t + i;
+        if (col >= nst) continue;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const long long rr = rbase + 16 * r + 4 * g + q;
+          if (rr < M) C[rr * ldc + col] = acc[r][t][q];
+        }
+      }
+  }
+}
+
+bool gemm_wide_ok(int N) { return N > 32 && N <= 128; }
 
 void launch_gemm_nn_wide(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
                          int trans_b, float *C, int ldc, const uint64_t *a_mask,
                          long long mask_base, long long mask_ld, float a_scale, hipStream_t s,
-                         int nst) {
-  PGCN_CHECK(gemm_wide_ok(N), PGCN_E_INVALID, "gemm_nn_wide: N must be in 65..128");
+                         int nst, const uint64_t *maskT) {
+  PGCN_CHECK(gemm_wide_ok(N), PGCN_E_INVALID, "gemm_nn_wide: N must be in 33..128");
+  PGCN_CHECK(!maskT || K <= 1024, PGCN_E_INVALID, "gemm_nn_wide: nibble masks need K <= 1024");
   if (M <= 0) return;
   note_path(KP_GEMM_NN_W);
   const dim3 grid((unsigned)ceil_div(M, WNN_ROWS)), block(256);
-#define WNN_LAUNCH(T, D)                                                                      \
-  PGCN_LAUNCH((k_gemm_nn_w<T, D>), grid, block, 0, s, M, N, K, A, lda, B, ldb, C, ldc, a_mask, \
-              mask_base, mask_ld, a_scale, nst)
-  if (trans_b) {
-    if (a_mask) WNN_LAUNCH(true, true);
-    else WNN_LAUNCH(true, false);
-  } else {
-    if (a_mask) WNN_LAUNCH(false, true);
-    else WNN_LAUNCH(false, false);
+  const int nt = (N + 15) / 16;
+  if (!a_mask && K <= 2 * WNN_KC) {  // B stays in LDS: persistent row-tile walk
+    const long long ntiles = ceil_div(M, WNN_ROWS);
+    const dim3 pgrid((unsigned)std::min<long long>(ntiles, 2LL * kCUs));
+#define WNP_LAUNCH(T, D, NCH)                                                                \
+  PGCN_LAUNCH((k_gemm_nn_wp<T, D, NCH>), pgrid, block, 0, s, M, N, K, A, lda, B, ldb, C, ldc, nst)
+#define WNP_CH(T, D) \
+  if (K <= WNN_KC) WNP_LAUNCH(T, D, 1); \
+  else WNP_LAUNCH(T, D, 2);
+#define WNP_T(T) \
+  if (trans_b) { WNP_CH(T, true) } else { WNP_CH(T, false) }
+    if (nt <= 3) { WNP_T(3) }
+    else if (nt == 4) { WNP_T(4) }
+    else { WNP_T(8) }
+#undef WNP_T
+#undef WNP_CH
+#undef WNP_LAUNCH
+    return;
   }
+  const int mk = maskT ? 2 : (a_mask ? 1 : 0);
+  const uint64_t *mp = maskT ? maskT : a_mask;
+#define WNN_LAUNCH(T, D, MK)                                                                  \
+  PGCN_LAUNCH((k_gemm_nn_w<T, D, MK>), grid, block, 0, s, M, N, K, A, lda, B, ldb, C, ldc, mp, \
+              mask_base, mask_ld, a_scale, nst)
+#define WNN_MK(T, D)                 \
+  if (mk == 2) WNN_LAUNCH(T, D, 2);  \
+  else if (mk == 1) WNN_LAUNCH(T, D, 1); \
+  else WNN_LAUNCH(T, D, 0);
+#define WNN_T(T)                \
+  if (trans_b) { WNN_MK(T, true) } else { WNN_MK(T, false) }
+  if (nt <= 3) { WNN_T(3) }
+  else if (nt == 4) { WNN_T(4) }
+  else { WNN_T(8) }
+#undef WNN_T
+#undef WNN_MK
 #undef WNN_LAUNCH
 }
 
@@ -287,7 +451,7 @@ void launch_gemm_nn_wide(int M, int N, int K, const float *A, int lda, const flo
 // -- output rows k = kb + 4i' + c (i' = the MFMA's row index), columns n = 64 (t / 4) + 4i'' +
 // t % 4 (i'' = its column index) -- reduces over the 4 rows g.  A ring of 4 steps: 3 load while
 // one computes.
-template <int WK, bool MASKED>
+template <int NH, int WK, int MK>
 __global__ __launch_bounds__(256, 2) void k_gemm_tn_w(int M, int N, int K, int slab,
                                                       const float *__restrict__ A, int lda,
                                                       const float *__restrict__ G, int ldg,
@@ -295,8 +459,9 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tn_w(int M, int N, int K, int s
                                                       long long mask_base, long long mask_ld,
                                                       float a_scale, float *__restrict__ partial,
                                                       int ldp) {
+  constexpr bool MASKED = MK != 0;
   constexpr int WR = 4 / WK;
-  constexpr int NT = 8;
+  constexpr int NT = 4 * NH;  // NH float4s of G per lane and step: 64 NH columns
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4, i = lane & 15;
   const int wk = w % WK, wr = w / WK;
@@ -327,9 +492,11 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tn_w(int M, int N, int K, int s
     st.a = *reinterpret_cast<const float4 *>(A + row * (long long)lda + kl);
     const float *gr = G + row * (long long)ldg;
     st.b0 = *reinterpret_cast<const float4 *>(gr + nl0);
-    st.b1 = *reinterpret_cast<const float4 *>(gr + nl1);
+    if constexpr (NH == 2) st.b1 = *reinterpret_cast<const float4 *>(gr + nl1);
     int sh = 0;
-    if constexpr (MASKED) {
+    if constexpr (MK == 2) {
+      st.w0 = a_mask[row * 16 + i];  // nibble kb / 64 holds bits ka .. ka + 3
+    } else if constexpr (MK == 1) {
       const long long p = mask_base + row * mask_ld + kl;
       const long long lo = p >> 6;
       sh = (int)(p & 63);
@@ -348,16 +515,27 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tn_w(int M, int N, int K, int s
     a.z = ka + 3 <= K ? a.z : 0.f;
     a.w = ka + 4 <= K ? a.w : 0.f;
     if constexpr (MASKED) {
-      const int sh = st.meta >> 1;
+      const int sh = MK == 2 ? kb / 16 : st.meta >> 1;
       // (bits past K: zero data anyway)
-      const uint64_t v = (st.w0 >> sh) | (sh > 60 ? st.w1 << (64 - sh) : 0ull);
+      const uint64_t v =
+          (st.w0 >> sh) | (MK == 1 && sh > 60 ? st.w1 << (64 - sh) : 0ull);
       const uint32_t bits = (uint32_t)v & 0xfu;
       a.x *= (bits & 1) ? a_scale : 0.0f;
       a.y *= (bits & 2) ? a_scale : 0.0f;
       a.z *= (bits & 4) ? a_scale : 0.0f;
       a.w *= (bits & 8) ? a_scale : 0.0f;
     }
-    float bv[NT] = {st.b0.x, st.b0.y, st.b0.z, st.b0.w, st.b1.x, st.b1.y, st.b1.z, st.b1.w};
+    float bv[NT];
+    bv[0] = st.b0.x;
+    bv[1] = st.b0.y;
+    bv[2] = st.b0.z;
+    bv[3] = st.b0.w;
+    if constexpr (NH == 2) {
+      bv[4] = st.b1.x;
+      bv[5] = st.b1.y;
+      bv[6] = st.b1.z;
+      bv[7] = st.b1.w;
+    }
 #pragma unroll
     for (int t = 0; t < NT; t++) {
       const int col = 64 * (t / 4) + 4 * i + t % 4;
@@ -443,8 +621,9 @@ struct TnWidePlan {
 static TnWidePlan tn_wide_plan(int M, int N, int K) {
   (void)N;
   TnWidePlan p;
-  p.ldp = 128;  // the partial's row: all 128 columns (zero past N)
+  p.ldp = N <= 64 ? 64 : 128;  // the partial's row: all 64 NH columns (zero past N)
   const int nkc = (K + 63) / 64;
+  // waves along k: one 64-k chunk each (r03: 4 along k spilled its epilogue, 6.4 vs 0.58 ms)
   p.wk = nkc >= 2 ? 2 : 1;
   p.kgroups = (nkc + p.wk - 1) / p.wk;
   const int wr = 4 / p.wk;
@@ -467,8 +646,9 @@ size_t gemm_tn_wide_workspace(int M, int N, int K) {
 void launch_gemm_tn_wide(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
                          float *C, int ldc, const uint64_t *a_mask, long long mask_base,
                          long long mask_ld, float a_scale, void *workspace, hipStream_t s,
-                         int nst) {
-  PGCN_CHECK(gemm_wide_ok(N), PGCN_E_INVALID, "gemm_tn_wide: N must be in 65..128");
+                         int nst, const uint64_t *maskT) {
+  PGCN_CHECK(gemm_wide_ok(N), PGCN_E_INVALID, "gemm_tn_wide: N must be in 33..128");
+  PGCN_CHECK(!maskT || K <= 1024, PGCN_E_INVALID, "gemm_tn_wide: nibble masks need K <= 1024");
   PGCN_CHECK(ldg % 4 == 0 && (reinterpret_cast<size_t>(G) & 15) == 0, PGCN_E_INVALID,
              "gemm_tn_wide: G rows must be 16-B aligned");
   const TnWidePlan p = tn_wide_plan(M, N, K);
@@ -476,16 +656,21 @@ void launch_gemm_tn_wide(int M, int N, int K, const float *A, int lda, const flo
   if (M > 0) {
     note_path(KP_GEMM_TN_W);
     const dim3 grid((unsigned)p.n_slabs, (unsigned)p.kgroups), block(256);
-#define WTN_LAUNCH(WK, D)                                                                     \
-  PGCN_LAUNCH((k_gemm_tn_w<WK, D>), grid, block, 0, s, M, N, K, p.slab, A, lda, G, ldg, a_mask, \
-              mask_base, mask_ld, a_scale, partial, p.ldp)
-    if (p.wk == 2) {
-      if (a_mask) WTN_LAUNCH(2, true);
-      else WTN_LAUNCH(2, false);
-    } else {
-      if (a_mask) WTN_LAUNCH(1, true);
-      else WTN_LAUNCH(1, false);
-    }
+    const int mk = maskT ? 2 : (a_mask ? 1 : 0);
+    const uint64_t *mp = maskT ? maskT : a_mask;
+#define WTN_LAUNCH(NH, WK, MK)                                                                 \
+  PGCN_LAUNCH((k_gemm_tn_w<NH, WK, MK>), grid, block, 0, s, M, N, K, p.slab, A, lda, G, ldg,   \
+              mp, mask_base, mask_ld, a_scale, partial, p.ldp)
+#define WTN_MK(NH, WK)                  \
+  if (mk == 2) WTN_LAUNCH(NH, WK, 2);     \
+  else if (mk == 1) WTN_LAUNCH(NH, WK, 1); \
+  else WTN_LAUNCH(NH, WK, 0);
+#define WTN_WK(NH)                          \
+  if (p.wk == 2) { WTN_MK(NH, 2) } else { WTN_MK(NH, 1) }
+    if (N <= 64) { WTN_WK(1) }
+    else { WTN_WK(2) }
+#undef WTN_WK
+#undef WTN_MK
 #undef WTN_LAUNCH
   }
   launch_slab_reduce(partial, M > 0 ? p.n_slabs : 0, K, N, p.ldp, C, ldc, nst, s);

@@ -96,21 +96,25 @@ void launch_graphsum_ring(const LdsSchedule &s, const float *in, int ld_in, floa
                           const int *col_map = nullptr, const GsEpilogue *epi = nullptr,
                           bool prestaged = false);
 
+// maskT (optional): the same dropout bits in the nibble layout, read by the wide kernels
 void launch_gemm_nn(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
                     int trans_b, float *C, int ldc, const uint64_t *a_mask, long long mask_base,
-                    long long mask_ld, float a_scale, hipStream_t s);
+                    long long mask_ld, float a_scale, hipStream_t s,
+                    const uint64_t *maskT = nullptr);
 size_t gemm_tn_workspace(int M, int N, int K);
-// wide outputs (k_gemm_wide.hip): N in 65..128 (the hidden-128 layers), register-blocked MFMA
+// wide outputs (k_gemm_wide.hip): N in 33..128 (the hidden-128 layers and their output layer),
+// register-blocked MFMA; maskT: A's dropout bits in the nibble layout (k_mask_nibbles, K <=
+// 1024) instead of the flat bitmap a_mask
 bool gemm_wide_ok(int N);
 void launch_gemm_nn_wide(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
                          int trans_b, float *C, int ldc, const uint64_t *a_mask,
                          long long mask_base, long long mask_ld, float a_scale, hipStream_t s,
-                         int nst);
+                         int nst, const uint64_t *maskT = nullptr);
 size_t gemm_tn_wide_workspace(int M, int N, int K);
 void launch_gemm_tn_wide(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
                          float *C, int ldc, const uint64_t *a_mask, long long mask_base,
                          long long mask_ld, float a_scale, void *workspace, hipStream_t s,
-                         int nst);
+                         int nst, const uint64_t *maskT = nullptr);
 // ordered reduce of n_slabs partials [K][ldp] (k_gemm.hip): slab order, deterministic
 void launch_slab_reduce(float *partial, int n_slabs, int K, int N, int ldp, float *C, int ldc,
                         int nst, hipStream_t s);
@@ -160,7 +164,8 @@ void launch_xstream_tn(int M, int N, int K, const float *A, int lda, const float
                        hipStream_t s);
 void launch_gemm_tn(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
                     float *C, int ldc, const uint64_t *a_mask, long long mask_base,
-                    long long mask_ld, float a_scale, void *workspace, hipStream_t s);
+                    long long mask_ld, float a_scale, void *workspace, hipStream_t s,
+                    const uint64_t *maskT = nullptr);
 
 void launch_spmm_csr(int m, int p, int ldc, const int *indptr, const int *indices,
                      const float *a, const uint64_t *mask, long long mask_base, float scale,

@@ -182,3 +182,27 @@ def test_xstream_ring_engine_matches_register_kernels(pgcn, rw_ds):
     cnt = helpers.split_counts(rw_ds)  # a near-tied row may flip: at most 3 rows per split
     for col, sp in ((1, 1), (3, 2)):
         assert np.abs(lines[1][:, col] - lines[0][:, col]).max() * cnt[sp] <= 3 + 1e-3
+
+
+def test_deep_reddit_width_matches_oracle(pgcn):
+    """4 layers x hidden 128 at reddit's feature width (F = 602, 10 k-chunks of 64): the first
+    layer's product and weight gradient run on the wide MFMA kernels (k_gemm_wide.hip) with
+    the input dropout in the nibble layout, the hidden layers' products and gradients on them
+    too (unmasked), against the oracle at 1e-4 (hpdga gcn.cpp:179-212 generalised to L layers,
+    src/gcn.cu:85-112)."""
+    ds = pgcn.Dataset.synthetic(24000, 602, 41, 240000, 43)
+    dims, drops = (128, 128, 128), (0.5, 0.5, 0.5, 0.5)
+    pgcn.reset_path_counts()
+    g = pgcn.GCN(pgcn.make_params(ds, hidden_dims=dims, dropouts=drops), ds)
+    ref = helpers.OracleGCN(helpers.ds_dict(ds), hidden_dims=dims, dropouts=drops)
+    cnt = helpers.split_counts(ds)
+    for e in range(2):
+        want, ties = ref.epoch_with_ties(ds.label, ds.split, ds.output_dim)
+        helpers.assert_line_close(g.train_epoch() + g.eval(2), want, cnt, what=f"epoch {e + 1}",
+                                  ties=ties)
+    paths = pgcn.path_counts()
+    g.close()
+    # per epoch: the wide NN for X W1 (training, masked), (Â X) W1 (eval), the hidden layers'
+    # products (train + eval) and input grads; the wide TN for every hidden weight gradient
+    assert paths["gemm_nn_w"] >= 2 * 8 and paths["gemm_tn_w"] >= 2 * 3, paths
+    assert paths["gemm_nn"] == 0 or paths["gemm_nn"] < paths["gemm_nn_w"], paths

@@ -37,7 +37,8 @@ def timeit(fn, reps=10):
 
 
 res = {"M": M}
-for (K, N, masked, tb) in ((602, 128, True, 0), (128, 128, False, 0), (41, 128, False, 1)):
+for (K, N, masked, tb) in ((602, 128, True, 0), (602, 128, False, 0), (128, 128, False, 0),
+                           (41, 128, False, 1), (128, 41, False, 0)):
     lda = (K + 3) // 4 * 4
     A = torch.zeros(M, lda, device=dev)
     A[:, :K] = torch.randn(M, K, device=dev)
@@ -48,7 +49,7 @@ for (K, N, masked, tb) in ((602, 128, True, 0), (128, 128, False, 0), (41, 128, 
     dW = torch.empty(K, N, device=dev)
     ws = torch.empty(lib.pgcn_gemm_tn_workspace(M, N, K) // 4 + 64, device=dev)
     flops = 2.0 * M * N * K
-    for variant in (0, 1):
+    for variant in ((0, 1) if os.environ.get("BOTH") else (0,)):
         lib.pgcn_debug_set(b"gemm_variant", variant)
 
         def nn():
@@ -60,7 +61,7 @@ for (K, N, masked, tb) in ((602, 128, True, 0), (128, 128, False, 0), (41, 128, 
                                       vp(mask) if masked else None, 0, K, 2.0, vp(ws), st), "tn")
         for name, fn in (("nn", nn), ("tn", tn)):
             ms = timeit(fn)
-            res[f"{name}_K{K}_N{N}_v{variant}"] = {"ms": round(ms, 4),
+            res[f"{name}_K{K}_N{N}{'m' if masked else ''}_v{variant}"] = {"ms": round(ms, 4),
                                                    "tflops": round(flops / ms / 1e9, 1),
                                                    "frac": round(flops / ms / 1e9 / 157.3, 3)}
     lib.pgcn_debug_set(b"gemm_variant", 0)
