@@ -205,8 +205,15 @@ int pgcn_loopback_create(int world, pgcn_loopback **out);
 int pgcn_loopback_destroy(pgcn_loopback *group);
 int pgcn_gcn_create_loopback(const pgcn_params *p, const pgcn_data *d, int device, int rank,
                              pgcn_loopback *group, pgcn_gcn **out);
+/* Diagnostics (timing only, tools/rank_epoch.py): rank `rank` of a `world`-rank edge-cut
+ * engine with no peers -- its kernels and stream order, collectives reduced to this rank's
+ * share ("comm" 3).  Its results are not the model's. */
+int pgcn_debug_gcn_create_solo(const pgcn_params *p, const pgcn_data *d, int device, int rank,
+                               int world, pgcn_gcn **out);
 int pgcn_gcn_destroy(pgcn_gcn *g);
-/* Engine facts: "world", "rank", "comm" (0 none, 1 RCCL, 2 loopback), "reassociated",
+/* Engine facts: "world", "rank", "comm" (0 none, 1 RCCL, 2 loopback, 3 solo), "comm_calls" /
+ * "comm_bytes" (collectives enqueued since creation and the bytes this rank sends in them,
+ * ring algorithm: a reduce-scatter (W-1)/W of its send buffer, an all-reduce twice that), "reassociated",
  * "graph_symmetric", "graphsum_lds" (width-16 GraphSums take the LDS kernel), "epochs",
  * "eval_ax_us" (device time of the Â X precompute at engine build, µs; 0 when not used).
  * Returns the value (>= 0) or PGCN_E_INVALID for an unknown key. */

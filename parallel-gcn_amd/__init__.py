@@ -103,6 +103,8 @@ _sig("pgcn_gcn_create_dist", c_int, P(PgcnParams), P(PgcnData), c_int, c_int, c_
      P(c_void_p))
 _sig("pgcn_gcn_destroy", c_int, c_void_p)
 _sig("pgcn_loopback_create", c_int, c_int, P(c_void_p))
+_sig("pgcn_debug_gcn_create_solo", c_int, P(PgcnParams), P(PgcnData), c_int, c_int, c_int,
+     P(c_void_p))
 _sig("pgcn_loopback_destroy", c_int, c_void_p)
 _sig("pgcn_gcn_create_loopback", c_int, P(PgcnParams), P(PgcnData), c_int, c_int, c_void_p,
      P(c_void_p))
@@ -278,10 +280,14 @@ class GCN:
     rank/world/unique_id are given (one process per GPU)."""
 
     def __init__(self, params, ds, device=0, rank=None, world=None, unique_id=None,
-                 loopback=None):
+                 loopback=None, solo=False):
         self.ds = ds  # keep the host data alive while the engine is built
         h = c_void_p()
-        if loopback is not None:
+        if solo:  # timing only: rank `rank` of `world` with no peers (pgcn_debug_gcn_create_solo)
+            check(lib.pgcn_debug_gcn_create_solo(ctypes.byref(params), ctypes.byref(ds.view),
+                                                 device, rank, world, ctypes.byref(h)),
+                  "gcn_create_solo")
+        elif loopback is not None:
             check(lib.pgcn_gcn_create_loopback(ctypes.byref(params), ctypes.byref(ds.view),
                                                device, rank, loopback._h, ctypes.byref(h)),
                   "gcn_create_loopback")
@@ -491,6 +497,7 @@ EXPORTED = [
     "pgcn_relu_bwd", "pgcn_xent_blocks", "pgcn_xent_fwd", "pgcn_finalize", "pgcn_adam",
     "pgcn_adam_step_size", "pgcn_params_default", "pgcn_gcn_create", "pgcn_comm_unique_id",
     "pgcn_gcn_create_dist", "pgcn_loopback_create", "pgcn_loopback_destroy",
+    "pgcn_debug_gcn_create_solo",
     "pgcn_gcn_create_loopback", "pgcn_gcn_query", "pgcn_gcn_destroy", "pgcn_gcn_train_epoch", "pgcn_gcn_eval",
     "pgcn_gcn_epoch_async", "pgcn_gcn_sync", "pgcn_gcn_results", "pgcn_gcn_run",
     "pgcn_gcn_get_var", "pgcn_gcn_num_vars", "pgcn_gcn_profile", "pgcn_gcn_profile_read",

@@ -391,6 +391,23 @@ int pgcn_gcn_create_dist(const pgcn_params *p, const pgcn_data *d, int device, i
   });
 }
 
+int pgcn_debug_gcn_create_solo(const pgcn_params *p, const pgcn_data *d, int device, int rank,
+                               int world, pgcn_gcn **out) {
+  return guarded([&] {
+    PGCN_CHECK(p && d && out && world >= 1 && rank >= 0 && rank < world, PGCN_E_INVALID,
+               "gcn_create_solo args");
+    check_device();
+    GCNData data = to_data(d, p);
+    DistSpec ds;
+    ds.rank = rank;
+    ds.world = world;
+    ds.solo = true;
+    auto h = std::make_unique<pgcn_gcn>();
+    h->g = std::make_unique<GCN>(to_params(p, d), to_adam(p), data, device, &ds);
+    *out = h.release();
+  });
+}
+
 int pgcn_loopback_create(int world, pgcn_loopback **out) {
   return guarded([&] {
     PGCN_CHECK(out, PGCN_E_INVALID, "loopback_create args");
@@ -427,7 +444,11 @@ long long pgcn_gcn_query(pgcn_gcn *g, const char *key) {
   const Comm *c = e.communicator();
   if (!std::strcmp(key, "world")) return c ? c->world() : 1;
   if (!std::strcmp(key, "rank")) return c ? c->rank() : 0;
-  if (!std::strcmp(key, "comm")) return c ? (!std::strcmp(c->kind(), "rccl") ? 1 : 2) : 0;
+  if (!std::strcmp(key, "comm"))
+    return c ? (!std::strcmp(c->kind(), "rccl") ? 1 : !std::strcmp(c->kind(), "loopback") ? 2 : 3)
+             : 0;
+  if (!std::strcmp(key, "comm_calls")) return c ? c->calls : 0;
+  if (!std::strcmp(key, "comm_bytes")) return c ? (long long)c->bytes : 0;
   if (!std::strcmp(key, "reassociated")) return e.reassociated() ? 1 : 0;
   if (!std::strcmp(key, "fused_tails")) return e.fused_tails();
   if (!std::strcmp(key, "graph_symmetric")) return e.symmetric() ? 1 : 0;

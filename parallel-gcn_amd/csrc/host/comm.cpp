@@ -148,13 +148,28 @@ RcclComm::~RcclComm() {
 
 void RcclComm::allreduce_sum(float *buf, size_t n, hipStream_t s) {
   if (world_ == 1 || n == 0) return;
+  count(n * sizeof(float), 2.0);
   PGCN_NCCL(ncclAllReduce(buf, buf, n, ncclFloat32, ncclSum, static_cast<ncclComm_t>(comm_), s));
 }
 
 void RcclComm::reduce_scatter_sum(const float *send, float *recv, size_t recvcount,
                                   hipStream_t s) {
+  count(recvcount * world_ * sizeof(float), 1.0);
   PGCN_NCCL(ncclReduceScatter(send, recv, recvcount, ncclFloat32, ncclSum,
                               static_cast<ncclComm_t>(comm_), s));
+}
+
+void SoloComm::allreduce_sum(float *buf, size_t n, hipStream_t s) {
+  (void)buf;
+  (void)s;
+  if (world_ > 1 && n > 0) count(n * sizeof(float), 2.0);
+}
+
+void SoloComm::reduce_scatter_sum(const float *send, float *recv, size_t recvcount,
+                                  hipStream_t s) {
+  count(recvcount * world_ * sizeof(float), 1.0);
+  PGCN_HIP(hipMemcpyAsync(recv, send + (size_t)rank_ * recvcount, recvcount * sizeof(float),
+                          hipMemcpyDeviceToDevice, s));
 }
 
 // ------------------------------------------------------------------------------------------
@@ -240,6 +255,7 @@ void LoopbackComm::collective(const float *send, float *dst, size_t count, size_
 
 void LoopbackComm::allreduce_sum(float *buf, size_t n, hipStream_t s) {
   if (world_ == 1 || n == 0) return;
+  count(n * sizeof(float), 2.0);
   if (tmp_n_ < n) {
     if (tmp_) PGCN_HIP(hipFree(tmp_));
     tmp_ = nullptr;
@@ -253,6 +269,7 @@ void LoopbackComm::allreduce_sum(float *buf, size_t n, hipStream_t s) {
 
 void LoopbackComm::reduce_scatter_sum(const float *send, float *recv, size_t recvcount,
                                       hipStream_t s) {
+  count(recvcount * world_ * sizeof(float), 1.0);
   collective(send, recv, recvcount, (size_t)rank_ * recvcount, s);
 }
 

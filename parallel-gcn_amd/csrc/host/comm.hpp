@@ -63,9 +63,29 @@ class Comm {
                                   hipStream_t s) = 0;
   virtual const char *kind() const = 0;
   static void unique_id(void *out128);  // RCCL unique id (rank 0 creates, all share)
+  // collectives enqueued and the bytes this rank sends into them (a ring reduce-scatter of a
+  // send buffer of B bytes moves B (world - 1) / world per rank; an all-reduce 2x that)
+  long long calls = 0;
+  double bytes = 0.0;
 
  protected:
+  void count(size_t send_bytes, double factor) {
+    calls++;
+    bytes += factor * (double)send_bytes * (world_ - 1) / world_;
+  }
   int rank_, world_;
+};
+
+// Timing only (tools/rank_epoch.py): rank `rank` of `world` with no peers -- a reduce-scatter
+// keeps this rank's own share, an all-reduce leaves the buffer.  The rank's kernels and
+// stream order are the edge-cut engine's; its numbers are not (no other rank contributes).
+class SoloComm : public Comm {
+ public:
+  SoloComm(int rank, int world) : Comm(rank, world) {}
+  void allreduce_sum(float *buf, size_t n, hipStream_t s) override;
+  void reduce_scatter_sum(const float *send, float *recv, size_t recvcount,
+                          hipStream_t s) override;
+  const char *kind() const override { return "solo"; }
 };
 
 // One process per GPU over RCCL (xGMI on one node).

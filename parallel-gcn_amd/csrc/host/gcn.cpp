@@ -262,7 +262,9 @@ GCN::GCN(const GCNParams &params_, const AdamParams &adam, const GCNData &data, 
   part = make_partition(params.num_nodes, data.graph.indptr.data(), world, rank,
                         dist ? kRsChunks : 1);
   if (dist) {  // the edge-cut path (also at world == 1, which exercises it on one GPU)
-    if (dist->loopback)
+    if (dist->solo)
+      comm = std::make_unique<SoloComm>(rank, world);
+    else if (dist->loopback)
       comm = std::make_unique<LoopbackComm>(rank, dist->loopback);
     else
       comm = std::make_unique<RcclComm>(rank, world, dist->unique_id);

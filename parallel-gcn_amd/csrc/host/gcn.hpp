@@ -76,6 +76,7 @@ struct DistSpec {
   const void *unique_id = nullptr;  // 128 bytes (RCCL)
   // in-process ranks on one device (LoopbackComm) instead of RCCL; world = group->world()
   std::shared_ptr<LoopbackGroup> loopback;
+  bool solo = false;  // timing only: SoloComm (no peers)
 };
 
 class GCN {
