@@ -169,7 +169,6 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
   // run up to 3 chunks past the stream's end (the entries array has 2 KB of slack)
   const char *esrc = reinterpret_cast<const char *>(entries) + kb0 * 128 + lane * 16;
   const unsigned ring_dst = lds_base + (unsigned)(RING_ERING_OFF + wave * RING_ERING_B);
-  const char *ring = lb + RING_ERING_OFF + wave * RING_ERING_B + g * 8;
   auto refill = [&](int c) {  // chunk c -> ring slot c % 4
     if (lane < 32) glds16(esrc, ring_dst + (unsigned)((c & (RING_ESLOTS - 1)) * RING_CHUNK));
     esrc += RING_CHUNK;
@@ -180,29 +179,42 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
   refill(3);
   asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // chunk 0
 
-  float4 acc[LDS_SLOTS];
+  f4v acc[LDS_SLOTS];
 #pragma unroll
-  for (int j = 0; j < LDS_SLOTS; j++) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int j = 0; j < LDS_SLOTS; j++) acc[j] = f4v{0.f, 0.f, 0.f, 0.f};
+  // Entry ring cursor: this lane's LDS byte address of the next block's entries, and the
+  // blocks left in the current 4-block chunk (r03: per block one VALU add and a scalar
+  // count-down, where the ring offset arithmetic and the chunk test took six scalar ops)
+  unsigned ecur = ring_dst + (unsigned)(g * 8);
+  const unsigned ering_end = ring_dst + (unsigned)RING_ERING_B;
+  int left = RING_CHUNK / 128;
   int chunk = 0;
-  int roff = 0;
-  static_assert((RING_ERING_B & (RING_ERING_B - 1)) == 0, "ring wraps by masking");
-  uint2 e_next = *reinterpret_cast<const uint2 *>(ring);
-  // next entry block (its refill when a chunk is entered).  The slot refilled holds the chunk
-  // before this one: the read of its last entry block (the caller's current entry, which
-  // hipcc waits for only where it is first used) must have returned before the DMA lands.
-  auto next_block = [&]() {
-    roff = (roff + 128) & (RING_ERING_B - 1);
-    if ((roff & (RING_CHUNK - 1)) == 0) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      ++chunk;
-      refill(chunk + 3);
-      asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-    }
-    e_next = *reinterpret_cast<const uint2 *>(ring + roff);
-  };
+  u2v e_next = ds_rd64(ecur);
   // lane (g, v) reads plane v: entry (ring row x 16 B) + this constant
-  const char *tb = lb + v * RING_PLANE_B;
-  auto rd = [&](unsigned off) { return *reinterpret_cast<const float4 *>(tb + off); };
+  const unsigned tb = lds_base + (unsigned)(v * RING_PLANE_B);
+  // One entry block: its four table addresses from the landed entries, then the next block's
+  // entry read (into the same registers: in-order issue reads them first), its chunk's refill
+  // when a chunk is entered (the slot refilled held the chunk before, whose last entries were
+  // waited for with the previous block), the four table reads, one wait, the adds.
+  auto block = [&](f4v &a) {
+    const unsigned a0 = tb + (e_next.x & 0xffffu), a1 = tb + (e_next.x >> 16),
+                   a2 = tb + (e_next.y & 0xffffu), a3 = tb + (e_next.y >> 16);
+    ecur += 128;
+    if (--left == 0) {
+      left = RING_CHUNK / 128;
+      ++chunk;
+      if (ecur >= ering_end) ecur -= RING_ERING_B;
+      refill(chunk + 3);
+      asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // chunk `chunk` landed
+    }
+    ds_rd64_into(e_next, ecur);
+    f4v x0 = ds_rd128(a0), x1 = ds_rd128(a1), x2 = ds_rd128(a2), x3 = ds_rd128(a3);
+    lgkm_wait<0>(x0, x1, x2, x3, e_next);
+    a += x0;
+    a += x1;
+    a += x2;
+    a += x3;
+  };
   for (int t = 0; t < T; t++) {
     lds_wait_ge(loaded, (unsigned)(t + RING_W));  // slices t .. t+2 and visit t's counts
     const uint4 *c4 = reinterpret_cast<const uint4 *>(lb + RING_CNT_OFF + (t % RING_NCB) * RING_CNT_B +
@@ -213,22 +225,13 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
         (unsigned)__builtin_amdgcn_readfirstlane(cw0.z), (unsigned)__builtin_amdgcn_readfirstlane(cw0.w),
         (unsigned)__builtin_amdgcn_readfirstlane(cw1.x), (unsigned)__builtin_amdgcn_readfirstlane(cw1.y),
         (unsigned)__builtin_amdgcn_readfirstlane(cw1.z), (unsigned)__builtin_amdgcn_readfirstlane(cw1.w)};
+    // per (rowset, visit): 0 blocks (half the pairs on reddit), 1 (92 % of the blocks) or more
 #pragma unroll
     for (int j = 0; j < LDS_SLOTS; j++) {
-      const int n = (cw[j >> 1] >> (16 * (j & 1))) & 0xffff;  // steps of rowset j (x 4)
-      for (int k = 0; k < n; k += 4) {
-        const uint2 e = e_next;
-        next_block();
-        // the next entry read goes out before this block's table reads: it returns first
-        // (LDS reads complete in order), so the next block finds it landed
-        asm volatile("" ::: "memory");
-        const float4 x0 = rd(e.x & 0xffffu), x1 = rd(e.x >> 16), x2 = rd(e.y & 0xffffu),
-                     x3 = rd(e.y >> 16);
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // one lgkmcnt(0) wait, then the adds
-        f4_acc(acc[j], x0);
-        f4_acc(acc[j], x1);
-        f4_acc(acc[j], x2);
-        f4_acc(acc[j], x3);
+      const unsigned n = (cw[j >> 1] >> (16 * (j & 1))) & 0xffffu;  // steps of rowset j (x 4)
+      if (n != 0) {
+        block(acc[j]);
+        for (unsigned k = 4; k < n; k += 4) block(acc[j]);
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every read of slice t returned
@@ -257,7 +260,7 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
   for (int j = 0; j < LDS_SLOTS; j++) {
     const int u = rw[j * 16];
     const int sp = __builtin_amdgcn_readfirstlane((int)((unsigned)u >> 28));
-    float4 a = acc[j];
+    float4 a = make_float4(acc[j].x, acc[j].y, acc[j].z, acc[j].w);
     for (int k = 0; k < sp; k++) {
       const int d = 4 << k;
       a.x += __shfl_xor(a.x, d);

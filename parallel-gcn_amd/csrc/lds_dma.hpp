@@ -54,6 +54,45 @@ __device__ __forceinline__ void glds16x4(const void *gsrc, unsigned lds_dst) {
       : "memory");
 }
 
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef unsigned u2v __attribute__((ext_vector_type(2)));
+
+// LDS reads issued from inline asm (LDS byte addresses): hipcc does not count them, so its
+// automatic waits do not drain them; every use goes behind an lgkm_wait<N> naming the
+// registers it waits for (the asm operands order the uses after it).
+__device__ __forceinline__ f4v ds_rd128(unsigned addr) {
+  f4v r;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(addr));
+  return r;
+}
+__device__ __forceinline__ u2v ds_rd64(unsigned addr) {
+  u2v r;
+  asm volatile("ds_read_b64 %0, %1" : "=v"(r) : "v"(addr));
+  return r;
+}
+// the same read into registers that hold the previous value (read first by earlier code)
+__device__ __forceinline__ void ds_rd64_into(u2v &r, unsigned addr) {
+  asm volatile("ds_read_b64 %0, %1" : "+v"(r) : "v"(addr));
+}
+// s_waitcnt lgkmcnt(N): at most N LDS operations of this wave still in flight
+template <int N>
+__device__ __forceinline__ void lgkm_wait(u2v &e) {
+  static_assert(N >= 0 && N < 16, "lgkmcnt is 4 bits");
+  asm volatile("s_waitcnt lgkmcnt(%c1)" : "+v"(e) : "n"(N));
+}
+template <int N>
+__device__ __forceinline__ void lgkm_wait(f4v &x0, f4v &x1, f4v &x2, f4v &x3, u2v &e) {
+  static_assert(N >= 0 && N < 16, "lgkmcnt is 4 bits");
+  asm volatile("s_waitcnt lgkmcnt(%c5)"
+               : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "+v"(e)
+               : "n"(N));
+}
+template <int N>
+__device__ __forceinline__ void lgkm_wait(f4v &x0, f4v &x1, f4v &x2, f4v &x3) {
+  static_assert(N >= 0 && N < 16, "lgkmcnt is 4 bits");
+  asm volatile("s_waitcnt lgkmcnt(%c4)" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3) : "n"(N));
+}
+
 __device__ __forceinline__ unsigned lds_wait_ge(const unsigned *p, unsigned target) {
   unsigned spins = 0;
   while (true) {
