@@ -27,6 +27,7 @@ extern int g_fuse_output;           // host/gcn.cpp
 extern int g_mm_side;               // host/gcn.cpp
 extern int g_eval_ax;               // host/gcn.cpp
 extern int g_epoch_graph;           // host/gcn.cpp
+extern int g_wide_prescale;        // host/graph.cpp
 extern long long g_lds_min_bytes;   // host/graph.cpp
 extern int g_lds_blocks;            // host/graph.cpp
 extern int g_xstream_ring;          // k_xstream_lds.hip
@@ -624,6 +625,7 @@ int pgcn_debug_set(const char *key, int value) {
       return PGCN_E_INVALID;
     pgcn::g_lds_blocks = value;
   } else if (!std::strcmp(key, "parse_threads")) pgcn::g_parse_threads = value;
+  else if (!std::strcmp(key, "wide_prescale")) pgcn::g_wide_prescale = value;
   else return PGCN_E_INVALID;
   return PGCN_OK;
 }

@@ -115,6 +115,7 @@ DevGraph::DevGraph(int n_rows, int n_cols, const int *indptr, const int *indices
 // padded rows): 3.7 MB table (4 ranks) LDS 0.123 vs plain 0.249 ms, 1.9 MB (8 ranks) 0.083 vs
 // 0.114 ms; 15 MB (1 rank) 0.33 vs 1.04 ms
 long long g_lds_min_bytes = DevGraph::kLdsMinBytes;
+int g_wide_prescale = 1;  // diagnostics ("wide_prescale" 0: one prescale launch per pass)
 
 int DevGraph::column_blocks(int dim) {
   const int vec = (dim + 3) / 4;
@@ -467,12 +468,23 @@ void DevGraph::graphsum(const float *in, int ld_in, float *out, int ld_out, int 
     const int ldm = std::min(ld_in, ld_out);
     PGCN_CHECK(!prestaged || (dim <= 16 && !col_map), PGCN_E_INVALID,
                "graphsum: prestaged input on a path without a ring table");
-    for (int c0 = 0; c0 < dim; c0 += 16) {
-      const int c = std::min(c0, ldm - 16);
+    const size_t table = (size_t)ceil_div(n_cols_, RING_SR) * RING_SR * 16;
+    RingPasses ps;
+    for (int c0 = 0; c0 < dim; c0 += 16) ps.c[ps.n++] = std::min(c0, ldm - 16);
+    // several passes: one launch prescales all of them (each pass then reads its own table)
+    const bool batch = ps.n > 1 && !col_map && ld_in <= 128 && g_wide_prescale;
+    if (batch) {
+      if (lds_->tables.size() < table * ps.n) lds_->tables.allocate(table * ps.n);
+      launch_ring_prescale_wide(lds_->s, in, ld_in, std::min(ld_in, ps.c[ps.n - 1] + 16), ps,
+                                lds_->tables.get(), (long long)table, s);
+    }
+    for (int p = 0; p < ps.n; p++) {
+      const int c = ps.c[p];
       GsEpilogue ep = epi ? *epi : GsEpilogue{};
       ep.col0 = c;
-      launch_graphsum_ring(lds_->s, in + c, ld_in, out + c, ld_out, lds_->scratch.get(),
-                           lds_->partial.get(), s, col_map, &ep, prestaged);
+      launch_graphsum_ring(lds_->s, in + c, ld_in, out + c, ld_out,
+                           batch ? lds_->tables.get() + table * p : lds_->scratch.get(),
+                           lds_->partial.get(), s, col_map, &ep, prestaged || batch);
     }
     return;
   }

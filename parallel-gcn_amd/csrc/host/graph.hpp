@@ -127,6 +127,7 @@ class DevGraph {
     DeviceBuffer<int2> slices;
     DeviceBuffer<int> n_slices, rows;
     DeviceBuffer<float> row_scale, col_scale, scratch, partial;
+    DeviceBuffer<float> tables;  // every pass's prescaled table of a wide call (lazily)
   };
   std::unique_ptr<LdsSched> lds_;
   std::vector<float> h_row_scale_, h_col_scale_;

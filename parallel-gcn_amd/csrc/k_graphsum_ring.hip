@@ -68,6 +68,45 @@ __global__ __launch_bounds__(256) void k_ring_prescale(const float4 *__restrict_
   out[(r / RING_SR) * (4 * RING_SR) + v * RING_SR + r % RING_SR] = x;
 }
 
+// Every 16-column pass of a wide GraphSum prescaled by one launch (r03): table p = the
+// k_ring_prescale output for input columns c[p] .. c[p] + 15.  A block stages 64 rows x up to
+// 128 columns through LDS (coalesced row reads, rows padded to 132 floats so 16 consecutive
+// rows' float4s are bank-distinct) and writes each (pass, plane) as 64 consecutive float4s
+// (1 KB) of its slice plane.  The same products as the per-pass prescale: same bits.
+constexpr int RPW_ROWS = 64;
+constexpr int RPW_LD = 132;
+static_assert(RING_SR % RPW_ROWS == 0, "a block's rows stay inside one slice");
+__global__ __launch_bounds__(256) void k_ring_prescale_wide(const float *__restrict__ in, int ld_in,
+                                                            int width, const float *__restrict__ scale,
+                                                            int n, RingPasses passes,
+                                                            float4 *__restrict__ out,
+                                                            long long table_f4) {
+  __shared__ float rows[RPW_ROWS * RPW_LD];
+  const int r0 = blockIdx.x * RPW_ROWS;
+  const int w4 = width / 4;  // float4s per row staged (width: multiple of 4, <= 128)
+  for (int e = threadIdx.x; e < RPW_ROWS * w4; e += 256) {
+    const int r = e / w4, q = e - r * w4;
+    float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r0 + r < n) {
+      x = *reinterpret_cast<const float4 *>(in + (long long)(r0 + r) * ld_in + 4 * q);
+      const float s = scale[r0 + r];
+      x.x *= s;
+      x.y *= s;
+      x.z *= s;
+      x.w *= s;
+    }
+    *reinterpret_cast<float4 *>(&rows[r * RPW_LD + 4 * q]) = x;
+  }
+  __syncthreads();
+  const long long slot0 = (long long)(r0 / RING_SR) * (4 * RING_SR) + r0 % RING_SR;
+  for (int e = threadIdx.x; e < passes.n * 4 * RPW_ROWS; e += 256) {
+    const int r = e % RPW_ROWS, pv = e / RPW_ROWS, p = pv >> 2, v = pv & 3;
+    if (r0 + r >= n) continue;
+    const float4 x = *reinterpret_cast<const float4 *>(&rows[r * RPW_LD + passes.c[p] + 4 * v]);
+    out[p * table_f4 + slot0 + v * RING_SR + r] = x;
+  }
+}
+
 // out[r] = scale[r] * sum_{b < nb} partial[b][r]   (block order => deterministic), then the
 // fused element-wise tail (gs_epilogue.hpp)
 __global__ __launch_bounds__(256) void k_gs_lds_combine(const float4 *__restrict__ partial,
@@ -278,6 +317,20 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
 // all 61 batches then runs at the kernel's end on 61 CUs), one prescale / combine launch for
 // all 16-column passes of a wide row (1.677 vs 1.594 ms per d = 128 call: the 8 passes'
 // partials no longer stay in the Infinity Cache), fixed issue priority (hand-off waits 22 %).
+
+void launch_ring_prescale_wide(const LdsSchedule &s, const float *in, int ld_in, int width,
+                               const RingPasses &passes, float *tables, long long table_floats,
+                               hipStream_t st) {
+  PGCN_CHECK(ld_in % 4 == 0 && width % 4 == 0 && width <= 128 && passes.n >= 1 && passes.n <= 8,
+             PGCN_E_INVALID, "ring_prescale_wide: shape");
+  for (int p = 0; p < passes.n; p++)
+    PGCN_CHECK(passes.c[p] % 4 == 0 && passes.c[p] + 16 <= width, PGCN_E_INVALID,
+               "ring_prescale_wide: pass columns");
+  PGCN_LAUNCH(k_ring_prescale_wide, dim3((unsigned)ceil_div(s.n_cols, RPW_ROWS)), dim3(256), 0, st,
+              in, ld_in, width, s.col_scale, s.n_cols, passes, reinterpret_cast<float4 *>(tables),
+              table_floats / 4);
+  PGCN_HIP(hipGetLastError());
+}
 
 void launch_graphsum_ring(const LdsSchedule &s, const float *in, int ld_in, float *out,
                           int ld_out, float *scratch_in, float *partial, hipStream_t st,

@@ -91,6 +91,15 @@ struct LdsSchedule {
 // prescale (skipped when `prestaged`: scratch_in already holds this call's prescaled input,
 // written by the epilogue of the kernel that produced `in`) + ring kernel + combine (+ epi);
 // scratch_in holds ceil(n_cols / RING_SR) slices
+// the column offsets of a wide GraphSum's 16-column passes (<= 8: d <= 128)
+struct RingPasses {
+  int n = 0;
+  int c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+};
+// every pass's prescaled table in one launch: tables + p * table_floats = pass p's scratch
+void launch_ring_prescale_wide(const LdsSchedule &s, const float *in, int ld_in, int width,
+                               const RingPasses &passes, float *tables, long long table_floats,
+                               hipStream_t st);
 void launch_graphsum_ring(const LdsSchedule &s, const float *in, int ld_in, float *out,
                           int ld_out, float *scratch_in, float *partial, hipStream_t st,
                           const int *col_map = nullptr, const GsEpilogue *epi = nullptr,

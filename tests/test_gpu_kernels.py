@@ -149,12 +149,15 @@ def test_graphsum_lds_wide_rows(pgcn, dim, ld):
                                           ctypes.byref(g)), "graph_create")
     xin = torch.from_numpy(x).to(DEV)
     outs = []
-    for _ in range(2):
-        out = torch.full((n, ld), float("nan"), device=DEV)
-        pgcn.check(pgcn.lib.pgcn_graphsum(g, vp(xin), ld, vp(out), ld, dim, stream()), "gs")
+    # runs 0, 1: every pass's table prescaled by one launch (default); run 2: one prescale
+    # launch per pass -- the same products, so the same bits
+    for wide in (1, 1, 0):
+        with helpers.knobs(pgcn, wide_prescale=wide):
+            out = torch.full((n, ld), float("nan"), device=DEV)
+            pgcn.check(pgcn.lib.pgcn_graphsum(g, vp(xin), ld, vp(out), ld, dim, stream()), "gs")
+            torch.cuda.synchronize()
         outs.append(out)
-    torch.cuda.synchronize()
-    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
     ours = outs[0].cpu().numpy()
     ref = oracle_graphsum(indptr, indices, x, dim)
     bound = abs_bound(indptr, indices, x, dim)
