@@ -507,13 +507,19 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tn_w(int M, int N, int K, int s
     }
     st.meta = (ok ? 1 : 0) | sh << 1;
   };
-  auto compute = [&](const Step &st) {
-    const bool ok = st.meta & 1;
+  // full: the step's 4 rows inside the slab (the loop's uniform test) -- then only the K and N
+  // tails (uniform per wave) need selects.  Operands are formed before the MFMAs (one write
+  // per register: a select rewriting an MFMA's source register while the MFMAs before it
+  // read it stalls the issue, r03 counters: 73 % of the wave cycles)
+  const bool ktail = kb + 64 > K, ntail = N < 64 * NH;
+  auto compute = [&](const Step &st, bool full) {
     float4 a = st.a;
-    a.x = ka + 1 <= K ? a.x : 0.f;
-    a.y = ka + 2 <= K ? a.y : 0.f;
-    a.z = ka + 3 <= K ? a.z : 0.f;
-    a.w = ka + 4 <= K ? a.w : 0.f;
+    if (ktail) {
+      a.x = ka + 1 <= K ? a.x : 0.f;
+      a.y = ka + 2 <= K ? a.y : 0.f;
+      a.z = ka + 3 <= K ? a.z : 0.f;
+      a.w = ka + 4 <= K ? a.w : 0.f;
+    }
     if constexpr (MASKED) {
       const int sh = MK == 2 ? kb / 16 : st.meta >> 1;
       // (bits past K: zero data anyway)
@@ -536,11 +542,15 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tn_w(int M, int N, int K, int s
       bv[6] = st.b1.z;
       bv[7] = st.b1.w;
     }
+    if (!full || ntail) {
+      const bool ok = st.meta & 1;
 #pragma unroll
-    for (int t = 0; t < NT; t++) {
-      const int col = 64 * (t / 4) + 4 * i + t % 4;
-      bv[t] = ok && col < N ? bv[t] : 0.0f;
+      for (int t = 0; t < NT; t++) {
+        const int col = 64 * (t / 4) + 4 * i + t % 4;
+        bv[t] = ok && col < N ? bv[t] : 0.0f;
+      }
     }
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int t = 0; t < NT; t++) {
       acc[0][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, bv[t], acc[0][t], 0, 0, 0);
@@ -560,19 +570,19 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tn_w(int M, int N, int K, int s
     for (long long n = 0; n < steps; n += 4) {
       load(s3, m + 3 * stride);
       __builtin_amdgcn_sched_barrier(0);
-      compute(s0);
+      compute(s0, m + 4 <= m_end);
       if (n + 1 >= steps) break;
       load(s0, m + 4 * stride);
       __builtin_amdgcn_sched_barrier(0);
-      compute(s1);
+      compute(s1, m + stride + 4 <= m_end);
       if (n + 2 >= steps) break;
       load(s1, m + 5 * stride);
       __builtin_amdgcn_sched_barrier(0);
-      compute(s2);
+      compute(s2, m + 2 * stride + 4 <= m_end);
       if (n + 3 >= steps) break;
       load(s2, m + 6 * stride);
       __builtin_amdgcn_sched_barrier(0);
-      compute(s3);
+      compute(s3, m + 3 * stride + 4 <= m_end);
       m += 4 * stride;
     }
   }
