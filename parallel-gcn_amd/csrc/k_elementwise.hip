@@ -255,7 +255,12 @@ __device__ __forceinline__ float block_sum(float v, float *smem) {
 #endif
 constexpr int XR = PGCN_XENT_ROWS;  // rows per cross-entropy block
 constexpr int XT = 4 * XR;    // threads: a lane quad per row; wave w holds rows 16 w .. 16 w + 15
-__host__ __device__ inline int xent_stride(int ld) { return ld + 1 > 49 ? (ld + 1) | 1 : 49; }
+// tile row stride: a multiple of 4 (rows 16-B aligned: the copies move float4s), S / 4 odd (a
+// wave's quad-per-row walks and the MFMA's 4-row stores hit 64 distinct banks) and >= 48
+__host__ __device__ inline int xent_stride(int ld) {
+  const int s = ld > 48 ? (ld + 3) & ~3 : 48;
+  return (s / 4) % 2 ? s : s + 4;
+}
 typedef float floatx4e __attribute__((ext_vector_type(4)));
 
 // a wave's LDS writes are visible to its own later LDS reads (one wave: in-order LDS pipe);
@@ -265,6 +270,14 @@ __device__ __forceinline__ void wave_lds_fence() {
   asm volatile("" ::: "memory");
 }
 
+// a / b rounded to nearest from rb = RN(1 / b) (Markstein: q within an ulp, the residual exact
+// by fma, one correction step): the IEEE quotient's bits for normal operands and results
+__device__ __forceinline__ float div_rn(float a, float b, float rb) {
+  const float q = a * rb;
+  const float r = fmaf(-q, b, a);
+  return fmaf(r, rb, q);
+}
+
 // FUSED: the logits are computed here from the output layer's input H [n][ldh] (kh <= 16
 // columns) and W [kh][ldw] with k_gemm_nn's v_mfma_f32_16x16x4_f32 sequence, so the same bits
 // as the separate Matmul -- and then go through the same tile as the loaded ones (the output
@@ -272,7 +285,7 @@ __device__ __forceinline__ void wave_lds_fence() {
 // pass: the logits are written once, not written and read back).  Training: also the output
 // layer's input grad dH = grad W^T and (dWp) this block's partial of W.grad = H^T grad.
 template <bool FUSED>
-__global__ __launch_bounds__(XT) void k_xent_fwd(float *__restrict__ logits, int ld,
+__device__ __forceinline__ void xent_tile(float *__restrict__ logits, int ld,
                                                   float *__restrict__ grad,
                                                   const int *__restrict__ truth, int n, int c,
                                                   int count, int training,
@@ -285,8 +298,8 @@ __global__ __launch_bounds__(XT) void k_xent_fwd(float *__restrict__ logits, int
   // by nobody after the loss; hpdga's in-place shift is kept where the variable is visible)
   extern __shared__ float smem[];
   __shared__ float red[XT / 64];
-  // tile row stride: odd (conflict-free row walks) and >= 48, so a wave's 16 rows can take its
-  // [3][4][64] weight-grad partial once the grad has left the tile (no extra LDS: 8 blocks per CU)
+  // tile row stride (xent_stride) >= 48, so a wave's 16 rows can take its [3][4][64]
+  // weight-grad partial once the grad has left the tile (no extra LDS)
   const int S = xent_stride(ld);
   const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63, gi = ln >> 4, ii = ln & 15;
   const long long row0 = (long long)blockIdx.x * XR, wrow0 = row0 + 16 * wv;
@@ -301,30 +314,25 @@ __global__ __launch_bounds__(XT) void k_xent_fwd(float *__restrict__ logits, int
   const unsigned magic = (1u << 20) / (unsigned)ld4 + 1u;
   const long long base = wrow0 * ld;
   auto to_lds = [&](const float *src) {
-    float4 v[8];  // ld <= 124: 16 * 31 float4 <= 64 * 8
+    floatx4e v[8];  // ld <= 124: 16 * 31 float4 <= 64 * 8
 #pragma unroll
     for (int u = 0; u < 8; u++) {
       const int q = ln + 64 * u;
-      if (q < tile4) v[u] = reinterpret_cast<const float4 *>(src + base)[q];
+      if (q < tile4) v[u] = reinterpret_cast<const floatx4e *>(src + base)[q];
     }
 #pragma unroll
     for (int u = 0; u < 8; u++) {
       const int q = ln + 64 * u;
       if (q < tile4) {
         const int r = (int)(__umul24((unsigned)q, magic) >> 20), j = 4 * (q - r * ld4);
-        float *d = L + r * S + j;
-        d[0] = v[u].x;
-        d[1] = v[u].y;
-        d[2] = v[u].z;
-        d[3] = v[u].w;
+        *reinterpret_cast<floatx4e *>(L + r * S + j) = v[u];
       }
     }
   };
   auto from_lds = [&](float *dst) {
     for (int q = ln; q < tile4; q += 64) {
       const int r = (int)(__umul24((unsigned)q, magic) >> 20), j = 4 * (q - r * ld4);
-      const float *d = L + r * S + j;
-      reinterpret_cast<float4 *>(dst + base)[q] = make_float4(d[0], d[1], d[2], d[3]);
+      reinterpret_cast<float4 *>(dst + base)[q] = *reinterpret_cast<const float4 *>(L + r * S + j);
     }
   };
   // FUSED: W [k][j] (16 x ld) past the tile
@@ -401,14 +409,27 @@ __global__ __launch_bounds__(XT) void k_xent_fwd(float *__restrict__ logits, int
     }
     mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 2, 64));
-    float s = 0.0f;
+    // shifted logits to the tile, the true class's read back and compared, then (registers)
+    // each exp computed once and kept for the grad in place of its logit
+    bool w = false;
+    float lt, s = 0.0f;
     if (regs) {
 #pragma unroll
       for (int k = 0; k < NV; k++) {
         if (q + 4 * k < c) {
           v[k] -= mx;
           l[q + 4 * k] = v[k];
-          s += expf(v[k]);
+        }
+      }
+      wave_lds_fence();  // the quad's shifted logits are all in the tile
+      lt = l[t];
+#pragma unroll
+      for (int k = 0; k < NV; k++) w |= q + 4 * k < c && v[k] > lt;
+#pragma unroll
+      for (int k = 0; k < NV; k++) {
+        if (q + 4 * k < c) {
+          v[k] = expf(v[k]);
+          s += v[k];
         }
       }
     } else {
@@ -417,18 +438,12 @@ __global__ __launch_bounds__(XT) void k_xent_fwd(float *__restrict__ logits, int
         l[j] = x;
         s += expf(x);
       }
+      wave_lds_fence();  // the quad's shifted logits are all in the tile
+      lt = l[t];
+      for (int j = q; j < c; j += 4) w |= l[j] > lt;
     }
     s += __shfl_xor(s, 1, 64);      // lanes 0, 1: s0 + s1; lanes 2, 3: s2 + s3
     se = s + __shfl_xor(s, 2, 64);  // (s0 + s1) + (s2 + s3) on every lane
-    wave_lds_fence();               // the quad's shifted logits are all in the tile
-    const float lt = l[t];
-    bool w = false;
-    if (regs) {
-#pragma unroll
-      for (int k = 0; k < NV; k++) w |= q + 4 * k < c && v[k] > lt;
-    } else {
-      for (int j = q; j < c; j += 4) w |= l[j] > lt;
-    }
     const int wq = (int)w | __shfl_xor((int)w, 1, 64);
     const int wall = wq | __shfl_xor(wq, 2, 64);
     if (q == 0) {
@@ -442,22 +457,26 @@ __global__ __launch_bounds__(XT) void k_xent_fwd(float *__restrict__ logits, int
     wave_lds_fence();  // the shifted logits have been read out
     if (rq < wrows) {
       if (t >= 0) {
+        // prob = e / se and prob / count as correctly rounded quotients from the correctly
+        // rounded reciprocals (div_rn: the IEEE division's bits, 3 VALU ops instead of ~10);
+        // prob - 1 in float: the double temporary of hpdga module.cpp:145 rounds the same
+        // exact difference once
+        const float rse = 1.0f / se, cnt = (float)count, rcnt = 1.0f / cnt;
         if (regs) {
-          // (reciprocal multiplies instead of the two divisions measured no faster, r03)
 #pragma unroll
           for (int k = 0; k < NV; k++) {
             const int j = q + 4 * k;
             if (j < c) {
-              float prob = expf(v[k]) / se;
-              if (j == t) prob = (float)((double)prob - 1.0);  // hpdga module.cpp:145
-              l[j] = prob / (float)count;
+              float prob = div_rn(v[k], se, rse);
+              if (j == t) prob -= 1.0f;
+              l[j] = div_rn(prob, cnt, rcnt);
             }
           }
         } else {
           for (int j = q; j < c; j += 4) {
-            float prob = expf(l[j]) / se;
-            if (j == t) prob = (float)((double)prob - 1.0);  // hpdga module.cpp:145 (double temp)
-            l[j] = prob / (float)count;
+            float prob = div_rn(expf(l[j]), se, rse);
+            if (j == t) prob -= 1.0f;
+            l[j] = div_rn(prob, cnt, rcnt);
           }
         }
         for (int j = c + q; j < ld; j += 4) l[j] = 0.0f;
@@ -534,6 +553,25 @@ __global__ __launch_bounds__(XT) void k_xent_fwd(float *__restrict__ logits, int
     partials[2 * blockIdx.x + 1] = ws;
   }
 }
+
+#define PGCN_XENT_ARGS                                                                          \
+  float *__restrict__ logits, int ld, float *__restrict__ grad, const int *__restrict__ truth,   \
+      int n, int c, int count, int training, float *__restrict__ partials, int write_back,       \
+      const float *__restrict__ H, int ldh, int kh, const float *__restrict__ W, int ldw,        \
+      float *__restrict__ dH, int lddh, float *__restrict__ dWp
+// the loss over given logits (61 VGPRs at 8 waves per SIMD would spill its copy registers)
+__global__ __launch_bounds__(XT) void k_xent_fwd(PGCN_XENT_ARGS) {
+  xent_tile<false>(logits, ld, grad, truth, n, c, count, training, partials, write_back, H, ldh,
+                   kh, W, ldw, dH, lddh, dWp);
+}
+// the fused output layer + loss at 8 waves per SIMD (<= 64 VGPRs, no spill; reddit training
+// call 45.0 -> 43.2 us, r03)
+__global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(8))) void k_out_xent(
+    PGCN_XENT_ARGS) {
+  xent_tile<true>(logits, ld, grad, truth, n, c, count, training, partials, write_back, H, ldh,
+                  kh, W, ldw, dH, lddh, dWp);
+}
+#undef PGCN_XENT_ARGS
 
 // sums[0] = sum loss partials, sums[1] = sum wrong, sums[2] = sum w^2 (fixed order)
 __global__ __launch_bounds__(1024) void k_reduce_scalars(const float *__restrict__ partials,
@@ -676,8 +714,8 @@ void launch_xent_fwd(float *logits, int ld, float *grad, const int *truth, int n
   if (n <= 0) return;
   PGCN_CHECK(ld <= 124 && c <= ld && ld % 4 == 0, PGCN_E_INVALID,
              "xent: classes must be <= 124 (ld a multiple of 4)");
-  const size_t lds = (size_t)XR * xent_stride(ld) * sizeof(float);  // <= 64*125*4 = 31 KB
-  PGCN_LAUNCH(k_xent_fwd<false>, dim3(xent_blocks(n)), dim3(XT), lds, s, logits, ld, grad,
+  const size_t lds = (size_t)XR * xent_stride(ld) * sizeof(float);  // <= 64*124*4 = 31 KB
+  PGCN_LAUNCH(k_xent_fwd, dim3(xent_blocks(n)), dim3(XT), lds, s, logits, ld, grad,
                      truth, n, c, count, training, partials, write_back, nullptr, 0, 0, nullptr, 0,
                      nullptr, 0, nullptr);
 }
@@ -693,7 +731,7 @@ void launch_out_xent(const float *H, int ldh, int kh, const float *W, int ldw, f
   // the tile, and (weight-grad partials) room for the waves' [3][4][64] partials in it
   // the tile (which also takes the waves' weight-grad partials) and W
   const size_t lds = ((size_t)XR * xent_stride(ld) + (size_t)16 * ld) * sizeof(float);
-  PGCN_LAUNCH(k_xent_fwd<true>, dim3(xent_blocks(n)), dim3(XT), lds, s, logits, ld, grad,
+  PGCN_LAUNCH(k_out_xent, dim3(xent_blocks(n)), dim3(XT), lds, s, logits, ld, grad,
                      truth, n, c, count, training, partials, 1, H, ldh, kh, W, ldw,
                      training ? dH : nullptr, lddh, training ? dWp : nullptr);
 }

@@ -491,7 +491,7 @@ def test_adam_bit_exact(pgcn):
     np.testing.assert_array_equal(dv.cpu().numpy(), v)
 
 
-@pytest.mark.parametrize("n,c", [(2708, 7), (50000, 41), (1000, 3)])
+@pytest.mark.parametrize("n,c", [(2708, 7), (50000, 41), (1000, 3), (3000, 60), (2000, 113)])
 def test_xent_vs_oracle(pgcn, n, c):
     lib = helpers.oracle()
     rng = np.random.default_rng(n)
