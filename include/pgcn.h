@@ -319,6 +319,9 @@ long long pgcn_debug_path_count(const char *name, int reset);
 /* n empty kernels back to back on `stream` (the per-launch floor the small graphs' epochs are
  * compared with: launches per epoch x the time of one empty launch). */
 int pgcn_debug_empty_launches(int n, void *stream);
+/* mine[i] = the loss kernel's exp of x[i] (x <= 0: the device expf sequence without its
+ * overflow select), lib[i] = the device library's expf(x[i]); device pointers */
+int pgcn_debug_exp_check(const float *x, long long n, float *mine, float *lib, void *stream);
 
 #ifdef __cplusplus
 }

@@ -132,6 +132,7 @@ _sig("pgcn_dataset_free", c_int, c_void_p)
 _sig("pgcn_debug_set", c_int, ctypes.c_char_p, c_int)
 _sig("pgcn_debug_path_count", c_ll, ctypes.c_char_p, c_int)
 _sig("pgcn_debug_empty_launches", c_int, c_int, c_void_p)
+_sig("pgcn_debug_exp_check", c_int, c_void_p, c_ll, c_void_p, c_void_p, c_void_p)
 _sig("pgcn_debug_lds_check", c_int, c_int, c_int, c_void_p, c_void_p, c_int, P(ctypes.c_double),
      P(c_ll))
 _sig("pgcn_debug_lds_counts", c_ll, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_ll,
@@ -507,5 +508,5 @@ EXPORTED = [
     "pgcn_dataset_view",
     "pgcn_dataset_free", "pgcn_partition_bounds", "pgcn_partition_subgraph", "pgcn_debug_set",
     "pgcn_debug_lds_check", "pgcn_debug_lds_counts", "pgcn_debug_path_count",
-    "pgcn_debug_empty_launches",
+    "pgcn_debug_empty_launches", "pgcn_debug_exp_check",
 ]

@@ -692,6 +692,14 @@ int pgcn_debug_empty_launches(int n, void *stream) {
   });
 }
 
+int pgcn_debug_exp_check(const float *x, long long n, float *mine, float *lib, void *stream) {
+  return guarded([&] {
+    PGCN_CHECK(n >= 0 && (n == 0 || (x && mine && lib)), PGCN_E_INVALID, "exp_check args");
+    launch_exp_check(x, n, mine, lib, as_stream(stream));
+    PGCN_HIP(hipGetLastError());
+  });
+}
+
 long long pgcn_debug_path_count(const char *name, int reset) {
   if (!name) {
     if (!reset) return PGCN_E_INVALID;

@@ -270,6 +270,31 @@ __device__ __forceinline__ void wave_lds_fence() {
   asm volatile("" ::: "memory");
 }
 
+// expf for x <= 0 (a max-shifted logit): the device library's expf sequence without its
+// overflow select, which cannot fire there -- the same operations in the same order, so the
+// same bits (tests: the loss kernel against the oracle; `test_exp_nonpos_matches_expf`)
+__device__ __forceinline__ float exp_nonpos(float x) {
+  const float l2e = 0x1.715476p+0f, l2e_lo = 0x1.4ae0bep-26f;
+  const float ph = x * l2e;
+  const float e = __builtin_rintf(ph);
+  const float pl = fmaf(x, l2e_lo, fmaf(x, l2e, -ph));
+  const float r = __builtin_ldexpf(__builtin_amdgcn_exp2f((ph - e) + pl), (int)e);
+  return x < -0x1.9d1da0p+6f ? 0.0f : r;
+}
+
+__global__ void k_exp_check(const float *__restrict__ x, long long n, float *__restrict__ mine,
+                            float *__restrict__ lib) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    mine[i] = exp_nonpos(x[i]);
+    lib[i] = expf(x[i]);
+  }
+}
+void launch_exp_check(const float *x, long long n, float *mine, float *lib, hipStream_t s) {
+  if (n <= 0) return;
+  PGCN_LAUNCH(k_exp_check, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, x, n, mine, lib);
+}
+
 // a / b rounded to nearest from rb = RN(1 / b) (Markstein: q within an ulp, the residual exact
 // by fma, one correction step): the IEEE quotient's bits for normal operands and results
 __device__ __forceinline__ float div_rn(float a, float b, float rb) {
@@ -284,6 +309,14 @@ __device__ __forceinline__ float div_rn(float a, float b, float rb) {
 // layer's Matmul forward + CrossEntropyLoss forward, hpdga module.cpp:13-38, :122-153, in one
 // pass: the logits are written once, not written and read back).  Training: also the output
 // layer's input grad dH = grad W^T and (dWp) this block's partial of W.grad = H^T grad.
+#ifdef PGCN_XENT_STAMPS
+// diagnostic build only (tools/xent_stamps.py): per wave, shader-clock stamps at the kernel's
+// phase boundaries and the wall clock at its start and end
+__device__ unsigned long long g_xent_stamps[16384 * 12];
+#define XST(k) (st[k] = __builtin_amdgcn_s_memtime())
+#else
+#define XST(k) ((void)0)
+#endif
 template <bool FUSED>
 __device__ __forceinline__ void xent_tile(float *__restrict__ logits, int ld,
                                                   float *__restrict__ grad,
@@ -297,7 +330,12 @@ __device__ __forceinline__ void xent_tile(float *__restrict__ logits, int ld,
   // write_back 0: the shifted logits stay in LDS (the compact output layer's logits are read
   // by nobody after the loss; hpdga's in-place shift is kept where the variable is visible)
   extern __shared__ float smem[];
-  __shared__ float red[XT / 64];
+  __shared__ float red[2 * (XT / 64)];
+#ifdef PGCN_XENT_STAMPS
+  unsigned long long st[12] = {};
+  st[10] = __builtin_amdgcn_s_memrealtime();
+#endif
+  XST(0);
   // tile row stride (xent_stride) >= 48, so a wave's 16 rows can take its [3][4][64]
   // weight-grad partial once the grad has left the tile (no extra LDS)
   const int S = xent_stride(ld);
@@ -369,6 +407,7 @@ __device__ __forceinline__ void xent_tile(float *__restrict__ logits, int ld,
     for (int k = wv; k < 16; k += XT / 64)
       for (int j = ln; j < ld; j += 64) wt[k * ld + j] = (k < kh && j < c) ? W[(long long)k * ldw + j] : 0.0f;
     __syncthreads();  // W staged (the only barrier before the block's final sums)
+    XST(1);
     // logits of the wave's 16 rows on MFMA, as k_gemm_nn<3> computes them; lane holds
     // logits[4 gi + r][16 tt + ii] -> the tile
     for (int tt = 0; 16 * tt < ld; tt++) {
@@ -387,6 +426,7 @@ __device__ __forceinline__ void xent_tile(float *__restrict__ logits, int ld,
     to_lds(logits);
   }
   wave_lds_fence();
+  XST(2);
   float loss = 0.0f, wrong = 0.0f, se = 0.0f;
   float *l = L + rq * S;
   // up to 48 classes (reddit: 41) the lane's classes live in registers: every LDS read of the
@@ -428,7 +468,7 @@ __device__ __forceinline__ void xent_tile(float *__restrict__ logits, int ld,
 #pragma unroll
       for (int k = 0; k < NV; k++) {
         if (q + 4 * k < c) {
-          v[k] = expf(v[k]);
+          v[k] = exp_nonpos(v[k]);
           s += v[k];
         }
       }
@@ -436,7 +476,7 @@ __device__ __forceinline__ void xent_tile(float *__restrict__ logits, int ld,
       for (int j = q; j < c; j += 4) {
         const float x = l[j] - mx;
         l[j] = x;
-        s += expf(x);
+        s += exp_nonpos(x);
       }
       wave_lds_fence();  // the quad's shifted logits are all in the tile
       lt = l[t];
@@ -452,7 +492,9 @@ __device__ __forceinline__ void xent_tile(float *__restrict__ logits, int ld,
     }
   }
   wave_lds_fence();
+  XST(3);
   if (write_back || FUSED) from_lds(logits);
+  XST(4);
   if (training) {
     wave_lds_fence();  // the shifted logits have been read out
     if (rq < wrows) {
@@ -474,7 +516,7 @@ __device__ __forceinline__ void xent_tile(float *__restrict__ logits, int ld,
           }
         } else {
           for (int j = q; j < c; j += 4) {
-            float prob = div_rn(expf(l[j]), se, rse);
+            float prob = div_rn(exp_nonpos(l[j]), se, rse);
             if (j == t) prob -= 1.0f;
             l[j] = div_rn(prob, cnt, rcnt);
           }
@@ -485,6 +527,7 @@ __device__ __forceinline__ void xent_tile(float *__restrict__ logits, int ld,
       }
     }
     wave_lds_fence();  // the wave's grad rows are complete
+    XST(5);
     if (FUSED && dH) {
       // the output layer's input grad dH = grad W^T (Matmul::backward's a.grad) on MFMA in
       // k_xstream_nn's sequence (N = 16 outputs, K = c classes: step s, MFMA t, lane group g:
@@ -507,6 +550,7 @@ __device__ __forceinline__ void xent_tile(float *__restrict__ logits, int ld,
         }
       }
     }
+    XST(6);
     // the output layer's weight grad, this block's share: partial [kh][48] = H^T grad over
     // the block's rows (wave partials over their 16 rows on MFMA, added in wave order),
     // reduced over the blocks in block order by launch_tn_reduce_blocks
@@ -524,6 +568,7 @@ __device__ __forceinline__ void xent_tile(float *__restrict__ logits, int ld,
         }
       }
       from_lds(grad);
+      XST(7);
       wave_lds_fence();  // the grad has been read out: the wave's tile takes its partial
 #pragma unroll
       for (int tt = 0; tt < 3; tt++)
@@ -546,12 +591,37 @@ __device__ __forceinline__ void xent_tile(float *__restrict__ logits, int ld,
       from_lds(grad);
     }
   }
-  const float ls = block_sum<XT>(loss, red);
-  const float ws = block_sum<XT>(wrong, red);
+  XST(8);
+  // (loss, wrong) block sums in one pass: the wave sums (fixed xor tree), then thread 0 adds
+  // the waves' in wave order
+  loss = wave_sum(loss);
+  wrong = wave_sum(wrong);
+  if (ln == 0) {
+    red[2 * wv] = loss;
+    red[2 * wv + 1] = wrong;
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
+    float ls = red[0], ws = red[1];
+#pragma unroll
+    for (int w2 = 1; w2 < XT / 64; w2++) {
+      ls += red[2 * w2];
+      ws += red[2 * w2 + 1];
+    }
     partials[2 * blockIdx.x] = ls;
     partials[2 * blockIdx.x + 1] = ws;
   }
+  XST(9);
+#ifdef PGCN_XENT_STAMPS
+  st[11] = __builtin_amdgcn_s_memrealtime();
+  const long long wslot = (long long)blockIdx.x * (XT / 64) + wv;
+  if (ln < 12 && wslot < 16384) {
+    unsigned long long x = st[0];
+#pragma unroll
+    for (int k = 1; k < 12; k++) x = ln == k ? st[k] : x;
+    g_xent_stamps[wslot * 12 + ln] = x;
+  }
+#endif
 }
 
 #define PGCN_XENT_ARGS                                                                          \
@@ -783,4 +853,11 @@ void launch_adam(float *w, const float *g, float *m, float *v, long long n, floa
                      beta1, beta2, eps, wd, decay, step_table, ctr, table_cap);
 }
 
+#ifdef PGCN_XENT_STAMPS
+extern "C" int pgcn_debug_xent_stamps(unsigned long long *host, long long n) {
+  if (n > 16384LL * 12) n = 16384LL * 12;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_xent_stamps), (size_t)n * 8, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 }  // namespace pgcn

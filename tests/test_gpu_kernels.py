@@ -491,6 +491,27 @@ def test_adam_bit_exact(pgcn):
     np.testing.assert_array_equal(dv.cpu().numpy(), v)
 
 
+def test_exp_nonpos_matches_expf(pgcn):
+    """The loss kernel's exp of max-shifted logits (x <= 0) is the device expf's sequence
+    without the overflow select: bit-identical to expf over every x <= 0 it can see -- a dense
+    sweep of [-110, 0] (through the underflow cut at -103.97), denormal and tiny inputs, -0."""
+    rng = np.random.default_rng(5)
+    x = np.concatenate([
+        -np.linspace(0.0, 110.0, 2_000_001, dtype=np.float32),
+        -rng.exponential(5.0, 1_000_000).astype(np.float32),
+        -np.abs(rng.standard_normal(100_000).astype(np.float32)) * 1e-30,
+        np.array([-0.0, -1e-45, -103.972076, -103.97208, -103.97209, -87.33655, -88.7],
+                 np.float32)])
+    dx = torch.from_numpy(x).to(DEV)
+    mine = torch.empty_like(dx)
+    lib = torch.empty_like(dx)
+    pgcn.check(pgcn.lib.pgcn_debug_exp_check(vp(dx), x.size, vp(mine), vp(lib), stream()),
+               "exp_check")
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(mine.cpu().numpy().view(np.uint32),
+                                  lib.cpu().numpy().view(np.uint32))
+
+
 @pytest.mark.parametrize("n,c", [(2708, 7), (50000, 41), (1000, 3), (3000, 60), (2000, 113)])
 def test_xent_vs_oracle(pgcn, n, c):
     lib = helpers.oracle()
