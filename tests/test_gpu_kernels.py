@@ -336,7 +336,8 @@ def nibble_mask_ref(mask, base, M, K):
     return out
 
 
-@pytest.mark.parametrize("M,N,K,base", [(3001, 16, 602, 0), (1000, 16, 602, 41), (77, 12, 100, 63),
+@pytest.mark.parametrize("M,N,K,base", [(3001, 16, 602, 0), (40009, 16, 602, 9),
+                                        (1000, 16, 602, 41), (77, 12, 100, 63),
                                         (129, 16, 640, 5), (20, 3, 7, 0)])
 def test_gemm_xstream(pgcn, M, N, K, base):
     """X-stream NN/TN kernels with nibble-layout dropout bits vs fp64 references (the loader /
