@@ -26,9 +26,13 @@ namespace pgcn {
 // 64-bit xor/shift ops, so the kernel needs the waves to hide it.
 // ------------------------------------------------------------------------------------------
 // 64 draws from xorshift128+ state (s0, s1) -> 64 keep bits (bit j: draw j >= threshold)
+#ifndef PGCN_DROP_SHIFTIN
+#define PGCN_DROP_SHIFTIN 1
+#endif
 struct Xs64 {
   uint64_t s0, s1;
   uint32_t lo = 0, hi = 0;  // mask bits 0-31 / 32-63 (constant shifts: the loop is unrolled)
+  uint32_t thr2 = 0;          // threshold << 1 (PGCN_DROP_SHIFTIN)
   __device__ __forceinline__ void step(int j, int threshold) {
     uint64_t t = s0;
     const uint64_t u = s1;
@@ -37,12 +41,25 @@ struct Xs64 {
     t ^= t >> 17;
     t ^= u ^ (u >> 26);
     s1 = t;
+#if PGCN_DROP_SHIFTIN
+    // keep = ((t + u) & 0x7fffffff) >= threshold, compared as ((t + u) << 1) >= (threshold << 1)
+    // (both < 2^32: the same order), shifted in at bit 0 (draw j ends at bit 31 - j of its
+    // half; reversed once per half at the end)
+    const uint32_t r2 = ((uint32_t)t + (uint32_t)u) << 1;
+    uint32_t &w = j < 32 ? lo : hi;
+    // w = 2 w + (thr2 <= r2): the compare's carry straight into the add (2 VALU ops)
+    asm("v_cmp_le_u32_e32 vcc, %1, %2\n\tv_addc_co_u32_e32 %0, vcc, %0, %0, vcc"
+        : "+v"(w)
+        : "s"(thr2), "v"(r2)
+        : "vcc");
+#else
     const int r = (int)((uint32_t)(t + u) & 0x7fffffffu);
     const uint32_t bit = r >= threshold ? 1u : 0u;
     if (j < 32)
       lo |= bit << j;
     else
       hi |= bit << (j - 32);
+#endif
   }
 };
 
@@ -91,11 +108,18 @@ __global__ __launch_bounds__(256) void k_dropout_mask(uint64_t *__restrict__ sta
     const uint64_t a0 = states[2 * c], a1 = states[2 * c + 1];
     const uint64_t b0 = states[2 * cb], b1 = states[2 * cb + 1];
     Xs64 x{a0, a1}, y{b0, b1};
+    x.thr2 = y.thr2 = (uint32_t)threshold << 1;
 #pragma unroll
     for (int j = 0; j < 64; j++) {
       x.step(j, threshold);
       y.step(j, threshold);
     }
+#if PGCN_DROP_SHIFTIN
+    x.lo = __builtin_bitreverse32(x.lo);
+    x.hi = __builtin_bitreverse32(x.hi);
+    y.lo = __builtin_bitreverse32(y.lo);
+    y.hi = __builtin_bitreverse32(y.hi);
+#endif
     emit(c, a0, a1, ((uint64_t)x.hi << 32) | x.lo);
     if (two) emit(c2, b0, b1, ((uint64_t)y.hi << 32) | y.lo);
   }
@@ -317,13 +341,16 @@ __device__ unsigned long long g_xent_stamps[16384 * 12];
 #else
 #define XST(k) ((void)0)
 #endif
-template <bool FUSED>
-__device__ __forceinline__ void xent_tile(float *__restrict__ logits, int ld,
+// CC / LDC / KH > 0: the class count, the logits row stride and the hidden width as
+// compile-time constants (the launcher's specialisations: the bounds tests of the class
+// loops, the MFMA operand selects and the tile arithmetic fold away); 0: runtime values
+template <bool FUSED, int CC = 0, int LDC = 0, int KH = 0>
+__device__ __forceinline__ void xent_tile(float *__restrict__ logits, int ld_rt,
                                                   float *__restrict__ grad,
-                                                  const int *__restrict__ truth, int n, int c,
+                                                  const int *__restrict__ truth, int n, int c_rt,
                                                   int count, int training,
                                                   float *__restrict__ partials, int write_back,
-                                                  const float *__restrict__ H, int ldh, int kh,
+                                                  const float *__restrict__ H, int ldh, int kh_rt,
                                                   const float *__restrict__ W, int ldw,
                                                   float *__restrict__ dH, int lddh,
                                                   float *__restrict__ dWp) {
@@ -335,6 +362,7 @@ __device__ __forceinline__ void xent_tile(float *__restrict__ logits, int ld,
   unsigned long long st[12] = {};
   st[10] = __builtin_amdgcn_s_memrealtime();
 #endif
+  const int c = CC > 0 ? CC : c_rt, ld = LDC > 0 ? LDC : ld_rt, kh = KH > 0 ? KH : kh_rt;
   XST(0);
   // tile row stride (xent_stride) >= 48, so a wave's 16 rows can take its [3][4][64]
   // weight-grad partial once the grad has left the tile (no extra LDS)
@@ -636,10 +664,11 @@ __global__ __launch_bounds__(XT) void k_xent_fwd(PGCN_XENT_ARGS) {
 }
 // the fused output layer + loss at 8 waves per SIMD (<= 64 VGPRs, no spill; reddit training
 // call 45.0 -> 43.2 us, r03)
+template <int CC, int LDC, int KH>
 __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(8))) void k_out_xent(
     PGCN_XENT_ARGS) {
-  xent_tile<true>(logits, ld, grad, truth, n, c, count, training, partials, write_back, H, ldh,
-                  kh, W, ldw, dH, lddh, dWp);
+  xent_tile<true, CC, LDC, KH>(logits, ld, grad, truth, n, c, count, training, partials,
+                               write_back, H, ldh, kh, W, ldw, dH, lddh, dWp);
 }
 #undef PGCN_XENT_ARGS
 
@@ -654,13 +683,29 @@ __global__ __launch_bounds__(1024) void k_reduce_scalars(const float *__restrict
                                                          int ring_cap) {
   __shared__ float red[16];
   float l = 0.0f, wr = 0.0f, q = 0.0f;
-  for (int b = threadIdx.x; b < n_blocks; b += blockDim.x) {
-    l += partials[2 * b];
-    wr += partials[2 * b + 1];
+  // a thread's elements b = tid + 1024 u in u order, 8 loads in flight before their adds (r03
+  // late: one dependent load per add made this single-block launch 8 us)
+  constexpr int U = 8;
+  for (int b0 = threadIdx.x; b0 < n_blocks; b0 += U * 1024) {
+    float2 v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (b0 + u * 1024 < n_blocks) v[u] = reinterpret_cast<const float2 *>(partials)[b0 + u * 1024];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (b0 + u * 1024 < n_blocks) {
+        l += v[u].x;
+        wr += v[u].y;
+      }
   }
-  for (long long i = threadIdx.x; i < n_w; i += blockDim.x) {
-    const float x = w[i];
-    q += x * x;
+  for (long long i0 = threadIdx.x; i0 < n_w; i0 += U * 1024) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (i0 + u * 1024 < n_w) v[u] = w[i0 + u * 1024];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (i0 + u * 1024 < n_w) q += v[u] * v[u];
   }
   l = block_sum<1024>(l, red);
   wr = block_sum<1024>(wr, red);
@@ -801,9 +846,15 @@ void launch_out_xent(const float *H, int ldh, int kh, const float *W, int ldw, f
   // the tile, and (weight-grad partials) room for the waves' [3][4][64] partials in it
   // the tile (which also takes the waves' weight-grad partials) and W
   const size_t lds = ((size_t)XR * xent_stride(ld) + (size_t)16 * ld) * sizeof(float);
-  PGCN_LAUNCH(k_out_xent, dim3(xent_blocks(n)), dim3(XT), lds, s, logits, ld, grad,
-                     truth, n, c, count, training, partials, 1, H, ldh, kh, W, ldw,
-                     training ? dH : nullptr, lddh, training ? dWp : nullptr);
+#define OUT_XENT(...)                                                                          \
+  PGCN_LAUNCH((k_out_xent<__VA_ARGS__>), dim3(xent_blocks(n)), dim3(XT), lds, s, logits, ld, grad, \
+              truth, n, c, count, training, partials, 1, H, ldh, kh, W, ldw,                     \
+              training ? dH : nullptr, lddh, training ? dWp : nullptr)
+  if (c == 41 && ld == 44 && kh == 16)  // reddit (41 classes, hidden 16)
+    OUT_XENT(41, 44, 16);
+  else
+    OUT_XENT(0, 0, 0);
+#undef OUT_XENT
 }
 
 void launch_reduce_scalars(const float *partials, int n_blocks, const float *w, long long n_w,

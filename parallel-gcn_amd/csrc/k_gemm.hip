@@ -761,7 +761,11 @@ static TnPlan blocks_plan(int n_blocks, int ldp) {
   TnPlan p{};
   p.n_slabs = n_blocks;
   p.ldp = ldp;
-  p.spg = 16;
+  // ~sqrt(n) partials per group in each pass (r03 late: 16 per group left the second pass
+  // 228 serial loads per element for the loss kernel's 3,641 block partials, 8-11 us)
+  int spg = 16;
+  while ((long long)spg * spg < n_blocks) spg += 16;
+  p.spg = spg;
   p.n_groups = (n_blocks + p.spg - 1) / p.spg;
   return p;
 }

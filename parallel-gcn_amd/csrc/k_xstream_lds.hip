@@ -37,6 +37,10 @@
 #include "kernels.hpp"
 #include "lds_dma.hpp"
 
+#ifndef PGCN_XS_CHAINS
+#define PGCN_XS_CHAINS 1
+#endif
+
 namespace pgcn {
 
 // "xstream_ring": 1 = these kernels for the X-stream products where they apply (default),
@@ -227,6 +231,11 @@ __global__ __launch_bounds__(64 * (XL_NN_LOADERS + XL_NN_CONSUMERS), 1) void k_x
       xa[s] = 16 * s < K ? *reinterpret_cast<const float4 *>(a + 64 * s) : make_float4(0.f, 0.f, 0.f, 0.f);
     xl_release(freed, slot, t, lane);
     floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f}, acc2 = floatx4{0.f, 0.f, 0.f, 0.f};
+#if PGCN_XS_CHAINS == 2
+    // experiment: the single product's steps on two accumulators (even / odd steps), added
+    // at the end (MFMA dependent latency 40 vs 32 cycles issue)
+    floatx4 acch = floatx4{0.f, 0.f, 0.f, 0.f};
+#endif
 #pragma unroll
     for (int s = 0; s < NS; s++) {
       if (16 * s >= K) break;  // steps wholly past K add nothing
@@ -240,12 +249,19 @@ __global__ __launch_bounds__(64 * (XL_NN_LOADERS + XL_NN_CONSUMERS), 1) void k_x
       }
       if constexpr (MASKED)
         xl_apply4<FOLD>(x, (uint32_t)(mw[s & 3] >> (4 * (s >> 2))) & 0xfu, a_scale);
+#if PGCN_XS_CHAINS == 2
+      floatx4 &am = DUAL ? acc2 : ((s & 1) ? acch : acc);
+#else
       floatx4 &am = DUAL ? acc2 : acc;
+#endif
       am = __builtin_amdgcn_mfma_f32_16x16x4f32(x.x, bb.x, am, 0, 0, 0);
       am = __builtin_amdgcn_mfma_f32_16x16x4f32(x.y, bb.y, am, 0, 0, 0);
       am = __builtin_amdgcn_mfma_f32_16x16x4f32(x.z, bb.z, am, 0, 0, 0);
       am = __builtin_amdgcn_mfma_f32_16x16x4f32(x.w, bb.w, am, 0, 0, 0);
     }
+#if PGCN_XS_CHAINS == 2
+    if constexpr (!DUAL) acc = acc + acch;
+#endif
     if constexpr (MASKED && FOLD) {  // the masked product's scale, on its sums
       floatx4 &am = DUAL ? acc2 : acc;
       am = am * a_scale;
