@@ -156,18 +156,21 @@ __global__ __launch_bounds__(256) void k_mask_nibbles(const uint64_t *__restrict
   const int r = threadIdx.x >> 4, j = threadIdx.x & 15;
   if (r >= rows) return;
   const long long p0 = mask_base + (m0 + r) * mask_ld + 4 * j - (w_first << 6);  // local bit
-  uint64_t word = 0;
+  // nibble c sits at bit p0 + 64 c: word w0 + c, the same shift sh for every c (r03 late:
+  // one LDS word per nibble, the next nibble's low word reused as this one's high word)
+  const int w0 = (int)(p0 >> 6), sh = (int)(p0 & 63);
+  const int nc = (K - 4 * j + 63) >> 6;  // nibbles with kb = 64 c + 4 j < K
+  uint64_t word = 0, lo = bits[w0];
 #pragma unroll
   for (int c = 0; c < 16; c++) {
-    const int kb = 64 * c + 4 * j;
-    if (kb < K) {
-      const long long p = p0 + 64 * c;
-      const int w = (int)(p >> 6), sh = (int)(p & 63);
-      uint64_t v = bits[w] >> sh;
-      if (sh > 60) v |= bits[w + 1] << (64 - sh);
-      uint64_t nib = v & 0xfu;
+    if (c < nc) {
+      const uint64_t hi = bits[w0 + c + 1];
+      uint64_t nib = (lo >> sh) & 0xfu;
+      if (sh > 60) nib = (nib | (hi << (64 - sh))) & 0xfu;
+      const int kb = 64 * c + 4 * j;
       if (kb + 4 > K) nib &= (1ull << (K - kb)) - 1;  // keep bits of k >= K are 0
       word |= nib << (4 * c);
+      lo = hi;
     }
   }
   out[(m0 + r) * 16 + j] = word;
