@@ -256,21 +256,24 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
   };
   for (int t = 0; t < T; t++) {
     lds_wait_ge(loaded, (unsigned)(t + RING_W));  // slices t .. t+2 and visit t's counts
-    const uint4 *c4 = reinterpret_cast<const uint4 *>(lb + RING_CNT_OFF + (t % RING_NCB) * RING_CNT_B +
-                                                      wave * 32);
-    const uint4 cw0 = c4[0], cw1 = c4[1];
-    const unsigned cw[8] = {
-        (unsigned)__builtin_amdgcn_readfirstlane(cw0.x), (unsigned)__builtin_amdgcn_readfirstlane(cw0.y),
-        (unsigned)__builtin_amdgcn_readfirstlane(cw0.z), (unsigned)__builtin_amdgcn_readfirstlane(cw0.w),
-        (unsigned)__builtin_amdgcn_readfirstlane(cw1.x), (unsigned)__builtin_amdgcn_readfirstlane(cw1.y),
-        (unsigned)__builtin_amdgcn_readfirstlane(cw1.z), (unsigned)__builtin_amdgcn_readfirstlane(cw1.w)};
-    // per (rowset, visit): 0 blocks (half the pairs on reddit), 1 (92 % of the blocks) or more
+    // lane l reads rowset (l % 16)'s step count; two ballots give the rowsets with blocks this
+    // visit and those with more than one: per rowset a scalar bit test (the sign bit of the
+    // mask shifted), the count itself only for the few longer runs (r03 late: per visit 8
+    // readfirstlanes and 16 extract-compare-branch sequences were ~40 of the wave's SALU
+    // instructions; 254.8 -> 250.4 us per call, 536-538 -> 541-542 epochs/s).  Per (rowset,
+    // visit): 0 blocks (half the pairs on reddit), 1 (92 % of the blocks) or more
+    const unsigned short *c16 = reinterpret_cast<const unsigned short *>(
+        lb + RING_CNT_OFF + (t % RING_NCB) * RING_CNT_B + wave * 32);
+    const unsigned cl = c16[lane & 15];
+    const unsigned nz = (unsigned)__ballot(cl != 0u), big = (unsigned)__ballot(cl > 4u);
 #pragma unroll
     for (int j = 0; j < LDS_SLOTS; j++) {
-      const unsigned n = (cw[j >> 1] >> (16 * (j & 1))) & 0xffffu;  // steps of rowset j (x 4)
-      if (n != 0) {
+      if (__builtin_amdgcn_readfirstlane((int)(nz << (31 - j))) < 0) {  // bit j: the sign bit
         block(acc[j]);
-        for (unsigned k = 4; k < n; k += 4) block(acc[j]);
+        if ((big >> j) & 1u) {
+          const unsigned n = (unsigned)__builtin_amdgcn_readlane((int)cl, j);
+          for (unsigned k = 4; k < n; k += 4) block(acc[j]);
+        }
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every read of slice t returned
