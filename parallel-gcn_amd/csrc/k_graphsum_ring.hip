@@ -277,11 +277,23 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every read of slice t returned
-    unsigned rank = 0;
-    if (lane == 0)
-      rank = __hip_atomic_fetch_add(done + t % RING_K, 1u, __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_WORKGROUP);
-    asm volatile("" ::: "memory");
+    // the visit's done count += 1 by lane 0 alone (exec = lane 0 inside the asm; hipcc's
+    // atomic optimizer made the C++ form a 25-instruction ballot / mbcnt / nested-exec
+    // sequence; r03 late: 253.5 -> 247.5 us per call); the returned value is read from lane 0
+    unsigned rank;
+    {
+      unsigned long long saved;
+      const unsigned daddr = lds_base + (unsigned)(RING_FLAG_OFF + 4 * (1 + t % RING_K));
+      asm volatile(
+          "s_mov_b64 %1, exec\n\t"
+          "s_mov_b64 exec, 1\n\t"
+          "ds_add_rtn_u32 %0, %2, %3\n\t"
+          "s_waitcnt lgkmcnt(0)\n\t"
+          "s_mov_b64 exec, %1"
+          : "=&v"(rank), "=&s"(saved)
+          : "v"(daddr), "v"(1u)
+          : "memory");
+    }
     // The arbiter favours older waves, so the youngest waves of a workgroup fall behind and
     // the visits' hand-offs make everyone wait for them (r02 stamps: 395 vs 576 cycles per
     // block from the oldest to the youngest wave).  The last third of the waves to finish a
