@@ -296,7 +296,8 @@ int pgcn_debug_rank_graph(int n, const int *indptr, const int *indices, int worl
  *   "lds_blocks" 0 (by shape) or 1..32, "parse_threads" (0: up to 16), "wide_prescale" 0/1
  *   (a multi-pass GraphSum's tables prescaled by one launch, default 1);
  * diagnostics: "split_rows" 0/1 (stale logits outside the split), "gemm_variant" 0/1 (the
- * general GEMM kernels only).  Returns PGCN_E_INVALID on an unknown key or value. */
+ * general GEMM kernels only).  Returns PGCN_E_INVALID on an unknown key or on a value outside
+ * the key's range (nothing is changed then). */
 int pgcn_debug_set(const char *key, int value);
 /* Host-only check of the d = 16 LDS ring schedule (window must be 5) of a CSR pattern: builds
  * it, walks it as k_graphsum_ring consumes it over a seeded input and returns the max relative
@@ -313,7 +314,9 @@ long long pgcn_debug_lds_counts(int n_rows, int n_cols, const int *indptr, const
  * GraphSum), "gs_gather" (gather GraphSum), "out_xent" (output layer fused into the loss),
  * "gemm_nn" / "gemm_tn" (general MFMA GEMMs), "launches" (every kernel launch of the library).
  * A non-null name returns its count (then zeroes it
- * when reset != 0); a null name with reset != 0 zeroes every counter.  Status < 0 on an unknown
+ * when reset bit 0 is set); a null name with reset bit 0 zeroes every counter.  Bit 1 of reset
+ * selects the counters of the calling host thread instead of the process-wide ones (each rank
+ * of an in-process loopback group runs on a thread of its own).  Status < 0 on an unknown
  * name. */
 long long pgcn_debug_path_count(const char *name, int reset);
 /* n empty kernels back to back on `stream` (the per-launch floor the small graphs' epochs are
@@ -322,6 +325,9 @@ int pgcn_debug_empty_launches(int n, void *stream);
 /* mine[i] = the loss kernel's exp of x[i] (x <= 0: the device expf sequence without its
  * overflow select), lib[i] = the device library's expf(x[i]); device pointers */
 int pgcn_debug_exp_check(const float *x, long long n, float *mine, float *lib, void *stream);
+/* q[i] = the loss kernel's quotient a[i] / b[i] (div_rn: from the reciprocal of b[i], the IEEE
+ * division below 2^-125); device pointers */
+int pgcn_debug_div_check(const float *a, const float *b, long long n, float *q, void *stream);
 
 #ifdef __cplusplus
 }

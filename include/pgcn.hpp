@@ -152,7 +152,8 @@ class DevSparseIndex {
  private:
   SparseIndex host_;
   std::shared_ptr<void> dev_;
-  mutable std::vector<std::pair<std::vector<real>, std::shared_ptr<pgcn::DevGraph>>> graphs_;
+  // device graphs by value array; weak: a graph lives as long as a GraphSum holding it
+  mutable std::vector<std::pair<std::vector<real>, std::weak_ptr<pgcn::DevGraph>>> graphs_;
 };
 
 // include/module.cuh:21-30

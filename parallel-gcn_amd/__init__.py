@@ -164,21 +164,23 @@ KERNEL_PATHS = ("xs_nn_ring", "xs_tn_ring", "xs_nn", "xs_tn", "gs_ring", "gs_gat
                 "gemm_nn", "gemm_tn", "gemm_nn_w", "gemm_tn_w", "launches")
 
 
-def path_counts(reset=False):
-    """Launch counts of the kernel families since the last reset (pgcn_debug_path_count)."""
+def path_counts(reset=False, thread=False):
+    """Launch counts of the kernel families since the last reset (pgcn_debug_path_count);
+    thread: the calling host thread's launches only (a loopback rank's own)."""
     out = {}
+    t = 2 if thread else 0
     for k in KERNEL_PATHS:
-        n = lib.pgcn_debug_path_count(k.encode(), 0)
+        n = lib.pgcn_debug_path_count(k.encode(), t)
         if n < 0:
             raise PgcnError(int(n), "path_count " + k)
         out[k] = int(n)
     if reset:
-        lib.pgcn_debug_path_count(None, 1)
+        lib.pgcn_debug_path_count(None, 1 | t)
     return out
 
 
-def reset_path_counts():
-    check(int(lib.pgcn_debug_path_count(None, 1)), "path_count reset")
+def reset_path_counts(thread=False):
+    check(int(lib.pgcn_debug_path_count(None, 3 if thread else 1)), "path_count reset")
 
 
 # --------------------------------------------------------------------------- data
@@ -508,5 +510,5 @@ EXPORTED = [
     "pgcn_dataset_view",
     "pgcn_dataset_free", "pgcn_partition_bounds", "pgcn_partition_subgraph", "pgcn_debug_set",
     "pgcn_debug_lds_check", "pgcn_debug_lds_counts", "pgcn_debug_path_count",
-    "pgcn_debug_empty_launches", "pgcn_debug_exp_check",
+    "pgcn_debug_empty_launches", "pgcn_debug_exp_check", "pgcn_debug_div_check",
 ]

@@ -35,11 +35,15 @@ extern int g_parse_threads;         // host/data.cpp: pieces of the parallel tex
 
 namespace {
 std::atomic<long long> g_path_hits[KP_COUNT];
+thread_local long long t_path_hits[KP_COUNT];  // the launching host thread's (loopback ranks)
 const char *const kPathNames[KP_COUNT] = {"xs_nn_ring", "xs_tn_ring", "xs_nn",   "xs_tn",
                                           "gs_ring",    "gs_gather",  "out_xent", "gemm_nn",
                                           "gemm_tn",    "gemm_nn_w",  "gemm_tn_w", "launches"};
 }  // namespace
-void note_path(KernelPath p) { g_path_hits[p].fetch_add(1, std::memory_order_relaxed); }
+void note_path(KernelPath p) {
+  g_path_hits[p].fetch_add(1, std::memory_order_relaxed);
+  t_path_hits[p]++;
+}
 }  // namespace pgcn
 
 struct pgcn_graph {
@@ -603,30 +607,54 @@ int pgcn_dataset_free(pgcn_dataset *ds) {
 // ---------------------------------------------------------------- diagnostics
 int pgcn_debug_set(const char *key, int value) {
   if (!key) return PGCN_E_INVALID;
-  if (!std::strcmp(key, "train_ahead")) pgcn::g_train_ahead = value;
-  else if (!std::strcmp(key, "split_rows")) pgcn::g_split_rows = value;
-  else if (!std::strcmp(key, "split_cols")) pgcn::g_split_cols = value;
-  else if (!std::strcmp(key, "eval_ax")) pgcn::g_eval_ax = value;
-  else if (!std::strcmp(key, "epoch_graph")) pgcn::g_epoch_graph = value;
-  else if (!std::strcmp(key, "fuse_epilogue")) {
-    if (value < 0 || value > 7) return PGCN_E_INVALID;
+  // every key's value range is checked: an out-of-range value is refused, never reinterpreted
+  auto in = [&](int lo, int hi) { return value >= lo && value <= hi; };
+  if (!std::strcmp(key, "train_ahead")) {
+    if (!in(0, 1)) return PGCN_E_INVALID;
+    pgcn::g_train_ahead = value;
+  } else if (!std::strcmp(key, "split_rows")) {
+    if (!in(0, 1)) return PGCN_E_INVALID;
+    pgcn::g_split_rows = value;
+  } else if (!std::strcmp(key, "split_cols")) {
+    if (!in(0, 1)) return PGCN_E_INVALID;
+    pgcn::g_split_cols = value;
+  } else if (!std::strcmp(key, "eval_ax")) {
+    if (!in(0, 1)) return PGCN_E_INVALID;
+    pgcn::g_eval_ax = value;
+  } else if (!std::strcmp(key, "epoch_graph")) {
+    if (!in(0, 1)) return PGCN_E_INVALID;
+    pgcn::g_epoch_graph = value;
+  } else if (!std::strcmp(key, "fuse_epilogue")) {
+    if (!in(0, 7)) return PGCN_E_INVALID;
     pgcn::g_fuse_epilogue = value;
   } else if (!std::strcmp(key, "fuse_output")) {
-    if (value < 0 || value > 3) return PGCN_E_INVALID;
+    if (!in(0, 3)) return PGCN_E_INVALID;
     pgcn::g_fuse_output = value;
-  } else if (!std::strcmp(key, "mm_side")) pgcn::g_mm_side = value;
-  else if (!std::strcmp(key, "xstream_ring")) pgcn::g_xstream_ring = value;
-  else if (!std::strcmp(key, "gemm_variant")) pgcn::g_gemm_variant = value;
-  else if (!std::strcmp(key, "lds_min_kb"))  // < 0: the default
+  } else if (!std::strcmp(key, "mm_side")) {
+    if (!in(0, 2)) return PGCN_E_INVALID;
+    pgcn::g_mm_side = value;
+  } else if (!std::strcmp(key, "xstream_ring")) {
+    if (!in(0, 1)) return PGCN_E_INVALID;
+    pgcn::g_xstream_ring = value;
+  } else if (!std::strcmp(key, "gemm_variant")) {
+    if (!in(0, 1)) return PGCN_E_INVALID;
+    pgcn::g_gemm_variant = value;
+  } else if (!std::strcmp(key, "lds_min_kb")) {  // < 0: the default
     pgcn::g_lds_min_bytes = value < 0 ? DevGraph::kLdsMinBytes : 1024LL * value;
-  else if (!std::strcmp(key, "lds_blocks")) {
+  } else if (!std::strcmp(key, "lds_blocks")) {
     if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8 && value != 16 &&
         value != 32)
       return PGCN_E_INVALID;
     pgcn::g_lds_blocks = value;
-  } else if (!std::strcmp(key, "parse_threads")) pgcn::g_parse_threads = value;
-  else if (!std::strcmp(key, "wide_prescale")) pgcn::g_wide_prescale = value;
-  else return PGCN_E_INVALID;
+  } else if (!std::strcmp(key, "parse_threads")) {
+    if (!in(0, 4096)) return PGCN_E_INVALID;
+    pgcn::g_parse_threads = value;
+  } else if (!std::strcmp(key, "wide_prescale")) {
+    if (!in(0, 1)) return PGCN_E_INVALID;
+    pgcn::g_wide_prescale = value;
+  } else {
+    return PGCN_E_INVALID;
+  }
   return PGCN_OK;
 }
 
@@ -700,15 +728,34 @@ int pgcn_debug_exp_check(const float *x, long long n, float *mine, float *lib, v
   });
 }
 
+int pgcn_debug_div_check(const float *a, const float *b, long long n, float *q, void *stream) {
+  return guarded([&] {
+    PGCN_CHECK(n >= 0 && (n == 0 || (a && b && q)), PGCN_E_INVALID, "div_check args");
+    launch_div_check(a, b, n, q, as_stream(stream));
+    PGCN_HIP(hipGetLastError());
+  });
+}
+
 long long pgcn_debug_path_count(const char *name, int reset) {
+  const bool thread = (reset & 2) != 0, zero = (reset & 1) != 0;
+  if (reset & ~3) return PGCN_E_INVALID;
   if (!name) {
-    if (!reset) return PGCN_E_INVALID;
-    for (auto &h : pgcn::g_path_hits) h.store(0);
+    if (!zero) return PGCN_E_INVALID;
+    for (int p = 0; p < KP_COUNT; p++) {
+      if (thread) pgcn::t_path_hits[p] = 0;
+      else pgcn::g_path_hits[p].store(0);
+    }
     return 0;
   }
   for (int p = 0; p < KP_COUNT; p++)
-    if (!std::strcmp(name, pgcn::kPathNames[p]))
-      return reset ? pgcn::g_path_hits[p].exchange(0) : pgcn::g_path_hits[p].load();
+    if (!std::strcmp(name, pgcn::kPathNames[p])) {
+      if (thread) {
+        const long long n = pgcn::t_path_hits[p];
+        if (zero) pgcn::t_path_hits[p] = 0;
+        return n;
+      }
+      return zero ? pgcn::g_path_hits[p].exchange(0) : pgcn::g_path_hits[p].load();
+    }
   return PGCN_E_INVALID;
 }
 

@@ -7,6 +7,7 @@
 // workspace and the engine's ModuleContext.
 #include "../../../include/pgcn.hpp"
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -230,13 +231,17 @@ DevSparseIndex::DevSparseIndex(const SparseIndex &sparse_index) : host_(sparse_i
 }
 
 // One device graph per distinct value array (compared bit for bit, so NaNs compare equal to
-// themselves), all kept for as long as the index or a GraphSum built on them lives: two
-// GraphSums on one index with different values each keep their own graph.
+// themselves), shared by the GraphSums built on it and freed with the last of them: the index
+// keeps only weak references (entries whose graph is gone are dropped on lookup), so a
+// program rebuilding GraphSums with changing values does not accumulate device graphs.
 std::shared_ptr<DevGraph> DevSparseIndex::graph(const std::vector<real> &values) const {
+  graphs_.erase(std::remove_if(graphs_.begin(), graphs_.end(),
+                               [](const auto &gv) { return gv.second.expired(); }),
+                graphs_.end());
   for (const auto &gv : graphs_)
     if (gv.first.size() == values.size() &&
         std::memcmp(gv.first.data(), values.data(), values.size() * sizeof(real)) == 0)
-      return gv.second;
+      if (auto g = gv.second.lock()) return g;
   const int n = (int)indptr_size - 1;
   PGCN_CHECK(n > 0 && values.size() == host_.indices.size(), PGCN_E_INVALID,
              "GraphSum: graph values must match the pattern");

@@ -314,17 +314,33 @@ __global__ void k_exp_check(const float *__restrict__ x, long long n, float *__r
     lib[i] = expf(x[i]);
   }
 }
+
+// a / b rounded to nearest from rb = RN(1 / b) (Markstein: q within an ulp, the residual exact
+// by fma, one correction step): the IEEE quotient's bits for normal operands and results.
+// The loss kernel divides a in [0, 1] by b >= 1: q below 2^-125 (subnormal results, or the
+// residual no longer exact) takes the IEEE division itself; tests/test_gpu_kernels.py
+// test_div_rn_matches_ieee checks the bits over dense a (subnormals included) and b in [1, 128]
+__device__ __forceinline__ float div_rn(float a, float b, float rb) {
+  const float q = a * rb;
+  if (__builtin_expect(fabsf(q) < 0x1p-125f, 0)) return a / b;
+  const float r = fmaf(-q, b, a);
+  return fmaf(r, rb, q);
+}
+
+__global__ void k_div_check(const float *__restrict__ a, const float *__restrict__ b, long long n,
+                            float *__restrict__ q) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) q[i] = div_rn(a[i], b[i], 1.0f / b[i]);
+}
+
 void launch_exp_check(const float *x, long long n, float *mine, float *lib, hipStream_t s) {
   if (n <= 0) return;
   PGCN_LAUNCH(k_exp_check, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, x, n, mine, lib);
 }
 
-// a / b rounded to nearest from rb = RN(1 / b) (Markstein: q within an ulp, the residual exact
-// by fma, one correction step): the IEEE quotient's bits for normal operands and results
-__device__ __forceinline__ float div_rn(float a, float b, float rb) {
-  const float q = a * rb;
-  const float r = fmaf(-q, b, a);
-  return fmaf(r, rb, q);
+void launch_div_check(const float *a, const float *b, long long n, float *q, hipStream_t s) {
+  if (n <= 0) return;
+  PGCN_LAUNCH(k_div_check, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, a, b, n, q);
 }
 
 // FUSED: the logits are computed here from the output layer's input H [n][ldh] (kh <= 16

@@ -27,6 +27,7 @@ void note_path(KernelPath p);
 void launch_empty(int n, hipStream_t s);
 // mine[i] = the loss kernel's exp of x[i] <= 0, lib[i] = expf(x[i]) (pgcn_debug_exp_check)
 void launch_exp_check(const float *x, long long n, float *mine, float *lib, hipStream_t s);
+void launch_div_check(const float *a, const float *b, long long n, float *q, hipStream_t s);
 
 // GraphSum work schedule for one row width (VEC float4 per row); device arrays.
 struct GraphSchedule {

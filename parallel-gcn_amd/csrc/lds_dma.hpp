@@ -60,6 +60,14 @@ typedef unsigned u2v __attribute__((ext_vector_type(2)));
 // LDS reads issued from inline asm (LDS byte addresses): hipcc does not count them, so its
 // automatic waits do not drain them; every use goes behind an lgkm_wait<N> naming the
 // registers it waits for (the asm operands order the uses after it).
+// Invariants the compiler does not guarantee (checked on the built code object by
+// tests/test_cpu_host.py test_ring_kernel_lds_reads_wait_before_use):
+//  * the destination registers stay where the read lands them until the tied lgkm_wait: hipcc
+//    takes the asm outputs as ready at once, so a v_mov of one of them placed before the wait
+//    would copy stale data -- no instruction may name them before the next lgkmcnt(0);
+//  * an LDS atomic issued under a forced exec mask (k_graphsum_ring's hand-off count) sits in
+//    wave-uniform control flow with lane 0 active, and restores exec inside the same asm
+//    statement, so the hazard recognizer never sees a live exec write across statements.
 __device__ __forceinline__ f4v ds_rd128(unsigned addr) {
   f4v r;
   asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(addr));

@@ -35,3 +35,16 @@ def pgcn():
 def loaded(datasets, pgcn):
     root, names = datasets
     return {k: pgcn.Dataset.load(root, v) for k, v in names.items()}
+
+
+@pytest.fixture(scope="session")
+def rw_ds(pgcn):
+    """reddit's feature width (F = 602) and 41 classes on a 100 k-node power-law graph."""
+    g = helpers.RW_GRAPH
+    return pgcn.Dataset.synthetic(g["n"], g["f"], g["c"], g["edges"], g["seed"])
+
+
+@pytest.fixture(scope="session")
+def rw_oracle(rw_ds):
+    """3 oracle epochs + eval(3) on rw_ds (shared by the single-GPU and edge-cut tests)."""
+    return helpers.oracle_run(rw_ds, 3)

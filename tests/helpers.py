@@ -142,6 +142,22 @@ class OracleGCN:
             self.h = None
 
 
+def oracle_run(ds, epochs, **kw):
+    """The oracle's epochs x (train_epoch + eval(2)), then eval(3), with the near-tied rows of
+    every pass (the accuracy tolerance), the logits after eval(3) and the weights."""
+    ref = OracleGCN(ds_dict(ds), **kw)
+    c = ds.output_dim
+    runs = [ref.epoch_with_ties(ds.label, ds.split, c) for _ in range(epochs)]
+    test, tt = ref.eval_with_ties(3, ds.label, ds.split, c)
+    n = ref.lib.or_gcn_num_vars(ref.h)
+    return dict(lines=[r[0] for r in runs], ties=[r[1] for r in runs], test=test,
+                test_ties={1: tt, 2: tt}, logits=ref.logits(), w1=ref.var(2), w2=ref.var(n - 2))
+
+
+# reddit's feature width and class count (the X-stream ring kernels), ~3.1 M adjacency slots
+RW_GRAPH = dict(n=100000, f=602, c=41, edges=1500000, seed=41)
+
+
 def ds_dict(ds):
     """pgcn Dataset -> plain dict of arrays for the oracle."""
     return {"n": ds.num_nodes, "f": ds.input_dim, "c": ds.output_dim,

@@ -409,26 +409,47 @@ def test_cpp_api_header_and_driver_without_device(datasets):
     assert r.returncode != 0 and "no HIP device" in r.stderr, (r.returncode, r.stderr[-500:])
 
 
+LLVM_BIN = "/opt/rocm/lib/llvm/bin"
+
+
+def _kernel_objects():
+    """The built gfx950 kernel objects (skips when the build or the llvm tools are absent: a
+    CPU-only or sanitizer build checks nothing here)."""
+    import glob
+    objs = sorted(glob.glob(os.path.join(helpers.REPO, "parallel-gcn_amd", "build", "k_*.o")))
+    if not objs:
+        pytest.skip("libpgcn.so kernel objects not built")
+    for tool in ("llvm-objdump", "llvm-readelf"):
+        if not os.access(os.path.join(LLVM_BIN, tool), os.X_OK):
+            pytest.skip(f"{tool} not available")
+    return objs
+
+
+def _device_code(obj, tmp_path):
+    """The gfx950 code object inside a host object (llvm-objdump --offloading)."""
+    import glob
+    import shutil
+    import subprocess
+    local = tmp_path / os.path.basename(obj)
+    shutil.copy(obj, local)
+    subprocess.run([f"{LLVM_BIN}/llvm-objdump", "--offloading", str(local)], check=True,
+                   capture_output=True, cwd=tmp_path)
+    dev = glob.glob(str(local) + ".*gfx950")
+    assert dev, obj
+    return dev[0]
+
+
 def test_no_kernel_spills_to_scratch(tmp_path):
     """Every HIP kernel of libpgcn.so runs without scratch (private segment 0): a spill is a
     silent slowdown (r03: the X-stream TN kernel lost 40 % to 348 B of spills after an
     unrelated edit).  Reads the gfx950 code objects' metadata of the built objects."""
-    import glob
     import re
-    import shutil
     import subprocess
-    llvm = "/opt/rocm/lib/llvm/bin"
-    objs = sorted(glob.glob(os.path.join(helpers.REPO, "parallel-gcn_amd", "build", "k_*.o")))
-    assert objs, "libpgcn.so not built"
+    objs = _kernel_objects()
     seen = 0
     for o in objs:
-        local = tmp_path / os.path.basename(o)
-        shutil.copy(o, local)
-        subprocess.run([f"{llvm}/llvm-objdump", "--offloading", str(local)], check=True,
-                       capture_output=True, cwd=tmp_path)
-        dev = glob.glob(str(local) + ".*gfx950")
-        assert dev, o
-        notes = subprocess.run([f"{llvm}/llvm-readelf", "--notes", dev[0]], check=True,
+        dev = _device_code(o, tmp_path)
+        notes = subprocess.run([f"{LLVM_BIN}/llvm-readelf", "--notes", dev], check=True,
                                capture_output=True, text=True).stdout
         names = re.findall(r"^\s+\.name:\s+(\S+)", notes, re.M)
         scratch = [int(x) for x in re.findall(r"\.private_segment_fixed_size:\s+(\d+)", notes)]
@@ -437,3 +458,62 @@ def test_no_kernel_spills_to_scratch(tmp_path):
         assert not bad, bad
         seen += len(names)
     assert seen >= 20
+
+
+def test_ring_kernel_lds_reads_wait_before_use(tmp_path):
+    """k_graphsum_ring issues its LDS reads from inline asm (lds_dma.hpp ds_rd128 / ds_rd64_into):
+    hipcc believes their results ready at once, so correctness rests on no instruction reading
+    or moving a destination register before the s_waitcnt lgkmcnt(0) that the asm lgkm_wait
+    places.  Walks the gfx950 disassembly in order: from each ds_read_b128 / ds_read_b64 to the
+    next lgkmcnt(0) wait, no instruction may name its destination registers (a compiler upgrade
+    that inserted a v_mov there would otherwise show up only as wrong sums)."""
+    import re
+    import subprocess
+    obj = [o for o in _kernel_objects() if o.endswith("k_graphsum_ring.o")]
+    assert obj, "k_graphsum_ring.o not built"
+    dev = _device_code(obj[0], tmp_path)
+    asm = subprocess.run([f"{LLVM_BIN}/llvm-objdump", "-d", "--no-show-raw-insn", dev],
+                         check=True, capture_output=True, text=True).stdout.splitlines()
+    start = [i for i, l in enumerate(asm) if re.match(r"^[0-9a-f]+ <_ZN4pgcn15k_graphsum_ring", l)]
+    assert start, "k_graphsum_ring not in the code object"
+
+    def regs(ops):
+        out = set()
+        for m in re.finditer(r"\bv\[(\d+):(\d+)\]|\bv(\d+)\b", ops):
+            if m.group(3) is not None:
+                out.add(int(m.group(3)))
+            else:
+                out.update(range(int(m.group(1)), int(m.group(2)) + 1))
+        return out
+    pending, bad, reads = set(), [], 0
+    for line in asm[start[0] + 1:]:
+        if re.match(r"^[0-9a-f]+ <", line):
+            break
+        t = line.strip()
+        if not t or t.startswith(";"):
+            continue
+        op, _, ops = t.partition(" ")
+        ops = ops.split("//")[0]
+        if op == "s_waitcnt" and "lgkmcnt(0)" in ops:
+            pending.clear()
+        elif op in ("ds_read_b128", "ds_read_b64"):
+            pending |= regs(ops.split(",")[0])
+            reads += 1
+        elif pending & regs(ops):
+            bad.append(t)
+    assert reads >= 16, reads
+    assert not bad, bad[:10]
+
+
+def test_debug_set_refuses_out_of_range_values(pgcn):
+    """pgcn_debug_set range-checks every key (pgcn.h): an out-of-range value returns
+    PGCN_E_INVALID and leaves the knob unchanged (host only, no device)."""
+    lib = pgcn.lib
+    for key, bad in (("train_ahead", 2), ("split_rows", -1), ("split_cols", 5), ("eval_ax", 2),
+                     ("epoch_graph", 3), ("fuse_epilogue", 8), ("fuse_output", 4),
+                     ("mm_side", 3), ("xstream_ring", 2), ("gemm_variant", 7),
+                     ("lds_blocks", 3), ("parse_threads", -2), ("wide_prescale", 2)):
+        assert lib.pgcn_debug_set(key.encode(), bad) < 0, key
+    assert lib.pgcn_debug_set(b"no_such_knob", 0) < 0
+    for key, val in helpers.ENGINE_DEFAULTS.items():
+        assert lib.pgcn_debug_set(key.encode(), val) == 0, key

@@ -513,6 +513,27 @@ def test_exp_nonpos_matches_expf(pgcn):
                                   lib.cpu().numpy().view(np.uint32))
 
 
+def test_div_rn_matches_ieee(pgcn):
+    """The loss kernel's quotients (prob = e / sum and prob / count, div_rn) against IEEE fp32
+    division (numpy, round to nearest, subnormals kept): dense a in (0, 1] -- every 97th bit
+    pattern, so subnormal, tiny and normal numerators alike -- over b in [1, 128] (random
+    reals and every integer count)."""
+    rng = np.random.default_rng(5)
+    bits = np.arange(1, 0x3f800001, 97, dtype=np.uint32)
+    a = bits.view(np.float32)
+    b = np.where(rng.random(a.size) < 0.5, rng.uniform(1.0, 128.0, a.size),
+                 rng.integers(1, 129, a.size)).astype(np.float32)
+    want = (a / b).astype(np.float32)
+    da, db = torch.from_numpy(a).to(DEV), torch.from_numpy(b).to(DEV)
+    q = torch.empty_like(da)
+    pgcn.check(pgcn.lib.pgcn_debug_div_check(vp(da), vp(db), a.size, vp(q), stream()),
+               "div_check")
+    torch.cuda.synchronize()
+    got = q.cpu().numpy()
+    bad = np.flatnonzero(got.view(np.uint32) != want.view(np.uint32))
+    assert bad.size == 0, (bad.size, a[bad[:5]], b[bad[:5]], got[bad[:5]], want[bad[:5]])
+
+
 @pytest.mark.parametrize("n,c", [(2708, 7), (50000, 41), (1000, 3), (3000, 60), (2000, 113)])
 def test_xent_vs_oracle(pgcn, n, c):
     lib = helpers.oracle()

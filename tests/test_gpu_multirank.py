@@ -134,3 +134,81 @@ def test_loopback_deep_wide_matches_oracle(pgcn, deep_ds, deep_oracle, world):
         helpers.assert_line_close(ours, want, cnt, what=f"world {world} epoch {e + 1}", ties=tie)
     t = res[0]["test"]
     helpers.assert_line_close(t + t, test * 2, {1: cnt[3], 2: cnt[3]}, what="test", ties=test_ties)
+
+
+# ------------------------------------------------------------------ reddit's feature width
+def _run_world_rw(pgcn, ds, world, epochs, params=None):
+    """_run_world plus, per rank, the logits of its rows after eval(3) and the launch counts
+    of its own host thread (the rank's kernels only)."""
+    group = pgcn.LoopbackGroup(world)
+    p = params or pgcn.make_params(ds)
+
+    def rank_fn(r):
+        pgcn.reset_path_counts(thread=True)
+        g = pgcn.GCN(p, ds, device=0, rank=r, loopback=group)
+        info = {k: g.query(k) for k in ("world", "rank", "comm", "graphsum_lds", "reassociated")}
+        lines = [g.train_epoch() + g.eval(2) for _ in range(epochs)]
+        test = g.eval(3)
+        paths = pgcn.path_counts(thread=True)
+        rng = g.node_range()
+        logits = g.get_var(g.num_vars() - 1)
+        w1 = g.get_var(2)
+        g.close()
+        return dict(info=info, lines=lines, test=test, range=rng, w1=w1, logits=logits,
+                    paths=paths)
+    return pgcn.run_ranks(world, rank_fn)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_loopback_reddit_width_matches_oracle(pgcn, rw_ds, rw_oracle, world):
+    """The edge-cut engine at reddit's feature width (F = 602, 41 classes, 100 k nodes, 3.1 M
+    slots) at worlds 2 and 8: every rank's first layer runs the loader / MFMA-wave X-stream
+    kernels on its own row range (k_xs_nn_ring for the masked training product and eval's
+    (Â X) W1, k_xs_tn_ring for its W1.grad partial), proven by each rank thread's launch
+    counters; 3 epochs + eval(3), every rank's rows of the logits and the weights against the
+    oracle (hpdga gcn.cpp:179-212, module.cpp:49-72)."""
+    res = _run_world_rw(pgcn, rw_ds, world, 3)
+    _check_ranks(res, world, rw_ds.num_nodes)
+    cnt = helpers.split_counts(rw_ds)
+    want = rw_oracle
+    for e, (ours, ref, tie) in enumerate(zip(res[0]["lines"], want["lines"], want["ties"])):
+        helpers.assert_line_close(ours, ref, cnt, what=f"world {world} epoch {e + 1}", ties=tie)
+    t = res[0]["test"]
+    helpers.assert_line_close(t + t, want["test"] * 2, {1: cnt[3], 2: cnt[3]}, what="test",
+                              ties=want["test_ties"])
+    c = rw_ds.output_dim
+    ref_logits = want["logits"].reshape(-1, c)
+    for r, x in enumerate(res):
+        lo, hi = x["range"]
+        np.testing.assert_allclose(x["logits"].reshape(-1, c), ref_logits[lo:hi], rtol=1e-4,
+                                   atol=1e-4, err_msg=f"rank {r} logits")
+        p = x["paths"]
+        # per epoch: training drop(X) W1 + eval (Â X) W1 on NN, W1.grad on TN; + eval(3)
+        assert p["xs_nn_ring"] >= 7 and p["xs_tn_ring"] == 3, (r, p)
+        assert p["xs_nn"] == 0 and p["xs_tn"] == 0, (r, p)
+    w1, scale = res[0]["w1"], np.abs(want["w1"]).max()
+    err = np.abs(w1 - want["w1"])
+    assert np.quantile(err, 0.99) <= 1e-3 * scale and np.median(err) <= 1e-4 * scale
+
+
+def test_loopback_deep_reddit_width_matches_oracle(pgcn):
+    """4 layers x hidden 128 at reddit's feature width (F = 602) on the edge-cut engine at
+    world 2: each rank's first layer (masked product, eval (Â X) W1, W1.grad partial) and
+    hidden layers on the wide MFMA kernels over its own rows, 128-wide GraphSums reduce-
+    scattered, weight grads all-reduced -- against the oracle's L-layer restatement
+    (src/gcn.cu:85-112, hpdga gcn.cpp:179-212)."""
+    ds = pgcn.Dataset.synthetic(24000, 602, 41, 240000, 43)
+    dims, drops = (128, 128, 128), (0.5, 0.5, 0.5, 0.5)
+    p = pgcn.make_params(ds, hidden_dims=dims, dropouts=drops)
+    res = _run_world_rw(pgcn, ds, 2, 2, params=p)
+    _check_ranks(res, 2, ds.num_nodes)
+    ref = helpers.OracleGCN(helpers.ds_dict(ds), hidden_dims=dims, dropouts=drops)
+    cnt = helpers.split_counts(ds)
+    for e in range(2):
+        want, ties = ref.epoch_with_ties(ds.label, ds.split, ds.output_dim)
+        helpers.assert_line_close(res[0]["lines"][e], want, cnt, what=f"epoch {e + 1}", ties=ties)
+    for r, x in enumerate(res):
+        q = x["paths"]
+        # per epoch on every rank: the wide NN for X W1 (training) and (Â X) W1 (eval) and the
+        # hidden layers' products; the wide TN for the first layer's and hidden weight grads
+        assert q["gemm_nn_w"] >= 2 * 8 and q["gemm_tn_w"] >= 2 * 3, (r, q)

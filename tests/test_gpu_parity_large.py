@@ -26,8 +26,6 @@ pytestmark = pytest.mark.gpu
 
 # N > 62,500 (LDS path), hubs from the Chung-Lu power law, ~3.1 M adjacency slots
 LDS_GRAPH = dict(n=120000, f=64, c=41, edges=1500000, seed=21)
-# reddit's feature width and class count (the X-stream ring kernels), ~3.1 M slots
-RW_GRAPH = dict(n=100000, f=602, c=41, edges=1500000, seed=41)
 EPOCHS = 5
 
 
@@ -40,21 +38,9 @@ def lds_ds(pgcn):
     return _synthetic(pgcn, LDS_GRAPH)
 
 
-def _oracle_run(ds, epochs, **kw):
-    """epochs x (train_epoch + eval(2)), then eval(3), with the near-tied rows of every pass,
-    the logits after eval(3) and the weights."""
-    ref = helpers.OracleGCN(helpers.ds_dict(ds), **kw)
-    c = ds.output_dim
-    runs = [ref.epoch_with_ties(ds.label, ds.split, c) for _ in range(epochs)]
-    test, tt = ref.eval_with_ties(3, ds.label, ds.split, c)
-    n = ref.lib.or_gcn_num_vars(ref.h)
-    return dict(lines=[r[0] for r in runs], ties=[r[1] for r in runs], test=test,
-                test_ties={1: tt, 2: tt}, logits=ref.logits(), w1=ref.var(2), w2=ref.var(n - 2))
-
-
 @pytest.fixture(scope="module")
 def oracle_lines(lds_ds):
-    return _oracle_run(lds_ds, EPOCHS)
+    return helpers.oracle_run(lds_ds, EPOCHS)
 
 
 def _check_lines(ds, lines, test, want, what):
@@ -126,16 +112,7 @@ def test_deep_wide_lds_graph_matches_oracle(pgcn):
 
 
 # ------------------------------------------------------------------ reddit's feature width
-@pytest.fixture(scope="module")
-def rw_ds(pgcn):
-    return _synthetic(pgcn, RW_GRAPH)
-
-
-@pytest.fixture(scope="module")
-def rw_oracle(rw_ds):
-    return _oracle_run(rw_ds, 3)
-
-
+# (rw_ds / rw_oracle: tests/conftest.py, shared with the edge-cut tests)
 def test_reddit_width_epoch_matches_oracle(pgcn, rw_ds, rw_oracle):
     """The measured configuration at F = 602 (reddit's width), 41 classes, 100 k nodes, 3.1 M
     slots, every engine default: 3 epochs + eval(3) + every row of the logits + the weights

@@ -1,7 +1,11 @@
 """HBM traffic per GraphSum call from rocprofv3 PMC passes (diagnostic tool, run on the host
 after scripts/profile.sh's fetch/write passes).
 
-usage: python3 tools/traffic.py gpurun_out/<dir> [epoch_calls]
+usage: python3 tools/traffic.py gpurun_out/<dir> [epoch_calls] [--write <round>]
+
+With --write, profiles/traffic_graphsum.json is rewritten with the bytes, the round tag and
+the source stamp of the kernel the passes measured (tools/stamp.py): bench.py reports the
+bytes as roofline.traffic only while that stamp matches the sources it runs.
 
 A GraphSum call is its prescale (k_ring_prescale, or k_gs_prescale on the window-1 schedule;
 absent when a fused epilogue staged the table) + k_graphsum_ring / k_graphsum_lds +
@@ -16,8 +20,17 @@ import json
 import os
 import sys
 
-root = sys.argv[1]
-n_calls = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from stamp import REPO, graphsum_stamp  # noqa: E402
+
+argv = list(sys.argv[1:])
+write_round = None
+if "--write" in argv:
+    i = argv.index("--write")
+    write_round = argv[i + 1]
+    del argv[i:i + 2]
+root = argv[0]
+n_calls = int(argv[1]) if len(argv) > 1 else 20
 
 
 def per_dispatch(counter):
@@ -45,4 +58,25 @@ for counter in ("FETCH_SIZE", "WRITE_SIZE"):
     out[counter + "_KB_per_call"] = sum(calls) / max(len(calls), 1)
     out[counter + "_calls"] = len(calls)
 out["hbm_bytes_per_call"] = (2 * out["FETCH_SIZE_KB_per_call"] + out["WRITE_SIZE_KB_per_call"]) * 1024
+out["source_stamp"] = graphsum_stamp()
 print(json.dumps(out))
+if write_round:
+    path = os.path.join(REPO, "profiles", "traffic_graphsum.json")
+    doc = {
+        "reddit-114M": out["hbm_bytes_per_call"],
+        "source_stamp": out["source_stamp"],
+        "round": write_round,
+        "_doc": "HBM-side bytes per GraphSum call (ring prescale when not staged by a fused "
+                "epilogue + k_graphsum_ring + k_gs_lds_combine, the launches the bench's HIP "
+                "events bracket), averaged over the last %d GraphSum calls of bench.py "
+                "--profile-only on reddit-114M with the engine defaults (engine-build A X calls "
+                "excluded). Separate rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE; "
+                "scripts/profile.sh), corrected as MI355X_MICROARCH.md prescribes: FETCH_SIZE x2 "
+                "+ WRITE_SIZE. source_stamp = tools/stamp.py over the kernel's sources; bench.py "
+                "reports null when it no longer matches." % n_calls,
+        "raw_per_call_KB": {"FETCH_SIZE": out["FETCH_SIZE_KB_per_call"],
+                            "WRITE_SIZE": out["WRITE_SIZE_KB_per_call"]},
+        "calls": out["FETCH_SIZE_calls"],
+    }
+    with open(path, "w") as f:
+        json.dump(doc, f, indent=1)
