@@ -120,6 +120,15 @@ int pgcn_rng_jump_table(uint64_t period, void *host_table /* 16*256*16 bytes */)
 int pgcn_dropout_mask(uint64_t *chunk_states, long long n_chunks, long long n_elems,
                       long long elem0, float p, uint64_t *mask, const void *dev_jump_table,
                       void *stream);
+/* The same draw for a dense [rows][F] input (element m*F + k of the variable at mask bit
+ * mask_base + m*F + k, mask_base < 64; n_chunks must be (mask_base + rows*F + 63) / 64) written
+ * to `mask` AND to the nibble layout of pgcn_mask_nibbles (mask_nib [rows][16]) by one launch:
+ * the bits of pgcn_dropout_mask followed by pgcn_mask_nibbles(mask, mask_base, F, rows, F).
+ * PGCN_E_INVALID when F > 1024 or no row cut from mask_base is chunk-aligned. */
+int pgcn_dropout_mask_nib(uint64_t *chunk_states, long long n_chunks, long long n_elems,
+                          long long elem0, float p, uint64_t *mask, const void *dev_jump_table,
+                          long long mask_base, int F, int rows, uint64_t *mask_nib,
+                          void *stream);
 /* x[i] *= bit(i) ? scale : 0 for i in [0,n) (also the backward on grads). */
 int pgcn_dropout_apply(float *x, long long n, const uint64_t *mask, float scale, void *stream);
 
@@ -294,7 +303,9 @@ int pgcn_debug_rank_graph(int n, const int *indptr, const int *indices, int worl
  *   "fuse_epilogue" bits 1 tails | 2 prestaged tables | 4 X-stream epilogue (default 7),
  *   "fuse_output" 0..3 (default 2), "xstream_ring" 0/1, "lds_min_kb" (< 0: default),
  *   "lds_blocks" 0 (by shape) or 1..32, "parse_threads" (0: up to 16), "wide_prescale" 0/1
- *   (a multi-pass GraphSum's tables prescaled by one launch, default 1);
+ *   (a multi-pass GraphSum's tables prescaled by one launch, default 1), "rs_chunks" 1..4
+ *   (edge-cut GraphSum row chunks at world > 1, default 2), "mask_nib" 0/1 (dense X's input
+ *   dropout drawn into the flat bitmap and the GEMMs' nibble layout by one launch, default 1);
  * diagnostics: "split_rows" 0/1 (stale logits outside the split), "gemm_variant" 0/1 (the
  * general GEMM kernels only).  Returns PGCN_E_INVALID on an unknown key or on a value outside
  * the key's range (nothing is changed then). */

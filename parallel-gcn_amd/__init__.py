@@ -496,7 +496,7 @@ EXPORTED = [
     "pgcn_gemm_tn", "pgcn_mask_nibbles", "pgcn_gemm_xstream", "pgcn_gemm_xstream_dual",
     "pgcn_gemm_tn_xstream",
     "pgcn_spmm_csr", "pgcn_spmm_csc_bwd", "pgcn_csr_transpose",
-    "pgcn_rng_jump_table", "pgcn_dropout_mask", "pgcn_dropout_apply", "pgcn_relu_fwd",
+    "pgcn_rng_jump_table", "pgcn_dropout_mask", "pgcn_dropout_mask_nib", "pgcn_dropout_apply", "pgcn_relu_fwd",
     "pgcn_relu_bwd", "pgcn_xent_blocks", "pgcn_xent_fwd", "pgcn_finalize", "pgcn_adam",
     "pgcn_adam_step_size", "pgcn_params_default", "pgcn_gcn_create", "pgcn_comm_unique_id",
     "pgcn_gcn_create_dist", "pgcn_loopback_create", "pgcn_loopback_destroy",

@@ -302,6 +302,19 @@ int pgcn_dropout_mask(uint64_t *chunk_states, long long n_chunks, long long n_el
   });
 }
 
+int pgcn_dropout_mask_nib(uint64_t *chunk_states, long long n_chunks, long long n_elems,
+                          long long elem0, float p, uint64_t *mask, const void *dev_jump_table,
+                          long long mask_base, int F, int rows, uint64_t *mask_nib,
+                          void *stream) {
+  return guarded([&] {
+    PGCN_CHECK(mask_nib && dropout_mask_nib_ok(F, mask_base), PGCN_E_INVALID,
+               "dropout_mask_nib: F in [1, 1024] with chunk-aligned row cuts from mask_base");
+    launch_dropout_mask_nib(chunk_states, n_chunks, elem0, n_elems, p, mask, dev_jump_table,
+                            mask_base, F, rows, mask_nib, as_stream(stream));
+    PGCN_HIP(hipGetLastError());
+  });
+}
+
 int pgcn_dropout_apply(float *x, long long n, const uint64_t *mask, float scale, void *stream) {
   return guarded([&] {
     launch_dropout_apply_based(x, n, mask, 0, scale, as_stream(stream));
@@ -649,6 +662,12 @@ int pgcn_debug_set(const char *key, int value) {
   } else if (!std::strcmp(key, "parse_threads")) {
     if (!in(0, 4096)) return PGCN_E_INVALID;
     pgcn::g_parse_threads = value;
+  } else if (!std::strcmp(key, "mask_nib")) {
+    if (!in(0, 1)) return PGCN_E_INVALID;
+    pgcn::g_mask_nib = value;
+  } else if (!std::strcmp(key, "rs_chunks")) {
+    if (!in(1, 4)) return PGCN_E_INVALID;
+    pgcn::g_rs_chunks = value;
   } else if (!std::strcmp(key, "wide_prescale")) {
     if (!in(0, 1)) return PGCN_E_INVALID;
     pgcn::g_wide_prescale = value;

@@ -50,6 +50,12 @@ int g_fuse_output = 2;
 // stream hand-offs cost more than the ~7 us of kernels they hide)
 int g_mm_side = 0;
 constexpr int kMmSideRows = 65536;
+// "rs_chunks" (read at engine build): GraphSum row chunks of the edge-cut engine at world > 1
+// (chunk k's reduce-scatter overlaps chunk k+1's local sum)
+int g_rs_chunks = kRsChunks;
+// "mask_nib" (read per draw): dense X's input dropout mask drawn straight into the nibble
+// layout too (k_dropout_mask_nib, one launch); 0 = k_dropout_mask + k_mask_nibbles
+int g_mask_nib = 1;
 
 // ------------------------------------------------------------------------------------------
 // Adam (src/optim.cu:7-95; hpdga optim.cpp:16-35)
@@ -259,8 +265,9 @@ GCN::GCN(const GCNParams &params_, const AdamParams &adam, const GCNData &data, 
   side_stream = Stream::create(lo_prio);
   ctx.side_stream = side_stream.get();
   const int world = dist ? dist->world : 1, rank = dist ? dist->rank : 0;
+  // one row chunk on one rank: nothing to exchange, nothing to overlap
   part = make_partition(params.num_nodes, data.graph.indptr.data(), world, rank,
-                        dist ? kRsChunks : 1);
+                        dist && world > 1 ? g_rs_chunks : 1);
   if (dist) {  // the edge-cut path (also at world == 1, which exercises it on one GPU)
     if (dist->solo)
       comm = std::make_unique<SoloComm>(rank, world);
@@ -362,7 +369,10 @@ void GCN::build(const GCNData &data) {
       gk->set_scales(std::move(rs), cs);
       chunk_graphs.push_back(std::move(gk));
     }
+    // the chunks' columns are this rank's rows: one prescaled table serves them all
+    for (size_t k = 1; k < chunk_graphs.size(); k++) chunk_graphs[k]->share_tables(chunk_graphs[0].get());
     for (auto &gk : chunk_graphs) ctx.chunk_graphs.push_back(gk.get());
+    ctx.local_rows = part.local_rows();
   } else {
     std::vector<float> v = graph_coefs(N, data.graph.indptr.data(), data.graph.indices.data());
     graph = std::make_unique<DevGraph>(N, N, data.graph.indptr.data(), data.graph.indices.data(),
@@ -505,8 +515,13 @@ void GCN::build(const GCNData &data) {
     insert_layer(params.hidden_dims[(size_t)l - 1], params.hidden_dims[(size_t)l],
                  params.dropouts[(size_t)l], l);
   insert_last_layer();
-  if ((g_fuse_epilogue & kFuseTails) && !comm) fuse_epilogues();
-  if (g_fuse_output && !comm) fuse_output_layer();
+  // dense X: the input dropout draws straight into the nibble layout its GEMM reads
+  if (feats.dense && (feats.maskT || feats.maskW) && feats.cols <= 1024)
+    const_cast<Dropout *>(dropouts_[0])->set_nibbles(feats.maskT ? feats.maskT.get() : feats.maskW.get(), feats.cols,
+                              feats.rows);
+  // (edge-cut: the tails run in k_gs_finish on the rank's rows after the reduce-scatter)
+  if (g_fuse_epilogue & kFuseTails) fuse_epilogues();
+  if (g_fuse_output) fuse_output_layer();
   optimizer = Adam(weights, decays, adam_params);
   PGCN_HIP(hipDeviceSynchronize());
 }
@@ -700,8 +715,11 @@ void GCN::set_split(int split) {
   ctx.chunk_col_graphs.clear();
   if (g_split_cols && comm && !chunk_graphs.empty() && split == 1 &&
       !split_rows_host[1].empty()) {  // backward follows training
-    if (chunk_col_graphs.empty())
+    if (chunk_col_graphs.empty()) {
       for (auto &gk : chunk_graphs) chunk_col_graphs.push_back(gk->col_subset(split_rows_host[1]));
+      for (size_t k = 1; k < chunk_col_graphs.size(); k++)
+        chunk_col_graphs[k]->share_tables(chunk_col_graphs[0].get());
+    }
     for (auto &cg : chunk_col_graphs) ctx.chunk_col_graphs.push_back(cg.get());
   }
   if (g_split_cols && !comm && graph && split == 1) {  // backward only follows training

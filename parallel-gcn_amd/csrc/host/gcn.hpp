@@ -22,6 +22,7 @@ namespace pgcn {
 // GraphSum row chunks of the edge-cut engine: chunk k's reduce-scatter overlaps chunk k+1's
 // local sum (2: the LDS schedule keeps >= 1 workgroup per CU at 2 GPUs).
 constexpr int kRsChunks = 2;
+extern int g_rs_chunks;
 
 struct GCNParams {
   int num_nodes = 0, input_dim = 0, output_dim = 0;

@@ -407,8 +407,9 @@ void DevGraph::build_lds() {
   L->row_scale.upload(h_row_scale_);
   L->col_scale.allocate(h_col_scale_.size());
   L->col_scale.upload(h_col_scale_);
-  // whole slices of RING_SR rows (the loader copies 8-KB plane pieces)
-  L->scratch.allocate((size_t)ceil_div(n_cols_, RING_SR) * RING_SR * 16);
+  // whole slices of RING_SR rows (the loader copies 8-KB plane pieces); a graph sharing
+  // another's tables has none of its own
+  if (!table_owner_) L->scratch.allocate((size_t)ceil_div(n_cols_, RING_SR) * RING_SR * 16);
   L->partial.allocate((size_t)h.n_blocks * n_rows_ * 16);
   L->s.n_blocks = h.n_blocks;
   L->s.n_rows = n_rows_;
@@ -448,11 +449,39 @@ float *DevGraph::ring_table(int dim, const float **next_scale) {
   if (dim > 16 || !uses_lds(dim) || col_map_) return nullptr;
   if (!lds_) build_lds();
   *next_scale = lds_->s.col_scale;
-  return lds_->scratch.get();
+  return table_scratch();
+}
+
+void DevGraph::share_tables(DevGraph *owner) {
+  PGCN_CHECK(owner && owner != this && !owner->table_owner_ && owner->n_cols_ == n_cols_ &&
+                 owner->h_col_scale_ == h_col_scale_ && !owner->col_map_ == !col_map_,
+             PGCN_E_INVALID, "share_tables: the graphs' columns differ");
+  table_owner_ = owner;
+  lds_.reset();
+}
+
+bool DevGraph::can_share_tables(int dim) const {
+  if (!uses_lds(dim)) return false;
+  // one 16-column pass, or every pass's table from the batched prescale (graphsum below)
+  return dim <= 16 || (!col_map_ && g_wide_prescale);
+}
+
+float *DevGraph::table_scratch() {
+  if (!table_owner_) return lds_->scratch.get();
+  if (!table_owner_->lds_) table_owner_->build_lds();
+  return table_owner_->lds_->scratch.get();
+}
+
+float *DevGraph::table_wide(size_t floats) {
+  DevGraph *o = table_owner_ ? table_owner_ : this;
+  if (!o->lds_) o->build_lds();
+  if (o->lds_->tables.size() < floats) o->lds_->tables.allocate(floats);
+  return o->lds_->tables.get();
 }
 
 void DevGraph::graphsum(const float *in, int ld_in, float *out, int ld_out, int dim,
-                        hipStream_t s, bool compact_in, const GsEpilogue *epi, bool prestaged) {
+                        hipStream_t s, bool compact_in, const GsEpilogue *epi, bool prestaged,
+                        bool tables_ready) {
   const int *col_map = compact_in ? nullptr : col_map_.get();
   PGCN_CHECK(ld_in % 4 == 0 && ld_out % 4 == 0 && ld_in >= dim && ld_out >= dim,
              PGCN_E_INVALID, "graphsum: leading dims must be multiples of 4 and >= dim");
@@ -473,18 +502,19 @@ void DevGraph::graphsum(const float *in, int ld_in, float *out, int ld_out, int 
     for (int c0 = 0; c0 < dim; c0 += 16) ps.c[ps.n++] = std::min(c0, ldm - 16);
     // several passes: one launch prescales all of them (each pass then reads its own table)
     const bool batch = ps.n > 1 && !col_map && ld_in <= 128 && g_wide_prescale;
-    if (batch) {
-      if (lds_->tables.size() < table * ps.n) lds_->tables.allocate(table * ps.n);
+    PGCN_CHECK(!tables_ready || (can_share_tables(dim) && (ps.n == 1 || batch)), PGCN_E_INVALID,
+               "graphsum: shared tables on a call that prescales per pass");
+    float *tables = batch ? table_wide(table * ps.n) : nullptr;
+    if (batch && !tables_ready)
       launch_ring_prescale_wide(lds_->s, in, ld_in, std::min(ld_in, ps.c[ps.n - 1] + 16), ps,
-                                lds_->tables.get(), (long long)table, s);
-    }
+                                tables, (long long)table, s);
     for (int p = 0; p < ps.n; p++) {
       const int c = ps.c[p];
       GsEpilogue ep = epi ? *epi : GsEpilogue{};
       ep.col0 = c;
       launch_graphsum_ring(lds_->s, in + c, ld_in, out + c, ld_out,
-                           batch ? lds_->tables.get() + table * p : lds_->scratch.get(),
-                           lds_->partial.get(), s, col_map, &ep, prestaged || batch);
+                           batch ? tables + table * p : table_scratch(), lds_->partial.get(), s,
+                           col_map, &ep, prestaged || batch || tables_ready);
     }
     return;
   }

@@ -74,8 +74,18 @@ class DevGraph {
   // compact_in (column subsets): `in` holds the subset's columns as its rows (no gather)
   // epi: the element-wise tail applied to every output row as it is formed (one pass only:
   // dim <= 16, or a width with a kernel of its own and no 16-column passes)
+  // tables_ready: the prescaled table(s) this call reads were filled by a call of the same
+  // input on a graph sharing them (share_tables; can_share_tables(dim)): no prescale launch
   void graphsum(const float *in, int ld_in, float *out, int ld_out, int dim, hipStream_t s,
-                bool compact_in = false, const GsEpilogue *epi = nullptr, bool prestaged = false);
+                bool compact_in = false, const GsEpilogue *epi = nullptr, bool prestaged = false,
+                bool tables_ready = false);
+  // The ring schedule reads its prescaled input tables from `owner`'s buffers (same columns,
+  // column scales and column map: the edge-cut engine's row chunks of one column block), so
+  // one prescale serves every graph of the group.
+  void share_tables(DevGraph *owner);
+  // a graphsum() of this width prescales into tables a sharing graph can read as they are
+  bool can_share_tables(int dim) const;
+  const DevGraph *table_owner() const { return table_owner_; }
   // The ring schedule's prescaled-input table of a graphsum() of this width (one 16-column
   // pass, no column map), for a producer's epilogue to fill (then graphsum(.., prestaged));
   // null when this graph does not take that path.  next_scale = the table's column scales.
@@ -130,6 +140,9 @@ class DevGraph {
     DeviceBuffer<float> tables;  // every pass's prescaled table of a wide call (lazily)
   };
   std::unique_ptr<LdsSched> lds_;
+  DevGraph *table_owner_ = nullptr;  // share_tables: the graph whose table buffers this one reads
+  float *table_scratch();            // the one-pass table (own or the owner's)
+  float *table_wide(size_t floats);  // the multi-pass tables (own or the owner's), >= floats
   std::vector<float> h_row_scale_, h_col_scale_;
   // column subset: input row of compact column c (device), and the compacted input (plain path)
   DeviceBuffer<int> col_map_;

@@ -63,8 +63,26 @@ Dropout::Dropout(shared_ptr<Variable> in_, float p_, shared_ptr<DropoutRng> rng_
 
 void Dropout::draw(hipStream_t s, uint64_t *mask, int max_blocks) const {
   const DropoutRng &r = *rng;
+  if (nib_ && max_blocks == 0 && g_mask_nib && dropout_mask_nib_ok(nib_F_, r.mask_base)) {
+    launch_dropout_mask_nib(r.states.get(), r.n_chunks, 64 * r.chunk_lo, r.elem_end, p, mask,
+                            ctx->jump_table, r.mask_base, nib_F_, nib_rows_, nib_, s);
+    nib_from_ = mask;
+    return;
+  }
+  if (nib_from_ == mask) nib_from_ = nullptr;  // that layout no longer matches the bits
   launch_dropout_mask(r.states.get(), r.n_chunks, 64 * r.chunk_lo, r.elem_end, p, mask,
                       ctx->jump_table, s, max_blocks);
+}
+
+void Dropout::set_nibbles(uint64_t *nib, int F, int rows) {
+  PGCN_CHECK(!in && (!nib || (F >= 1 && F <= 1024 && rows >= 0)), PGCN_E_INVALID,
+             "dropout: nibble layout of the input dropout only");
+  PGCN_CHECK(!nib || rng->elem_end - rng->elem_begin == (long long)F * rows, PGCN_E_INVALID,
+             "dropout: the nibble layout needs dense rows x F elements");
+  nib_ = nib;
+  nib_F_ = F;
+  nib_rows_ = rows;
+  nib_from_ = nullptr;
 }
 
 void Dropout::draw_ahead(hipStream_t s, const Event *ready) const {
@@ -177,7 +195,8 @@ void SparseMatmul::forward(bool training, const Stream &s) const {
     else
       drop->draw_ahead(s.get());
     const uint64_t *m = drop->mask_ahead();
-    launch_mask_nibbles(m, base, x->cols, x->rows, x->cols, x->maskT.get(), s.get());
+    if (!drop->nibbles_of(m, x->maskT.get()))
+      launch_mask_nibbles(m, base, x->cols, x->rows, x->cols, x->maskT.get(), s.get());
     launch_xstream_nn(x->rows, b->cols, x->cols, x->x.get(), x->ldx, b->dev_data.get(), b->ld, 0,
                       c->dev_data.get(), c->ld, x->maskT.get(), scale, s.get(), ahead.get());
     ahead_valid = true;
@@ -185,7 +204,8 @@ void SparseMatmul::forward(bool training, const Stream &s) const {
   }
   MmProfile prof(ctx, s.get(), x->dense ? 2.0 * x->rows * b->cols * x->cols : 0.0);
   if (x->dense && x->maskT) {  // X-stream kernels (N <= 16, K <= 640)
-    if (mask) launch_mask_nibbles(mask, base, x->cols, x->rows, x->cols, x->maskT.get(), s.get());
+    if (mask && !drop->nibbles_of(mask, x->maskT.get()))
+      launch_mask_nibbles(mask, base, x->cols, x->rows, x->cols, x->maskT.get(), s.get());
     XsEpilogue e;  // the first GraphSum's prescaled input, written beside c
     if ((g_fuse_epilogue & kFuseXstream) && consumer && (training || !eval_out)) {
       e.next_table = consumer->claim_forward_table(x->rows, c->ld, &e.next_scale);
@@ -198,7 +218,8 @@ void SparseMatmul::forward(bool training, const Stream &s) const {
     // wide outputs: the mask in the nibble layout too (one pass over the bitmap; the wide
     // kernels then read one word per row and 4 steps, and the backward reuses it)
     const uint64_t *mw = mask && x->maskW ? x->maskW.get() : nullptr;
-    if (mw) launch_mask_nibbles(mask, base, x->cols, x->rows, x->cols, x->maskW.get(), s.get());
+    if (mw && !drop->nibbles_of(mask, mw))
+      launch_mask_nibbles(mask, base, x->cols, x->rows, x->cols, x->maskW.get(), s.get());
     launch_gemm_nn(x->rows, b->cols, x->cols, x->x.get(), x->ldx, b->dev_data.get(), b->ld, 0,
                    c->dev_data.get(), c->ld, mask, base, x->cols, scale, s.get(), mw);
   } else {
@@ -235,7 +256,7 @@ GraphSum::GraphSum(shared_ptr<Variable> in_, shared_ptr<Variable> out_, DevGraph
                    int dim_, ModuleContext *ctx_, bool last_layer_)
     : in(std::move(in_)), out(std::move(out_)), graph(graph_), dim(dim_), ctx(ctx_),
       last_layer(last_layer_) {
-  if (ctx->comm) {
+  if (ctx->comm && ctx->comm->world() > 1) {  // (one rank sums straight into `out`)
     for (DevGraph *gk : ctx->chunk_graphs) {
       partial.emplace_back();
       partial.back().allocate((size_t)gk->rows() * out->ld);
@@ -256,8 +277,22 @@ DevGraph *GraphSum::backward_graph() const {
   return last_layer && ctx->split_colgraph ? ctx->split_colgraph : graph;
 }
 
+// the graph whose prescaled input table this module's next forward / backward reads first
+// (edge-cut: row chunk 0's, which the other chunks share)
+DevGraph *GraphSum::forward_table_graph() const {
+  if (!ctx->comm) return forward_graph();
+  if (last_layer && !ctx->chunk_split_graphs.empty()) return nullptr;
+  return ctx->chunk_graphs.empty() ? nullptr : ctx->chunk_graphs[0];
+}
+
+DevGraph *GraphSum::backward_table_graph() const {
+  if (!ctx->comm) return backward_graph();
+  if (last_layer && !ctx->chunk_col_graphs.empty()) return ctx->chunk_col_graphs[0];
+  return ctx->chunk_graphs.empty() ? nullptr : ctx->chunk_graphs[0];
+}
+
 float4 *GraphSum::claim_forward_table(int rows, int ld, const float **scale) const {
-  DevGraph *g = forward_graph();
+  DevGraph *g = forward_table_graph();
   if (!g || !(g_fuse_epilogue & kFusePrestage) || dim != 16 || in->ld != 16 || ld != 16 || g->cols() != rows)
     return nullptr;
   float *t = g->ring_table(dim, scale);
@@ -277,11 +312,19 @@ void GraphSum::stage_next(GsEpilogue &e, GraphSum *next, DevGraph *ng, bool fwd)
   (fwd ? next->prestaged_fwd : next->prestaged_bwd) = true;
 }
 
+// Where this GraphSum's fused tails can run: in the kernel that forms the final rows (one
+// GPU: `g`'s combine), or (edge-cut) in k_gs_finish on this rank's rows once the
+// reduce-scatter has summed them
+bool GraphSum::tail_ok(const DevGraph *g, int ld_in, int ld_out) const {
+  if (ctx->comm) return dim % 4 == 0 && ld_out % 4 == 0;
+  return g && g->epilogue_ok(dim, ld_in, ld_out);
+}
+
 // The fused forward tail: ReLU on `out` (its mask when training), then the hidden Dropout
 // (training), both skipped as modules for this pass.  mode 0 when `g` cannot take an epilogue.
 GsEpilogue GraphSum::forward_epilogue(bool training, const Stream &s, const DevGraph *g) const {
   GsEpilogue e;
-  if (!fwd_relu || ctx->comm || !g || !g->epilogue_ok(dim, in->ld, out->ld)) return e;
+  if (!fwd_relu || !tail_ok(g, in->ld, out->ld)) return e;
   e.mode = 1;
   e.relu_mask = training ? fwd_relu->mask_ptr() : nullptr;
   e.relu_ld = out->ld;
@@ -294,7 +337,7 @@ GsEpilogue GraphSum::forward_epilogue(bool training, const Stream &s, const DevG
     e.drop_scale = fwd_drop->scale();
   }
   fwd_relu->skip_forward = true;
-  if (fwd_next) stage_next(e, fwd_next, fwd_next->forward_graph(), true);
+  if (fwd_next) stage_next(e, fwd_next, fwd_next->forward_table_graph(), true);
   return e;
 }
 
@@ -302,7 +345,7 @@ GsEpilogue GraphSum::forward_epilogue(bool training, const Stream &s, const DevG
 // forward), then the ReLU backward, both skipped as modules for this pass.
 GsEpilogue GraphSum::backward_epilogue(const DevGraph *g) const {
   GsEpilogue e;
-  if (!bwd_relu || ctx->comm || !g || !g->epilogue_ok(dim, out->ld, in->ld)) return e;
+  if (!bwd_relu || !tail_ok(g, out->ld, in->ld)) return e;
   e.mode = 2;
   e.relu_mask = bwd_relu->mask_ptr();
   e.relu_ld = in->ld;
@@ -315,7 +358,7 @@ GsEpilogue GraphSum::backward_epilogue(const DevGraph *g) const {
     bwd_drop->skip_backward = true;
   }
   bwd_relu->skip_backward = true;
-  if (bwd_next) stage_next(e, bwd_next, bwd_next->backward_graph(), false);
+  if (bwd_next) stage_next(e, bwd_next, bwd_next->backward_table_graph(), false);
   return e;
 }
 
@@ -328,10 +371,19 @@ void GraphSum::run(const float *src, float *dst, const Stream &s, int mode,
     e0.record(s.get());
   }
   double bytes = 0;
-  if (ctx->comm) {
+  const std::vector<DevGraph *> &cgs = mode == 2 ? ctx->chunk_col_graphs : ctx->chunk_graphs;
+  if (ctx->comm && ctx->comm->world() == 1 && cgs.size() == 1 && mode != 1) {
+    // one rank: its column block is all of Â and the reduce-scatter would be a copy -- the
+    // block's sums are final, formed with the tail in the combine as on one GPU
+    cgs[0]->graphsum(src, in->ld, dst, out->ld, dim, s.get(), false, epi, prestaged);
+    bytes = cgs[0]->algorithmic_bytes(dim);
+    if (ctx->profile) e1.record(s.get());
+  } else if (ctx->comm) {
     // Per row chunk: partial sums of the chunk's (padded) rows from this rank's columns on
     // the compute stream, then its reduce-scatter on the comm stream, which hands every rank
-    // its own rows of the chunk while the next chunk is summed.
+    // its own rows of the chunk while the next chunk is summed.  The chunks share one
+    // prescaled table of this rank's columns (DevGraph::share_tables): prescaled once, by
+    // the producer's epilogue (prestaged) or by chunk 0's call.
     const size_t h = (size_t)out->rows / ctx->chunk_graphs.size();
     for (size_t k = 0; k < ctx->chunk_graphs.size(); k++) {
       if (mode == 1) {
@@ -347,8 +399,10 @@ void GraphSum::run(const float *src, float *dst, const Stream &s, int mode,
           bytes += sk->algorithmic_bytes(dim);
         }
       } else {
-        DevGraph *gk = mode == 2 ? ctx->chunk_col_graphs[k] : ctx->chunk_graphs[k];
-        gk->graphsum(src, in->ld, partial[k].get(), out->ld, dim, s.get());
+        DevGraph *gk = cgs[k];
+        const bool shared = k > 0 && gk->table_owner() == cgs[0] && gk->can_share_tables(dim);
+        gk->graphsum(src, in->ld, partial[k].get(), out->ld, dim, s.get(), false, nullptr,
+                     k == 0 && prestaged, shared);
         bytes += gk->algorithmic_bytes(dim);
       }
       computed[k].record(s.get());
@@ -356,9 +410,11 @@ void GraphSum::run(const float *src, float *dst, const Stream &s, int mode,
       ctx->comm->reduce_scatter_sum(partial[k].get(), dst + k * h * out->ld, h * out->ld,
                                     ctx->comm_stream);
     }
-    if (ctx->profile) e1.record(s.get());
     reduced.record(ctx->comm_stream);
     reduced.wait_on(s.get());  // dst complete, partials free for the next call
+    // the fused tail on this rank's rows of the summed output (padding rows stay zero)
+    if (epi && epi->mode) launch_gs_finish(dst, out->ld, ctx->local_rows, dim, *epi, s.get());
+    if (ctx->profile) e1.record(s.get());
   } else {
     graph->graphsum(src, in->ld, dst, out->ld, dim, s.get(), false, epi, prestaged);
     bytes = graph->algorithmic_bytes(dim);
@@ -373,8 +429,9 @@ void GraphSum::run(const float *src, float *dst, const Stream &s, int mode,
 void GraphSum::forward(bool training, const Stream &s) const {
   const bool pre = prestaged_fwd;  // this call's input table was written by the producer
   prestaged_fwd = false;
-  PGCN_CHECK(!pre || (!ctx->comm && (training || !first_layer)), PGCN_E_INVALID,
-             "graphsum: prestaged input on a path that does not read it");
+  PGCN_CHECK(!pre || ((training || !first_layer) &&
+                      !(last_layer && ctx->comm && !ctx->chunk_split_graphs.empty())),
+             PGCN_E_INVALID, "graphsum: prestaged input on a path that does not read it");
   if (!training && first_layer) return;  // eval_ax: SparseMatmul wrote Â X W1 already
   if (last_layer && ctx->comm && !ctx->chunk_split_graphs.empty()) {
     run(in->dev_data.get(), out->dev_data.get(), s, 1);
@@ -417,11 +474,11 @@ void GraphSum::backward(const Stream &s) const {
   // the same gather on grads (Â symmetric): in.grad = Â out.grad (module.cpp:98-111)
   const bool pre = prestaged_bwd;  // out.grad's input table was written by its producer
   prestaged_bwd = false;
-  PGCN_CHECK(!pre || !ctx->comm, PGCN_E_INVALID, "graphsum: prestaged gradient, edge-cut");
   if (last_layer && ctx->comm && !ctx->chunk_col_graphs.empty()) {
     // edge-cut: out.grad is zero outside the training split's rows, so each chunk graph keeps
     // only the edges from those columns (all rows stay: the partials are written whole)
-    run(out->dev_grad.get(), in->dev_grad.get(), s, 2);
+    const GsEpilogue epi = backward_epilogue(ctx->chunk_col_graphs[0]);
+    run(out->dev_grad.get(), in->dev_grad.get(), s, 2, &epi, pre);
     return;
   }
   DevGraph *cg = last_layer && !ctx->comm ? ctx->split_colgraph : nullptr;

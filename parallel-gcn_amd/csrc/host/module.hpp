@@ -92,6 +92,7 @@ class Dropout;
 constexpr int kFuseTails = 1, kFusePrestage = 2, kFuseXstream = 4;
 extern int g_fuse_epilogue;
 extern int g_fuse_output;
+extern int g_mask_nib;
 
 // Shared per-GCN state the modules read (current split, comm, profiling, RNG table).
 struct ModuleContext {
@@ -129,6 +130,7 @@ struct ModuleContext {
   int xent_blocks = 0;
   Comm *comm = nullptr;        // null on one GPU
   hipStream_t comm_stream = nullptr;      // edge-cut: stream of the reduce-scatters
+  int local_rows = 0;                     // edge-cut: this rank's rows (the rest is padding)
   std::vector<DevGraph *> chunk_graphs;   // edge-cut: Â column block per RS row chunk
   // edge-cut output-layer row restriction: per RS chunk, the chunk graph restricted to the
   // current split's labelled rows (padded chunk row ids in chunk_split_rows); empty: off
@@ -184,11 +186,21 @@ class Dropout : public Module {
   const Variable *variable() const { return in.get(); }
   void draw_fused(hipStream_t s) const;
   mutable bool skip_forward = false, skip_backward = false;
+  // Dense X's input dropout: every draw also writes the X-stream / wide GEMM kernels' nibble
+  // layout of its bits into `nib` ([rows][16], k_dropout_mask_nib: one launch for both
+  // layouts); nibbles_of(mask, nib): `nib` holds the layout of the draw into `mask`
+  void set_nibbles(uint64_t *nib, int F, int rows);
+  bool nibbles_of(const uint64_t *mask, const uint64_t *nib) const {
+    return nib && nib == nib_ && nib_from_ == mask;
+  }
 
  private:
   void draw(hipStream_t s, uint64_t *mask, int max_blocks = 0) const;
   mutable bool ahead = false;
   mutable const Event *ahead_ready = nullptr;  // recorded after an ahead draw on a side stream
+  uint64_t *nib_ = nullptr;
+  int nib_F_ = 0, nib_rows_ = 0;
+  mutable const uint64_t *nib_from_ = nullptr;  // the mask whose nibble layout `nib_` holds
 };
 
 // include/module.cuh:47-68: c = drop(X) * W
@@ -255,6 +267,9 @@ class GraphSum : public Module {
   // the graph this module's next forward / backward sums over (single GPU)
   DevGraph *forward_graph() const;
   DevGraph *backward_graph() const;
+  // ... and the graph whose prescaled table that call reads (edge-cut: row chunk 0's)
+  DevGraph *forward_table_graph() const;
+  DevGraph *backward_table_graph() const;
   // for a producer of this GraphSum's next forward input with `rows` rows and 16 columns:
   // the ring table (and its scale) that call reads, marked as written by the producer
   // (prestaged_fwd); null when that call has none
@@ -268,6 +283,7 @@ class GraphSum : public Module {
   // points the epilogue's next_table at `next`'s input table on graph `ng`, if it has one
   void stage_next(GsEpilogue &e, GraphSum *next, DevGraph *ng, bool fwd) const;
   // the fused tails of this call (mode 0 when none applies)
+  bool tail_ok(const DevGraph *g, int ld_in, int ld_out) const;
   GsEpilogue forward_epilogue(bool training, const Stream &s, const DevGraph *g) const;
   GsEpilogue backward_epilogue(const DevGraph *g) const;
 };

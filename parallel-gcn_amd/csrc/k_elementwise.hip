@@ -8,6 +8,8 @@
 //
 // Float contraction is OFF in this file: every product/sum rounds where the sequential
 // CPU reference (hpdga-spring23) rounds, so Adam and dropout are bit-exact.
+#include <numeric>
+
 #include "common.hpp"
 #include "kernels.hpp"
 
@@ -122,6 +124,97 @@ __global__ __launch_bounds__(256) void k_dropout_mask(uint64_t *__restrict__ sta
 #endif
     emit(c, a0, a1, ((uint64_t)x.hi << 32) | x.lo);
     if (two) emit(c2, b0, b1, ((uint64_t)y.hi << 32) | y.lo);
+  }
+}
+
+// The input dropout of dense X straight into both layouts its users read (r04): the flat
+// element-order bitmap (hpdga's draw order, as k_dropout_mask) and the X-stream / wide GEMM
+// kernels' "nibble" layout (k_mask_nibbles: out[m][j] nibble c = keep bits of X[m][64c + 4j ..
+// + 3]), one launch instead of two.  A workgroup owns whole rows [r0, r1) whose bit range
+// starts and ends on chunk boundaries (mask_base + r * F = 0 mod 64 at every interior cut:
+// r0 - first_rows multiple of rows_per_wg, chosen by the launcher), so every chunk is drawn,
+// written and advanced by exactly one workgroup; its words stay in LDS for the nibble
+// assembly.  One chunk per thread (the launch's many workgroups hide the xorshift chain).
+constexpr int DMN_MAX_CHUNKS = 1024;
+__global__ __launch_bounds__(1024) void k_dropout_mask_nib(
+    uint64_t *__restrict__ states, long long n_chunks, long long elem0, long long elem_end,
+    int threshold, uint64_t *__restrict__ mask, const uint4 *__restrict__ table,
+    long long mask_base, int F, int rows, int rows_per_wg, int first_rows,
+    uint64_t *__restrict__ nib) {
+  __shared__ uint4 lut[32 * 16];
+  __shared__ uint64_t words[DMN_MAX_CHUNKS + 2];
+  for (int i = threadIdx.x; i < 32 * 16; i += blockDim.x) {
+    const int p = i >> 4, v = i & 15;
+    lut[i] = table[(p >> 1) * 256 + (v << (4 * (p & 1)))];
+  }
+  // rows of this workgroup: workgroup 0 takes [0, first_rows), then rows_per_wg each
+  const int b = blockIdx.x;
+  const int r0 = b == 0 ? 0 : min(rows, first_rows + (b - 1) * rows_per_wg);
+  const int r1 = b == 0 ? min(rows, first_rows) : min(rows, first_rows + b * rows_per_wg);
+  const long long c0 = (mask_base + (long long)r0 * F) >> 6;
+  const long long c1 = b == (int)gridDim.x - 1 ? n_chunks
+                                                : min(n_chunks, (mask_base + (long long)r1 * F + 63) >> 6);
+  const int nc = (int)(c1 - c0);
+  __syncthreads();
+  if ((int)threadIdx.x < nc) {
+    const long long c = c0 + threadIdx.x;
+    const uint64_t a0 = states[2 * c], a1 = states[2 * c + 1];
+    Xs64 x{a0, a1};
+    x.thr2 = (uint32_t)threshold << 1;
+#pragma unroll
+    for (int j = 0; j < 64; j++) x.step(j, threshold);
+#if PGCN_DROP_SHIFTIN
+    x.lo = __builtin_bitreverse32(x.lo);
+    x.hi = __builtin_bitreverse32(x.hi);
+#endif
+    uint64_t word = ((uint64_t)x.hi << 32) | x.lo;
+    const long long e = elem0 + 64 * c;
+    if (e + 64 > elem_end) {
+      const long long valid = elem_end - e;
+      word = valid <= 0 ? 0 : (word & ((valid >= 64) ? ~0ull : ((1ull << valid) - 1)));
+    }
+    mask[c] = word;
+    words[threadIdx.x] = word;
+    uint64_t n0 = 0, n1 = 0;
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+      const uint4 v = lut[q * 16 + ((a0 >> (4 * q)) & 0xf)];
+      n0 ^= ((uint64_t)v.y << 32) | v.x;
+      n1 ^= ((uint64_t)v.w << 32) | v.z;
+    }
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+      const uint4 v = lut[(16 + q) * 16 + ((a1 >> (4 * q)) & 0xf)];
+      n0 ^= ((uint64_t)v.y << 32) | v.x;
+      n1 ^= ((uint64_t)v.w << 32) | v.z;
+    }
+    states[2 * c] = n0;
+    states[2 * c + 1] = n1;
+  } else if ((int)threadIdx.x < nc + 2) {
+    words[threadIdx.x] = 0;  // a straddling last nibble peeks one word past the range
+  }
+  __syncthreads();
+  // nibble words of rows r0 .. r1 - 1 (k_mask_nibbles' assembly, from LDS)
+  const int total = (r1 - r0) * 16;
+  for (int t = threadIdx.x; t < total; t += blockDim.x) {
+    const int r = t >> 4, j = t & 15;
+    const long long p0 = mask_base + (long long)(r0 + r) * F + 4 * j - (c0 << 6);  // local bit
+    const int w0 = (int)(p0 >> 6), sh = (int)(p0 & 63);
+    const int ncb = (F - 4 * j + 63) >> 6;  // nibbles with kb = 64 c + 4 j < F
+    uint64_t out = 0, lo = words[w0];
+#pragma unroll
+    for (int c = 0; c < 16; c++) {
+      if (c < ncb) {
+        const uint64_t hi = words[w0 + c + 1];
+        uint64_t v = (lo >> sh) & 0xfu;
+        if (sh > 60) v = (v | (hi << (64 - sh))) & 0xfu;
+        const int kb = 64 * c + 4 * j;
+        if (kb + 4 > F) v &= (1ull << (F - kb)) - 1;  // keep bits of k >= F are 0
+        out |= v << (4 * c);
+        lo = hi;
+      }
+    }
+    nib[(long long)(r0 + r) * 16 + j] = out;
   }
 }
 
@@ -813,6 +906,43 @@ void launch_dropout_mask(uint64_t *states, long long n_chunks, long long elem0,
   const int grid = grid_for(ceil_div(n_chunks, 2), 256, max_blocks > 0 ? max_blocks : 8 * kCUs);
   PGCN_LAUNCH(k_dropout_mask, dim3(grid), dim3(256), 0, s, states, n_chunks, elem0,
                      elem_end, threshold, mask, static_cast<const uint4 *>(table));
+}
+
+// rows_per_wg: whole multiples of 64 / gcd(F, 64) rows (their bits end on a chunk boundary)
+// with at most DMN_MAX_CHUNKS chunks; the first workgroup takes the rows up to the first
+// such boundary.  False when the shape does not fit (the caller then draws + lays out in two
+// launches).
+bool dropout_mask_nib_ok(int F, long long mask_base) {
+  if (F < 1 || F > 1024) return false;
+  const int g = std::gcd(F, 64);
+  return (mask_base % g) == 0 && F / g <= DMN_MAX_CHUNKS && mask_base >= 0 && mask_base < 64;
+}
+
+void launch_dropout_mask_nib(uint64_t *states, long long n_chunks, long long elem0,
+                             long long elem_end, float p, uint64_t *mask, const void *table,
+                             long long mask_base, int F, int rows, uint64_t *nib, hipStream_t s) {
+  PGCN_CHECK(dropout_mask_nib_ok(F, mask_base), PGCN_E_INVALID, "dropout_mask_nib: shape");
+  if (n_chunks <= 0 || rows <= 0) return;
+  PGCN_CHECK(n_chunks == ((mask_base + (long long)rows * F + 63) >> 6), PGCN_E_INVALID,
+             "dropout_mask_nib: chunks must cover rows x F bits from mask_base");
+  const int threshold = (int)(p * (float)0x7fffffff);  // hpdga module.cpp:211
+  const int g = std::gcd(F, 64), r_unit = 64 / g, c_unit = F / g;  // rows / chunks per unit
+  const int units = std::max(1, std::min(DMN_MAX_CHUNKS / c_unit, 512 / c_unit));
+  const int rows_per_wg = r_unit * units;
+  // first interior cut: the smallest r > 0 with (mask_base + r F) = 0 mod 64
+  int first = 0;
+  for (int r = 1; r <= r_unit; r++)
+    if ((mask_base + (long long)r * F) % 64 == 0) {
+      first = r;
+      break;
+    }
+  PGCN_CHECK(first > 0, PGCN_E_INVALID, "dropout_mask_nib: no chunk-aligned row cut");
+  const long long wgs = 1 + (rows > first ? ceil_div((long long)(rows - first), rows_per_wg) : 0);
+  // (the first workgroup can hold one chunk more; 2 more threads zero the words past it)
+  const int threads = (int)std::min<long long>(1024, ceil_div((long long)c_unit * units + 3, 64) * 64);
+  PGCN_LAUNCH(k_dropout_mask_nib, dim3((unsigned)wgs), dim3(threads), 0, s, states, n_chunks,
+              elem0, elem_end, threshold, mask, static_cast<const uint4 *>(table), mask_base, F,
+              rows, rows_per_wg, first, nib);
 }
 
 void launch_dropout_apply_based(float *x, long long n, const uint64_t *mask, long long base,

@@ -141,6 +141,20 @@ __global__ __launch_bounds__(256) void k_gs_lds_combine(const float4 *__restrict
   out[r * ld4_out + v] = a;
 }
 
+// y[r] = epilogue(y[r]) for the n rows of a reduce-scattered GraphSum output (edge-cut engine:
+// the tail a one-GPU GraphSum applies in its combine, applied once the partial sums of every
+// rank have been added; the same operations on the same sums: bit-identical to the modules)
+__global__ __launch_bounds__(256) void k_gs_finish(float4 *__restrict__ y, int ld4, int n, int vec,
+                                                   GsEpilogue epi) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long r = t / vec;
+  if (r >= n) return;
+  const int v = (int)(t - r * vec);
+  float4 a = y[r * ld4 + v];
+  gs_epilogue(a, r, 4 * v, epi);
+  y[r * ld4 + v] = a;
+}
+
 __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
     const uint2 *__restrict__ entries, const long long *__restrict__ wave_off,
     const unsigned short *__restrict__ counts, int t_max, const int2 *__restrict__ slices,
@@ -332,6 +346,17 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
 // all 61 batches then runs at the kernel's end on 61 CUs), one prescale / combine launch for
 // all 16-column passes of a wide row (1.677 vs 1.594 ms per d = 128 call: the 8 passes'
 // partials no longer stay in the Infinity Cache), fixed issue priority (hand-off waits 22 %).
+
+void launch_gs_finish(float *y, int ld, int n, int dim, const GsEpilogue &epi, hipStream_t st) {
+  PGCN_CHECK(ld % 4 == 0 && dim % 4 == 0 && dim <= ld && n >= 0, PGCN_E_INVALID,
+             "gs_finish: shape");
+  PGCN_CHECK(!epi.next_table || dim == 16, PGCN_E_INVALID, "gs_finish: next table of a wide row");
+  if (n == 0 || epi.mode == 0) return;
+  const long long t = (long long)n * (dim / 4);
+  PGCN_LAUNCH(k_gs_finish, dim3((unsigned)ceil_div(t, 256)), dim3(256), 0, st,
+              reinterpret_cast<float4 *>(y), ld / 4, n, dim / 4, epi);
+  PGCN_HIP(hipGetLastError());
+}
 
 void launch_ring_prescale_wide(const LdsSchedule &s, const float *in, int ld_in, int width,
                                const RingPasses &passes, float *tables, long long table_floats,

@@ -107,6 +107,10 @@ void launch_graphsum_ring(const LdsSchedule &s, const float *in, int ld_in, floa
                           int ld_out, float *scratch_in, float *partial, hipStream_t st,
                           const int *col_map = nullptr, const GsEpilogue *epi = nullptr,
                           bool prestaged = false);
+// The edge-cut engine's GraphSum tail: after the reduce-scatter has summed every rank's
+// partials into this rank's rows y [n][ld] (ld % 4 == 0, dim % 4 == 0), the fused
+// element-wise epilogue (gs_epilogue.hpp: ReLU / Dropout, the next GraphSum's table) in place
+void launch_gs_finish(float *y, int ld, int n, int dim, const GsEpilogue &epi, hipStream_t st);
 
 // maskT (optional): the same dropout bits in the nibble layout, read by the wide kernels
 void launch_gemm_nn(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
@@ -190,6 +194,13 @@ void launch_spmm_csc_bwd(int nf, int p, int ldg, const int *csc_ptr, const int *
 void launch_dropout_mask(uint64_t *states, long long n_chunks, long long elem0,
                          long long elem_end, float p, uint64_t *mask, const void *table,
                          hipStream_t s, int max_blocks = 0);
+// the input dropout of dense X [rows][F] (element i = m F + k at local bit mask_base + i) into
+// the flat bitmap AND the nibble layout nib [rows][16] in one launch (k_dropout_mask_nib);
+// dropout_mask_nib_ok: the shape the kernel takes (F <= 1024, chunk-aligned row cuts)
+bool dropout_mask_nib_ok(int F, long long mask_base);
+void launch_dropout_mask_nib(uint64_t *states, long long n_chunks, long long elem0,
+                             long long elem_end, float p, uint64_t *mask, const void *table,
+                             long long mask_base, int F, int rows, uint64_t *nib, hipStream_t s);
 void launch_dropout_apply_based(float *x, long long n, const uint64_t *mask, long long base,
                                 float scale, hipStream_t s);
 void launch_relu_fwd(float *x, long long n, uint8_t *mask, int training, hipStream_t s);

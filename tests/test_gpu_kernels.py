@@ -230,6 +230,43 @@ def test_dropout_masks_bit_exact(pgcn):
         np.testing.assert_array_equal(ours, ref)
 
 
+@pytest.mark.parametrize("F,rows,mask_base", [(602, 1000, 0), (602, 777, 22), (64, 3000, 0),
+                                               (100, 513, 36), (1023, 97, 5), (600, 40, 8)])
+def test_dropout_mask_nib_matches_two_launches(pgcn, F, rows, mask_base):
+    """k_dropout_mask_nib (the input dropout of dense X drawn into the flat bitmap and the
+    GEMMs' nibble layout by one launch) against k_dropout_mask followed by k_mask_nibbles from
+    the same chunk states, over two epochs (state advance by the period): the same words in
+    both layouts, the same advanced states, bit for bit.  mask_base != 0 is an edge-cut rank's
+    first element inside its first chunk."""
+    period = 1_000_003
+    n_elems = mask_base + rows * F
+    nch = (n_elems + 63) // 64
+    st = pgcn.rng_jump(pgcn.rng_seed(), 777)
+    states = np.zeros((nch, 2), np.uint64)
+    for c in range(nch):
+        states[c] = st
+        st = pgcn.rng_jump(st, 64)
+    table = torch.from_numpy(pgcn.rng_jump_table(period).view(np.int64)).to(DEV)
+    sa = torch.from_numpy(states.view(np.int64).copy()).to(DEV)
+    sb = sa.clone()
+    ma = torch.zeros(nch + 1, dtype=torch.int64, device=DEV)
+    mb = torch.zeros(nch + 1, dtype=torch.int64, device=DEV)
+    na = torch.full((rows, 16), -1, dtype=torch.int64, device=DEV)
+    nb = torch.full((rows, 16), -1, dtype=torch.int64, device=DEV)
+    for _ in range(2):
+        pgcn.check(pgcn.lib.pgcn_dropout_mask(vp(sa), nch, n_elems, 0, 0.5, vp(ma), vp(table),
+                                              stream()), "dropout_mask")
+        pgcn.check(pgcn.lib.pgcn_mask_nibbles(vp(ma), mask_base, F, rows, F, vp(na), stream()),
+                   "nib")
+        pgcn.check(pgcn.lib.pgcn_dropout_mask_nib(vp(sb), nch, n_elems, 0, 0.5, vp(mb),
+                                                  vp(table), mask_base, F, rows, vp(nb),
+                                                  stream()), "dropout_mask_nib")
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(mb.cpu().numpy()[:nch], ma.cpu().numpy()[:nch])
+        np.testing.assert_array_equal(nb.cpu().numpy(), na.cpu().numpy())
+        np.testing.assert_array_equal(sb.cpu().numpy(), sa.cpu().numpy())
+
+
 def test_dropout_apply(pgcn):
     n = 10_007
     x = torch.randn(n, device=DEV)
