@@ -86,6 +86,8 @@ _sig("pgcn_spmm_csc_bwd", c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_v
      c_float, c_void_p, c_void_p, c_void_p)
 _sig("pgcn_csr_transpose", c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p)
 _sig("pgcn_dropout_mask", c_int, c_void_p, c_ll, c_ll, c_ll, c_float, c_void_p, c_void_p, c_void_p)
+_sig("pgcn_dropout_mask_nib", c_int, c_void_p, c_ll, c_ll, c_ll, c_float, c_void_p, c_void_p, c_ll,
+     c_int, c_int, c_void_p, c_void_p)
 _sig("pgcn_dropout_apply", c_int, c_void_p, c_ll, c_void_p, c_float, c_void_p)
 _sig("pgcn_relu_fwd", c_int, c_void_p, c_ll, c_void_p, c_int, c_void_p)
 _sig("pgcn_relu_bwd", c_int, c_void_p, c_ll, c_void_p, c_void_p)
@@ -133,6 +135,7 @@ _sig("pgcn_debug_set", c_int, ctypes.c_char_p, c_int)
 _sig("pgcn_debug_path_count", c_ll, ctypes.c_char_p, c_int)
 _sig("pgcn_debug_empty_launches", c_int, c_int, c_void_p)
 _sig("pgcn_debug_exp_check", c_int, c_void_p, c_ll, c_void_p, c_void_p, c_void_p)
+_sig("pgcn_debug_div_check", c_int, c_void_p, c_void_p, c_ll, c_void_p, c_void_p)
 _sig("pgcn_debug_lds_check", c_int, c_int, c_int, c_void_p, c_void_p, c_int, P(ctypes.c_double),
      P(c_ll))
 _sig("pgcn_debug_lds_counts", c_ll, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_ll,

@@ -132,17 +132,37 @@ __global__ __launch_bounds__(256) void k_dropout_mask(uint64_t *__restrict__ sta
 // kernels' "nibble" layout (k_mask_nibbles: out[m][j] nibble c = keep bits of X[m][64c + 4j ..
 // + 3]), one launch instead of two.  A workgroup owns whole rows [r0, r1) whose bit range
 // starts and ends on chunk boundaries (mask_base + r * F = 0 mod 64 at every interior cut:
-// r0 - first_rows multiple of rows_per_wg, chosen by the launcher), so every chunk is drawn,
+// r0 - first_rows a multiple of rows_per_wg, chosen by the launcher), so every chunk is drawn,
 // written and advanced by exactly one workgroup; its words stay in LDS for the nibble
-// assembly.  One chunk per thread (the launch's many workgroups hide the xorshift chain).
-constexpr int DMN_MAX_CHUNKS = 1024;
+// assembly.  Two chunks per thread, their xorshift chains interleaved (k_dropout_mask's
+// latency hiding).
+constexpr int DMN_MAX_CHUNKS = 2048;
+__device__ __forceinline__ uint64_t dmn_advance(const uint4 *lut, uint64_t a0, uint64_t a1,
+                                                uint64_t &n1) {
+  uint64_t n0 = 0;
+  n1 = 0;
+#pragma unroll
+  for (int q = 0; q < 16; q++) {
+    const uint4 v = lut[q * 16 + ((a0 >> (4 * q)) & 0xf)];
+    n0 ^= ((uint64_t)v.y << 32) | v.x;
+    n1 ^= ((uint64_t)v.w << 32) | v.z;
+  }
+#pragma unroll
+  for (int q = 0; q < 16; q++) {
+    const uint4 v = lut[(16 + q) * 16 + ((a1 >> (4 * q)) & 0xf)];
+    n0 ^= ((uint64_t)v.y << 32) | v.x;
+    n1 ^= ((uint64_t)v.w << 32) | v.z;
+  }
+  return n0;
+}
+
 __global__ __launch_bounds__(1024) void k_dropout_mask_nib(
     uint64_t *__restrict__ states, long long n_chunks, long long elem0, long long elem_end,
     int threshold, uint64_t *__restrict__ mask, const uint4 *__restrict__ table,
     long long mask_base, int F, int rows, int rows_per_wg, int first_rows,
     uint64_t *__restrict__ nib) {
   __shared__ uint4 lut[32 * 16];
-  __shared__ uint64_t words[DMN_MAX_CHUNKS + 2];
+  extern __shared__ uint64_t words[];  // this workgroup's chunk words (+ 2), dynamic
   for (int i = threadIdx.x; i < 32 * 16; i += blockDim.x) {
     const int p = i >> 4, v = i & 15;
     lut[i] = table[(p >> 1) * 256 + (v << (4 * (p & 1)))];
@@ -154,50 +174,50 @@ __global__ __launch_bounds__(1024) void k_dropout_mask_nib(
   const long long c0 = (mask_base + (long long)r0 * F) >> 6;
   const long long c1 = b == (int)gridDim.x - 1 ? n_chunks
                                                 : min(n_chunks, (mask_base + (long long)r1 * F + 63) >> 6);
-  const int nc = (int)(c1 - c0);
+  const int nc = (int)(c1 - c0), half = (nc + 1) >> 1;
+  const int t = threadIdx.x;
+  if (t < 2) words[nc + t] = 0;  // a straddling last nibble peeks one word past the range
   __syncthreads();
-  if ((int)threadIdx.x < nc) {
-    const long long c = c0 + threadIdx.x;
-    const uint64_t a0 = states[2 * c], a1 = states[2 * c + 1];
-    Xs64 x{a0, a1};
-    x.thr2 = (uint32_t)threshold << 1;
+  if (t < half) {
+    // chunks t and t + half (the second one absent when nc is odd and t is the last thread)
+    const bool two = t + half < nc;
+    const long long ca = c0 + t, cb = two ? ca + half : ca;
+    const uint64_t a0 = states[2 * ca], a1 = states[2 * ca + 1];
+    const uint64_t b0 = states[2 * cb], b1 = states[2 * cb + 1];
+    Xs64 x{a0, a1}, y{b0, b1};
+    x.thr2 = y.thr2 = (uint32_t)threshold << 1;
 #pragma unroll
-    for (int j = 0; j < 64; j++) x.step(j, threshold);
+    for (int j = 0; j < 64; j++) {
+      x.step(j, threshold);
+      y.step(j, threshold);
+    }
 #if PGCN_DROP_SHIFTIN
     x.lo = __builtin_bitreverse32(x.lo);
     x.hi = __builtin_bitreverse32(x.hi);
+    y.lo = __builtin_bitreverse32(y.lo);
+    y.hi = __builtin_bitreverse32(y.hi);
 #endif
-    uint64_t word = ((uint64_t)x.hi << 32) | x.lo;
-    const long long e = elem0 + 64 * c;
-    if (e + 64 > elem_end) {
-      const long long valid = elem_end - e;
-      word = valid <= 0 ? 0 : (word & ((valid >= 64) ? ~0ull : ((1ull << valid) - 1)));
-    }
-    mask[c] = word;
-    words[threadIdx.x] = word;
-    uint64_t n0 = 0, n1 = 0;
-#pragma unroll
-    for (int q = 0; q < 16; q++) {
-      const uint4 v = lut[q * 16 + ((a0 >> (4 * q)) & 0xf)];
-      n0 ^= ((uint64_t)v.y << 32) | v.x;
-      n1 ^= ((uint64_t)v.w << 32) | v.z;
-    }
-#pragma unroll
-    for (int q = 0; q < 16; q++) {
-      const uint4 v = lut[(16 + q) * 16 + ((a1 >> (4 * q)) & 0xf)];
-      n0 ^= ((uint64_t)v.y << 32) | v.x;
-      n1 ^= ((uint64_t)v.w << 32) | v.z;
-    }
-    states[2 * c] = n0;
-    states[2 * c + 1] = n1;
-  } else if ((int)threadIdx.x < nc + 2) {
-    words[threadIdx.x] = 0;  // a straddling last nibble peeks one word past the range
+    auto finish = [&](long long c, uint64_t word, uint64_t s0, uint64_t s1) {
+      const long long e = elem0 + 64 * c;
+      if (e + 64 > elem_end) {
+        const long long valid = elem_end - e;
+        word = valid <= 0 ? 0 : (word & ((valid >= 64) ? ~0ull : ((1ull << valid) - 1)));
+      }
+      mask[c] = word;
+      words[c - c0] = word;
+      uint64_t n1;
+      const uint64_t n0 = dmn_advance(lut, s0, s1, n1);
+      states[2 * c] = n0;
+      states[2 * c + 1] = n1;
+    };
+    finish(ca, ((uint64_t)x.hi << 32) | x.lo, a0, a1);
+    if (two) finish(cb, ((uint64_t)y.hi << 32) | y.lo, b0, b1);
   }
   __syncthreads();
   // nibble words of rows r0 .. r1 - 1 (k_mask_nibbles' assembly, from LDS)
   const int total = (r1 - r0) * 16;
-  for (int t = threadIdx.x; t < total; t += blockDim.x) {
-    const int r = t >> 4, j = t & 15;
+  for (int u = t; u < total; u += blockDim.x) {
+    const int r = u >> 4, j = u & 15;
     const long long p0 = mask_base + (long long)(r0 + r) * F + 4 * j - (c0 << 6);  // local bit
     const int w0 = (int)(p0 >> 6), sh = (int)(p0 & 63);
     const int ncb = (F - 4 * j + 63) >> 6;  // nibbles with kb = 64 c + 4 j < F
@@ -915,7 +935,8 @@ void launch_dropout_mask(uint64_t *states, long long n_chunks, long long elem0,
 bool dropout_mask_nib_ok(int F, long long mask_base) {
   if (F < 1 || F > 1024) return false;
   const int g = std::gcd(F, 64);
-  return (mask_base % g) == 0 && F / g <= DMN_MAX_CHUNKS && mask_base >= 0 && mask_base < 64;
+  return (mask_base % g) == 0 && F / g + 1 <= DMN_MAX_CHUNKS - 64 && mask_base >= 0 &&
+         mask_base < 64;
 }
 
 void launch_dropout_mask_nib(uint64_t *states, long long n_chunks, long long elem0,
@@ -927,7 +948,8 @@ void launch_dropout_mask_nib(uint64_t *states, long long n_chunks, long long ele
              "dropout_mask_nib: chunks must cover rows x F bits from mask_base");
   const int threshold = (int)(p * (float)0x7fffffff);  // hpdga module.cpp:211
   const int g = std::gcd(F, 64), r_unit = 64 / g, c_unit = F / g;  // rows / chunks per unit
-  const int units = std::max(1, std::min(DMN_MAX_CHUNKS / c_unit, 512 / c_unit));
+  // about 300 chunks per workgroup (two per thread), 8 KB of LUT + the words in LDS
+  const int units = std::max(1, std::min((DMN_MAX_CHUNKS - 64) / c_unit, 300 / c_unit));
   const int rows_per_wg = r_unit * units;
   // first interior cut: the smallest r > 0 with (mask_base + r F) = 0 mod 64
   int first = 0;
@@ -938,9 +960,11 @@ void launch_dropout_mask_nib(uint64_t *states, long long n_chunks, long long ele
     }
   PGCN_CHECK(first > 0, PGCN_E_INVALID, "dropout_mask_nib: no chunk-aligned row cut");
   const long long wgs = 1 + (rows > first ? ceil_div((long long)(rows - first), rows_per_wg) : 0);
-  // (the first workgroup can hold one chunk more; 2 more threads zero the words past it)
-  const int threads = (int)std::min<long long>(1024, ceil_div((long long)c_unit * units + 3, 64) * 64);
-  PGCN_LAUNCH(k_dropout_mask_nib, dim3((unsigned)wgs), dim3(threads), 0, s, states, n_chunks,
+  // (the first workgroup can hold one chunk more than a unit's; two chunks per thread)
+  const long long max_nc = std::max<long long>((long long)c_unit * units, c_unit + 1);
+  const int threads = (int)std::min<long long>(1024, ceil_div(ceil_div(max_nc, 2), 64) * 64);
+  const size_t words_bytes = (size_t)(max_nc + 2) * sizeof(uint64_t);
+  PGCN_LAUNCH(k_dropout_mask_nib, dim3((unsigned)wgs), dim3(threads), words_bytes, s, states, n_chunks,
               elem0, elem_end, threshold, mask, static_cast<const uint4 *>(table), mask_base, F,
               rows, rows_per_wg, first, nib);
 }

@@ -22,6 +22,10 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 import helpers  # noqa: E402
 
 pg = helpers.pgcn()
+# RANK_KNOBS="rs_chunks=1,...": engine knobs for every engine built here
+for kv in filter(None, os.environ.get("RANK_KNOBS", "").split(",")):
+    k, v = kv.split("=")
+    pg.check(pg.lib.pgcn_debug_set(k.encode(), int(v)), "knob " + k)
 worlds = [int(w) for w in (sys.argv[1] if len(sys.argv) > 1 else "1,2,4,8").split(",")]
 ranks = [int(r) for r in (sys.argv[2] if len(sys.argv) > 2 else "0").split(",")]
 hidden = tuple(int(h) for h in (sys.argv[3] if len(sys.argv) > 3 else "16").split(","))
