@@ -378,6 +378,19 @@ void GraphSum::run(const float *src, float *dst, const Stream &s, int mode,
     cgs[0]->graphsum(src, in->ld, dst, out->ld, dim, s.get(), false, epi, prestaged);
     bytes = cgs[0]->algorithmic_bytes(dim);
     if (ctx->profile) e1.record(s.get());
+  } else if (ctx->comm && partial.empty()) {
+    // one rank, the split's rows only (split_rows): their sums scattered straight into `out`
+    // (the other rows keep their last values, as the partials' do at world > 1)
+    DevGraph *sk = ctx->chunk_split_graphs[0];
+    if (sk->rows() > 0) {
+      const size_t need = (size_t)sk->rows() * out->ld;
+      if (compact.size() < need) compact.allocate(need);
+      sk->graphsum(src, in->ld, compact.get(), out->ld, dim, s.get());
+      launch_scatter_rows(compact.get(), ctx->chunk_split_rows[0], sk->rows(), out->ld, dst,
+                          s.get());
+      bytes = sk->algorithmic_bytes(dim);
+    }
+    if (ctx->profile) e1.record(s.get());
   } else if (ctx->comm) {
     // Per row chunk: partial sums of the chunk's (padded) rows from this rank's columns on
     // the compute stream, then its reduce-scatter on the comm stream, which hands every rank
