@@ -304,7 +304,7 @@ int pgcn_debug_rank_graph(int n, const int *indptr, const int *indices, int worl
  *   "fuse_output" 0..3 (default 2), "xstream_ring" 0/1, "lds_min_kb" (< 0: default),
  *   "lds_blocks" 0 (by shape) or 1..32, "parse_threads" (0: up to 16), "wide_prescale" 0/1
  *   (a multi-pass GraphSum's tables prescaled by one launch, default 1), "rs_chunks" 1..4
- *   (edge-cut GraphSum row chunks at world > 1, default 2), "mask_nib" 0/1 (dense X's input
+ *   (edge-cut GraphSum row chunks at world > 1, default 1), "mask_nib" 0/1 (dense X's input
  *   dropout drawn into the flat bitmap and the GEMMs' nibble layout by one launch, default 1);
  * diagnostics: "split_rows" 0/1 (stale logits outside the split), "gemm_variant" 0/1 (the
  * general GEMM kernels only).  Returns PGCN_E_INVALID on an unknown key or on a value outside

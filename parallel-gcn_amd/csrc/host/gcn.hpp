@@ -19,9 +19,13 @@
 
 namespace pgcn {
 
-// GraphSum row chunks of the edge-cut engine: chunk k's reduce-scatter overlaps chunk k+1's
-// local sum (2: the LDS schedule keeps >= 1 workgroup per CU at 2 GPUs).
-constexpr int kRsChunks = 2;
+// GraphSum row chunks of the edge-cut engine at world > 1 (knob rs_chunks): chunk k's
+// reduce-scatter overlaps chunk k+1's local sum.  1 by default (r04, reddit-114M, one rank's
+// GraphSum timed on one GPU: 58.7 us at world 8 for the whole column block against 81.3 us
+// for two row chunks, whose 30 rowset batches leave half the CUs idle; a 13 MB exchange at
+// 300 GB/s then fits in the 22.6 us the second chunk would have hidden, and above that rate
+// one chunk is ahead; profiles/r04/rank_graphsum_c1.json, rank_graphsum_c2.json)
+constexpr int kRsChunks = 1;
 extern int g_rs_chunks;
 
 struct GCNParams {

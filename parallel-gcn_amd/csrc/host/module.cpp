@@ -418,13 +418,21 @@ void GraphSum::run(const float *src, float *dst, const Stream &s, int mode,
                      k == 0 && prestaged, shared);
         bytes += gk->algorithmic_bytes(dim);
       }
+      if (ctx->chunk_graphs.size() == 1) {
+        // one chunk: nothing to overlap -- the reduce-scatter follows on the compute stream
+        // (two cross-stream hand-offs per GraphSum cost ~10 us each on the rank epoch)
+        ctx->comm->reduce_scatter_sum(partial[k].get(), dst, h * out->ld, s.get());
+        continue;
+      }
       computed[k].record(s.get());
       computed[k].wait_on(ctx->comm_stream);
       ctx->comm->reduce_scatter_sum(partial[k].get(), dst + k * h * out->ld, h * out->ld,
                                     ctx->comm_stream);
     }
-    reduced.record(ctx->comm_stream);
-    reduced.wait_on(s.get());  // dst complete, partials free for the next call
+    if (ctx->chunk_graphs.size() > 1) {
+      reduced.record(ctx->comm_stream);
+      reduced.wait_on(s.get());  // dst complete, partials free for the next call
+    }
     // the fused tail on this rank's rows of the summed output (padding rows stay zero)
     if (epi && epi->mode) launch_gs_finish(dst, out->ld, ctx->local_rows, dim, *epi, s.get());
     if (ctx->profile) e1.record(s.get());

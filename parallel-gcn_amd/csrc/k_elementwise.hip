@@ -430,12 +430,14 @@ __global__ void k_exp_check(const float *__restrict__ x, long long n, float *__r
 
 // a / b rounded to nearest from rb = RN(1 / b) (Markstein: q within an ulp, the residual exact
 // by fma, one correction step): the IEEE quotient's bits for normal operands and results.
-// The loss kernel divides a in [0, 1] by b >= 1: q below 2^-125 (subnormal results, or the
-// residual no longer exact) takes the IEEE division itself; tests/test_gpu_kernels.py
-// test_div_rn_matches_ieee checks the bits over dense a (subnormals included) and b in [1, 128]
+// The residual r = a - q b is exact only while its lowest bit (ulp(q) ulp(b) = 2^(e_q - 46))
+// is representable, i.e. q >= 2^-103: below 2^-100 (r03's form missed bits for quotients up to
+// 3e-38, the advisor's case) the loss kernel takes the IEEE division itself;
+// tests/test_gpu_kernels.py test_div_rn_matches_ieee checks the bits over dense a (subnormals
+// included) and b in [1, 128]
 __device__ __forceinline__ float div_rn(float a, float b, float rb) {
   const float q = a * rb;
-  if (__builtin_expect(fabsf(q) < 0x1p-125f, 0)) return a / b;
+  if (__builtin_expect(fabsf(q) < 0x1p-100f, 0)) return a / b;
   const float r = fmaf(-q, b, a);
   return fmaf(r, rb, q);
 }
@@ -948,8 +950,8 @@ void launch_dropout_mask_nib(uint64_t *states, long long n_chunks, long long ele
              "dropout_mask_nib: chunks must cover rows x F bits from mask_base");
   const int threshold = (int)(p * (float)0x7fffffff);  // hpdga module.cpp:211
   const int g = std::gcd(F, 64), r_unit = 64 / g, c_unit = F / g;  // rows / chunks per unit
-  // about 300 chunks per workgroup (two per thread), 8 KB of LUT + the words in LDS
-  const int units = std::max(1, std::min((DMN_MAX_CHUNKS - 64) / c_unit, 300 / c_unit));
+  // about 600 chunks per workgroup (two per thread), 8 KB of LUT + the words in LDS
+  const int units = std::max(1, std::min((DMN_MAX_CHUNKS - 64) / c_unit, 640 / c_unit));
   const int rows_per_wg = r_unit * units;
   // first interior cut: the smallest r > 0 with (mask_base + r F) = 0 mod 64
   int first = 0;

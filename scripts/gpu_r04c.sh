@@ -1,0 +1,25 @@
+#!/bin/bash
+# r04 box 3: full GPU suite, A/B of the fused input-dropout kernel (wider workgroups), the
+# edge-cut rank epochs with the one-chunk same-stream reduce-scatter, the W = 8 rank trace.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+O=gpurun_out/r04c
+mkdir -p $O
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc"; grep -E "FAILED|ERROR" $O/pytest.log | head; tail -2 $O/pytest.log
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+for i in 1 2 3; do
+  for v in 1 0; do
+    timeout -k 10 300 python3 bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-extra --knob mask_nib=$v \
+        > $O/ab_nib${v}_$i.json 2> $O/ab_nib${v}_$i.err || exit $?
+    python3 -c "import json;d=json.load(open('$O/ab_nib${v}_$i.json'));print('mask_nib=$v', round(d['value'],1), round(d['value_unamortised'],1))"
+  done
+done
+timeout -k 10 300 python3 tools/rank_epoch.py 1,2,4,8 0 16 > $O/rank_epoch.json 2> $O/rank_epoch.err || exit $?
+cat $O/rank_epoch.json
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_rank8 -o run -f csv -- \
+    python3 tools/rank_epoch.py 8 0 16 > $O/prof_rank8.log 2>&1; echo "rank8 trace rc=$?"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o run -f csv -- \
+    python3 bench.py --profile-only --steps 5 --warmup 1 > $O/trace.log 2>&1; echo "trace rc=$?"
+python3 tools/epoch_breakdown.py $O/trace > $O/breakdown.txt 2>&1; head -14 $O/breakdown.txt

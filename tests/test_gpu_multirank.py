@@ -79,10 +79,15 @@ def big_oracle(big_ds):
     return [r[0] for r in runs], [r[1] for r in runs], test, {1: tt, 2: tt}
 
 
-@pytest.mark.parametrize("world,split_rows,lds", [(2, 0, 1), (2, 1, 1), (4, 0, 1), (8, 0, 1),
-                                                   (4, 0, 0)])
-def test_loopback_lds_graph_matches_oracle(pgcn, big_ds, big_oracle, world, split_rows, lds):
-    with helpers.knobs(pgcn, split_rows=split_rows, lds_min_kb=-1 if lds else 1 << 20):
+@pytest.mark.parametrize("world,split_rows,lds,chunks", [(2, 0, 1, 1), (2, 1, 1, 1), (4, 0, 1, 1),
+                                                          (8, 0, 1, 1), (4, 0, 0, 1), (2, 0, 1, 2),
+                                                          (4, 1, 1, 2), (8, 0, 1, 2)])
+def test_loopback_lds_graph_matches_oracle(pgcn, big_ds, big_oracle, world, split_rows, lds,
+                                           chunks):
+    """chunks: GraphSum row chunks (rs_chunks; 2 = each chunk's reduce-scatter on the comm
+    stream while the next chunk is summed)."""
+    with helpers.knobs(pgcn, split_rows=split_rows, lds_min_kb=-1 if lds else 1 << 20,
+                       rs_chunks=chunks):
         res = _run_world(pgcn, big_ds, world, 4)
     _check_ranks(res, world, big_ds.num_nodes)
     assert res[0]["info"]["graphsum_lds"] == lds
