@@ -9,10 +9,15 @@ timeout -k 10 900 python3 -u -m pytest tests -m gpu -v --timeout 300 --timeout-m
 rc=$?; echo "pytest rc=$rc"; grep -E "FAILED|ERROR" $O/pytest.log | head; tail -2 $O/pytest.log
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 for i in 1 2 3; do
-  for v in 1 0; do
-    timeout -k 10 300 python3 bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-extra --knob mask_nib=$v \
-        > $O/ab_nib${v}_$i.json 2> $O/ab_nib${v}_$i.err || exit $?
-    python3 -c "import json;d=json.load(open('$O/ab_nib${v}_$i.json'));print('mask_nib=$v', round(d['value'],1), round(d['value_unamortised'],1))"
+  for arm in nib0 nib1 old; do
+    case $arm in
+      nib0) env=""; k="--knob mask_nib=0" ;;
+      nib1) env=""; k="--knob mask_nib=1" ;;
+      old) env="PGCN_LIB=parallel-gcn_amd/ab_noxor3/libpgcn.so"; k="--knob mask_nib=0" ;;
+    esac
+    env $env timeout -k 10 300 python3 bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-extra $k \
+        > $O/ab_${arm}_$i.json 2> $O/ab_${arm}_$i.err || exit $?
+    python3 -c "import json;d=json.load(open('$O/ab_${arm}_$i.json'));print('$arm', round(d['value'],1), round(d['value_unamortised'],1))"
   done
 done
 timeout -k 10 300 python3 tools/rank_epoch.py 1,2,4,8 0 16 > $O/rank_epoch.json 2> $O/rank_epoch.err || exit $?
