@@ -342,9 +342,9 @@ int pgcn_xent_fwd(float *logits, int ld, float *grad, const int *truth, int n, i
 int pgcn_finalize(const float *partials, int n_blocks, int count, const float *w_l2,
                   long long n_l2, float weight_decay, float *out4, void *stream) {
   return guarded([&] {
-    // out4[0..1] = {loss, acc}; out4[2..3] hold the raw sums (loss_sum, wrong)
-    launch_reduce_scalars(partials, n_blocks, w_l2, n_l2, out4 + 2, as_stream(stream));
-    launch_compose(out4 + 2, count, weight_decay, out4, as_stream(stream));
+    // out4[0..1] = {loss, acc}; out4[2..3] hold the raw sums (loss_sum, wrong); one launch
+    launch_reduce_scalars(partials, n_blocks, w_l2, n_l2, out4 + 2, as_stream(stream), count,
+                          weight_decay, out4);
   });
 }
 

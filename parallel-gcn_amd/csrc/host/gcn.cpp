@@ -483,6 +483,10 @@ void GCN::build(const GCNData &data) {
   sums.allocate(4);
   results_ring.allocate((size_t)ring_cap * 4);
   results_ring.zero();
+  if (comm) {
+    raw_ring.allocate((size_t)ring_cap * 8);
+    raw_ring.zero();
+  }
   pinned = PinnedBuffer<float>(8);
   size_t ws = 0;
   for (int l = 0; l < L; l++)
@@ -751,15 +755,24 @@ void GCN::finalize(int dst_offset, bool graph) {
                           ring_cap);
     return;
   }
+  // edge-cut: {loss sum, wrong, sum W1^2, count} into the raw ring slot, the first two summed
+  // over the ranks in place; the host composes them when it reads the results (compose_raw:
+  // k_compose's arithmetic in the same float operations, the same bits)
+  PGCN_CHECK(!graph, PGCN_E_INVALID, "edge-cut epochs are not captured");
+  float *raw = raw_ring.get() + (size_t)dst_offset * 2;  // slot * 8 + pass * 4
   launch_reduce_scalars(xent_partials.get(), ctx.xent_blocks, w1->dev_data.get(), w1->size,
-                        sums.get(), stream.get());
-  if (comm) comm->allreduce_sum(sums.get(), 2, stream.get());
-  if (graph)
-    launch_compose(sums.get(), ctx.count, adam_params.weight_decay, results_ring.get() + dst_offset,
-                   stream.get(), dev_ctr.get(), ring_cap);
-  else
-    launch_compose(sums.get(), ctx.count, adam_params.weight_decay, results_ring.get() + dst_offset,
-                   stream.get());
+                        nullptr, stream.get(), ctx.count, 0.0f, nullptr, nullptr, 1, raw);
+  comm->allreduce_sum(raw, 2, stream.get());
+}
+
+// k_compose (hpdga gcn.cpp:167-198) on the host: {loss_sum/count + wd*l2/2, (count-wrong)/count}
+void GCN::compose_raw(const float *raw4, float *out2) const {
+  const int count = (int)raw4[3];
+  const float loss = raw4[0] / (float)count;
+  const float l2 = adam_params.weight_decay * raw4[2] / 2.0f;
+  out2[0] = loss + l2;
+  const int wrong = (int)raw4[1];
+  out2[1] = (float)(count - wrong) / (float)count;
 }
 
 // the weight gradients a Matmul::backward left on the side stream are complete on `stream`
@@ -868,7 +881,21 @@ std::pair<float, float> GCN::train_epoch() {
   optimizer.step(stream);
   ctr_valid = false;
   last_forward_training = true;
-  PGCN_HIP(hipMemcpyAsync(pinned.get(), results_ring.get() + slot * 4, 2 * sizeof(float),
+  return read_slot((int)(slot * 4));
+}
+
+// results_ring[off .. off + 1] (one GPU), or the host's composition of the raw ring's sums of
+// that pass (edge-cut)
+std::pair<float, float> GCN::read_slot(int off) {
+  if (comm) {
+    PGCN_HIP(hipMemcpyAsync(pinned.get(), raw_ring.get() + (size_t)off * 2, 4 * sizeof(float),
+                            hipMemcpyDeviceToHost, stream.get()));
+    stream.sync();
+    float r[2];
+    compose_raw(pinned.get(), r);
+    return {r[0], r[1]};
+  }
+  PGCN_HIP(hipMemcpyAsync(pinned.get(), results_ring.get() + off, 2 * sizeof(float),
                           hipMemcpyDeviceToHost, stream.get()));
   stream.sync();
   return {pinned.get()[0], pinned.get()[1]};
@@ -882,11 +909,9 @@ std::pair<float, float> GCN::eval(int split) {
   finalize((int)(slot * 4 + 2));
   last_forward_training = false;
   ctr_valid = false;
-  PGCN_HIP(hipMemcpyAsync(pinned.get(), results_ring.get() + slot * 4 + 2, 2 * sizeof(float),
-                          hipMemcpyDeviceToHost, stream.get()));
-  stream.sync();
+  const std::pair<float, float> r = read_slot((int)(slot * 4 + 2));
   if (split == 2) epoch_count++;  // a train_epoch + eval(2) pair fills one ring slot
-  return {pinned.get()[0], pinned.get()[1]};
+  return r;
 }
 
 void GCN::sync() {
@@ -897,7 +922,13 @@ void GCN::sync() {
 std::vector<float> GCN::results(int n) {
   sync();
   std::vector<float> all((size_t)ring_cap * 4);
-  results_ring.download(all.data(), all.size());
+  if (comm) {
+    std::vector<float> raw((size_t)ring_cap * 8);
+    raw_ring.download(raw.data(), raw.size());
+    for (int k = 0; k < ring_cap * 2; k++) compose_raw(&raw[(size_t)k * 4], &all[(size_t)k * 2]);
+  } else {
+    results_ring.download(all.data(), all.size());
+  }
   n = (int)std::min<long long>(n, std::min<long long>(epoch_count, ring_cap));
   std::vector<float> out((size_t)n * 4);
   for (int k = 0; k < n; k++) {

@@ -176,6 +176,11 @@ class GCN {
   DeviceBuffer<uint8_t> jump_table;
   DeviceBuffer<float> gemm_ws, gemm_ws_side;
   DeviceBuffer<float> xent_partials, sums, results_ring;
+  // edge-cut: per ring slot and pass, the all-reduced {loss sum, wrong, sum W1^2, count}; the
+  // host composes loss and accuracy from them (compose_raw), so a pass needs no compose launch
+  DeviceBuffer<float> raw_ring;
+  void compose_raw(const float *raw4, float *out2) const;
+  std::pair<float, float> read_slot(int off);
   PinnedBuffer<float> pinned;
   int ring_cap = 1024;
   long long epoch_count = 0;

@@ -831,7 +831,7 @@ __global__ __launch_bounds__(1024) void k_reduce_scalars(const float *__restrict
                                                          int count, float wd,
                                                          float *__restrict__ out2,
                                                          const int *__restrict__ ctr,
-                                                         int ring_cap) {
+                                                         int ring_cap, float *__restrict__ raw4) {
   __shared__ float red[16];
   float l = 0.0f, wr = 0.0f, q = 0.0f;
   // a thread's elements b = tid + 1024 u in u order, 8 loads in flight before their adds (r03
@@ -862,28 +862,21 @@ __global__ __launch_bounds__(1024) void k_reduce_scalars(const float *__restrict
   wr = block_sum<1024>(wr, red);
   q = block_sum<1024>(q, red);
   if (threadIdx.x == 0) {
-    sums[0] = l;
-    sums[1] = wr;
-    sums[2] = q;
+    if (sums) {
+      sums[0] = l;
+      sums[1] = wr;
+    }
+    if (raw4) {  // edge-cut: all-reduced in place, then composed by the host
+      raw4[0] = l;
+      raw4[1] = wr;
+      raw4[2] = q;
+      raw4[3] = (float)count;
+    }
     if (out2) {  // one GPU: k_compose's arithmetic here, no second launch
       if (ctr) out2 += 4 * (ctr[1] % ring_cap);
       out2[0] = l / (float)count + wd * q / 2.0f;
       out2[1] = (float)(count - (int)wr) / (float)count;
     }
-  }
-}
-
-// out2 = {loss_sum/count + wd*l2/2, (count-wrong)/count}   (hpdga gcn.cpp:167-198)
-__global__ void k_compose(const float *__restrict__ sums, int count, float wd,
-                          float *__restrict__ out2, const int *__restrict__ ctr, int ring_cap) {
-  if (threadIdx.x == 0) {
-    // epoch graphs: the results-ring slot from the device epoch counter (ctr[1])
-    if (ctr) out2 += 4 * (ctr[1] % ring_cap);
-    const float loss = sums[0] / (float)count;
-    const float l2 = wd * sums[2] / 2.0f;
-    out2[0] = loss + l2;
-    const int wrong = (int)sums[1];
-    out2[1] = (float)(count - wrong) / (float)count;
   }
 }
 
@@ -1051,14 +1044,9 @@ void launch_out_xent(const float *H, int ldh, int kh, const float *W, int ldw, f
 
 void launch_reduce_scalars(const float *partials, int n_blocks, const float *w, long long n_w,
                            float *sums, hipStream_t s, int count, float wd, float *out2,
-                           const int *ctr, int ring_cap) {
+                           const int *ctr, int ring_cap, float *raw4) {
   PGCN_LAUNCH(k_reduce_scalars, dim3(1), dim3(1024), 0, s, partials, n_blocks, w, n_w,
-                     sums, count, wd, out2, ctr, ring_cap);
-}
-
-void launch_compose(const float *sums, int count, float wd, float *out2, hipStream_t s,
-                    const int *ctr, int ring_cap) {
-  PGCN_LAUNCH(k_compose, dim3(1), dim3(64), 0, s, sums, count, wd, out2, ctr, ring_cap);
+                     sums, count, wd, out2, ctr, ring_cap, raw4);
 }
 
 // epoch graphs: the device copy of the host's (Adam step, epoch) counters

@@ -222,12 +222,13 @@ void launch_tn_reduce_blocks(float *partial, int n_blocks, int K, int N, int ldp
 size_t tn_reduce_blocks_workspace(int n_blocks, int K, int ldp);
 void launch_xent_fwd(float *logits, int ld, float *grad, const int *truth, int n, int c,
                      int count, int training, float *partials, hipStream_t s, int write_back = 1);
+// sums (optional): {loss sum, wrong}; out2 (optional): the composed {loss + l2, accuracy};
+// raw4 (optional): {loss sum, wrong, sum w^2, count} for a composition after an all-reduce
 void launch_reduce_scalars(const float *partials, int n_blocks, const float *w, long long n_w,
                            float *sums, hipStream_t s, int count = 0, float wd = 0.0f,
-                           float *out2 = nullptr, const int *ctr = nullptr, int ring_cap = 1);
-// ctr (epoch graphs, device {Adam step, epoch} counters): slot 4 * (ctr[1] % ring_cap) of out2
-void launch_compose(const float *sums, int count, float wd, float *out2, hipStream_t s,
-                    const int *ctr = nullptr, int ring_cap = 1);
+                           float *out2 = nullptr, const int *ctr = nullptr, int ring_cap = 1,
+                           float *raw4 = nullptr);
+// ctr (epoch graphs, device {Adam step, epoch} counters): out2 is slot 4 * (ctr[1] % ring_cap)
 // step_table (epoch graphs): step_size = step_table[ctr[0] % table_cap]
 void launch_adam(float *w, const float *g, float *m, float *v, long long n, float step_size,
                  float beta1, float beta2, float eps, float wd, int decay, hipStream_t s,
