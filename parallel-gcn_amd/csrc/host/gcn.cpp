@@ -41,7 +41,7 @@ int g_fuse_epilogue = kFuseTails | kFusePrestage | kFuseXstream;
 // Matmul forward and input grad run inside the loss (launch_out_xent) when the Matmul produces
 // the logits (the reassociated order: GraphSum, then Matmul) from at most 16 columns
 // (bit-identical); 2 (default) = ... and its weight grad's block partials on graphs of >=
-// 65,536 rows (the same sums in another grouping); 3 = ... on any graph
+// 65,536 rows or on an edge-cut rank (the same sums in another grouping); 3 = ... on any graph
 int g_fuse_output = 2;
 // "mm_side" (read at engine build): Matmul weight gradients on the side stream (ModuleContext)
 // on graphs of at least kMmSideRows rows; 2 = on every graph.  Off: r02 A/B on reddit-114M,

@@ -631,7 +631,9 @@ void CrossEntropyLoss::forward(bool training, const Stream &s) const {
     float *dH = Hv.dev_grad ? Hv.dev_grad.get() : nullptr;
     const int nb = xent_blocks(logits->rows);
     float *dWp = nullptr;
-    if (training && g_fuse_output >= 2 && (g_fuse_output == 3 || logits->rows >= 65536) &&
+    // (an edge-cut rank's rows are a slice of a large graph: the block partials too)
+    if (training && g_fuse_output >= 2 &&
+        (g_fuse_output == 3 || logits->rows >= 65536 || ctx->comm) &&
         Wv.dev_grad && logits->ld <= 48 &&
         !ctx->mm_side &&
         tn_reduce_blocks_workspace(nb, fused->inner(), 48) <= ctx->gemm_workspace_bytes)

@@ -22,6 +22,8 @@ for i in 1 2 3; do
 done
 timeout -k 10 300 python3 tools/rank_epoch.py 1,2,4,8 0 16 > $O/rank_epoch.json 2> $O/rank_epoch.err || exit $?
 cat $O/rank_epoch.json
+RANK_KNOBS=xstream_ring=0 timeout -k 10 300 python3 tools/rank_epoch.py 8 0 16 > $O/rank_epoch_xs0.json 2> $O/rank_epoch_xs0.err || exit $?
+echo "xstream_ring=0"; cat $O/rank_epoch_xs0.json
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_rank8 -o run -f csv -- \
     python3 tools/rank_epoch.py 8 0 16 > $O/prof_rank8.log 2>&1; echo "rank8 trace rc=$?"
