@@ -36,7 +36,25 @@ __global__ __launch_bounds__(256) void k_spmm_csr(int m, int p, int ldc,
   const int k = (int)(t - i * p);
   if (i >= m) return;
   float sum = 0.0f;
-  for (int jj = indptr[i]; jj < indptr[i + 1]; jj++) {
+  int jj = indptr[i];
+  const int je = indptr[i + 1];
+  // r04: 8 nonzeros' index / value / mask loads issued together, then their B gathers, then
+  // the adds in CSR order (one dependent load chain per 8 nonzeros instead of per nonzero;
+  // the same products and the same order: the same bits)
+  for (; jj + 8 <= je; jj += 8) {
+    int ix[8];
+    float av[8], bv[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      ix[u] = indices[jj + u];
+      av[u] = drop_val(a[jj + u], mask, mask_base + jj + u, scale);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) bv[u] = b[(long long)ix[u] * p + k];
+#pragma unroll
+    for (int u = 0; u < 8; u++) sum += av[u] * bv[u];
+  }
+  for (; jj < je; jj++) {
     const float av = drop_val(a[jj], mask, mask_base + jj, scale);
     sum += av * b[(long long)indices[jj] * p + k];
   }
@@ -86,8 +104,17 @@ __global__ __launch_bounds__(kCscChunk) void k_spmm_csc_bwd(int nf, int p, int l
     }
     __syncthreads();
     if (tid < 16) {
+      // (r04: 32 LDS reads in flight per wait, was 8: the serial add chain of a long column
+      // no longer waits on the LDS between every 8 adds)
       const int n = min(kCscChunk, e1 - base);
       int j = 0;
+      for (; j + 32 <= n; j += 32) {
+        float v[32];
+#pragma unroll
+        for (int u = 0; u < 32; u++) v[u] = prod[j + u][tid];
+#pragma unroll
+        for (int u = 0; u < 32; u++) sum += v[u];
+      }
       for (; j + 8 <= n; j += 8) {
         float v[8];
 #pragma unroll

@@ -28,5 +28,7 @@ cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_rank8 -o run -f csv -- \
     python3 tools/rank_epoch.py 8 0 16 > $O/prof_rank8.log 2>&1; echo "rank8 trace rc=$?"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o run -f csv -- \
-    python3 bench.py --profile-only --steps 5 --warmup 1 > $O/trace.log 2>&1; echo "trace rc=$?"
+    python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-extra > $O/trace_bench.json 2> $O/trace.log
+echo "trace rc=$?"
 python3 tools/epoch_breakdown.py $O/trace > $O/breakdown.txt 2>&1; head -14 $O/breakdown.txt
+python3 tools/gs_fraction.py $O/trace $O/trace_bench.json > $O/gs_fraction.json; cat $O/gs_fraction.json
