@@ -31,9 +31,6 @@ namespace pgcn {
 #ifndef PGCN_DROP_SHIFTIN
 #define PGCN_DROP_SHIFTIN 1
 #endif
-#ifndef PGCN_DROP_XOR3
-#define PGCN_DROP_XOR3 1
-#endif
 struct Xs64 {
   uint64_t s0, s1;
   uint32_t lo = 0, hi = 0;  // mask bits 0-31 / 32-63 (constant shifts: the loop is unrolled)
@@ -43,25 +40,8 @@ struct Xs64 {
     const uint64_t u = s1;
     s0 = u;
     t ^= t << 23;
-#if PGCN_DROP_XOR3
-    // t ^ (t >> 17) ^ u ^ (u >> 26) per 32-bit half: one gfx950 v_bitop3_b32 (truth table
-    // 0x96: a ^ b ^ c) and a v_xor_b32 each (the compiler's form takes three xors per half);
-    // the same bits
-    uint64_t a, b;  // t >> 17, u >> 26 as single 64-bit shifts (not alignbit + shift pairs)
-    asm("v_lshrrev_b64 %0, 17, %1" : "=v"(a) : "v"(t));
-    asm("v_lshrrev_b64 %0, 26, %1" : "=v"(b) : "v"(u));
-    uint32_t tl, th;  // (not lo / hi: those are the mask-bit members)
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96"
-        : "=v"(tl)
-        : "v"((uint32_t)t), "v"((uint32_t)a), "v"((uint32_t)u));
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96"
-        : "=v"(th)
-        : "v"((uint32_t)(t >> 32)), "v"((uint32_t)(a >> 32)), "v"((uint32_t)(u >> 32)));
-    t = ((uint64_t)(th ^ (uint32_t)(b >> 32)) << 32) | (tl ^ (uint32_t)b);
-#else
     t ^= t >> 17;
     t ^= u ^ (u >> 26);
-#endif
     s1 = t;
 #if PGCN_DROP_SHIFTIN
     // keep = ((t + u) & 0x7fffffff) >= threshold, compared as ((t + u) << 1) >= (threshold << 1)

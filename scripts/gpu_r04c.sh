@@ -32,3 +32,8 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o run -f csv -- 
 echo "trace rc=$?"
 python3 tools/epoch_breakdown.py $O/trace > $O/breakdown.txt 2>&1; head -14 $O/breakdown.txt
 python3 tools/gs_fraction.py $O/trace $O/trace_bench.json > $O/gs_fraction.json; cat $O/gs_fraction.json
+timeout -k 10 400 python3 tools/datasets_bench.py --epochs 300 --graph 0 --out $O/datasets.json > $O/datasets.log 2>&1
+echo "datasets rc=$?"; python3 -c "
+import json; d=json.load(open('$O/datasets.json'))
+for k,v in d.items():
+    if isinstance(v, dict): print(k, round(v.get('eager_async_epochs_s',0),1), round(v.get('eager_frac_of_launch_floor',0),3))"

@@ -118,8 +118,9 @@ def deep_ds(pgcn):
 def deep_oracle(deep_ds):
     ref = helpers.OracleGCN(helpers.ds_dict(deep_ds), hidden_dims=DEEP_DIMS, dropouts=DEEP_DROPS)
     c = deep_ds.output_dim
-    runs = [ref.epoch_with_ties(deep_ds.label, deep_ds.split, c) for _ in range(2)]
-    test, tt = ref.eval_with_ties(3, deep_ds.label, deep_ds.split, c)
+    tol = helpers.DEEP_TIE_TOL
+    runs = [ref.epoch_with_ties(deep_ds.label, deep_ds.split, c, tol) for _ in range(2)]
+    test, tt = ref.eval_with_ties(3, deep_ds.label, deep_ds.split, c, tol)
     return [r[0] for r in runs], [r[1] for r in runs], test, {1: tt, 2: tt}
 
 
@@ -210,7 +211,8 @@ def test_loopback_deep_reddit_width_matches_oracle(pgcn):
     ref = helpers.OracleGCN(helpers.ds_dict(ds), hidden_dims=dims, dropouts=drops)
     cnt = helpers.split_counts(ds)
     for e in range(2):
-        want, ties = ref.epoch_with_ties(ds.label, ds.split, ds.output_dim)
+        want, ties = ref.epoch_with_ties(ds.label, ds.split, ds.output_dim,
+                                         helpers.DEEP_TIE_TOL)
         helpers.assert_line_close(res[0]["lines"][e], want, cnt, what=f"epoch {e + 1}", ties=ties)
     for r, x in enumerate(res):
         q = x["paths"]

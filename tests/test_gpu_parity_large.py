@@ -105,7 +105,8 @@ def test_deep_wide_lds_graph_matches_oracle(pgcn):
     ref = helpers.OracleGCN(helpers.ds_dict(ds), hidden_dims=dims, dropouts=drops)
     cnt = helpers.split_counts(ds)
     for e in range(2):
-        want, ties = ref.epoch_with_ties(ds.label, ds.split, ds.output_dim)
+        want, ties = ref.epoch_with_ties(ds.label, ds.split, ds.output_dim,
+                                         helpers.DEEP_TIE_TOL)
         helpers.assert_line_close(g.train_epoch() + g.eval(2), want, cnt, what=f"epoch {e + 1}",
                                   ties=ties)
     g.close()
@@ -174,7 +175,8 @@ def test_deep_reddit_width_matches_oracle(pgcn):
     ref = helpers.OracleGCN(helpers.ds_dict(ds), hidden_dims=dims, dropouts=drops)
     cnt = helpers.split_counts(ds)
     for e in range(2):
-        want, ties = ref.epoch_with_ties(ds.label, ds.split, ds.output_dim)
+        want, ties = ref.epoch_with_ties(ds.label, ds.split, ds.output_dim,
+                                         helpers.DEEP_TIE_TOL)
         helpers.assert_line_close(g.train_epoch() + g.eval(2), want, cnt, what=f"epoch {e + 1}",
                                   ties=ties)
     paths = pgcn.path_counts()
