@@ -302,7 +302,8 @@ int pgcn_debug_rank_graph(int n, const int *indptr, const int *indices, int worl
  *   "train_ahead" 0/1, "eval_ax" 0/1, "split_cols" 0/1, "epoch_graph" 0/1, "mm_side" 0/1/2,
  *   "fuse_epilogue" bits 1 tails | 2 prestaged tables | 4 X-stream epilogue (default 7),
  *   "fuse_output" 0..3 (default 2), "xstream_ring" 0/1, "lds_min_kb" (< 0: default),
- *   "lds_blocks" 0 (by shape) or 1..32, "parse_threads" (0: up to 16), "wide_prescale" 0/1
+ *   "lds_blocks" 0 (by shape) or 1..32, "lds_slots" 0 (by shape) / 8 / 16 (rowsets per summing
+ *   wave of the LDS schedule), "parse_threads" (0: up to 16), "wide_prescale" 0/1
  *   (a multi-pass GraphSum's tables prescaled by one launch, default 1), "rs_chunks" 1..4
  *   (edge-cut GraphSum row chunks at world > 1, default 1), "mask_nib" 0/1 (dense X's input
  *   dropout drawn into the flat bitmap and the GEMMs' nibble layout by one launch, default 1);

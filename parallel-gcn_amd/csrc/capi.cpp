@@ -30,6 +30,7 @@ extern int g_epoch_graph;           // host/gcn.cpp
 extern int g_wide_prescale;        // host/graph.cpp
 extern long long g_lds_min_bytes;   // host/graph.cpp
 extern int g_lds_blocks;            // host/graph.cpp
+extern int g_lds_slots;             // host/graph.cpp
 extern int g_xstream_ring;          // k_xstream_lds.hip
 extern int g_parse_threads;         // host/data.cpp: pieces of the parallel text parse
 
@@ -659,6 +660,9 @@ int pgcn_debug_set(const char *key, int value) {
         value != 32)
       return PGCN_E_INVALID;
     pgcn::g_lds_blocks = value;
+  } else if (!std::strcmp(key, "lds_slots")) {
+    if (value != 0 && !ring_slots_ok(value)) return PGCN_E_INVALID;
+    pgcn::g_lds_slots = value;
   } else if (!std::strcmp(key, "parse_threads")) {
     if (!in(0, 4096)) return PGCN_E_INVALID;
     pgcn::g_parse_threads = value;
@@ -690,14 +694,14 @@ long long pgcn_debug_lds_counts(int n_rows, int n_cols, const int *indptr, const
                PGCN_E_INVALID, "lds_counts args");
     std::vector<int> ip(indptr, indptr + n_rows + 1), ix(indices, indices + indptr[n_rows]);
     const std::vector<int> cut = ring_cuts(n_cols, ix, lds_blocks(n_rows, n_cols));
-    const LdsHost h = build_ring_host(n_rows, n_cols, ip, ix, cut);
+    const LdsHost h = build_ring_host(n_rows, n_cols, ip, ix, cut, lds_slots(n_rows, n_cols));
     n = (long long)h.counts.size();
     if (dst) std::copy(h.counts.begin(), h.counts.begin() + std::min(n, cap), dst);
     if (shape5) {
       shape5[0] = h.n_batches;
       shape5[1] = h.t_max;
       shape5[2] = LDS_CW;
-      shape5[3] = LDS_SLOTS;
+      shape5[3] = h.ns;
       shape5[4] = kRingWindow;
     }
   });
@@ -711,7 +715,7 @@ int pgcn_debug_lds_check(int n_rows, int n_cols, const int *indptr, const int *i
                PGCN_E_INVALID, "lds_check args");
     std::vector<int> ip(indptr, indptr + n_rows + 1), ix(indices, indices + indptr[n_rows]);
     const std::vector<int> cut = ring_cuts(n_cols, ix, lds_blocks(n_rows, n_cols));
-    const LdsHost h = build_ring_host(n_rows, n_cols, ip, ix, cut);
+    const LdsHost h = build_ring_host(n_rows, n_cols, ip, ix, cut, lds_slots(n_rows, n_cols));
     std::vector<float> in((size_t)n_cols);
     uint64_t st[2] = {12345, 67890};
     for (auto &x : in) x = (float)((double)(xs_next(st) & 0xffffff) / (double)0x1000000 - 0.5);

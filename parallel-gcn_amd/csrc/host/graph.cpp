@@ -346,15 +346,24 @@ void DevGraph::set_scales(std::vector<float> row_scale, std::vector<float> col_s
 // 256 workgroups, half the partials; the same kernel time, combine 18 -> 11 us), 8 for a small
 // row subset (its 256 workgroups then stream half the table each: val rows 0.11 vs 0.22 ms)
 int g_lds_blocks = 0;
+// "lds_slots": rowsets per summing wave of the LDS schedule, 0 = by shape (16), or 8 / 16
+int g_lds_slots = 0;
+
+int lds_slots(int n_rows, int n_cols) {
+  (void)n_rows;
+  (void)n_cols;
+  return g_lds_slots ? g_lds_slots : LDS_SLOTS;
+}
 
 int lds_blocks(int n_rows, int n_cols) {
   if (g_lds_blocks) return g_lds_blocks;
+  const long long cap = (long long)LDS_CW * lds_slots(n_rows, n_cols);
   if ((double)n_rows >= 0.9 * (double)n_cols) {
     // square-ish: 4 blocks, or 8 when the rowset batches fill the chip only then and every
     // block keeps >= 20 slices of 512 columns (r02, edge-cut chunk graphs of reddit-114M,
     // tools/rank_graphsum.py: 1 rank 0.336 vs 0.400 ms, 2 ranks 0.202 vs 0.223; 4 ranks
     // (14 slices per block at 8) 0.130 vs 0.125)
-    const long long nrs = ((long long)n_rows + 15) / 16, cap = (long long)LDS_CW * LDS_SLOTS;
+    const long long nrs = ((long long)n_rows + 15) / 16;
     const long long nb = std::max(1LL, (nrs + cap - 1) / cap);
     if (nb * 8 <= kCUs && n_cols / 8 >= 20 * RING_SR) return 8;
     return 4;
@@ -362,7 +371,7 @@ int lds_blocks(int n_rows, int n_cols) {
   // row subsets: 8 blocks, or more when few batches of rowsets would leave each workgroup a
   // long sweep over its block's slices with little work per slice (the validation rows: 7
   // batches -> 32 blocks, a quarter of the slices per workgroup)
-  const long long nrs = ((long long)n_rows + 15) / 16, cap = (long long)LDS_CW * LDS_SLOTS;
+  const long long nrs = ((long long)n_rows + 15) / 16;
   const long long nb = std::max(1LL, (nrs + cap - 1) / cap);
   int B = 8;
   while (B < 32 && nb * B * 2 <= kCUs) B *= 2;
@@ -389,7 +398,8 @@ std::vector<int> column_cuts(int n_cols, const std::vector<int> &indices, int n_
 void DevGraph::build_lds() {
   if (lds_cut_.empty()) lds_cut_ = ring_cuts(n_cols_, h_indices_, lds_blocks(n_rows_, n_cols_));
   auto L = std::make_unique<LdsSched>();
-  LdsHost h = build_ring_host(n_rows_, n_cols_, h_indptr_, h_indices_, lds_cut_);
+  LdsHost h = build_ring_host(n_rows_, n_cols_, h_indptr_, h_indices_, lds_cut_,
+                              lds_slots(n_rows_, n_cols_));
   // + 2 KB slack: ring refills read whole 512-B chunks (up to 3) past a wave's last block
   L->entries.allocate(h.entries.size() / 4 + 256);
   L->entries.upload(reinterpret_cast<const uint2 *>(h.entries.data()), h.entries.size() / 4);
@@ -412,6 +422,7 @@ void DevGraph::build_lds() {
   if (!table_owner_) L->scratch.allocate((size_t)ceil_div(n_cols_, RING_SR) * RING_SR * 16);
   L->partial.allocate((size_t)h.n_blocks * n_rows_ * 16);
   L->s.n_blocks = h.n_blocks;
+  L->s.ns = h.ns;
   L->s.n_rows = n_rows_;
   L->s.n_cols = n_cols_;
   L->s.n_batches = h.n_batches;

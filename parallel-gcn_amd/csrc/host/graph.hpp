@@ -42,25 +42,28 @@ std::vector<float> degree_scales(int n, const int *indptr);
 
 // Host image of the d = 16 LDS ring schedule (k_graphsum_ring.hip), before upload.
 struct LdsHost {
-  int n_batches = 0, t_max = 0, n_blocks = 4;
+  int n_batches = 0, t_max = 0, n_blocks = 4, ns = LDS_SLOTS;
   std::vector<int> nsl;                 // slices per column block
   std::vector<int2> slices;             // [block][t_max] {first column, rows}
-  std::vector<int> rows;                // [batch][LDS_CW][LDS_SLOTS][16] row | spread
-  std::vector<unsigned short> counts;   // [wg][t_max][LDS_CW][LDS_SLOTS]
+  std::vector<int> rows;                // [batch][LDS_CW][ns][16] row | spread
+  std::vector<unsigned short> counts;   // [wg][t_max][LDS_CW][ns]
   std::vector<long long> wave_off;      // [wg*LDS_CW + 1] entry-block offsets
   std::vector<unsigned short> entries;  // [kb][16 groups][4 steps] ring-row byte offsets
 };
 // nnz-balanced column cuts (kGraphBlocks + 1 boundaries)
 std::vector<int> column_cuts(int n_cols, const std::vector<int> &indices,
                              int n_blocks = kGraphBlocks);
-// column blocks of the LDS GraphSum schedule of an n_rows x n_cols graph (XCD-affine)
+// column blocks of the LDS GraphSum schedule of an n_rows x n_cols graph (XCD-affine), and
+// its rowsets per summing wave (ring_slots_ok; knob "lds_slots")
 int lds_blocks(int n_rows, int n_cols);
+int lds_slots(int n_rows, int n_cols);
 // ring schedule (host/ring.cpp): block cuts on RING_SR multiples, the schedule, and its CPU
 // walk as the kernel consumes it: out[row] += sum of in[col] (throws on an inconsistent
 // schedule)
 std::vector<int> ring_cuts(int n_cols, const std::vector<int> &indices, int n_blocks);
 LdsHost build_ring_host(int n_rows, int n_cols, const std::vector<int> &indptr,
-                        const std::vector<int> &indices, const std::vector<int> &bcut);
+                        const std::vector<int> &indices, const std::vector<int> &bcut,
+                        int ns = LDS_SLOTS);
 void ring_emulate(const LdsHost &h, int n_rows, const float *in, double *out);
 
 class DevGraph {

@@ -79,10 +79,11 @@ std::vector<int> ring_cuts(int n_cols, const std::vector<int> &indices, int n_bl
 }
 
 LdsHost build_ring_host(int n_rows, int n_cols, const std::vector<int> &indptr,
-                        const std::vector<int> &indices, const std::vector<int> &bcut) {
+                        const std::vector<int> &indices, const std::vector<int> &bcut, int ns) {
   (void)n_cols;
   const int B = (int)bcut.size() - 1, SR = RING_SR, W = RING_W, K = RING_K;
-  const int CW = LDS_CW, NS = LDS_SLOTS;
+  const int CW = LDS_CW, NS = ns;
+  PGCN_CHECK(ring_slots_ok(ns), PGCN_E_INVALID, "graphsum_ring: rowsets per wave");
   PGCN_CHECK(B >= 1 && kCUs % B == 0, PGCN_E_INVALID, "graphsum_ring: column blocks");
   for (int b = 0; b < B; b++)
     PGCN_CHECK(bcut[(size_t)b] % SR == 0, PGCN_E_INVALID, "graphsum_ring: block cut alignment");
@@ -366,6 +367,7 @@ LdsHost build_ring_host(int n_rows, int n_cols, const std::vector<int> &indptr,
       }
   }, 0, 2);
   LdsHost h;
+  h.ns = NS;
   h.n_blocks = B;
   h.n_batches = nbat;
   h.t_max = t_max;
@@ -382,7 +384,7 @@ LdsHost build_ring_host(int n_rows, int n_cols, const std::vector<int> &indptr,
 // (ring buffer t % 4 holds slice t), entry blocks in wave order, zero rows; adds each row's
 // sum of in[col] into out[row].  Throws on anything the kernel would turn into a wrong sum.
 void ring_emulate(const LdsHost &h, int n_rows, const float *in, double *out) {
-  const int B = h.n_blocks, CW = LDS_CW, NS = LDS_SLOTS, SR = RING_SR, K = RING_K, W = RING_W;
+  const int B = h.n_blocks, CW = LDS_CW, NS = h.ns, SR = RING_SR, K = RING_K, W = RING_W;
   const long long n_wg = (long long)h.n_batches * B;
   std::vector<double> acc((size_t)NS * 16);
   for (long long wg = 0; wg < n_wg; wg++) {

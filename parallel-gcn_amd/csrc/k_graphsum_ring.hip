@@ -27,13 +27,13 @@ namespace pgcn {
 
 constexpr int RING_PLANE_B = RING_P * 16;                   // 32,832 B per quarter plane
 constexpr int RING_TABLE_B = 4 * RING_PLANE_B;              // 131,328 B
-constexpr int RING_CNT_USED = LDS_CW * LDS_SLOTS * 2;       // 480 B of counts per visit
+constexpr int RING_CNT_USED = LDS_CW * LDS_SLOTS * 2;       // <= 480 B of counts per visit
 constexpr int RING_CNT_B = 512;
 // counts buffers: visit v's counts land with slice v + W - 1, up to K - W visits ahead of the
 // slowest wave's visit
 constexpr int RING_NCB = RING_K - RING_W + 1;
 constexpr int RING_CNT_OFF = RING_TABLE_B;
-// loaded, done[K] in the tail of counts buffer 0
+// loaded, done[K] in the tail of counts buffer 0 (past the largest counts block)
 constexpr int RING_FLAG_OFF = RING_CNT_OFF + RING_CNT_USED;
 constexpr int RING_NFLAGS = 1 + RING_K;
 constexpr int RING_ERING_OFF = RING_CNT_OFF + RING_NCB * RING_CNT_B;
@@ -155,11 +155,15 @@ __global__ __launch_bounds__(256) void k_gs_finish(float4 *__restrict__ y, int l
   y[r * ld4 + v] = a;
 }
 
+// NS: rowsets per summing wave (16, or 8: half the rows per workgroup, twice the batches)
+template <int NS>
 __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
     const uint2 *__restrict__ entries, const long long *__restrict__ wave_off,
     const unsigned short *__restrict__ counts, int t_max, const int2 *__restrict__ slices,
     const int *__restrict__ n_slices, const int *__restrict__ rows, const char *__restrict__ table,
     float4 *__restrict__ partial, long long part_stride, int n_blocks) {
+  static_assert(NS == 8 || NS == 16, "rowsets per wave");
+  constexpr int CNT_USED = LDS_CW * NS * 2;  // counts of one visit (bytes)
   __shared__ float4 lds[RING_TOTAL_B / 16];
   const int nb = n_blocks;
   const int b = blockIdx.x % nb, batch = blockIdx.x / nb;
@@ -185,7 +189,7 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
     __builtin_amdgcn_s_setprio(3);
     const int2 *sl = slices + (long long)b * t_max;
     const char *cnt_src =
-        reinterpret_cast<const char *>(counts) + (long long)blockIdx.x * t_max * RING_CNT_USED;
+        reinterpret_cast<const char *>(counts) + (long long)blockIdx.x * t_max * CNT_USED;
     const int iters = T + RING_W - 1;
     for (int s = 0; s < iters; s++) {
       // buffer s % K (and counts buffer (s - W + 1) & 1) free: visit s - K done everywhere
@@ -205,8 +209,8 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
         }
       }
       const int cv = s - (RING_W - 1);  // the visit whose last slice this is
-      if (cv >= 0 && lane * 16 < RING_CNT_USED)
-        glds16(cnt_src + (long long)cv * RING_CNT_USED + lane * 16,
+      if (cv >= 0 && lane * 16 < CNT_USED)
+        glds16(cnt_src + (long long)cv * CNT_USED + lane * 16,
                lds_base + (unsigned)(RING_CNT_OFF + (cv % RING_NCB) * RING_CNT_B));
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // slice s and counts landed
       if (lane == 0) __atomic_store_n(loaded, (unsigned)(s + 1), __ATOMIC_RELAXED);
@@ -232,9 +236,9 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
   refill(3);
   asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // chunk 0
 
-  f4v acc[LDS_SLOTS];
+  f4v acc[NS];
 #pragma unroll
-  for (int j = 0; j < LDS_SLOTS; j++) acc[j] = f4v{0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < NS; j++) acc[j] = f4v{0.f, 0.f, 0.f, 0.f};
   // Entry ring cursor: this lane's LDS byte address of the next block's entries, and the
   // blocks left in the current 4-block chunk (r03: per block one VALU add and a scalar
   // count-down, where the ring offset arithmetic and the chunk test took six scalar ops)
@@ -277,11 +281,11 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
     // instructions; 254.8 -> 250.4 us per call, 536-538 -> 541-542 epochs/s).  Per (rowset,
     // visit): 0 blocks (half the pairs on reddit), 1 (92 % of the blocks) or more
     const unsigned short *c16 = reinterpret_cast<const unsigned short *>(
-        lb + RING_CNT_OFF + (t % RING_NCB) * RING_CNT_B + wave * 32);
-    const unsigned cl = c16[lane & 15];
+        lb + RING_CNT_OFF + (t % RING_NCB) * RING_CNT_B + wave * (2 * NS));
+    const unsigned cl = c16[lane & (NS - 1)];
     const unsigned nz = (unsigned)__ballot(cl != 0u), big = (unsigned)__ballot(cl > 4u);
 #pragma unroll
-    for (int j = 0; j < LDS_SLOTS; j++) {
+    for (int j = 0; j < NS; j++) {
       if (__builtin_amdgcn_readfirstlane((int)(nz << (31 - j))) < 0) {  // bit j: the sign bit
         block(acc[j]);
         if ((big >> j) & 1u) {
@@ -322,10 +326,10 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
   // rows[] = row | log2(m) << 28: a row spread over m lane groups (host/ring.cpp) has its m
   // partial sums added across lane groups g ^ 1, g ^ 2, .. (xor butterfly, fixed order for the
   // writing lane group g % m == 0); m is uniform per rowset
-  const int *rw = rows + (((long long)batch * LDS_CW + wave) * LDS_SLOTS) * 16 + g;
+  const int *rw = rows + (((long long)batch * LDS_CW + wave) * NS) * 16 + g;
   float4 *pb = partial + (long long)b * part_stride * 4 + v;
 #pragma unroll
-  for (int j = 0; j < LDS_SLOTS; j++) {
+  for (int j = 0; j < NS; j++) {
     const int u = rw[j * 16];
     const int sp = __builtin_amdgcn_readfirstlane((int)((unsigned)u >> 28));
     float4 a = make_float4(acc[j].x, acc[j].y, acc[j].z, acc[j].w);
@@ -383,10 +387,17 @@ void launch_graphsum_ring(const LdsSchedule &s, const float *in, int ld_in, floa
                        reinterpret_cast<const float4 *>(in), ld_in / 4, s.col_scale, s.n_cols,
                        reinterpret_cast<float4 *>(scratch_in), col_map);
   const long long n_wg = (long long)s.n_batches * s.n_blocks;
-  PGCN_LAUNCH(k_graphsum_ring, dim3((unsigned)n_wg), dim3(LDS_THREADS), 0, st, s.entries,
-                     s.wave_off, s.counts, s.t_max, s.slices, s.n_slices, s.rows,
-                     reinterpret_cast<const char *>(scratch_in), reinterpret_cast<float4 *>(partial),
-                     (long long)s.n_rows, s.n_blocks);
+#define RING_LAUNCH(NS_)                                                                        \
+  PGCN_LAUNCH(k_graphsum_ring<NS_>, dim3((unsigned)n_wg), dim3(LDS_THREADS), 0, st, s.entries, \
+              s.wave_off, s.counts, s.t_max, s.slices, s.n_slices, s.rows,                      \
+              reinterpret_cast<const char *>(scratch_in), reinterpret_cast<float4 *>(partial), \
+              (long long)s.n_rows, s.n_blocks)
+  PGCN_CHECK(ring_slots_ok(s.ns), PGCN_E_INVALID, "graphsum_ring: rowsets per wave");
+  if (s.ns == 8)
+    RING_LAUNCH(8);
+  else
+    RING_LAUNCH(16);
+#undef RING_LAUNCH
   const GsEpilogue none{};
   const long long post = (long long)s.n_rows * 4;
   PGCN_LAUNCH(k_gs_lds_combine, dim3((unsigned)ceil_div(post, 256)), dim3(256), 0, st,

@@ -52,7 +52,10 @@ bool graphsum_vec_supported(int vec);
 // ---- d = 16 GraphSum with LDS-staged feature slices (k_graphsum_ring.hip) -----------------
 constexpr int kGraphBlocks = 8;                      // plain kernel: column blocks (one per XCD)
 constexpr int LDS_CW = 15;                           // summing waves per workgroup
-constexpr int LDS_SLOTS = 16;                        // rowsets (16 rows) per summing wave
+constexpr int LDS_SLOTS = 16;                        // rowsets (16 rows) per summing wave (max)
+// the ring schedule's rowsets per summing wave: 16, or 8 for half the rows per workgroup (twice
+// the rowset batches: row chunks of the edge-cut engine fill the chip; knob "lds_slots")
+constexpr bool ring_slots_ok(int ns) { return ns == 8 || ns == 16; }
 constexpr int LDS_THREADS = 64 * (LDS_CW + 1);       // + one slice loader wave
 // Sliding-window ring schedule (k_graphsum_ring.hip, host/ring.cpp): slices of RING_SR rows,
 // a ring of RING_K slices in LDS as 4 quarter planes of RING_P rows, visits read RING_W slices
@@ -82,12 +85,13 @@ struct LdsSchedule {
   int n_batches = 0;  // workgroups = n_batches * n_blocks
   int n_blocks = 4;   // column blocks (workgroup w serves block w % n_blocks)
   int t_max = 0;      // max slices per column block
+  int ns = LDS_SLOTS;  // rowsets per summing wave (ring_slots_ok)
   const uint2 *entries = nullptr;            // [kb][16 lane groups] x 4 uint16 row offsets
   const long long *wave_off = nullptr;       // [wg][LDS_CW] first kb of each wave's stream
-  const unsigned short *counts = nullptr;    // [wg][t_max][LDS_CW][LDS_SLOTS] steps
+  const unsigned short *counts = nullptr;    // [wg][t_max][LDS_CW][ns] steps
   const int2 *slices = nullptr;              // [block][t_max] {first column, rows}
   const int *n_slices = nullptr;             // [block]
-  const int *rows = nullptr;                 // [batch][LDS_CW][LDS_SLOTS][16] row | spread
+  const int *rows = nullptr;                 // [batch][LDS_CW][ns][16] row | spread
   const float *row_scale = nullptr;          // 1/sqrt(deg) of output rows
   const float *col_scale = nullptr;          // 1/sqrt(deg) of input rows
 };

@@ -320,6 +320,23 @@ def test_lds_schedule_walk_sums_every_edge(pgcn):
                                          ctypes.byref(n)) == pgcn.PGCN_E_INVALID
 
 
+@pytest.mark.parametrize("slots", [8, 16])
+def test_lds_schedule_rowsets_per_wave(pgcn, slots):
+    """The ring schedule with 8 or 16 rowsets per summing wave (knob lds_slots: 8 halves a
+    workgroup's rows) walks to every row's exact CSR sum; 8 slots build twice the batches."""
+    ds = pgcn.Dataset.synthetic(70000, 8, 4, 2000000, 1)
+    ip = np.ascontiguousarray(ds.graph_indptr)
+    ix = np.ascontiguousarray(ds.graph_indices)
+    with helpers.knobs(pgcn, lds_slots=slots):
+        err, nb = _lds_check(pgcn, ip, ix, ds.num_nodes, RING)
+        shape = (ctypes.c_int * 5)()
+        n = pgcn.lib.pgcn_debug_lds_counts(ds.num_nodes, ds.num_nodes, helpers.ptr(ip),
+                                           helpers.ptr(ix), RING, None, 0, shape)
+    assert n > 0 and err < 1e-12
+    assert shape[3] == slots
+    assert nb * 64 < 4 * len(ix), nb * 64 / len(ix)
+
+
 def test_lds_schedule_ragged_graph(pgcn):
     """Isolated rows, a hub adjacent to everything, duplicate edges: the ring schedule stays
     exact."""
@@ -474,8 +491,8 @@ def test_ring_kernel_lds_reads_wait_before_use(tmp_path):
     dev = _device_code(obj[0], tmp_path)
     asm = subprocess.run([f"{LLVM_BIN}/llvm-objdump", "-d", "--no-show-raw-insn", dev],
                          check=True, capture_output=True, text=True).stdout.splitlines()
-    start = [i for i, l in enumerate(asm) if re.match(r"^[0-9a-f]+ <_ZN4pgcn15k_graphsum_ring", l)]
-    assert start, "k_graphsum_ring not in the code object"
+    starts = [i for i, l in enumerate(asm) if re.match(r"^[0-9a-f]+ <_ZN4pgcn15k_graphsum_ring", l)]
+    assert len(starts) >= 2, "k_graphsum_ring<8> / <16> not in the code object"
 
     def regs(ops):
         out = set()
@@ -485,24 +502,25 @@ def test_ring_kernel_lds_reads_wait_before_use(tmp_path):
             else:
                 out.update(range(int(m.group(1)), int(m.group(2)) + 1))
         return out
-    pending, bad, reads = set(), [], 0
-    for line in asm[start[0] + 1:]:
-        if re.match(r"^[0-9a-f]+ <", line):
-            break
-        t = line.strip()
-        if not t or t.startswith(";"):
-            continue
-        op, _, ops = t.partition(" ")
-        ops = ops.split("//")[0]
-        if op == "s_waitcnt" and "lgkmcnt(0)" in ops:
-            pending.clear()
-        elif op in ("ds_read_b128", "ds_read_b64"):
-            pending |= regs(ops.split(",")[0])
-            reads += 1
-        elif pending & regs(ops):
-            bad.append(t)
-    assert reads >= 16, reads
-    assert not bad, bad[:10]
+    for start in starts:
+        pending, bad, reads = set(), [], 0
+        for line in asm[start + 1:]:
+            if re.match(r"^[0-9a-f]+ <", line):
+                break
+            t = line.strip()
+            if not t or t.startswith(";"):
+                continue
+            op, _, ops = t.partition(" ")
+            ops = ops.split("//")[0]
+            if op == "s_waitcnt" and "lgkmcnt(0)" in ops:
+                pending.clear()
+            elif op in ("ds_read_b128", "ds_read_b64"):
+                pending |= regs(ops.split(",")[0])
+                reads += 1
+            elif pending & regs(ops):
+                bad.append(t)
+        assert reads >= 16, reads
+        assert not bad, bad[:10]
 
 
 def test_debug_set_refuses_out_of_range_values(pgcn):
