@@ -52,6 +52,13 @@ typedef struct pgcn_graph pgcn_graph;
  * it), computes coef = 1/sqrtf(deg_src*deg_dst) bit-exactly as hpdga module.cpp:88-90 and
  * builds the wavefront work schedule. Host pointers. */
 int pgcn_graph_create(int n_nodes, const int *indptr, const int *indices, pgcn_graph **out);
+/* The reference's full GraphSum contract (include/module.cuh:82, the dev_graph_value array of
+ * src/gcn.cu:30-43): any per-slot values, aligned with `indices` (host pointers).  Values equal
+ * to the parser's coefficients (as pgcn_graph_create computes them) take the LDS ring path;
+ * any other values take the per-edge gather kernels.  The pattern need not be symmetric (the
+ * call is out = A in for the given A; the engine's backward identity needs A = A^T). */
+int pgcn_graph_create_values(int n_nodes, const int *indptr, const int *indices,
+                             const float *values, pgcn_graph **out);
 int pgcn_graph_destroy(pgcn_graph *g);
 long long pgcn_graph_nnz(const pgcn_graph *g);
 /* out[i, 0:dim] = sum_j coef_ij * in[j, 0:dim]  (GraphSum::forward/backward,

@@ -65,6 +65,7 @@ _sig("pgcn_rng_seed_glibc", None, ctypes.c_uint, P(c_u64))
 _sig("pgcn_rng_jump", None, P(c_u64), c_u64)
 _sig("pgcn_rng_jump_table", c_int, c_u64, c_void_p)
 _sig("pgcn_graph_create", c_int, c_int, c_void_p, c_void_p, P(c_void_p))
+_sig("pgcn_graph_create_values", c_int, c_int, c_void_p, c_void_p, c_void_p, P(c_void_p))
 _sig("pgcn_graph_destroy", c_int, c_void_p)
 _sig("pgcn_graph_nnz", c_ll, c_void_p)
 _sig("pgcn_graphsum", c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p)
@@ -494,7 +495,7 @@ def csr_transpose(indptr, indices, n_cols):
 
 EXPORTED = [
     "pgcn_status_string", "pgcn_version", "pgcn_rng_seed", "pgcn_rng_seed_glibc", "pgcn_rng_jump",
-    "pgcn_graph_create", "pgcn_debug_rank_graph",
+    "pgcn_graph_create", "pgcn_graph_create_values", "pgcn_debug_rank_graph",
     "pgcn_graph_destroy", "pgcn_graph_nnz", "pgcn_graphsum", "pgcn_gemm", "pgcn_gemm_tn_workspace",
     "pgcn_gemm_tn", "pgcn_mask_nibbles", "pgcn_gemm_xstream", "pgcn_gemm_xstream_dual",
     "pgcn_gemm_tn_xstream",

@@ -137,6 +137,30 @@ int pgcn_graph_create(int n, const int *indptr, const int *indices, pgcn_graph *
     *out = h.release();
   });
 }
+int pgcn_graph_create_values(int n, const int *indptr, const int *indices, const float *values,
+                             pgcn_graph **out) {
+  return guarded([&] {
+    PGCN_CHECK(n > 0 && indptr && indices && values && out, PGCN_E_INVALID,
+               "graph_create_values args");
+    PGCN_CHECK(indptr[0] == 0 && indptr[n] >= 0, PGCN_E_INVALID, "graph_create_values: indptr");
+    for (int i = 0; i < n; i++)
+      PGCN_CHECK(indptr[i + 1] >= indptr[i], PGCN_E_INVALID, "graph_create_values: indptr order");
+    for (long long k = 0; k < indptr[n]; k++)
+      PGCN_CHECK(indices[k] >= 0 && indices[k] < n, PGCN_E_INVALID,
+                 "graph_create_values: column id out of range");
+    check_device();
+    auto h = std::make_unique<pgcn_graph>();
+    h->g = std::make_unique<DevGraph>(n, n, indptr, indices, values);
+    // the parser's coefficients exactly: the factorised LDS path applies
+    const std::vector<float> coef = graph_coefs(n, indptr, indices);
+    if (std::memcmp(coef.data(), values, coef.size() * sizeof(float)) == 0) {
+      std::vector<float> sc = degree_scales(n, indptr);
+      h->g->set_scales(sc, sc);
+    }
+    *out = h.release();
+  });
+}
+
 int pgcn_debug_rank_graph(int n, const int *indptr, const int *indices, int world, int rank,
                           int chunks, int chunk, pgcn_graph **out, int *rows, int *cols) {
   return guarded([&] {

@@ -25,3 +25,4 @@ timeout -k 10 300 python3 tools/rank_graphsum.py 2,4,8 1 > $O/rankgs_c1.json 2> 
 timeout -k 10 300 python3 tools/rank_graphsum.py 2,4,8 2 > $O/rankgs_c2.json 2> $O/rankgs_c2.err; echo "c2 rc=$?"; tail -1 $O/rankgs_c2.json
 RANK_KNOBS=rs_chunks=2,lds_slots=8 timeout -k 10 300 python3 tools/rank_epoch.py 2,4,8 0 16 > $O/rank_epoch_c2s8.json 2> $O/rank_epoch_c2s8.err
 echo "rank_epoch c2 s8 rc=$?"; cat $O/rank_epoch_c2s8.json
+bash scripts/gpu_traffic.sh r04d_traffic

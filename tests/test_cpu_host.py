@@ -298,6 +298,25 @@ def _lds_check(pgcn, ip, ix, n, window):
     return err.value, nb.value
 
 
+def test_graph_create_values_rejects_bad_csr(pgcn):
+    """pgcn_graph_create_values validates the CSR before touching a device: a column id out
+    of range, a decreasing indptr or a null values pointer is PGCN_E_INVALID (host only)."""
+    lib = pgcn.lib
+    ip = np.array([0, 2, 3], np.int32)
+    vals = np.ones(3, np.float32)
+    g = ctypes.c_void_p()
+    for ix in (np.array([0, 2, 1], np.int32), np.array([0, -1, 1], np.int32)):
+        assert lib.pgcn_graph_create_values(2, helpers.ptr(ip), helpers.ptr(ix),
+                                            helpers.ptr(vals), ctypes.byref(g)) \
+            == pgcn.PGCN_E_INVALID
+    ix = np.array([0, 1, 1], np.int32)
+    bad = np.array([0, 3, 2], np.int32)
+    assert lib.pgcn_graph_create_values(2, helpers.ptr(bad), helpers.ptr(ix), helpers.ptr(vals),
+                                        ctypes.byref(g)) == pgcn.PGCN_E_INVALID
+    assert lib.pgcn_graph_create_values(2, helpers.ptr(ip), helpers.ptr(ix), None,
+                                        ctypes.byref(g)) == pgcn.PGCN_E_INVALID
+
+
 RING = 5  # pgcn_debug_lds_check's schedule kind: the ring schedule, the only LDS schedule
 
 

@@ -108,6 +108,66 @@ def test_graphsum_vs_oracle(pgcn, n, deg, dim, hubs):
     pgcn.lib.pgcn_graph_destroy(g)
 
 
+@pytest.mark.parametrize("kind", ["coef", "random", "directed"])
+def test_graphsum_with_values(pgcn, kind):
+    """pgcn_graph_create_values (the reference's GraphSum contract: any dev_graph_value array,
+    include/module.cuh:82): the parser's own coefficients take the LDS ring path and give
+    pgcn_graph_create's bits; arbitrary values (and a directed pattern) take the gather
+    kernels; every case against a float64 CSR product of the given values."""
+    n, dim = 120000, 16
+    indptr, indices = random_graph(n, 30, seed=3, hubs=10, hub_deg=2000)
+    if kind == "directed":  # drop every other slot of each row past the self loop
+        keep = np.ones(len(indices), bool)
+        keep[1::2] = False
+        rows = np.repeat(np.arange(n), np.diff(indptr))
+        keep[indptr[:-1]] = True
+        indices = np.ascontiguousarray(indices[keep])
+        indptr = np.zeros(n + 1, np.int32)
+        np.add.at(indptr, rows[keep] + 1, 1)
+        indptr = np.ascontiguousarray(np.cumsum(indptr).astype(np.int32))
+    deg = np.diff(indptr)
+    rows = np.repeat(np.arange(n), np.diff(indptr))
+    if kind == "coef":
+        # graph_coef's expression (src/parser.cpp:164-181): float sqrt of the int product,
+        # double division, stored to float
+        prod = (deg[rows].astype(np.int64) * deg[indices].astype(np.int64)).astype(np.float32)
+        vals = (1.0 / np.sqrt(prod).astype(np.float64)).astype(np.float32)
+        g0 = ctypes.c_void_p()
+        pgcn.check(pgcn.lib.pgcn_graph_create(n, helpers.ptr(indptr), helpers.ptr(indices),
+                                              ctypes.byref(g0)), "graph_create")
+    else:
+        vals = np.random.default_rng(9).uniform(-1, 1, len(indices)).astype(np.float32)
+    vals = np.ascontiguousarray(vals)
+    g = ctypes.c_void_p()
+    st = pgcn.lib.pgcn_graph_create_values(n, helpers.ptr(indptr), helpers.ptr(indices),
+                                           helpers.ptr(vals), ctypes.byref(g))
+    pgcn.check(st, "graph_create_values")
+    x = np.random.default_rng(4).standard_normal((n, dim)).astype(np.float32)
+    xin = torch.from_numpy(x).to(DEV)
+    out = torch.full((n, dim), float("nan"), device=DEV)
+    pgcn.reset_path_counts()
+    pgcn.check(pgcn.lib.pgcn_graphsum(g, vp(xin), dim, vp(out), dim, dim, stream()), "graphsum")
+    torch.cuda.synchronize()
+    paths = pgcn.path_counts()
+    ref = np.zeros((n, dim))
+    np.add.at(ref, rows, vals[:, None].astype(np.float64) * x[indices].astype(np.float64))
+    bound = np.zeros((n, dim))
+    np.add.at(bound, rows, np.abs(vals[:, None].astype(np.float64) * x[indices]))
+    err = np.abs(out.cpu().numpy() - ref)
+    assert (err <= 1e-5 * bound + 1e-30).all(), (err / (bound + 1e-30)).max()
+    if kind == "coef":
+        # the parser's coefficients bit for bit: the ring path, pgcn_graph_create's bits
+        assert paths["gs_ring"] >= 1, paths
+        out0 = torch.empty_like(out)
+        pgcn.check(pgcn.lib.pgcn_graphsum(g0, vp(xin), dim, vp(out0), dim, dim, stream()), "gs0")
+        torch.cuda.synchronize()
+        assert torch.equal(out, out0)
+        pgcn.lib.pgcn_graph_destroy(g0)
+    else:
+        assert paths["gs_ring"] == 0 and paths["gs_gather"] >= 1, paths
+    pgcn.lib.pgcn_graph_destroy(g)
+
+
 @pytest.mark.parametrize("blocks", [2, 8, 16, 32])
 def test_graphsum_lds_column_blocks(pgcn, blocks):
     """The LDS ring schedule with other column-block counts than the shape rule picks (4 for
