@@ -61,6 +61,7 @@ constexpr int XL_TN_LOADERS = 1, XL_TN_CONSUMERS = 3;
 constexpr int XL_LDS = 159 * 1024;  // ring + hand-off words (one workgroup per CU)
 constexpr int XL_FLAGS = 64;        // ready[8], freed[8] at the end
 constexpr int XL_KC = 10;           // the instantiated width: K in (576, 640] (reddit: 602)
+constexpr int XL_S0 = 4 * (XL_KC - 1) + 1;  // NN steps (16 k each) inside every such K
 constexpr int XL_BS = 648;          // B^T row stride in floats (== 8 mod 16: conflict-free)
 constexpr int XL_BT_BYTES = 16 * XL_BS * 4 / 1024 * 1024 + 1024;  // NN: B^T ahead of the ring
 
@@ -213,6 +214,20 @@ __global__ __launch_bounds__(64 * (XL_NN_LOADERS + XL_NN_CONSUMERS), 1) void k_x
   // alternate: a copy would wait for the prefetch)
   auto group = [&](int t, const uint64_t(&mw)[4], uint64_t(&mwn)[4]) {
     if (MASKED && t + XL_NN_CONSUMERS < T) load_mask(t + XL_NN_CONSUMERS, mwn);
+    const long long rgi = blockIdx.x + (long long)t * gridDim.x;
+    // the epilogue's row scales, loaded before the slot wait (whose memory clobber keeps them
+    // here) so they land during the MFMAs: loaded at their use, each load waited for alone
+    // behind the stores before it (vmcnt counts stores), four HBM round trips per group
+    float nsc[4];  // read only under epi.next_table
+    if constexpr (!DUAL) {
+      if (epi.next_table) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const long long rr = rgi * 16 + 4 * g + r;
+          nsc[r] = epi.next_scale[rr < M ? rr : M - 1];
+        }
+      }
+    }
     const int slot = t % rg.nslot;
     lds_wait_ge(ready + slot, (unsigned)(t + 1));
     char *const sb = lds + rg.off + slot * (NI * 1024);
@@ -224,11 +239,14 @@ __global__ __launch_bounds__(64 * (XL_NN_LOADERS + XL_NN_CONSUMERS), 1) void k_x
       asm volatile("" ::: "memory");
     }
     // the group's fragments into registers, then the slot goes back to the loader
+    // (K > 64 (XL_KC - 1) on this kernel: steps s < XL_S0 always lie inside K, so only the
+    // last few test it -- no per-step branch for hipcc to schedule around)
     const char *a = sb + i * rg.st * 16 + g * 16;
     float4 xa[NS];
 #pragma unroll
     for (int s = 0; s < NS; s++)
-      xa[s] = 16 * s < K ? *reinterpret_cast<const float4 *>(a + 64 * s) : make_float4(0.f, 0.f, 0.f, 0.f);
+      xa[s] = (s < XL_S0 || 16 * s < K) ? *reinterpret_cast<const float4 *>(a + 64 * s)
+                                        : make_float4(0.f, 0.f, 0.f, 0.f);
     xl_release(freed, slot, t, lane);
     floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f}, acc2 = floatx4{0.f, 0.f, 0.f, 0.f};
 #if PGCN_XS_CHAINS == 2
@@ -238,7 +256,7 @@ __global__ __launch_bounds__(64 * (XL_NN_LOADERS + XL_NN_CONSUMERS), 1) void k_x
 #endif
 #pragma unroll
     for (int s = 0; s < NS; s++) {
-      if (16 * s >= K) break;  // steps wholly past K add nothing
+      if (s >= XL_S0 && 16 * s >= K) break;  // steps wholly past K add nothing
       float4 x = xa[s];
       const float4 bb = *reinterpret_cast<const float4 *>(bl + 16 * s);
       if constexpr (DUAL) {
@@ -267,7 +285,6 @@ __global__ __launch_bounds__(64 * (XL_NN_LOADERS + XL_NN_CONSUMERS), 1) void k_x
       am = am * a_scale;
     }
     // lane holds C[16 rg + 4 g + r][i] (k_xstream_nn's epilogue)
-    const long long rgi = blockIdx.x + (long long)t * gridDim.x;
     if (i < ldc) {
 #pragma unroll
       for (int r = 0; r < 4; r++) {
@@ -280,7 +297,7 @@ __global__ __launch_bounds__(64 * (XL_NN_LOADERS + XL_NN_CONSUMERS), 1) void k_x
               const long long sr = epi.next_sr;
               float *tb = reinterpret_cast<float *>(epi.next_table + (rr / sr) * 4 * sr +
                                                     (i >> 2) * sr + rr % sr);
-              tb[i & 3] = c * epi.next_scale[rr];
+              tb[i & 3] = c * nsc[r];
             }
           }
           C[rr * ldc + i] = c;
@@ -325,24 +342,31 @@ __global__ __launch_bounds__(64 * (XL_TN_LOADERS + XL_TN_CONSUMERS), 1) void k_x
     xl_load<NI, XL_TN_LOADERS>(A, lda, M, T, wave, lane, rg, lds, ready, freed);
   } else {
     const int cid = wave - XL_TN_LOADERS;
-    auto load_rows = [&](int t, float(&bv)[4], uint64_t(&m)[4]) {  // dZ and keep bits, group t
+    // dZ and keep bits of group t, raw: unconditional loads whose values are first used a
+    // group later (a select or multiply here made hipcc branch around each load and wait for
+    // it on the spot: four HBM round trips per group)
+    auto load_rows = [&](int t, float(&bv)[4], uint64_t(&m)[4]) {
       const long long row0 = (blockIdx.x + (long long)t * gridDim.x) * 16;
 #pragma unroll
       for (int q = 0; q < 4; q++) {
         const long long mr = row0 + 4 * q + g;
         const long long row = mr < M ? mr : M - 1;
-        const float v = G[row * ldg + (i < N ? i : 0)];
-        bv[q] = (mr < M && i < N) ? (MASKED && FOLD ? v * a_scale : v) : 0.0f;
+        bv[q] = G[row * ldg + (i < N ? i : 0)];
         if constexpr (MASKED) m[q] = maskT[row * 16 + i];
       }
     };
     // group t with dZ / keep bits in bj / mw, the next group's into bjn / mwn (alternating
     // static buffers)
-    auto group = [&](int t, const float(&bj)[4], const uint64_t(&mw)[4], float(&bjn)[4],
+    auto group = [&](int t, const float(&bv)[4], const uint64_t(&mw)[4], float(&bjn)[4],
                      uint64_t(&mwn)[4]) {
       if (t + XL_TN_CONSUMERS < T) load_rows(t + XL_TN_CONSUMERS, bjn, mwn);
       const int slot = t % rg.nslot;
       lds_wait_ge(ready + slot, (unsigned)(t + 1));
+      float bj[4];  // rows past M and columns past N feed zeros
+      const long long row0 = (blockIdx.x + (long long)t * gridDim.x) * 16;
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+        bj[q] = (row0 + 4 * q + g < M && i < N) ? (MASKED && FOLD ? bv[q] * a_scale : bv[q]) : 0.0f;
       // the group's fragments into registers, then the slot goes back to the loader
       const char *sp = lds + rg.off + slot * (NI * 1024) + i * 16;
       float4 xa[4][KC];
