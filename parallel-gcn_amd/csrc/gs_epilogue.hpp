@@ -42,9 +42,32 @@ __device__ __forceinline__ uint32_t gs_epi_bits4(const uint64_t *__restrict__ ma
   return (uint32_t)v & 0xfu;
 }
 
+// The epilogue's loads (dropout words, ReLU mask bytes, the next table's row scale), issued
+// together before the sums they apply to are formed: a kernel that loads them inside the
+// epilogue waits for each behind the stores before it (hipcc cannot hoist a load over a store
+// through a byte pointer), one HBM round trip apiece.
+struct GsEpiIn {
+  uint64_t w0 = 0, w1 = 0;  // dropout words (w1: a nibble that straddles two words)
+  uint32_t rm = 0;          // mode 2: the forward's ReLU keep bytes
+  float ns = 0.0f;          // next_scale[r]
+};
+
+__device__ __forceinline__ void gs_epi_load(GsEpiIn &in, long long r, int c0, const GsEpilogue &e) {
+  if (e.mode == 0) return;
+  c0 += e.col0;
+  if (e.drop_mask) {
+    const long long idx = e.drop_base + r * e.drop_cols + c0;
+    in.w0 = e.drop_mask[idx >> 6];
+    if ((idx & 63) > 60) in.w1 = e.drop_mask[(idx >> 6) + 1];
+  }
+  if (e.mode == 2) in.rm = *reinterpret_cast<const uint32_t *>(e.relu_mask + r * e.relu_ld + c0);
+  if (e.next_table) in.ns = e.next_scale[r];
+}
+
 // a = the float4 of columns c0 .. c0+3 of row r (c0 % 4 == 0) of the output pointer, i.e.
-// columns e.col0 + c0 .. of the variable
-__device__ __forceinline__ void gs_epilogue(float4 &a, long long r, int c0, const GsEpilogue &e) {
+// columns e.col0 + c0 .. of the variable; `in` from gs_epi_load(r, c0, e)
+__device__ __forceinline__ void gs_epilogue(float4 &a, long long r, int c0, const GsEpilogue &e,
+                                            const GsEpiIn &in) {
   if (e.mode == 0) return;
   c0 += e.col0;
   if (e.mode == 1) {
@@ -59,7 +82,11 @@ __device__ __forceinline__ void gs_epilogue(float4 &a, long long r, int c0, cons
     if (!k3) a.w = 0.0f;
   }
   if (e.drop_mask) {
-    const uint32_t bits = gs_epi_bits4(e.drop_mask, e.drop_base + r * e.drop_cols + c0);
+    const long long idx = e.drop_base + r * e.drop_cols + c0;
+    const int sh = (int)(idx & 63);
+    uint64_t v = in.w0 >> sh;
+    if (sh > 60) v |= in.w1 << (64 - sh);
+    const uint32_t bits = (uint32_t)v & 0xfu;
     const float s = e.drop_scale;
     a.x *= (bits & 1) ? s : 0.0f;
     a.y *= (bits & 2) ? s : 0.0f;
@@ -67,18 +94,25 @@ __device__ __forceinline__ void gs_epilogue(float4 &a, long long r, int c0, cons
     a.w *= (bits & 8) ? s : 0.0f;
   }
   if (e.mode == 2) {
-    const uint32_t m = *reinterpret_cast<const uint32_t *>(e.relu_mask + r * e.relu_ld + c0);
+    const uint32_t m = in.rm;
     if (!(m & 0xffu)) a.x = 0.0f;
     if (!(m & 0xff00u)) a.y = 0.0f;
     if (!(m & 0xff0000u)) a.z = 0.0f;
     if (!(m & 0xff000000u)) a.w = 0.0f;
   }
   if (e.next_table) {  // as k_ring_prescale computes it from the stored output
-    const float s = e.next_scale[r];
+    const float s = in.ns;
     const long long sr = e.next_sr;
     e.next_table[(r / sr) * 4 * sr + (c0 >> 2) * sr + r % sr] =
         make_float4(a.x * s, a.y * s, a.z * s, a.w * s);
   }
+}
+
+// loads and application in one (kernels whose epilogue inputs cannot be loaded earlier)
+__device__ __forceinline__ void gs_epilogue(float4 &a, long long r, int c0, const GsEpilogue &e) {
+  GsEpiIn in;
+  gs_epi_load(in, r, c0, e);
+  gs_epilogue(a, r, c0, e, in);
 }
 
 }  // namespace pgcn

@@ -118,6 +118,10 @@ __global__ __launch_bounds__(256) void k_gs_lds_combine(const float4 *__restrict
   const long long r = t >> 2;
   if (r >= n) return;
   const int v = (int)(t & 3);
+  // the row scale and the epilogue's inputs with the partials: one round trip, not one each
+  const float s = scale[r];
+  GsEpiIn ein;
+  gs_epi_load(ein, r, 4 * v, epi);
   float4 a;
   if (nb <= 8) {  // every block's partial loaded before the (ordered) adds
     float4 p[8];
@@ -132,12 +136,11 @@ __global__ __launch_bounds__(256) void k_gs_lds_combine(const float4 *__restrict
     a = partial[r * 4 + v];
     for (int b = 1; b < nb; b++) f4_acc(a, partial[((long long)b * part_stride + r) * 4 + v]);
   }
-  const float s = scale[r];
   a.x *= s;
   a.y *= s;
   a.z *= s;
   a.w *= s;
-  gs_epilogue(a, r, 4 * v, epi);
+  gs_epilogue(a, r, 4 * v, epi, ein);
   out[r * ld4_out + v] = a;
 }
 
@@ -150,8 +153,10 @@ __global__ __launch_bounds__(256) void k_gs_finish(float4 *__restrict__ y, int l
   const long long r = t / vec;
   if (r >= n) return;
   const int v = (int)(t - r * vec);
+  GsEpiIn ein;
+  gs_epi_load(ein, r, 4 * v, epi);
   float4 a = y[r * ld4 + v];
-  gs_epilogue(a, r, 4 * v, epi);
+  gs_epilogue(a, r, 4 * v, epi, ein);
   y[r * ld4 + v] = a;
 }
 
@@ -326,11 +331,16 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
   // rows[] = row | log2(m) << 28: a row spread over m lane groups (host/ring.cpp) has its m
   // partial sums added across lane groups g ^ 1, g ^ 2, .. (xor butterfly, fixed order for the
   // writing lane group g % m == 0); m is uniform per rowset
+  // (every rowset's row word first, one wait for all: loaded at its use, each load waited
+  // behind the store before it, NS round trips at the kernel's end)
   const int *rw = rows + (((long long)batch * LDS_CW + wave) * NS) * 16 + g;
   float4 *pb = partial + (long long)b * part_stride * 4 + v;
+  int uw[NS];
+#pragma unroll
+  for (int j = 0; j < NS; j++) uw[j] = rw[j * 16];
 #pragma unroll
   for (int j = 0; j < NS; j++) {
-    const int u = rw[j * 16];
+    const int u = uw[j];
     const int sp = __builtin_amdgcn_readfirstlane((int)((unsigned)u >> 28));
     float4 a = make_float4(acc[j].x, acc[j].y, acc[j].z, acc[j].w);
     for (int k = 0; k < sp; k++) {
