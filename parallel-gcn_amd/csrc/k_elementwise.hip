@@ -40,8 +40,18 @@ struct Xs64 {
     const uint64_t u = s1;
     s0 = u;
     t ^= t << 23;
-    t ^= t >> 17;
-    t ^= u ^ (u >> 26);
+    {  // t ^ (t >> 17) ^ u ^ (u >> 26) per half: one three-input xor and one xor (r04: 14 ->
+       // 12 VALU per draw; k_dropout_mask 111 -> 94 us alone on reddit's input mask)
+      uint64_t y, z;  // full-rate 64-bit shifts (hipcc would split them into 32-bit pieces)
+      asm("v_lshrrev_b64 %0, 17, %1" : "=v"(y) : "v"(t));
+      asm("v_lshrrev_b64 %0, 26, %1" : "=v"(z) : "v"(u));
+      uint32_t l = (uint32_t)t, h = (uint32_t)(t >> 32);
+      asm("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(l) : "v"((uint32_t)y), "v"((uint32_t)z));
+      asm("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96"
+          : "+v"(h)
+          : "v"((uint32_t)(y >> 32)), "v"((uint32_t)(z >> 32)));
+      t = ((uint64_t)(h ^ (uint32_t)(u >> 32)) << 32) | (l ^ (uint32_t)u);
+    }
     s1 = t;
 #if PGCN_DROP_SHIFTIN
     // keep = ((t + u) & 0x7fffffff) >= threshold, compared as ((t + u) << 1) >= (threshold << 1)
@@ -65,6 +75,30 @@ struct Xs64 {
   }
 };
 
+// a ^ b ^ c in one VALU op (v_bitop3_b32, truth table 0x96)
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  asm("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a) : "v"(b), "v"(c));
+  return a;
+}
+// M^period (a0, a1) from the nibble tables: 32 lookups xor-ed, two per three-input xor
+__device__ __forceinline__ uint64_t dmn_advance(const uint4 *lut, uint64_t a0, uint64_t a1,
+                                                uint64_t &n1) {
+  uint4 n = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+  for (int q = 0; q < 32; q += 2) {
+    const uint64_t a = q < 16 ? a0 : a1;
+    const int sh = 4 * (q & 15);
+    const uint4 v = lut[q * 16 + ((a >> sh) & 0xf)];
+    const uint4 w = lut[(q + 1) * 16 + ((a >> (sh + 4)) & 0xf)];
+    n.x = xor3(n.x, v.x, w.x);
+    n.y = xor3(n.y, v.y, w.y);
+    n.z = xor3(n.z, v.z, w.z);
+    n.w = xor3(n.w, v.w, w.w);
+  }
+  n1 = ((uint64_t)n.w << 32) | n.z;
+  return ((uint64_t)n.y << 32) | n.x;
+}
+
 __global__ __launch_bounds__(256) void k_dropout_mask(uint64_t *__restrict__ states,
                                                       long long n_chunks, long long elem0,
                                                       long long elem_end, int threshold,
@@ -84,19 +118,8 @@ __global__ __launch_bounds__(256) void k_dropout_mask(uint64_t *__restrict__ sta
       word = valid <= 0 ? 0 : (word & ((valid >= 64) ? ~0ull : ((1ull << valid) - 1)));
     }
     mask[c] = word;
-    uint64_t n0 = 0, n1 = 0;
-#pragma unroll
-    for (int q = 0; q < 16; q++) {
-      const uint4 v = lut[q * 16 + ((a0 >> (4 * q)) & 0xf)];
-      n0 ^= ((uint64_t)v.y << 32) | v.x;
-      n1 ^= ((uint64_t)v.w << 32) | v.z;
-    }
-#pragma unroll
-    for (int q = 0; q < 16; q++) {
-      const uint4 v = lut[(16 + q) * 16 + ((a1 >> (4 * q)) & 0xf)];
-      n0 ^= ((uint64_t)v.y << 32) | v.x;
-      n1 ^= ((uint64_t)v.w << 32) | v.z;
-    }
+    uint64_t n1;
+    const uint64_t n0 = dmn_advance(lut, a0, a1, n1);
     states[2 * c] = n0;
     states[2 * c + 1] = n1;
   };
@@ -137,25 +160,6 @@ __global__ __launch_bounds__(256) void k_dropout_mask(uint64_t *__restrict__ sta
 // assembly.  Two chunks per thread, their xorshift chains interleaved (k_dropout_mask's
 // latency hiding).
 constexpr int DMN_MAX_CHUNKS = 2048;
-__device__ __forceinline__ uint64_t dmn_advance(const uint4 *lut, uint64_t a0, uint64_t a1,
-                                                uint64_t &n1) {
-  uint64_t n0 = 0;
-  n1 = 0;
-#pragma unroll
-  for (int q = 0; q < 16; q++) {
-    const uint4 v = lut[q * 16 + ((a0 >> (4 * q)) & 0xf)];
-    n0 ^= ((uint64_t)v.y << 32) | v.x;
-    n1 ^= ((uint64_t)v.w << 32) | v.z;
-  }
-#pragma unroll
-  for (int q = 0; q < 16; q++) {
-    const uint4 v = lut[(16 + q) * 16 + ((a1 >> (4 * q)) & 0xf)];
-    n0 ^= ((uint64_t)v.y << 32) | v.x;
-    n1 ^= ((uint64_t)v.w << 32) | v.z;
-  }
-  return n0;
-}
-
 __global__ __launch_bounds__(1024) void k_dropout_mask_nib(
     uint64_t *__restrict__ states, long long n_chunks, long long elem0, long long elem_end,
     int threshold, uint64_t *__restrict__ mask, const uint4 *__restrict__ table,

@@ -232,7 +232,7 @@ ENGINE_DEFAULTS = {"train_ahead": 1, "split_rows": 0, "split_cols": 1, "eval_ax"
                    "epoch_graph": 0, "fuse_epilogue": 7, "fuse_output": 2, "mm_side": 0,
                    "xstream_ring": 1, "gemm_variant": 0, "lds_min_kb": -1, "lds_blocks": 0,
                    "parse_threads": 0, "wide_prescale": 1, "rs_chunks": 1, "lds_slots": 0,
-                   "mask_nib": 1}
+                   "mask_nib": 0}
 
 
 @contextlib.contextmanager
