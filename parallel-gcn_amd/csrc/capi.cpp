@@ -32,6 +32,7 @@ extern long long g_lds_min_bytes;   // host/graph.cpp
 extern int g_lds_blocks;            // host/graph.cpp
 extern int g_lds_slots;             // host/graph.cpp
 extern int g_xstream_ring;          // k_xstream_lds.hip
+extern int g_plain_blocks;          // host/graph.cpp
 extern int g_parse_threads;         // host/data.cpp: pieces of the parallel text parse
 
 namespace {
@@ -684,6 +685,9 @@ int pgcn_debug_set(const char *key, int value) {
         value != 32)
       return PGCN_E_INVALID;
     pgcn::g_lds_blocks = value;
+  } else if (!std::strcmp(key, "plain_blocks")) {
+    if (!in(0, 1)) return PGCN_E_INVALID;
+    pgcn::g_plain_blocks = value;
   } else if (!std::strcmp(key, "lds_slots")) {
     if (value != 0 && !ring_slots_ok(value)) return PGCN_E_INVALID;
     pgcn::g_lds_slots = value;

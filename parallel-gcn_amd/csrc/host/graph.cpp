@@ -117,7 +117,12 @@ DevGraph::DevGraph(int n_rows, int n_cols, const int *indptr, const int *indices
 long long g_lds_min_bytes = DevGraph::kLdsMinBytes;
 int g_wide_prescale = 1;  // diagnostics ("wide_prescale" 0: one prescale launch per pass)
 
+// "plain_blocks" (read at schedule build): 0 = the plain path blocks its columns per XCD above
+// kL2Budget, 1 = never (one block: whole rows per item)
+int g_plain_blocks = 0;
+
 int DevGraph::column_blocks(int dim) {
+  if (g_plain_blocks == 1) return 1;
   const int vec = (dim + 3) / 4;
   const double table = (double)n_cols_ * vec * 16.0;
   return (graphsum_group_lanes(vec) < 64 && table > kL2Budget) ? kBlocks : 1;
