@@ -833,13 +833,15 @@ __global__ __launch_bounds__(1024) void k_reduce_scalars(const float *__restrict
         wr += v[u].y;
       }
   }
-  for (long long i0 = threadIdx.x; i0 < n_w; i0 += U * 1024) {
-    float v[U];
+  // the weights: 32 loads in flight per thread (r04: citeseer's 59 k-float W1 took 7 rounds
+  // of 8; a thread's elements are still added in index order, so the same bits)
+  constexpr int UW = 32;
+  for (long long i0 = threadIdx.x; i0 < n_w; i0 += UW * 1024) {
+    float v[UW];
 #pragma unroll
-    for (int u = 0; u < U; u++)
-      if (i0 + u * 1024 < n_w) v[u] = w[i0 + u * 1024];
+    for (int u = 0; u < UW; u++) v[u] = i0 + u * 1024 < n_w ? w[i0 + u * 1024] : 0.0f;
 #pragma unroll
-    for (int u = 0; u < U; u++)
+    for (int u = 0; u < UW; u++)
       if (i0 + u * 1024 < n_w) q += v[u] * v[u];
   }
   l = block_sum<1024>(l, red);

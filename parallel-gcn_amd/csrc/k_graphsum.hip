@@ -75,7 +75,25 @@ __global__ __launch_bounds__(256) void k_graphsum(const int4 *__restrict__ items
         acc = f4_fma(w2, x2, acc);
         acc = f4_fma(w3, x3, acc);
       }
-      for (; j < end; j += NB) acc = f4_fma(vals[j], in[(long long)indices[j] * ld4_in + v], acc);
+      // the last (at most 3) neighbours of this lane: predicated, their index / value loads
+      // together and then their gathers (r04: one dependent load pair per neighbour made a
+      // low-degree row -- cora's are 4-5 -- several round trips long); same adds, same order
+      if (j < end) {
+        int cc[3];
+        float ww[3];
+#pragma unroll
+        for (int u = 0; u < 3; u++) {  // (clamped, unpredicated: a missing neighbour re-reads
+          const int jj = min(j + u * NB, end - 1);  // the last one and is not added)
+          cc[u] = indices[jj];
+          ww[u] = vals[jj];
+        }
+        float4 xx[3];
+#pragma unroll
+        for (int u = 0; u < 3; u++) xx[u] = in[(long long)cc[u] * ld4_in + v];
+#pragma unroll
+        for (int u = 0; u < 3; u++)
+          if (j + u * NB < end) acc = f4_fma(ww[u], xx[u], acc);
+      }
     }
     if constexpr (POW2) {
 #pragma unroll

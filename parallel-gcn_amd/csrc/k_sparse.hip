@@ -62,42 +62,53 @@ __global__ __launch_bounds__(256) void k_spmm_csr(int m, int p, int ldc,
 }
 
 // One workgroup per (feature f, 16 gradient columns).  The serial chain of a column's
-// contributions (row order, the CPU's scatter order) is latency-free: all 256 threads gather a
-// chunk of 256 entries' products into LDS at once (one 64-B row of G per entry), then 16 lanes
+// contributions (row order, the CPU's scatter order) is latency-free: all CH threads gather a
+// chunk of CH entries' products into LDS at once (one 64-B row of G per entry), then 16 lanes
 // add them in entry order from LDS.  Same products, same order => the same bits as a lane
 // walking the column alone (the r01 kernel, 1.9 ms on pubmed: 32 workgroups, one dependent
-// gather per entry).
-constexpr int kCscChunk = 256;
-__global__ __launch_bounds__(kCscChunk) void k_spmm_csc_bwd(int nf, int p, int ldg,
-                                                            const int *__restrict__ csc_ptr,
-                                                            const int *__restrict__ csc_row,
-                                                            const int *__restrict__ csc_pos,
-                                                            const float *__restrict__ a,
-                                                            const uint64_t *__restrict__ mask,
-                                                            long long mask_base, float scale,
-                                                            const float *__restrict__ cgrad,
-                                                            float *__restrict__ bgrad) {
-  __shared__ float prod[kCscChunk][17];
+// gather per entry).  CH = 256, or 1024 when the features average more than 512 entries (r04:
+// pubmed's ~2,000-entry columns took 8 chunks of two dependent load rounds each, 38.9 us per
+// call; each chunk's adds wait for its loads, so fewer, longer chunks shorten the chain).
+template <int CH>
+__global__ __launch_bounds__(CH) void k_spmm_csc_bwd(int nf, int p, int ldg,
+                                                     const int *__restrict__ csc_ptr,
+                                                     const int *__restrict__ csc_row,
+                                                     const int *__restrict__ csc_pos,
+                                                     const float *__restrict__ a,
+                                                     const uint64_t *__restrict__ mask,
+                                                     long long mask_base, float scale,
+                                                     const float *__restrict__ cgrad,
+                                                     float *__restrict__ bgrad) {
+  __shared__ float prod[CH][17];
   const int f = blockIdx.x, k0 = blockIdx.y * 16, tid = threadIdx.x;
   const int e0 = csc_ptr[f], e1 = csc_ptr[f + 1];
   float sum = 0.0f;
-  for (int base = e0; base < e1; base += kCscChunk) {
+  for (int base = e0; base < e1; base += CH) {
     const int e = base + tid;
     if (e < e1) {
       const int pos = csc_pos[e];
-      const float av = drop_val(a[pos], mask, mask_base + pos, scale);
       const float *g = cgrad + (long long)csc_row[e] * ldg + k0;
       if ((ldg & 3) == 0) {  // engine layout: ld a multiple of 4, padding columns zero
+        // the value, its mask word and the G row in one round trip (drop_val's product
+        // after them: a load used where it is issued is waited for alone)
+        const float ar = a[pos];
+        const uint64_t mw = mask ? mask[(mask_base + pos) >> 6] : 0ull;
+        float4 gv[4];
+#pragma unroll
+        for (int c4 = 0; c4 < 4; c4++)
+          gv[c4] = k0 + 4 * c4 < ldg ? *reinterpret_cast<const float4 *>(g + 4 * c4)
+                                     : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        const float av = mask ? ar * (((mw >> ((mask_base + pos) & 63)) & 1) ? scale : 0.0f) : ar;
 #pragma unroll
         for (int c4 = 0; c4 < 4; c4++) {
-          float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-          if (k0 + 4 * c4 < ldg) v = *reinterpret_cast<const float4 *>(g + 4 * c4);
+          const float4 v = gv[c4];
           prod[tid][4 * c4 + 0] = v.x * av;
           prod[tid][4 * c4 + 1] = v.y * av;
           prod[tid][4 * c4 + 2] = v.z * av;
           prod[tid][4 * c4 + 3] = v.w * av;
         }
       } else {
+        const float av = drop_val(a[pos], mask, mask_base + pos, scale);
 #pragma unroll
         for (int c = 0; c < 16; c++) prod[tid][c] = k0 + c < p ? g[c] * av : 0.0f;
       }
@@ -106,7 +117,7 @@ __global__ __launch_bounds__(kCscChunk) void k_spmm_csc_bwd(int nf, int p, int l
     if (tid < 16) {
       // (r04: 32 LDS reads in flight per wait, was 8: the serial add chain of a long column
       // no longer waits on the LDS between every 8 adds)
-      const int n = min(kCscChunk, e1 - base);
+      const int n = min(CH, e1 - base);
       int j = 0;
       for (; j + 32 <= n; j += 32) {
         float v[32];
@@ -141,11 +152,15 @@ void launch_spmm_csr(int m, int p, int ldc, const int *indptr, const int *indice
 void launch_spmm_csc_bwd(int nf, int p, int ldg, const int *csc_ptr, const int *csc_row,
                          const int *csc_pos, const float *a, const uint64_t *mask,
                          long long mask_base, float scale, const float *cgrad, float *bgrad,
-                         hipStream_t s) {
+                         hipStream_t s, long long nnz) {
   if (nf <= 0 || p <= 0) return;
-  PGCN_LAUNCH(k_spmm_csc_bwd, dim3((unsigned)nf, (unsigned)ceil_div(p, 16)),
-                     dim3(kCscChunk), 0, s, nf, p, ldg, csc_ptr, csc_row, csc_pos, a, mask,
-                     mask_base, scale, cgrad, bgrad);
+  const dim3 grid((unsigned)nf, (unsigned)ceil_div(p, 16));
+  if (nnz > 512LL * nf)
+    PGCN_LAUNCH(k_spmm_csc_bwd<1024>, grid, dim3(1024), 0, s, nf, p, ldg, csc_ptr, csc_row,
+                csc_pos, a, mask, mask_base, scale, cgrad, bgrad);
+  else
+    PGCN_LAUNCH(k_spmm_csc_bwd<256>, grid, dim3(256), 0, s, nf, p, ldg, csc_ptr, csc_row,
+                csc_pos, a, mask, mask_base, scale, cgrad, bgrad);
 }
 
 }  // namespace pgcn

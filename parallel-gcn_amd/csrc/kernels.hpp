@@ -190,10 +190,11 @@ void launch_gemm_tn(int M, int N, int K, const float *A, int lda, const float *G
 void launch_spmm_csr(int m, int p, int ldc, const int *indptr, const int *indices,
                      const float *a, const uint64_t *mask, long long mask_base, float scale,
                      const float *b, float *c, hipStream_t s);
+// nnz: the entries of all nf columns (picks the chunk size; 0 = unknown: 256)
 void launch_spmm_csc_bwd(int nf, int p, int ldg, const int *csc_ptr, const int *csc_row,
                          const int *csc_pos, const float *a, const uint64_t *mask,
                          long long mask_base, float scale, const float *cgrad, float *bgrad,
-                         hipStream_t s);
+                         hipStream_t s, long long nnz = 0);
 
 void launch_dropout_mask(uint64_t *states, long long n_chunks, long long elem0,
                          long long elem_end, float p, uint64_t *mask, const void *table,
