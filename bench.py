@@ -149,8 +149,11 @@ def maybe_launch(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # (r04: the GPU's epoch time settles over its first ~15 epochs -- clocks ramping --
+    # 572.6 epochs/s timed over 20 steps after 3 warmup epochs, 591.7 over 100 after 20 and
+    # 591.5 over 200 after 50 on one box, profiles/r04/bench_window.txt; 100 steps take ~0.2 s)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default="reddit-114M", choices=sorted(WORKLOADS))
     ap.add_argument("--cpu-epochs", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
