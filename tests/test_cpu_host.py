@@ -499,10 +499,10 @@ def test_no_kernel_spills_to_scratch(tmp_path):
 def test_ring_kernel_lds_reads_wait_before_use(tmp_path):
     """k_graphsum_ring issues its LDS reads from inline asm (lds_dma.hpp ds_rd128 / ds_rd64_into):
     hipcc believes their results ready at once, so correctness rests on no instruction reading
-    or moving a destination register before the s_waitcnt lgkmcnt(0) that the asm lgkm_wait
-    places.  Walks the gfx950 disassembly in order: from each ds_read_b128 / ds_read_b64 to the
-    next lgkmcnt(0) wait, no instruction may name its destination registers (a compiler upgrade
-    that inserted a v_mov there would otherwise show up only as wrong sums)."""
+    or moving a destination register before the s_waitcnt lgkmcnt(N) that retires the read
+    (the asm lgkm_wait).  Walks the gfx950 disassembly in order, keeping the lgkm queue: until
+    a wait retires a read, no instruction may name its destination registers (a compiler
+    upgrade that inserted a v_mov there would otherwise show up only as wrong sums)."""
     import re
     import subprocess
     obj = [o for o in _kernel_objects() if o.endswith("k_graphsum_ring.o")]
@@ -521,8 +521,12 @@ def test_ring_kernel_lds_reads_wait_before_use(tmp_path):
             else:
                 out.update(range(int(m.group(1)), int(m.group(2)) + 1))
         return out
+    # every LDS / scalar-memory operation takes a place in the lgkm queue (LDS operations
+    # complete in issue order); s_waitcnt lgkmcnt(N) retires all but the newest N, so a read's
+    # destination is free once N is below the number of operations issued after it
+    lgkm_ops = ("ds_", "s_load", "s_buffer_load", "s_sendmsg")
     for start in starts:
-        pending, bad, reads = set(), [], 0
+        queue, bad, reads = [], [], 0
         for line in asm[start + 1:]:
             if re.match(r"^[0-9a-f]+ <", line):
                 break
@@ -531,11 +535,22 @@ def test_ring_kernel_lds_reads_wait_before_use(tmp_path):
                 continue
             op, _, ops = t.partition(" ")
             ops = ops.split("//")[0]
-            if op == "s_waitcnt" and "lgkmcnt(0)" in ops:
-                pending.clear()
-            elif op in ("ds_read_b128", "ds_read_b64"):
-                pending |= regs(ops.split(",")[0])
+            if op == "s_waitcnt":
+                m = re.search(r"lgkmcnt\((\d+)\)", ops)
+                if m:
+                    n = int(m.group(1))
+                    queue = queue[len(queue) - n:] if n else []
+                continue
+            pending = set().union(*queue) if queue else set()
+            if op in ("ds_read_b128", "ds_read_b64"):
+                if pending & regs(ops.split(",", 1)[1] if "," in ops else ""):
+                    bad.append(t)
+                queue.append(regs(ops.split(",")[0]))
                 reads += 1
+            elif op.startswith(lgkm_ops):
+                if pending & regs(ops):
+                    bad.append(t)
+                queue.append(set())
             elif pending & regs(ops):
                 bad.append(t)
         assert reads >= 16, reads
