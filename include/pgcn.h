@@ -313,9 +313,10 @@ int pgcn_debug_rank_graph(int n, const int *indptr, const int *indices, int worl
  *   wave of the LDS schedule), "parse_threads" (0: up to 16), "wide_prescale" 0/1
  *   (a multi-pass GraphSum's tables prescaled by one launch, default 1), "rs_chunks" 1..4
  *   (edge-cut GraphSum row chunks at world > 1, default 1), "mask_nib" 0/1 (dense X's input
- *   dropout drawn into the flat bitmap and the GEMMs' nibble layout by one launch, default 1);
- * diagnostics: "split_rows" 0/1 (stale logits outside the split), "gemm_variant" 0/1 (the
- * general GEMM kernels only).  Returns PGCN_E_INVALID on an unknown key or on a value outside
+ *   dropout drawn into the flat bitmap and the GEMMs' nibble layout by one launch, default 0:
+ *   two launches); diagnostics: "split_rows" 0/1 (stale logits outside the split),
+ * "gemm_variant" 0/1 (the general GEMM kernels only), "plain_blocks" 0/1 (1: the plain
+ * GraphSum kernels never split rows into per-XCD column blocks).  Returns PGCN_E_INVALID on an unknown key or on a value outside
  * the key's range (nothing is changed then). */
 int pgcn_debug_set(const char *key, int value);
 /* Host-only check of the d = 16 LDS ring schedule (window must be 5) of a CSR pattern: builds
