@@ -45,8 +45,9 @@ namespace pgcn {
 
 // "xstream_ring": 1 = these kernels for the X-stream products where they apply (default),
 // 0 = the register-streamed k_xstream_nn / k_xstream_tn (the oracle-tested fallback of every
-// other width).  Measured and removed (r02): two groups in flight per loader wave, fewer
-// slots, and a TN split in which every consumer takes a share of K of every group (173 vs 137
+// other width).  Measured and removed (r02): two groups in flight per loader wave with fewer
+// slots (r04 keeps two in flight at the same slot count, publishing group t-1 after group t's
+// DMAs are issued: xl_load), and a TN split in which every consumer takes a share of K of every group (173 vs 137
 // us on reddit: every consumer then waits on every group).
 int g_xstream_ring = 1;
 
@@ -138,6 +139,7 @@ __device__ __forceinline__ void xl_load(const float *__restrict__ A, int lda, lo
     if (lane == 0) __atomic_store_n(ready + u % rg.nslot, (unsigned)(u + 1), __ATOMIC_RELAXED);
     asm volatile("" ::: "memory");
   };
+  int pend = -1;  // the group issued last, not yet published (its DMAs may still land)
   for (int t = wave; t < T; t += NL) {
     const int slot = t % rg.nslot;
     if (t >= rg.nslot) lds_wait_ge(freed + slot, (unsigned)(t - rg.nslot + 1));
@@ -158,8 +160,18 @@ __device__ __forceinline__ void xl_load(const float *__restrict__ A, int lda, lo
         glds16_nt(blk + (off < left ? off : 0), dst + (unsigned)(q * 1024));
       }
     }
+    // two groups in flight: the previous one lands while this one's DMAs are issued (at most
+    // NI of this group's pieces still counted; r04: X-stream passes 339 -> 329 us per epoch,
+    // most of it on TN, whose single loader had one group in flight)
+    if (pend >= 0) {
+      asm volatile("s_waitcnt vmcnt(%c0)" ::"n"(NI) : "memory");
+      publish(pend);
+    }
+    pend = t;
+  }
+  if (pend >= 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    publish(t);
+    publish(pend);
   }
 }
 
