@@ -33,6 +33,10 @@ extern int g_lds_blocks;            // host/graph.cpp
 extern int g_lds_slots;             // host/graph.cpp
 extern int g_xstream_ring;          // k_xstream_lds.hip
 extern int g_plain_blocks;          // host/graph.cpp
+extern int g_gs_split;              // host/graph.cpp
+extern int g_co_draw;               // host/gcn.cpp
+extern int g_gs_item_iters;         // host/graph.cpp
+extern int g_gs_orig_cols;          // host/graph.cpp
 extern int g_parse_threads;         // host/data.cpp: pieces of the parallel text parse
 
 namespace {
@@ -664,7 +668,7 @@ int pgcn_debug_set(const char *key, int value) {
     if (!in(0, 1)) return PGCN_E_INVALID;
     pgcn::g_epoch_graph = value;
   } else if (!std::strcmp(key, "fuse_epilogue")) {
-    if (!in(0, 7)) return PGCN_E_INVALID;
+    if (!in(0, 15)) return PGCN_E_INVALID;
     pgcn::g_fuse_epilogue = value;
   } else if (!std::strcmp(key, "fuse_output")) {
     if (!in(0, 3)) return PGCN_E_INVALID;
@@ -688,6 +692,18 @@ int pgcn_debug_set(const char *key, int value) {
   } else if (!std::strcmp(key, "plain_blocks")) {
     if (!in(0, 1)) return PGCN_E_INVALID;
     pgcn::g_plain_blocks = value;
+  } else if (!std::strcmp(key, "gs_orig_cols")) {
+    if (!in(0, 1)) return PGCN_E_INVALID;
+    pgcn::g_gs_orig_cols = value;
+  } else if (!std::strcmp(key, "co_draw")) {
+    if (!in(0, 1)) return PGCN_E_INVALID;
+    pgcn::g_co_draw = value;
+  } else if (!std::strcmp(key, "gs_split")) {
+    if (!in(0, 3)) return PGCN_E_INVALID;
+    pgcn::g_gs_split = value;
+  } else if (!std::strcmp(key, "gs_item_iters")) {
+    if (value != 2 && value != 4 && value != 8 && value != 16 && value != 32) return PGCN_E_INVALID;
+    pgcn::g_gs_item_iters = value;
   } else if (!std::strcmp(key, "lds_slots")) {
     if (value != 0 && !ring_slots_ok(value)) return PGCN_E_INVALID;
     pgcn::g_lds_slots = value;

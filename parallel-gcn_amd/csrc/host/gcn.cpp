@@ -35,14 +35,20 @@ int g_split_cols = 1;
 //   2 (kFusePrestage) ... and that epilogue also writes the next GraphSum's prescaled input
 //                     table, which then skips its prescale launch;
 //   4 (kFuseXstream)  the first layer's X-stream product applies the eval ReLU / writes the
-//                     first GraphSum's table.
-int g_fuse_epilogue = kFuseTails | kFusePrestage | kFuseXstream;
+//                     first GraphSum's table;
+//   8 (kFuseMatmulTails) the Dropout / ReLU backward before a Matmul run in its input-grad
+//                     product's final write (k_xstream_nn: outputs of <= 16 columns; the
+//                     small graphs' second layer -- two launches fewer per epoch).
+int g_fuse_epilogue = kFuseTails | kFusePrestage | kFuseXstream | kFuseMatmulTails;
 // "fuse_output" (read at engine build): 0 = separate Matmul + loss; 1 = the output layer's
 // Matmul forward and input grad run inside the loss (launch_out_xent) when the Matmul produces
 // the logits (the reassociated order: GraphSum, then Matmul) from at most 16 columns
 // (bit-identical); 2 (default) = ... and its weight grad's block partials on graphs of >=
 // 65,536 rows or on an edge-cut rank (the same sums in another grouping); 3 = ... on any graph
 int g_fuse_output = 2;
+// "co_draw" (read at engine build): the hidden dropout's mask drawn in the input dropout's
+// launch (sparse X; bit-identical)
+int g_co_draw = 1;
 // "mm_side" (read at engine build): Matmul weight gradients on the side stream (ModuleContext)
 // on graphs of at least kMmSideRows rows; 2 = on every graph.  Off: r02 A/B on reddit-114M,
 // three runs each, 486.5 (on) vs 487.4 (off) epochs/s -- the LDS GraphSum holds every CU with
@@ -526,6 +532,9 @@ void GCN::build(const GCNData &data) {
                               feats.rows);
   // (edge-cut: the tails run in k_gs_finish on the rank's rows after the reduce-scatter)
   if (g_fuse_epilogue & kFuseTails) fuse_epilogues();
+  if (g_fuse_epilogue & kFuseMatmulTails) fuse_matmul_tails();
+  if (g_co_draw && dropouts_.size() >= 2 && !feats.dense && dropouts_[0] && dropouts_[1])
+    const_cast<Dropout *>(dropouts_[0])->co_draw = dropouts_[1];
   if (g_fuse_output) fuse_output_layer();
   optimizer = Adam(weights, decays, adam_params);
   PGCN_HIP(hipDeviceSynchronize());
@@ -578,6 +587,34 @@ void GCN::fuse_epilogues() {
         if (next && next->output() == in) gs->bwd_next = next;
       }
     }
+  }
+}
+
+// ReLU(a) [-> Dropout(a)] -> Matmul(a, W): the backward of the Dropout and the ReLU follow the
+// Matmul's, which applies them to a.grad as it writes it (Matmul::backward decides per call
+// whether its product runs on the kernel that can).  Only where a's element order is its
+// storage order, and not for a ReLU a GraphSum backward already applies.
+void GCN::fuse_matmul_tails() {
+  const size_t n = modules.size();
+  for (size_t i = 1; i < n; i++) {
+    auto *mm = dynamic_cast<Matmul *>(modules[i].get());
+    if (!mm || mm->input()->ld != mm->input()->cols) continue;
+    const Variable *a = mm->input(), *c = mm->output();
+    if (!xstream_ok(a->cols, c->cols) || xstream_ring_ok(c->cols, c->ld)) continue;
+    auto *drop = dynamic_cast<Dropout *>(modules[i - 1].get());
+    if (drop && drop->variable() != a) drop = nullptr;
+    const size_t ri = drop ? i - 2 : i - 1;
+    auto *relu = ri < n ? dynamic_cast<ReLU *>(modules[ri].get()) : nullptr;
+    if (!relu || relu->variable() != a) continue;
+    bool taken = false;
+    for (auto &m : modules) {
+      auto *gs = dynamic_cast<GraphSum *>(m.get());
+      if (gs && gs->bwd_relu == relu) taken = true;
+    }
+    if (taken) continue;
+    mm->bwd_relu = relu;
+    mm->bwd_drop = drop;
+    fused_tails_++;
   }
 }
 

@@ -122,6 +122,7 @@ class GCN {
   void insert_layer(int in_dim, int out_dim, float dropout, int layer);
   void insert_last_layer();
   void fuse_epilogues();
+  void fuse_matmul_tails();
   void fuse_output_layer();
   void join_side();
   int fused_tails_ = 0;  // GraphSum epilogues carrying ReLU / Dropout work (forward + backward)

@@ -121,6 +121,25 @@ int g_wide_prescale = 1;  // diagnostics ("wide_prescale" 0: one prescale launch
 // kL2Budget, 1 = never (one block: whole rows per item)
 int g_plain_blocks = 0;
 
+// "gs_split" (read at schedule build), the rows of the plain unblocked path longer than one
+// work item: 0 = their items write slots that a combine launch sums; 1 = the last of a row's
+// items to finish sums them in the same launch (an arrival counter per row, the combine's
+// order: the same bits), on graphs of <= kSmallNnz slots (each arrival writes its XCD's L2
+// back: costly when many rows split -- pubmed_synth lost 4 % at 8-iteration items); 2 = on
+// those graphs, rows up to 8 items long stay one item (no slots; another summation order);
+// 3 = as 1, but rows of up to 8 workgroup-wide iterations are summed by one whole workgroup
+// (4 waves, an LDS reduce in wave order: no cross-workgroup hand-off; another summation
+// order), power-of-two row widths
+int g_gs_split = 3;
+// "gs_item_iters" (read at schedule build): group iterations per work item of the plain
+// unblocked path on graphs of <= kSmallNnz slots with gs_split 1 (32 elsewhere).  A small
+// graph's GraphSum lasts as long as its longest item (one index -> gather round trip per
+// iteration), so its hub rows are cut short and summed in-kernel.
+int g_gs_item_iters = 8;
+// "gs_orig_cols" (read per call): a column subset's unblocked plain GraphSum gathers the
+// input's own rows through the original column ids (1) instead of compacting them first (0)
+int g_gs_orig_cols = 1;
+
 int DevGraph::column_blocks(int dim) {
   if (g_plain_blocks == 1) return 1;
   const int vec = (dim + 3) / 4;
@@ -199,18 +218,28 @@ DevGraph::Sched &DevGraph::schedule(int vec) {
   std::vector<int> block_items(1, 0);
   long long slots = 0;
   int chunk;
+  std::vector<int> slot_comb;
+  std::vector<int4> wide;
   if (nbc == 1) {
+    const bool small = nnz_ <= kSmallNnz;
+    const bool arrive = (g_gs_split == 1 || g_gs_split == 3) && small;
     chunk = nb * 32;  // 32 group iterations per work item
+    if (arrive) chunk = nb * g_gs_item_iters;
+    const int whole = g_gs_split == 2 && small ? 8 * chunk : chunk;
+    const int wide_max = g_gs_split == 3 && small && (vec & (vec - 1)) == 0 ? 256 / vec * 8 : 0;
     items.reserve((size_t)n_rows_ + (size_t)(nnz_ / chunk) + 1);
     for (int r = 0; r < n_rows_; r++) {
       const int b = h_indptr_[(size_t)r], e = h_indptr_[(size_t)r + 1];
-      if (e - b <= chunk) {
+      if (e - b <= whole) {
         items.push_back(make_int4(r, b, e, -1));
+      } else if (e - b <= wide_max) {
+        wide.push_back(make_int4(r, b, e, -1));
       } else {
         const int first = (int)slots;
         int cnt = 0;
         for (int p = b; p < e; p += chunk) {
           items.push_back(make_int4(r, p, std::min(e, p + chunk), (int)slots++));
+          if (arrive) slot_comb.push_back((int)comb.size());
           cnt++;
         }
         comb.push_back(make_int4(r, first, cnt, 0));
@@ -276,6 +305,23 @@ DevGraph::Sched &DevGraph::schedule(int vec) {
   sp->s.items = sp->items.get();
   sp->s.block_items = sp->block_items.get();
   sp->s.comb = sp->comb.get();
+  if (!wide.empty()) {
+    // longest first: they start in the launch's first workgroups
+    std::stable_sort(wide.begin(), wide.end(),
+                     [](const int4 &a, const int4 &c) { return (a.z - a.y) > (c.z - c.y); });
+    sp->wide.allocate(wide.size());
+    sp->wide.upload(wide);
+    sp->s.n_wide = (int)wide.size();
+    sp->s.wide = sp->wide.get();
+  }
+  if (!slot_comb.empty()) {
+    sp->slot_comb.allocate(slot_comb.size());
+    sp->slot_comb.upload(slot_comb);
+    sp->comb_ctr.allocate(comb.size());
+    sp->comb_ctr.zero();
+    sp->s.slot_comb = sp->slot_comb.get();
+    sp->s.comb_ctr = sp->comb_ctr.get();
+  }
   auto &ref = *sp;
   scheds_[vec] = std::move(sp);
   return ref;
@@ -335,6 +381,11 @@ std::unique_ptr<DevGraph> DevGraph::col_subset(const std::vector<int> &cols) con
   }
   g->col_map_.allocate(std::max<size_t>(cols.size(), 1));
   g->col_map_.upload(cols.empty() ? std::vector<int>{0} : cols);
+  std::vector<int> ox(ix.size());
+  for (size_t k = 0; k < ix.size(); k++) ox[k] = cols.empty() ? 0 : cols[(size_t)ix[k]];
+  g->orig_indices_.allocate(ox.size() + 64);  // the same slack as indices_
+  g->orig_indices_.upload(ox);
+  PGCN_HIP(hipMemset(g->orig_indices_.get() + ox.size(), 0, 64 * sizeof(int)));
   return g;
 }
 
@@ -544,16 +595,17 @@ void DevGraph::graphsum(const float *in, int ld_in, float *out, int ld_out, int 
     }
     return;
   }
-  if (col_map) {  // plain path of a column subset: compact the input rows first
+  const int vec = (dim + 3) / 4;
+  Sched &sc = schedule(vec);
+  const bool blocked = sc.s.nbc > 1;
+  const bool orig = col_map && !blocked && g_gs_orig_cols;
+  if (col_map && !orig) {  // plain path of a column subset: compact the input rows first
     const size_t need = (size_t)n_cols_ * ld_in;
     if (col_in_.size() < need) col_in_.allocate(need);
     launch_gather_rows(in, col_map, n_cols_, ld_in, col_in_.get(), s);
     in = col_in_.get();
   }
-  const int vec = (dim + 3) / 4;
-  Sched &sc = schedule(vec);
-  const bool blocked = sc.s.nbc > 1;
-  launch_graphsum(sc.s, blocked ? bindices_.get() : indices_.get(),
+  launch_graphsum(sc.s, blocked ? bindices_.get() : (orig ? orig_indices_.get() : indices_.get()),
                   blocked ? bvals_.get() : vals_.get(), in, ld_in, out, ld_out, sc.partial.get(), s,
                   epi);
 }

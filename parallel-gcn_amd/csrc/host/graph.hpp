@@ -118,14 +118,15 @@ class DevGraph {
 
   static constexpr int kBlocks = kGraphBlocks;   // one column block per XCD
   static constexpr double kL2Budget = 4.0e6;     // one XCD's L2: tables the plain kernel keeps whole
+  static constexpr long long kSmallNnz = 1 << 20;  // g_gs_split 2: graphs that keep long rows whole
   static constexpr long long kLdsMinBytes = 1 << 20;  // d = 16 tables above: LDS GraphSum ...
   static constexpr int kLdsMinRows = 32768;           // ... when the rows fill its workgroups
 
  private:
   struct Sched {
     GraphSchedule s;
-    DeviceBuffer<int4> items, comb;
-    DeviceBuffer<int> block_items;
+    DeviceBuffer<int4> items, comb, wide;
+    DeviceBuffer<int> block_items, slot_comb, comb_ctr;
     DeviceBuffer<float> partial;
   };
   Sched &schedule(int vec);
@@ -150,6 +151,9 @@ class DevGraph {
   // column subset: input row of compact column c (device), and the compacted input (plain path)
   DeviceBuffer<int> col_map_;
   DeviceBuffer<float> col_in_;
+  // column subset, unblocked plain path: every slot's ORIGINAL column id, so the gather kernel
+  // reads the caller's full input rows (no compacting launch; the same values, the same bits)
+  DeviceBuffer<int> orig_indices_;
   int n_rows_, n_cols_;
   long long nnz_;
   std::vector<int> h_indptr_, h_indices_;

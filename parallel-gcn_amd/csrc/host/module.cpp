@@ -108,7 +108,10 @@ void Dropout::wait_ahead(hipStream_t s) const {
 
 void Dropout::draw_fused(hipStream_t s) const {
   PGCN_CHECK(in && !ahead, PGCN_E_INVALID, "dropout: fused draw of a hidden dropout only");
-  draw(s, rng->mask.get());
+  if (pre_drawn)
+    pre_drawn = false;
+  else
+    draw(s, rng->mask.get());
   skip_forward = true;
 }
 
@@ -123,6 +126,15 @@ void Dropout::forward(bool training, const Stream &s) const {
     wait_ahead(s.get());
     std::swap(rng->mask, rng->mask_ahead);
     ahead = false;
+  } else if (pre_drawn) {  // drawn with the input dropout's mask (co_draw)
+    pre_drawn = false;
+  } else if (co_draw && !nib_ && !co_draw->pre_drawn && !co_draw->ahead) {
+    const DropoutRng &q = co_draw->state();
+    const MaskDraw a{r.states.get(), r.n_chunks, 64 * r.chunk_lo, r.elem_end, p, r.mask.get()};
+    const MaskDraw b{q.states.get(), q.n_chunks, 64 * q.chunk_lo, q.elem_end, co_draw->p,
+                     q.mask.get()};
+    launch_dropout_mask2(a, b, ctx->jump_table, s.get());
+    co_draw->pre_drawn = true;
   } else {
     draw(s.get(), rng->mask.get());
   }
@@ -598,10 +610,24 @@ void Matmul::backward(const Stream &s) const {
                    b->ld, nullptr, 0, 0, 1.0f, ctx->gemm_workspace_side, ctx->side_stream);
     ctx->side_pending = true;
   }
-  // a.grad = c.grad * b^T   (b stored [n][p] => trans_b)
-  if (!a_done)
+  // a.grad = c.grad * b^T   (b stored [n][p] => trans_b); the Dropout / ReLU backward on a
+  // in its final write when gemm_nn would take k_xstream_nn anyway (same product, same bits)
+  if (!a_done && bwd_relu && !cmp && A.ld == n && xstream_ok(n, p) && !xstream_ring_ok(p, C.ld)) {
+    XsEpilogue e;
+    if (bwd_drop) {
+      e.bwd_drop = bwd_drop->state().mask.get();
+      e.drop_base = bwd_drop->state().mask_base;
+      e.drop_scale = bwd_drop->scale();
+      bwd_drop->skip_backward = true;
+    }
+    e.bwd_relu = bwd_relu->mask_ptr();
+    bwd_relu->skip_backward = true;
+    launch_xstream_nn(rows, n, p, C.dev_grad.get(), C.ld, b->dev_data.get(), b->ld, 1,
+                      A.dev_grad.get(), A.ld, nullptr, 1.0f, s.get(), nullptr, &e);
+  } else if (!a_done) {
     launch_gemm_nn(rows, n, p, C.dev_grad.get(), C.ld, b->dev_data.get(), b->ld, 1,
                    A.dev_grad.get(), A.ld, nullptr, 0, 0, 1.0f, s.get());
+  }
   // b.grad = a^T * c.grad (deterministic split-M reduction)
   if (!side && !b_done)
     launch_gemm_tn(rows, p, n, A.dev_data.get(), A.ld, C.dev_grad.get(), C.ld, b->dev_grad.get(),

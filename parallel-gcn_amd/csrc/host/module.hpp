@@ -89,7 +89,7 @@ class GraphSum;
 class Dropout;
 
 // "fuse_epilogue" bits (host/gcn.cpp g_fuse_epilogue) and "fuse_output" (g_fuse_output)
-constexpr int kFuseTails = 1, kFusePrestage = 2, kFuseXstream = 4;
+constexpr int kFuseTails = 1, kFusePrestage = 2, kFuseXstream = 4, kFuseMatmulTails = 8;
 extern int g_fuse_epilogue;
 extern int g_fuse_output;
 extern int g_mask_nib;
@@ -186,6 +186,11 @@ class Dropout : public Module {
   const Variable *variable() const { return in.get(); }
   void draw_fused(hipStream_t s) const;
   mutable bool skip_forward = false, skip_backward = false;
+  // the input dropout's training draw also draws `co_draw`'s mask (one launch: the same stream
+  // positions, so the same bits); that module's next forward / fused draw then uses it
+  // (GCN::build, "co_draw"; sparse X only: the dense input has its own layouts)
+  const Dropout *co_draw = nullptr;
+  mutable bool pre_drawn = false;
   // Dense X's input dropout: every draw also writes the X-stream / wide GEMM kernels' nibble
   // layout of its bits into `nib` ([rows][16], k_dropout_mask_nib: one launch for both
   // layouts); nibbles_of(mask, nib): `nib` holds the layout of the draw into `mask`
@@ -313,6 +318,10 @@ class Matmul : public Module {
   bool fused_forward = false;  // its forward runs inside the loss's (CrossEntropyLoss::fused)
   mutable bool input_grad_done = false;  // ... which also wrote a.grad (this training pass)
   mutable bool weight_grad_done = false;  // ... and b.grad
+  // the Dropout (and ReLU) on `a` whose backward follows this one's: applied in the a.grad
+  // product's final write when that product runs on k_xstream_nn (GCN::fuse_epilogues)
+  const Dropout *bwd_drop = nullptr;
+  ReLU *bwd_relu = nullptr;
   Matmul(shared_ptr<Variable> a_, shared_ptr<Variable> b_, shared_ptr<Variable> c_, int m_,
          int n_, int p_, ModuleContext *ctx_);
   const Variable *input() const { return a.get(); }

@@ -99,17 +99,23 @@ __device__ __forceinline__ uint64_t dmn_advance(const uint4 *lut, uint64_t a0, u
   return ((uint64_t)n.y << 32) | n.x;
 }
 
-__global__ __launch_bounds__(256) void k_dropout_mask(uint64_t *__restrict__ states,
-                                                      long long n_chunks, long long elem0,
-                                                      long long elem_end, int threshold,
-                                                      uint64_t *__restrict__ mask,
-                                                      const uint4 *__restrict__ table) {
-  __shared__ uint4 lut[32 * 16];
-  for (int i = threadIdx.x; i < 32 * 16; i += blockDim.x) {
-    const int p = i >> 4, v = i & 15;
-    lut[i] = table[(p >> 1) * 256 + (v << (4 * (p & 1)))];
-  }
-  __syncthreads();
+// One launch draws one or two variables' masks (MaskSeg b: the small graphs' hidden dropout
+// drawn beside the input's, r04 late: one launch fewer per epoch); workgroups [0, blocks_a)
+// take segment a, the rest segment b.  Every variable's chunk states advance by the same
+// period (the whole epoch's draws), so one jump table serves both.
+struct MaskSeg {
+  uint64_t *states = nullptr;
+  long long n_chunks = 0, elem0 = 0, elem_end = 0;
+  int threshold = 0;
+  uint64_t *mask = nullptr;
+};
+
+__device__ __forceinline__ void dropout_mask_seg(const MaskSeg &sg, const uint4 *lut, long long bid,
+                                                 long long nblk) {
+  uint64_t *__restrict__ states = sg.states;
+  uint64_t *__restrict__ mask = sg.mask;
+  const long long n_chunks = sg.n_chunks, elem0 = sg.elem0, elem_end = sg.elem_end;
+  const int threshold = sg.threshold;
   // mask word of chunk c, then its state advanced by `period` draws: M^period * (a0, a1)
   auto emit = [&](long long c, uint64_t a0, uint64_t a1, uint64_t word) {
     const long long e = elem0 + 64 * c;  // first element of this chunk
@@ -125,8 +131,8 @@ __global__ __launch_bounds__(256) void k_dropout_mask(uint64_t *__restrict__ sta
   };
   // two chunks per thread and iteration: two independent xorshift chains interleaved (each
   // draw is a serial chain of 64-bit ops; the pair hides their latency at low occupancy)
-  const long long G = (long long)gridDim.x * blockDim.x;
-  for (long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x; c < n_chunks; c += 2 * G) {
+  const long long G = nblk * blockDim.x;
+  for (long long c = bid * blockDim.x + threadIdx.x; c < n_chunks; c += 2 * G) {
     const long long c2 = c + G;
     const bool two = c2 < n_chunks;
     const long long cb = two ? c2 : c;
@@ -148,6 +154,20 @@ __global__ __launch_bounds__(256) void k_dropout_mask(uint64_t *__restrict__ sta
     emit(c, a0, a1, ((uint64_t)x.hi << 32) | x.lo);
     if (two) emit(c2, b0, b1, ((uint64_t)y.hi << 32) | y.lo);
   }
+}
+
+__global__ __launch_bounds__(256) void k_dropout_mask(MaskSeg a, MaskSeg b, int blocks_a,
+                                                      const uint4 *__restrict__ table) {
+  __shared__ uint4 lut[32 * 16];
+  for (int i = threadIdx.x; i < 32 * 16; i += blockDim.x) {
+    const int p = i >> 4, v = i & 15;
+    lut[i] = table[(p >> 1) * 256 + (v << (4 * (p & 1)))];
+  }
+  __syncthreads();
+  if ((int)blockIdx.x < blocks_a)
+    dropout_mask_seg(a, lut, blockIdx.x, blocks_a);
+  else
+    dropout_mask_seg(b, lut, blockIdx.x - blocks_a, gridDim.x - blocks_a);
 }
 
 // The input dropout of dense X straight into both layouts its users read (r04): the flat
@@ -925,8 +945,34 @@ void launch_dropout_mask(uint64_t *states, long long n_chunks, long long elem0,
   const int threshold = (int)(p * (float)0x7fffffff);
   // 8 KB LDS: up to 8 workgroups per CU (a side-stream draw takes fewer: max_blocks)
   const int grid = grid_for(ceil_div(n_chunks, 2), 256, max_blocks > 0 ? max_blocks : 8 * kCUs);
-  PGCN_LAUNCH(k_dropout_mask, dim3(grid), dim3(256), 0, s, states, n_chunks, elem0,
-                     elem_end, threshold, mask, static_cast<const uint4 *>(table));
+  MaskSeg a;
+  a.states = states;
+  a.n_chunks = n_chunks;
+  a.elem0 = elem0;
+  a.elem_end = elem_end;
+  a.threshold = threshold;
+  a.mask = mask;
+  PGCN_LAUNCH(k_dropout_mask, dim3(grid), dim3(256), 0, s, a, MaskSeg{}, grid,
+              static_cast<const uint4 *>(table));
+}
+
+void launch_dropout_mask2(const MaskDraw &d0, const MaskDraw &d1, const void *table,
+                          hipStream_t s) {
+  MaskSeg sg[2];
+  int g[2];
+  const MaskDraw *d[2] = {&d0, &d1};
+  for (int i = 0; i < 2; i++) {
+    sg[i].states = d[i]->states;
+    sg[i].n_chunks = d[i]->n_chunks;
+    sg[i].elem0 = d[i]->elem0;
+    sg[i].elem_end = d[i]->elem_end;
+    sg[i].threshold = (int)(d[i]->p * (float)0x7fffffff);  // as launch_dropout_mask
+    sg[i].mask = d[i]->mask;
+    g[i] = sg[i].n_chunks > 0 ? grid_for(ceil_div(sg[i].n_chunks, 2), 256, 8 * kCUs) : 0;
+  }
+  if (g[0] + g[1] == 0) return;
+  PGCN_LAUNCH(k_dropout_mask, dim3(g[0] + g[1]), dim3(256), 0, s, sg[0], sg[1], g[0],
+              static_cast<const uint4 *>(table));
 }
 
 // rows_per_wg: whole multiples of 64 / gcd(F, 64) rows (their bits end on a chunk boundary)

@@ -261,6 +261,11 @@ __global__ __launch_bounds__(256, 2) void k_xstream_nn(int M, int N, int K, int 
         if (rr < M) {
           float c = acc[r];
           if constexpr (!DUAL) {
+            if (epi.bwd_drop) {
+              const long long b = epi.drop_base + rr * ldc + i;
+              c *= ((epi.bwd_drop[b >> 6] >> (b & 63)) & 1) ? epi.drop_scale : 0.0f;
+            }
+            if (epi.bwd_relu && !epi.bwd_relu[rr * ldc + i]) c = 0.0f;
             if (epi.relu && !(c > 0.0f)) c = 0.0f;  // k_relu_fwd's test (NaN -> 0)
             if (epi.next_table) {  // k_ring_prescale of the stored value: s_r * C[r][i]
               const long long sr = epi.next_sr;
@@ -338,6 +343,10 @@ __device__ __forceinline__ void tn_compute(TnStep<KC, MASKED> &st, floatx4 (&acc
 #define PGCN_TN_SETS 3
 #endif
 constexpr int XS_TN_BLOCKS = 256;  // one 4-wave block per CU (1 wave per SIMD, ~300 registers)
+// small products (<= XS_TN_SMALL_ROWS rows: the small graphs' layers) take 32 blocks, whose
+// partials one ordered pass reduces (r04 late: one launch fewer per call; the blocks' steps
+// stay a few per wave)
+constexpr int XS_TN_SMALL_ROWS = 16384, XS_TN_SMALL_BLOCKS = 32, TN_ONE_PASS = 32;
 
 template <int KC, bool MASKED>
 __global__ __launch_bounds__(256, 1) void k_xstream_tn(int M, int N, int K,
@@ -603,7 +612,8 @@ void launch_xstream_nn(int M, int N, int K, const float *A, int lda, const float
                        hipStream_t s, float *C2, const XsEpilogue *epi) {
   const XsEpilogue none{};
   const XsEpilogue &e = epi ? *epi : none;
-  PGCN_CHECK(!C2 || (!e.relu && !e.next_table), PGCN_E_INVALID, "xstream_nn: dual + epilogue");
+  PGCN_CHECK(!C2 || (!e.relu && !e.next_table && !e.bwd_drop && !e.bwd_relu), PGCN_E_INVALID,
+             "xstream_nn: dual + epilogue");
   PGCN_CHECK(!e.next_table || (N <= 16 && ldc == 16), PGCN_E_INVALID,
              "xstream_nn: a staged table needs 16-column rows");
   PGCN_CHECK(xstream_ok(N, K), PGCN_E_INVALID, "xstream_nn: needs N <= 16, K <= 640");
@@ -611,6 +621,7 @@ void launch_xstream_nn(int M, int N, int K, const float *A, int lda, const float
   PGCN_CHECK(lda % 4 == 0 && lda >= K, PGCN_E_INVALID, "gemm: lda must be a multiple of 4 >= K");
   if (M <= 0) return;
   if (xstream_ring_ok(K, lda)) {
+    PGCN_CHECK(!e.bwd_drop && !e.bwd_relu, PGCN_E_INVALID, "xstream_nn: backward tails on the ring form");
     launch_xstream_nn_ring(M, N, K, A, lda, B, ldb, trans_b, C, ldc, maskT, a_scale, s, C2, e);
     return;
   }
@@ -714,12 +725,16 @@ static TnPlan tn_plan(int M, int N, int K) {
   return p;
 }
 
-static TnPlan xs_tn_plan(int K) {  // k_xstream_tn: one [K][16] partial per block
+static int xs_tn_blocks(int M, int K, int lda) {
+  return M <= XS_TN_SMALL_ROWS && !xstream_ring_ok(K, lda) ? XS_TN_SMALL_BLOCKS : XS_TN_BLOCKS;
+}
+
+static TnPlan xs_tn_plan(int K, int blocks) {  // k_xstream_tn: one [K][16] partial per block
   TnPlan p{};
   p.nj = 1;
   p.ldp = 16;
   p.nkc = (K + 63) / 64;
-  p.n_slabs = XS_TN_BLOCKS;
+  p.n_slabs = blocks;
   p.spg = 16;
   p.n_groups = (p.n_slabs + p.spg - 1) / p.spg;
   return p;
@@ -733,7 +748,7 @@ size_t gemm_tn_workspace(int M, int N, int K) {
   N = std::min(N, 128);  // wider outputs run in 128-column slabs
   size_t ws = plan_bytes(tn_plan(M, N, K), K);  // either kernel family may run
   if (gemm_wide_ok(N)) ws = std::max(ws, gemm_tn_wide_workspace(M, N, K));
-  if (N <= 16) ws = std::max(ws, plan_bytes(xs_tn_plan(K), K));
+  if (N <= 16) ws = std::max(ws, plan_bytes(xs_tn_plan(K, XS_TN_BLOCKS), K));
   return ws;
 }
 
@@ -743,6 +758,11 @@ static void tn_reduce(const TnPlan &p, int M, int N, int K, float *partial, floa
   if (nst < 0) nst = ldc;
   float *part2 = partial + (size_t)p.n_slabs * K * p.ldp;
   const long long elems = (long long)K * p.ldp;
+  if (M > 0 && p.n_slabs <= TN_ONE_PASS) {  // one ordered pass over the partials themselves
+    PGCN_LAUNCH(k_gemm_tn_reduce, dim3((unsigned)ceil_div(elems, 256)), dim3(256), 0, s,
+                partial, p.n_slabs, K, N, p.ldp, C, ldc, nst);
+    return;
+  }
   if (M > 0)
     PGCN_LAUNCH(k_slab_reduce1, dim3((unsigned)ceil_div(elems, 256), (unsigned)p.n_groups),
                        dim3(256), 0, s, partial, p.n_slabs, elems, p.spg, part2);
@@ -787,7 +807,8 @@ void launch_xstream_tn(int M, int N, int K, const float *A, int lda, const float
                        hipStream_t s) {
   PGCN_CHECK(xstream_ok(N, K), PGCN_E_INVALID, "xstream_tn: needs N <= 16, K <= 640");
   PGCN_CHECK(lda % 4 == 0 && lda >= K, PGCN_E_INVALID, "gemm_tn: lda must be a multiple of 4 >= K");
-  const TnPlan p = xs_tn_plan(K);
+  const int blocks = xs_tn_blocks(M, K, lda);
+  const TnPlan p = xs_tn_plan(K, blocks);
   float *partial = static_cast<float *>(workspace);
   if (M > 0 && xstream_ring_ok(K, lda)) {
     launch_xstream_tn_ring(M, N, K, A, lda, G, ldg, maskT, a_scale, partial, XS_TN_BLOCKS, s);
@@ -796,10 +817,10 @@ void launch_xstream_tn(int M, int N, int K, const float *A, int lda, const float
 #define XTN_CASE(KC)                                                                           \
   case KC:                                                                                     \
     if (maskT)                                                                                 \
-      PGCN_LAUNCH((k_xstream_tn<KC, true>), dim3(XS_TN_BLOCKS), dim3(256), 0, s, M, N, K, \
+      PGCN_LAUNCH((k_xstream_tn<KC, true>), dim3(blocks), dim3(256), 0, s, M, N, K,       \
                          A, lda, G, ldg, maskT, a_scale, partial);                             \
     else                                                                                       \
-      PGCN_LAUNCH((k_xstream_tn<KC, false>), dim3(XS_TN_BLOCKS), dim3(256), 0, s, M, N,  \
+      PGCN_LAUNCH((k_xstream_tn<KC, false>), dim3(blocks), dim3(256), 0, s, M, N,        \
                          K, A, lda, G, ldg, maskT, a_scale, partial);                          \
     break;
     switch (p.nkc) {

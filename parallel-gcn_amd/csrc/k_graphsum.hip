@@ -39,6 +39,63 @@ __device__ __forceinline__ float4 f4_shfl_xor(float4 v, int m) {
                      __shfl_xor(v.w, m, 64));
 }
 
+// One row by a whole workgroup (g_gs_split 3: the small graphs' hub rows): sub-group s of
+// VEC lanes walks slots begin + s, + 256 / VEC, ...; the sub-groups are summed in a fixed
+// xor-tree per wave, then the four waves in wave order through LDS.
+template <int VEC>
+__device__ __forceinline__ void wide_item(const int4 item, const int *__restrict__ indices,
+                                          const float *__restrict__ vals,
+                                          const float4 *__restrict__ in, int ld4_in,
+                                          float4 *__restrict__ out, int ld4_out,
+                                          const GsEpilogue &epi) {
+  constexpr int NS = 256 / VEC;
+  __shared__ float4 red[4][VEC];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int sg = threadIdx.x / VEC, v = threadIdx.x - sg * VEC;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  int j = item.y + sg;
+  const int end = item.z;
+  for (; j + 3 * NS < end; j += 4 * NS) {
+    int c[4];
+    float wv[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      c[u] = indices[j + u * NS];
+      wv[u] = vals[j + u * NS];
+    }
+    float4 x[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) x[u] = in[(long long)c[u] * ld4_in + v];
+#pragma unroll
+    for (int u = 0; u < 4; u++) acc = f4_fma(wv[u], x[u], acc);
+  }
+  if (j < end) {  // the last (at most 3) neighbours: clamped loads, guarded adds
+    int c[3];
+    float wv[3];
+#pragma unroll
+    for (int u = 0; u < 3; u++) {
+      const int jj = min(j + u * NS, end - 1);
+      c[u] = indices[jj];
+      wv[u] = vals[jj];
+    }
+    float4 x[3];
+#pragma unroll
+    for (int u = 0; u < 3; u++) x[u] = in[(long long)c[u] * ld4_in + v];
+#pragma unroll
+    for (int u = 0; u < 3; u++)
+      if (j + u * NS < end) acc = f4_fma(wv[u], x[u], acc);
+  }
+#pragma unroll
+  for (int m = VEC; m < 64; m <<= 1) acc = f4_add(acc, f4_shfl_xor(acc, m));
+  if (lane < VEC) red[w][lane] = acc;
+  __syncthreads();
+  if (threadIdx.x < VEC) {
+    float4 tot = f4_add(f4_add(f4_add(red[0][v], red[1][v]), red[2][v]), red[3][v]);
+    gs_epilogue(tot, item.x, 4 * v, epi);
+    out[(long long)item.x * ld4_out + v] = tot;
+  }
+}
+
 // G lanes per item (G | 64); VEC float4 per row.
 template <int VEC, int G>
 __global__ __launch_bounds__(256) void k_graphsum(const int4 *__restrict__ items,
@@ -47,19 +104,34 @@ __global__ __launch_bounds__(256) void k_graphsum(const int4 *__restrict__ items
                                                   const float *__restrict__ vals,
                                                   const float4 *__restrict__ in, int ld4_in,
                                                   float4 *__restrict__ out, int ld4_out,
-                                                  float4 *__restrict__ partial, GsEpilogue epi) {
+                                                  float4 *__restrict__ partial, GsEpilogue epi,
+                                                  const int *__restrict__ slot_comb,
+                                                  int *__restrict__ comb_ctr,
+                                                  const int4 *__restrict__ comb,
+                                                  const int4 *__restrict__ wide, int n_wide) {
   constexpr int NB = G / VEC;  // neighbours per group per iteration
   constexpr int IPW = 64 / G;  // items per wave
   constexpr bool POW2 = (VEC & (VEC - 1)) == 0;
   const int lane = threadIdx.x & 63, wib = threadIdx.x >> 6;
+  if constexpr (POW2) {
+    if ((int)blockIdx.x < n_wide) {  // a workgroup item: 256 / VEC neighbour sub-groups
+      wide_item<VEC>(wide[blockIdx.x], indices, vals, in, ld4_in, out, ld4_out, epi);
+      return;
+    }
+  }
   const int q = lane / G, r = lane - q * G;
   const int nb = r / VEC, v = r - nb * VEC;
   const bool active = nb < NB;
-  const int b = blockIdx.x % nbc;
-  const int wg = blockIdx.x / nbc, nwg = gridDim.x / nbc;
+  const int bid = blockIdx.x - n_wide, nblk = gridDim.x - n_wide;
+  const int b = bid % nbc;
+  const int wg = bid / nbc, nwg = nblk / nbc;
   const int first = block_items[b], last = block_items[b + 1];
   for (int it = first + (wg * 4 + wib) * IPW + q; it < last; it += nwg * 4 * IPW) {
     const int4 item = items[it];  // {row, begin, end, slot}
+    // in-kernel combine: this split row's {row, first slot, count}, loaded beside the walk
+    const bool arrive = slot_comb && item.w >= 0;
+    int4 cm = make_int4(0, 0, 0, 0);
+    if (arrive) cm = comb[slot_comb[item.w]];
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     if (active) {
       int j = item.y + nb;
@@ -115,6 +187,27 @@ __global__ __launch_bounds__(256) void k_graphsum(const int4 *__restrict__ items
         out[(long long)item.x * ld4_out + v] = acc;
       } else {
         partial[(long long)item.w * VEC + v] = acc;
+      }
+    }
+    if (arrive) {  // (uniform over the item's G lanes)
+      // release this slot, count the arrival; the row's last arrival acquires the others' and
+      // adds the slots in slot order from zero, as k_graphsum_combine does: the same bits
+      const int ci = slot_comb[item.w];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      int old = 0;
+      if (r == 0)
+        old = __hip_atomic_fetch_add(comb_ctr + ci, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      old = __shfl(old, q * G, 64);
+      if (old == cm.z - 1) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (nb == 0) {
+          float4 tot = make_float4(0.f, 0.f, 0.f, 0.f);
+          for (int k = 0; k < cm.z; k++)
+            tot = f4_add(tot, partial[(long long)(cm.y + k) * VEC + v]);
+          gs_epilogue(tot, cm.x, 4 * v, epi);
+          out[(long long)cm.x * ld4_out + v] = tot;
+        }
+        if (r == 0) comb_ctr[ci] = 0;  // (no other item of the row is left: ready for the next call)
       }
     }
   }
@@ -219,14 +312,14 @@ template <int VEC, int G>
 static void launch_vec(const GraphSchedule &s, const int *indices, const float *vals,
                        const float *in, int ld_in, float *out, int ld_out, float *partial,
                        hipStream_t st, const GsEpilogue &epi) {
-  if (s.n_items > 0) {
+  if (s.n_items > 0 || s.n_wide > 0) {
     constexpr int per_wg = 4 * (64 / G);  // items one workgroup takes per sweep
     long long per_block = ceil_div(s.max_block_items, per_wg);
     // enough workgroups per column block to fill the block's XCD several times over
     const long long cap = 4096 / s.nbc;
     if (per_block > cap) per_block = cap;
     if (per_block < 1) per_block = 1;
-    const dim3 grid((unsigned)(per_block * s.nbc)), block(256);
+    const dim3 grid((unsigned)(per_block * s.nbc + s.n_wide)), block(256);
     // (measured and removed, r01: a software-pipelined k_graphsum16, 132 VGPRs at 3 waves per
     // SIMD, slower)
     if (VEC == 4 && s.nbc > 1)
@@ -238,9 +331,10 @@ static void launch_vec(const GraphSchedule &s, const int *indices, const float *
       PGCN_LAUNCH((k_graphsum<VEC, G>), grid, block, 0, st, s.items, s.block_items, s.nbc,
                          indices, vals, reinterpret_cast<const float4 *>(in), ld_in / 4,
                          reinterpret_cast<float4 *>(out), ld_out / 4,
-                         reinterpret_cast<float4 *>(partial), epi);
+                         reinterpret_cast<float4 *>(partial), epi, s.slot_comb, s.comb_ctr,
+                         s.comb, s.wide, s.n_wide);
   }
-  if (s.n_comb > 0) {
+  if (s.n_comb > 0 && !s.slot_comb) {
     const long long threads = (long long)s.n_comb * VEC;
     PGCN_LAUNCH(k_graphsum_combine<VEC>, dim3((unsigned)ceil_div(threads, 256)),
                        dim3(256), 0, st, s.comb, s.n_comb,

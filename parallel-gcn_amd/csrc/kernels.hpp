@@ -41,6 +41,14 @@ struct GraphSchedule {
   const int4 *items = nullptr;
   const int *block_items = nullptr;  // nbc + 1 offsets into items
   const int4 *comb = nullptr;
+  // in-kernel combine (g_gs_split 1): the comb index of each slot, and one arrival counter per
+  // comb row (zero between calls); the last item of a split row to finish sums its slots
+  const int *slot_comb = nullptr;
+  int *comb_ctr = nullptr;
+  // workgroup items (g_gs_split 3): rows one whole workgroup sums ({row, begin, end, -1}),
+  // taken by the launch's first n_wide workgroups
+  int n_wide = 0;
+  const int4 *wide = nullptr;
 };
 int graphsum_group_lanes(int vec);
 
@@ -148,6 +156,13 @@ void launch_mask_nibbles(const uint64_t *mask, long long mask_base, long long ma
 // layout of k_ring_prescale), so neither the ReLU nor the prescale needs a launch
 struct XsEpilogue {
   int relu = 0;
+  // backward tails of the product's rows [M][ldc] (Matmul input grad): element e = r*ldc + j
+  // times Dropout's keep-bit (base + e) ? scale : 0, then 0 where the ReLU's mask byte e is 0
+  // (k_dropout_apply then k_relu_bwd: the same bits)
+  const uint64_t *bwd_drop = nullptr;
+  long long drop_base = 0;
+  float drop_scale = 0.0f;
+  const uint8_t *bwd_relu = nullptr;
   float4 *next_table = nullptr;
   const float *next_scale = nullptr;
   int next_sr = 0;
@@ -199,6 +214,15 @@ void launch_spmm_csc_bwd(int nf, int p, int ldg, const int *csc_ptr, const int *
 void launch_dropout_mask(uint64_t *states, long long n_chunks, long long elem0,
                          long long elem_end, float p, uint64_t *mask, const void *table,
                          hipStream_t s, int max_blocks = 0);
+// two variables' draws (each as launch_dropout_mask's arguments) in one launch
+struct MaskDraw {
+  uint64_t *states;
+  long long n_chunks, elem0, elem_end;
+  float p;
+  uint64_t *mask;
+};
+void launch_dropout_mask2(const MaskDraw &d0, const MaskDraw &d1, const void *table,
+                          hipStream_t s);
 // the input dropout of dense X [rows][F] (element i = m F + k at local bit mask_base + i) into
 // the flat bitmap AND the nibble layout nib [rows][16] in one launch (k_dropout_mask_nib);
 // dropout_mask_nib_ok: the shape the kernel takes (F <= 1024, chunk-aligned row cuts)

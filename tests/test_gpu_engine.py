@@ -440,8 +440,10 @@ def test_fused_epilogue_bit_identical(loaded, pgcn, case):
     their gradients (gs_epilogue.hpp; plain gather kernels on cora, LDS ring + combine on the
     dense graph, where the epilogue also writes the next GraphSum's prescaled input table and
     that GraphSum skips its prescale: compared without that bit too; and the first layer's
-    X-stream product applying the eval ReLU / writing the ring tables, compared without it:
-    fuse_epilogue 7 = all, 0 = none, 5 = no prestaged tables, 3 = no X-stream epilogue)."""
+    X-stream product applying the eval ReLU / writing the ring tables, compared without it; and
+    on cora's module order the Dropout + ReLU backward in the output Matmul's input-grad
+    product (k_xstream_nn epilogue), compared without it: fuse_epilogue 15 = all, 0 = none,
+    13 = no prestaged tables, 11 = no X-stream epilogue, 7 = no Matmul tails)."""
     if case == "lds_dense":
         ds, make, tails = pgcn.Dataset.synthetic(120000, 64, 41, 1500000, 21), {}, 2
     elif case == "lds_deep":  # 128-wide rows: the tails ride the wide (all-pass) combine
@@ -449,16 +451,48 @@ def test_fused_epilogue_bit_identical(loaded, pgcn, case):
         make, tails = dict(hidden_dims=(128, 128, 128), dropouts=(0.5,) * 4), 3
     else:
         ds = loaded["cora"]
-        make, tails = ({"hidden_dims": (4,)}, 2) if case == "cora_h4" else ({}, 1)
-    on = _fused_run(pgcn, ds, 7, 4, **make)
+        make, tails = ({"hidden_dims": (4,)}, 2) if case == "cora_h4" else ({}, 2)
+    on = _fused_run(pgcn, ds, 15, 4, **make)
     off = _fused_run(pgcn, ds, 0, 4, **make)
-    no_stage = _fused_run(pgcn, ds, 5, 4, **make)
-    no_xs = _fused_run(pgcn, ds, 3, 4, **make)
+    no_stage = _fused_run(pgcn, ds, 13, 4, **make)
+    no_xs = _fused_run(pgcn, ds, 11, 4, **make)
+    no_mm = _fused_run(pgcn, ds, 7, 4, **make)
     assert on["tails"] == tails and off["tails"] == 0
-    for other in (off, no_stage, no_xs):
+    assert no_mm["tails"] == (1 if case == "cora" else tails)
+    for other in (off, no_stage, no_xs, no_mm):
         np.testing.assert_array_equal(on["lines"], other["lines"])
         for a, b in zip(on["vars"] + on["grads"], other["vars"] + other["grads"]):
             np.testing.assert_array_equal(a, b)
+
+
+def test_co_draw_and_split_rows_bit_identical(loaded, pgcn):
+    """cora's small-graph launch cuts give the same bits as the launches they replace: the
+    hidden dropout's mask drawn in the input dropout's launch (co_draw 1 vs 0), the hub rows'
+    slots summed by the last item of the row in the GraphSum launch (gs_split 1 vs 0 at one
+    item length), and the output layer's column-subset backward gathering through original
+    column ids instead of compacting its input (gs_orig_cols 1 vs 0); the cut launches show in
+    the launch counter."""
+    ds = loaded["cora"]
+    runs = {}
+    for name, kn in (("base", dict(co_draw=0, gs_split=0, gs_item_iters=32, gs_orig_cols=0)),
+                     ("cut", dict(co_draw=1, gs_split=1, gs_item_iters=32, gs_orig_cols=1))):
+        with helpers.knobs(pgcn, **kn):
+            g = pgcn.GCN(pgcn.make_params(ds), ds)
+            g.train_epoch()
+            pgcn.reset_path_counts()
+            lines = [g.train_epoch() + g.eval(2) for _ in range(4)]
+            n = pgcn.path_counts()["launches"]
+            g.train_epoch()
+            runs[name] = dict(lines=np.array(lines, np.float32), launches=n,
+                              vars=[g.get_var(i) for i in (2, 3, 5)],
+                              grads=[g.get_var(i, 1) for i in (1, 3)])
+            g.close()
+    a, b = runs["base"], runs["cut"]
+    np.testing.assert_array_equal(a["lines"], b["lines"])
+    for x, y in zip(a["vars"] + a["grads"], b["vars"] + b["grads"]):
+        np.testing.assert_array_equal(x, y)
+    # per epoch: one mask launch, cora's d = 16 GraphSum combines (3 calls), one row gather
+    assert b["launches"] <= a["launches"] - 5 * 4, (a["launches"], b["launches"])
 
 
 @pytest.mark.parametrize("case", ["cora_h4", "lds_dense"])

@@ -49,6 +49,16 @@ def random_graph(n, avg_deg, seed, hubs=0, hub_deg=0, empty_rows=0):
     return indptr, dst.astype(np.int32)
 
 
+def _merge_graphs(ip1, ix1, ip2, ix2):
+    """Row-wise concatenation of two CSR patterns on the same nodes (symmetric if both are)."""
+    n = len(ip1) - 1
+    ip = np.zeros(n + 1, np.int64)
+    ip[1:] = np.cumsum(np.diff(ip1) + np.diff(ip2))
+    ix = np.concatenate([np.concatenate([ix1[ip1[i]:ip1[i + 1]], ix2[ip2[i]:ip2[i + 1]]])
+                         for i in range(n)])
+    return ip.astype(np.int32), ix.astype(np.int32)
+
+
 def oracle_graphsum(indptr, indices, x, dim):
     lib = helpers.oracle()
     n = len(indptr) - 1
@@ -106,6 +116,57 @@ def test_graphsum_vs_oracle(pgcn, n, deg, dim, hubs):
     torch.cuda.synchronize()
     assert torch.equal(out, out2)
     pgcn.lib.pgcn_graph_destroy(g)
+
+
+@pytest.mark.parametrize("dim", [16, 7, 41])
+def test_graphsum_split_rows_in_kernel(pgcn, dim):
+    """Rows longer than one work item on the plain path (cora's hubs): gs_split 1 (default: the
+    last of a row's items to finish adds the row's slots, one launch) gives gs_split 0's bits
+    (the combine launch) on every call at the same item length (gs_item_iters 32) -- the arrival
+    counters are left at zero for the next one; short items (8 iterations: more split rows,
+    more arrivals), gs_split 2 (long rows as one item) and the default gs_split 3 (rows of up
+    to 8 workgroup iterations summed by one workgroup, longer ones split with arrivals) agree
+    with the oracle and repeat their bits."""
+    n = 4000
+    # hubs of ~300 (workgroup items at d <= 16) and ~2,000 neighbours (split at every width)
+    indptr, indices = random_graph(n, 6, seed=dim, hubs=12, hub_deg=300)
+    i2, x2 = random_graph(n, 1, seed=dim + 1, hubs=6, hub_deg=2000)
+    indptr, indices = _merge_graphs(indptr, indices, i2, x2)
+    ld = (dim + 3) // 4 * 4
+    x = np.zeros((n, ld), np.float32)
+    x[:, :dim] = np.random.default_rng(dim).standard_normal((n, dim)).astype(np.float32)
+    xin = torch.from_numpy(x).to(DEV)
+    outs = {}
+    try:
+        for mode in (0, 1, 2, 3, 4):
+            assert pgcn.lib.pgcn_debug_set(b"gs_split", (0, 1, 2, 1, 3)[mode]) == 0
+            assert pgcn.lib.pgcn_debug_set(b"gs_item_iters", 8 if mode >= 3 else 32) == 0
+            g = ctypes.c_void_p()
+            pgcn.check(pgcn.lib.pgcn_graph_create(n, helpers.ptr(indptr), helpers.ptr(indices),
+                                                  ctypes.byref(g)), "graph_create")
+            pgcn.reset_path_counts()
+            res = []
+            for _ in range(3):
+                out = torch.full((n, ld), float("nan"), device=DEV)
+                pgcn.check(pgcn.lib.pgcn_graphsum(g, vp(xin), ld, vp(out), ld, dim, stream()), "gs")
+                res.append(out)
+            torch.cuda.synchronize()
+            outs[mode] = (res, pgcn.path_counts()["launches"])
+            pgcn.lib.pgcn_graph_destroy(g)
+    finally:
+        pgcn.lib.pgcn_debug_set(b"gs_split", 3)
+        pgcn.lib.pgcn_debug_set(b"gs_item_iters", 8)
+    for r in outs[1][0] + outs[0][0][1:]:
+        assert torch.equal(r, outs[0][0][0])
+    assert outs[1][1] < outs[0][1], (outs[1][1], outs[0][1])  # no combine launches
+    ref = oracle_graphsum(indptr, indices, x, dim)
+    bound = abs_bound(indptr, indices, x, dim)
+    for mode in (3, 4):
+        for r in outs[mode][0][1:]:
+            assert torch.equal(r, outs[mode][0][0])
+    for mode in (0, 2, 3, 4):
+        err = np.abs(outs[mode][0][2].cpu().numpy()[:, :dim] - ref)
+        assert (err <= 1e-5 * bound + 1e-30).all(), (mode, (err / (bound + 1e-30)).max())
 
 
 @pytest.mark.parametrize("kind", ["coef", "random", "directed"])

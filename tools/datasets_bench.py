@@ -102,9 +102,14 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--only", default=None, help="one dataset (e.g. under rocprofv3)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--set", action="append", default=[], metavar="KNOB=VALUE",
+                    help="engine knob (pgcn_debug_set) for every engine built (A/B runs)")
     args = ap.parse_args()
     sys.path.insert(0, REPO)
     pg = helpers.pgcn()
+    for kv in args.set:
+        k, v = kv.split("=")
+        pg.check(pg.lib.pgcn_debug_set(k.encode(), int(v)), "knob " + k)
     modes = [0, 1] if args.graph == "both" else [int(args.graph)]
     out = {}
     floor_us = launch_floor_us(pg)
