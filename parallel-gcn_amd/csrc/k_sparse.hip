@@ -58,9 +58,23 @@ __global__ __launch_bounds__(256) void k_spmm_csr(int m, int p, int ldc,
 #pragma unroll
     for (int u = 0; u < 8; u++) sum += av[u] * bv[u];
   }
-  for (; jj < je; jj++) {
-    const float av = drop_val(a[jj], mask, mask_base + jj, scale);
-    sum += av * b[(long long)indices[jj] * p + k];
+  if (jj < je) {
+    // the last (at most 7) nonzeros the same way: clamped, unpredicated loads (r04 late: one
+    // dependent load pair per nonzero made cora's rows -- 18 nonzeros on average -- up to 7
+    // round trips longer); the adds guarded, in CSR order
+    int ix[7];
+    float av[7], bv[7];
+#pragma unroll
+    for (int u = 0; u < 7; u++) {
+      const int j = min(jj + u, je - 1);
+      ix[u] = indices[j];
+      av[u] = drop_val(a[j], mask, mask_base + j, scale);
+    }
+#pragma unroll
+    for (int u = 0; u < 7; u++) bv[u] = b[(long long)ix[u] * p + k];
+#pragma unroll
+    for (int u = 0; u < 7; u++)
+      if (jj + u < je) sum += av[u] * bv[u];
   }
   c[i * ldc + k] = sum;
 }
