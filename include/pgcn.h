@@ -307,14 +307,22 @@ int pgcn_debug_rank_graph(int n, const int *indptr, const int *indices, int worl
 /* Engine options (process-wide; most are read when an engine is built).  Every option but the
  * diagnostic ones selects between bit-identical or oracle-tested forms of the same epoch:
  *   "train_ahead" 0/1, "eval_ax" 0/1, "split_cols" 0/1, "epoch_graph" 0/1, "mm_side" 0/1/2,
- *   "fuse_epilogue" bits 1 tails | 2 prestaged tables | 4 X-stream epilogue (default 7),
+ *   "fuse_epilogue" bits 1 tails | 2 prestaged tables | 4 X-stream epilogue | 8 Dropout /
+ *   ReLU backward in a Matmul's input-grad product (default 15),
  *   "fuse_output" 0..3 (default 2), "xstream_ring" 0/1, "lds_min_kb" (< 0: default),
  *   "lds_blocks" 0 (by shape) or 1..32, "lds_slots" 0 (by shape) / 8 / 16 (rowsets per summing
  *   wave of the LDS schedule), "parse_threads" (0: up to 16), "wide_prescale" 0/1
  *   (a multi-pass GraphSum's tables prescaled by one launch, default 1), "rs_chunks" 1..4
  *   (edge-cut GraphSum row chunks at world > 1, default 1), "mask_nib" 0/1 (dense X's input
  *   dropout drawn into the flat bitmap and the GEMMs' nibble layout by one launch, default 0:
- *   two launches); diagnostics: "split_rows" 0/1 (stale logits outside the split),
+ *   two launches), "co_draw" 0/1 (sparse X: the hidden dropout's mask drawn in the input
+ *   dropout's launch, default 1), "gs_split" 0..3 (the plain GraphSum's rows longer than one
+ *   work item on graphs of <= 2^20 slots: 0 a combine launch, 1 the row's last item sums the
+ *   slots, 2 long rows as one item, 3 (default) rows of up to 8 workgroup iterations summed
+ *   by one workgroup, longer ones as 1), "gs_item_iters" 2/4/8/16/32 (group iterations per work
+ *   item there, default 8), "gs_orig_cols" 0/1 (a column subset's plain GraphSum gathers through
+ *   the original column ids instead of compacting its input, default 1); diagnostics:
+ *   "split_rows" 0/1 (stale logits outside the split),
  * "gemm_variant" 0/1 (the general GEMM kernels only), "plain_blocks" 0/1 (1: the plain
  * GraphSum kernels never split rows into per-XCD column blocks).  Returns PGCN_E_INVALID on an unknown key or on a value outside
  * the key's range (nothing is changed then). */

@@ -26,3 +26,5 @@ done
 for d in cora pubmed_synth; do
   timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $O/prof_$d -o run -f csv -- python3 tools/datasets_bench.py --graph 0 --no-cpu --epochs 500 --only $d > $O/prof_$d.log 2>&1 || exit $?
 done
+timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-extra > $O/bench.json 2> $O/bench.err || exit $?
+python3 -c "import json;d=json.load(open('$O/bench.json'));print('bench', round(d['value'],1), d['roofline']['frac'])"
