@@ -15,10 +15,6 @@
 
 #pragma clang fp contract(off)
 
-#ifndef PGCN_CSC_U
-#define PGCN_CSC_U 4  // entries per thread per round of the 256-thread backward (A/B builds)
-#endif
-
 namespace pgcn {
 
 __device__ __forceinline__ float drop_val(float a, const uint64_t *__restrict__ mask,
@@ -80,15 +76,18 @@ __global__ __launch_bounds__(256) void k_spmm_csr(int m, int p, int ldc,
 }
 
 // One workgroup per (feature f, 16 gradient columns).  The serial chain of a column's
-// contributions (row order, the CPU's scatter order) is latency-free: the CH threads gather
-// U chunks of CH entries' products at once (U entries per thread: one round trip for the
-// indices, one for the values, mask words and 64-B rows of G), then, chunk by chunk, stage
-// them in LDS where 16 lanes add them in entry order.  Same products, same order => the same
-// bits as a lane walking the column alone (the r01 kernel, 1.9 ms on pubmed: 32 workgroups,
-// one dependent gather per entry).  <256, 4> (r04 late: cora's 1,083-entry column took five
-// 256-entry rounds of two dependent loads each, 12.7 us per call), or <1024, 1> when the
-// features average more than 512 entries (pubmed: 8 chunks of 256 took 38.9 us per call).
-template <int CH, int U>
+// contributions (row order, the CPU's scatter order) is latency-free: all CH threads gather a
+// chunk of CH entries' products into LDS at once (one 64-B row of G per entry), then 16 lanes
+// add them in entry order from LDS.  Same products, same order => the same bits as a lane
+// walking the column alone (the r01 kernel, 1.9 ms on pubmed: 32 workgroups, one dependent
+// gather per entry).  CH = 256, or 1024 when the features average more than 512 entries (r04:
+// pubmed's ~2,000-entry columns took 8 chunks of 256, 38.9 us per call).  r04 late: the next
+// chunk's loads are issued before this chunk's adds (its values, mask words and G rows, and
+// the indices of the chunk after it: two dependent round trips per chunk were exposed, cora's
+// 1,083-entry column took 12.7 us); measured and dropped there: U = 2 or 4 chunks' loads at
+// once (U 4: 14.8 us, 110 VGPRs halve the resident workgroups; U 2: no gain in the epoch,
+// profiles/r04/ab_csc_u.txt).
+template <int CH>
 __global__ __launch_bounds__(CH) void k_spmm_csc_bwd(int nf, int p, int ldg,
                                                      const int *__restrict__ csc_ptr,
                                                      const int *__restrict__ csc_row,
@@ -98,85 +97,119 @@ __global__ __launch_bounds__(CH) void k_spmm_csc_bwd(int nf, int p, int ldg,
                                                      long long mask_base, float scale,
                                                      const float *__restrict__ cgrad,
                                                      float *__restrict__ bgrad) {
-  __shared__ float prod[CH][17];
+  // products column-major (prod[c][entry], rows padded to CH + 4 floats): an adding lane
+  // reads 4 consecutive entries of its column with one ds_read_b128 (16 lanes, 4 banks apart)
+  __shared__ __attribute__((aligned(16))) float prod[16][CH + 4];
   const int f = blockIdx.x, k0 = blockIdx.y * 16, tid = threadIdx.x;
   const int e0 = csc_ptr[f], e1 = csc_ptr[f + 1];
   float sum = 0.0f;
-  for (int base = e0; base < e1; base += CH * U) {
-    float4 gv[U][4];
-    float av[U];
-    if ((ldg & 3) == 0) {  // engine layout: ld a multiple of 4, padding columns zero
-      // every entry's index pair, then every value / mask word / G row: two round trips for
-      // U * CH entries (clamped, unpredicated loads; entries past the column get 0)
-      int pos[U], row[U];
+  // the 16 lanes' ordered adds of the chunk at cb (its reads a batch ahead of the adds)
+  auto add_chunk = [&](int cb) {
+    const float *col = prod[tid];
+    const int n = min(CH, e1 - cb);
+    int j = 0;
+    if (n >= 16) {
+      float4 va[4], vb[4];
 #pragma unroll
-      for (int u = 0; u < U; u++) {
-        const int e = min(base + u * CH + tid, e1 - 1);
-        pos[u] = csc_pos[e];
-        row[u] = csc_row[e];
-      }
-      float ar[U];
-      uint64_t mw[U];
+      for (int q = 0; q < 4; q++) va[q] = *reinterpret_cast<const float4 *>(col + 4 * q);
+      for (;;) {
+        bool more = j + 32 <= n;
+        if (more) {
 #pragma unroll
-      for (int u = 0; u < U; u++) {
-        const float *g = cgrad + (long long)row[u] * ldg + k0;
-        ar[u] = a[pos[u]];
-        mw[u] = mask ? mask[(mask_base + pos[u]) >> 6] : 0ull;
-#pragma unroll
-        for (int c4 = 0; c4 < 4; c4++)
-          gv[u][c4] = k0 + 4 * c4 < ldg ? *reinterpret_cast<const float4 *>(g + 4 * c4)
-                                        : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      }
-#pragma unroll
-      for (int u = 0; u < U; u++)
-        av[u] = mask ? ar[u] * (((mw[u] >> ((mask_base + pos[u]) & 63)) & 1) ? scale : 0.0f)
-                     : ar[u];
-    }
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      const int cb = base + u * CH;  // this chunk's first entry (uniform)
-      if (cb >= e1) break;
-      const int e = cb + tid;
-      if (e < e1) {
-        if ((ldg & 3) == 0) {
-#pragma unroll
-          for (int c4 = 0; c4 < 4; c4++) {
-            const float4 v = gv[u][c4];
-            prod[tid][4 * c4 + 0] = v.x * av[u];
-            prod[tid][4 * c4 + 1] = v.y * av[u];
-            prod[tid][4 * c4 + 2] = v.z * av[u];
-            prod[tid][4 * c4 + 3] = v.w * av[u];
-          }
-        } else {
-          const int pos = csc_pos[e];
-          const float *g = cgrad + (long long)csc_row[e] * ldg + k0;
-          const float v = drop_val(a[pos], mask, mask_base + pos, scale);
-#pragma unroll
-          for (int c = 0; c < 16; c++) prod[tid][c] = k0 + c < p ? g[c] * v : 0.0f;
+          for (int q = 0; q < 4; q++) vb[q] = *reinterpret_cast<const float4 *>(col + j + 16 + 4 * q);
         }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          sum += va[q].x;
+          sum += va[q].y;
+          sum += va[q].z;
+          sum += va[q].w;
+        }
+        j += 16;
+        if (!more) break;
+        more = j + 32 <= n;
+        if (more) {
+#pragma unroll
+          for (int q = 0; q < 4; q++) va[q] = *reinterpret_cast<const float4 *>(col + j + 16 + 4 * q);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          sum += vb[q].x;
+          sum += vb[q].y;
+          sum += vb[q].z;
+          sum += vb[q].w;
+        }
+        j += 16;
+        if (!more) break;
+      }
+    }
+    for (; j + 4 <= n; j += 4) {
+      const float4 t = *reinterpret_cast<const float4 *>(col + j);
+      sum += t.x;
+      sum += t.y;
+      sum += t.z;
+      sum += t.w;
+    }
+    for (; j < n; j++) sum += col[j];
+  };
+  if ((ldg & 3) == 0 && e0 < e1) {  // engine layout: ld a multiple of 4, padding columns zero
+    // clamped, unpredicated loads (entries past the column are never added)
+    int pos, row;  // indices of the chunk after the current one
+    auto idx = [&](int cb, int &ps, int &rw) {
+      const int e = min(cb + tid, e1 - 1);
+      ps = csc_pos[e];
+      rw = csc_row[e];
+    };
+    float ar;
+    uint64_t mw;
+    float4 gv[4];
+    auto vals = [&](int ps, int rw, float &av_, uint64_t &mw_, float4 *g4) {
+      const float *g = cgrad + (long long)rw * ldg + k0;
+      av_ = a[ps];
+      mw_ = mask ? mask[(mask_base + ps) >> 6] : 0ull;
+#pragma unroll
+      for (int c4 = 0; c4 < 4; c4++)
+        g4[c4] = k0 + 4 * c4 < ldg ? *reinterpret_cast<const float4 *>(g + 4 * c4)
+                                   : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    };
+    int cpos;  // the current chunk's value positions (its mask bits)
+    idx(e0, cpos, row);
+    vals(cpos, row, ar, mw, gv);
+    if (e0 + CH < e1) idx(e0 + CH, pos, row);
+    for (int base = e0; base < e1; base += CH) {
+      const float av = mask ? ar * (((mw >> ((mask_base + cpos) & 63)) & 1) ? scale : 0.0f) : ar;
+      if (base + tid < e1) {
+#pragma unroll
+        for (int c4 = 0; c4 < 4; c4++) {
+          prod[4 * c4 + 0][tid] = gv[c4].x * av;
+          prod[4 * c4 + 1][tid] = gv[c4].y * av;
+          prod[4 * c4 + 2][tid] = gv[c4].z * av;
+          prod[4 * c4 + 3][tid] = gv[c4].w * av;
+        }
+      }
+      // the next chunk's values and the indices of the one after it, in flight over the adds
+      const bool next = base + CH < e1;  // (uniform)
+      if (next) {
+        cpos = pos;
+        vals(pos, row, ar, mw, gv);
+        if (base + 2 * CH < e1) idx(base + 2 * CH, pos, row);
       }
       __syncthreads();
-      if (tid < 16) {
-        // (r04: 32 LDS reads in flight per wait, was 8: the serial add chain of a long
-        // column no longer waits on the LDS between every 8 adds)
-        const int n = min(CH, e1 - cb);
-        int j = 0;
-        for (; j + 32 <= n; j += 32) {
-          float v[32];
+      if (tid < 16) add_chunk(base);
+      __syncthreads();
+    }
+  } else {
+    for (int base = e0; base < e1; base += CH) {
+      const int e = base + tid;
+      if (e < e1) {
+        const int ps = csc_pos[e];
+        const float *g = cgrad + (long long)csc_row[e] * ldg + k0;
+        const float v = drop_val(a[ps], mask, mask_base + ps, scale);
 #pragma unroll
-          for (int w = 0; w < 32; w++) v[w] = prod[j + w][tid];
-#pragma unroll
-          for (int w = 0; w < 32; w++) sum += v[w];
-        }
-        for (; j + 8 <= n; j += 8) {
-          float v[8];
-#pragma unroll
-          for (int w = 0; w < 8; w++) v[w] = prod[j + w][tid];
-#pragma unroll
-          for (int w = 0; w < 8; w++) sum += v[w];
-        }
-        for (; j < n; j++) sum += prod[j][tid];
+        for (int c = 0; c < 16; c++) prod[c][tid] = k0 + c < p ? g[c] * v : 0.0f;
       }
+      __syncthreads();
+      if (tid < 16) add_chunk(base);
       __syncthreads();
     }
   }
@@ -199,10 +232,10 @@ void launch_spmm_csc_bwd(int nf, int p, int ldg, const int *csc_ptr, const int *
   if (nf <= 0 || p <= 0) return;
   const dim3 grid((unsigned)nf, (unsigned)ceil_div(p, 16));
   if (nnz > 512LL * nf)
-    PGCN_LAUNCH((k_spmm_csc_bwd<1024, 1>), grid, dim3(1024), 0, s, nf, p, ldg, csc_ptr, csc_row,
+    PGCN_LAUNCH(k_spmm_csc_bwd<1024>, grid, dim3(1024), 0, s, nf, p, ldg, csc_ptr, csc_row,
                 csc_pos, a, mask, mask_base, scale, cgrad, bgrad);
   else
-    PGCN_LAUNCH((k_spmm_csc_bwd<256, PGCN_CSC_U>), grid, dim3(256), 0, s, nf, p, ldg, csc_ptr, csc_row,
+    PGCN_LAUNCH(k_spmm_csc_bwd<256>, grid, dim3(256), 0, s, nf, p, ldg, csc_ptr, csc_row,
                 csc_pos, a, mask, mask_base, scale, cgrad, bgrad);
 }
 
