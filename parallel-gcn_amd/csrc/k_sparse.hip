@@ -81,13 +81,14 @@ __global__ __launch_bounds__(256) void k_spmm_csr(int m, int p, int ldc,
 // add them in entry order from LDS.  Same products, same order => the same bits as a lane
 // walking the column alone (the r01 kernel, 1.9 ms on pubmed: 32 workgroups, one dependent
 // gather per entry).  CH = 256, or 1024 when the features average more than 512 entries (r04:
-// pubmed's ~2,000-entry columns took 8 chunks of 256, 38.9 us per call).  r04 late: the next
-// chunk's loads are issued before this chunk's adds (its values, mask words and G rows, and
-// the indices of the chunk after it: two dependent round trips per chunk were exposed, cora's
-// 1,083-entry column took 12.7 us); measured and dropped there: U = 2 or 4 chunks' loads at
-// once (U 4: 14.8 us, 110 VGPRs halve the resident workgroups; U 2: no gain in the epoch,
-// profiles/r04/ab_csc_u.txt).
-template <int CH>
+// pubmed's ~2,000-entry columns took 8 chunks of 256, 38.9 us per call).  r04 late, PIPE (the
+// 1024-thread form): the next chunk's loads are issued before this chunk's adds (its values,
+// mask words and G rows, and the indices of the chunk after it): pubmed_synth 6.26-6.33k ->
+// 6.77-6.79k epochs/s; in the 256-thread form cora lost 5 % with it (10.8k -> 10.2k,
+// profiles/r04/ab_csc_pipe.txt), so that form loads each chunk after the last one's adds.
+// Measured and dropped: U = 2 or 4 chunks' loads at once (U 4: 14.8 us on cora, 110 VGPRs
+// halve the resident workgroups; U 2: no gain in the epoch, profiles/r04/ab_csc_u.txt).
+template <int CH, bool PIPE = (CH >= 1024)>
 __global__ __launch_bounds__(CH) void k_spmm_csc_bwd(int nf, int p, int ldg,
                                                      const int *__restrict__ csc_ptr,
                                                      const int *__restrict__ csc_row,
@@ -175,8 +176,12 @@ __global__ __launch_bounds__(CH) void k_spmm_csc_bwd(int nf, int p, int ldg,
     int cpos;  // the current chunk's value positions (its mask bits)
     idx(e0, cpos, row);
     vals(cpos, row, ar, mw, gv);
-    if (e0 + CH < e1) idx(e0 + CH, pos, row);
+    if (PIPE && e0 + CH < e1) idx(e0 + CH, pos, row);
     for (int base = e0; base < e1; base += CH) {
+      if (!PIPE && base != e0) {  // this chunk's loads, after the last chunk's adds
+        idx(base, cpos, row);
+        vals(cpos, row, ar, mw, gv);
+      }
       const float av = mask ? ar * (((mw >> ((mask_base + cpos) & 63)) & 1) ? scale : 0.0f) : ar;
       if (base + tid < e1) {
 #pragma unroll
@@ -188,7 +193,7 @@ __global__ __launch_bounds__(CH) void k_spmm_csc_bwd(int nf, int p, int ldg,
         }
       }
       // the next chunk's values and the indices of the one after it, in flight over the adds
-      const bool next = base + CH < e1;  // (uniform)
+      const bool next = PIPE && base + CH < e1;  // (uniform)
       if (next) {
         cpos = pos;
         vals(pos, row, ar, mw, gv);
