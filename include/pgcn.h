@@ -316,7 +316,8 @@ int pgcn_debug_rank_graph(int n, const int *indptr, const int *indices, int worl
  *   (edge-cut GraphSum row chunks at world > 1, default 1), "mask_nib" 0/1 (dense X's input
  *   dropout drawn into the flat bitmap and the GEMMs' nibble layout by one launch, default 0:
  *   two launches), "co_draw" 0/1 (sparse X: the hidden dropout's mask drawn in the input
- *   dropout's launch, default 1), "gs_split" 0..3 (the plain GraphSum's rows longer than one
+ *   dropout's launch, default 1), "sparse_dual" 0/1 (sparse X: eval's first-layer product also
+ *   computes the next training forward's, default 1), "gs_split" 0..3 (the plain GraphSum's rows longer than one
  *   work item on graphs of <= 2^20 slots: 0 a combine launch, 1 the row's last item sums the
  *   slots, 2 long rows as one item, 3 (default) rows of up to 8 workgroup iterations summed
  *   by one workgroup, longer ones as 1), "gs_item_iters" 2/4/8/16/32 (group iterations per work

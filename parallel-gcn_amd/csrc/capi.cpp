@@ -35,6 +35,7 @@ extern int g_xstream_ring;          // k_xstream_lds.hip
 extern int g_plain_blocks;          // host/graph.cpp
 extern int g_gs_split;              // host/graph.cpp
 extern int g_co_draw;               // host/gcn.cpp
+extern int g_sparse_dual;           // host/gcn.cpp
 extern int g_gs_item_iters;         // host/graph.cpp
 extern int g_gs_orig_cols;          // host/graph.cpp
 extern int g_parse_threads;         // host/data.cpp: pieces of the parallel text parse
@@ -695,6 +696,9 @@ int pgcn_debug_set(const char *key, int value) {
   } else if (!std::strcmp(key, "gs_orig_cols")) {
     if (!in(0, 1)) return PGCN_E_INVALID;
     pgcn::g_gs_orig_cols = value;
+  } else if (!std::strcmp(key, "sparse_dual")) {
+    if (!in(0, 1)) return PGCN_E_INVALID;
+    pgcn::g_sparse_dual = value;
   } else if (!std::strcmp(key, "co_draw")) {
     if (!in(0, 1)) return PGCN_E_INVALID;
     pgcn::g_co_draw = value;

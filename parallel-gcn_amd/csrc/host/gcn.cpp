@@ -49,6 +49,9 @@ int g_fuse_output = 2;
 // "co_draw" (read at engine build): the hidden dropout's mask drawn in the input dropout's
 // launch (sparse X; bit-identical)
 int g_co_draw = 1;
+// "sparse_dual" (read per eval forward): sparse X with train_ahead: eval's first-layer product
+// also computes the next training forward's (k_spmm_csr<true>, one pass; bit-identical)
+int g_sparse_dual = 1;
 // "mm_side" (read at engine build): Matmul weight gradients on the side stream (ModuleContext)
 // on graphs of at least kMmSideRows rows; 2 = on every graph.  Off: r02 A/B on reddit-114M,
 // three runs each, 486.5 (on) vs 487.4 (off) epochs/s -- the LDS GraphSum holds every CU with
@@ -847,6 +850,7 @@ void GCN::enqueue_epoch(bool graph) {
 bool GCN::graph_eligible() const {
   if (!g_epoch_graph || !warm || comm || ctx.profile) return false;
   if (ctx.train_ahead && feats.dense && feats.maskT && !feats.ax) return false;
+  if (ctx.train_ahead && !feats.dense && g_sparse_dual) return false;  // (the same host swaps)
   return true;
 }
 

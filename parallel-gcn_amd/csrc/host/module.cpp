@@ -92,8 +92,19 @@ void Dropout::draw_ahead(hipStream_t s, const Event *ready) const {
     rng->mask_ahead.allocate(rng->mask.size());
     rng->mask_ahead.zero();
   }
-  // on a side stream: two workgroups per CU, leaving room for the main stream's kernels
-  draw(s, rng->mask_ahead.get(), ready ? 2 * kCUs : 0);
+  if (co_draw && !ready && !nib_ && !co_draw->pre_drawn && !co_draw->ahead) {
+    // with the hidden dropout's next mask (co_draw; the eval forward uses neither)
+    const DropoutRng &r = *rng, &q = co_draw->state();
+    const MaskDraw a{r.states.get(), r.n_chunks, 64 * r.chunk_lo, r.elem_end, p,
+                     rng->mask_ahead.get()};
+    const MaskDraw b{q.states.get(), q.n_chunks, 64 * q.chunk_lo, q.elem_end, co_draw->p,
+                     q.mask.get()};
+    launch_dropout_mask2(a, b, ctx->jump_table, s);
+    co_draw->pre_drawn = true;
+  } else {
+    // on a side stream: two workgroups per CU, leaving room for the main stream's kernels
+    draw(s, rng->mask_ahead.get(), ready ? 2 * kCUs : 0);
+  }
   if (ready) ready->record(s);
   ahead_ready = ready;
   ahead = true;
@@ -193,6 +204,23 @@ void SparseMatmul::forward(bool training, const Stream &s) const {
   if (training && ahead_valid) {  // computed by the eval forward before this one
     std::swap(c->dev_data, ahead);
     ahead_valid = false;
+    return;
+  }
+  if (!training && ctx->train_ahead && !x->dense && g_sparse_dual && !ahead_valid) {
+    // sparse X: eval's X W1 and the next training forward's drop(X) W1 from one pass over X
+    // (k_spmm_csr<true>; the next input mask -- and its co-drawn hidden mask -- drawn now)
+    if (!ahead) {
+      ahead.allocate(c->dev_data.size());
+      ahead.zero();
+    }
+    if (drop->drawn_ahead())
+      drop->wait_ahead(s.get());
+    else
+      drop->draw_ahead(s.get());
+    launch_spmm_csr_dual(x->rows, b->cols, c->ld, x->indptr.get(), x->indices.get(),
+                         x->values.get(), drop->mask_ahead(), base, scale, b->dev_data.get(),
+                         c->dev_data.get(), ahead.get(), s.get());
+    ahead_valid = true;
     return;
   }
   if (!training && ctx->train_ahead && x->dense && x->maskT && !ahead_valid) {

@@ -93,6 +93,7 @@ constexpr int kFuseTails = 1, kFusePrestage = 2, kFuseXstream = 4, kFuseMatmulTa
 extern int g_fuse_epilogue;
 extern int g_fuse_output;
 extern int g_mask_nib;
+extern int g_sparse_dual;
 
 // Shared per-GCN state the modules read (current split, comm, profiling, RNG table).
 struct ModuleContext {

@@ -23,6 +23,10 @@ __device__ __forceinline__ float drop_val(float a, const uint64_t *__restrict__ 
   return a * (((mask[bit >> 6] >> (bit & 63)) & 1) ? scale : 0.0f);
 }
 
+// DUAL: c2 = drop(X) B beside c = X B from the same index / value / B loads (the eval forward
+// and the next training forward share B: no optimizer step between them); each sum keeps its
+// own products in CSR order, so c2 has the masked kernel's bits and c the unmasked one's.
+template <bool DUAL>
 __global__ __launch_bounds__(256) void k_spmm_csr(int m, int p, int ldc,
                                                   const int *__restrict__ indptr,
                                                   const int *__restrict__ indices,
@@ -30,49 +34,61 @@ __global__ __launch_bounds__(256) void k_spmm_csr(int m, int p, int ldc,
                                                   const uint64_t *__restrict__ mask,
                                                   long long mask_base, float scale,
                                                   const float *__restrict__ b,
-                                                  float *__restrict__ c) {
+                                                  float *__restrict__ c, float *__restrict__ c2) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long i = t / p;
   const int k = (int)(t - i * p);
   if (i >= m) return;
-  float sum = 0.0f;
+  float sum = 0.0f, sum2 = 0.0f;
   int jj = indptr[i];
   const int je = indptr[i + 1];
+  const uint64_t *m1 = DUAL ? nullptr : mask;  // c's mask (DUAL: c is the unmasked product)
   // r04: 8 nonzeros' index / value / mask loads issued together, then their B gathers, then
   // the adds in CSR order (one dependent load chain per 8 nonzeros instead of per nonzero;
   // the same products and the same order: the same bits)
   for (; jj + 8 <= je; jj += 8) {
     int ix[8];
-    float av[8], bv[8];
+    float av[8], aw[8], bv[8];
 #pragma unroll
     for (int u = 0; u < 8; u++) {
       ix[u] = indices[jj + u];
-      av[u] = drop_val(a[jj + u], mask, mask_base + jj + u, scale);
+      const float ar = a[jj + u];
+      av[u] = drop_val(ar, m1, mask_base + jj + u, scale);
+      if constexpr (DUAL) aw[u] = drop_val(ar, mask, mask_base + jj + u, scale);
     }
 #pragma unroll
     for (int u = 0; u < 8; u++) bv[u] = b[(long long)ix[u] * p + k];
 #pragma unroll
-    for (int u = 0; u < 8; u++) sum += av[u] * bv[u];
+    for (int u = 0; u < 8; u++) {
+      sum += av[u] * bv[u];
+      if constexpr (DUAL) sum2 += aw[u] * bv[u];
+    }
   }
   if (jj < je) {
     // the last (at most 7) nonzeros the same way: clamped, unpredicated loads (r04 late: one
     // dependent load pair per nonzero made cora's rows -- 18 nonzeros on average -- up to 7
     // round trips longer); the adds guarded, in CSR order
     int ix[7];
-    float av[7], bv[7];
+    float av[7], aw[7], bv[7];
 #pragma unroll
     for (int u = 0; u < 7; u++) {
       const int j = min(jj + u, je - 1);
       ix[u] = indices[j];
-      av[u] = drop_val(a[j], mask, mask_base + j, scale);
+      const float ar = a[j];
+      av[u] = drop_val(ar, m1, mask_base + j, scale);
+      if constexpr (DUAL) aw[u] = drop_val(ar, mask, mask_base + j, scale);
     }
 #pragma unroll
     for (int u = 0; u < 7; u++) bv[u] = b[(long long)ix[u] * p + k];
 #pragma unroll
     for (int u = 0; u < 7; u++)
-      if (jj + u < je) sum += av[u] * bv[u];
+      if (jj + u < je) {
+        sum += av[u] * bv[u];
+        if constexpr (DUAL) sum2 += aw[u] * bv[u];
+      }
   }
   c[i * ldc + k] = sum;
+  if constexpr (DUAL) c2[i * ldc + k] = sum2;
 }
 
 // One workgroup per (feature f, 16 gradient columns).  The serial chain of a column's
@@ -226,8 +242,18 @@ void launch_spmm_csr(int m, int p, int ldc, const int *indptr, const int *indice
                      const float *b, float *c, hipStream_t s) {
   if (m <= 0) return;
   const long long threads = (long long)m * p;
-  PGCN_LAUNCH(k_spmm_csr, dim3((unsigned)ceil_div(threads, 256)), dim3(256), 0, s, m, p,
-                     ldc, indptr, indices, a, mask, mask_base, scale, b, c);
+  PGCN_LAUNCH(k_spmm_csr<false>, dim3((unsigned)ceil_div(threads, 256)), dim3(256), 0, s, m, p,
+              ldc, indptr, indices, a, mask, mask_base, scale, b, c, nullptr);
+}
+
+void launch_spmm_csr_dual(int m, int p, int ldc, const int *indptr, const int *indices,
+                          const float *a, const uint64_t *mask, long long mask_base, float scale,
+                          const float *b, float *c, float *c2, hipStream_t s) {
+  PGCN_CHECK(mask && c2, PGCN_E_INVALID, "spmm_csr_dual: needs the mask and the second output");
+  if (m <= 0) return;
+  const long long threads = (long long)m * p;
+  PGCN_LAUNCH(k_spmm_csr<true>, dim3((unsigned)ceil_div(threads, 256)), dim3(256), 0, s, m, p,
+              ldc, indptr, indices, a, mask, mask_base, scale, b, c, c2);
 }
 
 void launch_spmm_csc_bwd(int nf, int p, int ldg, const int *csc_ptr, const int *csc_row,

@@ -205,6 +205,10 @@ void launch_gemm_tn(int M, int N, int K, const float *A, int lda, const float *G
 void launch_spmm_csr(int m, int p, int ldc, const int *indptr, const int *indices,
                      const float *a, const uint64_t *mask, long long mask_base, float scale,
                      const float *b, float *c, hipStream_t s);
+// c = X b and c2 = drop(X) b from one pass over X (the sparse form of the X-stream dual)
+void launch_spmm_csr_dual(int m, int p, int ldc, const int *indptr, const int *indices,
+                          const float *a, const uint64_t *mask, long long mask_base, float scale,
+                          const float *b, float *c, float *c2, hipStream_t s);
 // nnz: the entries of all nf columns (picks the chunk size; 0 = unknown: 256)
 void launch_spmm_csc_bwd(int nf, int p, int ldg, const int *csc_ptr, const int *csc_row,
                          const int *csc_pos, const float *a, const uint64_t *mask,

@@ -234,7 +234,7 @@ ENGINE_DEFAULTS = {"train_ahead": 1, "split_rows": 0, "split_cols": 1, "eval_ax"
                    "parse_threads": 0, "wide_prescale": 1, "rs_chunks": 1, "lds_slots": 0,
                    "mask_nib": 0, "plain_blocks": 0, "gs_split": 3,
                    "gs_item_iters": 8, "co_draw": 1,
-                   "gs_orig_cols": 1}
+                   "gs_orig_cols": 1, "sparse_dual": 1}
 
 
 @contextlib.contextmanager

@@ -565,7 +565,7 @@ def test_debug_set_refuses_out_of_range_values(pgcn):
                      ("epoch_graph", 3), ("fuse_epilogue", 16), ("fuse_output", 4),
                      ("mm_side", 3), ("xstream_ring", 2), ("gemm_variant", 7),
                      ("lds_blocks", 3), ("parse_threads", -2), ("wide_prescale", 2),
-                     ("plain_blocks", 2), ("gs_split", 4), ("gs_item_iters", 5), ("co_draw", 2), ("gs_orig_cols", 2)):
+                     ("plain_blocks", 2), ("gs_split", 4), ("gs_item_iters", 5), ("co_draw", 2), ("gs_orig_cols", 2), ("sparse_dual", 2)):
         assert lib.pgcn_debug_set(key.encode(), bad) < 0, key
     assert lib.pgcn_debug_set(b"no_such_knob", 0) < 0
     for key, val in helpers.ENGINE_DEFAULTS.items():

@@ -469,13 +469,16 @@ def test_co_draw_and_split_rows_bit_identical(loaded, pgcn):
     """cora's small-graph launch cuts give the same bits as the launches they replace: the
     hidden dropout's mask drawn in the input dropout's launch (co_draw 1 vs 0), the hub rows'
     slots summed by the last item of the row in the GraphSum launch (gs_split 1 vs 0 at one
-    item length), and the output layer's column-subset backward gathering through original
-    column ids instead of compacting its input (gs_orig_cols 1 vs 0); the cut launches show in
-    the launch counter."""
+    item length), the output layer's column-subset backward gathering through original column
+    ids instead of compacting its input (gs_orig_cols 1 vs 0), and eval's sparse product also
+    computing the next training forward's, its masks drawn ahead (sparse_dual 1 vs 0); the cut
+    launches show in the launch counter."""
     ds = loaded["cora"]
     runs = {}
-    for name, kn in (("base", dict(co_draw=0, gs_split=0, gs_item_iters=32, gs_orig_cols=0)),
-                     ("cut", dict(co_draw=1, gs_split=1, gs_item_iters=32, gs_orig_cols=1))):
+    for name, kn in (("base", dict(co_draw=0, gs_split=0, gs_item_iters=32, gs_orig_cols=0,
+                                   sparse_dual=0)),
+                     ("cut", dict(co_draw=1, gs_split=1, gs_item_iters=32, gs_orig_cols=1,
+                                  sparse_dual=1))):
         with helpers.knobs(pgcn, **kn):
             g = pgcn.GCN(pgcn.make_params(ds), ds)
             g.train_epoch()
