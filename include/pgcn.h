@@ -320,8 +320,8 @@ int pgcn_debug_rank_graph(int n, const int *indptr, const int *indices, int worl
  *   computes the next training forward's, default 1), "gs_split" 0..3 (the plain GraphSum's rows longer than one
  *   work item on graphs of <= 2^20 slots: 0 a combine launch, 1 the row's last item sums the
  *   slots, 2 long rows as one item, 3 (default) rows of up to 8 workgroup iterations summed
- *   by one workgroup, longer ones as 1), "gs_item_iters" 2/4/8/16/32 (group iterations per work
- *   item there, default 8), "gs_orig_cols" 0/1 (a column subset's plain GraphSum gathers through
+ *   by one workgroup, longer ones as 1), "gs_item_iters" 0/2/4/8/16/32 (group iterations per
+ *   work item there; 0 (default): by shape, the shortest leaving <= 1,536 workgroup items), "gs_orig_cols" 0/1 (a column subset's plain GraphSum gathers through
  *   the original column ids instead of compacting its input, default 1); diagnostics:
  *   "split_rows" 0/1 (stale logits outside the split),
  * "gemm_variant" 0/1 (the general GEMM kernels only), "plain_blocks" 0/1 (1: the plain

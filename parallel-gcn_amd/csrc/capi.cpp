@@ -706,7 +706,8 @@ int pgcn_debug_set(const char *key, int value) {
     if (!in(0, 3)) return PGCN_E_INVALID;
     pgcn::g_gs_split = value;
   } else if (!std::strcmp(key, "gs_item_iters")) {
-    if (value != 2 && value != 4 && value != 8 && value != 16 && value != 32) return PGCN_E_INVALID;
+    if (value != 0 && value != 2 && value != 4 && value != 8 && value != 16 && value != 32)
+      return PGCN_E_INVALID;
     pgcn::g_gs_item_iters = value;
   } else if (!std::strcmp(key, "lds_slots")) {
     if (value != 0 && !ring_slots_ok(value)) return PGCN_E_INVALID;

@@ -132,10 +132,13 @@ int g_plain_blocks = 0;
 // order), power-of-two row widths
 int g_gs_split = 3;
 // "gs_item_iters" (read at schedule build): group iterations per work item of the plain
-// unblocked path on graphs of <= kSmallNnz slots with gs_split 1 (32 elsewhere).  A small
+// unblocked path on graphs of <= kSmallNnz slots with gs_split 1 / 3 (32 elsewhere).  A small
 // graph's GraphSum lasts as long as its longest item (one index -> gather round trip per
-// iteration), so its hub rows are cut short and summed in-kernel.
-int g_gs_item_iters = 8;
+// iteration), so its long rows are cut short and summed in-kernel or by workgroup items.
+// 0 (default) = by shape with gs_split 3: the shortest of 2, 4, 8, 16, 32 that leaves at most
+// kWideCap workgroup items (r04 late: cora 224 rows at 2 iterations, 11.5k vs 11.1k epochs/s
+// at 8; pubmed_synth 3,215 rows at 2 lost 2 %, 1,321 at 4 gained 1 %: profiles/r04/ab_item_iters.txt)
+int g_gs_item_iters = 0;
 // "gs_orig_cols" (read per call): a column subset's unblocked plain GraphSum gathers the
 // input's own rows through the original column ids (1) instead of compacting them first (0)
 int g_gs_orig_cols = 1;
@@ -224,9 +227,22 @@ DevGraph::Sched &DevGraph::schedule(int vec) {
     const bool small = nnz_ <= kSmallNnz;
     const bool arrive = (g_gs_split == 1 || g_gs_split == 3) && small;
     chunk = nb * 32;  // 32 group iterations per work item
-    if (arrive) chunk = nb * g_gs_item_iters;
-    const int whole = g_gs_split == 2 && small ? 8 * chunk : chunk;
     const int wide_max = g_gs_split == 3 && small && (vec & (vec - 1)) == 0 ? 256 / vec * 8 : 0;
+    if (arrive && g_gs_item_iters > 0) {
+      chunk = nb * g_gs_item_iters;
+    } else if (arrive) {
+      int it = 2;
+      for (; it < 32; it *= 2) {
+        long long wide_rows = 0;
+        for (int r = 0; r < n_rows_; r++) {
+          const int len = h_indptr_[(size_t)r + 1] - h_indptr_[(size_t)r];
+          wide_rows += len > nb * it && len <= wide_max;
+        }
+        if (wide_rows <= kWideCap) break;
+      }
+      chunk = nb * (wide_max ? it : 8);
+    }
+    const int whole = g_gs_split == 2 && small ? 8 * chunk : chunk;
     items.reserve((size_t)n_rows_ + (size_t)(nnz_ / chunk) + 1);
     for (int r = 0; r < n_rows_; r++) {
       const int b = h_indptr_[(size_t)r], e = h_indptr_[(size_t)r + 1];

@@ -118,7 +118,8 @@ class DevGraph {
 
   static constexpr int kBlocks = kGraphBlocks;   // one column block per XCD
   static constexpr double kL2Budget = 4.0e6;     // one XCD's L2: tables the plain kernel keeps whole
-  static constexpr long long kSmallNnz = 1 << 20;  // g_gs_split 2: graphs that keep long rows whole
+  static constexpr long long kSmallNnz = 1 << 20;  // g_gs_split 1-3: the small-graph schedules
+  static constexpr int kWideCap = 1536;  // g_gs_item_iters 0: workgroup items (6 per CU) at most
   static constexpr long long kLdsMinBytes = 1 << 20;  // d = 16 tables above: LDS GraphSum ...
   static constexpr int kLdsMinRows = 32768;           // ... when the rows fill its workgroups
 

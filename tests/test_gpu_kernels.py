@@ -138,9 +138,9 @@ def test_graphsum_split_rows_in_kernel(pgcn, dim):
     xin = torch.from_numpy(x).to(DEV)
     outs = {}
     try:
-        for mode in (0, 1, 2, 3, 4):
-            assert pgcn.lib.pgcn_debug_set(b"gs_split", (0, 1, 2, 1, 3)[mode]) == 0
-            assert pgcn.lib.pgcn_debug_set(b"gs_item_iters", 8 if mode >= 3 else 32) == 0
+        for mode in (0, 1, 2, 3, 4, 5):  # mode 5: the defaults (item length by shape)
+            assert pgcn.lib.pgcn_debug_set(b"gs_split", (0, 1, 2, 1, 3, 3)[mode]) == 0
+            assert pgcn.lib.pgcn_debug_set(b"gs_item_iters", (32, 32, 32, 8, 8, 0)[mode]) == 0
             g = ctypes.c_void_p()
             pgcn.check(pgcn.lib.pgcn_graph_create(n, helpers.ptr(indptr), helpers.ptr(indices),
                                                   ctypes.byref(g)), "graph_create")
@@ -155,16 +155,16 @@ def test_graphsum_split_rows_in_kernel(pgcn, dim):
             pgcn.lib.pgcn_graph_destroy(g)
     finally:
         pgcn.lib.pgcn_debug_set(b"gs_split", 3)
-        pgcn.lib.pgcn_debug_set(b"gs_item_iters", 8)
+        pgcn.lib.pgcn_debug_set(b"gs_item_iters", 0)
     for r in outs[1][0] + outs[0][0][1:]:
         assert torch.equal(r, outs[0][0][0])
     assert outs[1][1] < outs[0][1], (outs[1][1], outs[0][1])  # no combine launches
     ref = oracle_graphsum(indptr, indices, x, dim)
     bound = abs_bound(indptr, indices, x, dim)
-    for mode in (3, 4):
+    for mode in (3, 4, 5):
         for r in outs[mode][0][1:]:
             assert torch.equal(r, outs[mode][0][0])
-    for mode in (0, 2, 3, 4):
+    for mode in (0, 2, 3, 4, 5):
         err = np.abs(outs[mode][0][2].cpu().numpy()[:, :dim] - ref)
         assert (err <= 1e-5 * bound + 1e-30).all(), (mode, (err / (bound + 1e-30)).max())
 
