@@ -345,8 +345,12 @@ __device__ __forceinline__ void tn_compute(TnStep<KC, MASKED> &st, floatx4 (&acc
 constexpr int XS_TN_BLOCKS = 256;  // one 4-wave block per CU (1 wave per SIMD, ~300 registers)
 // small products (<= XS_TN_SMALL_ROWS rows: the small graphs' layers) take 32 blocks, whose
 // partials one ordered pass reduces (r04 late: one launch fewer per call; the blocks' steps
-// stay a few per wave)
-constexpr int XS_TN_SMALL_ROWS = 16384, XS_TN_SMALL_BLOCKS = 32, TN_ONE_PASS = 32;
+// stay a few per wave; 64 blocks measured equal, 16 slower: profiles/r04/ab_tn_small_blocks.txt)
+#ifndef PGCN_TN_SMALL_BLOCKS
+#define PGCN_TN_SMALL_BLOCKS 32
+#endif
+constexpr int XS_TN_SMALL_ROWS = 16384, XS_TN_SMALL_BLOCKS = PGCN_TN_SMALL_BLOCKS,
+              TN_ONE_PASS = XS_TN_SMALL_BLOCKS > 32 ? XS_TN_SMALL_BLOCKS : 32;
 
 template <int KC, bool MASKED>
 __global__ __launch_bounds__(256, 1) void k_xstream_tn(int M, int N, int K,
