@@ -146,6 +146,47 @@ def maybe_launch(args):
         sys.exit(2)
 
 
+def dry_run(args):
+    """--dry-run: no GPU, one process.  Builds the edge-cut partition of the workload for
+    --gpus N (the contiguous nnz-balanced node ranges every rank computes for itself) and
+    prints, per rank, its rows, the nnz of its column block of Â and the bytes it sends per
+    GraphSum exchange and per epoch; one JSON line."""
+    pgcn = load_pkg()
+    t0 = time.perf_counter()
+    # the adjacency does not depend on the feature width: 2 features keep this cheap
+    ds = pgcn.Dataset.synthetic(N_NODES, 2, N_CLASS, WORKLOADS[args.workload], seed=1)
+    hidden = tuple(int(h) for h in args.hidden.split(","))
+    world = args.gpus
+    ip = np.asarray(ds.graph_indptr, np.int64)
+    bounds, maxrows = pgcn.partition_bounds(ds.graph_indptr, world)
+    # per epoch (2 layers, reassociated output layer): GraphSums over widths -- training
+    # forward h1, output-layer h_last forward (train and eval), its backward, first-layer
+    # backward h1 (eval's first layer comes from Â X); L layers: each hidden layer adds one
+    # forward (train), one forward (eval) and one backward
+    dims = [hidden[0]] + [h for h in hidden[1:] for _ in range(3)] + [hidden[-1]] * 3 + [hidden[0]]
+    weights = N_FEAT * hidden[0] + sum(a * b for a, b in zip(hidden, hidden[1:])) + \
+        hidden[-1] * N_CLASS
+    ranks = []
+    for r in range(world):
+        lo, hi = int(bounds[r]), int(bounds[r + 1])
+        # a row's partial sums go to its owner: this rank sends every other rank's rows
+        other = sum(int(bounds[q + 1] - bounds[q]) for q in range(world) if q != r)
+        per_gs = {d: other * ((d + 3) // 4 * 4) * 4 for d in sorted(set(dims))}
+        ranks.append({"rank": r, "nodes": [lo, hi], "rows": hi - lo,
+                      # Â is symmetric: the column block's nnz is the row block's
+                      "column_block_nnz": int(ip[hi] - ip[lo]),
+                      "graphsum_send_bytes": per_gs,
+                      # + the weight-gradient all-reduce and the two passes' (loss, wrong)
+                      "epoch_send_bytes": sum(per_gs[d] for d in dims) +
+                      (world - 1) * 4 * (weights + 2 * 2)})
+    out = {"dry_run": True, "workload": args.workload, "gpus": world, "hidden": hidden,
+           "nodes": N_NODES, "adjacency_nnz": int(ip[-1]), "maxrows": int(maxrows),
+           "graphsums_per_epoch": len(dims), "ranks": ranks,
+           "nnz_imbalance": max(x["column_block_nnz"] for x in ranks) /
+           (int(ip[-1]) / world), "setup_s": time.perf_counter() - t0}
+    print(json.dumps(out))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -167,20 +208,31 @@ def main():
                     help="skip the secondary measurements (restricted / reference order)")
     ap.add_argument("--knob", action="append", default=[],
                     help="engine knob for the headline engine, key=value (pgcn_debug_set)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: print the --gpus N partition (per-rank nnz, exchange bytes)")
     args = ap.parse_args()
+    if args.dry_run:
+        dry_run(args)
+        return
     maybe_launch(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    # this rank's GPU before anything touches HIP through torch (torch.cuda.synchronize()
-    # below would otherwise open a context on GPU 0 from every rank)
-    torch.cuda.set_device(local_rank)
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        with stdout_to_stderr():  # gloo's connection banner: stdout is the JSON line's
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+    # the product has no CPU path: a rank without its GPU stops here, naming itself
+    if torch.cuda.device_count() <= local_rank:
+        print(f"bench.py: rank {rank}/{world} (local {local_rank}): no HIP device "
+              f"{local_rank} ({torch.cuda.device_count()} visible)", file=sys.stderr)
+        sys.exit(3)
+    # this rank's GPU before anything touches HIP through torch (torch.cuda.synchronize()
+    # below would otherwise open a context on GPU 0 from every rank)
+    torch.cuda.set_device(local_rank)
 
     pgcn = load_pkg()
     import helpers

@@ -124,6 +124,8 @@ class GCN {
   void fuse_epilogues();
   void fuse_matmul_tails();
   void fuse_output_layer();
+  void prepare_graphs();
+  void build_eval_ax();
   void join_side();
   int fused_tails_ = 0;  // GraphSum epilogues carrying ReLU / Dropout work (forward + backward)
   void set_split(int split);

@@ -543,10 +543,11 @@ void DevGraph::share_tables(DevGraph *owner) {
   lds_.reset();
 }
 
-bool DevGraph::can_share_tables(int dim) const {
+bool DevGraph::can_share_tables(int dim, int ld_in) const {
   if (!uses_lds(dim)) return false;
-  // one 16-column pass, or every pass's table from the batched prescale (graphsum below)
-  return dim <= 16 || (!col_map_ && g_wide_prescale);
+  // one 16-column pass, or every pass's table from the batched prescale -- graphsum()'s
+  // `batch` condition below (ld_in <= 128); wider inputs prescale per pass
+  return dim <= 16 || (!col_map_ && g_wide_prescale && ld_in <= 128);
 }
 
 float *DevGraph::table_scratch() {
@@ -581,18 +582,24 @@ void DevGraph::graphsum(const float *in, int ld_in, float *out, int ld_out, int 
     PGCN_CHECK(!prestaged || (dim <= 16 && !col_map), PGCN_E_INVALID,
                "graphsum: prestaged input on a path without a ring table");
     const size_t table = (size_t)ceil_div(n_cols_, RING_SR) * RING_SR * 16;
+    const int n_pass = ceil_div(dim, 16);
+    auto pass_col = [&](int p) { return std::min(16 * p, ldm - 16); };
+    // several passes: one launch prescales all of them (each pass then reads its own table);
+    // inputs up to 128 wide (at most 8 passes: RingPasses), wider ones prescale per pass
+    const bool batch = n_pass > 1 && !col_map && ld_in <= 128 && g_wide_prescale;
+    PGCN_CHECK(!tables_ready || (can_share_tables(dim, ld_in) && (n_pass == 1 || batch)),
+               PGCN_E_INVALID, "graphsum: shared tables on a call that prescales per pass");
     RingPasses ps;
-    for (int c0 = 0; c0 < dim; c0 += 16) ps.c[ps.n++] = std::min(c0, ldm - 16);
-    // several passes: one launch prescales all of them (each pass then reads its own table)
-    const bool batch = ps.n > 1 && !col_map && ld_in <= 128 && g_wide_prescale;
-    PGCN_CHECK(!tables_ready || (can_share_tables(dim) && (ps.n == 1 || batch)), PGCN_E_INVALID,
-               "graphsum: shared tables on a call that prescales per pass");
-    float *tables = batch ? table_wide(table * ps.n) : nullptr;
+    if (batch) {
+      PGCN_CHECK(n_pass <= 8, PGCN_E_INVALID, "graphsum: batched passes");
+      for (int p = 0; p < n_pass; p++) ps.c[ps.n++] = pass_col(p);
+    }
+    float *tables = batch ? table_wide(table * n_pass) : nullptr;
     if (batch && !tables_ready)
       launch_ring_prescale_wide(lds_->s, in, ld_in, std::min(ld_in, ps.c[ps.n - 1] + 16), ps,
                                 tables, (long long)table, s);
-    for (int p = 0; p < ps.n; p++) {
-      const int c = ps.c[p];
+    for (int p = 0; p < n_pass; p++) {
+      const int c = pass_col(p);
       GsEpilogue ep = epi ? *epi : GsEpilogue{};
       ep.col0 = c;
       launch_graphsum_ring(lds_->s, in + c, ld_in, out + c, ld_out,

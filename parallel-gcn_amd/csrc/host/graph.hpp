@@ -78,7 +78,7 @@ class DevGraph {
   // epi: the element-wise tail applied to every output row as it is formed (one pass only:
   // dim <= 16, or a width with a kernel of its own and no 16-column passes)
   // tables_ready: the prescaled table(s) this call reads were filled by a call of the same
-  // input on a graph sharing them (share_tables; can_share_tables(dim)): no prescale launch
+  // input on a graph sharing them (share_tables; can_share_tables(dim, ld_in)): no prescale launch
   void graphsum(const float *in, int ld_in, float *out, int ld_out, int dim, hipStream_t s,
                 bool compact_in = false, const GsEpilogue *epi = nullptr, bool prestaged = false,
                 bool tables_ready = false);
@@ -87,7 +87,7 @@ class DevGraph {
   // one prescale serves every graph of the group.
   void share_tables(DevGraph *owner);
   // a graphsum() of this width prescales into tables a sharing graph can read as they are
-  bool can_share_tables(int dim) const;
+  bool can_share_tables(int dim, int ld_in) const;
   const DevGraph *table_owner() const { return table_owner_; }
   // The ring schedule's prescaled-input table of a graphsum() of this width (one 16-column
   // pass, no column map), for a producer's epilogue to fill (then graphsum(.., prestaged));

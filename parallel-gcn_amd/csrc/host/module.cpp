@@ -356,7 +356,13 @@ void GraphSum::stage_next(GsEpilogue &e, GraphSum *next, DevGraph *ng, bool fwd)
 // GPU: `g`'s combine), or (edge-cut) in k_gs_finish on this rank's rows once the
 // reduce-scatter has summed them
 bool GraphSum::tail_ok(const DevGraph *g, int ld_in, int ld_out) const {
-  if (ctx->comm) return dim % 4 == 0 && ld_out % 4 == 0;
+  if (ctx->comm) {
+    if (dim % 4 != 0 || ld_out % 4 != 0) return false;
+    if (ctx->comm->world() > 1) return true;
+    // one rank: run() hands the tail to the column block's own GraphSum (its combine)
+    const DevGraph *cg = g ? g : (ctx->chunk_graphs.empty() ? nullptr : ctx->chunk_graphs[0]);
+    return cg && cg->epilogue_ok(dim, ld_in, ld_out);
+  }
   return g && g->epilogue_ok(dim, ld_in, ld_out);
 }
 
@@ -453,7 +459,7 @@ void GraphSum::run(const float *src, float *dst, const Stream &s, int mode,
         }
       } else {
         DevGraph *gk = cgs[k];
-        const bool shared = k > 0 && gk->table_owner() == cgs[0] && gk->can_share_tables(dim);
+        const bool shared = k > 0 && gk->table_owner() == cgs[0] && gk->can_share_tables(dim, in->ld);
         gk->graphsum(src, in->ld, partial[k].get(), out->ld, dim, s.get(), false, nullptr,
                      k == 0 && prestaged, shared);
         bytes += gk->algorithmic_bytes(dim);

@@ -258,6 +258,7 @@ class GraphSum : public Module {
   void backward(const Stream &s) const override;
   const Variable *input() const { return in.get(); }
   const Variable *output() const { return out.get(); }
+  int width() const { return dim; }
   // Element-wise tails fused into this GraphSum's final writes (GCN::fuse_epilogues; null: the
   // modules run on their own): forward, the ReLU (and Dropout) on `out` that follow it;
   // backward, the Dropout (and ReLU) on `in` whose backward follows it

@@ -757,12 +757,15 @@ size_t gemm_tn_workspace(int M, int N, int K) {
 }
 
 // ordered two-pass reduction of p.n_slabs partials [K][ldp] into C[K][ldc]
+// One pass over the partials when they fit one first-pass group (the same sequential sum the
+// two passes form), or up to `one_pass` partials (the small X-stream TN plan only: its 32 block
+// partials in one sequential sum, r04 late -- another grouping than two passes of 16)
 static void tn_reduce(const TnPlan &p, int M, int N, int K, float *partial, float *C, int ldc,
-                      hipStream_t s, int nst = -1) {
+                      hipStream_t s, int nst = -1, int one_pass = 0) {
   if (nst < 0) nst = ldc;
   float *part2 = partial + (size_t)p.n_slabs * K * p.ldp;
   const long long elems = (long long)K * p.ldp;
-  if (M > 0 && p.n_slabs <= TN_ONE_PASS) {  // one ordered pass over the partials themselves
+  if (M > 0 && p.n_slabs <= std::max(one_pass, p.spg)) {  // one ordered pass over the partials
     PGCN_LAUNCH(k_gemm_tn_reduce, dim3((unsigned)ceil_div(elems, 256)), dim3(256), 0, s,
                 partial, p.n_slabs, K, N, p.ldp, C, ldc, nst);
     return;
@@ -833,7 +836,7 @@ void launch_xstream_tn(int M, int N, int K, const float *A, int lda, const float
     }
 #undef XTN_CASE
   }
-  tn_reduce(p, M, N, K, partial, C, ldc, s);
+  tn_reduce(p, M, N, K, partial, C, ldc, s, -1, blocks == XS_TN_SMALL_BLOCKS ? TN_ONE_PASS : 0);
 }
 
 static void gemm_tn_slab(int M, int N, int K, const float *A, int lda, const float *G, int ldg,

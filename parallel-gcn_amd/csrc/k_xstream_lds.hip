@@ -142,6 +142,14 @@ __device__ __forceinline__ void xl_load(const float *__restrict__ A, int lda, lo
   int pend = -1;  // the group issued last, not yet published (its DMAs may still land)
   for (int t = wave; t < T; t += NL) {
     const int slot = t % rg.nslot;
+    // the slot's last group is this wave's own unpublished one when nslot <= NL (NN at lda
+    // 628..640: 2 slots for 2 loaders): land and publish it first, or its consumers never
+    // free the slot this wave waits for
+    if (pend >= 0 && t - rg.nslot >= pend) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      publish(pend);
+      pend = -1;
+    }
     if (t >= rg.nslot) lds_wait_ge(freed + slot, (unsigned)(t - rg.nslot + 1));
     const long long b0 = (blockIdx.x + (long long)t * gridDim.x) * 16 * (long long)lda * 4;
     const char *blk = reinterpret_cast<const char *>(A) + b0;

@@ -201,6 +201,23 @@ def test_edge_cut_engine_world1(loaded, pgcn, name):
     g.close()
 
 
+def test_edge_cut_world1_hidden80_matches_single(loaded, pgcn):
+    """Edge-cut engine at world 1 with a hidden width the plain GraphSum has no fused-tail
+    kernel for (80 = 20 float4s): its ReLU / Dropout run as modules, as on the one-GPU
+    engine (the tail was handed to a combine that cannot take it)."""
+    ds = loaded["cora"]
+    p = pgcn.make_params(ds, hidden_dims=(80,), dropouts=(0.5, 0.5))
+    single = pgcn.GCN(p, ds, device=0)
+    cut = pgcn.GCN(p, ds, device=0, rank=0, world=1, unique_id=pgcn.comm_unique_id())
+    for e in range(3):
+        a = single.train_epoch() + single.eval(2)
+        b = cut.train_epoch() + cut.eval(2)
+        for k in (0, 2):
+            assert abs(a[k] - b[k]) <= 1e-4 * abs(a[k]), (e, k, a, b)
+    single.close()
+    cut.close()
+
+
 def test_edge_cut_world1_large_matches_single(pgcn):
     """Edge-cut engine at world 1 on a graph whose feature table takes the LDS GraphSum path:
     the chunked partial sums + reduce-scatters (two row chunks, comm stream) give the same

@@ -496,7 +496,11 @@ def nibble_mask_ref(mask, base, M, K):
 
 @pytest.mark.parametrize("M,N,K,base", [(3001, 16, 602, 0), (40009, 16, 602, 9),
                                         (1000, 16, 602, 41), (77, 12, 100, 63),
-                                        (129, 16, 640, 5), (20, 3, 7, 0)])
+                                        (129, 16, 640, 5), (20, 3, 7, 0),
+                                        # lda 628..640: 2 NN ring slots for 2 loader waves, and
+                                        # >= 3 groups per workgroup (the loader
+                                        # waited for its own unpublished group)
+                                        (40009, 16, 636, 3), (50001, 7, 629, 0)])
 def test_gemm_xstream(pgcn, M, N, K, base):
     """X-stream NN/TN kernels with nibble-layout dropout bits vs fp64 references (the loader /
     MFMA-wave split of k_xstream_lds.hip and the register-streamed kernels); the dual NN

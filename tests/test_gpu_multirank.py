@@ -101,6 +101,24 @@ def test_loopback_lds_graph_matches_oracle(pgcn, big_ds, big_oracle, world, spli
                               ties=test_ties)
 
 
+def test_loopback_chunks_hidden_above_128(pgcn, big_ds):
+    """Two row chunks (rs_chunks 2) at world 2 with a hidden width above 128 on the LDS path:
+    those GraphSums prescale per 16-column pass, so chunk 1 cannot share chunk 0's batched
+    tables and prescales its own (the shared-table check threw here)."""
+    dims, drops = (256,), (0.5, 0.5)
+    p = pgcn.make_params(big_ds, hidden_dims=dims, dropouts=drops)
+    with helpers.knobs(pgcn, rs_chunks=2):
+        res = _run_world(pgcn, big_ds, 2, 2, params=p)
+    _check_ranks(res, 2, big_ds.num_nodes)
+    assert res[0]["info"]["graphsum_lds"] == 1
+    ref = helpers.OracleGCN(helpers.ds_dict(big_ds), hidden_dims=dims, dropouts=drops)
+    cnt = helpers.split_counts(big_ds)
+    for e in range(2):
+        want, ties = ref.epoch_with_ties(big_ds.label, big_ds.split, big_ds.output_dim,
+                                         helpers.DEEP_TIE_TOL)
+        helpers.assert_line_close(res[0]["lines"][e], want, cnt, what=f"epoch {e + 1}", ties=ties)
+
+
 # BASELINE configs[4] (4 layers, hidden 128) on the edge-cut path: 140k nodes, so a rank's
 # column block takes the LDS GraphSum at world 8 too (17.5k columns x 64 B > 1 MB); every
 # d = 128 GraphSum then runs as 16-column LDS passes over the rank's chunk graphs, each chunk
