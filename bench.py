@@ -208,6 +208,9 @@ def main():
                     help="skip the secondary measurements (restricted / reference order)")
     ap.add_argument("--knob", action="append", default=[],
                     help="engine knob for the headline engine, key=value (pgcn_debug_set)")
+    ap.add_argument("--comm", choices=("peer", "rccl"), default="peer",
+                    help="N > 1: the exchange -- peer-mapped slots over xGMI (hipIpc; RCCL if "
+                         "the peers cannot be mapped) or RCCL reduce-scatters")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: print the --gpus N partition (per-rank nnz, exchange bytes)")
     args = ap.parse_args()
@@ -244,21 +247,36 @@ def main():
     model = (f"{len(hidden) + 1}-layer GCN, hidden={hidden[0]}" if len(set(hidden)) == 1
              else f"{len(hidden) + 1}-layer GCN, hidden={args.hidden}")
     uid = None
-    if world > 1:
+    comm_kind = [args.comm if world > 1 else ("rccl" if args.edge_cut else None)]
+
+    def rccl_uid():
         with stdout_to_stderr():
-            uid = [pgcn.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        uid = uid[0]
-    elif args.edge_cut:
-        with stdout_to_stderr():
-            uid = pgcn.comm_unique_id()
+            u = [pgcn.comm_unique_id() if rank == 0 else None]
+        if dist is not None:
+            dist.broadcast_object_list(u, src=0)
+        return u[0]
+
+    if comm_kind[0] == "rccl":
+        uid = rccl_uid()
 
     def engine():
-        if uid is not None:
+        if comm_kind[0] == "peer":
+            try:
+                return pgcn.GCN(params, ds, device=local_rank, rank=rank, world=world,
+                                allgather=pgcn.torch_allgather())
+            except pgcn.PgcnError as e:
+                # every rank fails together (the engine agrees on it): RCCL instead
+                print(f"bench.py: rank {rank}: peer exchange unavailable ({e}); RCCL",
+                      file=sys.stderr)
+                comm_kind[0] = "rccl"
+        if comm_kind[0] == "rccl":
+            nonlocal_uid[0] = nonlocal_uid[0] or rccl_uid()
             with stdout_to_stderr():
                 return pgcn.GCN(params, ds, device=local_rank, rank=rank, world=world,
-                                unique_id=uid)
+                                unique_id=nonlocal_uid[0])
         return pgcn.GCN(params, ds, device=local_rank)
+
+    nonlocal_uid = [uid]
 
     def barrier(g):
         g.sync()
@@ -343,6 +361,7 @@ def main():
         "dtype": "fp32",
         "data": "synthetic reddit-shaped (Chung-Lu power-law graph, dense N(0,1) features, seed 1)",
         "config": {"workload": f"{args.workload} {model} dropout=0.5 Adam",
+                   "exchange": comm_kind[0],
                    "nodes": N_NODES, "features": N_FEAT, "classes": N_CLASS,
                    "adjacency_nnz": int(ds.graph_indptr[-1]),
                    "parallelism": (f"edge-cut x{world}" if world > 1 or args.edge_cut

@@ -127,15 +127,6 @@ int pgcn_rng_jump_table(uint64_t period, void *host_table /* 16*256*16 bytes */)
 int pgcn_dropout_mask(uint64_t *chunk_states, long long n_chunks, long long n_elems,
                       long long elem0, float p, uint64_t *mask, const void *dev_jump_table,
                       void *stream);
-/* The same draw for a dense [rows][F] input (element m*F + k of the variable at mask bit
- * mask_base + m*F + k, mask_base < 64; n_chunks must be (mask_base + rows*F + 63) / 64) written
- * to `mask` AND to the nibble layout of pgcn_mask_nibbles (mask_nib [rows][16]) by one launch:
- * the bits of pgcn_dropout_mask followed by pgcn_mask_nibbles(mask, mask_base, F, rows, F).
- * PGCN_E_INVALID when F > 1024 or no row cut from mask_base is chunk-aligned. */
-int pgcn_dropout_mask_nib(uint64_t *chunk_states, long long n_chunks, long long n_elems,
-                          long long elem0, float p, uint64_t *mask, const void *dev_jump_table,
-                          long long mask_base, int F, int rows, uint64_t *mask_nib,
-                          void *stream);
 /* x[i] *= bit(i) ? scale : 0 for i in [0,n) (also the backward on grads). */
 int pgcn_dropout_apply(float *x, long long n, const uint64_t *mask, float scale, void *stream);
 
@@ -209,13 +200,25 @@ int pgcn_gcn_create(const pgcn_params *p, const pgcn_data *d, int device, pgcn_g
 int pgcn_comm_unique_id(void *unique_id_128);
 int pgcn_gcn_create_dist(const pgcn_params *p, const pgcn_data *d, int device, int rank,
                          int world, const void *unique_id_128, pgcn_gcn **out);
+/* Edge-cut variant over peer-mapped memory instead of RCCL (one process per GPU, DESIGN.md
+ * §6): every rank's receive slots are mapped into every other rank with hipIpc handles, and a
+ * GraphSum's partial sums travel as one-sided stores over xGMI straight from the kernel that
+ * forms them into their owner's slot, summed there in rank order (deterministic).  `allgather`
+ * is the caller's host channel (MPI_Allgather, torch.distributed, ...): the engine calls it
+ * with every rank in the same order -- at creation (the handles; all ranks fail together with
+ * PGCN_E_COMM if any cannot map its peers) and at destruction (a barrier before the regions are
+ * unmapped and freed) -- and it must fill all[q * bytes, (q + 1) * bytes) with rank q's `mine`
+ * and return 0.  A peer that never signals fails the next sync with PGCN_E_COMM after 20 s. */
+typedef int (*pgcn_allgather_fn)(const void *mine, size_t bytes, void *all, void *user);
+int pgcn_gcn_create_peer(const pgcn_params *p, const pgcn_data *d, int device, int rank,
+                         int world, pgcn_allgather_fn allgather, void *user, pgcn_gcn **out);
 /* In-process ranks ("fake RCCL"): `world` edge-cut engines in ONE process on
- * one device, each created and driven by its own host thread (every call that runs a
- * collective -- create, train_epoch, eval, epoch_async -- rendezvouses with the peers' same
- * call).  Collectives are stream-ordered device sums of the peers' buffers in rank order, so
- * the multi-rank engine (partition, chunked reduce-scatters, global dropout offsets, weight
- * all-reduce) runs unchanged without RCCL.  The group may be destroyed after the engines are
- * created (they keep it alive). */
+ * one device, each created and driven by its own host thread (creation and destruction
+ * rendezvous with the peers' same call).  Their collectives are pgcn_gcn_create_peer's
+ * kernels over raw device pointers (the same pushes, flags and rank-order sums), so the
+ * multi-rank engine (partition, peer exchange, global dropout offsets, weight all-reduce)
+ * runs unchanged without RCCL.  The group may be destroyed after the engines are created
+ * (they keep it alive). */
 typedef struct pgcn_loopback pgcn_loopback;
 int pgcn_loopback_create(int world, pgcn_loopback **out);
 int pgcn_loopback_destroy(pgcn_loopback *group);
@@ -227,7 +230,7 @@ int pgcn_gcn_create_loopback(const pgcn_params *p, const pgcn_data *d, int devic
 int pgcn_debug_gcn_create_solo(const pgcn_params *p, const pgcn_data *d, int device, int rank,
                                int world, pgcn_gcn **out);
 int pgcn_gcn_destroy(pgcn_gcn *g);
-/* Engine facts: "world", "rank", "comm" (0 none, 1 RCCL, 2 loopback, 3 solo), "comm_calls" /
+/* Engine facts: "world", "rank", "comm" (0 none, 1 RCCL, 2 loopback, 3 solo, 4 peer), "comm_calls" /
  * "comm_bytes" (collectives enqueued since creation and the bytes this rank sends in them,
  * ring algorithm: a reduce-scatter (W-1)/W of its send buffer, an all-reduce twice that), "reassociated",
  * "graph_symmetric", "graphsum_lds" (width-16 GraphSums take the LDS kernel), "epochs",
@@ -304,29 +307,26 @@ long long pgcn_partition_subgraph(int n, const int *indptr, const int *indices, 
  * one GPU.  *rows / *cols give its shape. */
 int pgcn_debug_rank_graph(int n, const int *indptr, const int *indices, int world, int rank,
                           int chunks, int chunk, pgcn_graph **out, int *rows, int *cols);
-/* Engine options (process-wide; most are read when an engine is built).  Every option but the
- * diagnostic ones selects between bit-identical or oracle-tested forms of the same epoch:
+/* Engine options (process-wide; most are read when an engine is built).  Each selects between
+ * bit-identical or oracle-tested forms of the same reference epoch (17 keys, r05):
  *   "train_ahead" 0/1, "eval_ax" 0/1, "split_cols" 0/1, "epoch_graph" 0/1, "mm_side" 0/1/2,
  *   "fuse_epilogue" bits 1 tails | 2 prestaged tables | 4 X-stream epilogue | 8 Dropout /
  *   ReLU backward in a Matmul's input-grad product (default 15),
  *   "fuse_output" 0..3 (default 2), "xstream_ring" 0/1, "lds_min_kb" (< 0: default),
- *   "lds_blocks" 0 (by shape) or 1..32, "lds_slots" 0 (by shape) / 8 / 16 (rowsets per summing
- *   wave of the LDS schedule), "parse_threads" (0: up to 16), "wide_prescale" 0/1
- *   (a multi-pass GraphSum's tables prescaled by one launch, default 1), "rs_chunks" 1..4
- *   (edge-cut GraphSum row chunks at world > 1, default 1), "mask_nib" 0/1 (dense X's input
- *   dropout drawn into the flat bitmap and the GEMMs' nibble layout by one launch, default 0:
- *   two launches), "co_draw" 0/1 (sparse X: the hidden dropout's mask drawn in the input
- *   dropout's launch, default 1), "sparse_dual" 0/1 (sparse X: eval's first-layer product also
- *   computes the next training forward's, default 1), "gs_split" 0..3 (the plain GraphSum's rows longer than one
+ *   "lds_blocks" 0 (by shape) or 1..32, "parse_threads" (0: up to 16),
+ *   "co_draw" 0/1 (sparse X: the hidden dropout's mask drawn in the input dropout's launch,
+ *   default 1), "sparse_dual" 0/1 (sparse X: eval's first-layer product also computes the next
+ *   training forward's, default 1), "gs_split" 0..3 (the plain GraphSum's rows longer than one
  *   work item on graphs of <= 2^20 slots: 0 a combine launch, 1 the row's last item sums the
  *   slots, 2 long rows as one item, 3 (default) rows of up to 8 workgroup iterations summed
  *   by one workgroup, longer ones as 1), "gs_item_iters" 0/2/4/8/16/32 (group iterations per
- *   work item there; 0 (default): by shape, the shortest leaving <= 1,536 workgroup items), "gs_orig_cols" 0/1 (a column subset's plain GraphSum gathers through
- *   the original column ids instead of compacting its input, default 1); diagnostics:
- *   "split_rows" 0/1 (stale logits outside the split),
- * "gemm_variant" 0/1 (the general GEMM kernels only), "plain_blocks" 0/1 (1: the plain
- * GraphSum kernels never split rows into per-XCD column blocks).  Returns PGCN_E_INVALID on an unknown key or on a value outside
- * the key's range (nothing is changed then). */
+ *   work item there; 0 (default): by shape, the shortest leaving <= 1,536 workgroup items),
+ *   "gs_orig_cols" 0/1 (a column subset's plain GraphSum gathers through the original column
+ *   ids instead of compacting its input, default 1);
+ * and one diagnostic, not reference-equivalent: "split_rows" 0/1 (the output layer's forward
+ *   over the current split's rows only: stale logits elsewhere, which get_var refuses).
+ * Returns PGCN_E_INVALID on an unknown key or on a value outside the key's range (nothing is
+ * changed then). */
 int pgcn_debug_set(const char *key, int value);
 /* Host-only check of the d = 16 LDS ring schedule (window must be 5) of a CSR pattern: builds
  * it, walks it as k_graphsum_ring consumes it over a seeded input and returns the max relative

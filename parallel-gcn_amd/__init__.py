@@ -87,8 +87,6 @@ _sig("pgcn_spmm_csc_bwd", c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_v
      c_float, c_void_p, c_void_p, c_void_p)
 _sig("pgcn_csr_transpose", c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p)
 _sig("pgcn_dropout_mask", c_int, c_void_p, c_ll, c_ll, c_ll, c_float, c_void_p, c_void_p, c_void_p)
-_sig("pgcn_dropout_mask_nib", c_int, c_void_p, c_ll, c_ll, c_ll, c_float, c_void_p, c_void_p, c_ll,
-     c_int, c_int, c_void_p, c_void_p)
 _sig("pgcn_dropout_apply", c_int, c_void_p, c_ll, c_void_p, c_float, c_void_p)
 _sig("pgcn_relu_fwd", c_int, c_void_p, c_ll, c_void_p, c_int, c_void_p)
 _sig("pgcn_relu_bwd", c_int, c_void_p, c_ll, c_void_p, c_void_p)
@@ -105,6 +103,10 @@ _sig("pgcn_comm_unique_id", c_int, c_void_p)
 _sig("pgcn_gcn_create_dist", c_int, P(PgcnParams), P(PgcnData), c_int, c_int, c_int, c_void_p,
      P(c_void_p))
 _sig("pgcn_gcn_destroy", c_int, c_void_p)
+# the caller's host all-gather for the peer-mapped engine (pgcn_allgather_fn)
+ALLGATHER_FN = ctypes.CFUNCTYPE(c_int, c_void_p, ctypes.c_size_t, c_void_p, c_void_p)
+_sig("pgcn_gcn_create_peer", c_int, P(PgcnParams), P(PgcnData), c_int, c_int, c_int,
+     ALLGATHER_FN, c_void_p, P(c_void_p))
 _sig("pgcn_loopback_create", c_int, c_int, P(c_void_p))
 _sig("pgcn_debug_gcn_create_solo", c_int, P(PgcnParams), P(PgcnData), c_int, c_int, c_int,
      P(c_void_p))
@@ -287,10 +289,18 @@ class GCN:
     rank/world/unique_id are given (one process per GPU)."""
 
     def __init__(self, params, ds, device=0, rank=None, world=None, unique_id=None,
-                 loopback=None, solo=False):
+                 loopback=None, solo=False, allgather=None):
         self.ds = ds  # keep the host data alive while the engine is built
         h = c_void_p()
-        if solo:  # timing only: rank `rank` of `world` with no peers (pgcn_debug_gcn_create_solo)
+        self._ag = None
+        if allgather is not None:
+            # peer-mapped exchange (pgcn_gcn_create_peer): allgather(bytes) -> [bytes of every
+            # rank], called at creation and at close (kept alive with the engine)
+            self._ag = peer_allgather_fn(allgather)
+            check(lib.pgcn_gcn_create_peer(ctypes.byref(params), ctypes.byref(ds.view), device,
+                                           rank, world, self._ag, None, ctypes.byref(h)),
+                  "gcn_create_peer")
+        elif solo:  # timing only: rank `rank` of `world` with no peers (pgcn_debug_gcn_create_solo)
             check(lib.pgcn_debug_gcn_create_solo(ctypes.byref(params), ctypes.byref(ds.view),
                                                  device, rank, world, ctypes.byref(h)),
                   "gcn_create_solo")
@@ -405,6 +415,36 @@ class LoopbackGroup:
             self._h = c_void_p()
 
 
+def peer_allgather_fn(allgather):
+    """A pgcn_allgather_fn over a Python all-gather: allgather(data: bytes) -> list of every
+    rank's bytes in rank order (torch.distributed, a TCP store, ...)."""
+    def cb(mine, nbytes, out, user):
+        try:
+            parts = allgather(ctypes.string_at(mine, nbytes))
+            buf = b"".join(parts)
+            if len(buf) != nbytes * len(parts):
+                return -1
+            ctypes.memmove(out, buf, len(buf))
+            return 0
+        except Exception:  # noqa: BLE001 -- reported to the engine as a failed all-gather
+            return -1
+    return ALLGATHER_FN(cb)
+
+
+def torch_allgather(group=None):
+    """allgather(bytes) over torch.distributed (gloo: CPU tensors)."""
+    import torch
+    import torch.distributed as dist
+
+    def ag(data):
+        n = dist.get_world_size(group)
+        t = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+        out = [torch.empty_like(t) for _ in range(n)]
+        dist.all_gather(out, t, group=group)
+        return [bytes(o.numpy().tobytes()) for o in out]
+    return ag
+
+
 def run_ranks(world, fn):
     """Calls fn(rank) for every rank in its own thread (ctypes releases the GIL during the
     engine's calls, so the ranks' collectives rendezvous); returns the results in rank order
@@ -500,10 +540,11 @@ EXPORTED = [
     "pgcn_gemm_tn", "pgcn_mask_nibbles", "pgcn_gemm_xstream", "pgcn_gemm_xstream_dual",
     "pgcn_gemm_tn_xstream",
     "pgcn_spmm_csr", "pgcn_spmm_csc_bwd", "pgcn_csr_transpose",
-    "pgcn_rng_jump_table", "pgcn_dropout_mask", "pgcn_dropout_mask_nib", "pgcn_dropout_apply", "pgcn_relu_fwd",
+    "pgcn_rng_jump_table", "pgcn_dropout_mask", "pgcn_dropout_apply", "pgcn_relu_fwd",
     "pgcn_relu_bwd", "pgcn_xent_blocks", "pgcn_xent_fwd", "pgcn_finalize", "pgcn_adam",
     "pgcn_adam_step_size", "pgcn_params_default", "pgcn_gcn_create", "pgcn_comm_unique_id",
-    "pgcn_gcn_create_dist", "pgcn_loopback_create", "pgcn_loopback_destroy",
+    "pgcn_gcn_create_dist", "pgcn_gcn_create_peer", "pgcn_loopback_create",
+    "pgcn_loopback_destroy",
     "pgcn_debug_gcn_create_solo",
     "pgcn_gcn_create_loopback", "pgcn_gcn_query", "pgcn_gcn_destroy", "pgcn_gcn_train_epoch", "pgcn_gcn_eval",
     "pgcn_gcn_epoch_async", "pgcn_gcn_sync", "pgcn_gcn_results", "pgcn_gcn_run",

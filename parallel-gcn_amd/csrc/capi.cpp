@@ -18,7 +18,6 @@ using namespace pgcn;
 
 namespace pgcn {
 // engine knobs (pgcn_debug_set): defaults and meaning at their definitions
-extern int g_gemm_variant;          // k_gemm.hip
 extern int g_train_ahead;           // host/gcn.cpp
 extern int g_split_rows;            // host/gcn.cpp
 extern int g_split_cols;            // host/gcn.cpp
@@ -27,12 +26,9 @@ extern int g_fuse_output;           // host/gcn.cpp
 extern int g_mm_side;               // host/gcn.cpp
 extern int g_eval_ax;               // host/gcn.cpp
 extern int g_epoch_graph;           // host/gcn.cpp
-extern int g_wide_prescale;        // host/graph.cpp
 extern long long g_lds_min_bytes;   // host/graph.cpp
 extern int g_lds_blocks;            // host/graph.cpp
-extern int g_lds_slots;             // host/graph.cpp
 extern int g_xstream_ring;          // k_xstream_lds.hip
-extern int g_plain_blocks;          // host/graph.cpp
 extern int g_gs_split;              // host/graph.cpp
 extern int g_co_draw;               // host/gcn.cpp
 extern int g_sparse_dual;           // host/gcn.cpp
@@ -333,19 +329,6 @@ int pgcn_dropout_mask(uint64_t *chunk_states, long long n_chunks, long long n_el
   });
 }
 
-int pgcn_dropout_mask_nib(uint64_t *chunk_states, long long n_chunks, long long n_elems,
-                          long long elem0, float p, uint64_t *mask, const void *dev_jump_table,
-                          long long mask_base, int F, int rows, uint64_t *mask_nib,
-                          void *stream) {
-  return guarded([&] {
-    PGCN_CHECK(mask_nib && dropout_mask_nib_ok(F, mask_base), PGCN_E_INVALID,
-               "dropout_mask_nib: F in [1, 1024] with chunk-aligned row cuts from mask_base");
-    launch_dropout_mask_nib(chunk_states, n_chunks, elem0, n_elems, p, mask, dev_jump_table,
-                            mask_base, F, rows, mask_nib, as_stream(stream));
-    PGCN_HIP(hipGetLastError());
-  });
-}
-
 int pgcn_dropout_apply(float *x, long long n, const uint64_t *mask, float scale, void *stream) {
   return guarded([&] {
     launch_dropout_apply_based(x, n, mask, 0, scale, as_stream(stream));
@@ -440,6 +423,27 @@ int pgcn_gcn_create_dist(const pgcn_params *p, const pgcn_data *d, int device, i
   });
 }
 
+int pgcn_gcn_create_peer(const pgcn_params *p, const pgcn_data *d, int device, int rank,
+                         int world, pgcn_allgather_fn allgather, void *user, pgcn_gcn **out) {
+  return guarded([&] {
+    PGCN_CHECK(p && d && out && allgather && world >= 1 && world <= kPeerMaxRanks && rank >= 0 &&
+                   rank < world,
+               PGCN_E_INVALID, "gcn_create_peer args");
+    check_device();
+    GCNData data = to_data(d, p);
+    DistSpec ds;
+    ds.rank = rank;
+    ds.world = world;
+    ds.allgather = [allgather, user](const void *mine, size_t bytes, void *all) {
+      if (allgather(mine, bytes, all, user) != 0)
+        throw Error(PGCN_E_COMM, "peer comm: the caller's all-gather failed");
+    };
+    auto h = std::make_unique<pgcn_gcn>();
+    h->g = std::make_unique<GCN>(to_params(p, d), to_adam(p), data, device, &ds);
+    *out = h.release();
+  });
+}
+
 int pgcn_debug_gcn_create_solo(const pgcn_params *p, const pgcn_data *d, int device, int rank,
                                int world, pgcn_gcn **out) {
   return guarded([&] {
@@ -494,7 +498,10 @@ long long pgcn_gcn_query(pgcn_gcn *g, const char *key) {
   if (!std::strcmp(key, "world")) return c ? c->world() : 1;
   if (!std::strcmp(key, "rank")) return c ? c->rank() : 0;
   if (!std::strcmp(key, "comm"))
-    return c ? (!std::strcmp(c->kind(), "rccl") ? 1 : !std::strcmp(c->kind(), "loopback") ? 2 : 3)
+    return c ? (!std::strcmp(c->kind(), "rccl")       ? 1
+                : !std::strcmp(c->kind(), "loopback") ? 2
+                : !std::strcmp(c->kind(), "solo")     ? 3
+                                                      : 4)
              : 0;
   if (!std::strcmp(key, "comm_calls")) return c ? c->calls : 0;
   if (!std::strcmp(key, "comm_bytes")) return c ? (long long)c->bytes : 0;
@@ -680,9 +687,6 @@ int pgcn_debug_set(const char *key, int value) {
   } else if (!std::strcmp(key, "xstream_ring")) {
     if (!in(0, 1)) return PGCN_E_INVALID;
     pgcn::g_xstream_ring = value;
-  } else if (!std::strcmp(key, "gemm_variant")) {
-    if (!in(0, 1)) return PGCN_E_INVALID;
-    pgcn::g_gemm_variant = value;
   } else if (!std::strcmp(key, "lds_min_kb")) {  // < 0: the default
     pgcn::g_lds_min_bytes = value < 0 ? DevGraph::kLdsMinBytes : 1024LL * value;
   } else if (!std::strcmp(key, "lds_blocks")) {
@@ -690,9 +694,6 @@ int pgcn_debug_set(const char *key, int value) {
         value != 32)
       return PGCN_E_INVALID;
     pgcn::g_lds_blocks = value;
-  } else if (!std::strcmp(key, "plain_blocks")) {
-    if (!in(0, 1)) return PGCN_E_INVALID;
-    pgcn::g_plain_blocks = value;
   } else if (!std::strcmp(key, "gs_orig_cols")) {
     if (!in(0, 1)) return PGCN_E_INVALID;
     pgcn::g_gs_orig_cols = value;
@@ -709,21 +710,9 @@ int pgcn_debug_set(const char *key, int value) {
     if (value != 0 && value != 2 && value != 4 && value != 8 && value != 16 && value != 32)
       return PGCN_E_INVALID;
     pgcn::g_gs_item_iters = value;
-  } else if (!std::strcmp(key, "lds_slots")) {
-    if (value != 0 && !ring_slots_ok(value)) return PGCN_E_INVALID;
-    pgcn::g_lds_slots = value;
   } else if (!std::strcmp(key, "parse_threads")) {
     if (!in(0, 4096)) return PGCN_E_INVALID;
     pgcn::g_parse_threads = value;
-  } else if (!std::strcmp(key, "mask_nib")) {
-    if (!in(0, 1)) return PGCN_E_INVALID;
-    pgcn::g_mask_nib = value;
-  } else if (!std::strcmp(key, "rs_chunks")) {
-    if (!in(1, 4)) return PGCN_E_INVALID;
-    pgcn::g_rs_chunks = value;
-  } else if (!std::strcmp(key, "wide_prescale")) {
-    if (!in(0, 1)) return PGCN_E_INVALID;
-    pgcn::g_wide_prescale = value;
   } else {
     return PGCN_E_INVALID;
   }

@@ -187,7 +187,7 @@ struct LoopbackGroup::Impl {
 };
 
 LoopbackGroup::LoopbackGroup(int world) : impl_(std::make_shared<Impl>()), world_(world) {
-  PGCN_CHECK(world >= 1 && world <= kLoopbackMaxRanks, PGCN_E_INVALID,
+  PGCN_CHECK(world >= 1 && world <= kPeerMaxRanks, PGCN_E_INVALID,
              "loopback group: world must be in [1, 16]");
   impl_->ptrs.assign((size_t)world, nullptr);
   impl_->evs.assign((size_t)world, nullptr);
@@ -220,57 +220,176 @@ void LoopbackGroup::exchange(int rank, const void *ptr, hipEvent_t ev,
   *evs = m.out_evs;
 }
 
-LoopbackComm::LoopbackComm(int rank, std::shared_ptr<LoopbackGroup> group)
-    : Comm(rank, group->world()), group_(std::move(group)) {
-  PGCN_CHECK(rank >= 0 && rank < world_, PGCN_E_INVALID, "loopback comm: rank");
-  PGCN_HIP(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
-  PGCN_HIP(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
-}
+}  // namespace pgcn
 
-LoopbackComm::~LoopbackComm() {
-  if (ready_) (void)hipEventDestroy(ready_);
-  if (done_) (void)hipEventDestroy(done_);
-  if (tmp_) (void)hipFree(tmp_);
-}
+namespace pgcn {
 
-// dst[0, count) = sum over ranks q (in rank order) of send_q[src_offset, src_offset + count)
-void LoopbackComm::collective(const float *send, float *dst, size_t count, size_t src_offset,
-                              hipStream_t s) {
+// ------------------------------------------------------------------------------------------
+// Peer-mapped collectives (k_peer.hip)
+// ------------------------------------------------------------------------------------------
+void LoopbackGroup::barrier(int rank) {
   std::vector<const void *> ptrs;
   std::vector<hipEvent_t> evs;
-  PGCN_HIP(hipEventRecord(ready_, s));  // this rank's send buffer is complete
-  group_->exchange(rank_, send, ready_, &ptrs, &evs);
-  LoopbackSrcs srcs{};
-  for (int q = 0; q < world_; q++) {
-    if (q != rank_) PGCN_HIP(hipStreamWaitEvent(s, evs[(size_t)q], 0));
-    srcs.p[q] = static_cast<const float *>(ptrs[(size_t)q]) + src_offset;
-  }
-  srcs.n = world_;
-  launch_loopback_sum(srcs, dst, count, s);
-  PGCN_HIP(hipEventRecord(done_, s));  // this rank has read every peer's buffer
-  group_->exchange(rank_, nullptr, done_, &ptrs, &evs);
-  for (int q = 0; q < world_; q++)
-    if (q != rank_) PGCN_HIP(hipStreamWaitEvent(s, evs[(size_t)q], 0));
+  exchange(rank, nullptr, nullptr, &ptrs, &evs);
 }
 
-void LoopbackComm::allreduce_sum(float *buf, size_t n, hipStream_t s) {
+void LoopbackGroup::allgather(int rank, const void *mine, size_t bytes, void *all) {
+  std::vector<const void *> ptrs;
+  std::vector<hipEvent_t> evs;
+  exchange(rank, mine, nullptr, &ptrs, &evs);
+  for (int q = 0; q < world_; q++)
+    std::memcpy(static_cast<char *>(all) + (size_t)q * bytes, ptrs[(size_t)q], bytes);
+  exchange(rank, nullptr, nullptr, &ptrs, &evs);  // every rank has copied: `mine` may go
+}
+
+namespace {
+// region layout: [flags: kPeerMaxRanks words][arrival counter][error word] ... 4 KB, slots
+constexpr size_t kPeerHeader = 4096;
+constexpr size_t kArriveOff = kPeerMaxRanks * 4, kErrOff = kArriveOff + 4;
+
+struct PeerBlob {  // what a rank publishes at construction
+  hipIpcMemHandle_t handle;
+  unsigned long long ptr;  // in-process: the region's device address
+  int ok;
+  int pad;
+};
+}  // namespace
+
+PeerComm::PeerComm(int rank, int world, size_t slot_floats, AllGather ag, bool ipc,
+                   std::function<void()> host_order)
+    : Comm(rank, world), ag_(std::move(ag)), ipc_(ipc), host_order_(std::move(host_order)) {
+  PGCN_CHECK(world >= 1 && world <= kPeerMaxRanks && rank >= 0 && rank < world && ag_,
+             PGCN_E_INVALID, "peer comm: rank / world");
+  slot_floats_ = (std::max<size_t>(slot_floats, 4) + 63) / 64 * 64;  // 256-B aligned slots
+  bytes_ = kPeerHeader + 2 * (size_t)world * slot_floats_ * sizeof(float);
+  // uncached: no cache of this GPU or a peer holds a line of the flags or the slots
+  void *p = nullptr;
+  if (hipExtMallocWithFlags(&p, bytes_, hipDeviceMallocUncached) != hipSuccess || !p)
+    throw Error(PGCN_E_NOMEM, "peer comm: uncached region of " + std::to_string(bytes_) + " B");
+  region_ = static_cast<char *>(p);
+  PGCN_HIP(hipMemset(region_, 0, kPeerHeader));
+  PGCN_HIP(hipDeviceSynchronize());
+  PeerBlob mine{};
+  mine.ptr = (unsigned long long)(uintptr_t)region_;
+  mine.ok = 1;
+  if (ipc_ && hipIpcGetMemHandle(&mine.handle, region_) != hipSuccess) mine.ok = 0;
+  std::vector<PeerBlob> all((size_t)world);
+  ag_(&mine, sizeof mine, all.data());
+  // every rank reports whether it could map every peer; all fail together
+  int ok = 1;
+  std::string why;
+  for (int q = 0; q < world; q++) ok &= all[(size_t)q].ok;
+  if (!ok) why = "a rank could not export its region";
+  peer_.assign((size_t)world, nullptr);
+  for (int q = 0; q < world && ok; q++) {
+    if (q == rank || !ipc_) {
+      peer_[(size_t)q] = q == rank ? region_ : reinterpret_cast<char *>((uintptr_t)all[(size_t)q].ptr);
+      continue;
+    }
+    void *m = nullptr;
+    const hipError_t e = hipIpcOpenMemHandle(&m, all[(size_t)q].handle, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess || !m) {
+      ok = 0;
+      why = std::string("hipIpcOpenMemHandle of rank ") + std::to_string(q) + ": " + hipGetErrorString(e);
+      break;
+    }
+    peer_[(size_t)q] = static_cast<char *>(m);
+  }
+  int oks[kPeerMaxRanks];
+  ag_(&ok, sizeof ok, oks);
+  for (int q = 0; q < world; q++) ok &= oks[q];
+  if (!ok) {
+    for (int q = 0; q < world; q++)
+      if (ipc_ && q != rank && peer_[(size_t)q]) (void)hipIpcCloseMemHandle(peer_[(size_t)q]);
+    peer_.clear();
+    (void)hipFree(region_);
+    region_ = nullptr;
+    throw Error(PGCN_E_COMM, "peer comm: " + (why.empty() ? std::string("a peer failed to map") : why));
+  }
+}
+
+PeerComm::~PeerComm() {
+  if (!region_) return;
+  (void)hipDeviceSynchronize();
+  // nobody closes or frees before every rank is done with every collective, and nobody frees
+  // before every peer has closed its mapping of this region
+  int token = 0;
+  std::vector<int> all((size_t)world_);
+  try {
+    ag_(&token, sizeof token, all.data());
+  } catch (...) {
+  }
+  if (ipc_)
+    for (int q = 0; q < world_; q++)
+      if (q != rank_ && peer_[(size_t)q]) (void)hipIpcCloseMemHandle(peer_[(size_t)q]);
+  try {
+    ag_(&token, sizeof token, all.data());
+  } catch (...) {
+  }
+  (void)hipFree(region_);
+}
+
+float *PeerComm::slot(char *region, int parity, int sender) const {
+  return reinterpret_cast<float *>(region + kPeerHeader) +
+         ((size_t)parity * world_ + (size_t)sender) * slot_floats_;
+}
+
+PeerSink PeerComm::sink(int rows_per_rank, size_t row_floats) {
+  PGCN_CHECK((size_t)rows_per_rank * row_floats <= slot_floats_, PGCN_E_INVALID,
+             "peer comm: collective larger than its slots");
+  const unsigned g = ++gen_;
+  PeerSink k{};
+  for (int q = 0; q < world_; q++) {
+    k.dst[q] = slot(peer_[(size_t)q], (int)(g & 1), rank_);
+    k.flag[q] = reinterpret_cast<unsigned *>(peer_[(size_t)q]) + rank_;
+  }
+  k.arrive = reinterpret_cast<unsigned *>(region_ + kArriveOff);
+  k.gen = g;
+  k.world = world_;
+  k.rows_per_rank = rows_per_rank;
+  k.signal = 1;
+  return k;
+}
+
+void PeerComm::wait(hipStream_t s) {
+  if (host_order_) host_order_();
+  launch_peer_wait(reinterpret_cast<const unsigned *>(region_), world_, gen_,
+                   reinterpret_cast<unsigned *>(region_ + kErrOff), s);
+}
+
+PeerRecv PeerComm::recv() const {
+  PeerRecv r{};
+  for (int q = 0; q < world_; q++) r.slot[q] = slot(region_, (int)(gen_ & 1), q);
+  r.world = world_;
+  return r;
+}
+
+void PeerComm::check() const {
+  unsigned e = 0;
+  PGCN_HIP(hipMemcpy(&e, region_ + kErrOff, sizeof e, hipMemcpyDeviceToHost));
+  if (e)
+    throw Error(PGCN_E_COMM, "peer exchange: rank " + std::to_string(e & 0xffff) +
+                                 " did not signal rank " + std::to_string(rank_) + " in time");
+}
+
+void PeerComm::allreduce_sum(float *buf, size_t n, hipStream_t s) {
   if (world_ == 1 || n == 0) return;
   count(n * sizeof(float), 2.0);
-  if (tmp_n_ < n) {
-    if (tmp_) PGCN_HIP(hipFree(tmp_));
-    tmp_ = nullptr;
-    PGCN_HIP(hipMalloc(&tmp_, n * sizeof(float)));
-    tmp_n_ = n;
-  }
-  // every peer has read `buf` once collective() returns on the stream: then overwrite it
-  collective(buf, tmp_, n, 0, s);
-  PGCN_HIP(hipMemcpyAsync(buf, tmp_, n * sizeof(float), hipMemcpyDeviceToDevice, s));
+  PeerSink k = sink(1, n);
+  // every receiver gets the same n floats: send[q * n ..) = buf for every q (stride 0)
+  k.rows_per_rank = 0;
+  launch_peer_push(buf, n, k, s, /*same_for_all=*/true);
+  wait(s);
+  launch_peer_sum(recv(), buf, n, s);
 }
 
-void LoopbackComm::reduce_scatter_sum(const float *send, float *recv, size_t recvcount,
-                                      hipStream_t s) {
+void PeerComm::reduce_scatter_sum(const float *send, float *recv_buf, size_t recvcount,
+                                  hipStream_t s) {
   count(recvcount * world_ * sizeof(float), 1.0);
-  collective(send, recv, recvcount, (size_t)rank_ * recvcount, s);
+  PeerSink k = sink(1, recvcount);
+  launch_peer_push(send, recvcount, k, s, false);
+  wait(s);
+  launch_peer_sum(recv(), recv_buf, recvcount, s);
 }
 
 }  // namespace pgcn

@@ -9,10 +9,13 @@
 // reduce-scatter per GraphSum call.  Weight gradients and loss scalars are all-reduced.
 #pragma once
 #include <cstddef>
+#include <functional>
 #include <memory>
 #include <vector>
 
 #include <hip/hip_runtime.h>
+
+#include "../kernels.hpp"
 
 namespace pgcn {
 
@@ -67,6 +70,8 @@ class Comm {
   // send buffer of B bytes moves B (world - 1) / world per rank; an all-reduce 2x that)
   long long calls = 0;
   double bytes = 0.0;
+  // a collective enqueued outside the calls above (PeerComm's fused GraphSum exchange)
+  void note(size_t send_bytes, double factor) { count(send_bytes, factor); }
 
  protected:
   void count(size_t send_bytes, double factor) {
@@ -102,13 +107,10 @@ class RcclComm : public Comm {
   void *comm_ = nullptr;  // ncclComm_t
 };
 
-// In-process "fake RCCL" (SURVEY.md §4): `world` engines in one process on one device, each
-// driven by its own host thread.  A collective is a host rendezvous of the ranks (each posts
-// its buffer and an event recorded after its producer), then every rank's stream waits for
-// all peers' events and sums the peers' buffers in rank order with a device kernel, then a
-// second rendezvous on "read done" events before any rank may overwrite its send buffer.
-// Same stream semantics as RCCL, so the edge-cut engine runs unchanged at world 2, 4, ... on
-// one GPU (RCCL itself refuses two ranks on one device).
+// In-process ranks (SURVEY.md §4 "fake RCCL"): `world` engines in one process on one device,
+// each driven by its own host thread; their PeerComms exchange raw device pointers through
+// this group's host rendezvous, and then run exactly the multi-process exchange's kernels
+// (RCCL itself refuses two ranks on one device).
 class LoopbackGroup {
  public:
   explicit LoopbackGroup(int world);
@@ -117,6 +119,9 @@ class LoopbackGroup {
   // ranks, return every rank's (ptr, ev).  Throws PGCN_E_COMM after `timeout_s` seconds.
   void exchange(int rank, const void *ptr, hipEvent_t ev, std::vector<const void *> *ptrs,
                 std::vector<hipEvent_t> *evs);
+  // PeerComm::AllGather between the group's ranks (host threads of one process)
+  void allgather(int rank, const void *mine, size_t bytes, void *all);
+  void barrier(int rank);  // every rank of the group has called it
   double timeout_s = 60.0;
 
  private:
@@ -125,21 +130,51 @@ class LoopbackGroup {
   int world_;
 };
 
-class LoopbackComm : public Comm {
+// One-sided exchange over peer-mapped receive slots (k_peer.hip).  Every rank
+// owns one uncached device region: its flag words (one per sender), an arrival counter, an
+// error word, and 2 x world receive slots (generation parity x sender) of slot_floats floats.
+// Every region is mapped into every rank: hipIpcGetMemHandle / hipIpcOpenMemHandle between
+// processes (`ipc`, one process per GPU), raw device pointers between the in-process loopback
+// ranks on one device.  A collective is: pushes into the receivers' slots (k_peer_push, or the
+// GraphSum combine itself: k_gs_lds_combine's push mode), the flags, one wave waiting for them,
+// a rank-order sum of the received slots.  Stream-ordered like RCCL; every collective of a
+// rank runs on one stream, in the same order on every rank.
+class PeerComm : public Comm {
  public:
-  LoopbackComm(int rank, std::shared_ptr<LoopbackGroup> group);
-  ~LoopbackComm() override;
+  // all[q * bytes, (q + 1) * bytes) = rank q's `mine` (every rank calls it, in the same order;
+  // throws on failure).  The engine calls it at construction and destruction only.
+  using AllGather = std::function<void(const void *mine, size_t bytes, void *all)>;
+  // slot_floats: the largest collective's floats per rank
+  // host_order (in-process ranks): before a rank enqueues a wait, every rank has enqueued the
+  // push it waits for -- ranks of one process may share hardware queues (GPU_MAX_HW_QUEUES),
+  // where a wait ahead of a peer's push would block that push (a host rendezvous per wait)
+  PeerComm(int rank, int world, size_t slot_floats, AllGather ag, bool ipc,
+           std::function<void()> host_order = nullptr);
+  ~PeerComm() override;
   void allreduce_sum(float *buf, size_t n, hipStream_t s) override;
   void reduce_scatter_sum(const float *send, float *recv, size_t recvcount,
                           hipStream_t s) override;
-  const char *kind() const override { return "loopback"; }
+  const char *kind() const override { return ipc_ ? "peer" : "loopback"; }
+  // The GraphSum exchange fused into the combine: sink() opens the next collective and returns
+  // where this rank's rows go (rows_per_rank padded rows per owner, owner-major); after the
+  // push, wait() enqueues the wait for every sender and recv() names the received slots
+  PeerSink sink(int rows_per_rank, size_t row_floats);
+  void wait(hipStream_t s);
+  PeerRecv recv() const;
+  size_t slot_floats() const { return slot_floats_; }
+  // throws PGCN_E_COMM when a wait gave up (a peer never signalled); call after a sync
+  void check() const;
 
  private:
-  void collective(const float *send, float *dst, size_t count, size_t src_offset, hipStream_t s);
-  std::shared_ptr<LoopbackGroup> group_;
-  hipEvent_t ready_ = nullptr, done_ = nullptr;
-  float *tmp_ = nullptr;  // all-reduce result before it overwrites `buf`
-  size_t tmp_n_ = 0;
+  float *slot(char *region, int parity, int sender) const;
+  char *region_ = nullptr;                   // this rank's region
+  std::vector<char *> peer_;                 // every rank's region as mapped here
+  size_t slot_floats_ = 0, bytes_ = 0;
+  unsigned gen_ = 0;                         // the last collective's generation
+  AllGather ag_;
+  bool ipc_ = false;
+  std::function<void()> host_order_;
 };
+
 
 }  // namespace pgcn

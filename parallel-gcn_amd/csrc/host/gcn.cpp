@@ -59,13 +59,6 @@ int g_sparse_dual = 1;
 // stream hand-offs cost more than the ~7 us of kernels they hide)
 int g_mm_side = 0;
 constexpr int kMmSideRows = 65536;
-// "rs_chunks" (read at engine build): GraphSum row chunks of the edge-cut engine at world > 1
-// (chunk k's reduce-scatter overlaps chunk k+1's local sum)
-int g_rs_chunks = kRsChunks;
-// "mask_nib" (read per draw): 1 = dense X's input dropout mask drawn straight into the nibble
-// layout too (k_dropout_mask_nib, one launch); 0 = k_dropout_mask + k_mask_nibbles (default:
-// r04h, alone on reddit's mask 91 vs 96 us, the epoch equal within 0.3 %)
-int g_mask_nib = 0;
 
 // ------------------------------------------------------------------------------------------
 // Adam (src/optim.cu:7-95; hpdga optim.cpp:16-35)
@@ -277,14 +270,35 @@ GCN::GCN(const GCNParams &params_, const AdamParams &adam, const GCNData &data, 
   const int world = dist ? dist->world : 1, rank = dist ? dist->rank : 0;
   // one row chunk on one rank: nothing to exchange, nothing to overlap
   part = make_partition(params.num_nodes, data.graph.indptr.data(), world, rank,
-                        dist && world > 1 ? g_rs_chunks : 1);
+                        1);
   if (dist) {  // the edge-cut path (also at world == 1, which exercises it on one GPU)
-    if (dist->solo)
+    if (dist->solo) {
       comm = std::make_unique<SoloComm>(rank, world);
-    else if (dist->loopback)
-      comm = std::make_unique<LoopbackComm>(rank, dist->loopback);
-    else
+    } else if (dist->loopback || dist->allgather) {
+      // peer-mapped slots sized for the largest collective: a GraphSum's rows of one owner at
+      // the widest row, the weight-gradient all-reduce, Â X's 16-column reduce-scatters
+      size_t ld = 16;
+      for (int h : params.hidden_dims) ld = std::max(ld, (size_t)round_up4(h));
+      ld = std::max(ld, (size_t)round_up4(params.output_dim));
+      long long wtotal = 0;
+      for (int l = 0; l < L; l++) {
+        const int a = l == 0 ? params.input_dim : params.hidden_dims[(size_t)l - 1];
+        const int b = l == L - 1 ? params.output_dim : params.hidden_dims[(size_t)l];
+        wtotal += (long long)a * b;
+      }
+      const size_t cap = std::max((size_t)part.maxrows * ld, (size_t)wtotal);
+      if (dist->loopback) {
+        auto grp = dist->loopback;
+        comm = std::make_unique<PeerComm>(
+            rank, world, cap,
+            [grp, rank](const void *m, size_t b, void *all) { grp->allgather(rank, m, b, all); },
+            false, [grp, rank] { grp->barrier(rank); });
+      } else {
+        comm = std::make_unique<PeerComm>(rank, world, cap, dist->allgather, true);
+      }
+    } else {
       comm = std::make_unique<RcclComm>(rank, world, dist->unique_id);
+    }
     ctx.comm = comm.get();
     comm_stream = Stream::create(hi_prio);
     ctx.comm_stream = comm_stream.get();
@@ -391,6 +405,12 @@ void GCN::build(const GCNData &data) {
     graph->set_scales(sg, sg);
   }
   upload_features(data);
+  // eval_ax (dense X): Â X's buffer now -- the modules built below read it -- and its sums at
+  // the end of the build (build_eval_ax)
+  if (g_eval_ax && feats.dense && feats.cols >= 16 && (comm || graph)) {
+    feats.ax.allocate(feats.x.size());
+    feats.ax.zero();
+  }
   // truth per split for this rank's rows, padded with -1 (set_truth, src/gcn.cu:204-226)
   const int first = part.first(), rows = part.local_rows(), prow = part.maxrows;
   for (int s = 1; s <= 3; s++) {
@@ -484,10 +504,6 @@ void GCN::build(const GCNData &data) {
     insert_layer(params.hidden_dims[(size_t)l - 1], params.hidden_dims[(size_t)l],
                  params.dropouts[(size_t)l], l);
   insert_last_layer();
-  // dense X: the input dropout draws straight into the nibble layout its GEMM reads
-  if (feats.dense && (feats.maskT || feats.maskW) && feats.cols <= 1024)
-    const_cast<Dropout *>(dropouts_[0])->set_nibbles(feats.maskT ? feats.maskT.get() : feats.maskW.get(), feats.cols,
-                              feats.rows);
   // (edge-cut: the tails run in k_gs_finish on the rank's rows after the reduce-scatter)
   if (g_fuse_epilogue & kFuseTails) fuse_epilogues();
   if (g_fuse_epilogue & kFuseMatmulTails) fuse_matmul_tails();
@@ -510,9 +526,7 @@ void GCN::build_eval_ax() {
   // (its device time is kept in ax_build_ms: bench.py amortises it over the reference's
   // 100-epoch run)
   Event ax0 = Event::create(true), ax1 = Event::create(true);
-  if (g_eval_ax && !comm && graph && feats.dense && feats.cols >= 16) {
-    feats.ax.allocate(feats.x.size());
-    feats.ax.zero();
+  if (feats.ax && !comm) {
     graph->prepare(16);  // the schedule's host build is set-up, not Â X's device time
     ax0.record(stream.get());
     for (int c0 = 0; c0 < feats.cols; c0 += 16) {
@@ -526,10 +540,8 @@ void GCN::build_eval_ax() {
   // the same for the edge-cut engine: per 16-column chunk of X, every row chunk's partial
   // sums from this rank's columns reduce-scattered exactly as GraphSum::run does (this rank
   // receives its own rows), then placed into Â X's columns
-  if (g_eval_ax && comm && feats.dense && feats.cols >= 16) {
+  if (feats.ax && comm) {
     const int h = part.chunk_rows(), nk = (int)chunk_graphs.size();
-    feats.ax.allocate(feats.x.size());
-    feats.ax.zero();
     DeviceBuffer<float> partial((size_t)part.world * h * 16), own((size_t)nk * h * 16);
     for (auto &gk : chunk_graphs) gk->prepare(16);
     ax0.record(stream.get());
@@ -961,6 +973,7 @@ std::pair<float, float> GCN::read_slot(int off) {
     PGCN_HIP(hipMemcpyAsync(pinned.get(), raw_ring.get() + (size_t)off * 2, 4 * sizeof(float),
                             hipMemcpyDeviceToHost, stream.get()));
     stream.sync();
+    check_comm();
     float r[2];
     compose_raw(pinned.get(), r);
     return {r[0], r[1]};
@@ -987,6 +1000,12 @@ std::pair<float, float> GCN::eval(int split) {
 void GCN::sync() {
   stream.sync();
   side_stream.sync();
+  check_comm();
+}
+
+// a peer exchange that gave up waiting (a rank never signalled) fails the call that syncs
+void GCN::check_comm() const {
+  if (const auto *pc = dynamic_cast<const PeerComm *>(comm.get())) pc->check();
 }
 
 std::vector<float> GCN::results(int n) {

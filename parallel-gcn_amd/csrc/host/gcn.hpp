@@ -25,8 +25,6 @@ namespace pgcn {
 // for two row chunks, whose 30 rowset batches leave half the CUs idle; a 13 MB exchange at
 // 300 GB/s then fits in the 22.6 us the second chunk would have hidden, and above that rate
 // one chunk is ahead; profiles/r04/rank_graphsum_c1.json, rank_graphsum_c2.json)
-constexpr int kRsChunks = 1;
-extern int g_rs_chunks;
 
 struct GCNParams {
   int num_nodes = 0, input_dim = 0, output_dim = 0;
@@ -79,8 +77,11 @@ class Adam {
 struct DistSpec {
   int rank = 0, world = 1;
   const void *unique_id = nullptr;  // 128 bytes (RCCL)
-  // in-process ranks on one device (LoopbackComm) instead of RCCL; world = group->world()
+  // in-process ranks on one device (PeerComm over raw pointers); world = group->world()
   std::shared_ptr<LoopbackGroup> loopback;
+  // one process per GPU over peer-mapped slots (PeerComm over hipIpc handles, exchanged by
+  // this host all-gather) instead of RCCL
+  PeerComm::AllGather allgather;
   bool solo = false;  // timing only: SoloComm (no peers)
 };
 
@@ -125,6 +126,7 @@ class GCN {
   void fuse_matmul_tails();
   void fuse_output_layer();
   void prepare_graphs();
+  void check_comm() const;
   void build_eval_ax();
   void join_side();
   int fused_tails_ = 0;  // GraphSum epilogues carrying ReLU / Dropout work (forward + backward)

@@ -115,11 +115,7 @@ DevGraph::DevGraph(int n_rows, int n_cols, const int *indptr, const int *indices
 // padded rows): 3.7 MB table (4 ranks) LDS 0.123 vs plain 0.249 ms, 1.9 MB (8 ranks) 0.083 vs
 // 0.114 ms; 15 MB (1 rank) 0.33 vs 1.04 ms
 long long g_lds_min_bytes = DevGraph::kLdsMinBytes;
-int g_wide_prescale = 1;  // diagnostics ("wide_prescale" 0: one prescale launch per pass)
 
-// "plain_blocks" (read at schedule build): 0 = the plain path blocks its columns per XCD above
-// kL2Budget, 1 = never (one block: whole rows per item)
-int g_plain_blocks = 0;
 
 // "gs_split" (read at schedule build), the rows of the plain unblocked path longer than one
 // work item: 0 = their items write slots that a combine launch sums; 1 = the last of a row's
@@ -144,7 +140,6 @@ int g_gs_item_iters = 0;
 int g_gs_orig_cols = 1;
 
 int DevGraph::column_blocks(int dim) {
-  if (g_plain_blocks == 1) return 1;
   const int vec = (dim + 3) / 4;
   const double table = (double)n_cols_ * vec * 16.0;
   return (graphsum_group_lanes(vec) < 64 && table > kL2Budget) ? kBlocks : 1;
@@ -418,13 +413,11 @@ void DevGraph::set_scales(std::vector<float> row_scale, std::vector<float> col_s
 // 256 workgroups, half the partials; the same kernel time, combine 18 -> 11 us), 8 for a small
 // row subset (its 256 workgroups then stream half the table each: val rows 0.11 vs 0.22 ms)
 int g_lds_blocks = 0;
-// "lds_slots": rowsets per summing wave of the LDS schedule, 0 = by shape (16), or 8 / 16
-int g_lds_slots = 0;
 
 int lds_slots(int n_rows, int n_cols) {
   (void)n_rows;
   (void)n_cols;
-  return g_lds_slots ? g_lds_slots : LDS_SLOTS;
+  return LDS_SLOTS;
 }
 
 int lds_blocks(int n_rows, int n_cols) {
@@ -547,7 +540,7 @@ bool DevGraph::can_share_tables(int dim, int ld_in) const {
   if (!uses_lds(dim)) return false;
   // one 16-column pass, or every pass's table from the batched prescale -- graphsum()'s
   // `batch` condition below (ld_in <= 128); wider inputs prescale per pass
-  return dim <= 16 || (!col_map_ && g_wide_prescale && ld_in <= 128);
+  return dim <= 16 || (!col_map_ && ld_in <= 128);
 }
 
 float *DevGraph::table_scratch() {
@@ -565,7 +558,7 @@ float *DevGraph::table_wide(size_t floats) {
 
 void DevGraph::graphsum(const float *in, int ld_in, float *out, int ld_out, int dim,
                         hipStream_t s, bool compact_in, const GsEpilogue *epi, bool prestaged,
-                        bool tables_ready) {
+                        bool tables_ready, const PeerSink *push) {
   const int *col_map = compact_in ? nullptr : col_map_.get();
   PGCN_CHECK(ld_in % 4 == 0 && ld_out % 4 == 0 && ld_in >= dim && ld_out >= dim,
              PGCN_E_INVALID, "graphsum: leading dims must be multiples of 4 and >= dim");
@@ -586,7 +579,7 @@ void DevGraph::graphsum(const float *in, int ld_in, float *out, int ld_out, int 
     auto pass_col = [&](int p) { return std::min(16 * p, ldm - 16); };
     // several passes: one launch prescales all of them (each pass then reads its own table);
     // inputs up to 128 wide (at most 8 passes: RingPasses), wider ones prescale per pass
-    const bool batch = n_pass > 1 && !col_map && ld_in <= 128 && g_wide_prescale;
+    const bool batch = n_pass > 1 && !col_map && ld_in <= 128;
     PGCN_CHECK(!tables_ready || (can_share_tables(dim, ld_in) && (n_pass == 1 || batch)),
                PGCN_E_INVALID, "graphsum: shared tables on a call that prescales per pass");
     RingPasses ps;
@@ -602,12 +595,19 @@ void DevGraph::graphsum(const float *in, int ld_in, float *out, int ld_out, int 
       const int c = pass_col(p);
       GsEpilogue ep = epi ? *epi : GsEpilogue{};
       ep.col0 = c;
-      launch_graphsum_ring(lds_->s, in + c, ld_in, out + c, ld_out,
+      PeerSink pk;
+      if (push) {  // this pass's columns of every owner's slot; the last pass signals
+        pk = *push;
+        for (int q = 0; q < pk.world; q++) pk.dst[q] += c;
+        pk.signal = p == n_pass - 1 ? push->signal : 0;
+      }
+      launch_graphsum_ring(lds_->s, in + c, ld_in, out ? out + c : nullptr, ld_out,
                            batch ? tables + table * p : table_scratch(), lds_->partial.get(), s,
-                           col_map, &ep, prestaged || batch || tables_ready);
+                           col_map, &ep, prestaged || batch || tables_ready, push ? &pk : nullptr);
     }
     return;
   }
+  PGCN_CHECK(!push, PGCN_E_INVALID, "graphsum: push on the plain path");
   if (dim > 16 && !graphsum_vec_supported((dim + 3) / 4)) {
     // widths without a kernel instantiation (PART2 hidden 72, 600): 16-column passes, the
     // last one overlapping the one before it (recomputed columns get the same bits)

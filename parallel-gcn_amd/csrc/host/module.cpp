@@ -63,26 +63,8 @@ Dropout::Dropout(shared_ptr<Variable> in_, float p_, shared_ptr<DropoutRng> rng_
 
 void Dropout::draw(hipStream_t s, uint64_t *mask, int max_blocks) const {
   const DropoutRng &r = *rng;
-  if (nib_ && max_blocks == 0 && g_mask_nib && dropout_mask_nib_ok(nib_F_, r.mask_base)) {
-    launch_dropout_mask_nib(r.states.get(), r.n_chunks, 64 * r.chunk_lo, r.elem_end, p, mask,
-                            ctx->jump_table, r.mask_base, nib_F_, nib_rows_, nib_, s);
-    nib_from_ = mask;
-    return;
-  }
-  if (nib_from_ == mask) nib_from_ = nullptr;  // that layout no longer matches the bits
   launch_dropout_mask(r.states.get(), r.n_chunks, 64 * r.chunk_lo, r.elem_end, p, mask,
                       ctx->jump_table, s, max_blocks);
-}
-
-void Dropout::set_nibbles(uint64_t *nib, int F, int rows) {
-  PGCN_CHECK(!in && (!nib || (F >= 1 && F <= 1024 && rows >= 0)), PGCN_E_INVALID,
-             "dropout: nibble layout of the input dropout only");
-  PGCN_CHECK(!nib || rng->elem_end - rng->elem_begin == (long long)F * rows, PGCN_E_INVALID,
-             "dropout: the nibble layout needs dense rows x F elements");
-  nib_ = nib;
-  nib_F_ = F;
-  nib_rows_ = rows;
-  nib_from_ = nullptr;
 }
 
 void Dropout::draw_ahead(hipStream_t s, const Event *ready) const {
@@ -92,7 +74,7 @@ void Dropout::draw_ahead(hipStream_t s, const Event *ready) const {
     rng->mask_ahead.allocate(rng->mask.size());
     rng->mask_ahead.zero();
   }
-  if (co_draw && !ready && !nib_ && !co_draw->pre_drawn && !co_draw->ahead) {
+  if (co_draw && !ready && !co_draw->pre_drawn && !co_draw->ahead) {
     // with the hidden dropout's next mask (co_draw; the eval forward uses neither)
     const DropoutRng &r = *rng, &q = co_draw->state();
     const MaskDraw a{r.states.get(), r.n_chunks, 64 * r.chunk_lo, r.elem_end, p,
@@ -139,7 +121,7 @@ void Dropout::forward(bool training, const Stream &s) const {
     ahead = false;
   } else if (pre_drawn) {  // drawn with the input dropout's mask (co_draw)
     pre_drawn = false;
-  } else if (co_draw && !nib_ && !co_draw->pre_drawn && !co_draw->ahead) {
+  } else if (co_draw && !co_draw->pre_drawn && !co_draw->ahead) {
     const DropoutRng &q = co_draw->state();
     const MaskDraw a{r.states.get(), r.n_chunks, 64 * r.chunk_lo, r.elem_end, p, r.mask.get()};
     const MaskDraw b{q.states.get(), q.n_chunks, 64 * q.chunk_lo, q.elem_end, co_draw->p,
@@ -235,8 +217,7 @@ void SparseMatmul::forward(bool training, const Stream &s) const {
     else
       drop->draw_ahead(s.get());
     const uint64_t *m = drop->mask_ahead();
-    if (!drop->nibbles_of(m, x->maskT.get()))
-      launch_mask_nibbles(m, base, x->cols, x->rows, x->cols, x->maskT.get(), s.get());
+    launch_mask_nibbles(m, base, x->cols, x->rows, x->cols, x->maskT.get(), s.get());
     launch_xstream_nn(x->rows, b->cols, x->cols, x->x.get(), x->ldx, b->dev_data.get(), b->ld, 0,
                       c->dev_data.get(), c->ld, x->maskT.get(), scale, s.get(), ahead.get());
     ahead_valid = true;
@@ -244,7 +225,7 @@ void SparseMatmul::forward(bool training, const Stream &s) const {
   }
   MmProfile prof(ctx, s.get(), x->dense ? 2.0 * x->rows * b->cols * x->cols : 0.0);
   if (x->dense && x->maskT) {  // X-stream kernels (N <= 16, K <= 640)
-    if (mask && !drop->nibbles_of(mask, x->maskT.get()))
+    if (mask)
       launch_mask_nibbles(mask, base, x->cols, x->rows, x->cols, x->maskT.get(), s.get());
     XsEpilogue e;  // the first GraphSum's prescaled input, written beside c
     if ((g_fuse_epilogue & kFuseXstream) && consumer && (training || !eval_out)) {
@@ -258,7 +239,7 @@ void SparseMatmul::forward(bool training, const Stream &s) const {
     // wide outputs: the mask in the nibble layout too (one pass over the bitmap; the wide
     // kernels then read one word per row and 4 steps, and the backward reuses it)
     const uint64_t *mw = mask && x->maskW ? x->maskW.get() : nullptr;
-    if (mw && !drop->nibbles_of(mask, mw))
+    if (mw)
       launch_mask_nibbles(mask, base, x->cols, x->rows, x->cols, x->maskW.get(), s.get());
     launch_gemm_nn(x->rows, b->cols, x->cols, x->x.get(), x->ldx, b->dev_data.get(), b->ld, 0,
                    c->dev_data.get(), c->ld, mask, base, x->cols, scale, s.get(), mw);
@@ -436,6 +417,24 @@ void GraphSum::run(const float *src, float *dst, const Stream &s, int mode,
                           s.get());
       bytes = sk->algorithmic_bytes(dim);
     }
+    if (ctx->profile) e1.record(s.get());
+  } else if (ctx->comm && mode != 1 && ctx->chunk_graphs.size() == 1 &&
+             dynamic_cast<PeerComm *>(ctx->comm) && cgs[0]->uses_lds(dim)) {
+    // Peer-mapped exchange (PeerComm, k_peer.hip): the ring sums of every padded row from this
+    // rank's columns, combined over the column blocks and pushed straight into each owner's
+    // receive slot of this rank (k_gs_lds_combine's push mode, over xGMI); then the wait for
+    // every rank's push and one kernel that sums the W slots of this rank's rows in rank order
+    // and applies the fused tail (k_gs_gather_finish).  No partial buffer, no reduce-scatter.
+    auto *pc = static_cast<PeerComm *>(ctx->comm);
+    DevGraph *gk = cgs[0];
+    const int h = out->rows;  // padded rows per rank (one chunk)
+    PeerSink k = pc->sink(h, (size_t)out->ld);
+    pc->note((size_t)h * out->ld * ctx->comm->world() * sizeof(float), 1.0);
+    gk->graphsum(src, in->ld, nullptr, out->ld, dim, s.get(), false, nullptr, prestaged, false, &k);
+    bytes = gk->algorithmic_bytes(dim);
+    pc->wait(s.get());
+    launch_gs_gather_finish(dst, out->ld, ctx->local_rows, (dim + 3) / 4 * 4,
+                            epi && epi->mode ? *epi : GsEpilogue{}, pc->recv(), s.get());
     if (ctx->profile) e1.record(s.get());
   } else if (ctx->comm) {
     // Per row chunk: partial sums of the chunk's (padded) rows from this rank's columns on

@@ -92,7 +92,6 @@ class Dropout;
 constexpr int kFuseTails = 1, kFusePrestage = 2, kFuseXstream = 4, kFuseMatmulTails = 8;
 extern int g_fuse_epilogue;
 extern int g_fuse_output;
-extern int g_mask_nib;
 extern int g_sparse_dual;
 
 // Shared per-GCN state the modules read (current split, comm, profiling, RNG table).
@@ -192,21 +191,11 @@ class Dropout : public Module {
   // (GCN::build, "co_draw"; sparse X only: the dense input has its own layouts)
   const Dropout *co_draw = nullptr;
   mutable bool pre_drawn = false;
-  // Dense X's input dropout: every draw also writes the X-stream / wide GEMM kernels' nibble
-  // layout of its bits into `nib` ([rows][16], k_dropout_mask_nib: one launch for both
-  // layouts); nibbles_of(mask, nib): `nib` holds the layout of the draw into `mask`
-  void set_nibbles(uint64_t *nib, int F, int rows);
-  bool nibbles_of(const uint64_t *mask, const uint64_t *nib) const {
-    return nib && nib == nib_ && nib_from_ == mask;
-  }
 
  private:
   void draw(hipStream_t s, uint64_t *mask, int max_blocks = 0) const;
   mutable bool ahead = false;
   mutable const Event *ahead_ready = nullptr;  // recorded after an ahead draw on a side stream
-  uint64_t *nib_ = nullptr;
-  int nib_F_ = 0, nib_rows_ = 0;
-  mutable const uint64_t *nib_from_ = nullptr;  // the mask whose nibble layout `nib_` holds
 };
 
 // include/module.cuh:47-68: c = drop(X) * W

@@ -170,98 +170,6 @@ __global__ __launch_bounds__(256) void k_dropout_mask(MaskSeg a, MaskSeg b, int 
     dropout_mask_seg(b, lut, blockIdx.x - blocks_a, gridDim.x - blocks_a);
 }
 
-// The input dropout of dense X straight into both layouts its users read (r04): the flat
-// element-order bitmap (hpdga's draw order, as k_dropout_mask) and the X-stream / wide GEMM
-// kernels' "nibble" layout (k_mask_nibbles: out[m][j] nibble c = keep bits of X[m][64c + 4j ..
-// + 3]), one launch instead of two.  A workgroup owns whole rows [r0, r1) whose bit range
-// starts and ends on chunk boundaries (mask_base + r * F = 0 mod 64 at every interior cut:
-// r0 - first_rows a multiple of rows_per_wg, chosen by the launcher), so every chunk is drawn,
-// written and advanced by exactly one workgroup; its words stay in LDS for the nibble
-// assembly.  Two chunks per thread, their xorshift chains interleaved (k_dropout_mask's
-// latency hiding).
-constexpr int DMN_MAX_CHUNKS = 2048;
-__global__ __launch_bounds__(1024) void k_dropout_mask_nib(
-    uint64_t *__restrict__ states, long long n_chunks, long long elem0, long long elem_end,
-    int threshold, uint64_t *__restrict__ mask, const uint4 *__restrict__ table,
-    long long mask_base, int F, int rows, int rows_per_wg, int first_rows,
-    uint64_t *__restrict__ nib) {
-  __shared__ uint4 lut[32 * 16];
-  extern __shared__ uint64_t words[];  // this workgroup's chunk words (+ 2), dynamic
-  for (int i = threadIdx.x; i < 32 * 16; i += blockDim.x) {
-    const int p = i >> 4, v = i & 15;
-    lut[i] = table[(p >> 1) * 256 + (v << (4 * (p & 1)))];
-  }
-  // rows of this workgroup: workgroup 0 takes [0, first_rows), then rows_per_wg each
-  const int b = blockIdx.x;
-  const int r0 = b == 0 ? 0 : min(rows, first_rows + (b - 1) * rows_per_wg);
-  const int r1 = b == 0 ? min(rows, first_rows) : min(rows, first_rows + b * rows_per_wg);
-  const long long c0 = (mask_base + (long long)r0 * F) >> 6;
-  const long long c1 = b == (int)gridDim.x - 1 ? n_chunks
-                                                : min(n_chunks, (mask_base + (long long)r1 * F + 63) >> 6);
-  const int nc = (int)(c1 - c0), half = (nc + 1) >> 1;
-  const int t = threadIdx.x;
-  if (t < 2) words[nc + t] = 0;  // a straddling last nibble peeks one word past the range
-  __syncthreads();
-  if (t < half) {
-    // chunks t and t + half (the second one absent when nc is odd and t is the last thread)
-    const bool two = t + half < nc;
-    const long long ca = c0 + t, cb = two ? ca + half : ca;
-    const uint64_t a0 = states[2 * ca], a1 = states[2 * ca + 1];
-    const uint64_t b0 = states[2 * cb], b1 = states[2 * cb + 1];
-    Xs64 x{a0, a1}, y{b0, b1};
-    x.thr2 = y.thr2 = (uint32_t)threshold << 1;
-#pragma unroll
-    for (int j = 0; j < 64; j++) {
-      x.step(j, threshold);
-      y.step(j, threshold);
-    }
-#if PGCN_DROP_SHIFTIN
-    x.lo = __builtin_bitreverse32(x.lo);
-    x.hi = __builtin_bitreverse32(x.hi);
-    y.lo = __builtin_bitreverse32(y.lo);
-    y.hi = __builtin_bitreverse32(y.hi);
-#endif
-    auto finish = [&](long long c, uint64_t word, uint64_t s0, uint64_t s1) {
-      const long long e = elem0 + 64 * c;
-      if (e + 64 > elem_end) {
-        const long long valid = elem_end - e;
-        word = valid <= 0 ? 0 : (word & ((valid >= 64) ? ~0ull : ((1ull << valid) - 1)));
-      }
-      mask[c] = word;
-      words[c - c0] = word;
-      uint64_t n1;
-      const uint64_t n0 = dmn_advance(lut, s0, s1, n1);
-      states[2 * c] = n0;
-      states[2 * c + 1] = n1;
-    };
-    finish(ca, ((uint64_t)x.hi << 32) | x.lo, a0, a1);
-    if (two) finish(cb, ((uint64_t)y.hi << 32) | y.lo, b0, b1);
-  }
-  __syncthreads();
-  // nibble words of rows r0 .. r1 - 1 (k_mask_nibbles' assembly, from LDS)
-  const int total = (r1 - r0) * 16;
-  for (int u = t; u < total; u += blockDim.x) {
-    const int r = u >> 4, j = u & 15;
-    const long long p0 = mask_base + (long long)(r0 + r) * F + 4 * j - (c0 << 6);  // local bit
-    const int w0 = (int)(p0 >> 6), sh = (int)(p0 & 63);
-    const int ncb = (F - 4 * j + 63) >> 6;  // nibbles with kb = 64 c + 4 j < F
-    uint64_t out = 0, lo = words[w0];
-#pragma unroll
-    for (int c = 0; c < 16; c++) {
-      if (c < ncb) {
-        const uint64_t hi = words[w0 + c + 1];
-        uint64_t v = (lo >> sh) & 0xfu;
-        if (sh > 60) v = (v | (hi << (64 - sh))) & 0xfu;
-        const int kb = 64 * c + 4 * j;
-        if (kb + 4 > F) v &= (1ull << (F - kb)) - 1;  // keep bits of k >= F are 0
-        out |= v << (4 * c);
-        lo = hi;
-      }
-    }
-    nib[(long long)(r0 + r) * 16 + j] = out;
-  }
-}
-
 // x[i] *= bit(base + i) ? scale : 0   (Dropout::forward on a grad-carrying variable and
 // Dropout::backward on its grad; hpdga module.cpp:215, :226).
 __device__ __forceinline__ uint32_t mask_bits4(const uint64_t *__restrict__ mask, long long idx) {
@@ -314,24 +222,6 @@ void launch_scatter_rows(const float *src, const int *rows, int n, int ld, float
   PGCN_LAUNCH(k_scatter_rows, dim3((unsigned)ceil_div(tot, 256)), dim3(256), 0, s,
                      reinterpret_cast<const float4 *>(src), rows, n, ld / 4,
                      reinterpret_cast<float4 *>(out));
-}
-
-// loopback reduce-scatter / all-reduce: one element per thread, peers summed in rank order
-// (deterministic; RCCL's own order is unspecified)
-__global__ __launch_bounds__(256) void k_loopback_sum(LoopbackSrcs srcs, float *__restrict__ dst,
-                                                      size_t count) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= count) return;
-  float acc = srcs.p[0][i];
-  for (int q = 1; q < srcs.n; q++) acc += srcs.p[q][i];
-  dst[i] = acc;
-}
-
-void launch_loopback_sum(const LoopbackSrcs &srcs, float *dst, size_t count, hipStream_t s) {
-  PGCN_CHECK(srcs.n >= 1 && srcs.n <= kLoopbackMaxRanks, PGCN_E_INVALID, "loopback_sum: ranks");
-  if (count == 0) return;
-  PGCN_LAUNCH(k_loopback_sum, dim3((unsigned)ceil_div((long long)count, 256)), dim3(256), 0,
-                     s, srcs, dst, count);
 }
 
 // out[r] = src[rows[r]] (float4s): the input of a column-subset GraphSum on the plain path
@@ -973,47 +863,6 @@ void launch_dropout_mask2(const MaskDraw &d0, const MaskDraw &d1, const void *ta
   if (g[0] + g[1] == 0) return;
   PGCN_LAUNCH(k_dropout_mask, dim3(g[0] + g[1]), dim3(256), 0, s, sg[0], sg[1], g[0],
               static_cast<const uint4 *>(table));
-}
-
-// rows_per_wg: whole multiples of 64 / gcd(F, 64) rows (their bits end on a chunk boundary)
-// with at most DMN_MAX_CHUNKS chunks; the first workgroup takes the rows up to the first
-// such boundary.  False when the shape does not fit (the caller then draws + lays out in two
-// launches).
-bool dropout_mask_nib_ok(int F, long long mask_base) {
-  if (F < 1 || F > 1024) return false;
-  const int g = std::gcd(F, 64);
-  return (mask_base % g) == 0 && F / g + 1 <= DMN_MAX_CHUNKS - 64 && mask_base >= 0 &&
-         mask_base < 64;
-}
-
-void launch_dropout_mask_nib(uint64_t *states, long long n_chunks, long long elem0,
-                             long long elem_end, float p, uint64_t *mask, const void *table,
-                             long long mask_base, int F, int rows, uint64_t *nib, hipStream_t s) {
-  PGCN_CHECK(dropout_mask_nib_ok(F, mask_base), PGCN_E_INVALID, "dropout_mask_nib: shape");
-  if (n_chunks <= 0 || rows <= 0) return;
-  PGCN_CHECK(n_chunks == ((mask_base + (long long)rows * F + 63) >> 6), PGCN_E_INVALID,
-             "dropout_mask_nib: chunks must cover rows x F bits from mask_base");
-  const int threshold = (int)(p * (float)0x7fffffff);  // hpdga module.cpp:211
-  const int g = std::gcd(F, 64), r_unit = 64 / g, c_unit = F / g;  // rows / chunks per unit
-  // about 600 chunks per workgroup (two per thread), 8 KB of LUT + the words in LDS
-  const int units = std::max(1, std::min((DMN_MAX_CHUNKS - 64) / c_unit, 640 / c_unit));
-  const int rows_per_wg = r_unit * units;
-  // first interior cut: the smallest r > 0 with (mask_base + r F) = 0 mod 64
-  int first = 0;
-  for (int r = 1; r <= r_unit; r++)
-    if ((mask_base + (long long)r * F) % 64 == 0) {
-      first = r;
-      break;
-    }
-  PGCN_CHECK(first > 0, PGCN_E_INVALID, "dropout_mask_nib: no chunk-aligned row cut");
-  const long long wgs = 1 + (rows > first ? ceil_div((long long)(rows - first), rows_per_wg) : 0);
-  // (the first workgroup can hold one chunk more than a unit's; two chunks per thread)
-  const long long max_nc = std::max<long long>((long long)c_unit * units, c_unit + 1);
-  const int threads = (int)std::min<long long>(1024, ceil_div(ceil_div(max_nc, 2), 64) * 64);
-  const size_t words_bytes = (size_t)(max_nc + 2) * sizeof(uint64_t);
-  PGCN_LAUNCH(k_dropout_mask_nib, dim3((unsigned)wgs), dim3(threads), words_bytes, s, states, n_chunks,
-              elem0, elem_end, threshold, mask, static_cast<const uint4 *>(table), mask_base, F,
-              rows, rows_per_wg, first, nib);
 }
 
 void launch_dropout_apply_based(float *x, long long n, const uint64_t *mask, long long base,

@@ -433,7 +433,6 @@ __global__ __launch_bounds__(256, 1) void k_xstream_tn(int M, int N, int K,
   }
 }
 
-int g_gemm_variant = 0;  // diagnostics ("gemm_variant"): 1 = the general kernels only
 
 // ------------------------------------------------------------------------------------------
 // TN split-M.  Block = 4 waves over a slab of rows; the K columns are cut into 64-wide chunks.
@@ -593,7 +592,7 @@ __global__ __launch_bounds__(256) void k_gemm_tn_reduce(const float *__restrict_
 // launchers
 // ------------------------------------------------------------------------------------------
 bool xstream_ok(int N, int K) {
-  return g_gemm_variant != 1 && N >= 1 && N <= 16 && K >= 1 && (K + 63) / 64 <= XS_MAX_KC;
+  return N >= 1 && N <= 16 && K >= 1 && (K + 63) / 64 <= XS_MAX_KC;
 }
 
 static int xs_stride(int K) {  // LDS row stride of B^T: >= 64*KC, = 8 mod 16 dwords
@@ -685,7 +684,7 @@ static void gemm_nn_slab(int M, int N, int K, const float *A, int lda, const flo
     launch_xstream_nn(M, N, K, A, lda, B, ldb, trans_b, C, ldc, nullptr, 1.0f, s, nullptr);
     return;
   }
-  if (g_gemm_variant != 1 && gemm_wide_ok(N)) {
+  if (gemm_wide_ok(N)) {
     launch_gemm_nn_wide(M, N, K, A, lda, B, ldb, trans_b, C, ldc, a_mask, mask_base, mask_ld,
                         a_scale, s, nst, a_mask && K <= 1024 ? maskT : nullptr);
     return;
@@ -870,7 +869,7 @@ static void gemm_tn_slab(int M, int N, int K, const float *A, int lda, const flo
     launch_xstream_tn(M, N, K, A, lda, G, ldg, C, ldc, nullptr, 1.0f, workspace, s);
     return;
   }
-  if (g_gemm_variant != 1 && gemm_wide_ok(N) && ldg % 4 == 0 &&
+  if (gemm_wide_ok(N) && ldg % 4 == 0 &&
       (reinterpret_cast<size_t>(G) & 15) == 0) {
     launch_gemm_tn_wide(M, N, K, A, lda, G, ldg, C, ldc, a_mask, mask_base, mask_ld, a_scale,
                         workspace, s, nst, a_mask && K <= 1024 ? maskT : nullptr);

@@ -22,6 +22,7 @@
 #include "gs_epilogue.hpp"
 #include "kernels.hpp"
 #include "lds_dma.hpp"
+#include "peer_sync.hpp"
 
 namespace pgcn {
 
@@ -109,13 +110,48 @@ __global__ __launch_bounds__(256) void k_ring_prescale_wide(const float *__restr
 
 // out[r] = scale[r] * sum_{b < nb} partial[b][r]   (block order => deterministic), then the
 // fused element-wise tail (gs_epilogue.hpp)
+//
+// Push mode (PUSH, the edge-cut engine's peer exchange, k_peer.hip): row r belongs to rank
+// q = r / rows_per_rank, and its sum goes straight into q's receive slot of this rank (over
+// xGMI when q is a peer) instead of `out`; the launch's last workgroup then signals the
+// receivers (peer_arrive).  No epilogue: the receiver applies it after summing the ranks.
+template <bool PUSH>
 __global__ __launch_bounds__(256) void k_gs_lds_combine(const float4 *__restrict__ partial,
                                                         long long part_stride, int nb,
                                                         const float *__restrict__ scale, int n,
                                                         float4 *__restrict__ out, int ld4_out,
-                                                        GsEpilogue epi) {
+                                                        GsEpilogue epi, PeerSink push) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long r = t >> 2;
+  if (PUSH) {
+    if (r < n) {
+      const int v = (int)(t & 3);
+      const float s = scale[r];
+      float4 a;
+      if (nb <= 8) {
+        float4 p[8];
+#pragma unroll
+        for (int b = 0; b < 8; b++)
+          if (b < nb) p[b] = partial[((long long)b * part_stride + r) * 4 + v];
+        a = p[0];
+#pragma unroll
+        for (int b = 1; b < 8; b++)
+          if (b < nb) f4_acc(a, p[b]);
+      } else {
+        a = partial[r * 4 + v];
+        for (int b = 1; b < nb; b++) f4_acc(a, partial[((long long)b * part_stride + r) * 4 + v]);
+      }
+      a.x *= s;
+      a.y *= s;
+      a.z *= s;
+      a.w *= s;
+      const int q = (int)(r / push.rows_per_rank);
+      const long long j = r - (long long)q * push.rows_per_rank;
+      reinterpret_cast<float4 *>(push.dst[q])[j * ld4_out + v] = a;
+    }
+    peer_arrive(push);
+    return;
+  }
   if (r >= n) return;
   const int v = (int)(t & 3);
   // the row scale and the epilogue's inputs with the partials: one round trip, not one each
@@ -160,14 +196,37 @@ __global__ __launch_bounds__(256) void k_gs_finish(float4 *__restrict__ y, int l
   y[r * ld4 + v] = a;
 }
 
-// NS: rowsets per summing wave (16, or 8: half the rows per workgroup, twice the batches)
+// The receiving end of a pushed GraphSum (k_peer.hip): y[r] = the sum over ranks q (rank
+// order) of slot q's row r, then the fused tail as k_gs_finish (the same operations on the
+// same sums as the reduce-scattered form with a rank-order sum)
+__global__ __launch_bounds__(256) void k_gs_gather_finish(float4 *__restrict__ y, int ld4, int n,
+                                                          int vec, GsEpilogue epi, PeerRecv rv) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long r = t / vec;
+  if (r >= n) return;
+  const int v = (int)(t - r * vec);
+  GsEpiIn ein;
+  gs_epi_load(ein, r, 4 * v, epi);
+  float4 p[kPeerMaxRanks];
+#pragma unroll
+  for (int q = 0; q < kPeerMaxRanks; q++)
+    if (q < rv.world) p[q] = reinterpret_cast<const float4 *>(rv.slot[q])[r * ld4 + v];
+  float4 a = p[0];
+#pragma unroll
+  for (int q = 1; q < kPeerMaxRanks; q++)
+    if (q < rv.world) f4_acc(a, p[q]);
+  gs_epilogue(a, r, 4 * v, epi, ein);
+  y[r * ld4 + v] = a;
+}
+
+// NS: rowsets per summing wave (LDS_SLOTS)
 template <int NS>
 __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
     const uint2 *__restrict__ entries, const long long *__restrict__ wave_off,
     const unsigned short *__restrict__ counts, int t_max, const int2 *__restrict__ slices,
     const int *__restrict__ n_slices, const int *__restrict__ rows, const char *__restrict__ table,
     float4 *__restrict__ partial, long long part_stride, int n_blocks) {
-  static_assert(NS == 8 || NS == 16, "rowsets per wave");
+  static_assert(NS == 16, "rowsets per wave");
   constexpr int CNT_USED = LDS_CW * NS * 2;  // counts of one visit (bytes)
   __shared__ float4 lds[RING_TOTAL_B / 16];
   const int nb = n_blocks;
@@ -372,6 +431,20 @@ void launch_gs_finish(float *y, int ld, int n, int dim, const GsEpilogue &epi, h
   PGCN_HIP(hipGetLastError());
 }
 
+void launch_gs_gather_finish(float *y, int ld, int n, int dim, const GsEpilogue &epi,
+                             const PeerRecv &r, hipStream_t st) {
+  PGCN_CHECK(ld % 4 == 0 && dim % 4 == 0 && dim <= ld && n >= 0 && r.world >= 1 &&
+                 r.world <= kPeerMaxRanks,
+             PGCN_E_INVALID, "gs_gather_finish: shape");
+  PGCN_CHECK(!epi.next_table || dim == 16, PGCN_E_INVALID,
+             "gs_gather_finish: next table of a wide row");
+  if (n == 0) return;
+  const long long t = (long long)n * (dim / 4);
+  PGCN_LAUNCH(k_gs_gather_finish, dim3((unsigned)ceil_div(t, 256)), dim3(256), 0, st,
+              reinterpret_cast<float4 *>(y), ld / 4, n, dim / 4, epi, r);
+  PGCN_HIP(hipGetLastError());
+}
+
 void launch_ring_prescale_wide(const LdsSchedule &s, const float *in, int ld_in, int width,
                                const RingPasses &passes, float *tables, long long table_floats,
                                hipStream_t st) {
@@ -388,7 +461,8 @@ void launch_ring_prescale_wide(const LdsSchedule &s, const float *in, int ld_in,
 
 void launch_graphsum_ring(const LdsSchedule &s, const float *in, int ld_in, float *out,
                           int ld_out, float *scratch_in, float *partial, hipStream_t st,
-                          const int *col_map, const GsEpilogue *epi, bool prestaged) {
+                          const int *col_map, const GsEpilogue *epi, bool prestaged,
+                          const PeerSink *push) {
   note_path(KP_GS_RING);
   PGCN_CHECK(ld_in % 4 == 0 && ld_out % 4 == 0, PGCN_E_INVALID, "graphsum_ring: ld % 4");
   const long long pre = (long long)s.n_cols * 4;
@@ -403,17 +477,23 @@ void launch_graphsum_ring(const LdsSchedule &s, const float *in, int ld_in, floa
               reinterpret_cast<const char *>(scratch_in), reinterpret_cast<float4 *>(partial), \
               (long long)s.n_rows, s.n_blocks)
   PGCN_CHECK(ring_slots_ok(s.ns), PGCN_E_INVALID, "graphsum_ring: rowsets per wave");
-  if (s.ns == 8)
-    RING_LAUNCH(8);
-  else
-    RING_LAUNCH(16);
+  RING_LAUNCH(16);
 #undef RING_LAUNCH
   const GsEpilogue none{};
   const long long post = (long long)s.n_rows * 4;
-  PGCN_LAUNCH(k_gs_lds_combine, dim3((unsigned)ceil_div(post, 256)), dim3(256), 0, st,
-                     reinterpret_cast<const float4 *>(partial), (long long)s.n_rows, s.n_blocks,
-                     s.row_scale, s.n_rows, reinterpret_cast<float4 *>(out), ld_out / 4,
-                     epi ? *epi : none);
+  if (push) {
+    PGCN_CHECK((!epi || epi->mode == 0) && push->world >= 1 && push->world <= kPeerMaxRanks &&
+                   push->rows_per_rank > 0 && (long long)push->rows_per_rank * push->world >= s.n_rows,
+               PGCN_E_INVALID, "graphsum_ring: push shape");
+    PGCN_LAUNCH(k_gs_lds_combine<true>, dim3((unsigned)ceil_div(post, 256)), dim3(256), 0, st,
+                reinterpret_cast<const float4 *>(partial), (long long)s.n_rows, s.n_blocks,
+                s.row_scale, s.n_rows, nullptr, ld_out / 4, none, *push);
+  } else {
+    PGCN_LAUNCH(k_gs_lds_combine<false>, dim3((unsigned)ceil_div(post, 256)), dim3(256), 0, st,
+                reinterpret_cast<const float4 *>(partial), (long long)s.n_rows, s.n_blocks,
+                s.row_scale, s.n_rows, reinterpret_cast<float4 *>(out), ld_out / 4,
+                epi ? *epi : none, PeerSink{});
+  }
   PGCN_HIP(hipGetLastError());
 }
 

@@ -1,0 +1,117 @@
+// parallel-gcn_amd/csrc/k_peer.hip -- the edge-cut engine's peer-mapped exchange (PeerComm,
+// host/comm.cpp): every rank's receive region is mapped into every other rank's address space
+// (hipIpcOpenMemHandle across processes; plain pointers between the in-process loopback
+// ranks), so a collective is one-sided stores over xGMI plus a flag per (receiver, sender).
+//
+// Replaces, for the reference's GraphSum at partition boundaries (src/module.cu:188-210) and
+// the weight-gradient all-reduce, RCCL's reduce-scatter / all-reduce: rank r's partial sums of
+// the rows owned by rank q are written straight into q's slot r (in the kernel that forms
+// them: k_gs_lds_combine's push mode), and q sums its W slots in rank order (deterministic,
+// the same order on every rank).
+//
+// Ordering, with receive regions, flags and arrival counters in uncached device memory
+// (MTYPE UC: no cache holds a line of them, on this GPU or a peer):
+//   producer  -- every store of a workgroup acknowledged (s_waitcnt vmcnt(0)), the workgroup's
+//                barrier, one arrival on the launch's counter; the last workgroup to arrive
+//                stores gen into flag[rank] of every peer, and resets the counter;
+//   consumer  -- one wave polls its own flags until every peer's reads gen (bounded: an error
+//                word and an early exit after kPeerTimeoutTicks), then the sum kernel reads
+//                the slots (stream order after the wait).
+// Slots are double-buffered by generation parity: a rank's push of generation g + 2 into
+// peer q's slot follows (in its stream) its wait for g + 1, which needs q's push of g + 1,
+// which follows (in q's stream) q's reads of generation g.
+#include "common.hpp"
+#include "kernels.hpp"
+#include "lds_dma.hpp"
+#include "peer_sync.hpp"
+
+namespace pgcn {
+
+// send [world][count] (stride 0: the same count floats for every receiver) -> receiver q's
+// slot (sink.dst[q]); blockIdx.y = q
+// (T = float4 when count % 4 == 0, else float)
+template <typename T>
+__global__ __launch_bounds__(256) void k_peer_push(const T *__restrict__ send, long long n,
+                                                   long long stride, PeerSink k) {
+  const int q = blockIdx.y;
+  T *dst = reinterpret_cast<T *>(k.dst[q]);
+  const T *src = send + (long long)q * stride;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+  peer_arrive(k);
+}
+
+// one wave: lane q < world polls flags[q] (this rank's own flag words) until it reads gen;
+// after kPeerTimeoutTicks of the 100 MHz clock an error word names the peer and every later
+// wait returns at once (the host turns it into PGCN_E_COMM)
+__global__ __launch_bounds__(64) void k_peer_wait(const unsigned *flags, int world, unsigned gen,
+                                                  unsigned *err) {
+  const int q = threadIdx.x;
+  if (flag_load(err)) return;
+  if (q >= world) return;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while ((int)(flag_load(flags + q) - gen) < 0) {
+    __builtin_amdgcn_s_sleep(2);
+    if (__builtin_amdgcn_s_memrealtime() - t0 > kPeerTimeoutTicks) {
+      __hip_atomic_store(err, 0x10000u | (unsigned)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+  }
+}
+
+__device__ __forceinline__ void peer_acc(float &a, float b) { a += b; }
+__device__ __forceinline__ void peer_acc(float4 &a, const float4 &b) { f4_acc(a, b); }
+
+// dst[i] = sum over q (rank order) of slot[q][i]
+template <typename T>
+__global__ __launch_bounds__(256) void k_peer_sum(PeerRecv r, T *__restrict__ dst, long long n) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  T p[kPeerMaxRanks];
+#pragma unroll
+  for (int q = 0; q < kPeerMaxRanks; q++)
+    if (q < r.world) p[q] = reinterpret_cast<const T *>(r.slot[q])[i];
+  T a = p[0];
+#pragma unroll
+  for (int q = 1; q < kPeerMaxRanks; q++)
+    if (q < r.world) peer_acc(a, p[q]);
+  dst[i] = a;
+}
+
+void launch_peer_push(const float *send, size_t count, const PeerSink &k, hipStream_t s,
+                      bool same_for_all) {
+  PGCN_CHECK(k.world >= 1 && k.world <= kPeerMaxRanks, PGCN_E_INVALID, "peer_push: world");
+  const bool v4 = count % 4 == 0;
+  const long long n = (long long)(v4 ? count / 4 : count);
+  const dim3 grid((unsigned)std::max<long long>(1, std::min<long long>(ceil_div(n, 256), 64)),
+                  (unsigned)k.world);
+  const long long stride = same_for_all ? 0 : n;
+  if (v4)
+    PGCN_LAUNCH(k_peer_push<float4>, grid, dim3(256), 0, s, reinterpret_cast<const float4 *>(send),
+                n, stride, k);
+  else
+    PGCN_LAUNCH(k_peer_push<float>, grid, dim3(256), 0, s, send, n, stride, k);
+  PGCN_HIP(hipGetLastError());
+}
+
+void launch_peer_wait(const unsigned *flags, int world, unsigned gen, unsigned *err,
+                      hipStream_t s) {
+  PGCN_LAUNCH(k_peer_wait, dim3(1), dim3(64), 0, s, flags, world, gen, err);
+  PGCN_HIP(hipGetLastError());
+}
+
+void launch_peer_sum(const PeerRecv &r, float *dst, size_t count, hipStream_t s) {
+  PGCN_CHECK(r.world >= 1 && r.world <= kPeerMaxRanks, PGCN_E_INVALID, "peer_sum: world");
+  const bool v4 = count % 4 == 0;
+  const long long n = (long long)(v4 ? count / 4 : count);
+  if (n == 0) return;
+  if (v4)
+    PGCN_LAUNCH(k_peer_sum<float4>, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, r,
+                reinterpret_cast<float4 *>(dst), n);
+  else
+    PGCN_LAUNCH(k_peer_sum<float>, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, r, dst, n);
+  PGCN_HIP(hipGetLastError());
+}
+
+}  // namespace pgcn

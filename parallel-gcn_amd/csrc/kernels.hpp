@@ -61,9 +61,9 @@ bool graphsum_vec_supported(int vec);
 constexpr int kGraphBlocks = 8;                      // plain kernel: column blocks (one per XCD)
 constexpr int LDS_CW = 15;                           // summing waves per workgroup
 constexpr int LDS_SLOTS = 16;                        // rowsets (16 rows) per summing wave (max)
-// the ring schedule's rowsets per summing wave: 16, or 8 for half the rows per workgroup (twice
-// the rowset batches: row chunks of the edge-cut engine fill the chip; knob "lds_slots")
-constexpr bool ring_slots_ok(int ns) { return ns == 8 || ns == 16; }
+// the ring schedule's rowsets per summing wave (r04: 8, half the rows per workgroup and twice
+// the batches, measured slower and removed)
+constexpr bool ring_slots_ok(int ns) { return ns == LDS_SLOTS; }
 constexpr int LDS_THREADS = 64 * (LDS_CW + 1);       // + one slice loader wave
 // Sliding-window ring schedule (k_graphsum_ring.hip, host/ring.cpp): slices of RING_SR rows,
 // a ring of RING_K slices in LDS as 4 quarter planes of RING_P rows, visits read RING_W slices
@@ -118,7 +118,7 @@ void launch_ring_prescale_wide(const LdsSchedule &s, const float *in, int ld_in,
 void launch_graphsum_ring(const LdsSchedule &s, const float *in, int ld_in, float *out,
                           int ld_out, float *scratch_in, float *partial, hipStream_t st,
                           const int *col_map = nullptr, const GsEpilogue *epi = nullptr,
-                          bool prestaged = false);
+                          bool prestaged = false, const struct PeerSink *push = nullptr);
 // The edge-cut engine's GraphSum tail: after the reduce-scatter has summed every rank's
 // partials into this rank's rows y [n][ld] (ld % 4 == 0, dim % 4 == 0), the fused
 // element-wise epilogue (gs_epilogue.hpp: ReLU / Dropout, the next GraphSum's table) in place
@@ -184,13 +184,41 @@ void launch_xstream_tn_ring(int M, int N, int K, const float *A, int lda, const 
 // out[r][0:ld] = src[rows[r]][0:ld]  (ld % 4 == 0)
 void launch_gather_rows(const float *src, const int *rows, int n, int ld, float *out,
                         hipStream_t s);
-// loopback collectives (host/comm.cpp): dst[i] = sum over q < n (in order) of p[q][i]
-constexpr int kLoopbackMaxRanks = 16;
-struct LoopbackSrcs {
-  const float *p[kLoopbackMaxRanks];
-  int n;
+// ---- peer-mapped exchange (k_peer.hip, host/comm.cpp PeerComm) -----------------------------
+constexpr int kPeerMaxRanks = 16;
+// a wait gives up after this many ticks of the 100 MHz s_memrealtime clock (20 s)
+constexpr unsigned long long kPeerTimeoutTicks = 2000000000ull;
+// where one collective's pushes of this rank go: receiver q's slot of this rank (dst[q], in q's
+// memory or, q == rank, this rank's own) and q's flag word of this rank
+struct PeerSink {
+  float *dst[kPeerMaxRanks];
+  unsigned *flag[kPeerMaxRanks];
+  unsigned *arrive = nullptr;  // this rank's arrival counter (zero between launches)
+  unsigned gen = 0;            // the collective's generation, stored into the flags
+  int world = 0;               // 0: not pushing
+  int rows_per_rank = 0;       // GraphSum push: padded rows per owner (row r -> owner r / this)
+  int signal = 1;              // 0: an earlier pass of a multi-pass push (no flags yet)
 };
-void launch_loopback_sum(const LoopbackSrcs &srcs, float *dst, size_t count, hipStream_t s);
+// this rank's received slots of one collective: slot[q] = what rank q pushed
+struct PeerRecv {
+  const float *slot[kPeerMaxRanks];
+  int world = 0;
+};
+// send [world][count] -> sink.dst[q] (same_for_all: send [count] to every q); then the flags
+// (the launch's last workgroup)
+void launch_peer_push(const float *send, size_t count, const PeerSink &k, hipStream_t s,
+                      bool same_for_all);
+// one wave until flags[q] == gen for every q < world (err: set on a timeout, then no waiting)
+void launch_peer_wait(const unsigned *flags, int world, unsigned gen, unsigned *err,
+                      hipStream_t s);
+// dst[i] = sum over q (rank order) of r.slot[q][i]
+void launch_peer_sum(const PeerRecv &r, float *dst, size_t count, hipStream_t s);
+// the GraphSum exchange's receiving end: y[j] (j < n local rows, [ld] floats, dim columns) =
+// sum over q (rank order) of r.slot[q] row j, then the fused element-wise epilogue (as
+// launch_gs_finish)
+void launch_gs_gather_finish(float *y, int ld, int n, int dim, const GsEpilogue &epi,
+                             const PeerRecv &r, hipStream_t st);
+
 // out[rows[r]][0:ld] = src[r][0:ld]  (ld % 4 == 0)
 void launch_scatter_rows(const float *src, const int *rows, int n, int ld, float *out,
                          hipStream_t s);
@@ -227,13 +255,6 @@ struct MaskDraw {
 };
 void launch_dropout_mask2(const MaskDraw &d0, const MaskDraw &d1, const void *table,
                           hipStream_t s);
-// the input dropout of dense X [rows][F] (element i = m F + k at local bit mask_base + i) into
-// the flat bitmap AND the nibble layout nib [rows][16] in one launch (k_dropout_mask_nib);
-// dropout_mask_nib_ok: the shape the kernel takes (F <= 1024, chunk-aligned row cuts)
-bool dropout_mask_nib_ok(int F, long long mask_base);
-void launch_dropout_mask_nib(uint64_t *states, long long n_chunks, long long elem0,
-                             long long elem_end, float p, uint64_t *mask, const void *table,
-                             long long mask_base, int F, int rows, uint64_t *nib, hipStream_t s);
 void launch_dropout_apply_based(float *x, long long n, const uint64_t *mask, long long base,
                                 float scale, hipStream_t s);
 void launch_relu_fwd(float *x, long long n, uint8_t *mask, int training, hipStream_t s);

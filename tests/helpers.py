@@ -230,10 +230,8 @@ def parse_line(line):
 # pgcn_debug_set defaults of the engine (include/pgcn.h; parallel-gcn_amd/csrc/host/gcn.cpp)
 ENGINE_DEFAULTS = {"train_ahead": 1, "split_rows": 0, "split_cols": 1, "eval_ax": 1,
                    "epoch_graph": 0, "fuse_epilogue": 15, "fuse_output": 2, "mm_side": 0,
-                   "xstream_ring": 1, "gemm_variant": 0, "lds_min_kb": -1, "lds_blocks": 0,
-                   "parse_threads": 0, "wide_prescale": 1, "rs_chunks": 1, "lds_slots": 0,
-                   "mask_nib": 0, "plain_blocks": 0, "gs_split": 3,
-                   "gs_item_iters": 0, "co_draw": 1,
+                   "xstream_ring": 1, "lds_min_kb": -1, "lds_blocks": 0,
+                   "parse_threads": 0, "gs_split": 3, "gs_item_iters": 0, "co_draw": 1,
                    "gs_orig_cols": 1, "sparse_dual": 1}
 
 

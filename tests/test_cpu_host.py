@@ -339,23 +339,6 @@ def test_lds_schedule_walk_sums_every_edge(pgcn):
                                          ctypes.byref(n)) == pgcn.PGCN_E_INVALID
 
 
-@pytest.mark.parametrize("slots", [8, 16])
-def test_lds_schedule_rowsets_per_wave(pgcn, slots):
-    """The ring schedule with 8 or 16 rowsets per summing wave (knob lds_slots: 8 halves a
-    workgroup's rows) walks to every row's exact CSR sum; 8 slots build twice the batches."""
-    ds = pgcn.Dataset.synthetic(70000, 8, 4, 2000000, 1)
-    ip = np.ascontiguousarray(ds.graph_indptr)
-    ix = np.ascontiguousarray(ds.graph_indices)
-    with helpers.knobs(pgcn, lds_slots=slots):
-        err, nb = _lds_check(pgcn, ip, ix, ds.num_nodes, RING)
-        shape = (ctypes.c_int * 5)()
-        n = pgcn.lib.pgcn_debug_lds_counts(ds.num_nodes, ds.num_nodes, helpers.ptr(ip),
-                                           helpers.ptr(ix), RING, None, 0, shape)
-    assert n > 0 and err < 1e-12
-    assert shape[3] == slots
-    assert nb * 64 < 4 * len(ix), nb * 64 / len(ix)
-
-
 def test_lds_schedule_ragged_graph(pgcn):
     """Isolated rows, a hub adjacent to everything, duplicate edges: the ring schedule stays
     exact."""
@@ -511,7 +494,7 @@ def test_ring_kernel_lds_reads_wait_before_use(tmp_path):
     asm = subprocess.run([f"{LLVM_BIN}/llvm-objdump", "-d", "--no-show-raw-insn", dev],
                          check=True, capture_output=True, text=True).stdout.splitlines()
     starts = [i for i, l in enumerate(asm) if re.match(r"^[0-9a-f]+ <_ZN4pgcn15k_graphsum_ring", l)]
-    assert len(starts) >= 2, "k_graphsum_ring<8> / <16> not in the code object"
+    assert len(starts) >= 1, "k_graphsum_ring<16> not in the code object"
 
     def regs(ops):
         out = set()
@@ -563,10 +546,14 @@ def test_debug_set_refuses_out_of_range_values(pgcn):
     lib = pgcn.lib
     for key, bad in (("train_ahead", 2), ("split_rows", -1), ("split_cols", 5), ("eval_ax", 2),
                      ("epoch_graph", 3), ("fuse_epilogue", 16), ("fuse_output", 4),
-                     ("mm_side", 3), ("xstream_ring", 2), ("gemm_variant", 7),
-                     ("lds_blocks", 3), ("parse_threads", -2), ("wide_prescale", 2),
-                     ("plain_blocks", 2), ("gs_split", 4), ("gs_item_iters", 5), ("co_draw", 2), ("gs_orig_cols", 2), ("sparse_dual", 2)):
+                     ("mm_side", 3), ("xstream_ring", 2),
+                     ("lds_blocks", 3), ("parse_threads", -2),
+                     ("gs_split", 4), ("gs_item_iters", 5), ("co_draw", 2), ("gs_orig_cols", 2), ("sparse_dual", 2)):
         assert lib.pgcn_debug_set(key.encode(), bad) < 0, key
     assert lib.pgcn_debug_set(b"no_such_knob", 0) < 0
+    # diagnostic arms removed in r05: refused like any unknown key
+    for key in ("gemm_variant", "plain_blocks", "lds_slots", "mask_nib", "rs_chunks",
+                "wide_prescale"):
+        assert lib.pgcn_debug_set(key.encode(), 0) < 0, key
     for key, val in helpers.ENGINE_DEFAULTS.items():
         assert lib.pgcn_debug_set(key.encode(), val) == 0, key

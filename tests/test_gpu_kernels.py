@@ -270,15 +270,21 @@ def test_graphsum_lds_wide_rows(pgcn, dim, ld):
                                           ctypes.byref(g)), "graph_create")
     xin = torch.from_numpy(x).to(DEV)
     outs = []
-    # runs 0, 1: every pass's table prescaled by one launch (default); run 2: one prescale
-    # launch per pass -- the same products, so the same bits
-    for wide in (1, 1, 0):
-        with helpers.knobs(pgcn, wide_prescale=wide):
-            out = torch.full((n, ld), float("nan"), device=DEV)
-            pgcn.check(pgcn.lib.pgcn_graphsum(g, vp(xin), ld, vp(out), ld, dim, stream()), "gs")
-            torch.cuda.synchronize()
+    # runs 0, 1: every pass's table prescaled by one launch (the batched prescale); then each
+    # 16-column pass as a d = 16 call of its own (its own prescale launch): the same products,
+    # so the same bits
+    for _ in range(2):
+        out = torch.full((n, ld), float("nan"), device=DEV)
+        pgcn.check(pgcn.lib.pgcn_graphsum(g, vp(xin), ld, vp(out), ld, dim, stream()), "gs")
+        torch.cuda.synchronize()
         outs.append(out)
-    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    assert torch.equal(outs[0], outs[1])
+    for c0 in range(0, dim, 16):
+        c = min(c0, ld - 16)
+        one = torch.full((n, 16), float("nan"), device=DEV)
+        pgcn.check(pgcn.lib.pgcn_graphsum(g, vp(xin[:, c:]), ld, vp(one), 16, 16, stream()), "gs16")
+        torch.cuda.synchronize()
+        assert torch.equal(one, outs[0][:, c:c + 16]), c
     ours = outs[0].cpu().numpy()
     ref = oracle_graphsum(indptr, indices, x, dim)
     bound = abs_bound(indptr, indices, x, dim)
@@ -351,43 +357,6 @@ def test_dropout_masks_bit_exact(pgcn):
         np.testing.assert_array_equal(ours, ref)
 
 
-@pytest.mark.parametrize("F,rows,mask_base", [(602, 1000, 0), (602, 777, 22), (64, 3000, 0),
-                                               (100, 513, 36), (1023, 97, 5), (600, 40, 8)])
-def test_dropout_mask_nib_matches_two_launches(pgcn, F, rows, mask_base):
-    """k_dropout_mask_nib (the input dropout of dense X drawn into the flat bitmap and the
-    GEMMs' nibble layout by one launch) against k_dropout_mask followed by k_mask_nibbles from
-    the same chunk states, over two epochs (state advance by the period): the same words in
-    both layouts, the same advanced states, bit for bit.  mask_base != 0 is an edge-cut rank's
-    first element inside its first chunk."""
-    period = 1_000_003
-    n_elems = mask_base + rows * F
-    nch = (n_elems + 63) // 64
-    st = pgcn.rng_jump(pgcn.rng_seed(), 777)
-    states = np.zeros((nch, 2), np.uint64)
-    for c in range(nch):
-        states[c] = st
-        st = pgcn.rng_jump(st, 64)
-    table = torch.from_numpy(pgcn.rng_jump_table(period).view(np.int64)).to(DEV)
-    sa = torch.from_numpy(states.view(np.int64).copy()).to(DEV)
-    sb = sa.clone()
-    ma = torch.zeros(nch + 1, dtype=torch.int64, device=DEV)
-    mb = torch.zeros(nch + 1, dtype=torch.int64, device=DEV)
-    na = torch.full((rows, 16), -1, dtype=torch.int64, device=DEV)
-    nb = torch.full((rows, 16), -1, dtype=torch.int64, device=DEV)
-    for _ in range(2):
-        pgcn.check(pgcn.lib.pgcn_dropout_mask(vp(sa), nch, n_elems, 0, 0.5, vp(ma), vp(table),
-                                              stream()), "dropout_mask")
-        pgcn.check(pgcn.lib.pgcn_mask_nibbles(vp(ma), mask_base, F, rows, F, vp(na), stream()),
-                   "nib")
-        pgcn.check(pgcn.lib.pgcn_dropout_mask_nib(vp(sb), nch, n_elems, 0, 0.5, vp(mb),
-                                                  vp(table), mask_base, F, rows, vp(nb),
-                                                  stream()), "dropout_mask_nib")
-        torch.cuda.synchronize()
-        np.testing.assert_array_equal(mb.cpu().numpy()[:nch], ma.cpu().numpy()[:nch])
-        np.testing.assert_array_equal(nb.cpu().numpy(), na.cpu().numpy())
-        np.testing.assert_array_equal(sb.cpu().numpy(), sa.cpu().numpy())
-
-
 def test_dropout_apply(pgcn):
     n = 10_007
     x = torch.randn(n, device=DEV)
@@ -405,17 +374,16 @@ def mask_window(mask, base, M, K):
     return mask_bits(mask, base + M * K)[base:].reshape(M, K)
 
 
-GEMM_VARIANTS = [0, 1]  # 0: N <= 16 streaming kernels where they apply; 1: general kernels
-
-
-@pytest.mark.parametrize("variant", GEMM_VARIANTS)
+# every shape on the kernel the product dispatches it to: N <= 16 streaming (X-stream) kernels,
+# 33..128 the wide MFMA kernels, the general MFMA kernels elsewhere (17..32, > 128)
 @pytest.mark.parametrize("M,N,K,drop,base", [(1000, 16, 602, True, 0), (777, 41, 16, False, 0),
+                                             (400, 24, 100, True, 3), (999, 32, 602, True, 0),
                                              (513, 16, 41, False, 0), (300, 128, 128, False, 0),
                                              (64, 16, 1433, True, 0), (2011, 16, 602, True, 37),
                                              (99, 13, 70, True, 63), (5, 16, 602, True, 1),
                                              (500, 200, 72, True, 5), (300, 300, 41, False, 0),
                                              (257, 136, 16, False, 0)])
-def test_gemm_nn(pgcn, M, N, K, drop, base, variant):
+def test_gemm_nn(pgcn, M, N, K, drop, base):
     rng = np.random.default_rng(M + N + K)
     lda = (K + 3) // 4 * 4
     A = np.zeros((M, lda), np.float32)
@@ -427,7 +395,6 @@ def test_gemm_nn(pgcn, M, N, K, drop, base, variant):
     Ae = A[:, :K].astype(np.float64)
     if drop:
         Ae = Ae * np.where(mask_window(mask, base, M, K), 2.0, 0.0)
-    pgcn.lib.pgcn_debug_set(b"gemm_variant", variant)
     ref = Ae @ B.astype(np.float64)
     dA, dB = torch.from_numpy(A).to(DEV), torch.from_numpy(B).to(DEV)
     dm = torch.from_numpy(mask.view(np.int64)).to(DEV)
@@ -441,7 +408,6 @@ def test_gemm_nn(pgcn, M, N, K, drop, base, variant):
     pgcn.check(pgcn.lib.pgcn_gemm(M, N, K, vp(dA), lda, vp(dBt), K, 1, vp(C2), ldc,
                                   vp(dm) if drop else None, base, K, 2.0, stream()), "gemm_t")
     torch.cuda.synchronize()
-    pgcn.lib.pgcn_debug_set(b"gemm_variant", 0)
     bound = np.abs(Ae) @ np.abs(B.astype(np.float64))
     for out in (C, C2):
         o = out.cpu().numpy()
@@ -449,14 +415,14 @@ def test_gemm_nn(pgcn, M, N, K, drop, base, variant):
         np.testing.assert_array_equal(o[:, N:], 0.0)
 
 
-@pytest.mark.parametrize("variant", GEMM_VARIANTS)
 @pytest.mark.parametrize("M,N,K,drop,base", [(5000, 16, 602, True, 0), (3000, 41, 16, False, 0),
+                                             (2000, 24, 100, True, 3), (3001, 32, 602, True, 0),
                                              (2000, 128, 128, False, 0), (100, 16, 1433, True, 0),
                                              (70000, 16, 602, False, 0), (4099, 16, 602, True, 29),
                                              (333, 16, 200, True, 63), (7, 11, 602, True, 5),
                                              (3000, 128, 602, True, 0), (2000, 80, 300, True, 3),
                                              (1000, 200, 72, True, 3), (600, 136, 16, False, 0)])
-def test_gemm_tn(pgcn, M, N, K, drop, base, variant):
+def test_gemm_tn(pgcn, M, N, K, drop, base):
     rng = np.random.default_rng(M + 3 * N + K)
     lda = (K + 3) // 4 * 4
     A = np.zeros((M, lda), np.float32)
@@ -468,7 +434,6 @@ def test_gemm_tn(pgcn, M, N, K, drop, base, variant):
     if drop:
         Ae = Ae * np.where(mask_window(mask, base, M, K), 2.0, 0.0)
     ref = Ae.T @ Gm.astype(np.float64)
-    pgcn.lib.pgcn_debug_set(b"gemm_variant", variant)
     ws = torch.empty(pgcn.lib.pgcn_gemm_tn_workspace(M, N, K) // 4 + 16, device=DEV)
     dA, dG = torch.from_numpy(A).to(DEV), torch.from_numpy(Gm).to(DEV)
     dm = torch.from_numpy(mask.view(np.int64)).to(DEV)
@@ -477,7 +442,6 @@ def test_gemm_tn(pgcn, M, N, K, drop, base, variant):
                                      vp(dm) if drop else None, base, K, 2.0, vp(ws), stream()),
                "tn")
     torch.cuda.synchronize()
-    pgcn.lib.pgcn_debug_set(b"gemm_variant", 0)
     bound = np.abs(Ae).T @ np.abs(Gm.astype(np.float64))
     assert (np.abs(C.cpu().numpy() - ref) <= 1e-5 * bound + 1e-30).all()
 

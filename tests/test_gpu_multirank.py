@@ -1,12 +1,13 @@
-"""The edge-cut engine at world 2 and 4 on ONE GPU through the in-process loopback
-communicator (SURVEY.md §4 "fake RCCL"; RCCL itself refuses two ranks on one device).
+"""The edge-cut engine at worlds 2, 4 and 8 on ONE GPU through the in-process loopback
+ranks (SURVEY.md §4 "fake RCCL"; RCCL itself refuses two ranks on one device).
 
 Each rank is an engine created and driven by its own host thread; its collectives are the
-loopback group's stream-ordered device sums.  Everything else is the multi-GPU path the
-8-GPU bench runs: nnz-balanced contiguous node ranges, chunked partial GraphSums reduce-
-scattered on the comm stream, dropout masks drawn at the global stream offsets of each rank's
-elements, per-rank Â X for eval, the training split's column-subset backward, the weight-
-gradient all-reduce.  Compared with the oracle (single process, the reference's algorithm)
+peer-mapped exchange's kernels (PeerComm, k_peer.hip) over raw device pointers -- the same
+pushes, flags and rank-order sums as one process per GPU.  Everything else is the multi-GPU
+path the 8-GPU bench runs: nnz-balanced contiguous node ranges, GraphSum partials pushed into
+their owners' slots by the combine, dropout masks drawn at the global stream offsets of each
+rank's elements, per-rank Â X for eval, the training split's column-subset backward, the
+weight-gradient all-reduce.  Compared with the oracle (single process, the reference's algorithm)
 with dropout 0.5 at the north star's 1e-4 on the losses.
 """
 import numpy as np
@@ -79,15 +80,14 @@ def big_oracle(big_ds):
     return [r[0] for r in runs], [r[1] for r in runs], test, {1: tt, 2: tt}
 
 
-@pytest.mark.parametrize("world,split_rows,lds,chunks", [(2, 0, 1, 1), (2, 1, 1, 1), (4, 0, 1, 1),
-                                                          (8, 0, 1, 1), (4, 0, 0, 1), (2, 0, 1, 2),
-                                                          (4, 1, 1, 2), (8, 0, 1, 2)])
-def test_loopback_lds_graph_matches_oracle(pgcn, big_ds, big_oracle, world, split_rows, lds,
-                                           chunks):
-    """chunks: GraphSum row chunks (rs_chunks; 2 = each chunk's reduce-scatter on the comm
-    stream while the next chunk is summed)."""
-    with helpers.knobs(pgcn, split_rows=split_rows, lds_min_kb=-1 if lds else 1 << 20,
-                       rs_chunks=chunks):
+@pytest.mark.parametrize("world,split_rows,lds", [(2, 0, 1), (2, 1, 1), (4, 0, 1), (8, 0, 1),
+                                                  (4, 0, 0), (4, 1, 1)])
+def test_loopback_lds_graph_matches_oracle(pgcn, big_ds, big_oracle, world, split_rows, lds):
+    """lds 1: every rank's column block takes the LDS ring GraphSum, whose combine pushes the
+    partial sums into the owners' receive slots (PeerComm); lds 0: the plain kernels, whose
+    partials go through the generic push / wait / rank-order sum; split_rows 1: the output
+    layer's forward over the split's rows (the generic path too)."""
+    with helpers.knobs(pgcn, split_rows=split_rows, lds_min_kb=-1 if lds else 1 << 20):
         res = _run_world(pgcn, big_ds, world, 4)
     _check_ranks(res, world, big_ds.num_nodes)
     assert res[0]["info"]["graphsum_lds"] == lds
@@ -101,14 +101,13 @@ def test_loopback_lds_graph_matches_oracle(pgcn, big_ds, big_oracle, world, spli
                               ties=test_ties)
 
 
-def test_loopback_chunks_hidden_above_128(pgcn, big_ds):
-    """Two row chunks (rs_chunks 2) at world 2 with a hidden width above 128 on the LDS path:
-    those GraphSums prescale per 16-column pass, so chunk 1 cannot share chunk 0's batched
-    tables and prescales its own (the shared-table check threw here)."""
+def test_loopback_hidden_above_128(pgcn, big_ds):
+    """A hidden width above 128 on the LDS path at world 2: 16 passes of 16 columns, each pass's
+    combine pushing its columns into the owners' slots and only the last one signalling; those
+    GraphSums prescale per pass (the batched prescale takes <= 128 columns)."""
     dims, drops = (256,), (0.5, 0.5)
     p = pgcn.make_params(big_ds, hidden_dims=dims, dropouts=drops)
-    with helpers.knobs(pgcn, rs_chunks=2):
-        res = _run_world(pgcn, big_ds, 2, 2, params=p)
+    res = _run_world(pgcn, big_ds, 2, 2, params=p)
     _check_ranks(res, 2, big_ds.num_nodes)
     assert res[0]["info"]["graphsum_lds"] == 1
     ref = helpers.OracleGCN(helpers.ds_dict(big_ds), hidden_dims=dims, dropouts=drops)

@@ -162,22 +162,6 @@ def test_xstream_ring_engine_matches_register_kernels(pgcn, rw_ds):
         assert np.abs(lines[1][:, col] - lines[0][:, col]).max() * cnt[sp] <= 3 + 1e-3
 
 
-def test_mask_nib_engine_bit_identical(pgcn, rw_ds):
-    """The input mask drawn by one launch into both layouts (mask_nib 1, k_dropout_mask_nib)
-    against k_dropout_mask + k_mask_nibbles (mask_nib 0, the default) in whole runs at reddit's
-    width: the same masks reach the same kernels, so every line and the weights are identical."""
-    out = {}
-    for nib in (0, 1):
-        with helpers.knobs(pgcn, mask_nib=nib):
-            g = pgcn.GCN(pgcn.make_params(rw_ds), rw_ds)
-            lines = np.array([g.train_epoch() + g.eval(2) for _ in range(3)], np.float64)
-            out[nib] = (lines, g.get_var(2), g.get_var(5))
-            g.close()
-    np.testing.assert_array_equal(out[0][0], out[1][0])
-    np.testing.assert_array_equal(out[0][1], out[1][1])
-    np.testing.assert_array_equal(out[0][2], out[1][2])
-
-
 def test_deep_reddit_width_matches_oracle(pgcn):
     """4 layers x hidden 128 at reddit's feature width (F = 602, 10 k-chunks of 64): the first
     layer's product and weight gradient run on the wide MFMA kernels (k_gemm_wide.hip) with

@@ -1,7 +1,7 @@
 """Wide-output GEMM timing on the reddit hidden-128 shapes (GPU box): pgcn_gemm (NN) and
 pgcn_gemm_tn (TN) at M = 232,965 for (K, N) = (602, 128) masked, (128, 128), (128, 41 via
-trans B) -- the 4-layer hidden-128 model's contractions -- with the wide kernels (gemm_variant
-0) and the general ones (gemm_variant 1).  HIP events on torch's stream; one JSON line with ms
+trans B) -- the 4-layer hidden-128 model's contractions -- with the wide kernels
+(r05: the general-kernel arm was removed).  HIP events on torch's stream; one JSON line with ms
 per call and TF/s against the 157.3 TF fp32 MFMA peak."""
 import ctypes
 import json
@@ -49,8 +49,7 @@ for (K, N, masked, tb) in ((602, 128, True, 0), (602, 128, False, 0), (128, 128,
     dW = torch.empty(K, N, device=dev)
     ws = torch.empty(lib.pgcn_gemm_tn_workspace(M, N, K) // 4 + 64, device=dev)
     flops = 2.0 * M * N * K
-    for variant in ((0, 1) if os.environ.get("BOTH") else (0,)):
-        lib.pgcn_debug_set(b"gemm_variant", variant)
+    for variant in (0,):  # (r05: the general-kernel arm "gemm_variant" 1 was removed)
 
         def nn():
             pg.check(lib.pgcn_gemm(M, N, K, vp(A), lda, vp(B), K if tb else N, tb, vp(C), N,
@@ -64,5 +63,4 @@ for (K, N, masked, tb) in ((602, 128, True, 0), (602, 128, False, 0), (128, 128,
             res[f"{name}_K{K}_N{N}{'m' if masked else ''}_v{variant}"] = {"ms": round(ms, 4),
                                                    "tflops": round(flops / ms / 1e9, 1),
                                                    "frac": round(flops / ms / 1e9 / 157.3, 3)}
-    lib.pgcn_debug_set(b"gemm_variant", 0)
 print(json.dumps(res))

@@ -23,8 +23,7 @@ ip, ix = ds.graph_indptr, ds.graph_indices
 x = torch.randn(n, 16, device="cuda")
 o = torch.empty(n, 16, device="cuda")
 st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-PATHS = {"ring": {}, "plain_blocked": {"lds_min_kb": 1 << 30},
-         "plain_rows": {"lds_min_kb": 1 << 30, "plain_blocks": 1}}
+PATHS = {"ring": {}, "plain_blocked": {"lds_min_kb": 1 << 30}}
 out = {"nodes": n, "nnz": int(ip[-1]), "calls": calls}
 ref = None
 for name, kn in PATHS.items():
