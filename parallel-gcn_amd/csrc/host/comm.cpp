@@ -159,19 +159,6 @@ void RcclComm::reduce_scatter_sum(const float *send, float *recv, size_t recvcou
                               static_cast<ncclComm_t>(comm_), s));
 }
 
-void SoloComm::allreduce_sum(float *buf, size_t n, hipStream_t s) {
-  (void)buf;
-  (void)s;
-  if (world_ > 1 && n > 0) count(n * sizeof(float), 2.0);
-}
-
-void SoloComm::reduce_scatter_sum(const float *send, float *recv, size_t recvcount,
-                                  hipStream_t s) {
-  count(recvcount * world_ * sizeof(float), 1.0);
-  PGCN_HIP(hipMemcpyAsync(recv, send + (size_t)rank_ * recvcount, recvcount * sizeof(float),
-                          hipMemcpyDeviceToDevice, s));
-}
-
 // ------------------------------------------------------------------------------------------
 // Loopback (in-process) collectives
 // ------------------------------------------------------------------------------------------
@@ -243,95 +230,126 @@ void LoopbackGroup::allgather(int rank, const void *mine, size_t bytes, void *al
 }
 
 namespace {
-// region layout: [flags: kPeerMaxRanks words][arrival counter][error word] ... 4 KB, slots
+// header (uncached): [flags: kPeerMaxRanks words][arrival counter][error word], 4 KB
 constexpr size_t kPeerHeader = 4096;
 constexpr size_t kArriveOff = kPeerMaxRanks * 4, kErrOff = kArriveOff + 4;
 
 struct PeerBlob {  // what a rank publishes at construction
-  hipIpcMemHandle_t handle;
-  unsigned long long ptr;  // in-process: the region's device address
+  hipIpcMemHandle_t slots, header;
+  unsigned long long slots_ptr, header_ptr;  // in-process: the regions' device addresses
   int ok;
   int pad;
 };
 }  // namespace
 
 PeerComm::PeerComm(int rank, int world, size_t slot_floats, AllGather ag, bool ipc,
-                   std::function<void()> host_order)
-    : Comm(rank, world), ag_(std::move(ag)), ipc_(ipc), host_order_(std::move(host_order)) {
-  PGCN_CHECK(world >= 1 && world <= kPeerMaxRanks && rank >= 0 && rank < world && ag_,
+                   std::function<void()> host_order, bool solo)
+    : Comm(rank, world), ag_(std::move(ag)), ipc_(ipc && !solo), solo_(solo),
+      host_order_(std::move(host_order)) {
+  PGCN_CHECK(world >= 1 && world <= kPeerMaxRanks && rank >= 0 && rank < world && (ag_ || solo),
              PGCN_E_INVALID, "peer comm: rank / world");
   slot_floats_ = (std::max<size_t>(slot_floats, 4) + 63) / 64 * 64;  // 256-B aligned slots
-  bytes_ = kPeerHeader + 2 * (size_t)world * slot_floats_ * sizeof(float);
-  // uncached: no cache of this GPU or a peer holds a line of the flags or the slots
+  bytes_ = 2 * (size_t)world * slot_floats_ * sizeof(float);
+  // slots: plain device memory (written through by the pushers' sc0 sc1 stores, read by
+  // plain loads after a kernel boundary: MTYPE RW lines are kept coherent by the memory
+  // probes); header: uncached (the flags and counters every rank polls and adds to)
   void *p = nullptr;
-  if (hipExtMallocWithFlags(&p, bytes_, hipDeviceMallocUncached) != hipSuccess || !p)
-    throw Error(PGCN_E_NOMEM, "peer comm: uncached region of " + std::to_string(bytes_) + " B");
-  region_ = static_cast<char *>(p);
-  PGCN_HIP(hipMemset(region_, 0, kPeerHeader));
+  PGCN_HIP(hipMalloc(&p, bytes_));
+  slots_ = static_cast<char *>(p);
+  p = nullptr;
+  if (hipExtMallocWithFlags(&p, kPeerHeader, hipDeviceMallocUncached) != hipSuccess || !p) {
+    (void)hipFree(slots_);
+    throw Error(PGCN_E_NOMEM, "peer comm: uncached flag region");
+  }
+  header_ = static_cast<char *>(p);
+  PGCN_HIP(hipMemset(header_, 0, kPeerHeader));
   PGCN_HIP(hipDeviceSynchronize());
+  if (solo_) {
+    peer_slots_.assign((size_t)world, slots_);
+    peer_header_.assign((size_t)world, header_);
+    return;
+  }
   PeerBlob mine{};
-  mine.ptr = (unsigned long long)(uintptr_t)region_;
+  mine.slots_ptr = (unsigned long long)(uintptr_t)slots_;
+  mine.header_ptr = (unsigned long long)(uintptr_t)header_;
   mine.ok = 1;
-  if (ipc_ && hipIpcGetMemHandle(&mine.handle, region_) != hipSuccess) mine.ok = 0;
+  if (ipc_ && (hipIpcGetMemHandle(&mine.slots, slots_) != hipSuccess ||
+               hipIpcGetMemHandle(&mine.header, header_) != hipSuccess))
+    mine.ok = 0;
   std::vector<PeerBlob> all((size_t)world);
   ag_(&mine, sizeof mine, all.data());
   // every rank reports whether it could map every peer; all fail together
   int ok = 1;
   std::string why;
   for (int q = 0; q < world; q++) ok &= all[(size_t)q].ok;
-  if (!ok) why = "a rank could not export its region";
-  peer_.assign((size_t)world, nullptr);
+  if (!ok) why = "a rank could not export its regions";
+  peer_slots_.assign((size_t)world, nullptr);
+  peer_header_.assign((size_t)world, nullptr);
   for (int q = 0; q < world && ok; q++) {
     if (q == rank || !ipc_) {
-      peer_[(size_t)q] = q == rank ? region_ : reinterpret_cast<char *>((uintptr_t)all[(size_t)q].ptr);
+      peer_slots_[(size_t)q] = q == rank ? slots_ : reinterpret_cast<char *>((uintptr_t)all[(size_t)q].slots_ptr);
+      peer_header_[(size_t)q] = q == rank ? header_ : reinterpret_cast<char *>((uintptr_t)all[(size_t)q].header_ptr);
       continue;
     }
-    void *m = nullptr;
-    const hipError_t e = hipIpcOpenMemHandle(&m, all[(size_t)q].handle, hipIpcMemLazyEnablePeerAccess);
-    if (e != hipSuccess || !m) {
-      ok = 0;
-      why = std::string("hipIpcOpenMemHandle of rank ") + std::to_string(q) + ": " + hipGetErrorString(e);
-      break;
+    for (int h = 0; h < 2 && ok; h++) {
+      void *m = nullptr;
+      const hipError_t e = hipIpcOpenMemHandle(&m, h ? all[(size_t)q].header : all[(size_t)q].slots,
+                                               hipIpcMemLazyEnablePeerAccess);
+      if (e != hipSuccess || !m) {
+        ok = 0;
+        why = std::string("hipIpcOpenMemHandle of rank ") + std::to_string(q) + ": " + hipGetErrorString(e);
+        break;
+      }
+      (h ? peer_header_ : peer_slots_)[(size_t)q] = static_cast<char *>(m);
     }
-    peer_[(size_t)q] = static_cast<char *>(m);
   }
   int oks[kPeerMaxRanks];
   ag_(&ok, sizeof ok, oks);
   for (int q = 0; q < world; q++) ok &= oks[q];
   if (!ok) {
-    for (int q = 0; q < world; q++)
-      if (ipc_ && q != rank && peer_[(size_t)q]) (void)hipIpcCloseMemHandle(peer_[(size_t)q]);
-    peer_.clear();
-    (void)hipFree(region_);
-    region_ = nullptr;
+    unmap();
+    (void)hipFree(slots_);
+    (void)hipFree(header_);
+    slots_ = header_ = nullptr;
     throw Error(PGCN_E_COMM, "peer comm: " + (why.empty() ? std::string("a peer failed to map") : why));
   }
 }
 
-PeerComm::~PeerComm() {
-  if (!region_) return;
-  (void)hipDeviceSynchronize();
-  // nobody closes or frees before every rank is done with every collective, and nobody frees
-  // before every peer has closed its mapping of this region
-  int token = 0;
-  std::vector<int> all((size_t)world_);
-  try {
-    ag_(&token, sizeof token, all.data());
-  } catch (...) {
-  }
+void PeerComm::unmap() {
   if (ipc_)
-    for (int q = 0; q < world_; q++)
-      if (q != rank_ && peer_[(size_t)q]) (void)hipIpcCloseMemHandle(peer_[(size_t)q]);
-  try {
-    ag_(&token, sizeof token, all.data());
-  } catch (...) {
-  }
-  (void)hipFree(region_);
+    for (int q = 0; q < world_; q++) {
+      if (q == rank_) continue;
+      if (q < (int)peer_slots_.size() && peer_slots_[(size_t)q]) (void)hipIpcCloseMemHandle(peer_slots_[(size_t)q]);
+      if (q < (int)peer_header_.size() && peer_header_[(size_t)q]) (void)hipIpcCloseMemHandle(peer_header_[(size_t)q]);
+    }
+  peer_slots_.clear();
+  peer_header_.clear();
 }
 
-float *PeerComm::slot(char *region, int parity, int sender) const {
-  return reinterpret_cast<float *>(region + kPeerHeader) +
-         ((size_t)parity * world_ + (size_t)sender) * slot_floats_;
+PeerComm::~PeerComm() {
+  if (!slots_) return;
+  (void)hipDeviceSynchronize();
+  if (!solo_) {
+    // nobody closes or frees before every rank is done with every collective, and nobody
+    // frees before every peer has closed its mappings of this rank's regions
+    int token = 0;
+    std::vector<int> all((size_t)world_);
+    try {
+      ag_(&token, sizeof token, all.data());
+    } catch (...) {
+    }
+    unmap();
+    try {
+      ag_(&token, sizeof token, all.data());
+    } catch (...) {
+    }
+  }
+  (void)hipFree(slots_);
+  (void)hipFree(header_);
+}
+
+float *PeerComm::slot(char *slots, int parity, int sender) const {
+  return reinterpret_cast<float *>(slots) + ((size_t)parity * world_ + (size_t)sender) * slot_floats_;
 }
 
 PeerSink PeerComm::sink(int rows_per_rank, size_t row_floats) {
@@ -340,10 +358,11 @@ PeerSink PeerComm::sink(int rows_per_rank, size_t row_floats) {
   const unsigned g = ++gen_;
   PeerSink k{};
   for (int q = 0; q < world_; q++) {
-    k.dst[q] = slot(peer_[(size_t)q], (int)(g & 1), rank_);
-    k.flag[q] = reinterpret_cast<unsigned *>(peer_[(size_t)q]) + rank_;
+    k.dst[q] = slot(peer_slots_[(size_t)q], (int)(g & 1), rank_);
+    k.flag[q] = reinterpret_cast<unsigned *>(peer_header_[(size_t)q]) + rank_;
   }
-  k.arrive = reinterpret_cast<unsigned *>(region_ + kArriveOff);
+  k.arrive = reinterpret_cast<unsigned *>(header_ + kArriveOff);
+  k.slot_bytes = (long long)(slot_floats_ * sizeof(float));
   k.gen = g;
   k.world = world_;
   k.rows_per_rank = rows_per_rank;
@@ -353,20 +372,21 @@ PeerSink PeerComm::sink(int rows_per_rank, size_t row_floats) {
 
 void PeerComm::wait(hipStream_t s) {
   if (host_order_) host_order_();
-  launch_peer_wait(reinterpret_cast<const unsigned *>(region_), world_, gen_,
-                   reinterpret_cast<unsigned *>(region_ + kErrOff), s);
+  // (solo: every push signalled this rank's own flag word only)
+  launch_peer_wait(reinterpret_cast<const unsigned *>(header_) + (solo_ ? rank_ : 0),
+                   solo_ ? 1 : world_, gen_, reinterpret_cast<unsigned *>(header_ + kErrOff), s);
 }
 
 PeerRecv PeerComm::recv() const {
   PeerRecv r{};
-  for (int q = 0; q < world_; q++) r.slot[q] = slot(region_, (int)(gen_ & 1), q);
+  for (int q = 0; q < world_; q++) r.slot[q] = slot(slots_, (int)(gen_ & 1), q);
   r.world = world_;
   return r;
 }
 
 void PeerComm::check() const {
   unsigned e = 0;
-  PGCN_HIP(hipMemcpy(&e, region_ + kErrOff, sizeof e, hipMemcpyDeviceToHost));
+  PGCN_HIP(hipMemcpy(&e, header_ + kErrOff, sizeof e, hipMemcpyDeviceToHost));
   if (e)
     throw Error(PGCN_E_COMM, "peer exchange: rank " + std::to_string(e & 0xffff) +
                                  " did not signal rank " + std::to_string(rank_) + " in time");
@@ -376,6 +396,14 @@ void PeerComm::allreduce_sum(float *buf, size_t n, hipStream_t s) {
   if (world_ == 1 || n == 0) return;
   count(n * sizeof(float), 2.0);
   PeerSink k = sink(1, n);
+  if (!host_order_ && n <= (size_t)kPeerSmallAllreduce) {
+    // separate processes (or solo): push, wait and sum in one workgroup
+    launch_peer_allreduce_small(buf, (int)n, k, recv(),
+                                reinterpret_cast<const unsigned *>(header_) + (solo_ ? rank_ : 0),
+                                solo_ ? 1 : world_, reinterpret_cast<unsigned *>(header_ + kErrOff),
+                                s);
+    return;
+  }
   // every receiver gets the same n floats: send[q * n ..) = buf for every q (stride 0)
   k.rows_per_rank = 0;
   launch_peer_push(buf, n, k, s, /*same_for_all=*/true);

@@ -81,17 +81,6 @@ class Comm {
   int rank_, world_;
 };
 
-// Timing only (tools/rank_epoch.py): rank `rank` of `world` with no peers -- a reduce-scatter
-// keeps this rank's own share, an all-reduce leaves the buffer.  The rank's kernels and
-// stream order are the edge-cut engine's; its numbers are not (no other rank contributes).
-class SoloComm : public Comm {
- public:
-  SoloComm(int rank, int world) : Comm(rank, world) {}
-  void allreduce_sum(float *buf, size_t n, hipStream_t s) override;
-  void reduce_scatter_sum(const float *send, float *recv, size_t recvcount,
-                          hipStream_t s) override;
-  const char *kind() const override { return "solo"; }
-};
 
 // One process per GPU over RCCL (xGMI on one node).
 class RcclComm : public Comm {
@@ -131,8 +120,9 @@ class LoopbackGroup {
 };
 
 // One-sided exchange over peer-mapped receive slots (k_peer.hip).  Every rank
-// owns one uncached device region: its flag words (one per sender), an arrival counter, an
-// error word, and 2 x world receive slots (generation parity x sender) of slot_floats floats.
+// owns two device regions: 2 x world receive slots (generation parity x sender) of slot_floats
+// floats, and an uncached header of flag words (one per sender), an arrival counter and an
+// error word.
 // Every region is mapped into every rank: hipIpcGetMemHandle / hipIpcOpenMemHandle between
 // processes (`ipc`, one process per GPU), raw device pointers between the in-process loopback
 // ranks on one device.  A collective is: pushes into the receivers' slots (k_peer_push, or the
@@ -148,13 +138,16 @@ class PeerComm : public Comm {
   // host_order (in-process ranks): before a rank enqueues a wait, every rank has enqueued the
   // push it waits for -- ranks of one process may share hardware queues (GPU_MAX_HW_QUEUES),
   // where a wait ahead of a peer's push would block that push (a host rendezvous per wait)
+  // solo (timing only, tools/rank_epoch.py): rank `rank` of `world` with no peers -- every
+  // peer's region is this rank's own, so the pushes, waits and sums run with this rank's
+  // kernels and bytes (every store local), but the results are not the model's
   PeerComm(int rank, int world, size_t slot_floats, AllGather ag, bool ipc,
-           std::function<void()> host_order = nullptr);
+           std::function<void()> host_order = nullptr, bool solo = false);
   ~PeerComm() override;
   void allreduce_sum(float *buf, size_t n, hipStream_t s) override;
   void reduce_scatter_sum(const float *send, float *recv, size_t recvcount,
                           hipStream_t s) override;
-  const char *kind() const override { return ipc_ ? "peer" : "loopback"; }
+  const char *kind() const override { return solo_ ? "solo" : ipc_ ? "peer" : "loopback"; }
   // The GraphSum exchange fused into the combine: sink() opens the next collective and returns
   // where this rank's rows go (rows_per_rank padded rows per owner, owner-major); after the
   // push, wait() enqueues the wait for every sender and recv() names the received slots
@@ -166,13 +159,14 @@ class PeerComm : public Comm {
   void check() const;
 
  private:
-  float *slot(char *region, int parity, int sender) const;
-  char *region_ = nullptr;                   // this rank's region
-  std::vector<char *> peer_;                 // every rank's region as mapped here
+  float *slot(char *slots, int parity, int sender) const;
+  void unmap();
+  char *slots_ = nullptr, *header_ = nullptr;     // this rank's regions
+  std::vector<char *> peer_slots_, peer_header_;  // every rank's regions as mapped here
   size_t slot_floats_ = 0, bytes_ = 0;
   unsigned gen_ = 0;                         // the last collective's generation
   AllGather ag_;
-  bool ipc_ = false;
+  bool ipc_ = false, solo_ = false;
   std::function<void()> host_order_;
 };
 

@@ -272,9 +272,7 @@ GCN::GCN(const GCNParams &params_, const AdamParams &adam, const GCNData &data, 
   part = make_partition(params.num_nodes, data.graph.indptr.data(), world, rank,
                         1);
   if (dist) {  // the edge-cut path (also at world == 1, which exercises it on one GPU)
-    if (dist->solo) {
-      comm = std::make_unique<SoloComm>(rank, world);
-    } else if (dist->loopback || dist->allgather) {
+    if (dist->loopback || dist->allgather || dist->solo) {
       // peer-mapped slots sized for the largest collective: a GraphSum's rows of one owner at
       // the widest row, the weight-gradient all-reduce, Â X's 16-column reduce-scatters
       size_t ld = 16;
@@ -287,7 +285,9 @@ GCN::GCN(const GCNParams &params_, const AdamParams &adam, const GCNData &data, 
         wtotal += (long long)a * b;
       }
       const size_t cap = std::max((size_t)part.maxrows * ld, (size_t)wtotal);
-      if (dist->loopback) {
+      if (dist->solo) {  // timing only: every peer is this rank (PeerComm's solo form)
+        comm = std::make_unique<PeerComm>(rank, world, cap, nullptr, false, nullptr, true);
+      } else if (dist->loopback) {
         auto grp = dist->loopback;
         comm = std::make_unique<PeerComm>(
             rank, world, cap,

@@ -82,7 +82,7 @@ struct DistSpec {
   // one process per GPU over peer-mapped slots (PeerComm over hipIpc handles, exchanged by
   // this host all-gather) instead of RCCL
   PeerComm::AllGather allgather;
-  bool solo = false;  // timing only: SoloComm (no peers)
+  bool solo = false;  // timing only: PeerComm with no peers (every push lands in this rank)
 };
 
 class GCN {

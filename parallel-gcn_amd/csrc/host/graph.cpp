@@ -599,6 +599,7 @@ void DevGraph::graphsum(const float *in, int ld_in, float *out, int ld_out, int 
       if (push) {  // this pass's columns of every owner's slot; the last pass signals
         pk = *push;
         for (int q = 0; q < pk.world; q++) pk.dst[q] += c;
+        pk.slot_bytes -= 4LL * c;
         pk.signal = p == n_pass - 1 ? push->signal : 0;
       }
       launch_graphsum_ring(lds_->s, in + c, ld_in, out ? out + c : nullptr, ld_out,

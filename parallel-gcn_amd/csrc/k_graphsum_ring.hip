@@ -121,10 +121,15 @@ __global__ __launch_bounds__(256) void k_gs_lds_combine(const float4 *__restrict
                                                         const float *__restrict__ scale, int n,
                                                         float4 *__restrict__ out, int ld4_out,
                                                         GsEpilogue epi, PeerSink push) {
-  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long r = t >> 2;
   if (PUSH) {
-    if (r < n) {
+    // consecutive workgroups serve different owners (block b: owner b % world, its rows
+    // 64 (b / world) ..): the pushes in flight at any time spread over every peer's link
+    // instead of draining the owners one after another
+    const int q0 = (int)(blockIdx.x % (unsigned)push.world);
+    const long long j0 = (long long)(blockIdx.x / (unsigned)push.world) * 64 + (threadIdx.x >> 2);
+    const long long r = (long long)q0 * push.rows_per_rank + j0;
+    const long long t = r * 4 + (threadIdx.x & 3);
+    if (j0 < push.rows_per_rank && r < n) {
       const int v = (int)(t & 3);
       const float s = scale[r];
       float4 a;
@@ -147,11 +152,13 @@ __global__ __launch_bounds__(256) void k_gs_lds_combine(const float4 *__restrict
       a.w *= s;
       const int q = (int)(r / push.rows_per_rank);
       const long long j = r - (long long)q * push.rows_per_rank;
-      reinterpret_cast<float4 *>(push.dst[q])[j * ld4_out + v] = a;
+      peer_store16(push.dst[q], push.slot_bytes, j * ld4_out + v, a);
     }
     peer_arrive(push);
     return;
   }
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long r = t >> 2;
   if (r >= n) return;
   const int v = (int)(t & 3);
   // the row scale and the epilogue's inputs with the partials: one round trip, not one each
@@ -485,7 +492,8 @@ void launch_graphsum_ring(const LdsSchedule &s, const float *in, int ld_in, floa
     PGCN_CHECK((!epi || epi->mode == 0) && push->world >= 1 && push->world <= kPeerMaxRanks &&
                    push->rows_per_rank > 0 && (long long)push->rows_per_rank * push->world >= s.n_rows,
                PGCN_E_INVALID, "graphsum_ring: push shape");
-    PGCN_LAUNCH(k_gs_lds_combine<true>, dim3((unsigned)ceil_div(post, 256)), dim3(256), 0, st,
+    const long long blocks = (long long)push->world * ceil_div(push->rows_per_rank, 64);
+    PGCN_LAUNCH(k_gs_lds_combine<true>, dim3((unsigned)blocks), dim3(256), 0, st,
                 reinterpret_cast<const float4 *>(partial), (long long)s.n_rows, s.n_blocks,
                 s.row_scale, s.n_rows, nullptr, ld_out / 4, none, *push);
   } else {

@@ -28,17 +28,21 @@
 namespace pgcn {
 
 // send [world][count] (stride 0: the same count floats for every receiver) -> receiver q's
-// slot (sink.dst[q]); blockIdx.y = q
+// slot (sink.dst[q]); blockIdx.x = q (consecutive workgroups push to different peers: every
+// link busy at once), blockIdx.y = the workgroup's piece of the count
 // (T = float4 when count % 4 == 0, else float)
 template <typename T>
 __global__ __launch_bounds__(256) void k_peer_push(const T *__restrict__ send, long long n,
                                                    long long stride, PeerSink k) {
-  const int q = blockIdx.y;
-  T *dst = reinterpret_cast<T *>(k.dst[q]);
+  const int q = blockIdx.x;
   const T *src = send + (long long)q * stride;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (long long)gridDim.x * blockDim.x)
-    dst[i] = src[i];
+  for (long long i = (long long)blockIdx.y * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.y * blockDim.x) {
+    if constexpr (sizeof(T) == 16)
+      peer_store16(k.dst[q], k.slot_bytes, i, src[i]);
+    else
+      peer_store4(k.dst[q], k.slot_bytes, i, src[i]);
+  }
   peer_arrive(k);
 }
 
@@ -63,6 +67,81 @@ __global__ __launch_bounds__(64) void k_peer_wait(const unsigned *flags, int wor
 __device__ __forceinline__ void peer_acc(float &a, float b) { a += b; }
 __device__ __forceinline__ void peer_acc(float4 &a, const float4 &b) { f4_acc(a, b); }
 
+// A small all-reduce in ONE workgroup (separate processes only: their kernels never share a
+// hardware queue, so this rank's spin cannot sit ahead of a peer's push): buf [n] pushed to
+// every receiver's slot of this rank, the flags, one wave polling this rank's flags (waited[q],
+// q < nwait), one system-scope acquire (the slots were written by other agents within this
+// kernel's lifetime: no kernel boundary in between), the rank-order sum back into buf.
+// Replaces push + wait + sum launches (3 x ~5 us per collective at W = 8) for the weight
+// gradients and the loss scalars.
+__global__ __launch_bounds__(256) void k_peer_allreduce_small(float *__restrict__ buf, int n,
+                                                              PeerSink k, PeerRecv r,
+                                                              const unsigned *waited, int nwait,
+                                                              unsigned *err) {
+  const bool v4 = (n & 3) == 0;
+  for (int q = 0; q < k.world; q++) {
+    if (v4)
+      for (int i = threadIdx.x; i < n / 4; i += blockDim.x)
+        peer_store16(k.dst[q], k.slot_bytes, i, reinterpret_cast<const float4 *>(buf)[i]);
+    else
+      for (int i = threadIdx.x; i < n; i += blockDim.x) peer_store4(k.dst[q], k.slot_bytes, i, buf[i]);
+  }
+  stores_acked();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int q = 0; q < k.world; q++) flag_store(k.flag[q], k.gen);
+    stores_acked();
+  }
+  __shared__ int failed;
+  if (threadIdx.x < 64) {
+    const int q = threadIdx.x;
+    bool bad = flag_load(err) != 0;
+    if (!bad && q < nwait) {
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      while ((int)(flag_load(waited + q) - k.gen) < 0) {
+        __builtin_amdgcn_s_sleep(2);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kPeerTimeoutTicks) {
+          __hip_atomic_store(err, 0x10000u | (unsigned)q, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+          bad = true;
+          break;
+        }
+      }
+    }
+    const unsigned long long any_bad = __ballot(bad);
+    if (threadIdx.x == 0) {
+      failed = any_bad != 0;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: L1 (and NC lines) dropped
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (failed) return;
+  if (v4) {
+    for (int i = threadIdx.x; i < n / 4; i += blockDim.x) {
+      float4 a = reinterpret_cast<const float4 *>(r.slot[0])[i];
+      for (int q = 1; q < r.world; q++) f4_acc(a, reinterpret_cast<const float4 *>(r.slot[q])[i]);
+      reinterpret_cast<float4 *>(buf)[i] = a;
+    }
+  } else {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      float a = r.slot[0][i];
+      for (int q = 1; q < r.world; q++) a += r.slot[q][i];
+      buf[i] = a;
+    }
+  }
+}
+
+void launch_peer_allreduce_small(float *buf, int n, const PeerSink &k, const PeerRecv &r,
+                                 const unsigned *waited, int nwait, unsigned *err,
+                                 hipStream_t s) {
+  PGCN_CHECK(k.world >= 1 && k.world <= kPeerMaxRanks && r.world == k.world && n >= 0 &&
+                 n <= kPeerSmallAllreduce,
+             PGCN_E_INVALID, "peer_allreduce_small: shape");
+  PGCN_LAUNCH(k_peer_allreduce_small, dim3(1), dim3(256), 0, s, buf, n, k, r, waited, nwait, err);
+  PGCN_HIP(hipGetLastError());
+}
+
 // dst[i] = sum over q (rank order) of slot[q][i]
 template <typename T>
 __global__ __launch_bounds__(256) void k_peer_sum(PeerRecv r, T *__restrict__ dst, long long n) {
@@ -84,8 +163,8 @@ void launch_peer_push(const float *send, size_t count, const PeerSink &k, hipStr
   PGCN_CHECK(k.world >= 1 && k.world <= kPeerMaxRanks, PGCN_E_INVALID, "peer_push: world");
   const bool v4 = count % 4 == 0;
   const long long n = (long long)(v4 ? count / 4 : count);
-  const dim3 grid((unsigned)std::max<long long>(1, std::min<long long>(ceil_div(n, 256), 64)),
-                  (unsigned)k.world);
+  const dim3 grid((unsigned)k.world,
+                  (unsigned)std::max<long long>(1, std::min<long long>(ceil_div(n, 256), 64)));
   const long long stride = same_for_all ? 0 : n;
   if (v4)
     PGCN_LAUNCH(k_peer_push<float4>, grid, dim3(256), 0, s, reinterpret_cast<const float4 *>(send),

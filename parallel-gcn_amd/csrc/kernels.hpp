@@ -194,6 +194,7 @@ struct PeerSink {
   float *dst[kPeerMaxRanks];
   unsigned *flag[kPeerMaxRanks];
   unsigned *arrive = nullptr;  // this rank's arrival counter (zero between launches)
+  long long slot_bytes = 0;    // bytes from dst[q] to the end of q's slot
   unsigned gen = 0;            // the collective's generation, stored into the flags
   int world = 0;               // 0: not pushing
   int rows_per_rank = 0;       // GraphSum push: padded rows per owner (row r -> owner r / this)
@@ -211,6 +212,11 @@ void launch_peer_push(const float *send, size_t count, const PeerSink &k, hipStr
 // one wave until flags[q] == gen for every q < world (err: set on a timeout, then no waiting)
 void launch_peer_wait(const unsigned *flags, int world, unsigned gen, unsigned *err,
                       hipStream_t s);
+// one workgroup: push buf [n] to every receiver, signal, wait for waited[q < nwait], sum the
+// received slots in rank order back into buf (separate processes only: see k_peer.hip)
+constexpr int kPeerSmallAllreduce = 1 << 16;
+void launch_peer_allreduce_small(float *buf, int n, const PeerSink &k, const PeerRecv &r,
+                                 const unsigned *waited, int nwait, unsigned *err, hipStream_t s);
 // dst[i] = sum over q (rank order) of r.slot[q][i]
 void launch_peer_sum(const PeerRecv &r, float *dst, size_t count, hipStream_t s);
 // the GraphSum exchange's receiving end: y[j] (j < n local rows, [ld] floats, dim columns) =
