@@ -46,6 +46,33 @@ def test_create_without_device_fails_loudly(pgcn, loaded):
     ds = loaded["cora"]
     with pytest.raises(pgcn.PgcnError):
         pgcn.GCN(pgcn.make_params(ds), ds)
+    # the peer-mapped engine: NODEVICE before its host all-gather is ever called
+    calls = []
+
+    def ag(data):
+        calls.append(data)
+        return [data, data]
+    with pytest.raises(pgcn.PgcnError) as e:
+        pgcn.GCN(pgcn.make_params(ds), ds, rank=0, world=2, allgather=ag)
+    assert e.value.status == pgcn.PGCN_E_NODEVICE and not calls
+
+
+def test_peer_allgather_callback(pgcn):
+    """pgcn_allgather_fn over a Python all-gather (what bench.py hands the peer engine): the
+    ranks' byte strings land in rank order; a failing or short all-gather reports -1."""
+    import ctypes
+    fn = pgcn.peer_allgather_fn(lambda d: [d, bytes(reversed(d)), d])
+    mine = ctypes.create_string_buffer(b"abcd", 4)
+    out = ctypes.create_string_buffer(12)
+    assert fn(ctypes.cast(mine, ctypes.c_void_p), 4, ctypes.cast(out, ctypes.c_void_p), None) == 0
+    assert out.raw == b"abcddcbaabcd"
+    bad = pgcn.peer_allgather_fn(lambda d: [d, d[:2]])
+    assert bad(ctypes.cast(mine, ctypes.c_void_p), 4, ctypes.cast(out, ctypes.c_void_p), None) == -1
+
+    def boom(d):
+        raise RuntimeError("channel down")
+    assert pgcn.peer_allgather_fn(boom)(ctypes.cast(mine, ctypes.c_void_p), 4,
+                                        ctypes.cast(out, ctypes.c_void_p), None) == -1
 
 
 @pytest.mark.parametrize("name", ["cora", "citeseer", "pubmed_synth"])
