@@ -148,8 +148,10 @@ void launch_slab_reduce(float *partial, int n_slabs, int K, int N, int ldp, floa
                         int nst, hipStream_t s);
 // X-stream kernels (k_gemm.hip): N <= 16, K <= 640, dropout bits in the nibble layout
 bool xstream_ok(int N, int K);
+// side_blocks > 0: the LDS-free grid-stride form on at most that many workgroups (the same
+// words), for a build beside the ring GraphSum
 void launch_mask_nibbles(const uint64_t *mask, long long mask_base, long long mask_ld, int M,
-                         int K, uint64_t *out, hipStream_t s);
+                         int K, uint64_t *out, hipStream_t s, int side_blocks = 0);
 // What the first layer's X-stream product feeds (single C output, N <= 16): relu = the ReLU
 // of the GraphSum it stands for (eval from Â X; no mask: eval only), next_table = that
 // GraphSum's or the next one's prescaled ring table (next_scale[r] * value at the ring
@@ -249,16 +251,29 @@ void launch_spmm_csc_bwd(int nf, int p, int ldg, const int *csc_ptr, const int *
                          long long mask_base, float scale, const float *cgrad, float *bgrad,
                          hipStream_t s, long long nnz = 0);
 
-void launch_dropout_mask(uint64_t *states, long long n_chunks, long long elem0,
+// Mask words of n_chunks 64-element chunks from one xorshift128+ state per `group` chunks
+// (states[2q], states[2q + 1]: the state at chunk q * group's first draw), each state then
+// jumped by the table's period.  side_blocks > 0: the LDS-free form on at most that many
+// workgroups (k_dropout_mask_side, the same bits), for a draw beside the ring GraphSum
+void launch_dropout_mask(uint64_t *states, long long n_chunks, int group, long long elem0,
                          long long elem_end, float p, uint64_t *mask, const void *table,
-                         hipStream_t s, int max_blocks = 0);
+                         hipStream_t s, int max_blocks = 0, int side_blocks = 0);
 // two variables' draws (each as launch_dropout_mask's arguments) in one launch
 struct MaskDraw {
   uint64_t *states;
   long long n_chunks, elem0, elem_end;
   float p;
   uint64_t *mask;
+  int group = 1;
 };
+// chunks per state for a mask of n_chunks chunks: the largest of 1, 2, 4, .. 32 that leaves at
+// least kMaskMinPairs threads (each draws two groups side by side)
+constexpr long long kMaskMinPairs = 65536;
+inline int mask_group(long long n_chunks) {
+  int g = 1;
+  while (g < 32 && n_chunks / (4LL * g) >= kMaskMinPairs) g *= 2;
+  return g;
+}
 void launch_dropout_mask2(const MaskDraw &d0, const MaskDraw &d1, const void *table,
                           hipStream_t s);
 void launch_dropout_apply_based(float *x, long long n, const uint64_t *mask, long long base,

@@ -29,7 +29,8 @@ for kv in filter(None, os.environ.get("RANK_KNOBS", "").split(",")):
 worlds = [int(w) for w in (sys.argv[1] if len(sys.argv) > 1 else "1,2,4,8").split(",")]
 ranks = [int(r) for r in (sys.argv[2] if len(sys.argv) > 2 else "0").split(",")]
 hidden = tuple(int(h) for h in (sys.argv[3] if len(sys.argv) > 3 else "16").split(","))
-steps = 10
+steps = int(os.environ.get("RANK_STEPS", "10"))
+warmup = int(os.environ.get("RANK_WARMUP", "2"))  # the clock settles over ~18 epochs
 ds = pg.Dataset.synthetic(232965, 602, 41, 57307946, 1)
 params = pg.make_params(ds, hidden_dims=hidden, dropouts=(0.5,) * (len(hidden) + 1))
 out = {"hidden": list(hidden), "steps": steps, "ranks": {}}
@@ -38,7 +39,7 @@ for w in worlds:
         if r >= w:
             continue
         g = pg.GCN(params, ds, device=0, rank=r, world=w, solo=True)
-        for _ in range(2):
+        for _ in range(warmup):
             g.epoch_async()
         g.sync()
         torch.cuda.synchronize()
