@@ -127,12 +127,6 @@ int pgcn_rng_jump_table(uint64_t period, void *host_table /* 16*256*16 bytes */)
 int pgcn_dropout_mask(uint64_t *chunk_states, long long n_chunks, long long n_elems,
                       long long elem0, float p, uint64_t *mask, const void *dev_jump_table,
                       void *stream);
-/* The same words from one state per `group` consecutive chunks (state q: the state at the
- * draw element 64*(q*group) consumes; chunk c+1's draws continue where chunk c's end), each
- * state advanced by `period`: the engine's layout (r05), group 1 = pgcn_dropout_mask. */
-int pgcn_dropout_mask_groups(uint64_t *group_states, long long n_chunks, int group,
-                             long long n_elems, long long elem0, float p, uint64_t *mask,
-                             const void *dev_jump_table, void *stream);
 /* x[i] *= bit(i) ? scale : 0 for i in [0,n) (also the backward on grads). */
 int pgcn_dropout_apply(float *x, long long n, const uint64_t *mask, float scale, void *stream);
 
@@ -314,12 +308,8 @@ long long pgcn_partition_subgraph(int n, const int *indptr, const int *indices, 
 int pgcn_debug_rank_graph(int n, const int *indptr, const int *indices, int world, int rank,
                           int chunks, int chunk, pgcn_graph **out, int *rows, int *cols);
 /* Engine options (process-wide; most are read when an engine is built).  Each selects between
- * bit-identical or oracle-tested forms of the same reference epoch (19 keys, r05):
+ * bit-identical or oracle-tested forms of the same reference epoch (17 keys, r05):
  *   "train_ahead" 0/1, "eval_ax" 0/1, "split_cols" 0/1, "epoch_graph" 0/1, "mm_side" 0/1/2,
- *   "mask_side" 0..4 (dense X: the next input mask -- and, with eval_ax, its nibble words --
- *   built on a side stream beside the GraphSums by LDS-free kernels on that many workgroups
- *   per CU; 0: at the training forward), "mask_group" 0..64 (chunks per dropout state; 0: by
- *   mask size),
  *   "fuse_epilogue" bits 1 tails | 2 prestaged tables | 4 X-stream epilogue | 8 Dropout /
  *   ReLU backward in a Matmul's input-grad product (default 15),
  *   "fuse_output" 0..3 (default 2), "xstream_ring" 0/1, "lds_min_kb" (< 0: default),
@@ -367,14 +357,6 @@ int pgcn_debug_exp_check(const float *x, long long n, float *mine, float *lib, v
 /* q[i] = the loss kernel's quotient a[i] / b[i] (div_rn: from the reciprocal of b[i], the IEEE
  * division below 2^-125); device pointers */
 int pgcn_debug_div_check(const float *a, const float *b, long long n, float *q, void *stream);
-/* The LDS-free forms the engine runs on its side stream beside the ring GraphSum ("mask_side"),
- * on at most `blocks` workgroups: pgcn_dropout_mask_groups's and pgcn_mask_nibbles's results,
- * bit for bit (the same arguments otherwise). */
-int pgcn_debug_dropout_mask_side(uint64_t *group_states, long long n_chunks, int group,
-                                 long long n_elems, long long elem0, float p, uint64_t *mask,
-                                 const void *dev_jump_table, int blocks, void *stream);
-int pgcn_debug_mask_nibbles_side(const uint64_t *mask, long long mask_base, long long mask_ld,
-                                 int M, int K, uint64_t *out, int blocks, void *stream);
 
 #ifdef __cplusplus
 }

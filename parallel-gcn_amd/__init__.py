@@ -139,12 +139,6 @@ _sig("pgcn_debug_path_count", c_ll, ctypes.c_char_p, c_int)
 _sig("pgcn_debug_empty_launches", c_int, c_int, c_void_p)
 _sig("pgcn_debug_exp_check", c_int, c_void_p, c_ll, c_void_p, c_void_p, c_void_p)
 _sig("pgcn_debug_div_check", c_int, c_void_p, c_void_p, c_ll, c_void_p, c_void_p)
-_sig("pgcn_debug_dropout_mask_side", c_int, c_void_p, c_ll, c_int, c_ll, c_ll, c_float,
-     c_void_p, c_void_p, c_int, c_void_p)
-_sig("pgcn_dropout_mask_groups", c_int, c_void_p, c_ll, c_int, c_ll, c_ll, c_float, c_void_p,
-     c_void_p, c_void_p)
-_sig("pgcn_debug_mask_nibbles_side", c_int, c_void_p, c_ll, c_ll, c_int, c_int, c_void_p, c_int,
-     c_void_p)
 _sig("pgcn_debug_lds_check", c_int, c_int, c_int, c_void_p, c_void_p, c_int, P(ctypes.c_double),
      P(c_ll))
 _sig("pgcn_debug_lds_counts", c_ll, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_ll,
@@ -546,7 +540,7 @@ EXPORTED = [
     "pgcn_gemm_tn", "pgcn_mask_nibbles", "pgcn_gemm_xstream", "pgcn_gemm_xstream_dual",
     "pgcn_gemm_tn_xstream",
     "pgcn_spmm_csr", "pgcn_spmm_csc_bwd", "pgcn_csr_transpose",
-    "pgcn_rng_jump_table", "pgcn_dropout_mask", "pgcn_dropout_mask_groups", "pgcn_dropout_apply", "pgcn_relu_fwd",
+    "pgcn_rng_jump_table", "pgcn_dropout_mask", "pgcn_dropout_apply", "pgcn_relu_fwd",
     "pgcn_relu_bwd", "pgcn_xent_blocks", "pgcn_xent_fwd", "pgcn_finalize", "pgcn_adam",
     "pgcn_adam_step_size", "pgcn_params_default", "pgcn_gcn_create", "pgcn_comm_unique_id",
     "pgcn_gcn_create_dist", "pgcn_gcn_create_peer", "pgcn_loopback_create",
@@ -562,5 +556,4 @@ EXPORTED = [
     "pgcn_dataset_free", "pgcn_partition_bounds", "pgcn_partition_subgraph", "pgcn_debug_set",
     "pgcn_debug_lds_check", "pgcn_debug_lds_counts", "pgcn_debug_path_count",
     "pgcn_debug_empty_launches", "pgcn_debug_exp_check", "pgcn_debug_div_check",
-    "pgcn_debug_dropout_mask_side", "pgcn_debug_mask_nibbles_side",
 ]

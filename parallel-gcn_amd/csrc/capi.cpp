@@ -24,8 +24,6 @@ extern int g_split_cols;            // host/gcn.cpp
 extern int g_fuse_epilogue;         // host/gcn.cpp
 extern int g_fuse_output;           // host/gcn.cpp
 extern int g_mm_side;               // host/gcn.cpp
-extern int g_mask_side;             // host/gcn.cpp
-extern int g_mask_group;            // host/gcn.cpp
 extern int g_eval_ax;               // host/gcn.cpp
 extern int g_epoch_graph;           // host/gcn.cpp
 extern long long g_lds_min_bytes;   // host/graph.cpp
@@ -325,40 +323,8 @@ int pgcn_dropout_mask(uint64_t *chunk_states, long long n_chunks, long long n_el
                       long long elem0, float p, uint64_t *mask, const void *dev_jump_table,
                       void *stream) {
   return guarded([&] {
-    launch_dropout_mask(chunk_states, n_chunks, 1, elem0, n_elems, p, mask, dev_jump_table,
+    launch_dropout_mask(chunk_states, n_chunks, elem0, n_elems, p, mask, dev_jump_table,
                         as_stream(stream));
-    PGCN_HIP(hipGetLastError());
-  });
-}
-
-int pgcn_dropout_mask_groups(uint64_t *group_states, long long n_chunks, int group,
-                             long long n_elems, long long elem0, float p, uint64_t *mask,
-                             const void *dev_jump_table, void *stream) {
-  return guarded([&] {
-    PGCN_CHECK(group >= 1, PGCN_E_INVALID, "dropout_mask_groups: group >= 1");
-    launch_dropout_mask(group_states, n_chunks, group, elem0, n_elems, p, mask, dev_jump_table,
-                        as_stream(stream));
-    PGCN_HIP(hipGetLastError());
-  });
-}
-
-int pgcn_debug_dropout_mask_side(uint64_t *group_states, long long n_chunks, int group,
-                                 long long n_elems, long long elem0, float p, uint64_t *mask,
-                                 const void *dev_jump_table, int blocks, void *stream) {
-  return guarded([&] {
-    PGCN_CHECK(blocks > 0 && group >= 1, PGCN_E_INVALID, "dropout_mask_side: blocks, group");
-    launch_dropout_mask(group_states, n_chunks, group, elem0, n_elems, p, mask, dev_jump_table,
-                        as_stream(stream), 0, blocks);
-    PGCN_HIP(hipGetLastError());
-  });
-}
-
-int pgcn_debug_mask_nibbles_side(const uint64_t *mask, long long mask_base, long long mask_ld,
-                                 int M, int K, uint64_t *out, int blocks, void *stream) {
-  return guarded([&] {
-    PGCN_CHECK(mask && out && M >= 0 && K > 0 && blocks > 0, PGCN_E_INVALID,
-               "mask_nibbles_side args");
-    launch_mask_nibbles(mask, mask_base, mask_ld, M, K, out, as_stream(stream), blocks);
     PGCN_HIP(hipGetLastError());
   });
 }
@@ -718,12 +684,6 @@ int pgcn_debug_set(const char *key, int value) {
   } else if (!std::strcmp(key, "mm_side")) {
     if (!in(0, 2)) return PGCN_E_INVALID;
     pgcn::g_mm_side = value;
-  } else if (!std::strcmp(key, "mask_side")) {
-    if (!in(0, 4)) return PGCN_E_INVALID;
-    pgcn::g_mask_side = value;
-  } else if (!std::strcmp(key, "mask_group")) {
-    if (!in(0, 64)) return PGCN_E_INVALID;
-    pgcn::g_mask_group = value;
   } else if (!std::strcmp(key, "xstream_ring")) {
     if (!in(0, 1)) return PGCN_E_INVALID;
     pgcn::g_xstream_ring = value;

@@ -59,12 +59,6 @@ int g_sparse_dual = 1;
 // stream hand-offs cost more than the ~7 us of kernels they hide)
 int g_mm_side = 0;
 constexpr int kMmSideRows = 65536;
-// "mask_side" (read at engine build): workgroups per CU of the side-stream draw of the next
-// input mask (ModuleContext::mask_side; dense X on the X-stream path); 0 = off
-int g_mask_side = 0;
-// "mask_group" (read at engine build): chunks per dropout state (DropoutRng::group); 0 = by
-// mask size (mask_group in kernels.hpp)
-int g_mask_group = 0;
 
 // ------------------------------------------------------------------------------------------
 // Adam (src/optim.cu:7-95; hpdga optim.cpp:16-35)
@@ -219,10 +213,9 @@ void build_dev_features(DevFeatures &feats, const int *fptr, const int *indices,
   }
 }
 
-// States of a dropout over global elements [elem_begin, elem_end) whose first training
+// Chunk states of a dropout over global elements [elem_begin, elem_end) whose first training
 // forward draws stream positions offset + element (hpdga: one xorshift128+ draw per element,
-// module.cpp:208-219): the state at the first draw of every group of r.group 64-element chunks
-// (the rank's chunks counted from its first), jumped to from the seed state.
+// module.cpp:208-219), each 64-element chunk's state jumped to from the seed state.
 void init_dropout_rng_range(DropoutRng &r, const uint64_t seed[2], unsigned long long offset,
                             long long elem_begin, long long elem_end) {
   r.elem_begin = elem_begin;
@@ -231,19 +224,15 @@ void init_dropout_rng_range(DropoutRng &r, const uint64_t seed[2], unsigned long
   const long long chunk_hi = ceil_div(r.elem_end, kDropChunk);
   r.n_chunks = std::max(0LL, chunk_hi - r.chunk_lo);
   r.mask_base = r.elem_begin - kDropChunk * r.chunk_lo;
-  r.group = g_mask_group > 0 ? g_mask_group : mask_group(r.n_chunks);
-  const long long n_groups = ceil_div(r.n_chunks, (long long)r.group);
-  std::vector<uint64_t> st((size_t)std::max(1LL, n_groups) * 2, 0);
+  std::vector<uint64_t> st((size_t)std::max(1LL, r.n_chunks) * 2, 0);
   const unsigned long long base = offset + (unsigned long long)kDropChunk * r.chunk_lo;
-  const unsigned long long step = (unsigned long long)kDropChunk * r.group;
-  parallel_for(n_groups, [&](long long b, long long e) {
+  parallel_for(r.n_chunks, [&](long long b, long long e) {
     uint64_t s[2] = {seed[0], seed[1]};
-    xs_jump(s, base + step * b);
-    for (long long q = b; q < e; q++) {
-      st[(size_t)q * 2] = s[0];
-      st[(size_t)q * 2 + 1] = s[1];
-      if (q + 1 < e)
-        for (unsigned long long k = 0; k < step; k++) xs_advance(s);
+    xs_jump(s, base + (unsigned long long)kDropChunk * b);
+    for (long long c = b; c < e; c++) {
+      st[(size_t)c * 2] = s[0];
+      st[(size_t)c * 2 + 1] = s[1];
+      for (int k = 0; k < kDropChunk; k++) xs_advance(s);
     }
   });
   r.states.allocate(st.size());
@@ -499,11 +488,6 @@ void GCN::build(const GCNData &data) {
     ctx.side_join = Event::create();
   }
   ctx.train_ahead = g_train_ahead != 0;
-  if (g_mask_side > 0) {
-    ctx.mask_side = g_mask_side;
-    ctx.mask_fork = Event::create();
-    ctx.mask_ready = Event::create();
-  }
   ctx.xent_partials = xent_partials.get();
   ctx.xent_blocks = xent_blocks(prow);
   ctx.gemm_workspace = gemm_ws.get();
@@ -905,7 +889,6 @@ void GCN::enqueue_epoch(bool graph) {
 // eval and the next training forward).
 bool GCN::graph_eligible() const {
   if (!g_epoch_graph || !warm || comm || ctx.profile) return false;
-  if (ctx.mask_side) return false;  // (an ahead draw on the side stream between epochs)
   if (ctx.train_ahead && feats.dense && feats.maskT && !feats.ax) return false;
   if (ctx.train_ahead && !feats.dense && g_sparse_dual) return false;  // (the same host swaps)
   return true;

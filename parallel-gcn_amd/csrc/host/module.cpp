@@ -61,10 +61,10 @@ Dropout::Dropout(shared_ptr<Variable> in_, float p_, shared_ptr<DropoutRng> rng_
                  ModuleContext *ctx_)
     : in(std::move(in_)), rng(std::move(rng_)), p(p_), ctx(ctx_) {}
 
-void Dropout::draw(hipStream_t s, uint64_t *mask, int max_blocks, int side_blocks) const {
+void Dropout::draw(hipStream_t s, uint64_t *mask, int max_blocks) const {
   const DropoutRng &r = *rng;
-  launch_dropout_mask(r.states.get(), r.n_chunks, r.group, 64 * r.chunk_lo, r.elem_end, p, mask,
-                      ctx->jump_table, s, max_blocks, side_blocks);
+  launch_dropout_mask(r.states.get(), r.n_chunks, 64 * r.chunk_lo, r.elem_end, p, mask,
+                      ctx->jump_table, s, max_blocks);
 }
 
 void Dropout::draw_ahead(hipStream_t s, const Event *ready) const {
@@ -78,16 +78,14 @@ void Dropout::draw_ahead(hipStream_t s, const Event *ready) const {
     // with the hidden dropout's next mask (co_draw; the eval forward uses neither)
     const DropoutRng &r = *rng, &q = co_draw->state();
     const MaskDraw a{r.states.get(), r.n_chunks, 64 * r.chunk_lo, r.elem_end, p,
-                     rng->mask_ahead.get(), r.group};
+                     rng->mask_ahead.get()};
     const MaskDraw b{q.states.get(), q.n_chunks, 64 * q.chunk_lo, q.elem_end, co_draw->p,
-                     q.mask.get(), q.group};
+                     q.mask.get()};
     launch_dropout_mask2(a, b, ctx->jump_table, s);
     co_draw->pre_drawn = true;
-  } else if (ready) {
-    // on the side stream: the LDS-free form on mask_side workgroups per CU (SparseMatmul)
-    draw(s, rng->mask_ahead.get(), 0, std::max(1, ctx->mask_side) * kCUs);
   } else {
-    draw(s, rng->mask_ahead.get());
+    // on a side stream: two workgroups per CU, leaving room for the main stream's kernels
+    draw(s, rng->mask_ahead.get(), ready ? 2 * kCUs : 0);
   }
   if (ready) ready->record(s);
   ahead_ready = ready;
@@ -125,10 +123,9 @@ void Dropout::forward(bool training, const Stream &s) const {
     pre_drawn = false;
   } else if (co_draw && !co_draw->pre_drawn && !co_draw->ahead) {
     const DropoutRng &q = co_draw->state();
-    const MaskDraw a{r.states.get(), r.n_chunks, 64 * r.chunk_lo, r.elem_end, p, r.mask.get(),
-                     r.group};
+    const MaskDraw a{r.states.get(), r.n_chunks, 64 * r.chunk_lo, r.elem_end, p, r.mask.get()};
     const MaskDraw b{q.states.get(), q.n_chunks, 64 * q.chunk_lo, q.elem_end, co_draw->p,
-                     q.mask.get(), q.group};
+                     q.mask.get()};
     launch_dropout_mask2(a, b, ctx->jump_table, s.get());
     co_draw->pre_drawn = true;
   } else {
@@ -220,29 +217,24 @@ void SparseMatmul::forward(bool training, const Stream &s) const {
     else
       drop->draw_ahead(s.get());
     const uint64_t *m = drop->mask_ahead();
-    launch_mask_nibbles(m, base, x->cols, x->rows, x->cols, nib(), s.get());
+    launch_mask_nibbles(m, base, x->cols, x->rows, x->cols, x->maskT.get(), s.get());
     launch_xstream_nn(x->rows, b->cols, x->cols, x->x.get(), x->ldx, b->dev_data.get(), b->ld, 0,
-                      c->dev_data.get(), c->ld, nib(), scale, s.get(), ahead.get());
+                      c->dev_data.get(), c->ld, x->maskT.get(), scale, s.get(), ahead.get());
     ahead_valid = true;
     return;
   }
   MmProfile prof(ctx, s.get(), x->dense ? 2.0 * x->rows * b->cols * x->cols : 0.0);
   if (x->dense && x->maskT) {  // X-stream kernels (N <= 16, K <= 640)
-    if (mask && nib_next) {  // built on the side stream (Dropout::forward waited for it)
-      nib_flip = !nib_flip;
-      nib_next = false;
-    } else if (mask) {
-      launch_mask_nibbles(mask, base, x->cols, x->rows, x->cols, nib(), s.get());
-    }
+    if (mask)
+      launch_mask_nibbles(mask, base, x->cols, x->rows, x->cols, x->maskT.get(), s.get());
     XsEpilogue e;  // the first GraphSum's prescaled input, written beside c
     if ((g_fuse_epilogue & kFuseXstream) && consumer && (training || !eval_out)) {
       e.next_table = consumer->claim_forward_table(x->rows, c->ld, &e.next_scale);
       e.next_sr = RING_SR;
     }
     launch_xstream_nn(x->rows, b->cols, x->cols, x->x.get(), x->ldx, b->dev_data.get(), b->ld, 0,
-                      c->dev_data.get(), c->ld, mask ? nib() : nullptr, scale, s.get(),
+                      c->dev_data.get(), c->ld, mask ? x->maskT.get() : nullptr, scale, s.get(),
                       nullptr, &e);
-    if (mask && ctx->mask_side && !drop->drawn_ahead()) launch_side_mask(s);
   } else if (x->dense) {
     // wide outputs: the mask in the nibble layout too (one pass over the bitmap; the wide
     // kernels then read one word per row and 4 steps, and the backward reuses it)
@@ -257,29 +249,6 @@ void SparseMatmul::forward(bool training, const Stream &s) const {
   }
 }
 
-// mask_side: the next training forward's input mask on the side stream, beside the GraphSums
-// that follow this forward's X-stream product.  Its flat bitmap buffer was last read by the
-// nibble build of the mask before this one, the chunk states by this mask's draw, both ahead
-// of this point; with eval_ax (eval never builds nibble words then) its nibble words follow
-// into the buffer this epoch does not read -- the last reader of that one, the previous
-// epoch's weight-gradient pass, is ahead of the fork too.
-void SparseMatmul::launch_side_mask(const Stream &s) const {
-  hipStream_t side = ctx->side_stream;
-  ctx->mask_fork.record(s.get());
-  ctx->mask_fork.wait_on(side);
-  drop->draw_ahead(side, &ctx->mask_ready);
-  if (x->ax && eval_out) {
-    if (!nib_alt) {
-      nib_alt.allocate(x->maskT.size());
-      nib_alt.zero();
-    }
-    launch_mask_nibbles(drop->mask_ahead(), drop->state().mask_base, x->cols, x->rows, x->cols,
-                        nib_other(), side, ctx->mask_side * kCUs);
-    ctx->mask_ready.record(side);  // the forward's wait_ahead then covers the nibbles too
-    nib_next = true;
-  }
-}
-
 void SparseMatmul::backward(const Stream &s) const {
   // b.grad = drop(X)^T * c.grad  (the dropped X of the last training forward)
   const uint64_t *mask = last_training ? drop->state().mask.get() : nullptr;
@@ -288,7 +257,7 @@ void SparseMatmul::backward(const Stream &s) const {
   MmProfile prof(ctx, s.get(), x->dense ? 2.0 * x->rows * b->cols * x->cols : 0.0);
   if (x->dense && x->maskT) {  // the nibble mask of the last training forward
     launch_xstream_tn(x->rows, b->cols, x->cols, x->x.get(), x->ldx, c->dev_grad.get(), c->ld,
-                      b->dev_grad.get(), b->ld, mask ? nib() : nullptr, scale,
+                      b->dev_grad.get(), b->ld, mask ? x->maskT.get() : nullptr, scale,
                       ctx->gemm_workspace, s.get());
   } else if (x->dense) {
     launch_gemm_tn(x->rows, b->cols, x->cols, x->x.get(), x->ldx, c->dev_grad.get(), c->ld,

@@ -67,11 +67,10 @@ struct DevFeatures {
 
 // Dropout mask + xorshift chunk states for one Dropout module on this rank.
 struct DropoutRng {
-  DeviceBuffer<uint64_t> states;  // 2 per group of `group` chunks
+  DeviceBuffer<uint64_t> states;  // 2 per chunk
   DeviceBuffer<uint64_t> mask;    // 1 word per chunk: the last training forward's mask
   DeviceBuffer<uint64_t> mask_ahead;  // the next one, when drawn ahead (input dropout)
   long long chunk_lo = 0, n_chunks = 0;
-  int group = 1;  // chunks per state (r05: mask_group, so the period jumps fall per group)
   long long elem_begin = 0, elem_end = 0;  // global element range of this rank
   long long mask_base = 0;                 // bit of local element 0 in `mask`
 };
@@ -102,12 +101,6 @@ struct ModuleContext {
   // weight-gradient pass, the eval forward's X-stream product or its output layer -- the RNG
   // kernel and the pass beside it slow each other down, DESIGN.md §3 "Streams")
   hipStream_t side_stream = nullptr;  // mm_side's stream
-  // "mask_side" (r05): the NEXT input mask drawn on side_stream right after the training
-  // forward's X-stream product, by the LDS-free k_dropout_mask_side on mask_side workgroups
-  // per CU, so it runs beside the ring GraphSums (one LDS-bound workgroup per CU) in their
-  // VALU idle cycles; 0 = drawn on the stream at the forward
-  int mask_side = 0;
-  Event mask_fork, mask_ready;
   // "mm_side": a Matmul's weight gradient (b.grad = a^T c.grad, needed only by the optimizer)
   // runs on side_stream beside the rest of the backward pass (the reference's S2/S3 streams,
   // src/module.cu:445-472); GCN joins it (side_join) before the all-reduce / optimizer
@@ -200,7 +193,7 @@ class Dropout : public Module {
   mutable bool pre_drawn = false;
 
  private:
-  void draw(hipStream_t s, uint64_t *mask, int max_blocks = 0, int side_blocks = 0) const;
+  void draw(hipStream_t s, uint64_t *mask, int max_blocks = 0) const;
   mutable bool ahead = false;
   mutable const Event *ahead_ready = nullptr;  // recorded after an ahead draw on a side stream
 };
@@ -217,18 +210,6 @@ class SparseMatmul : public Module {
   // that forward then swaps in instead of streaming X again
   mutable DeviceBuffer<float> ahead;
   mutable bool ahead_valid = false;
-  // mask_side with eval_ax: the next mask's nibble words are built on the side stream too,
-  // into the other of two nibble buffers (x->maskT / nib_alt; the current one is read by this
-  // epoch's backward meanwhile); the next training forward flips to it
-  mutable DeviceBuffer<uint64_t> nib_alt;
-  mutable bool nib_flip = false, nib_next = false;
-  uint64_t *nib() const {
-    return nib_flip ? nib_alt.get() : const_cast<uint64_t *>(x->maskT.get());
-  }
-  uint64_t *nib_other() const {
-    return nib_flip ? const_cast<uint64_t *>(x->maskT.get()) : nib_alt.get();
-  }
-  void launch_side_mask(const Stream &s) const;
 
  public:
   SparseMatmul(const DevFeatures *x_, shared_ptr<Variable> b_, shared_ptr<Variable> c_,

@@ -80,31 +80,16 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   asm("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a) : "v"(b), "v"(c));
   return a;
 }
-// Nibble table q, entry v: in LDS (built by the workgroup), or read straight out of the byte
-// tables in global memory (LDS-free draws beside the LDS-bound GraphSum: the 8 KB they touch
-// stay in the L1 / L2)
-struct LutLds {
-  const uint4 *lut;
-  __device__ __forceinline__ uint4 at(int q, uint32_t v) const { return lut[q * 16 + v]; }
-};
-struct LutGlobal {
-  const uint4 *__restrict__ table;
-  __device__ __forceinline__ uint4 at(int q, uint32_t v) const {
-    return table[(q >> 1) * 256 + (v << (4 * (q & 1)))];
-  }
-};
-
 // M^period (a0, a1) from the nibble tables: 32 lookups xor-ed, two per three-input xor
-template <class Lut>
-__device__ __forceinline__ uint64_t dmn_advance(const Lut &lut, uint64_t a0, uint64_t a1,
+__device__ __forceinline__ uint64_t dmn_advance(const uint4 *lut, uint64_t a0, uint64_t a1,
                                                 uint64_t &n1) {
   uint4 n = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
   for (int q = 0; q < 32; q += 2) {
     const uint64_t a = q < 16 ? a0 : a1;
     const int sh = 4 * (q & 15);
-    const uint4 v = lut.at(q, (uint32_t)(a >> sh) & 0xf);
-    const uint4 w = lut.at(q + 1, (uint32_t)(a >> (sh + 4)) & 0xf);
+    const uint4 v = lut[q * 16 + ((a >> sh) & 0xf)];
+    const uint4 w = lut[(q + 1) * 16 + ((a >> (sh + 4)) & 0xf)];
     n.x = xor3(n.x, v.x, w.x);
     n.y = xor3(n.y, v.y, w.y);
     n.z = xor3(n.z, v.z, w.z);
@@ -116,76 +101,58 @@ __device__ __forceinline__ uint64_t dmn_advance(const Lut &lut, uint64_t a0, uin
 
 // One launch draws one or two variables' masks (MaskSeg b: the small graphs' hidden dropout
 // drawn beside the input's, r04 late: one launch fewer per epoch); workgroups [0, blocks_a)
-// take segment a, the rest segment b.  Every variable's states advance by the same period (the
-// whole epoch's draws), so one jump table serves both.
-//
-// r05: one state per GROUP of `group` consecutive chunks.  Chunk c + 1's draws continue the
-// stream where chunk c's end, so a thread draws its group's chunks one after another from the
-// group's first state and jumps only that state by the period: the table lookups (32 per jump)
-// fall from one set per chunk to one per group -- on reddit's input mask 1.1 GB of lookups per
-// draw at group 1.  The host picks the group so that enough threads remain (DropoutRng).
+// take segment a, the rest segment b.  Every variable's chunk states advance by the same
+// period (the whole epoch's draws), so one jump table serves both.
 struct MaskSeg {
   uint64_t *states = nullptr;
   long long n_chunks = 0, elem0 = 0, elem_end = 0;
   int threshold = 0;
   uint64_t *mask = nullptr;
-  int group = 1;
 };
 
-template <class Lut>
-__device__ __forceinline__ void dropout_mask_seg(const MaskSeg &sg, const Lut &lut, long long bid,
+__device__ __forceinline__ void dropout_mask_seg(const MaskSeg &sg, const uint4 *lut, long long bid,
                                                  long long nblk) {
   uint64_t *__restrict__ states = sg.states;
   uint64_t *__restrict__ mask = sg.mask;
   const long long n_chunks = sg.n_chunks, elem0 = sg.elem0, elem_end = sg.elem_end;
-  const int threshold = sg.threshold, grp = sg.group;
-  const long long n_groups = (n_chunks + grp - 1) / grp;
-  // mask word of chunk c (bits past elem_end cleared)
-  auto put = [&](long long c, uint64_t word) {
+  const int threshold = sg.threshold;
+  // mask word of chunk c, then its state advanced by `period` draws: M^period * (a0, a1)
+  auto emit = [&](long long c, uint64_t a0, uint64_t a1, uint64_t word) {
     const long long e = elem0 + 64 * c;  // first element of this chunk
     if (e + 64 > elem_end) {
       const long long valid = elem_end - e;
       word = valid <= 0 ? 0 : (word & ((valid >= 64) ? ~0ull : ((1ull << valid) - 1)));
     }
     mask[c] = word;
-  };
-  // group q's state advanced by `period` draws for the next epoch: M^period * (a0, a1)
-  auto advance = [&](long long q, uint64_t a0, uint64_t a1) {
     uint64_t n1;
     const uint64_t n0 = dmn_advance(lut, a0, a1, n1);
-    states[2 * q] = n0;
-    states[2 * q + 1] = n1;
+    states[2 * c] = n0;
+    states[2 * c + 1] = n1;
   };
-  // two groups per thread and iteration: two independent xorshift chains interleaved (each
+  // two chunks per thread and iteration: two independent xorshift chains interleaved (each
   // draw is a serial chain of 64-bit ops; the pair hides their latency at low occupancy)
   const long long G = nblk * blockDim.x;
-  for (long long q = bid * blockDim.x + threadIdx.x; q < n_groups; q += 2 * G) {
-    const long long q2 = q + G;
-    const bool two = q2 < n_groups;
-    const long long qb = two ? q2 : q;
-    const uint64_t a0 = states[2 * q], a1 = states[2 * q + 1];
-    const uint64_t b0 = states[2 * qb], b1 = states[2 * qb + 1];
+  for (long long c = bid * blockDim.x + threadIdx.x; c < n_chunks; c += 2 * G) {
+    const long long c2 = c + G;
+    const bool two = c2 < n_chunks;
+    const long long cb = two ? c2 : c;
+    const uint64_t a0 = states[2 * c], a1 = states[2 * c + 1];
+    const uint64_t b0 = states[2 * cb], b1 = states[2 * cb + 1];
     Xs64 x{a0, a1}, y{b0, b1};
     x.thr2 = y.thr2 = (uint32_t)threshold << 1;
-    for (int k = 0; k < grp; k++) {
-      x.lo = x.hi = y.lo = y.hi = 0;
 #pragma unroll
-      for (int j = 0; j < 64; j++) {
-        x.step(j, threshold);
-        y.step(j, threshold);
-      }
-#if PGCN_DROP_SHIFTIN
-      x.lo = __builtin_bitreverse32(x.lo);
-      x.hi = __builtin_bitreverse32(x.hi);
-      y.lo = __builtin_bitreverse32(y.lo);
-      y.hi = __builtin_bitreverse32(y.hi);
-#endif
-      const long long c = q * grp + k, c2 = qb * grp + k;
-      if (c < n_chunks) put(c, ((uint64_t)x.hi << 32) | x.lo);
-      if (two && c2 < n_chunks) put(c2, ((uint64_t)y.hi << 32) | y.lo);
+    for (int j = 0; j < 64; j++) {
+      x.step(j, threshold);
+      y.step(j, threshold);
     }
-    advance(q, a0, a1);
-    if (two) advance(q2, b0, b1);
+#if PGCN_DROP_SHIFTIN
+    x.lo = __builtin_bitreverse32(x.lo);
+    x.hi = __builtin_bitreverse32(x.hi);
+    y.lo = __builtin_bitreverse32(y.lo);
+    y.hi = __builtin_bitreverse32(y.hi);
+#endif
+    emit(c, a0, a1, ((uint64_t)x.hi << 32) | x.lo);
+    if (two) emit(c2, b0, b1, ((uint64_t)y.hi << 32) | y.lo);
   }
 }
 
@@ -197,20 +164,10 @@ __global__ __launch_bounds__(256) void k_dropout_mask(MaskSeg a, MaskSeg b, int 
     lut[i] = table[(p >> 1) * 256 + (v << (4 * (p & 1)))];
   }
   __syncthreads();
-  const LutLds l{lut};
   if ((int)blockIdx.x < blocks_a)
-    dropout_mask_seg(a, l, blockIdx.x, blocks_a);
+    dropout_mask_seg(a, lut, blockIdx.x, blocks_a);
   else
-    dropout_mask_seg(b, l, blockIdx.x - blocks_a, gridDim.x - blocks_a);
-}
-
-// The same draws without LDS (one variable): a side-stream draw whose workgroups fit beside the
-// ring GraphSum's (which holds ~159 KB of a CU's 160 KB LDS) and fill its VALU idle cycles.
-// At most 64 VGPRs (51 used): two of these workgroups and the ring's 16 waves of 96 fit a CU's
-// 512 per SIMD, so a workgroup already resident never keeps the next ring launch off its CU
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_dropout_mask_side(
-    MaskSeg a, const uint4 *__restrict__ table) {
-  dropout_mask_seg(a, LutGlobal{table}, blockIdx.x, gridDim.x);
+    dropout_mask_seg(b, lut, blockIdx.x - blocks_a, gridDim.x - blocks_a);
 }
 
 // x[i] *= bit(base + i) ? scale : 0   (Dropout::forward on a grad-carrying variable and
@@ -870,14 +827,14 @@ static int grid_for(long long work, int block = 256, int cap = 2048) {
   return (int)(g > cap ? cap : g);
 }
 
-void launch_dropout_mask(uint64_t *states, long long n_chunks, int group, long long elem0,
+void launch_dropout_mask(uint64_t *states, long long n_chunks, long long elem0,
                          long long elem_end, float p, uint64_t *mask, const void *table,
-                         hipStream_t s, int max_blocks, int side_blocks) {
+                         hipStream_t s, int max_blocks) {
   if (n_chunks <= 0) return;
-  PGCN_CHECK(group >= 1, PGCN_E_INVALID, "dropout_mask: group >= 1");
   // hpdga module.cpp:211: threshold = int(p * MY_RAND_MAX) evaluated in float
   const int threshold = (int)(p * (float)0x7fffffff);
-  const long long pairs = ceil_div(ceil_div(n_chunks, group), 2);  // threads with work
+  // 8 KB LDS: up to 8 workgroups per CU (a side-stream draw takes fewer: max_blocks)
+  const int grid = grid_for(ceil_div(n_chunks, 2), 256, max_blocks > 0 ? max_blocks : 8 * kCUs);
   MaskSeg a;
   a.states = states;
   a.n_chunks = n_chunks;
@@ -885,14 +842,6 @@ void launch_dropout_mask(uint64_t *states, long long n_chunks, int group, long l
   a.elem_end = elem_end;
   a.threshold = threshold;
   a.mask = mask;
-  a.group = group;
-  if (side_blocks > 0) {
-    PGCN_LAUNCH(k_dropout_mask_side, dim3(grid_for(pairs, 256, side_blocks)), dim3(256), 0, s, a,
-                static_cast<const uint4 *>(table));
-    return;
-  }
-  // 8 KB LDS: up to 8 workgroups per CU (max_blocks: fewer)
-  const int grid = grid_for(pairs, 256, max_blocks > 0 ? max_blocks : 8 * kCUs);
   PGCN_LAUNCH(k_dropout_mask, dim3(grid), dim3(256), 0, s, a, MaskSeg{}, grid,
               static_cast<const uint4 *>(table));
 }
@@ -903,17 +852,13 @@ void launch_dropout_mask2(const MaskDraw &d0, const MaskDraw &d1, const void *ta
   int g[2];
   const MaskDraw *d[2] = {&d0, &d1};
   for (int i = 0; i < 2; i++) {
-    PGCN_CHECK(d[i]->group >= 1, PGCN_E_INVALID, "dropout_mask2: group >= 1");
     sg[i].states = d[i]->states;
     sg[i].n_chunks = d[i]->n_chunks;
     sg[i].elem0 = d[i]->elem0;
     sg[i].elem_end = d[i]->elem_end;
     sg[i].threshold = (int)(d[i]->p * (float)0x7fffffff);  // as launch_dropout_mask
     sg[i].mask = d[i]->mask;
-    sg[i].group = d[i]->group;
-    g[i] = sg[i].n_chunks > 0
-               ? grid_for(ceil_div(ceil_div(sg[i].n_chunks, sg[i].group), 2), 256, 8 * kCUs)
-               : 0;
+    g[i] = sg[i].n_chunks > 0 ? grid_for(ceil_div(sg[i].n_chunks, 2), 256, 8 * kCUs) : 0;
   }
   if (g[0] + g[1] == 0) return;
   PGCN_LAUNCH(k_dropout_mask, dim3(g[0] + g[1]), dim3(256), 0, s, sg[0], sg[1], g[0],

@@ -176,40 +176,6 @@ __global__ __launch_bounds__(256) void k_mask_nibbles(const uint64_t *__restrict
   out[(m0 + r) * 16 + j] = word;
 }
 
-// The same words without LDS, grid-stride on a fixed grid (a side-stream build beside the ring
-// GraphSum, which leaves no LDS and must find its CUs free again at its next launch): thread
-// (row, j) reads its bitmap words straight from memory (the 16 threads of a row share them
-// through the L1).  A word index past the last element's word can only hold bits of k >= K of
-// the last row, which the K mask clears, so it is clamped instead of read past the bitmap.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_mask_nibbles_side(
-    const uint64_t *__restrict__ mask, long long mask_base, long long mask_ld, int M, int K,
-    uint64_t *__restrict__ out) {
-  const long long last = (mask_base + (long long)M * mask_ld - 1) >> 6;
-  for (long long t = (long long)blockIdx.x * 256 + threadIdx.x; t < 16LL * M;
-       t += (long long)gridDim.x * 256) {
-    const long long m = t >> 4;
-    const int j = (int)(t & 15);
-    const long long p0 = mask_base + m * mask_ld + 4 * j;
-    const long long w0 = p0 >> 6;
-    const int sh = (int)(p0 & 63);
-    const int nc = (K - 4 * j + 63) >> 6;
-    uint64_t word = 0, lo = mask[min(w0, last)];
-#pragma unroll
-    for (int c = 0; c < 16; c++) {
-      if (c < nc) {
-        const uint64_t hi = mask[min(w0 + c + 1, last)];
-        uint64_t nib = (lo >> sh) & 0xfu;
-        if (sh > 60) nib = (nib | (hi << (64 - sh))) & 0xfu;
-        const int kb = 64 * c + 4 * j;
-        if (kb + 4 > K) nib &= (1ull << (K - kb)) - 1;
-        word |= nib << (4 * c);
-        lo = hi;
-      }
-    }
-    out[t] = word;
-  }
-}
-
 // NN: Z[M][N<=16] = drop(X) W.  A wave owns a 16-row group at a time (grid-stride over
 // groups) and issues all of the group's A loads (one float4 per lane per 16-wide k-step:
 // lane (i, g) reads X[row i][16 s + 4 g ..]) before its first MFMA; 2 waves per SIMD keep one
@@ -636,16 +602,10 @@ static int xs_stride(int K) {  // LDS row stride of B^T: >= 64*KC, = 8 mod 16 dw
 }
 
 void launch_mask_nibbles(const uint64_t *mask, long long mask_base, long long mask_ld, int M,
-                         int K, uint64_t *out, hipStream_t s, int side_blocks) {
+                         int K, uint64_t *out, hipStream_t s) {
   PGCN_CHECK(K >= 1 && K <= 1024, PGCN_E_INVALID, "mask_nibbles: K must be in [1,1024]");
   if (M <= 0) return;
   PGCN_CHECK(mask_ld >= K && mask_ld <= 1024, PGCN_E_INVALID, "mask_nibbles: K <= mask_ld <= 1024");
-  if (side_blocks > 0) {
-    const long long g = std::min<long long>(side_blocks, ceil_div(16LL * M, 256));
-    PGCN_LAUNCH(k_mask_nibbles_side, dim3((unsigned)g), dim3(256), 0, s, mask, mask_base, mask_ld,
-                M, K, out);
-    return;
-  }
   PGCN_LAUNCH(k_mask_nibbles, dim3((unsigned)ceil_div(M, NIB_ROWS)), dim3(256), 0, s, mask,
                      mask_base, mask_ld, M, K, out);
 }

@@ -148,10 +148,8 @@ void launch_slab_reduce(float *partial, int n_slabs, int K, int N, int ldp, floa
                         int nst, hipStream_t s);
 // X-stream kernels (k_gemm.hip): N <= 16, K <= 640, dropout bits in the nibble layout
 bool xstream_ok(int N, int K);
-// side_blocks > 0: the LDS-free grid-stride form on at most that many workgroups (the same
-// words), for a build beside the ring GraphSum
 void launch_mask_nibbles(const uint64_t *mask, long long mask_base, long long mask_ld, int M,
-                         int K, uint64_t *out, hipStream_t s, int side_blocks = 0);
+                         int K, uint64_t *out, hipStream_t s);
 // What the first layer's X-stream product feeds (single C output, N <= 16): relu = the ReLU
 // of the GraphSum it stands for (eval from Â X; no mask: eval only), next_table = that
 // GraphSum's or the next one's prescaled ring table (next_scale[r] * value at the ring
@@ -215,8 +213,12 @@ void launch_peer_push(const float *send, size_t count, const PeerSink &k, hipStr
 void launch_peer_wait(const unsigned *flags, int world, unsigned gen, unsigned *err,
                       hipStream_t s);
 // one workgroup: push buf [n] to every receiver, signal, wait for waited[q < nwait], sum the
-// received slots in rank order back into buf (separate processes only: see k_peer.hip)
-constexpr int kPeerSmallAllreduce = 1 << 16;
+// received slots in rank order back into buf (separate processes only: see k_peer.hip).
+// Up to 1,024 floats (the loss / wrong-count pairs): the weight gradients (10.3 k floats on
+// reddit) took 51 us in one workgroup at W = 8 (its write-through pushes run at one
+// workgroup's rate, profiles/r05/g/rank8_breakdown.txt) against ~15 us for the three-kernel
+// form's whole-grid push, wait and sum
+constexpr int kPeerSmallAllreduce = 1 << 10;
 void launch_peer_allreduce_small(float *buf, int n, const PeerSink &k, const PeerRecv &r,
                                  const unsigned *waited, int nwait, unsigned *err, hipStream_t s);
 // dst[i] = sum over q (rank order) of r.slot[q][i]
@@ -251,29 +253,16 @@ void launch_spmm_csc_bwd(int nf, int p, int ldg, const int *csc_ptr, const int *
                          long long mask_base, float scale, const float *cgrad, float *bgrad,
                          hipStream_t s, long long nnz = 0);
 
-// Mask words of n_chunks 64-element chunks from one xorshift128+ state per `group` chunks
-// (states[2q], states[2q + 1]: the state at chunk q * group's first draw), each state then
-// jumped by the table's period.  side_blocks > 0: the LDS-free form on at most that many
-// workgroups (k_dropout_mask_side, the same bits), for a draw beside the ring GraphSum
-void launch_dropout_mask(uint64_t *states, long long n_chunks, int group, long long elem0,
+void launch_dropout_mask(uint64_t *states, long long n_chunks, long long elem0,
                          long long elem_end, float p, uint64_t *mask, const void *table,
-                         hipStream_t s, int max_blocks = 0, int side_blocks = 0);
+                         hipStream_t s, int max_blocks = 0);
 // two variables' draws (each as launch_dropout_mask's arguments) in one launch
 struct MaskDraw {
   uint64_t *states;
   long long n_chunks, elem0, elem_end;
   float p;
   uint64_t *mask;
-  int group = 1;
 };
-// chunks per state for a mask of n_chunks chunks: the largest of 1, 2, 4, .. 32 that leaves at
-// least kMaskMinPairs threads (each draws two groups side by side)
-constexpr long long kMaskMinPairs = 65536;
-inline int mask_group(long long n_chunks) {
-  int g = 1;
-  while (g < 32 && n_chunks / (4LL * g) >= kMaskMinPairs) g *= 2;
-  return g;
-}
 void launch_dropout_mask2(const MaskDraw &d0, const MaskDraw &d1, const void *table,
                           hipStream_t s);
 void launch_dropout_apply_based(float *x, long long n, const uint64_t *mask, long long base,

@@ -318,60 +318,6 @@ def test_train_ahead_bit_identical(pgcn):
             np.testing.assert_array_equal(np.asarray(a, np.float32), np.asarray(b, np.float32))
 
 
-@pytest.mark.parametrize("eval_ax,train_ahead", [(1, 1), (0, 1), (0, 0)])
-def test_mask_side_bit_identical(pgcn, eval_ax, train_ahead):
-    """The next input mask drawn on the side stream by the LDS-free k_dropout_mask_side
-    (mask_side 1 and 2 workgroups per CU) right after the training forward's X-stream product:
-    the same bits as drawing it on the stream at the forward -- epoch lines (with an epoch
-    without eval and a repeated eval), async epochs, the dropped input the last training
-    forward saw (get_var 0) and W1; with eval_ax off and train-ahead on, eval's ahead product
-    uses the side-drawn mask."""
-    ds = pgcn.Dataset.synthetic(20000, 96, 8, 300000, 5)  # dense N(0,1) features
-    p = pgcn.make_params(ds)
-    runs = []
-    for side in (0, 1, 2):
-        with helpers.knobs(pgcn, mask_side=side, eval_ax=eval_ax, train_ahead=train_ahead):
-            g = pgcn.GCN(p, ds, device=0)
-            lines = []
-            for e in range(5):
-                lines.append(g.train_epoch())
-                if e == 2:
-                    lines.append(tuple(g.get_var(0).ravel()[:200000]))
-                if e != 3:
-                    lines.append(g.eval(2))
-                if e == 1:
-                    lines.append(g.eval(3))
-            for _ in range(3):
-                g.epoch_async()
-            lines.append(tuple(g.results(3).ravel()))
-            lines.append(tuple(g.get_var(2).ravel()))  # W1
-            runs.append(lines)
-            g.close()
-    for other in runs[1:]:
-        for a, b in zip(runs[0], other):
-            np.testing.assert_array_equal(np.asarray(a, np.float32), np.asarray(b, np.float32))
-
-
-def test_mask_group_bit_identical(pgcn):
-    """One dropout state per group of chunks (mask_group: 1, by size -- 2 on this 36 M-element
-    input mask -- and 5, a partial last group) draws the same masks: the same epoch lines,
-    dropped input and W1 after three epochs, with and without mask_side."""
-    ds = pgcn.Dataset.synthetic(60000, 602, 8, 600000, 9)
-    p = pgcn.make_params(ds)
-    runs = []
-    for group, side in ((1, 0), (0, 0), (5, 0), (0, 1)):
-        with helpers.knobs(pgcn, mask_group=group, mask_side=side):
-            g = pgcn.GCN(p, ds, device=0)
-            lines = [g.train_epoch() + g.eval(2) for _ in range(3)]
-            lines.append(tuple(g.get_var(0).ravel()[-300000:]))
-            lines.append(tuple(g.get_var(2).ravel()))
-            runs.append(lines)
-            g.close()
-    for other in runs[1:]:
-        for a, b in zip(runs[0], other):
-            np.testing.assert_array_equal(np.asarray(a, np.float32), np.asarray(b, np.float32))
-
-
 def test_split_rows_restriction_matches_all_rows(pgcn):
     """Output-layer row restriction (the last GraphSum's forward sums only the current split's
     labelled rows) on a graph that takes the LDS GraphSum path: the same losses, accuracies and

@@ -328,14 +328,9 @@ def mask_bits(mask_words, n):
     return b[:n].astype(bool)
 
 
-@pytest.mark.parametrize("side,group", [(0, 1), (0, 2), (0, 7), (0, 16), (0, 64), (3, 1),
-                                        (512, 1), (5, 16), (512, 9)])
-def test_dropout_masks_bit_exact(pgcn, side, group):
-    """Group states + GPU mask kernel reproduce the sequential xorshift128+ stream exactly,
-    across two 'epochs' (state advance by the period through the byte tables): one state per
-    `group` chunks (group 1: pgcn_dropout_mask; 7, 9: a partial last group, 1,563 chunks);
-    side > 0: the LDS-free side-stream kernel on that many workgroups (3, 5: many grid-stride
-    rounds)."""
+def test_dropout_masks_bit_exact(pgcn):
+    """Chunk states + GPU mask kernel reproduce the sequential xorshift128+ stream exactly,
+    across two 'epochs' (state advance by the period through the byte tables)."""
     lib = helpers.oracle()
     offset, n, period = 12345, 100_003, 250_007
     # sequential reference: draws offset .. offset+n (epoch 1) and offset+period .. (epoch 2)
@@ -346,27 +341,17 @@ def test_dropout_masks_bit_exact(pgcn, side, group):
     ref1 = seq[offset:offset + n] >= thr
     ref2 = seq[offset + period:offset + period + n] >= thr
     nch = (n + 63) // 64
-    ngr = (nch + group - 1) // group
-    states = np.zeros((ngr, 2), np.uint64)
+    states = np.zeros((nch, 2), np.uint64)
     st = pgcn.rng_jump(pgcn.rng_seed(), offset)
-    for q in range(ngr):
-        states[q] = st
-        st = pgcn.rng_jump(st, 64 * group)
+    for c in range(nch):
+        states[c] = st
+        st = pgcn.rng_jump(st, 64)
     table = torch.from_numpy(pgcn.rng_jump_table(period).view(np.int64)).to(DEV)
     dstates = torch.from_numpy(states.view(np.int64)).to(DEV)
     mask = torch.zeros(nch + 1, dtype=torch.int64, device=DEV)
     for ref in (ref1, ref2):
-        if side:
-            pgcn.check(pgcn.lib.pgcn_debug_dropout_mask_side(vp(dstates), nch, group, n, 0, 0.5,
-                                                             vp(mask), vp(table), side, stream()),
-                       "dropout_mask_side")
-        elif group == 1:
-            pgcn.check(pgcn.lib.pgcn_dropout_mask(vp(dstates), nch, n, 0, 0.5, vp(mask),
-                                                  vp(table), stream()), "dropout_mask")
-        else:
-            pgcn.check(pgcn.lib.pgcn_dropout_mask_groups(vp(dstates), nch, group, n, 0, 0.5,
-                                                         vp(mask), vp(table), stream()),
-                       "dropout_mask_groups")
+        pgcn.check(pgcn.lib.pgcn_dropout_mask(vp(dstates), nch, n, 0, 0.5, vp(mask), vp(table),
+                                              stream()), "dropout_mask")
         torch.cuda.synchronize()
         ours = mask_bits(mask.cpu().numpy()[:nch].view(np.uint64), n)
         np.testing.assert_array_equal(ours, ref)
@@ -498,14 +483,8 @@ def test_gemm_xstream(pgcn, M, N, K, base):
     nib = torch.empty((M, 16), dtype=torch.int64, device=DEV)
     pgcn.check(pgcn.lib.pgcn_mask_nibbles(vp(dm), base, K, M, K, vp(nib), stream()), "nib")
     torch.cuda.synchronize()
-    nib_ref = nibble_mask_ref(mask, base, M, K)
-    np.testing.assert_array_equal(nib.cpu().numpy().view(np.uint64), nib_ref)
-    for blocks in (1, 7, 256):  # the LDS-free side-stream form, grid-stride
-        nib2 = torch.full((M, 16), -1, dtype=torch.int64, device=DEV)
-        pgcn.check(pgcn.lib.pgcn_debug_mask_nibbles_side(vp(dm), base, K, M, K, vp(nib2), blocks,
-                                                         stream()), "nib_side")
-        torch.cuda.synchronize()
-        np.testing.assert_array_equal(nib2.cpu().numpy().view(np.uint64), nib_ref)
+    np.testing.assert_array_equal(nib.cpu().numpy().view(np.uint64),
+                                  nibble_mask_ref(mask, base, M, K))
     ldc = (N + 3) // 4 * 4
     ws = torch.empty(pgcn.lib.pgcn_gemm_tn_workspace(M, N, K) // 4 + 16, device=DEV)
     outs = {}
