@@ -392,18 +392,27 @@ void PeerComm::check() const {
                                  " did not signal rank " + std::to_string(rank_) + " in time");
 }
 
+bool PeerComm::small_allreduce(size_t n, PeerSmall *p) {
+  if (world_ == 1 || n == 0 || host_order_ || n > (size_t)kPeerSmallAllreduce) return false;
+  count(n * sizeof(float), 2.0);
+  p->k = sink(1, n);
+  p->r = recv();
+  p->waited = reinterpret_cast<const unsigned *>(header_) + (solo_ ? rank_ : 0);
+  p->nwait = solo_ ? 1 : world_;
+  p->err = reinterpret_cast<unsigned *>(header_ + kErrOff);
+  return true;
+}
+
 void PeerComm::allreduce_sum(float *buf, size_t n, hipStream_t s) {
+  PeerSmall p;
+  if (small_allreduce(n, &p)) {
+    // separate processes (or solo): push, wait and sum in one workgroup
+    launch_peer_allreduce_small(buf, (int)n, p.k, p.r, p.waited, p.nwait, p.err, s);
+    return;
+  }
   if (world_ == 1 || n == 0) return;
   count(n * sizeof(float), 2.0);
   PeerSink k = sink(1, n);
-  if (!host_order_ && n <= (size_t)kPeerSmallAllreduce) {
-    // separate processes (or solo): push, wait and sum in one workgroup
-    launch_peer_allreduce_small(buf, (int)n, k, recv(),
-                                reinterpret_cast<const unsigned *>(header_) + (solo_ ? rank_ : 0),
-                                solo_ ? 1 : world_, reinterpret_cast<unsigned *>(header_ + kErrOff),
-                                s);
-    return;
-  }
   // every receiver gets the same n floats: send[q * n ..) = buf for every q (stride 0)
   k.rows_per_rank = 0;
   launch_peer_push(buf, n, k, s, /*same_for_all=*/true);

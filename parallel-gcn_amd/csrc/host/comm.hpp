@@ -155,6 +155,10 @@ class PeerComm : public Comm {
   void wait(hipStream_t s);
   PeerRecv recv() const;
   size_t slot_floats() const { return slot_floats_; }
+  // An all-reduce of n floats that the caller's own one-workgroup kernel completes
+  // (peer_allreduce_block): opens the collective and fills *p, or returns false when that
+  // form does not apply (in-process ranks, n above kPeerSmallAllreduce, world 1)
+  bool small_allreduce(size_t n, PeerSmall *p);
   // throws PGCN_E_COMM when a wait gave up (a peer never signalled); call after a sync
   void check() const;
 

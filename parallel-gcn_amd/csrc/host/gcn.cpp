@@ -841,9 +841,13 @@ void GCN::finalize(int dst_offset, bool graph) {
   // k_compose's arithmetic in the same float operations, the same bits)
   PGCN_CHECK(!graph, PGCN_E_INVALID, "edge-cut epochs are not captured");
   float *raw = raw_ring.get() + (size_t)dst_offset * 2;  // slot * 8 + pass * 4
+  PeerSmall ps;
+  auto *pc = dynamic_cast<PeerComm *>(comm.get());
+  const bool fused = pc && pc->small_allreduce(2, &ps);  // between processes: in this launch
   launch_reduce_scalars(xent_partials.get(), ctx.xent_blocks, w1->dev_data.get(), w1->size,
-                        nullptr, stream.get(), ctx.count, 0.0f, nullptr, nullptr, 1, raw);
-  comm->allreduce_sum(raw, 2, stream.get());
+                        nullptr, stream.get(), ctx.count, 0.0f, nullptr, nullptr, 1, raw,
+                        fused ? &ps : nullptr);
+  if (!fused) comm->allreduce_sum(raw, 2, stream.get());
 }
 
 // k_compose (hpdga gcn.cpp:167-198) on the host: {loss_sum/count + wd*l2/2, (count-wrong)/count}

@@ -12,6 +12,7 @@
 
 #include "common.hpp"
 #include "kernels.hpp"
+#include "peer_sync.hpp"
 
 #pragma clang fp contract(off)
 
@@ -725,7 +726,8 @@ __global__ __launch_bounds__(1024) void k_reduce_scalars(const float *__restrict
                                                          int count, float wd,
                                                          float *__restrict__ out2,
                                                          const int *__restrict__ ctr,
-                                                         int ring_cap, float *__restrict__ raw4) {
+                                                         int ring_cap, float *__restrict__ raw4,
+                                                         PeerSmall peer) {
   __shared__ float red[16];
   float l = 0.0f, wr = 0.0f, q = 0.0f;
   // a thread's elements b = tid + 1024 u in u order, 8 loads in flight before their adds (r03
@@ -773,6 +775,12 @@ __global__ __launch_bounds__(1024) void k_reduce_scalars(const float *__restrict
       out2[0] = l / (float)count + wd * q / 2.0f;
       out2[1] = (float)(count - (int)wr) / (float)count;
     }
+  }
+  // edge-cut between processes: the loss / wrong pair all-reduced over the ranks in this
+  // launch (one launch per pass fewer; the same pushes and rank-order sum as PeerComm's)
+  if (raw4 && peer.k.world) {
+    __syncthreads();
+    (void)peer_allreduce_block(raw4, 2, peer);
   }
 }
 
@@ -925,9 +933,11 @@ void launch_out_xent(const float *H, int ldh, int kh, const float *W, int ldw, f
 
 void launch_reduce_scalars(const float *partials, int n_blocks, const float *w, long long n_w,
                            float *sums, hipStream_t s, int count, float wd, float *out2,
-                           const int *ctr, int ring_cap, float *raw4) {
+                           const int *ctr, int ring_cap, float *raw4, const PeerSmall *peer) {
+  PGCN_CHECK(!peer || (raw4 && peer->k.world >= 1 && peer->k.world <= kPeerMaxRanks),
+             PGCN_E_INVALID, "reduce_scalars: peer all-reduce of the raw pair");
   PGCN_LAUNCH(k_reduce_scalars, dim3(1), dim3(1024), 0, s, partials, n_blocks, w, n_w,
-                     sums, count, wd, out2, ctr, ring_cap, raw4);
+                     sums, count, wd, out2, ctr, ring_cap, raw4, peer ? *peer : PeerSmall{});
 }
 
 // epoch graphs: the device copy of the host's (Adam step, epoch) counters

@@ -116,43 +116,56 @@ __global__ __launch_bounds__(256) void k_ring_prescale_wide(const float *__restr
 // xGMI when q is a peer) instead of `out`; the launch's last workgroup then signals the
 // receivers (peer_arrive).  No epilogue: the receiver applies it after summing the ranks.
 template <bool PUSH>
-__global__ __launch_bounds__(256) void k_gs_lds_combine(const float4 *__restrict__ partial,
-                                                        long long part_stride, int nb,
-                                                        const float *__restrict__ scale, int n,
-                                                        float4 *__restrict__ out, int ld4_out,
-                                                        GsEpilogue epi, PeerSink push) {
+__global__ __launch_bounds__(PUSH ? 1024 : 256) void k_gs_lds_combine(
+    const float4 *__restrict__ partial, long long part_stride, int nb,
+    const float *__restrict__ scale, int n, float4 *__restrict__ out, int ld4_out,
+    GsEpilogue epi, PeerSink push) {
   if (PUSH) {
-    // consecutive workgroups serve different owners (block b: owner b % world, its rows
-    // 64 (b / world) ..): the pushes in flight at any time spread over every peer's link
-    // instead of draining the owners one after another
-    const int q0 = (int)(blockIdx.x % (unsigned)push.world);
-    const long long j0 = (long long)(blockIdx.x / (unsigned)push.world) * 64 + (threadIdx.x >> 2);
-    const long long r = (long long)q0 * push.rows_per_rank + j0;
-    const long long t = r * 4 + (threadIdx.x & 3);
-    if (j0 < push.rows_per_rank && r < n) {
-      const int v = (int)(t & 3);
-      const float s = scale[r];
-      float4 a;
-      if (nb <= 8) {
-        float4 p[8];
+    // 64-row tiles; consecutive tiles serve different owners (tile b: owner b % world, its rows
+    // 64 (b / world) ..), so the pushes in flight at any time spread over every peer's link
+    // instead of draining the owners one after another.  A bounded grid of 1,024-thread
+    // workgroups walks the tiles (4 at a time per workgroup): each workgroup ends with one
+    // system-scope release (peer_arrive), and few workgroups keep those L2 write-backs few.
+    const long long n_tiles = (long long)push.world * ((push.rows_per_rank + 63) / 64);
+    // Two tiles per thread and iteration, both tiles' loads issued before either's adds.
+    const int v = (int)(threadIdx.x & 3);
+    const long long step = (long long)gridDim.x * 4;
+    for (long long tile = (long long)blockIdx.x * 4 + (threadIdx.x >> 8); tile < n_tiles;
+         tile += 2 * step) {
+      int q[2];
+      long long j[2], r[2];
+      bool ok[2];
+      float s[2];
+      float4 p[2][4];
 #pragma unroll
-        for (int b = 0; b < 8; b++)
-          if (b < nb) p[b] = partial[((long long)b * part_stride + r) * 4 + v];
-        a = p[0];
+      for (int u = 0; u < 2; u++) {
+        const long long t = tile + u * step;
+        q[u] = (int)(t % push.world);                                 // the owner
+        j[u] = (t / push.world) * 64 + ((threadIdx.x & 255) >> 2);    // its row
+        r[u] = (long long)q[u] * push.rows_per_rank + j[u];
+        ok[u] = t < n_tiles && j[u] < push.rows_per_rank && r[u] < n;
+        if (ok[u]) {
+          s[u] = scale[r[u]];
 #pragma unroll
-        for (int b = 1; b < 8; b++)
-          if (b < nb) f4_acc(a, p[b]);
-      } else {
-        a = partial[r * 4 + v];
-        for (int b = 1; b < nb; b++) f4_acc(a, partial[((long long)b * part_stride + r) * 4 + v]);
+          for (int b = 0; b < 4; b++)
+            if (b < nb) p[u][b] = partial[((long long)b * part_stride + r[u]) * 4 + v];
+        }
       }
-      a.x *= s;
-      a.y *= s;
-      a.z *= s;
-      a.w *= s;
-      const int q = (int)(r / push.rows_per_rank);
-      const long long j = r - (long long)q * push.rows_per_rank;
-      peer_store16(push.dst[q], push.slot_bytes, j * ld4_out + v, a);
+#pragma unroll
+      for (int u = 0; u < 2; u++) {
+        if (!ok[u]) continue;
+        float4 a = p[u][0];
+#pragma unroll
+        for (int b = 1; b < 4; b++)
+          if (b < nb) f4_acc(a, p[u][b]);
+        for (int b = 4; b < nb; b++)
+          f4_acc(a, partial[((long long)b * part_stride + r[u]) * 4 + v]);
+        a.x *= s[u];
+        a.y *= s[u];
+        a.z *= s[u];
+        a.w *= s[u];
+        peer_store16(push.dst[q[u]], push.slot_bytes, j[u] * ld4_out + v, a);
+      }
     }
     peer_arrive(push);
     return;
@@ -492,8 +505,11 @@ void launch_graphsum_ring(const LdsSchedule &s, const float *in, int ld_in, floa
     PGCN_CHECK((!epi || epi->mode == 0) && push->world >= 1 && push->world <= kPeerMaxRanks &&
                    push->rows_per_rank > 0 && (long long)push->rows_per_rank * push->world >= s.n_rows,
                PGCN_E_INVALID, "graphsum_ring: push shape");
-    const long long blocks = (long long)push->world * ceil_div(push->rows_per_rank, 64);
-    PGCN_LAUNCH(k_gs_lds_combine<true>, dim3((unsigned)blocks), dim3(256), 0, st,
+    const long long tiles = (long long)push->world * ceil_div(push->rows_per_rank, 64);
+    // one workgroup per CU: 2 / 4 / 8 per CU measured 0.542 / 0.590 / 0.586 ms per W = 8 rank
+    // epoch against 0.511 (profiles/r05/k): every workgroup's release writes back its L2
+    const long long blocks = std::min<long long>(ceil_div(tiles, 4), (long long)kCUs);
+    PGCN_LAUNCH(k_gs_lds_combine<true>, dim3((unsigned)blocks), dim3(1024), 0, st,
                 reinterpret_cast<const float4 *>(partial), (long long)s.n_rows, s.n_blocks,
                 s.row_scale, s.n_rows, nullptr, ld_out / 4, none, *push);
   } else {

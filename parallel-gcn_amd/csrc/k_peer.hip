@@ -9,11 +9,12 @@
 // them: k_gs_lds_combine's push mode), and q sums its W slots in rank order (deterministic,
 // the same order on every rank).
 //
-// Ordering, with receive regions, flags and arrival counters in uncached device memory
-// (MTYPE UC: no cache holds a line of them, on this GPU or a peer):
+// Ordering, with flags and arrival counters in uncached device memory (MTYPE UC: no cache
+// holds a line of them, on this GPU or a peer) and the receive slots in plain device memory:
 //   producer  -- every store of a workgroup acknowledged (s_waitcnt vmcnt(0)), the workgroup's
-//                barrier, one arrival on the launch's counter; the last workgroup to arrive
-//                stores gen into flag[rank] of every peer, and resets the counter;
+//                barrier, one system-scope release (L2 write-back, waited for), one arrival on
+//                the launch's counter; the last workgroup to arrive stores gen into flag[rank]
+//                of every peer, and resets the counter (peer_sync.hpp);
 //   consumer  -- one wave polls its own flags until every peer's reads gen (bounded: an error
 //                word and an early exit after kPeerTimeoutTicks), then the sum kernel reads
 //                the slots (stream order after the wait).
@@ -67,69 +68,11 @@ __global__ __launch_bounds__(64) void k_peer_wait(const unsigned *flags, int wor
 __device__ __forceinline__ void peer_acc(float &a, float b) { a += b; }
 __device__ __forceinline__ void peer_acc(float4 &a, const float4 &b) { f4_acc(a, b); }
 
-// A small all-reduce in ONE workgroup (separate processes only: their kernels never share a
-// hardware queue, so this rank's spin cannot sit ahead of a peer's push): buf [n] pushed to
-// every receiver's slot of this rank, the flags, one wave polling this rank's flags (waited[q],
-// q < nwait), one system-scope acquire (the slots were written by other agents within this
-// kernel's lifetime: no kernel boundary in between), the rank-order sum back into buf.
-// Replaces push + wait + sum launches (3 x ~5 us per collective at W = 8) for the weight
-// gradients and the loss scalars.
+// A small all-reduce in ONE workgroup (peer_allreduce_block): replaces push + wait + sum
+// launches (3 x ~5 us per collective at W = 8) for the loss scalars between processes.
 __global__ __launch_bounds__(256) void k_peer_allreduce_small(float *__restrict__ buf, int n,
-                                                              PeerSink k, PeerRecv r,
-                                                              const unsigned *waited, int nwait,
-                                                              unsigned *err) {
-  const bool v4 = (n & 3) == 0;
-  for (int q = 0; q < k.world; q++) {
-    if (v4)
-      for (int i = threadIdx.x; i < n / 4; i += blockDim.x)
-        peer_store16(k.dst[q], k.slot_bytes, i, reinterpret_cast<const float4 *>(buf)[i]);
-    else
-      for (int i = threadIdx.x; i < n; i += blockDim.x) peer_store4(k.dst[q], k.slot_bytes, i, buf[i]);
-  }
-  stores_acked();
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int q = 0; q < k.world; q++) flag_store(k.flag[q], k.gen);
-    stores_acked();
-  }
-  __shared__ int failed;
-  if (threadIdx.x < 64) {
-    const int q = threadIdx.x;
-    bool bad = flag_load(err) != 0;
-    if (!bad && q < nwait) {
-      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-      while ((int)(flag_load(waited + q) - k.gen) < 0) {
-        __builtin_amdgcn_s_sleep(2);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > kPeerTimeoutTicks) {
-          __hip_atomic_store(err, 0x10000u | (unsigned)q, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_SYSTEM);
-          bad = true;
-          break;
-        }
-      }
-    }
-    const unsigned long long any_bad = __ballot(bad);
-    if (threadIdx.x == 0) {
-      failed = any_bad != 0;
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: L1 (and NC lines) dropped
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  }
-  __syncthreads();
-  if (failed) return;
-  if (v4) {
-    for (int i = threadIdx.x; i < n / 4; i += blockDim.x) {
-      float4 a = reinterpret_cast<const float4 *>(r.slot[0])[i];
-      for (int q = 1; q < r.world; q++) f4_acc(a, reinterpret_cast<const float4 *>(r.slot[q])[i]);
-      reinterpret_cast<float4 *>(buf)[i] = a;
-    }
-  } else {
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
-      float a = r.slot[0][i];
-      for (int q = 1; q < r.world; q++) a += r.slot[q][i];
-      buf[i] = a;
-    }
-  }
+                                                              PeerSmall p) {
+  (void)peer_allreduce_block(buf, n, p);
 }
 
 void launch_peer_allreduce_small(float *buf, int n, const PeerSink &k, const PeerRecv &r,
@@ -138,7 +81,13 @@ void launch_peer_allreduce_small(float *buf, int n, const PeerSink &k, const Pee
   PGCN_CHECK(k.world >= 1 && k.world <= kPeerMaxRanks && r.world == k.world && n >= 0 &&
                  n <= kPeerSmallAllreduce,
              PGCN_E_INVALID, "peer_allreduce_small: shape");
-  PGCN_LAUNCH(k_peer_allreduce_small, dim3(1), dim3(256), 0, s, buf, n, k, r, waited, nwait, err);
+  PeerSmall p;
+  p.k = k;
+  p.r = r;
+  p.waited = waited;
+  p.nwait = nwait;
+  p.err = err;
+  PGCN_LAUNCH(k_peer_allreduce_small, dim3(1), dim3(256), 0, s, buf, n, p);
   PGCN_HIP(hipGetLastError());
 }
 

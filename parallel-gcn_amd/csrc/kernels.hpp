@@ -205,6 +205,15 @@ struct PeerRecv {
   const float *slot[kPeerMaxRanks];
   int world = 0;
 };
+// one small all-reduce done inside one workgroup (peer_allreduce_block, peer_sync.hpp): push,
+// signal, wait for waited[q < nwait], sum the received slots in rank order
+struct PeerSmall {
+  PeerSink k;
+  PeerRecv r;
+  const unsigned *waited = nullptr;
+  int nwait = 0;
+  unsigned *err = nullptr;
+};
 // send [world][count] -> sink.dst[q] (same_for_all: send [count] to every q); then the flags
 // (the launch's last workgroup)
 void launch_peer_push(const float *send, size_t count, const PeerSink &k, hipStream_t s,
@@ -291,7 +300,7 @@ void launch_xent_fwd(float *logits, int ld, float *grad, const int *truth, int n
 void launch_reduce_scalars(const float *partials, int n_blocks, const float *w, long long n_w,
                            float *sums, hipStream_t s, int count = 0, float wd = 0.0f,
                            float *out2 = nullptr, const int *ctr = nullptr, int ring_cap = 1,
-                           float *raw4 = nullptr);
+                           float *raw4 = nullptr, const PeerSmall *peer = nullptr);
 // ctr (epoch graphs, device {Adam step, epoch} counters): out2 is slot 4 * (ctr[1] % ring_cap)
 // step_table (epoch graphs): step_size = step_table[ctr[0] % table_cap]
 void launch_adam(float *w, const float *g, float *m, float *v, long long n, float step_size,
