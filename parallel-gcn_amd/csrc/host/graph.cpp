@@ -431,6 +431,11 @@ int lds_blocks(int n_rows, int n_cols) {
     const long long nrs = ((long long)n_rows + 15) / 16;
     const long long nb = std::max(1LL, (nrs + cap - 1) / cap);
     if (nb * 8 <= kCUs && n_cols / 8 >= 20 * RING_SR) return 8;
+    // tall (an edge-cut rank's column block at W = 8: 233 k rows x 29 k columns): 2 blocks,
+    // half the partials for the combine to add and push (r05, solo W = 8 rank epoch 0.488 vs
+    // 0.512 ms at 4, 0.548 at 1; at W = 4, 4x as tall, 4 blocks stay best: 0.669 vs 0.708 ms;
+    // profiles/r05/p)
+    if ((long long)n_rows >= 6LL * n_cols) return 2;
     return 4;
   }
   // row subsets: 8 blocks, or more when few batches of rowsets would leave each workgroup a

@@ -7,7 +7,7 @@ DIR=$1; shift
 mkdir -p "$DIR/obj"
 FL="-O3 -fPIC -std=c++17 --offload-arch=gfx950 -ffp-contract=off -Wall -Wno-unused-function $*"
 objs=()
-for f in csrc/k_graphsum.hip csrc/k_graphsum_ring.hip csrc/k_gemm.hip csrc/k_gemm_wide.hip csrc/k_xstream_lds.hip \
+for f in csrc/k_peer.hip csrc/k_graphsum.hip csrc/k_graphsum_ring.hip csrc/k_gemm.hip csrc/k_gemm_wide.hip csrc/k_xstream_lds.hip \
          csrc/k_sparse.hip csrc/k_elementwise.hip csrc/capi.cpp csrc/rng.cpp csrc/host/graph.cpp \
          csrc/host/ring.cpp csrc/host/data.cpp csrc/host/comm.cpp csrc/host/api.cpp \
          csrc/host/module.cpp csrc/host/gcn.cpp; do
