@@ -24,6 +24,7 @@ extern int g_split_cols;            // host/gcn.cpp
 extern int g_fuse_epilogue;         // host/gcn.cpp
 extern int g_fuse_output;           // host/gcn.cpp
 extern int g_mm_side;               // host/gcn.cpp
+extern int g_eval_tail;             // host/gcn.cpp
 extern int g_eval_ax;               // host/gcn.cpp
 extern int g_epoch_graph;           // host/gcn.cpp
 extern long long g_lds_min_bytes;   // host/graph.cpp
@@ -684,6 +685,9 @@ int pgcn_debug_set(const char *key, int value) {
   } else if (!std::strcmp(key, "mm_side")) {
     if (!in(0, 2)) return PGCN_E_INVALID;
     pgcn::g_mm_side = value;
+  } else if (!std::strcmp(key, "eval_tail")) {
+    if (!in(0, 1)) return PGCN_E_INVALID;
+    pgcn::g_eval_tail = value;
   } else if (!std::strcmp(key, "xstream_ring")) {
     if (!in(0, 1)) return PGCN_E_INVALID;
     pgcn::g_xstream_ring = value;

@@ -155,6 +155,7 @@ class PeerComm : public Comm {
   void wait(hipStream_t s);
   PeerRecv recv() const;
   size_t slot_floats() const { return slot_floats_; }
+  bool host_ordered() const { return (bool)host_order_; }  // in-process ranks
   // An all-reduce of n floats that the caller's own one-workgroup kernel completes
   // (peer_allreduce_block): opens the collective and fills *p, or returns false when that
   // form does not apply (in-process ranks, n above kPeerSmallAllreduce, world 1)

@@ -59,6 +59,14 @@ int g_sparse_dual = 1;
 // stream hand-offs cost more than the ~7 us of kernels they hide)
 int g_mm_side = 0;
 constexpr int kMmSideRows = 65536;
+// "eval_tail" (read at engine build): the edge-cut eval pass's last exchange and output layer
+// on the (high-priority) comm stream beside the next epoch's mask draw and first-layer product
+// (ModuleContext::tail_stream; peer exchange between processes only; bit-identical).  Off: on
+// the solo timing form, where the push has no link time to hide, the overlapped kernels slow
+// each other -- W = 8 rank epoch 0.511-0.514 vs 0.489-0.495 ms (0.502-0.506 on the low-priority
+// side stream; profiles/r05/s).  An 8-GPU run with slow links may still gain (the eval push's
+// link time beside ~48 us of compute): `bench.py --knob eval_tail=1`
+int g_eval_tail = 0;
 
 // ------------------------------------------------------------------------------------------
 // Adam (src/optim.cu:7-95; hpdga optim.cpp:16-35)
@@ -513,6 +521,16 @@ void GCN::build(const GCNData &data) {
   optimizer = Adam(weights, decays, adam_params);
   prepare_graphs();
   build_eval_ax();
+  // eval_tail: the peer exchange between processes (or the solo timing form) -- in-process
+  // ranks may share hardware queues, where a wait on one rank's side stream could sit ahead
+  // of the push it waits for
+  const auto *pc = dynamic_cast<const PeerComm *>(comm.get());
+  if (g_eval_tail && pc && !pc->host_ordered() && comm->world() > 1) {
+    for (int i = 0; i < (int)modules.size(); i++)
+      if (dynamic_cast<const GraphSum *>(modules[(size_t)i].get())) tail_gs = i;
+    ctx.tail_fork = Event::create();
+    ctx.tail_done = Event::create();
+  }
   PGCN_HIP(hipDeviceSynchronize());
 }
 
@@ -827,8 +845,9 @@ void GCN::set_split(int split) {
 
 // loss/acc of the pass just enqueued -> results_ring slot (finalize, src/gcn.cu:440-455);
 // graph: the slot from the device epoch counter
-void GCN::finalize(int dst_offset, bool graph) {
+void GCN::finalize(int dst_offset, bool graph, hipStream_t s) {
   const auto &w1 = weights.front();
+  if (!s) s = stream.get();
   if (!comm) {  // one launch: reduce + compose
     launch_reduce_scalars(xent_partials.get(), ctx.xent_blocks, w1->dev_data.get(), w1->size,
                           sums.get(), stream.get(), ctx.count, adam_params.weight_decay,
@@ -845,9 +864,36 @@ void GCN::finalize(int dst_offset, bool graph) {
   auto *pc = dynamic_cast<PeerComm *>(comm.get());
   const bool fused = pc && pc->small_allreduce(2, &ps);  // between processes: in this launch
   launch_reduce_scalars(xent_partials.get(), ctx.xent_blocks, w1->dev_data.get(), w1->size,
-                        nullptr, stream.get(), ctx.count, 0.0f, nullptr, nullptr, 1, raw,
+                        nullptr, s, ctx.count, 0.0f, nullptr, nullptr, 1, raw,
                         fused ? &ps : nullptr);
-  if (!fused) comm->allreduce_sum(raw, 2, stream.get());
+  if (!fused) comm->allreduce_sum(raw, 2, s);
+}
+
+// eval's forward pass (src/gcn.cu:293-303).  eval_tail: from its last GraphSum's push on, the
+// pass runs on comm_stream (ModuleContext::tail_stream), so the next epoch's mask draw and
+// first-layer product proceed on the stream beside the exchange and the output layer; the
+// next GraphSum waits for tail_done.
+void GCN::eval_forward(int off, bool graph) {
+  const bool tail = tail_gs >= 0;
+  for (int i = 0; i < (int)modules.size(); i++) {
+    if (tail && i == tail_gs) {
+      ctx.tail_stream = comm_stream.get();
+      ctx.tail_used = false;
+    }
+    modules[(size_t)i]->forward(false, tail && i > tail_gs ? comm_stream : stream);
+    if (tail && i == tail_gs) {
+      ctx.tail_stream = nullptr;
+      if (!ctx.tail_used) {  // that GraphSum ran whole on the stream: the rest follows it
+        ctx.tail_fork.record(stream.get());
+        ctx.tail_fork.wait_on(comm_stream.get());
+      }
+    }
+  }
+  finalize(off, graph, tail ? comm_stream.get() : nullptr);
+  if (tail) {
+    ctx.tail_done.record(comm_stream.get());
+    ctx.tail_pending = true;
+  }
 }
 
 // k_compose (hpdga gcn.cpp:167-198) on the host: {loss_sum/count + wd*l2/2, (count-wrong)/count}
@@ -882,8 +928,7 @@ void GCN::enqueue_epoch(bool graph) {
   else
     optimizer.step(stream);
   set_split(2);
-  for (const auto &m : modules) m->forward(false, stream);
-  finalize(slot4 + 2, graph);
+  eval_forward(slot4 + 2, graph);
   if (graph) launch_counters(dev_ctr.get(), 0, 0, 0, stream.get());
 }
 
@@ -974,6 +1019,7 @@ std::pair<float, float> GCN::train_epoch() {
 // that pass (edge-cut)
 std::pair<float, float> GCN::read_slot(int off) {
   if (comm) {
+    if (ctx.tail_pending) comm_stream.sync();  // an eval pass's scalars (eval_tail)
     PGCN_HIP(hipMemcpyAsync(pinned.get(), raw_ring.get() + (size_t)off * 2, 4 * sizeof(float),
                             hipMemcpyDeviceToHost, stream.get()));
     stream.sync();
@@ -992,8 +1038,7 @@ std::pair<float, float> GCN::eval(int split) {
   PGCN_CHECK(split >= 1 && split <= 3, PGCN_E_INVALID, "split must be 1, 2 or 3");
   const long long slot = epoch_count % ring_cap;
   set_split(split);
-  for (const auto &m : modules) m->forward(false, stream);
-  finalize((int)(slot * 4 + 2));
+  eval_forward((int)(slot * 4 + 2), false);
   last_forward_training = false;
   ctr_valid = false;
   const std::pair<float, float> r = read_slot((int)(slot * 4 + 2));
@@ -1004,6 +1049,7 @@ std::pair<float, float> GCN::eval(int split) {
 void GCN::sync() {
   stream.sync();
   side_stream.sync();
+  if (comm_stream.get()) comm_stream.sync();  // (eval_tail)
   check_comm();
 }
 

@@ -131,7 +131,11 @@ class GCN {
   void join_side();
   int fused_tails_ = 0;  // GraphSum epilogues carrying ReLU / Dropout work (forward + backward)
   void set_split(int split);
-  void finalize(int slot_offset, bool graph = false);
+  void finalize(int slot_offset, bool graph = false, hipStream_t s = nullptr);
+  // the eval forward + finalize of ring slot offset `off` (eval_tail: its last GraphSum's
+  // exchange and the output layer on side_stream, ModuleContext::tail_stream)
+  void eval_forward(int off, bool graph);
+  int tail_gs = -1;  // eval_tail: index in `modules` of the last GraphSum; -1 = off
   void enqueue_epoch(bool graph);
   bool graph_eligible() const;
   void capture_epoch();

@@ -563,7 +563,8 @@ float *DevGraph::table_wide(size_t floats) {
 
 void DevGraph::graphsum(const float *in, int ld_in, float *out, int ld_out, int dim,
                         hipStream_t s, bool compact_in, const GsEpilogue *epi, bool prestaged,
-                        bool tables_ready, const PeerSink *push) {
+                        bool tables_ready, const PeerSink *push, hipStream_t tail_st,
+                        hipEvent_t fork) {
   const int *col_map = compact_in ? nullptr : col_map_.get();
   PGCN_CHECK(ld_in % 4 == 0 && ld_out % 4 == 0 && ld_in >= dim && ld_out >= dim,
              PGCN_E_INVALID, "graphsum: leading dims must be multiples of 4 and >= dim");
@@ -581,6 +582,8 @@ void DevGraph::graphsum(const float *in, int ld_in, float *out, int ld_out, int 
                "graphsum: prestaged input on a path without a ring table");
     const size_t table = (size_t)ceil_div(n_cols_, RING_SR) * RING_SR * 16;
     const int n_pass = ceil_div(dim, 16);
+    PGCN_CHECK(!tail_st || (push && n_pass == 1), PGCN_E_INVALID,
+               "graphsum: a tail stream for a one-pass push only");
     auto pass_col = [&](int p) { return std::min(16 * p, ldm - 16); };
     // several passes: one launch prescales all of them (each pass then reads its own table);
     // inputs up to 128 wide (at most 8 passes: RingPasses), wider ones prescale per pass
@@ -609,7 +612,8 @@ void DevGraph::graphsum(const float *in, int ld_in, float *out, int ld_out, int 
       }
       launch_graphsum_ring(lds_->s, in + c, ld_in, out ? out + c : nullptr, ld_out,
                            batch ? tables + table * p : table_scratch(), lds_->partial.get(), s,
-                           col_map, &ep, prestaged || batch || tables_ready, push ? &pk : nullptr);
+                           col_map, &ep, prestaged || batch || tables_ready, push ? &pk : nullptr,
+                           tail_st, fork);
     }
     return;
   }

@@ -81,7 +81,8 @@ class DevGraph {
   // input on a graph sharing them (share_tables; can_share_tables(dim, ld_in)): no prescale launch
   void graphsum(const float *in, int ld_in, float *out, int ld_out, int dim, hipStream_t s,
                 bool compact_in = false, const GsEpilogue *epi = nullptr, bool prestaged = false,
-                bool tables_ready = false, const PeerSink *push = nullptr);
+                bool tables_ready = false, const PeerSink *push = nullptr,
+                hipStream_t tail_st = nullptr, hipEvent_t fork = nullptr);
   // The ring schedule reads its prescaled input tables from `owner`'s buffers (same columns,
   // column scales and column map: the edge-cut engine's row chunks of one column block), so
   // one prescale serves every graph of the group.

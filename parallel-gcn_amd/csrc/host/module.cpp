@@ -391,6 +391,11 @@ GsEpilogue GraphSum::backward_epilogue(const DevGraph *g) const {
 
 void GraphSum::run(const float *src, float *dst, const Stream &s, int mode,
                    const GsEpilogue *epi, bool prestaged) const {
+  if (ctx->tail_pending && !ctx->tail_stream) {
+    // the last eval pass's tail (eval_tail) still reads the partial buffer and its slots
+    ctx->tail_done.wait_on(s.get());
+    ctx->tail_pending = false;
+  }
   Event e0, e1;
   if (ctx->profile) {
     e0 = Event::create(true);
@@ -428,14 +433,22 @@ void GraphSum::run(const float *src, float *dst, const Stream &s, int mode,
     auto *pc = static_cast<PeerComm *>(ctx->comm);
     DevGraph *gk = cgs[0];
     const int h = out->rows;  // padded rows per rank (one chunk)
+    // eval_tail: this call's push, wait and sum on the tail stream (the eval pass's last
+    // GraphSum); any other call first waits for the last tail (partial buffer, slot parity)
+    hipStream_t ts = s.get();
+    if (ctx->tail_stream && dim <= 16) {
+      ts = ctx->tail_stream;
+      ctx->tail_used = true;
+    }
     PeerSink k = pc->sink(h, (size_t)out->ld);
     pc->note((size_t)h * out->ld * ctx->comm->world() * sizeof(float), 1.0);
-    gk->graphsum(src, in->ld, nullptr, out->ld, dim, s.get(), false, nullptr, prestaged, false, &k);
+    gk->graphsum(src, in->ld, nullptr, out->ld, dim, s.get(), false, nullptr, prestaged, false, &k,
+                 ts != s.get() ? ts : nullptr, ctx->tail_fork.get());
     bytes = gk->algorithmic_bytes(dim);
-    pc->wait(s.get());
+    pc->wait(ts);
     launch_gs_gather_finish(dst, out->ld, ctx->local_rows, (dim + 3) / 4 * 4,
-                            epi && epi->mode ? *epi : GsEpilogue{}, pc->recv(), s.get());
-    if (ctx->profile) e1.record(s.get());
+                            epi && epi->mode ? *epi : GsEpilogue{}, pc->recv(), ts);
+    if (ctx->profile) e1.record(ts);
   } else if (ctx->comm) {
     // Per row chunk: partial sums of the chunk's (padded) rows from this rank's columns on
     // the compute stream, then its reduce-scatter on the comm stream, which hands every rank

@@ -101,6 +101,15 @@ struct ModuleContext {
   // weight-gradient pass, the eval forward's X-stream product or its output layer -- the RNG
   // kernel and the pass beside it slow each other down, DESIGN.md §3 "Streams")
   hipStream_t side_stream = nullptr;  // mm_side's stream
+  // "eval_tail" (edge-cut, peer exchange between processes): the eval pass's last GraphSum
+  // pushes, waits and sums on tail_stream (set by GCN for that call), and the output layer and
+  // the loss follow there, beside the next epoch's mask draw and first-layer product on the
+  // stream; tail_done is recorded after them, and the next GraphSum on the stream waits for it
+  // (tail_pending) -- it reuses the partial buffer and the slots' parity
+  hipStream_t tail_stream = nullptr;
+  Event tail_fork, tail_done;
+  bool tail_pending = false;
+  bool tail_used = false;  // the GraphSum given tail_stream ran its exchange there
   // "mm_side": a Matmul's weight gradient (b.grad = a^T c.grad, needed only by the optimizer)
   // runs on side_stream beside the rest of the backward pass (the reference's S2/S3 streams,
   // src/module.cu:445-472); GCN joins it (side_join) before the all-reduce / optimizer

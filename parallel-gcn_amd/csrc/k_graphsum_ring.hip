@@ -482,8 +482,9 @@ void launch_ring_prescale_wide(const LdsSchedule &s, const float *in, int ld_in,
 void launch_graphsum_ring(const LdsSchedule &s, const float *in, int ld_in, float *out,
                           int ld_out, float *scratch_in, float *partial, hipStream_t st,
                           const int *col_map, const GsEpilogue *epi, bool prestaged,
-                          const PeerSink *push) {
+                          const PeerSink *push, hipStream_t tail_st, hipEvent_t fork) {
   note_path(KP_GS_RING);
+  PGCN_CHECK(!tail_st || (push && fork), PGCN_E_INVALID, "graphsum_ring: tail stream of a push");
   PGCN_CHECK(ld_in % 4 == 0 && ld_out % 4 == 0, PGCN_E_INVALID, "graphsum_ring: ld % 4");
   const long long pre = (long long)s.n_cols * 4;
   if (!prestaged)
@@ -509,6 +510,11 @@ void launch_graphsum_ring(const LdsSchedule &s, const float *in, int ld_in, floa
     // one workgroup per CU: 2 / 4 / 8 per CU measured 0.542 / 0.590 / 0.586 ms per W = 8 rank
     // epoch against 0.511 (profiles/r05/k): every workgroup's release writes back its L2
     const long long blocks = std::min<long long>(ceil_div(tiles, 4), (long long)kCUs);
+    if (tail_st) {  // the push (and what follows it) on another stream, after the ring
+      PGCN_HIP(hipEventRecord(fork, st));
+      PGCN_HIP(hipStreamWaitEvent(tail_st, fork, 0));
+      st = tail_st;
+    }
     PGCN_LAUNCH(k_gs_lds_combine<true>, dim3((unsigned)blocks), dim3(1024), 0, st,
                 reinterpret_cast<const float4 *>(partial), (long long)s.n_rows, s.n_blocks,
                 s.row_scale, s.n_rows, nullptr, ld_out / 4, none, *push);

@@ -118,7 +118,8 @@ void launch_ring_prescale_wide(const LdsSchedule &s, const float *in, int ld_in,
 void launch_graphsum_ring(const LdsSchedule &s, const float *in, int ld_in, float *out,
                           int ld_out, float *scratch_in, float *partial, hipStream_t st,
                           const int *col_map = nullptr, const GsEpilogue *epi = nullptr,
-                          bool prestaged = false, const struct PeerSink *push = nullptr);
+                          bool prestaged = false, const struct PeerSink *push = nullptr,
+                          hipStream_t tail_st = nullptr, hipEvent_t fork = nullptr);
 // The edge-cut engine's GraphSum tail: after the reduce-scatter has summed every rank's
 // partials into this rank's rows y [n][ld] (ld % 4 == 0, dim % 4 == 0), the fused
 // element-wise epilogue (gs_epilogue.hpp: ReLU / Dropout, the next GraphSum's table) in place

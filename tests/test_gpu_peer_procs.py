@@ -97,12 +97,14 @@ def test_peer_procs_cora_world2(pgcn, datasets, loaded, tmp_path):
         helpers.assert_line_close(ours, gold[e], cnt, what=f"peer procs epoch {e + 1}")
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_peer_procs_lds_graph(pgcn, world, tmp_path):
+@pytest.mark.parametrize("world,tail", [(2, 0), (4, 0), (4, 1)])
+def test_peer_procs_lds_graph(pgcn, world, tail, tmp_path):
     """140k nodes: every rank's column block takes the LDS ring GraphSum, whose combine pushes
-    the partial sums into the owners' slots (k_gs_lds_combine's push mode)."""
+    the partial sums into the owners' slots (k_gs_lds_combine's push mode).  tail 1: the eval
+    pass's last exchange and output layer on the comm stream beside the next epoch (eval_tail),
+    the same bits as the in-process ranks (which never take it)."""
     syn = dict(n=140000, f=64, c=41, edges=1500000, seed=31)
-    spec = {"synthetic": syn, "epochs": 3, "async": 2}
+    spec = {"synthetic": syn, "epochs": 3, "async": 2, "knobs": {"eval_tail": tail}}
     procs = _run_procs(world, spec, tmp_path)
     assert procs[0]["info"][3] == 1  # graphsum_lds
     ds = pgcn.Dataset.synthetic(syn["n"], syn["f"], syn["c"], syn["edges"], syn["seed"])
