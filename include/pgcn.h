@@ -308,8 +308,10 @@ long long pgcn_partition_subgraph(int n, const int *indptr, const int *indices, 
 int pgcn_debug_rank_graph(int n, const int *indptr, const int *indices, int world, int rank,
                           int chunks, int chunk, pgcn_graph **out, int *rows, int *cols);
 /* Engine options (process-wide; most are read when an engine is built).  Each selects between
- * bit-identical or oracle-tested forms of the same reference epoch (17 keys, r05):
+ * bit-identical or oracle-tested forms of the same reference epoch (18 keys, r05):
  *   "train_ahead" 0/1, "eval_ax" 0/1, "split_cols" 0/1, "epoch_graph" 0/1, "mm_side" 0/1/2,
+ *   "eval_tail" 0/1 (edge-cut between processes: the eval pass's last exchange and output
+ *   layer beside the next epoch's first kernels, default 0),
  *   "fuse_epilogue" bits 1 tails | 2 prestaged tables | 4 X-stream epilogue | 8 Dropout /
  *   ReLU backward in a Matmul's input-grad product (default 15),
  *   "fuse_output" 0..3 (default 2), "xstream_ring" 0/1, "lds_min_kb" (< 0: default),
