@@ -367,11 +367,21 @@ PeerSink PeerComm::sink(int rows_per_rank, size_t row_floats) {
   k.world = world_;
   k.rows_per_rank = rows_per_rank;
   k.signal = 1;
+  if (!host_order_) {
+    // separate processes (or solo): the push launch's last workgroup waits (wait() adds none:
+    // W = 8 / 4 solo rank epochs 0.483 / 0.667 ms against 0.486 / 0.674 with the one-wave wait
+    // kernel, three interleaved pairs, profiles/r05/u);
+    // in-process ranks may share a hardware queue, where that spin could block a peer's push
+    k.wait_flags = reinterpret_cast<const unsigned *>(header_) + (solo_ ? rank_ : 0);
+    k.nwait = solo_ ? 1 : world_;
+    k.err = reinterpret_cast<unsigned *>(header_ + kErrOff);
+  }
   return k;
 }
 
 void PeerComm::wait(hipStream_t s) {
-  if (host_order_) host_order_();
+  if (!host_order_) return;  // fused into the push (sink)
+  host_order_();
   // (solo: every push signalled this rank's own flag word only)
   launch_peer_wait(reinterpret_cast<const unsigned *>(header_) + (solo_ ? rank_ : 0),
                    solo_ ? 1 : world_, gen_, reinterpret_cast<unsigned *>(header_ + kErrOff), s);

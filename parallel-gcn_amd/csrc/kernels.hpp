@@ -200,6 +200,12 @@ struct PeerSink {
   int world = 0;               // 0: not pushing
   int rows_per_rank = 0;       // GraphSum push: padded rows per owner (row r -> owner r / this)
   int signal = 1;              // 0: an earlier pass of a multi-pass push (no flags yet)
+  // the wait fused into the push (separate processes): the signalling launch's last workgroup
+  // then polls this rank's flags wait_flags[q < nwait] for gen (bounded as k_peer_wait); 0: the
+  // receiver launches k_peer_wait itself
+  const unsigned *wait_flags = nullptr;
+  int nwait = 0;
+  unsigned *err = nullptr;
 };
 // this rank's received slots of one collective: slot[q] = what rank q pushed
 struct PeerRecv {

@@ -67,9 +67,27 @@ __device__ __forceinline__ void peer_arrive(const PeerSink &k) {
         __hip_atomic_fetch_add(k.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (old == n - 1) {
       __hip_atomic_store(k.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      if (k.signal)
+      if (k.signal) {
         for (int q = 0; q < k.world; q++) flag_store(k.flag[q], k.gen);
-      stores_acked();
+        stores_acked();
+        // the receiver's wait, fused (separate processes): the launch ends once every sender
+        // of this rank has signalled, so the next kernel may read the slots
+        if (k.nwait && !flag_load(k.err)) {
+          const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+          for (int q = 0; q < k.nwait; q++) {
+            while ((int)(flag_load(k.wait_flags + q) - k.gen) < 0) {
+              __builtin_amdgcn_s_sleep(2);
+              if (__builtin_amdgcn_s_memrealtime() - t0 > kPeerTimeoutTicks) {
+                __hip_atomic_store(k.err, 0x10000u | (unsigned)q, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+                return;
+              }
+            }
+          }
+        }
+      } else {
+        stores_acked();
+      }
     }
   }
 }
