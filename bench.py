@@ -71,7 +71,9 @@ def load_pkg():
 
 def cpu_baseline(ds, epochs):
     """The reference's sequential epoch (train_epoch + eval(2)) on this host, 1 thread.
-    Prefers oracle/_ref (the reference's own sources); falls back to the C restatement."""
+    Prefers oracle/_ref (the reference's own sources); falls back to the C restatement.
+    Returns (kind, epoch times, epoch lines, the output variable after the last eval: the
+    logits of every row, the reference's variable 6)."""
     import helpers
     n, f, c = ds.num_nodes, ds.input_dim, ds.output_dim
     args = [ds.graph_indptr, ds.graph_indices, ds.feat_indptr, ds.feat_indices, ds.feat_values,
@@ -91,6 +93,8 @@ def cpu_baseline(ds, epochs):
             ref.ref_eval(h, 2, helpers.ptr(va))
             times.append(time.perf_counter() - t0)
             lines.append([float(tr[0]), float(tr[1]), float(va[0]), float(va[1])])
+        logits = np.zeros(ref.ref_get_var(h, 6, 0, None), np.float32)
+        ref.ref_get_var(h, 6, 0, helpers.ptr(logits))
         ref.ref_free(h)
     else:
         kind = "port"
@@ -101,8 +105,9 @@ def cpu_baseline(ds, epochs):
             b = g.eval(2)
             times.append(time.perf_counter() - t0)
             lines.append(list(a + b))
+        logits = np.asarray(g.logits(), np.float32)
         del g
-    return kind, times, lines
+    return kind, times, lines, logits
 
 
 def cpu_model():
@@ -410,7 +415,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline and hidden != (16,):
         out["cpu_baseline"] = None  # the reference's sequential build is the 2-layer H = 16 GCN
     elif rank == 0 and world == 1 and not args.no_cpu_baseline:
-        kind, times, ref_lines = cpu_baseline(ds, args.cpu_epochs)
+        kind, times, ref_lines, ref_logits = cpu_baseline(ds, args.cpu_epochs)
         out["cpu_baseline"] = {"value": len(times) / sum(times), "unit": "epochs/s", "cores": 1,
                                "kind": kind,
                                "sample": f"{len(times)} full epochs (train_epoch + eval(2)) of "
@@ -422,7 +427,14 @@ def main():
         with helpers.knobs(pgcn, **{k: int(v) for k, v in head_knobs.items()}):
             g3 = engine()
             ours = [g3.train_epoch() + g3.eval(2) for _ in range(len(ref_lines))]
+            our_logits = np.asarray(g3.get_var(6), np.float32).ravel()
             g3.close()
+        # every row's logits after the last eval(2), as the GPU tests compare them at 1e-4
+        # (rtol and atol; tests/test_gpu_parity_large.py) -- here at the full graph's size
+        ref_l = np.asarray(ref_logits, np.float32).ravel()
+        same_n = our_logits.size == ref_l.size
+        dl = np.abs(our_logits.astype(np.float64) - ref_l) if same_n else np.array([np.inf])
+        within = dl <= 1e-4 + 1e-4 * np.abs(ref_l.astype(np.float64)) if same_n else dl < 0
         rel = [abs(o[k] - r[k]) / abs(r[k]) for o, r in zip(ours, ref_lines) for k in (0, 2)]
         cnt = helpers.split_counts(ds)
         acc_rows = [abs(o[k] - r[k]) * cnt[sp] for o, r in zip(ours, ref_lines)
@@ -432,7 +444,11 @@ def main():
                          "acc_max_row_diff": max(acc_rows), "tolerance": 1e-4,
                          "pass": bool(max(rel) <= 1e-4),
                          "engine_lines": [list(map(float, o)) for o in ours],
-                         "reference_lines": ref_lines}
+                         "reference_lines": ref_lines,
+                         "logits": {"values": int(ref_l.size), "max_abs_err": float(dl.max()),
+                                    "within_1e-4": float(within.mean()),
+                                    "rtol": 1e-4, "atol": 1e-4,
+                                    "pass": bool(same_n and within.all())}}
     if rank == 0:
         print(json.dumps(out))
     if dist is not None:

@@ -258,7 +258,8 @@ class Dataset:
         return Dataset(h.value)
 
     def __del__(self):
-        if getattr(self, "_h", None) and self._h.value:
+        # (at interpreter exit the module's globals may already be gone: nothing to free then)
+        if getattr(self, "_h", None) and self._h.value and lib is not None:
             lib.pgcn_dataset_free(self._h)
             self._h = c_void_p()
 
