@@ -21,3 +21,4 @@ T=$(dirname $(find $O/prof_rank8 -name run_kernel_trace.csv | head -1))
 python3 tools/epoch_breakdown.py $T > $O/rank8_breakdown.txt 2>&1; head -3 $O/rank8_breakdown.txt
 timeout -k 10 600 python3 bench.py --workload reddit-11.6M > $O/bench_11.6M.json 2> $O/bench_11.6M.err; echo "11.6M rc=$?"; cut -c1-200 $O/bench_11.6M.json
 timeout -k 10 900 python3 bench.py --hidden 128,128,128 --steps 20 --warmup 5 > $O/bench_4layer.json 2> $O/bench_4layer.err; echo "4layer rc=$?"; cut -c1-200 $O/bench_4layer.json
+timeout -k 10 600 python3 bench.py > $O/bench_head.json 2> $O/bench_head.err; echo "bench (logits parity) rc=$?"; python3 -c "import json;d=json.load(open('$O/bench_head.json'));print(d['value'], d['parity'].get('logits'), d['parity']['pass'])"
