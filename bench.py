@@ -227,6 +227,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # PGCN_BENCH_SHARE_GPU=1 (rehearsal on a one-GPU box only): every rank on device 0, so the
+    # --gpus N launch, rendezvous, peer exchange and reporting run end to end as processes
+    # sharing one GPU; the numbers are not a scaling measurement (tests/test_gpu_bench_procs.py)
+    if os.environ.get("PGCN_BENCH_SHARE_GPU") == "1":
+        local_rank = 0
     dist = None
     if world > 1:
         import torch.distributed as dist

@@ -1,0 +1,31 @@
+"""bench.py --gpus 2 end to end on one GPU: the launcher (torch.distributed.run), the gloo
+rendezvous, two rank processes whose peer-mapped exchange opens its regions with hipIpc handles,
+the timing with its barriers and max over ranks, and rank 0's one JSON line -- the path the
+driver's multi-GPU bench takes, with both ranks on device 0 (PGCN_BENCH_SHARE_GPU=1, a rehearsal:
+the value is not a scaling measurement)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_gpus2_shared_gpu():
+    env = dict(os.environ, PGCN_BENCH_SHARE_GPU="1")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps",
+                        "3", "--warmup", "1", "--workload", "reddit-11.6M", "--no-cpu-baseline",
+                        "--no-extra"], cwd=REPO, env=env, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]  # rank 0 only
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["steps"] == 3 and out["warmup"] == 1
+    assert out["value"] > 0 and out["ms_per_step"] > 0
+    assert out["config"].get("exchange") == "peer", out["config"]
