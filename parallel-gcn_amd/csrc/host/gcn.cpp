@@ -218,6 +218,15 @@ void build_dev_features(DevFeatures &feats, const int *fptr, const int *indices,
     feats.csc_row.upload(crow);
     feats.csc_pos.allocate(cpos.size() + 1);
     feats.csc_pos.upload(cpos);
+    // the weight-gradient pass's workgroups in descending column length: a column is one
+    // serial chain, so the longest ones start first and the short ones fill in around them
+    std::vector<int> order((size_t)F);
+    for (int f = 0; f < F; f++) order[(size_t)f] = f;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+      return cptr[(size_t)a + 1] - cptr[(size_t)a] > cptr[(size_t)b + 1] - cptr[(size_t)b];
+    });
+    feats.csc_order.allocate(order.size() + 1);
+    feats.csc_order.upload(order);
   }
 }
 

@@ -266,7 +266,7 @@ void SparseMatmul::backward(const Stream &s) const {
   } else {
     launch_spmm_csc_bwd(x->cols, b->cols, c->ld, x->csc_ptr.get(), x->csc_row.get(),
                         x->csc_pos.get(), x->values.get(), mask, base, scale, c->dev_grad.get(),
-                        b->dev_grad.get(), s.get(), x->nnz);
+                        b->dev_grad.get(), s.get(), x->nnz, x->csc_order.get());
   }
 }
 

@@ -61,6 +61,7 @@ struct DevFeatures {
   DeviceBuffer<uint64_t> maskW;
   // sparse: CSR (+ transposed index for the weight gradient)
   DeviceBuffer<int> indptr, indices, csc_ptr, csc_row, csc_pos;
+  DeviceBuffer<int> csc_order;  // features by descending column length (weight-gradient order)
   DeviceBuffer<float> values;
   std::vector<float> host_values;  // for reporting the dropped input (API parity)
 };

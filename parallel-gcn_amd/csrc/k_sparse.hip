@@ -113,11 +113,14 @@ __global__ __launch_bounds__(CH) void k_spmm_csc_bwd(int nf, int p, int ldg,
                                                      const uint64_t *__restrict__ mask,
                                                      long long mask_base, float scale,
                                                      const float *__restrict__ cgrad,
-                                                     float *__restrict__ bgrad) {
+                                                     float *__restrict__ bgrad,
+                                                     const int *__restrict__ order) {
   // products column-major (prod[c][entry], rows padded to CH + 4 floats): an adding lane
   // reads 4 consecutive entries of its column with one ds_read_b128 (16 lanes, 4 banks apart)
   __shared__ __attribute__((aligned(16))) float prod[16][CH + 4];
-  const int f = blockIdx.x, k0 = blockIdx.y * 16, tid = threadIdx.x;
+  // (order: the features by descending column length -- the longest chains start first)
+  const int f = order ? order[blockIdx.x] : (int)blockIdx.x, k0 = blockIdx.y * 16,
+            tid = threadIdx.x;
   const int e0 = csc_ptr[f], e1 = csc_ptr[f + 1];
   float sum = 0.0f;
   // the 16 lanes' ordered adds of the chunk at cb (its reads a batch ahead of the adds)
@@ -259,15 +262,15 @@ void launch_spmm_csr_dual(int m, int p, int ldc, const int *indptr, const int *i
 void launch_spmm_csc_bwd(int nf, int p, int ldg, const int *csc_ptr, const int *csc_row,
                          const int *csc_pos, const float *a, const uint64_t *mask,
                          long long mask_base, float scale, const float *cgrad, float *bgrad,
-                         hipStream_t s, long long nnz) {
+                         hipStream_t s, long long nnz, const int *order) {
   if (nf <= 0 || p <= 0) return;
   const dim3 grid((unsigned)nf, (unsigned)ceil_div(p, 16));
   if (nnz > 512LL * nf)
     PGCN_LAUNCH(k_spmm_csc_bwd<1024>, grid, dim3(1024), 0, s, nf, p, ldg, csc_ptr, csc_row,
-                csc_pos, a, mask, mask_base, scale, cgrad, bgrad);
+                csc_pos, a, mask, mask_base, scale, cgrad, bgrad, order);
   else
     PGCN_LAUNCH(k_spmm_csc_bwd<256>, grid, dim3(256), 0, s, nf, p, ldg, csc_ptr, csc_row,
-                csc_pos, a, mask, mask_base, scale, cgrad, bgrad);
+                csc_pos, a, mask, mask_base, scale, cgrad, bgrad, order);
 }
 
 }  // namespace pgcn

@@ -263,11 +263,12 @@ void launch_spmm_csr(int m, int p, int ldc, const int *indptr, const int *indice
 void launch_spmm_csr_dual(int m, int p, int ldc, const int *indptr, const int *indices,
                           const float *a, const uint64_t *mask, long long mask_base, float scale,
                           const float *b, float *c, float *c2, hipStream_t s);
-// nnz: the entries of all nf columns (picks the chunk size; 0 = unknown: 256)
+// nnz: the entries of all nf columns (picks the chunk size; 0 = unknown: 256); order (optional):
+// the nf feature ids in the order their workgroups launch (descending column length)
 void launch_spmm_csc_bwd(int nf, int p, int ldg, const int *csc_ptr, const int *csc_row,
                          const int *csc_pos, const float *a, const uint64_t *mask,
                          long long mask_base, float scale, const float *cgrad, float *bgrad,
-                         hipStream_t s, long long nnz = 0);
+                         hipStream_t s, long long nnz = 0, const int *order = nullptr);
 
 void launch_dropout_mask(uint64_t *states, long long n_chunks, long long elem0,
                          long long elem_end, float p, uint64_t *mask, const void *table,
