@@ -35,6 +35,7 @@ extern int g_co_draw;               // host/gcn.cpp
 extern int g_sparse_dual;           // host/gcn.cpp
 extern int g_gs_item_iters;         // host/graph.cpp
 extern int g_gs_orig_cols;          // host/graph.cpp
+extern int g_gs16_gather;           // host/graph.cpp
 extern int g_parse_threads;         // host/data.cpp: pieces of the parallel text parse
 
 namespace {
@@ -701,6 +702,9 @@ int pgcn_debug_set(const char *key, int value) {
   } else if (!std::strcmp(key, "gs_orig_cols")) {
     if (!in(0, 1)) return PGCN_E_INVALID;
     pgcn::g_gs_orig_cols = value;
+  } else if (!std::strcmp(key, "gs16_gather")) {
+    if (!in(0, 1)) return PGCN_E_INVALID;
+    pgcn::g_gs16_gather = value;
   } else if (!std::strcmp(key, "sparse_dual")) {
     if (!in(0, 1)) return PGCN_E_INVALID;
     pgcn::g_sparse_dual = value;

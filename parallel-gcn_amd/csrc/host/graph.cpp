@@ -138,6 +138,8 @@ int g_gs_item_iters = 0;
 // "gs_orig_cols" (read per call): a column subset's unblocked plain GraphSum gathers the
 // input's own rows through the original column ids (1) instead of compacting them first (0)
 int g_gs_orig_cols = 1;
+// "gs16_gather" (read at schedule build): GraphSchedule::gather16 of the blocked d = 16 path
+int g_gs16_gather = 0;
 
 int DevGraph::column_blocks(int dim) {
   const int vec = (dim + 3) / 4;
@@ -298,6 +300,7 @@ DevGraph::Sched &DevGraph::schedule(int vec) {
   for (size_t b = 0; b + 1 < block_items.size(); b++)
     max_block = std::max(max_block, block_items[b + 1] - block_items[b]);
   sp->s.vec = vec;
+  sp->s.gather16 = nbc > 1 && vec == 4 ? g_gs16_gather : 0;
   sp->s.chunk = chunk;
   sp->s.nbc = nbc;
   sp->s.n_items = (int)items.size();

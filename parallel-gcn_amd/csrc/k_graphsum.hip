@@ -322,7 +322,7 @@ static void launch_vec(const GraphSchedule &s, const int *indices, const float *
     const dim3 grid((unsigned)(per_block * s.nbc + s.n_wide)), block(256);
     // (measured and removed, r01: a software-pipelined k_graphsum16, 132 VGPRs at 3 waves per
     // SIMD, slower)
-    if (VEC == 4 && s.nbc > 1)
+    if (VEC == 4 && s.nbc > 1 && s.gather16 == 0)
       PGCN_LAUNCH(k_graphsum16, grid, block, 0, st, s.items, s.block_items, s.nbc, indices,
                          vals, reinterpret_cast<const float4 *>(in), ld_in / 4,
                          reinterpret_cast<float4 *>(out), ld_out / 4,

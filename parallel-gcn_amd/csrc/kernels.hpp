@@ -49,6 +49,9 @@ struct GraphSchedule {
   // taken by the launch's first n_wide workgroups
   int n_wide = 0;
   const int4 *wide = nullptr;
+  // d = 16 on the blocked layout: 0 = k_graphsum16 (an item's 64-slot sub-chunks, a 16-slot run
+  // per neighbour sub-group), 1 = k_graphsum<4, 16> (sub-group nb takes slots nb, nb + 4, ...)
+  int gather16 = 0;
 };
 int graphsum_group_lanes(int vec);
 

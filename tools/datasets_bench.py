@@ -90,7 +90,7 @@ def launches_per_epoch(pg, ds, epochs=20):
 
 def cpu_rate(ds, reps):
     import bench
-    kind, times, _ = bench.cpu_baseline(ds, reps)
+    kind, times = bench.cpu_baseline(ds, reps)[:2]
     return kind, len(times) / sum(times)
 
 
