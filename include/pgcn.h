@@ -308,7 +308,7 @@ long long pgcn_partition_subgraph(int n, const int *indptr, const int *indices, 
 int pgcn_debug_rank_graph(int n, const int *indptr, const int *indices, int world, int rank,
                           int chunks, int chunk, pgcn_graph **out, int *rows, int *cols);
 /* Engine options (process-wide; most are read when an engine is built).  Each selects between
- * bit-identical or oracle-tested forms of the same reference epoch (18 keys, r05):
+ * bit-identical or oracle-tested forms of the same reference epoch (19 keys, r05):
  *   "train_ahead" 0/1, "eval_ax" 0/1, "split_cols" 0/1, "epoch_graph" 0/1, "mm_side" 0/1/2,
  *   "eval_tail" 0/1 (edge-cut between processes: the eval pass's last exchange and output
  *   layer beside the next epoch's first kernels, default 0),
@@ -324,7 +324,8 @@ int pgcn_debug_rank_graph(int n, const int *indptr, const int *indices, int worl
  *   by one workgroup, longer ones as 1), "gs_item_iters" 0/2/4/8/16/32 (group iterations per
  *   work item there; 0 (default): by shape, the shortest leaving <= 1,536 workgroup items),
  *   "gs_orig_cols" 0/1 (a column subset's plain GraphSum gathers through the original column
- *   ids instead of compacting its input, default 1);
+ *   ids instead of compacting its input, default 1), "gs16_gather" 0..2 (the blocked d = 16
+ *   gather kernel: 0 (default) by mean segment length, 1 k_graphsum16, 2 interleaved slots);
  * and one diagnostic, not reference-equivalent: "split_rows" 0/1 (the output layer's forward
  *   over the current split's rows only: stale logits elsewhere, which get_var refuses).
  * Returns PGCN_E_INVALID on an unknown key or on a value outside the key's range (nothing is

@@ -703,7 +703,7 @@ int pgcn_debug_set(const char *key, int value) {
     if (!in(0, 1)) return PGCN_E_INVALID;
     pgcn::g_gs_orig_cols = value;
   } else if (!std::strcmp(key, "gs16_gather")) {
-    if (!in(0, 1)) return PGCN_E_INVALID;
+    if (!in(0, 2)) return PGCN_E_INVALID;
     pgcn::g_gs16_gather = value;
   } else if (!std::strcmp(key, "sparse_dual")) {
     if (!in(0, 1)) return PGCN_E_INVALID;

@@ -619,6 +619,10 @@ void GCN::fuse_output_layer() {
   if (ce->input()->ld > 116 || mm->input()->rows != ce->input()->rows) return;
   ce->fused = mm;
   mm->fused_forward = true;
+  // the reassociated output layer: GraphSum -> Matmul -> loss, the GraphSum's backward reads
+  // the Matmul's input grad, which the fused kernel writes
+  auto *gs = n >= 3 ? dynamic_cast<GraphSum *>(modules[n - 3].get()) : nullptr;
+  if (gs && gs->output() == mm->input()) ce->dh_reader = gs;
 }
 
 // GraphSum -> ReLU(out) [-> Dropout(out)] in the module list: the ReLU and the Dropout run in

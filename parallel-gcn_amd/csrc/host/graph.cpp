@@ -138,7 +138,11 @@ int g_gs_item_iters = 0;
 // "gs_orig_cols" (read per call): a column subset's unblocked plain GraphSum gathers the
 // input's own rows through the original column ids (1) instead of compacting them first (0)
 int g_gs_orig_cols = 1;
-// "gs16_gather" (read at schedule build): GraphSchedule::gather16 of the blocked d = 16 path
+// "gs16_gather" (read at schedule build): the blocked d = 16 path's kernel (GraphSchedule::
+// gather16): 0 = by shape -- the interleaved k_graphsum<4, 16> when a row's segment in a column
+// block averages under 16 slots (r05 late, one call: reddit-11.6M, ~12 slots, 341 vs 595 us;
+// reddit-114M, ~60 slots, k_graphsum16 1,016 vs 1,089 us; profiles/r05/y, z), 1 = k_graphsum16,
+// 2 = the interleaved kernel
 int g_gs16_gather = 0;
 
 int DevGraph::column_blocks(int dim) {
@@ -300,7 +304,10 @@ DevGraph::Sched &DevGraph::schedule(int vec) {
   for (size_t b = 0; b + 1 < block_items.size(); b++)
     max_block = std::max(max_block, block_items[b + 1] - block_items[b]);
   sp->s.vec = vec;
-  sp->s.gather16 = nbc > 1 && vec == 4 ? g_gs16_gather : 0;
+  if (nbc > 1 && vec == 4) {
+    const bool short_segments = nnz_ < 16LL * kBlocks * std::max(n_rows_, 1);
+    sp->s.gather16 = g_gs16_gather == 2 || (g_gs16_gather == 0 && short_segments) ? 1 : 0;
+  }
   sp->s.chunk = chunk;
   sp->s.nbc = nbc;
   sp->s.n_items = (int)items.size();
@@ -395,6 +402,9 @@ std::unique_ptr<DevGraph> DevGraph::col_subset(const std::vector<int> &cols) con
   }
   g->col_map_.allocate(std::max<size_t>(cols.size(), 1));
   g->col_map_.upload(cols.empty() ? std::vector<int>{0} : cols);
+  g->col_pos_.allocate(pos.size());
+  g->col_pos_.upload(pos);
+  g->col_pos_rows_ = n_cols_;
   std::vector<int> ox(ix.size());
   for (size_t k = 0; k < ix.size(); k++) ox[k] = cols.empty() ? 0 : cols[(size_t)ix[k]];
   g->orig_indices_.allocate(ox.size() + 64);  // the same slack as indices_
@@ -536,6 +546,16 @@ float *DevGraph::ring_table(int dim, const float **next_scale) {
   return table_scratch();
 }
 
+float *DevGraph::ring_table_mapped(int dim, const float **next_scale, const int **pos,
+                                   int *pos_rows) {
+  if (dim > 16 || !uses_lds(dim) || table_owner_ || (col_map_ && !col_pos_rows_)) return nullptr;
+  if (!lds_) build_lds();
+  *next_scale = lds_->s.col_scale;
+  *pos = col_map_ ? col_pos_.get() : nullptr;
+  *pos_rows = col_map_ ? col_pos_rows_ : n_cols_;
+  return table_scratch();
+}
+
 void DevGraph::share_tables(DevGraph *owner) {
   PGCN_CHECK(owner && owner != this && !owner->table_owner_ && owner->n_cols_ == n_cols_ &&
                  owner->h_col_scale_ == h_col_scale_ && !owner->col_map_ == !col_map_,
@@ -581,7 +601,8 @@ void DevGraph::graphsum(const float *in, int ld_in, float *out, int ld_out, int 
     // d = 128 on reddit: 8 passes ~2.7 ms against ~7 ms for the gather kernel, whose 512-B
     // rows come from the Infinity Cache at ~7.7 TB/s
     const int ldm = std::min(ld_in, ld_out);
-    PGCN_CHECK(!prestaged || (dim <= 16 && !col_map), PGCN_E_INVALID,
+    // (a column subset's table prestaged through its row map: ring_table_mapped)
+    PGCN_CHECK(!prestaged || dim <= 16, PGCN_E_INVALID,
                "graphsum: prestaged input on a path without a ring table");
     const size_t table = (size_t)ceil_div(n_cols_, RING_SR) * RING_SR * 16;
     const int n_pass = ceil_div(dim, 16);

@@ -94,6 +94,10 @@ class DevGraph {
   // pass, no column map), for a producer's epilogue to fill (then graphsum(.., prestaged));
   // null when this graph does not take that path.  next_scale = the table's column scales.
   float *ring_table(int dim, const float **next_scale);
+  // ... of a column subset too: its input rows map to table rows through *pos (input row i ->
+  // table row pos[i], -1 outside the subset; *pos_rows input rows; null pos: the identity over
+  // the graph's columns), for the fused loss kernel's dH (XentTable)
+  float *ring_table_mapped(int dim, const float **next_scale, const int **pos, int *pos_rows);
   // graphsum() of this width can take an epilogue (one pass over the columns)
   bool epilogue_ok(int dim, int ld_in, int ld_out) const;
   // graphsum() of this width runs the LDS ring kernel (k_graphsum_ring)
@@ -152,6 +156,8 @@ class DevGraph {
   std::vector<float> h_row_scale_, h_col_scale_;
   // column subset: input row of compact column c (device), and the compacted input (plain path)
   DeviceBuffer<int> col_map_;
+  DeviceBuffer<int> col_pos_;  // input row -> compact column (-1: outside), col_pos_rows_ rows
+  int col_pos_rows_ = 0;
   DeviceBuffer<float> col_in_;
   // column subset, unblocked plain path: every slot's ORIGINAL column id, so the gather kernel
   // reads the caller's full input rows (no compacting launch; the same values, the same bits)

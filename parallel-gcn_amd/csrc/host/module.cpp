@@ -322,6 +322,24 @@ float4 *GraphSum::claim_forward_table(int rows, int ld, const float **scale) con
   return reinterpret_cast<float4 *>(t);
 }
 
+bool GraphSum::claim_backward_table(int rows, int ld, XentTable *t) const {
+  if (ctx->comm || !(g_fuse_epilogue & kFusePrestage) || dim != 16 || ld != 16 ||
+      out->ld != 16 || out->rows != rows)
+    return false;
+  DevGraph *g = backward_graph();
+  const float *sc = nullptr;
+  const int *pos = nullptr;
+  int pos_rows = 0;
+  float *tab = g ? g->ring_table_mapped(dim, &sc, &pos, &pos_rows) : nullptr;
+  if (!tab || pos_rows != rows) return false;
+  t->table = tab;
+  t->scale = sc;
+  t->pos = pos;
+  t->rows = pos_rows;
+  prestaged_bwd = true;
+  return true;
+}
+
 void GraphSum::stage_next(GsEpilogue &e, GraphSum *next, DevGraph *ng, bool fwd) const {
   if (!next || !ng || !(g_fuse_epilogue & kFusePrestage)) return;
   const float *sc = nullptr;
@@ -710,10 +728,14 @@ void CrossEntropyLoss::forward(bool training, const Stream &s) const {
         !ctx->mm_side &&
         tn_reduce_blocks_workspace(nb, fused->inner(), 48) <= ctx->gemm_workspace_bytes)
       dWp = static_cast<float *>(ctx->gemm_workspace);
+    // training: dH also to the ring table of the GraphSum backward that reads it
+    XentTable tb;
+    const bool staged = training && dH && dh_reader && fused->inner() == 16 &&
+                        dh_reader->claim_backward_table(Hv.rows, Hv.ld, &tb);
     launch_out_xent(Hv.dev_data.get(), Hv.ld, fused->inner(), Wv.dev_data.get(), Wv.ld,
                     logits->dev_data.get(), logits->ld, training ? logits->dev_grad.get() : nullptr,
                     ctx->truth, logits->rows, num_classes, ctx->count, training ? 1 : 0,
-                    ctx->xent_partials, s.get(), dH, Hv.ld, dWp);
+                    ctx->xent_partials, s.get(), dH, Hv.ld, dWp, staged ? &tb : nullptr);
     if (dWp)
       launch_tn_reduce_blocks(dWp, nb, fused->inner(), num_classes, 48, Wv.dev_grad.get(), Wv.ld,
                               s.get());

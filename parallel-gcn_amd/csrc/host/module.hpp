@@ -280,6 +280,10 @@ class GraphSum : public Module {
   // the ring table (and its scale) that call reads, marked as written by the producer
   // (prestaged_fwd); null when that call has none
   float4 *claim_forward_table(int rows, int ld, const float **scale) const;
+  // for the fused loss kernel writing this GraphSum's next backward input (out.grad, `rows` x
+  // 16, ld 16): that call's ring table, scale and row map (XentTable), marked as written by
+  // it (prestaged_bwd); false when that call has none (single GPU only)
+  bool claim_backward_table(int rows, int ld, XentTable *t) const;
 
  private:
   // mode (edge-cut output layer): 0 all rows, 1 forward over ctx->chunk_split_graphs (the
@@ -350,6 +354,9 @@ class CrossEntropyLoss : public Module {
   CrossEntropyLoss(shared_ptr<Variable> logits_, int num_classes_, ModuleContext *ctx_);
   // the output layer's Matmul whose forward this loss computes with its own (null: none)
   const Matmul *fused = nullptr;
+  // ... and the GraphSum whose backward reads that Matmul's input grad (the reassociated
+  // output layer's): the fused kernel also writes its prescaled table (claim_backward_table)
+  const GraphSum *dh_reader = nullptr;
   const Variable *input() const { return logits.get(); }
   void forward(bool training, const Stream &s) const override;
   void backward(const Stream &s) const override;

@@ -399,7 +399,7 @@ __device__ __forceinline__ void xent_tile(float *__restrict__ logits, int ld_rt,
                                                   const float *__restrict__ H, int ldh, int kh_rt,
                                                   const float *__restrict__ W, int ldw,
                                                   float *__restrict__ dH, int lddh,
-                                                  float *__restrict__ dWp) {
+                                                  float *__restrict__ dWp, const XentTable &tb) {
   // write_back 0: the shifted logits stay in LDS (the compact output layer's logits are read
   // by nobody after the loss; hpdga's in-place shift is kept where the variable is visible)
   extern __shared__ float smem[];
@@ -457,6 +457,15 @@ __device__ __forceinline__ void xent_tile(float *__restrict__ logits, int ld_rt,
   // with the block's first loads
   const int rq = ln >> 2, q = ln & 3;
   const int t = rq < wrows ? truth[wrow0 + rq] : -1;
+  // FUSED training with tb.table: the table row of the dH row this lane writes (row 4 gi + q of
+  // the wave's group, q = ii & 3), loaded with the first loads, and its scale once W is staged
+  int tb_p = -1;
+  float tb_s = 0.0f;
+  if (FUSED && tb.table) {
+    const int rr = 4 * gi + (ii & 3);
+    const long long row = wrow0 + rr;
+    tb_p = rr >= wrows ? -1 : (tb.pos ? tb.pos[row] : (row < tb.rows ? (int)row : -1));
+  }
   if constexpr (FUSED) {
     const long long grow = wrow0 + ii < n ? wrow0 + ii : n - 1;
     const float *hr = H + grow * (long long)ldh;
@@ -481,6 +490,7 @@ __device__ __forceinline__ void xent_tile(float *__restrict__ logits, int ld_rt,
     for (int k = wv; k < 16; k += XT / 64)
       for (int j = ln; j < ld; j += 64) wt[k * ld + j] = (k < kh && j < c) ? W[(long long)k * ldw + j] : 0.0f;
     __syncthreads();  // W staged (the only barrier before the block's final sums)
+    if (tb_p >= 0) tb_s = tb.scale[tb_p];
     XST(1);
     // logits of the wave's 16 rows on MFMA, as k_gemm_nn<3> computes them; lane holds
     // logits[4 gi + r][16 tt + ii] -> the tile
@@ -623,6 +633,25 @@ __device__ __forceinline__ void xent_tile(float *__restrict__ logits, int ld_rt,
           if (rr < wrows) dH[(wrow0 + rr) * (long long)lddh + ii] = acc[r];
         }
       }
+      if (tb.table) {
+        // k_ring_prescale's s_p * dH[i][4 v .. 4 v + 3] as one float4 at table row p = pos[i]:
+        // lane (gi, 4 v + q) takes row 4 gi + q's plane v from its quad (a 4 x 4 transpose in
+        // four shuffles: in round k lane s of the quad sends acc[(s - k) & 3] to lane (s - k) & 3)
+        const int q = ii & 3, v = ii >> 2, p = tb_p;
+        float o[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const int out_r = (q - k) & 3, in_c = (q + k) & 3;
+          const float send = out_r == 0 ? acc[0] : out_r == 1 ? acc[1] : out_r == 2 ? acc[2] : acc[3];
+          const float got = __shfl(send, (ln & ~3) | in_c, 64);
+#pragma unroll
+          for (int m = 0; m < 4; m++) o[m] = in_c == m ? got : o[m];
+        }
+        if (p >= 0)
+          reinterpret_cast<float4 *>(tb.table)[(long long)(p / RING_SR) * (4 * RING_SR) +
+                                               v * RING_SR + p % RING_SR] =
+              make_float4(o[0] * tb_s, o[1] * tb_s, o[2] * tb_s, o[3] * tb_s);
+      }
     }
     XST(6);
     // the output layer's weight grad, this block's share: partial [kh][48] = H^T grad over
@@ -702,11 +731,11 @@ __device__ __forceinline__ void xent_tile(float *__restrict__ logits, int ld_rt,
   float *__restrict__ logits, int ld, float *__restrict__ grad, const int *__restrict__ truth,   \
       int n, int c, int count, int training, float *__restrict__ partials, int write_back,       \
       const float *__restrict__ H, int ldh, int kh, const float *__restrict__ W, int ldw,        \
-      float *__restrict__ dH, int lddh, float *__restrict__ dWp
+      float *__restrict__ dH, int lddh, float *__restrict__ dWp, XentTable tb
 // the loss over given logits (61 VGPRs at 8 waves per SIMD would spill its copy registers)
 __global__ __launch_bounds__(XT) void k_xent_fwd(PGCN_XENT_ARGS) {
   xent_tile<false>(logits, ld, grad, truth, n, c, count, training, partials, write_back, H, ldh,
-                   kh, W, ldw, dH, lddh, dWp);
+                   kh, W, ldw, dH, lddh, dWp, tb);
 }
 // the fused output layer + loss at 8 waves per SIMD (<= 64 VGPRs, no spill; reddit training
 // call 45.0 -> 43.2 us, r03)
@@ -714,7 +743,7 @@ template <int CC, int LDC, int KH>
 __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(8))) void k_out_xent(
     PGCN_XENT_ARGS) {
   xent_tile<true, CC, LDC, KH>(logits, ld, grad, truth, n, c, count, training, partials,
-                               write_back, H, ldh, kh, W, ldw, dH, lddh, dWp);
+                               write_back, H, ldh, kh, W, ldw, dH, lddh, dWp, tb);
 }
 #undef PGCN_XENT_ARGS
 
@@ -906,13 +935,17 @@ void launch_xent_fwd(float *logits, int ld, float *grad, const int *truth, int n
   const size_t lds = (size_t)XR * xent_stride(ld) * sizeof(float);  // <= 64*124*4 = 31 KB
   PGCN_LAUNCH(k_xent_fwd, dim3(xent_blocks(n)), dim3(XT), lds, s, logits, ld, grad,
                      truth, n, c, count, training, partials, write_back, nullptr, 0, 0, nullptr, 0,
-                     nullptr, 0, nullptr);
+                     nullptr, 0, nullptr, XentTable{});
 }
 
 void launch_out_xent(const float *H, int ldh, int kh, const float *W, int ldw, float *logits,
                      int ld, float *grad, const int *truth, int n, int c, int count, int training,
-                     float *partials, hipStream_t s, float *dH, int lddh, float *dWp) {
+                     float *partials, hipStream_t s, float *dH, int lddh, float *dWp,
+                     const XentTable *tb) {
   note_path(KP_OUT_XENT);
+  const XentTable t = training && dH && tb ? *tb : XentTable{};
+  PGCN_CHECK(!t.table || (kh == 16 && t.scale), PGCN_E_INVALID,
+             "out_xent: a prescaled table of a 16-column dH");
   if (n <= 0) return;
   PGCN_CHECK(ld <= 116 && c <= ld && ld % 4 == 0 && kh >= 1 && kh <= 16, PGCN_E_INVALID,
              "out_xent: classes <= 116, hidden <= 16");
@@ -923,7 +956,7 @@ void launch_out_xent(const float *H, int ldh, int kh, const float *W, int ldw, f
 #define OUT_XENT(...)                                                                          \
   PGCN_LAUNCH((k_out_xent<__VA_ARGS__>), dim3(xent_blocks(n)), dim3(XT), lds, s, logits, ld, grad, \
               truth, n, c, count, training, partials, 1, H, ldh, kh, W, ldw,                     \
-              training ? dH : nullptr, lddh, training ? dWp : nullptr)
+              training ? dH : nullptr, lddh, training ? dWp : nullptr, t)
   if (c == 41 && ld == 44 && kh == 16)  // reddit (41 classes, hidden 16)
     OUT_XENT(41, 44, 16);
   else

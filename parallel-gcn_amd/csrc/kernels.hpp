@@ -50,7 +50,8 @@ struct GraphSchedule {
   int n_wide = 0;
   const int4 *wide = nullptr;
   // d = 16 on the blocked layout: 0 = k_graphsum16 (an item's 64-slot sub-chunks, a 16-slot run
-  // per neighbour sub-group), 1 = k_graphsum<4, 16> (sub-group nb takes slots nb, nb + 4, ...)
+  // per neighbour sub-group), 1 = k_graphsum<4, 16> (sub-group nb takes slots nb, nb + 4, ...:
+  // short segments keep every sub-group busy)
   int gather16 = 0;
 };
 int graphsum_group_lanes(int vec);
@@ -295,10 +296,20 @@ int xent_blocks(int n);
 // write_back, then its loss / grad / wrong count; bit-identical to launch_gemm_nn + xent.
 // Training with dH: also dH [n][lddh] = grad W^T (columns >= kh zero), bit-identical to the
 // Matmul backward's launch_gemm_nn(trans_b)
+// Training with tb.table: dH row i also goes, prescaled, to the ring table of the GraphSum
+// backward that reads dH -- tb.scale[p] * dH[i][0:16] at table row p = tb.pos[i] (skipped when
+// p < 0; null pos: p = i for i < tb.rows), k_ring_prescale's products in its slice-plane
+// layout, so that call skips its prescale launch
+struct XentTable {
+  float *table = nullptr;
+  const float *scale = nullptr;
+  const int *pos = nullptr;
+  int rows = 0;
+};
 void launch_out_xent(const float *H, int ldh, int kh, const float *W, int ldw, float *logits,
                      int ld, float *grad, const int *truth, int n, int c, int count, int training,
                      float *partials, hipStream_t s, float *dH = nullptr, int lddh = 0,
-                     float *dWp = nullptr);
+                     float *dWp = nullptr, const XentTable *tb = nullptr);
 // with dWp (training, <= 48 classes): per-block partials [xent_blocks(n)][kh][48] of W.grad =
 // H^T grad, reduced in block order into C [kh][ldc] (N = c columns) by:
 void launch_tn_reduce_blocks(float *partial, int n_blocks, int K, int N, int ldp, float *C, int ldc,

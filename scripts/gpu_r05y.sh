@@ -5,6 +5,8 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/r05y
 mkdir -p $O
+timeout -k 10 300 python3 -u -m pytest -m gpu -x -q --timeout 120 --timeout-method thread tests/test_gpu_kernels.py -k "blocked_gather16 or with_values" > $O/pytest.log 2>&1 || exit $?
+tail -1 $O/pytest.log
 timeout -k 10 300 python3 tools/gs_sparse.py 20 > $O/gs_sparse.json 2> $O/gs_sparse.err || exit $?
 cat $O/gs_sparse.json
 timeout -k 10 300 python3 bench.py --workload reddit-11.6M --no-extra --no-cpu-baseline > $O/b_ring.json 2> $O/b_ring.err || exit $?

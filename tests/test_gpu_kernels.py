@@ -256,6 +256,38 @@ def test_graphsum_lds_column_blocks(pgcn, blocks):
         pgcn.lib.pgcn_debug_set(b"lds_blocks", 0)
 
 
+@pytest.mark.parametrize("gather16", [0, 1, 2])
+def test_graphsum_blocked_gather16(pgcn, gather16):
+    """d = 16 on the plain path's XCD-blocked layout (the LDS ring switched off by lds_min_kb):
+    k_graphsum16 (gs16_gather 1) and k_graphsum<4, 16> with interleaved neighbour slots
+    (gs16_gather 2; 0 = by shape, here the interleaved one: 40 slots per row over 8 column
+    blocks), hub rows split over several items, against the oracle; the same bits on a
+    rerun."""
+    n, dim = 120000, 16
+    indptr, indices = random_graph(n, 40, seed=11, hubs=20, hub_deg=3000)
+    x = np.random.default_rng(5).standard_normal((n, dim)).astype(np.float32)
+    with helpers.knobs(pgcn, lds_min_kb=1 << 30, gs16_gather=gather16):
+        g = ctypes.c_void_p()
+        pgcn.check(pgcn.lib.pgcn_graph_create(n, helpers.ptr(indptr), helpers.ptr(indices),
+                                              ctypes.byref(g)), "graph_create")
+        xin = torch.from_numpy(x).to(DEV)
+        pgcn.reset_path_counts()
+        outs = []
+        for _ in range(2):
+            out = torch.full((n, dim), float("nan"), device=DEV)
+            pgcn.check(pgcn.lib.pgcn_graphsum(g, vp(xin), dim, vp(out), dim, dim, stream()), "gs")
+            outs.append(out)
+        torch.cuda.synchronize()
+        paths = pgcn.path_counts()
+        pgcn.lib.pgcn_graph_destroy(g)
+    assert paths["gs_ring"] == 0 and paths["gs_gather"] == 2, paths
+    ref = oracle_graphsum(indptr, indices, x, dim)
+    bound = abs_bound(indptr, indices, x, dim)
+    err = np.abs(outs[0].cpu().numpy() - ref)
+    assert (err <= 1e-5 * bound + 1e-30).all(), (err / (bound + 1e-30)).max()
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("dim,ld", [(128, 128), (41, 44), (24, 24)])
 def test_graphsum_lds_wide_rows(pgcn, dim, ld):
     """Rows wider than 16 on a graph that takes the LDS GraphSum: one 16-column LDS pass per

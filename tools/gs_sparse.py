@@ -1,7 +1,7 @@
 """d = 16 GraphSum on the report-comparable reddit-11.6M graph (232,965 nodes, 11.6 M undirected edges)
 through the C ABI, per path: the ring (default), the plain gather kernels with their per-XCD
 column blocks (k_graphsum16, and k_graphsum<4, 16> with interleaved neighbour slots: knob
-gs16_gather 1).  HIP events over
+gs16_gather 1 / 2).  HIP events over
 `calls` back-to-back calls; each path on a fresh graph object (schedules are cached per graph).
 usage: python3 tools/gs_sparse.py [calls] [undirected_edges]; one JSON line (GPU box)."""
 import ctypes
@@ -24,8 +24,8 @@ ip, ix = ds.graph_indptr, ds.graph_indices
 x = torch.randn(n, 16, device="cuda")
 o = torch.empty(n, 16, device="cuda")
 st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-PATHS = {"ring": {}, "plain_blocked": {"lds_min_kb": 1 << 30},
-         "plain_blocked_interleaved": {"lds_min_kb": 1 << 30, "gs16_gather": 1}}
+PATHS = {"ring": {}, "plain_blocked": {"lds_min_kb": 1 << 30, "gs16_gather": 1},
+         "plain_blocked_interleaved": {"lds_min_kb": 1 << 30, "gs16_gather": 2}}
 out = {"nodes": n, "nnz": int(ip[-1]), "calls": calls}
 ref = None
 for name, kn in PATHS.items():
