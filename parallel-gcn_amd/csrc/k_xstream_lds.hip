@@ -305,23 +305,43 @@ __global__ __launch_bounds__(64 * (XL_NN_LOADERS + XL_NN_CONSUMERS), 1) void k_x
       am = am * a_scale;
     }
     // lane holds C[16 rg + 4 g + r][i] (k_xstream_nn's epilogue)
+    float cv[4];
     if (i < ldc) {
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         const long long rr = rgi * 16 + 4 * g + r;
+        float c = acc[r];
+        if constexpr (!DUAL) {
+          if (epi.relu && !(c > 0.0f)) c = 0.0f;  // k_relu_fwd's test (NaN -> 0)
+        }
+        cv[r] = c;
         if (rr < M) {
-          float c = acc[r];
-          if constexpr (!DUAL) {
-            if (epi.relu && !(c > 0.0f)) c = 0.0f;  // k_relu_fwd's test (NaN -> 0)
-            if (epi.next_table) {  // k_ring_prescale of the stored value: s_r * C[r][i]
-              const long long sr = epi.next_sr;
-              float *tb = reinterpret_cast<float *>(epi.next_table + (rr / sr) * 4 * sr +
-                                                    (i >> 2) * sr + rr % sr);
-              tb[i & 3] = c * nsc[r];
-            }
-          }
           C[rr * ldc + i] = c;
           if constexpr (DUAL) C2[rr * ldc + i] = acc2[r];
+        }
+      }
+    }
+    if constexpr (!DUAL) {
+      if (epi.next_table) {
+        // k_ring_prescale of the stored values, s_r * C[r][4 v .. 4 v + 3], one float4 per
+        // lane: lane (g, 4 v + q) takes row 4 g + q's plane v from its quad (ldc = 16: every
+        // lane holds a column; a 4 x 4 transpose in four shuffles, as the fused loss kernel's)
+        const int q = i & 3, v = i >> 2;
+        float o[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const int out_r = (q - k) & 3, in_c = (q + k) & 3;
+          const float send = out_r == 0 ? cv[0] : out_r == 1 ? cv[1] : out_r == 2 ? cv[2] : cv[3];
+          const float got = __shfl(send, (lane & ~3) | in_c, 64);
+#pragma unroll
+          for (int m = 0; m < 4; m++) o[m] = in_c == m ? got : o[m];
+        }
+        const long long rr = rgi * 16 + 4 * g + q;
+        const float s = q == 0 ? nsc[0] : q == 1 ? nsc[1] : q == 2 ? nsc[2] : nsc[3];
+        if (rr < M) {
+          const long long sr = epi.next_sr;
+          epi.next_table[(rr / sr) * 4 * sr + v * sr + rr % sr] =
+              make_float4(o[0] * s, o[1] * s, o[2] * s, o[3] * s);
         }
       }
     }
@@ -476,6 +496,8 @@ void launch_xstream_nn_ring(int M, int N, int K, const float *A, int lda, const 
   const int ni = xl_ni(lda);
   const XlRing rg = xl_ring(lda, ni, XL_BT_BYTES);
   PGCN_CHECK(rg.nslot >= 2, PGCN_E_INVALID, "xstream ring: LDS");
+  PGCN_CHECK(!e.next_table || ldc == 16, PGCN_E_INVALID,
+             "xstream ring: a prescaled table from 16-column rows only");
   const long long n_rg = (M + 15) / 16;
   const dim3 grid((unsigned)std::min<long long>(n_rg, kCUs)),
       block(64 * (XL_NN_LOADERS + XL_NN_CONSUMERS));
