@@ -105,6 +105,18 @@ int pgcn_gemm_xstream_dual(int M, int N, int K, const float *A, int lda, const f
 int pgcn_gemm_tn_xstream(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
                          float *C, int ldc, const uint64_t *mask_nib, float a_scale,
                          void *workspace, void *stream);
+/* The same products with the flat bitmap itself (keep bit of A[m][k] at mask_base + m*K + k;
+ * mask_words uint64 words at mask, an even count), which the engine passes on the shapes the
+ * loader-wave kernels take (K in 577..640, lda = K rounded up to 4; others: PGCN_E_INVALID):
+ * their loader waves stage each 16-row group's bits beside its rows, no pgcn_mask_nibbles
+ * pass.  C2 NULL: the single product.  Bit-identical to the nibble forms with the nibbles of
+ * the same bitmap. */
+int pgcn_gemm_xstream_flat(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
+                           int trans_b, float *C, float *C2, int ldc, const uint64_t *mask,
+                           long long mask_base, long long mask_words, float a_scale, void *stream);
+int pgcn_gemm_tn_xstream_flat(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
+                              float *C, int ldc, const uint64_t *mask, long long mask_base,
+                              long long mask_words, float a_scale, void *workspace, void *stream);
 
 /* --- sparse X (SparseMatmul, src/module.cu:104-163) ----------------------------------- */
 /* c[i,:] = sum_jj drop(a[jj]) * b[indices[jj], :], CSR order (bit-exact vs hpdga). */

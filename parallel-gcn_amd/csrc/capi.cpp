@@ -284,6 +284,35 @@ int pgcn_gemm_tn_xstream(int M, int N, int K, const float *A, int lda, const flo
   });
 }
 
+int pgcn_gemm_xstream_flat(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
+                           int trans_b, float *C, float *C2, int ldc, const uint64_t *mask,
+                           long long mask_base, long long mask_words, float a_scale,
+                           void *stream) {
+  return guarded([&] {
+    PGCN_CHECK(A && B && C && mask && mask_words > 0 && mask_base >= 0 && M >= 0 && ldc >= N &&
+                   xstream_ring_ok(K, lda),
+               PGCN_E_INVALID, "gemm_xstream_flat args");
+    const XsMask fm{mask, mask_base, K, mask_words};
+    launch_xstream_nn(M, N, K, A, lda, B, ldb, trans_b, C, ldc, nullptr, a_scale,
+                      as_stream(stream), C2, nullptr, &fm);
+    PGCN_HIP(hipGetLastError());
+  });
+}
+
+int pgcn_gemm_tn_xstream_flat(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
+                              float *C, int ldc, const uint64_t *mask, long long mask_base,
+                              long long mask_words, float a_scale, void *workspace, void *stream) {
+  return guarded([&] {
+    PGCN_CHECK(A && G && C && workspace && mask && mask_words > 0 && mask_base >= 0 && M >= 0 &&
+                   ldc >= N && xstream_ring_ok(K, lda),
+               PGCN_E_INVALID, "gemm_tn_xstream_flat args");
+    const XsMask fm{mask, mask_base, K, mask_words};
+    launch_xstream_tn(M, N, K, A, lda, G, ldg, C, ldc, nullptr, a_scale, workspace,
+                      as_stream(stream), &fm);
+    PGCN_HIP(hipGetLastError());
+  });
+}
+
 int pgcn_spmm_csr(int m, int p, const int *indptr, const int *indices, const float *a,
                   const uint64_t *a_mask, float a_scale, const float *b, float *c, void *stream) {
   return guarded([&] {

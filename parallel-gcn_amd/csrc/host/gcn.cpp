@@ -254,7 +254,8 @@ void init_dropout_rng_range(DropoutRng &r, const uint64_t seed[2], unsigned long
   });
   r.states.allocate(st.size());
   r.states.upload(st);
-  r.mask.allocate((size_t)std::max(1LL, r.n_chunks) + 1);
+  // (+1, rounded up to an even count: the X-stream ring kernels stage the bitmap in 16-B pieces)
+  r.mask.allocate(((size_t)std::max(1LL, r.n_chunks) + 2) & ~(size_t)1);
   r.mask.zero();
 }
 

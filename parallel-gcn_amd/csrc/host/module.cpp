@@ -157,6 +157,10 @@ SparseMatmul::SparseMatmul(const DevFeatures *x_, shared_ptr<Variable> b_,
                            shared_ptr<Variable> c_, const Dropout *drop_, ModuleContext *ctx_)
     : x(x_), b(std::move(b_)), c(std::move(c_)), drop(drop_), ctx(ctx_) {}
 
+// The X-stream ring kernels (xstream_ring_ok) read the dropout bitmap as it was drawn (XsMask);
+// the register-streamed ones read the nibble layout k_mask_nibbles builds from it (x->maskT)
+static bool xs_flat(const DevFeatures *x) { return xstream_ring_ok(x->cols, x->ldx); }
+
 void SparseMatmul::forward(bool training, const Stream &s) const {
   last_training = training;
   const uint64_t *mask = training ? drop->state().mask.get() : nullptr;
@@ -217,15 +221,20 @@ void SparseMatmul::forward(bool training, const Stream &s) const {
     else
       drop->draw_ahead(s.get());
     const uint64_t *m = drop->mask_ahead();
-    launch_mask_nibbles(m, base, x->cols, x->rows, x->cols, x->maskT.get(), s.get());
+    const bool flat = xs_flat(x);
+    const XsMask fm{m, base, x->cols, (long long)drop->state().mask.size()};  // (ahead: same size)
+    if (!flat) launch_mask_nibbles(m, base, x->cols, x->rows, x->cols, x->maskT.get(), s.get());
     launch_xstream_nn(x->rows, b->cols, x->cols, x->x.get(), x->ldx, b->dev_data.get(), b->ld, 0,
-                      c->dev_data.get(), c->ld, x->maskT.get(), scale, s.get(), ahead.get());
+                      c->dev_data.get(), c->ld, flat ? nullptr : x->maskT.get(), scale, s.get(),
+                      ahead.get(), nullptr, flat ? &fm : nullptr);
     ahead_valid = true;
     return;
   }
   MmProfile prof(ctx, s.get(), x->dense ? 2.0 * x->rows * b->cols * x->cols : 0.0);
   if (x->dense && x->maskT) {  // X-stream kernels (N <= 16, K <= 640)
-    if (mask)
+    const bool flat = mask && xs_flat(x);
+    const XsMask fm{mask, base, x->cols, (long long)drop->state().mask.size()};
+    if (mask && !flat)
       launch_mask_nibbles(mask, base, x->cols, x->rows, x->cols, x->maskT.get(), s.get());
     XsEpilogue e;  // the first GraphSum's prescaled input, written beside c
     if ((g_fuse_epilogue & kFuseXstream) && consumer && (training || !eval_out)) {
@@ -233,8 +242,8 @@ void SparseMatmul::forward(bool training, const Stream &s) const {
       e.next_sr = RING_SR;
     }
     launch_xstream_nn(x->rows, b->cols, x->cols, x->x.get(), x->ldx, b->dev_data.get(), b->ld, 0,
-                      c->dev_data.get(), c->ld, mask ? x->maskT.get() : nullptr, scale, s.get(),
-                      nullptr, &e);
+                      c->dev_data.get(), c->ld, mask && !flat ? x->maskT.get() : nullptr, scale,
+                      s.get(), nullptr, &e, flat ? &fm : nullptr);
   } else if (x->dense) {
     // wide outputs: the mask in the nibble layout too (one pass over the bitmap; the wide
     // kernels then read one word per row and 4 steps, and the backward reuses it)
@@ -255,10 +264,12 @@ void SparseMatmul::backward(const Stream &s) const {
   const long long base = drop->state().mask_base;
   const float scale = drop->scale();
   MmProfile prof(ctx, s.get(), x->dense ? 2.0 * x->rows * b->cols * x->cols : 0.0);
-  if (x->dense && x->maskT) {  // the nibble mask of the last training forward
+  if (x->dense && x->maskT) {  // the mask of the last training forward (flat or nibbles)
+    const bool flat = mask && xs_flat(x);
+    const XsMask fm{mask, base, x->cols, (long long)drop->state().mask.size()};
     launch_xstream_tn(x->rows, b->cols, x->cols, x->x.get(), x->ldx, c->dev_grad.get(), c->ld,
-                      b->dev_grad.get(), b->ld, mask ? x->maskT.get() : nullptr, scale,
-                      ctx->gemm_workspace, s.get());
+                      b->dev_grad.get(), b->ld, mask && !flat ? x->maskT.get() : nullptr, scale,
+                      ctx->gemm_workspace, s.get(), flat ? &fm : nullptr);
   } else if (x->dense) {
     launch_gemm_tn(x->rows, b->cols, x->cols, x->x.get(), x->ldx, c->dev_grad.get(), c->ld,
                    b->dev_grad.get(), b->ld, mask, base, x->cols, scale, ctx->gemm_workspace,

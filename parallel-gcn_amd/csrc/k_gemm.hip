@@ -612,20 +612,24 @@ void launch_mask_nibbles(const uint64_t *mask, long long mask_base, long long ma
 
 void launch_xstream_nn(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
                        int trans_b, float *C, int ldc, const uint64_t *maskT, float a_scale,
-                       hipStream_t s, float *C2, const XsEpilogue *epi) {
+                       hipStream_t s, float *C2, const XsEpilogue *epi, const XsMask *flat) {
   const XsEpilogue none{};
+  const bool fl = flat && flat->bits;
   const XsEpilogue &e = epi ? *epi : none;
   PGCN_CHECK(!C2 || (!e.relu && !e.next_table && !e.bwd_drop && !e.bwd_relu), PGCN_E_INVALID,
              "xstream_nn: dual + epilogue");
   PGCN_CHECK(!e.next_table || (N <= 16 && ldc == 16), PGCN_E_INVALID,
              "xstream_nn: a staged table needs 16-column rows");
   PGCN_CHECK(xstream_ok(N, K), PGCN_E_INVALID, "xstream_nn: needs N <= 16, K <= 640");
-  PGCN_CHECK(!C2 || maskT, PGCN_E_INVALID, "xstream_nn: the dual product needs the mask");
+  PGCN_CHECK(!C2 || maskT || fl, PGCN_E_INVALID, "xstream_nn: the dual product needs the mask");
+  PGCN_CHECK(!fl || xstream_ring_ok(K, lda), PGCN_E_INVALID,
+             "xstream_nn: a flat mask on the ring kernels' shapes only");
   PGCN_CHECK(lda % 4 == 0 && lda >= K, PGCN_E_INVALID, "gemm: lda must be a multiple of 4 >= K");
   if (M <= 0) return;
   if (xstream_ring_ok(K, lda)) {
     PGCN_CHECK(!e.bwd_drop && !e.bwd_relu, PGCN_E_INVALID, "xstream_nn: backward tails on the ring form");
-    launch_xstream_nn_ring(M, N, K, A, lda, B, ldb, trans_b, C, ldc, maskT, a_scale, s, C2, e);
+    launch_xstream_nn_ring(M, N, K, A, lda, B, ldb, trans_b, C, ldc, maskT, a_scale, s, C2, e,
+                           flat);
     return;
   }
   note_path(KP_XS_NN);
@@ -810,14 +814,17 @@ void launch_tn_reduce_blocks(float *partial, int n_blocks, int K, int N, int ldp
 
 void launch_xstream_tn(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
                        float *C, int ldc, const uint64_t *maskT, float a_scale, void *workspace,
-                       hipStream_t s) {
+                       hipStream_t s, const XsMask *flat) {
   PGCN_CHECK(xstream_ok(N, K), PGCN_E_INVALID, "xstream_tn: needs N <= 16, K <= 640");
+  PGCN_CHECK(!(flat && flat->bits) || xstream_ring_ok(K, lda), PGCN_E_INVALID,
+             "xstream_tn: a flat mask on the ring kernels' shapes only");
   PGCN_CHECK(lda % 4 == 0 && lda >= K, PGCN_E_INVALID, "gemm_tn: lda must be a multiple of 4 >= K");
   const int blocks = xs_tn_blocks(M, K, lda);
   const TnPlan p = xs_tn_plan(K, blocks);
   float *partial = static_cast<float *>(workspace);
   if (M > 0 && xstream_ring_ok(K, lda)) {
-    launch_xstream_tn_ring(M, N, K, A, lda, G, ldg, maskT, a_scale, partial, XS_TN_BLOCKS, s);
+    launch_xstream_tn_ring(M, N, K, A, lda, G, ldg, maskT, a_scale, partial, XS_TN_BLOCKS, s,
+                           flat);
   } else if (M > 0) {
     note_path(KP_XS_TN);
 #define XTN_CASE(KC)                                                                           \

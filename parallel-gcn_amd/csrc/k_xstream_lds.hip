@@ -23,7 +23,8 @@
 //                         MFMAs, with their state (B of the NN product, the TN accumulators)
 //                         in registers.
 // The slot is the group's bytes as they lie in X (row stride lda / 4 chunks, lda = K rounded
-// up to 4), plus the bytes after it up to NI KB.  In the last group of X, lanes past the end
+// up to 4), plus the bytes after it up to NI KB, then (flat mask, r05 late) the group's keep
+// bits from the dropout bitmap as drawn (FLATM: no nibble-layout pass over the mask).  In the last group of X, lanes past the end
 // of X copy the group's first chunk instead, so every value in a slot is finite data except
 // the ld padding (k in [K, lda), possibly NaN): NN zeroes it in the slot before use (B is 0
 // for k >= K, so the finite values past K add exact zeros); in TN it reaches only output rows
@@ -70,17 +71,29 @@ struct XlRing {
   int off;    // LDS byte offset of slot 0 (NN: past B^T)
   int st;     // row stride in 16-B chunks (lda / 4 = ceil(K / 4))
   int nslot;  // slots in the ring (<= 4)
+  int sb;     // bytes per slot: the group's NI KB of X, then mb bytes of its keep bits
+  int mb;     // (flat mask) the group's bitmap bytes from a 16-B boundary, 256-B multiple; or 0
 };
 
 // DMA instructions (1 KB) per group for a row of lda floats: the group's 64 * lda bytes
 __host__ __device__ constexpr int xl_ni(int lda) { return (64 * lda + 1023) / 1024; }
 
-XlRing xl_ring(int lda, int ni, int off) {
+// mask_ld > 0: the keep bits come as the flat bitmap (XsMask, mask_ld bits per row), staged
+// with the group: 16 rows' bits from the 16-B boundary below the first (<= 15 B ahead), 1 B
+// of slack, rounded up to 256 B (reddit: 1,220 -> 1,280 B)
+XlRing xl_ring(int lda, int ni, int off, long long mask_ld = 0) {
   XlRing r;
   r.off = off;
   r.st = lda / 4;
-  r.nslot = std::min(4, (XL_LDS - XL_FLAGS - off) / (ni * 1024));
+  r.mb = mask_ld > 0 ? (int)((15 + (16 * mask_ld + 7) / 8 + 1 + 255) / 256 * 256) : 0;
+  r.sb = ni * 1024 + r.mb;
+  r.nslot = std::min(4, (XL_LDS - XL_FLAGS - off) / r.sb);
   return r;
+}
+
+// byte offset (16-B aligned) in the bitmap of the first keep bit of group row0's rows
+__device__ __forceinline__ long long xl_mask_byte0(const XsMask &mk, long long row0) {
+  return ((mk.base + row0 * mk.ld) >> 3) & ~15LL;
 }
 
 // keep bit t of `bits` (as 0 / all ones by a 1-bit signed field extract) masks element t, then
@@ -124,16 +137,20 @@ __device__ __forceinline__ void xl_dma4(const char *gsrc, unsigned lds_dst) {
 
 // Loader wave `wave` of NL: groups wave, wave + NL, ... into slot t % nslot, NI pieces
 // each; a consumer per group releases the slot by storing t + 1 into freed.
-template <int NI, int NL>
+// FLATM: then the group's keep bits (rg.mb bytes of the flat bitmap from xl_mask_byte0) behind
+// its X in the slot, by up to two more LDS-DMA instructions (lanes past the bitmap's end copy
+// its first chunk: bits of rows past M, which no output reads)
+template <int NI, int NL, bool FLATM>
 __device__ __forceinline__ void xl_load(const float *__restrict__ A, int lda, long long M, int T,
                                         int wave, int lane, const XlRing &rg, char *lds,
-                                        unsigned *ready, unsigned *freed) {
-  static_assert(NI < 64, "vmcnt counts at most 63");
+                                        unsigned *ready, unsigned *freed, const XsMask &mk) {
+  constexpr int NM = FLATM ? 2 : 0;  // mask pieces per group (rg.mb <= 2 KB)
+  static_assert(NI + NM < 64, "vmcnt counts at most 63");
   __builtin_amdgcn_s_setprio(3);
   wave = __builtin_amdgcn_readfirstlane(wave);  // uniform (the LDS-DMA destination is an SGPR)
   const unsigned base = __builtin_amdgcn_readfirstlane(
       (unsigned)reinterpret_cast<size_t>((__attribute__((address_space(3))) char *)lds));
-  const unsigned slot_bytes = NI * 1024;
+  const unsigned slot_bytes = (unsigned)rg.sb;
   const long long x_bytes = M * (long long)lda * 4;
   auto publish = [&](int u) {
     if (lane == 0) __atomic_store_n(ready + u % rg.nslot, (unsigned)(u + 1), __ATOMIC_RELAXED);
@@ -168,11 +185,23 @@ __device__ __forceinline__ void xl_load(const float *__restrict__ A, int lda, lo
         glds16_nt(blk + (off < left ? off : 0), dst + (unsigned)(q * 1024));
       }
     }
+    if constexpr (FLATM) {
+      const long long byte0 = xl_mask_byte0(mk, (blockIdx.x + (long long)t * gridDim.x) * 16);
+      const char *mb = reinterpret_cast<const char *>(mk.bits);
+      const long long mbytes = mk.words * 8;
+#pragma unroll
+      for (int q = 0; q < NM; q++) {
+        const long long off = byte0 + q * 1024 + lane * 16;
+        const char *src = mb + (off + 16 <= mbytes ? off : 0);
+        // (the second piece: only the lanes inside rg.mb; one instruction either way)
+        if (q * 1024 + lane * 16 < rg.mb) glds16_nt(src, dst + (unsigned)(NI * 1024 + q * 1024));
+      }
+    }
     // two groups in flight: the previous one lands while this one's DMAs are issued (at most
-    // NI of this group's pieces still counted; r04: X-stream passes 339 -> 329 us per epoch,
-    // most of it on TN, whose single loader had one group in flight)
+    // NI (+ NM) of this group's pieces still counted; r04: X-stream passes 339 -> 329 us per
+    // epoch, most of it on TN, whose single loader had one group in flight)
     if (pend >= 0) {
-      asm volatile("s_waitcnt vmcnt(%c0)" ::"n"(NI) : "memory");
+      asm volatile("s_waitcnt vmcnt(%c0)" ::"n"(NI + NM) : "memory");
       publish(pend);
     }
     pend = t;
@@ -194,12 +223,17 @@ __device__ __forceinline__ void xl_release(unsigned *freed, int slot, int t, int
 // group holds B[16 s + 4 g + t][i] for every step s (registers) and feeds MFMA t of step s with
 // X[row i][16 s + 4 g + t] -- k_xstream_nn's feed and order, so the same bits (up to the sign
 // of zero products: see xl_apply4).  B^T sits in LDS ahead of the ring (as in k_xstream_nn).
-template <int NI, bool MASKED, bool DUAL, bool FOLD>
+// FLATM (with MASKED): the keep bits from the flat bitmap `mk`, staged in the slot by the loader
+// (no nibble-layout pass): lane (i, g) forms its row's bits as ten 64-bit words W[c] = row bits
+// 64 c .. 64 c + 63 (v_alignbit from the slot's dwords), and step s's nibble is bits
+// 16 (s & 3) + 4 g .. + 3 of W[s >> 2] -- the nibble maskT[row][4 (s & 3) + g] holds at 4 (s >> 2)
+template <int NI, bool MASKED, bool DUAL, bool FOLD, bool FLATM>
 __global__ __launch_bounds__(64 * (XL_NN_LOADERS + XL_NN_CONSUMERS), 1) void k_xs_nn_ring(
     int M, int N, int K, const float *__restrict__ A, int lda, const float *__restrict__ B,
     int ldb, int trans_b, float *__restrict__ C, int ldc, const uint64_t *__restrict__ maskT,
-    float a_scale, float *__restrict__ C2, XsEpilogue epi, XlRing rg) {
+    float a_scale, float *__restrict__ C2, XsEpilogue epi, XlRing rg, XsMask mk) {
   static_assert(!DUAL || MASKED, "dual: the second product is the masked one");
+  static_assert(!FLATM || MASKED, "a flat mask is a mask");
   constexpr int NS = 4 * XL_KC;
   __shared__ __attribute__((aligned(1024))) char lds[XL_LDS];
   unsigned *const ready = reinterpret_cast<unsigned *>(lds + XL_LDS - XL_FLAGS);
@@ -219,10 +253,11 @@ __global__ __launch_bounds__(64 * (XL_NN_LOADERS + XL_NN_CONSUMERS), 1) void k_x
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int T = xl_groups(M);
   if (wave < XL_NN_LOADERS) {
-    xl_load<NI, XL_NN_LOADERS>(A, lda, M, T, wave, lane, rg, lds, ready, freed);
+    xl_load<NI, XL_NN_LOADERS, FLATM>(A, lda, M, T, wave, lane, rg, lds, ready, freed, mk);
     return;
   }
   const int cid = wave - XL_NN_LOADERS, g = lane >> 4, i = lane & 15;
+  constexpr bool NIB = MASKED && !FLATM;  // keep bits from maskT (prefetched a group ahead)
   const float *bl = reinterpret_cast<const float *>(lds) + i * XL_BS + 4 * g;
   auto load_mask = [&](int t, uint64_t(&m)[4]) {  // keep bits of the lane's row of group t
     long long row = (blockIdx.x + (long long)t * gridDim.x) * 16 + i;
@@ -233,7 +268,7 @@ __global__ __launch_bounds__(64 * (XL_NN_LOADERS + XL_NN_CONSUMERS), 1) void k_x
   // group t with its keep bits in mw; the next group's go to mwn (two static buffers that
   // alternate: a copy would wait for the prefetch)
   auto group = [&](int t, const uint64_t(&mw)[4], uint64_t(&mwn)[4]) {
-    if (MASKED && t + XL_NN_CONSUMERS < T) load_mask(t + XL_NN_CONSUMERS, mwn);
+    if (NIB && t + XL_NN_CONSUMERS < T) load_mask(t + XL_NN_CONSUMERS, mwn);
     const long long rgi = blockIdx.x + (long long)t * gridDim.x;
     // the epilogue's row scales, loaded before the slot wait (whose memory clobber keeps them
     // here) so they land during the MFMAs: loaded at their use, each load waited for alone
@@ -250,7 +285,7 @@ __global__ __launch_bounds__(64 * (XL_NN_LOADERS + XL_NN_CONSUMERS), 1) void k_x
     }
     const int slot = t % rg.nslot;
     lds_wait_ge(ready + slot, (unsigned)(t + 1));
-    char *const sb = lds + rg.off + slot * (NI * 1024);
+    char *const sb = lds + rg.off + slot * rg.sb;
     if (K & 3) {  // the ld padding k >= K of each row's last chunk (may be NaN)
       if (lane < 16) {
         float *pc = reinterpret_cast<float *>(sb + (lane * rg.st + rg.st - 1) * 16);
@@ -267,6 +302,21 @@ __global__ __launch_bounds__(64 * (XL_NN_LOADERS + XL_NN_CONSUMERS), 1) void k_x
     for (int s = 0; s < NS; s++)
       xa[s] = (s < XL_S0 || 16 * s < K) ? *reinterpret_cast<const float4 *>(a + 64 * s)
                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+    unsigned wl[XL_KC], wh[XL_KC];  // FLATM: the row's keep bits, W[c] = wh[c]:wl[c]
+    if constexpr (FLATM) {
+      const long long row0 = rgi * 16;
+      const long long bit = mk.base + (row0 + i) * mk.ld - 8 * xl_mask_byte0(mk, row0);
+      const unsigned *dw = reinterpret_cast<const unsigned *>(sb + NI * 1024) + (bit >> 5);
+      const unsigned sh = (unsigned)bit & 31u;
+      unsigned d[2 * XL_KC + 1];
+#pragma unroll
+      for (int e = 0; e < 2 * XL_KC + 1; e++) d[e] = dw[e];
+#pragma unroll
+      for (int c = 0; c < XL_KC; c++) {
+        wl[c] = __builtin_amdgcn_alignbit(d[2 * c + 1], d[2 * c], sh);
+        wh[c] = __builtin_amdgcn_alignbit(d[2 * c + 2], d[2 * c + 1], sh);
+      }
+    }
     xl_release(freed, slot, t, lane);
     floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f}, acc2 = floatx4{0.f, 0.f, 0.f, 0.f};
 #if PGCN_XS_CHAINS == 2
@@ -285,7 +335,10 @@ __global__ __launch_bounds__(64 * (XL_NN_LOADERS + XL_NN_CONSUMERS), 1) void k_x
         acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x.z, bb.z, acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x.w, bb.w, acc, 0, 0, 0);
       }
-      if constexpr (MASKED)
+      if constexpr (FLATM)
+        xl_apply4<FOLD>(x, __builtin_amdgcn_ubfe((s & 2) ? wh[s >> 2] : wl[s >> 2],
+                                                 16 * (s & 1) + 4 * g, 4), a_scale);
+      else if constexpr (MASKED)
         xl_apply4<FOLD>(x, (uint32_t)(mw[s & 3] >> (4 * (s >> 2))) & 0xfu, a_scale);
 #if PGCN_XS_CHAINS == 2
       floatx4 &am = DUAL ? acc2 : ((s & 1) ? acch : acc);
@@ -347,7 +400,7 @@ __global__ __launch_bounds__(64 * (XL_NN_LOADERS + XL_NN_CONSUMERS), 1) void k_x
     }
   };
   uint64_t mwa[4] = {0, 0, 0, 0}, mwb[4] = {0, 0, 0, 0};
-  if (MASKED && cid < T) load_mask(cid, mwa);
+  if (NIB && cid < T) load_mask(cid, mwa);
   for (int t = cid; t < T; t += 2 * XL_NN_CONSUMERS) {
     group(t, mwa, mwb);
     if (t + XL_NN_CONSUMERS < T) group(t + XL_NN_CONSUMERS, mwb, mwa);
@@ -358,11 +411,13 @@ __global__ __launch_bounds__(64 * (XL_NN_LOADERS + XL_NN_CONSUMERS), 1) void k_x
 // A group is 4 steps of 4 rows; consumer lane (i, g) feeds MFMA (c, t) of step q with
 // X[row 4q + g][64 c + 4 i + t] and G[row 4q + g][i] (k_xstream_tn's feed); the two consumers'
 // accumulators (groups t = c mod 3 for consumer c) are added in consumer order at the end.
-template <int NI, bool MASKED, bool FOLD>
+template <int NI, bool MASKED, bool FOLD, bool FLATM>
 __global__ __launch_bounds__(64 * (XL_TN_LOADERS + XL_TN_CONSUMERS), 1) void k_xs_tn_ring(
     int M, int N, int K, const float *__restrict__ A, int lda, const float *__restrict__ G,
     int ldg, const uint64_t *__restrict__ maskT, float a_scale, float *__restrict__ partial,
-    XlRing rg) {
+    XlRing rg, XsMask mk) {
+  static_assert(!FLATM || MASKED, "a flat mask is a mask");
+  constexpr bool NIB = MASKED && !FLATM;
   constexpr int KC = XL_KC;
   __shared__ __attribute__((aligned(1024))) char lds[XL_LDS];
   unsigned *const ready = reinterpret_cast<unsigned *>(lds + XL_LDS - XL_FLAGS);
@@ -379,7 +434,7 @@ __global__ __launch_bounds__(64 * (XL_TN_LOADERS + XL_TN_CONSUMERS), 1) void k_x
 #pragma unroll
     for (int t = 0; t < 4; t++) acc[c][t] = floatx4{0.f, 0.f, 0.f, 0.f};
   if (wave < XL_TN_LOADERS) {
-    xl_load<NI, XL_TN_LOADERS>(A, lda, M, T, wave, lane, rg, lds, ready, freed);
+    xl_load<NI, XL_TN_LOADERS, FLATM>(A, lda, M, T, wave, lane, rg, lds, ready, freed, mk);
   } else {
     const int cid = wave - XL_TN_LOADERS;
     // dZ and keep bits of group t, raw: unconditional loads whose values are first used a
@@ -392,7 +447,7 @@ __global__ __launch_bounds__(64 * (XL_TN_LOADERS + XL_TN_CONSUMERS), 1) void k_x
         const long long mr = row0 + 4 * q + g;
         const long long row = mr < M ? mr : M - 1;
         bv[q] = G[row * ldg + (i < N ? i : 0)];
-        if constexpr (MASKED) m[q] = maskT[row * 16 + i];
+        if constexpr (NIB) m[q] = maskT[row * 16 + i];
       }
     };
     // group t with dZ / keep bits in bj / mw, the next group's into bjn / mwn (alternating
@@ -408,13 +463,36 @@ __global__ __launch_bounds__(64 * (XL_TN_LOADERS + XL_TN_CONSUMERS), 1) void k_x
       for (int q = 0; q < 4; q++)
         bj[q] = (row0 + 4 * q + g < M && i < N) ? (MASKED && FOLD ? bv[q] * a_scale : bv[q]) : 0.0f;
       // the group's fragments into registers, then the slot goes back to the loader
-      const char *sp = lds + rg.off + slot * (NI * 1024) + i * 16;
+      const char *sp = lds + rg.off + slot * rg.sb + i * 16;
       float4 xa[4][KC];
 #pragma unroll
       for (int q = 0; q < 4; q++)
 #pragma unroll
         for (int c = 0; c < KC; c++)
           xa[q][c] = *reinterpret_cast<const float4 *>(sp + (4 * q + g) * rg.st * 16 + 256 * c);
+      // FLATM: the nibbles maskT[row][i] holds (c: bits 64 c + 4 i .. + 3 of the row), from the
+      // keep bits the loader staged behind the group's X
+      uint64_t mf[4];
+      if constexpr (FLATM) {
+        const unsigned *dw = reinterpret_cast<const unsigned *>(lds + rg.off + slot * rg.sb + NI * 1024);
+        const long long b0 = mk.base - 8 * xl_mask_byte0(mk, row0) + 4 * i;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const long long bit = b0 + (row0 + 4 * q + g) * mk.ld;
+          const unsigned *d = dw + (bit >> 5);
+          const unsigned sh = (unsigned)bit & 31u;
+          unsigned lo = 0, hi = 0;
+#pragma unroll
+          for (int c = 0; c < KC; c++) {
+            const unsigned nib = __builtin_amdgcn_alignbit(d[2 * c + 1], d[2 * c], sh) & 0xfu;
+            if (c < 8)
+              lo |= nib << (4 * c);
+            else
+              hi |= nib << (4 * (c - 8));
+          }
+          mf[q] = ((uint64_t)hi << 32) | lo;
+        }
+      }
       xl_release(freed, slot, t, lane);
 #pragma unroll
       for (int q = 0; q < 4; q++) {
@@ -425,7 +503,10 @@ __global__ __launch_bounds__(64 * (XL_TN_LOADERS + XL_TN_CONSUMERS), 1) void k_x
 #pragma unroll
         for (int c = 0; c < KC; c++) {
           float4 x = xa[q][c];
-          if constexpr (MASKED) xl_apply4<FOLD>(x, (uint32_t)(mw[q] >> (4 * c)) & 0xfu, a_scale);
+          if constexpr (FLATM)
+            xl_apply4<FOLD>(x, (uint32_t)(mf[q] >> (4 * c)) & 0xfu, a_scale);
+          else if constexpr (MASKED)
+            xl_apply4<FOLD>(x, (uint32_t)(mw[q] >> (4 * c)) & 0xfu, a_scale);
           acc[c][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(x.x, bj[q], acc[c][0], 0, 0, 0);
           acc[c][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(x.y, bj[q], acc[c][1], 0, 0, 0);
           acc[c][2] = __builtin_amdgcn_mfma_f32_16x16x4f32(x.z, bj[q], acc[c][2], 0, 0, 0);
@@ -489,72 +570,88 @@ bool xstream_ring_ok(int K, int lda) {
 
 void launch_xstream_nn_ring(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
                             int trans_b, float *C, int ldc, const uint64_t *maskT, float a_scale,
-                            hipStream_t s, float *C2, const XsEpilogue &e) {
+                            hipStream_t s, float *C2, const XsEpilogue &e, const XsMask *flat) {
   note_path(KP_XS_NN_RING);
   PGCN_CHECK(xstream_ring_ok(K, lda) && N <= 16 && ldc <= 16, PGCN_E_INVALID,
              "xstream ring: K in 577..640, lda = K rounded to 4, N <= 16");
+  const XsMask mk = flat && flat->bits ? *flat : XsMask{};
+  PGCN_CHECK(!mk.bits || (!maskT && mk.ld >= K && mk.words > 0 && mk.words % 2 == 0),
+             PGCN_E_INVALID,
+             "xstream ring: one mask, the flat one of >= K bits per row in whole 16-B pieces");
   const int ni = xl_ni(lda);
-  const XlRing rg = xl_ring(lda, ni, XL_BT_BYTES);
+  const XlRing rg = xl_ring(lda, ni, XL_BT_BYTES, mk.bits ? mk.ld : 0);
   PGCN_CHECK(rg.nslot >= 2, PGCN_E_INVALID, "xstream ring: LDS");
+  PGCN_CHECK(!mk.bits || (rg.mb > 1024 && rg.mb <= 2048), PGCN_E_INVALID,
+             "xstream ring: the staged keep bits take two LDS-DMA pieces");
   PGCN_CHECK(!e.next_table || ldc == 16, PGCN_E_INVALID,
              "xstream ring: a prescaled table from 16-column rows only");
   const long long n_rg = (M + 15) / 16;
   const dim3 grid((unsigned)std::min<long long>(n_rg, kCUs)),
       block(64 * (XL_NN_LOADERS + XL_NN_CONSUMERS));
   const bool fold = xl_pow2(a_scale);
+  const bool masked = maskT || mk.bits;
+#define XNR_LAUNCH(NI, MS, DU, FO, FL)                                                          \
+  PGCN_LAUNCH((k_xs_nn_ring<NI, MS, DU, FO, FL>), grid, block, 0, s, M, N, K, A, lda, B, ldb,   \
+              trans_b, C, ldc, maskT, a_scale, C2, e, rg, mk)
 #define XNR_CASE(NI)                                                                           \
   case NI:                                                                                     \
-    if (C2 && fold)                                                                            \
-      PGCN_LAUNCH((k_xs_nn_ring<NI, true, true, true>), grid, block, 0, s, M, N, K, A,   \
-                         lda, B, ldb, trans_b, C, ldc, maskT, a_scale, C2, e, rg);             \
-    else if (C2)                                                                               \
-      PGCN_LAUNCH((k_xs_nn_ring<NI, true, true, false>), grid, block, 0, s, M, N, K, A,  \
-                         lda, B, ldb, trans_b, C, ldc, maskT, a_scale, C2, e, rg);             \
-    else if (maskT && fold)                                                                    \
-      PGCN_LAUNCH((k_xs_nn_ring<NI, true, false, true>), grid, block, 0, s, M, N, K, A,  \
-                         lda, B, ldb, trans_b, C, ldc, maskT, a_scale, nullptr, e, rg);        \
-    else if (maskT)                                                                            \
-      PGCN_LAUNCH((k_xs_nn_ring<NI, true, false, false>), grid, block, 0, s, M, N, K, A, \
-                         lda, B, ldb, trans_b, C, ldc, maskT, a_scale, nullptr, e, rg);        \
-    else                                                                                       \
-      PGCN_LAUNCH((k_xs_nn_ring<NI, false, false, false>), grid, block, 0, s, M, N, K,   \
-                         A, lda, B, ldb, trans_b, C, ldc, maskT, a_scale, nullptr, e, rg);     \
+    if (!masked)                                                                               \
+      XNR_LAUNCH(NI, false, false, false, false);                                              \
+    else if (mk.bits) {                                                                        \
+      if (C2 && fold) XNR_LAUNCH(NI, true, true, true, true);                                  \
+      else if (C2) XNR_LAUNCH(NI, true, true, false, true);                                    \
+      else if (fold) XNR_LAUNCH(NI, true, false, true, true);                                  \
+      else XNR_LAUNCH(NI, true, false, false, true);                                           \
+    } else {                                                                                   \
+      if (C2 && fold) XNR_LAUNCH(NI, true, true, true, false);                                 \
+      else if (C2) XNR_LAUNCH(NI, true, true, false, false);                                   \
+      else if (fold) XNR_LAUNCH(NI, true, false, true, false);                                 \
+      else XNR_LAUNCH(NI, true, false, false, false);                                          \
+    }                                                                                          \
     break;
   switch (ni) {
     XNR_CASE(37) XNR_CASE(38) XNR_CASE(39) XNR_CASE(40)
     default: PGCN_CHECK(false, PGCN_E_INVALID, "xstream ring: no kernel for this row width");
   }
 #undef XNR_CASE
+#undef XNR_LAUNCH
 }
 
 void launch_xstream_tn_ring(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
                             const uint64_t *maskT, float a_scale, float *partial, int n_blocks,
-                            hipStream_t s) {
+                            hipStream_t s, const XsMask *flat) {
   note_path(KP_XS_TN_RING);
   PGCN_CHECK(xstream_ring_ok(K, lda) && N <= 16, PGCN_E_INVALID,
              "xstream ring: K in 577..640, lda = K rounded to 4, N <= 16");
+  const XsMask mk = flat && flat->bits ? *flat : XsMask{};
+  PGCN_CHECK(!mk.bits || (!maskT && mk.ld >= K && mk.words > 0 && mk.words % 2 == 0),
+             PGCN_E_INVALID,
+             "xstream ring: one mask, the flat one of >= K bits per row in whole 16-B pieces");
   const int ni = xl_ni(lda);
-  const XlRing rg = xl_ring(lda, ni, 0);
+  const XlRing rg = xl_ring(lda, ni, 0, mk.bits ? mk.ld : 0);
+  PGCN_CHECK(rg.nslot >= 2, PGCN_E_INVALID, "xstream ring: LDS");
+  PGCN_CHECK(!mk.bits || (rg.mb > 1024 && rg.mb <= 2048), PGCN_E_INVALID,
+             "xstream ring: the staged keep bits take two LDS-DMA pieces");
   const dim3 grid((unsigned)n_blocks),
       block(64 * (XL_TN_LOADERS + XL_TN_CONSUMERS));  // every block writes its partial
   const bool fold = xl_pow2(a_scale);
+#define XTR_LAUNCH(NI, MS, FO, FL)                                                              \
+  PGCN_LAUNCH((k_xs_tn_ring<NI, MS, FO, FL>), grid, block, 0, s, M, N, K, A, lda, G, ldg,      \
+              maskT, a_scale, partial, rg, mk)
 #define XTR_CASE(NI)                                                                           \
   case NI:                                                                                     \
-    if (maskT && fold)                                                                         \
-      PGCN_LAUNCH((k_xs_tn_ring<NI, true, true>), grid, block, 0, s, M, N, K, A, lda, G, \
-                         ldg, maskT, a_scale, partial, rg);                                    \
-    else if (maskT)                                                                            \
-      PGCN_LAUNCH((k_xs_tn_ring<NI, true, false>), grid, block, 0, s, M, N, K, A, lda,   \
-                         G, ldg, maskT, a_scale, partial, rg);                                 \
-    else                                                                                       \
-      PGCN_LAUNCH((k_xs_tn_ring<NI, false, false>), grid, block, 0, s, M, N, K, A, lda,  \
-                         G, ldg, maskT, a_scale, partial, rg);                                 \
+    if (mk.bits && fold) XTR_LAUNCH(NI, true, true, true);                                     \
+    else if (mk.bits) XTR_LAUNCH(NI, true, false, true);                                       \
+    else if (maskT && fold) XTR_LAUNCH(NI, true, true, false);                                 \
+    else if (maskT) XTR_LAUNCH(NI, true, false, false);                                        \
+    else XTR_LAUNCH(NI, false, false, false);                                                  \
     break;
   switch (ni) {
     XTR_CASE(37) XTR_CASE(38) XTR_CASE(39) XTR_CASE(40)
     default: PGCN_CHECK(false, PGCN_E_INVALID, "xstream ring: no kernel for this row width");
   }
 #undef XTR_CASE
+#undef XTR_LAUNCH
 }
 
 }  // namespace pgcn

@@ -172,20 +172,30 @@ struct XsEpilogue {
   const float *next_scale = nullptr;
   int next_sr = 0;
 };
+// The flat dropout bitmap of X [M][K] (keep bit of X[m][k] at bit base + m * ld + k, the
+// element order rng.cpp draws), which the X-stream ring kernels read in place of the nibble
+// layout: their loader waves stage each 16-row group's bits beside its X (no nibble pass)
+struct XsMask {
+  const uint64_t *bits = nullptr;
+  long long base = 0, ld = 0;
+  long long words = 0;  // uint64 words at bits, even (staged in whole 16-B pieces inside them)
+};
+// flat: the mask as a flat bitmap instead of maskT (the ring kernels only: xstream_ring_ok)
 void launch_xstream_nn(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
                        int trans_b, float *C, int ldc, const uint64_t *maskT, float a_scale,
                        hipStream_t s, float *C2 = nullptr,  // C2: drop(X) W beside C = X W
-                       const XsEpilogue *epi = nullptr);
+                       const XsEpilogue *epi = nullptr, const XsMask *flat = nullptr);
 // k_xstream_lds.hip: the X-stream products with loader and MFMA waves split (the default
 // form, g_xstream_ring; the launchers above dispatch to them)
 bool xstream_ring_ok(int K, int lda);
 void launch_xstream_nn_ring(int M, int N, int K, const float *A, int lda, const float *B, int ldb,
                             int trans_b, float *C, int ldc, const uint64_t *maskT, float a_scale,
-                            hipStream_t s, float *C2, const XsEpilogue &e);
+                            hipStream_t s, float *C2, const XsEpilogue &e,
+                            const XsMask *flat = nullptr);
 // partial[n_blocks][K][16] (the workgroups' sums; reduced in block order by the caller)
 void launch_xstream_tn_ring(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
                             const uint64_t *maskT, float a_scale, float *partial, int n_blocks,
-                            hipStream_t s);
+                            hipStream_t s, const XsMask *flat = nullptr);
 // out[r][0:ld] = src[rows[r]][0:ld]  (ld % 4 == 0)
 void launch_gather_rows(const float *src, const int *rows, int n, int ld, float *out,
                         hipStream_t s);
@@ -254,7 +264,7 @@ void launch_scatter_rows(const float *src, const int *rows, int n, int ld, float
                          hipStream_t s);
 void launch_xstream_tn(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
                        float *C, int ldc, const uint64_t *maskT, float a_scale, void *workspace,
-                       hipStream_t s);
+                       hipStream_t s, const XsMask *flat = nullptr);
 void launch_gemm_tn(int M, int N, int K, const float *A, int lda, const float *G, int ldg,
                     float *C, int ldc, const uint64_t *a_mask, long long mask_base,
                     long long mask_ld, float a_scale, void *workspace, hipStream_t s,

@@ -500,15 +500,18 @@ def nibble_mask_ref(mask, base, M, K):
 def test_gemm_xstream(pgcn, M, N, K, base):
     """X-stream NN/TN kernels with nibble-layout dropout bits vs fp64 references (the loader /
     MFMA-wave split of k_xstream_lds.hip and the register-streamed kernels); the dual NN
-    kernel bit-identical to the plain and masked ones."""
+    kernel bit-identical to the plain and masked ones; on the loader-wave shapes the flat
+    bitmap (pgcn_gemm_*xstream_flat, the engine's form) bit-identical to the nibbles."""
     rng = np.random.default_rng(7 * M + K)
     lda = (K + 3) // 4 * 4
+    ring = 577 <= K <= 640  # the loader / MFMA-wave kernels' shapes
     A = np.zeros((M, lda), np.float32)
     A[:, :K] = rng.standard_normal((M, K))
     A[:, K:] = np.nan
     B = rng.standard_normal((K, N)).astype(np.float32)
     Gm = rng.standard_normal((M, N)).astype(np.float32)
     mask = rng.integers(0, 2**63, (base + M * K + 63) // 64, dtype=np.uint64)
+    mask = np.concatenate([mask, np.zeros(len(mask) % 2, np.uint64)])  # whole 16-B pieces (flat)
     keep = mask_window(mask, base, M, K)
     dA, dB, dG = (torch.from_numpy(a).to(DEV) for a in (A, B, Gm))
     dm = torch.from_numpy(mask.view(np.int64)).to(DEV)
@@ -551,6 +554,19 @@ def test_gemm_xstream(pgcn, M, N, K, base):
         bound_t = np.abs(Ae).T @ np.abs(Gm.astype(np.float64))
         for tn in (W, W0):  # the same products, rows summed in different orders
             assert (np.abs(tn.cpu().numpy() - ref_t) <= 1e-5 * bound_t + 1e-30).all()
+        if drop and ring:
+            # the flat bitmap staged by the loader waves (the engine's form on these shapes):
+            # the same bits as the nibble layout
+            Cf = torch.full((M, ldc), float("nan"), device=DEV)
+            Wf = torch.full((K, N), float("nan"), device=DEV)
+            pgcn.check(pgcn.lib.pgcn_gemm_xstream_flat(M, N, K, vp(dA), lda, vp(dB), N, 0, vp(Cf),
+                                                       None, ldc, vp(dm), base, len(mask), 2.0,
+                                                       stream()), "xnn flat")
+            pgcn.check(pgcn.lib.pgcn_gemm_tn_xstream_flat(M, N, K, vp(dA), lda, vp(dG), N, vp(Wf),
+                                                          N, vp(dm), base, len(mask), 2.0, vp(ws),
+                                                          stream()), "xtn flat")
+            torch.cuda.synchronize()
+            assert torch.equal(Cf, C) and torch.equal(Wf, W)
         outs[drop] = C
     # the dual kernel (eval + next training product in one pass) is bit-identical to both
     C1 = torch.full((M, ldc), float("nan"), device=DEV)
@@ -559,6 +575,17 @@ def test_gemm_xstream(pgcn, M, N, K, base):
                                                ldc, vp(nib), 2.0, stream()), "xnn dual")
     torch.cuda.synchronize()
     assert torch.equal(C1, outs[False]) and torch.equal(C2, outs[True])
+    if ring:
+        C1.fill_(float("nan"))
+        C2.fill_(float("nan"))
+        pgcn.check(pgcn.lib.pgcn_gemm_xstream_flat(M, N, K, vp(dA), lda, vp(dB), N, 0, vp(C1),
+                                                   vp(C2), ldc, vp(dm), base, len(mask), 2.0,
+                                                   stream()), "xnn dual flat")
+        torch.cuda.synchronize()
+        assert torch.equal(C1, outs[False]) and torch.equal(C2, outs[True])
+    else:  # the flat form exists for the loader-wave kernels' shapes only
+        assert pgcn.lib.pgcn_gemm_xstream_flat(M, N, K, vp(dA), lda, vp(dB), N, 0, vp(C1), None,
+                                               ldc, vp(dm), base, len(mask), 2.0, stream()) != 0
 
 
 def test_spmm_csr_and_csc_bit_exact(pgcn, loaded):

@@ -3,8 +3,9 @@ host side; the 4-layer model's d = 128 GraphSums).
 
 usage: python3 tools/epoch_traffic.py gpurun_out/<dir> [marker-substring]
 <dir> holds scripts/profile.sh's fetch/ and write/ passes.  The epoch is the dispatches from
-the second-to-last launch of the marker kernel (default k_mask_nibbles: the training forward's
-first-layer mask layout) up to the last.  Bytes as tools/traffic.py: FETCH_SIZE x 2 +
+the second-to-last launch of the marker kernel (default k_mask_nibbles: the 4-layer training
+forward's first-layer mask layout; the 2-layer epoch has no such pass since r05 late -- pass
+another marker there) up to the last.  Bytes as tools/traffic.py: FETCH_SIZE x 2 +
 WRITE_SIZE (KB).  Prints one JSON object: per family {launches, fetch_MB, write_MB, hbm_MB}.
 """
 import csv
