@@ -288,28 +288,151 @@ def main():
 
     nonlocal_uid = [uid]
 
-    def barrier(g):
-        g.sync()
-        torch.cuda.synchronize()
-        if dist is not None:
-            dist.barrier()
-
-    def max_over_ranks(x):
+    def reduce_over_ranks(x, op):
         if dist is None:
             return x
         t = torch.tensor([x], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=op)
         return float(t.item())
 
+    def max_over_ranks(x):
+        return reduce_over_ranks(x, dist.ReduceOp.MAX if dist else None)
+
+    def all_ok(ok):
+        """every rank learns whether every rank succeeded (one gloo all-reduce)"""
+        return int(reduce_over_ranks(int(ok), dist.ReduceOp.MIN if dist else None))
+
     def timed(g, steps, warmup):
-        for _ in range(warmup):
-            g.epoch_async()
-        barrier(g)
+        """(seconds, ok).  Every rank runs the same gloo collectives whatever happens on its GPU
+        (a peer wait that gave up raises PgcnError at its sync on ONE rank only): the error is
+        caught and recorded, the barriers and the max still run, and the ranks agree on `ok`
+        with one all-reduce at the end."""
+        ok = 1
+
+        def local_sync():
+            nonlocal ok
+            try:
+                g.sync()
+                torch.cuda.synchronize()
+            except pgcn.PgcnError as e:  # a peer that never signalled (PGCN_E_COMM)
+                print(f"bench.py: rank {rank}: {e}", file=sys.stderr)
+                ok = 0
+
+        try:
+            for _ in range(warmup):
+                g.epoch_async()
+        except pgcn.PgcnError as e:
+            print(f"bench.py: rank {rank}: {e}", file=sys.stderr)
+            ok = 0
+        local_sync()
+        if dist is not None:
+            dist.barrier()
         t0 = time.perf_counter()
-        for _ in range(steps):
-            g.epoch_async()
-        barrier(g)
-        return max_over_ranks(time.perf_counter() - t0)
+        if ok:
+            try:
+                for _ in range(steps):
+                    g.epoch_async()
+            except pgcn.PgcnError as e:
+                print(f"bench.py: rank {rank}: {e}", file=sys.stderr)
+                ok = 0
+        local_sync()
+        if dist is not None:
+            dist.barrier()
+        el = max_over_ranks(time.perf_counter() - t0)
+        return el, all_ok(ok)
+
+    # ---- N > 1: the exchange checked end to end against a one-GPU engine -------------------
+    # rank 0 holds a world-1 engine (same data, seed and knobs; at N = 1 the bench checks that
+    # engine against the reference's own epochs) and compares every rank's rows of the logits
+    # and the all-reduced epoch lines with it: first after 2 fresh epochs, before the timing
+    # (a failure there on the peer exchange moves the run to RCCL), then after the timed run
+    # (the same epoch count on both engines).  hpdga-spring23/src/gcn.cpp:179-212.
+    ref1 = [None]
+
+    def compare(lines, ref_lines, rows, ref_rows, epochs, after_timed=False):
+        cnt = helpers.split_counts(ds)
+        rel = [abs(o[k] - r[k]) / abs(r[k]) for o, r in zip(lines, ref_lines) for k in (0, 2)]
+        acc_rows = [abs(o[k] - r[k]) * cnt[sp] for o, r in zip(lines, ref_lines)
+                    for k, sp in ((1, 1), (3, 2))]
+        same_n = rows.size == ref_rows.size
+        dl = np.abs(rows.astype(np.float64) - ref_rows) if same_n else np.array([np.inf])
+        within = dl <= 1e-4 + 1e-4 * np.abs(ref_rows.astype(np.float64)) if same_n else dl < 0
+        tol = 1e-4
+        return {"against": "world-1 engine on rank 0's GPU (same data, seed and knobs; at N = 1 "
+                           "bench.py checks it against the reference's own epochs)",
+                "epochs": epochs, "lines_compared": len(ref_lines),
+                "loss_rel_err": max(rel) if rel else None,
+                "acc_max_row_diff": max(acc_rows) if acc_rows else None, "tolerance": tol,
+                "pass": bool(rel and max(rel) <= tol and same_n and within.all()),
+                "engine_lines": [list(map(float, o)) for o in lines],
+                "reference_lines": [list(map(float, r)) for r in ref_lines],
+                "logits": {"values": int(ref_rows.size), "max_abs_err": float(dl.max()),
+                           "within_1e-4": float(within.mean()), "rtol": 1e-4, "atol": 1e-4,
+                           "pass": bool(same_n and within.all()),
+                           "gathered_from_ranks": world}}
+
+    def gather_rows(g, ok):
+        """every rank's rows of the output variable (rank order) -> rank 0"""
+        rows = None
+        if ok:
+            try:
+                rows = np.asarray(g.get_var(g.num_vars() - 1), np.float32)
+            except pgcn.PgcnError as e:
+                print(f"bench.py: rank {rank}: {e}", file=sys.stderr)
+        allr = [None] * world if rank == 0 else None
+        dist.gather_object(rows, allr, dst=0)
+        if rank != 0:
+            return None
+        if any(r is None for r in allr):
+            return np.zeros(0, np.float32)
+        return np.concatenate([r.ravel() for r in allr])
+
+    def verify_fresh(g, epochs=2):
+        """2 synchronous epochs of the freshly built engine against rank 0's world-1 engine's
+        first 2 (built here, kept for the check after the timing)"""
+        ok, lines = 1, []
+        try:
+            lines = [list(g.train_epoch() + g.eval(2)) for _ in range(epochs)]
+        except pgcn.PgcnError as e:
+            print(f"bench.py: rank {rank}: {e}", file=sys.stderr)
+            ok = 0
+        rows = gather_rows(g, ok)
+        res = [None]
+        if rank == 0:
+            if ref1[0] is None:
+                with stdout_to_stderr():
+                    ref1[0] = pgcn.GCN(params, ds, device=local_rank)
+                ref1[0].lines = [list(ref1[0].train_epoch() + ref1[0].eval(2))
+                                 for _ in range(epochs)]
+                ref1[0].rows = np.asarray(ref1[0].get_var(ref1[0].num_vars() - 1), np.float32)
+                ref1[0].epochs = epochs
+            r1 = ref1[0]
+            res[0] = compare(lines, r1.lines, rows, r1.rows, epochs)
+        dist.broadcast_object_list(res, src=0)
+        return res[0]
+
+    def verify_after(g, epochs_run):
+        """the timed engine's last epoch lines and logits against the world-1 engine advanced to
+        the same epoch count"""
+        ok, lines = 1, []
+        try:
+            lines = [list(map(float, x)) for x in g.results(4)]
+        except pgcn.PgcnError as e:
+            print(f"bench.py: rank {rank}: {e}", file=sys.stderr)
+            ok = 0
+        rows = gather_rows(g, ok)
+        res = [None]
+        if rank == 0:
+            r1 = ref1[0]
+            for _ in range(epochs_run - r1.epochs):
+                r1.epoch_async()
+            ref_lines = [list(map(float, x)) for x in r1.results(4)]
+            ref_rows = np.asarray(r1.get_var(r1.num_vars() - 1), np.float32)
+            res[0] = compare(lines, ref_lines, rows, ref_rows, epochs_run, True)
+            r1.close()
+            ref1[0] = None
+        dist.broadcast_object_list(res, src=0)
+        return res[0]
 
     head_knobs = dict(kv.split("=") for kv in args.knob)
     # the headline knobs stay set through its timing and profiling (some are read per launch)
@@ -321,33 +444,47 @@ def main():
     info = {k: g.query(k) for k in ("world", "comm", "reassociated", "graph_symmetric", "fused_tails",
                                      "graphsum_lds")}
     ax_ms = max_over_ranks(g.query("eval_ax_us") / 1000.0)
-    try:
-        elapsed = timed(g, args.steps, args.warmup)
-        res = g.results(min(args.steps, 4))
-        ok = 1
-    except pgcn.PgcnError as e:  # a peer that never signalled (PGCN_E_COMM at a sync)
-        print(f"bench.py: rank {rank}: {e}", file=sys.stderr)
-        ok = 0
-    if dist is not None:  # every rank learns whether any rank failed
-        t = torch.tensor([ok], dtype=torch.int32)
-        dist.all_reduce(t, op=dist.ReduceOp.MIN)
-        ok = int(t.item())
-    if not ok:
-        if comm_kind[0] != "peer":
-            raise SystemExit("bench.py: the timed epochs failed")
-        # the peer exchange failed at run time on some rank: every rank measures again on RCCL
-        print(f"bench.py: rank {rank}: peer exchange failed at run time; RCCL", file=sys.stderr)
+    pre_epochs = 0
+    fallback = []
+
+    def to_rccl(g, why):
+        # every rank measures again on RCCL (every rank takes this branch: the decision is agreed)
+        print(f"bench.py: rank {rank}: {why}; RCCL", file=sys.stderr)
+        fallback.append(why)
         try:
             g.close()
         except pgcn.PgcnError:
             pass
         comm_kind[0] = "rccl"
         g = engine()
-        info = {k: g.query(k) for k in ("world", "comm", "reassociated", "graph_symmetric",
-                                         "fused_tails", "graphsum_lds")}
-        ax_ms = max_over_ranks(g.query("eval_ax_us") / 1000.0)
-        elapsed = timed(g, args.steps, args.warmup)
-        res = g.results(min(args.steps, 4))
+        return g, {k: g.query(k) for k in ("world", "comm", "reassociated", "graph_symmetric",
+                                             "fused_tails", "graphsum_lds")}, \
+            max_over_ranks(g.query("eval_ax_us") / 1000.0)
+
+    parity_fresh = None
+    if world > 1 and not args.profile_only:
+        parity_fresh = verify_fresh(g)
+        pre_epochs = parity_fresh["epochs"]
+        if not parity_fresh["pass"] and comm_kind[0] == "peer":
+            first = parity_fresh
+            g, info, ax_ms = to_rccl(g, "peer exchange differs from the one-GPU engine")
+            parity_fresh = verify_fresh(g)
+            parity_fresh["peer_exchange_check"] = {k: first[k] for k in
+                                                   ("loss_rel_err", "pass", "logits")}
+    elapsed, ok = timed(g, args.steps, args.warmup)
+    if not ok:
+        if comm_kind[0] != "peer":
+            raise SystemExit("bench.py: the timed epochs failed")
+        # the peer exchange failed at run time on some rank (a wait that gave up)
+        g, info, ax_ms = to_rccl(g, "peer exchange failed at run time")
+        pre_epochs = 0
+        if world > 1 and not args.profile_only:
+            parity_fresh = verify_fresh(g)
+            pre_epochs = parity_fresh["epochs"]
+        elapsed, ok = timed(g, args.steps, args.warmup)
+        if not ok:
+            raise SystemExit("bench.py: the timed epochs failed on RCCL too")
+    res = g.results(min(args.steps, 4))
 
     if args.profile_only:
         head_ctx.close()
@@ -362,6 +499,9 @@ def main():
     gs_ms, gs_calls, gs_bytes = g.profile_read()
     mm_ms, mm_calls, mm_flops = g.profile_read_mm()
     g.profile(False)
+    parity_after = None
+    if parity_fresh is not None:
+        parity_after = verify_after(g, pre_epochs + args.warmup + args.steps + 2)
     head_ctx.close()
     g.close()
     avg_ms = gs_ms / max(gs_calls, 1)
@@ -479,6 +619,10 @@ def main():
                                     "within_1e-4": float(within.mean()),
                                     "rtol": 1e-4, "atol": 1e-4,
                                     "pass": bool(same_n and within.all())}}
+    if parity_fresh is not None:
+        out["parity"] = dict(parity_fresh, after_timed=parity_after)
+        if fallback:
+            out["config"]["fallback"] = fallback
     if rank == 0:
         print(json.dumps(out))
     if dist is not None:

@@ -25,6 +25,7 @@ extern int g_fuse_epilogue;         // host/gcn.cpp
 extern int g_fuse_output;           // host/gcn.cpp
 extern int g_mm_side;               // host/gcn.cpp
 extern int g_eval_tail;             // host/gcn.cpp
+extern int g_peer_uncached;         // host/comm.cpp
 extern int g_eval_ax;               // host/gcn.cpp
 extern int g_epoch_graph;           // host/gcn.cpp
 extern long long g_lds_min_bytes;   // host/graph.cpp
@@ -535,6 +536,10 @@ long long pgcn_gcn_query(pgcn_gcn *g, const char *key) {
                                                       : 4)
              : 0;
   if (!std::strcmp(key, "comm_calls")) return c ? c->calls : 0;
+  if (!std::strcmp(key, "peer_uncached")) {  // the peer exchange's slots are uncached memory
+    const auto *pc = dynamic_cast<const pgcn::PeerComm *>(c);
+    return pc && pc->slots_uncached() ? 1 : 0;
+  }
   if (!std::strcmp(key, "comm_bytes")) return c ? (long long)c->bytes : 0;
   if (!std::strcmp(key, "reassociated")) return e.reassociated() ? 1 : 0;
   if (!std::strcmp(key, "fused_tails")) return e.fused_tails();
@@ -718,6 +723,9 @@ int pgcn_debug_set(const char *key, int value) {
   } else if (!std::strcmp(key, "eval_tail")) {
     if (!in(0, 1)) return PGCN_E_INVALID;
     pgcn::g_eval_tail = value;
+  } else if (!std::strcmp(key, "peer_uncached")) {
+    if (!in(0, 1)) return PGCN_E_INVALID;
+    pgcn::g_peer_uncached = value;
   } else if (!std::strcmp(key, "xstream_ring")) {
     if (!in(0, 1)) return PGCN_E_INVALID;
     pgcn::g_xstream_ring = value;

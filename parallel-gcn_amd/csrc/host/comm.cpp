@@ -16,6 +16,8 @@
 
 namespace pgcn {
 
+int g_peer_uncached = 0;
+
 int Partition::owner(int node) const {
   return (int)(std::upper_bound(bounds.begin(), bounds.end(), node) - bounds.begin()) - 1;
 }
@@ -147,6 +149,7 @@ RcclComm::~RcclComm() {
 }
 
 void RcclComm::allreduce_sum(float *buf, size_t n, hipStream_t s) {
+  enter(s);
   if (world_ == 1 || n == 0) return;
   count(n * sizeof(float), 2.0);
   PGCN_NCCL(ncclAllReduce(buf, buf, n, ncclFloat32, ncclSum, static_cast<ncclComm_t>(comm_), s));
@@ -154,6 +157,7 @@ void RcclComm::allreduce_sum(float *buf, size_t n, hipStream_t s) {
 
 void RcclComm::reduce_scatter_sum(const float *send, float *recv, size_t recvcount,
                                   hipStream_t s) {
+  enter(s);
   count(recvcount * world_ * sizeof(float), 1.0);
   PGCN_NCCL(ncclReduceScatter(send, recv, recvcount, ncclFloat32, ncclSum,
                               static_cast<ncclComm_t>(comm_), s));
@@ -250,11 +254,15 @@ PeerComm::PeerComm(int rank, int world, size_t slot_floats, AllGather ag, bool i
              PGCN_E_INVALID, "peer comm: rank / world");
   slot_floats_ = (std::max<size_t>(slot_floats, 4) + 63) / 64 * 64;  // 256-B aligned slots
   bytes_ = 2 * (size_t)world * slot_floats_ * sizeof(float);
-  // slots: plain device memory (written through by the pushers' sc0 sc1 stores, read by
-  // plain loads after a kernel boundary: MTYPE RW lines are kept coherent by the memory
-  // probes); header: uncached (the flags and counters every rank polls and adds to)
+  // slots: plain device memory (pushed with plain stores and one system-scope release per
+  // pushing workgroup; read after a system-scope acquire: peer_sync.hpp), or uncached
+  // (peer_uncached); header: uncached (the flags and counters every rank polls and adds to)
   void *p = nullptr;
-  PGCN_HIP(hipMalloc(&p, bytes_));
+  uncached_ = g_peer_uncached != 0 && !solo;
+  if (uncached_)
+    PGCN_HIP(hipExtMallocWithFlags(&p, bytes_, hipDeviceMallocUncached));
+  else
+    PGCN_HIP(hipMalloc(&p, bytes_));
   slots_ = static_cast<char *>(p);
   p = nullptr;
   if (hipExtMallocWithFlags(&p, kPeerHeader, hipDeviceMallocUncached) != hipSuccess || !p) {
@@ -313,6 +321,13 @@ PeerComm::PeerComm(int rank, int world, size_t slot_floats, AllGather ag, bool i
     slots_ = header_ = nullptr;
     throw Error(PGCN_E_COMM, "peer comm: " + (why.empty() ? std::string("a peer failed to map") : why));
   }
+}
+
+void PeerComm::host_barrier() {
+  if (solo_ || !ag_) return;
+  int token = 0;
+  std::vector<int> all((size_t)world_);
+  ag_(&token, sizeof token, all.data());
 }
 
 void PeerComm::unmap() {
@@ -414,6 +429,7 @@ bool PeerComm::small_allreduce(size_t n, PeerSmall *p) {
 }
 
 void PeerComm::allreduce_sum(float *buf, size_t n, hipStream_t s) {
+  enter(s);
   PeerSmall p;
   if (small_allreduce(n, &p)) {
     // separate processes (or solo): push, wait and sum in one workgroup
@@ -432,6 +448,7 @@ void PeerComm::allreduce_sum(float *buf, size_t n, hipStream_t s) {
 
 void PeerComm::reduce_scatter_sum(const float *send, float *recv_buf, size_t recvcount,
                                   hipStream_t s) {
+  enter(s);
   count(recvcount * world_ * sizeof(float), 1.0);
   PeerSink k = sink(1, recvcount);
   launch_peer_push(send, recvcount, k, s, false);

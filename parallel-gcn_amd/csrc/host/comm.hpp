@@ -15,9 +15,15 @@
 
 #include <hip/hip_runtime.h>
 
+#include "../common.hpp"
 #include "../kernels.hpp"
 
 namespace pgcn {
+
+// "peer_uncached" (read at engine build): the peer exchange's receive slots in uncached device
+// memory (hipDeviceMallocUncached, MTYPE UC) instead of plain device memory -- no cache holds
+// a slot line on the receiver; the pushes are then write-through (0.3 TB/s on one GPU, r05)
+extern int g_peer_uncached;
 
 struct Partition {
   int world = 1, rank = 0;
@@ -72,8 +78,23 @@ class Comm {
   double bytes = 0.0;
   // a collective enqueued outside the calls above (PeerComm's fused GraphSum exchange)
   void note(size_t send_bytes, double factor) { count(send_bytes, factor); }
+  // Work on another stream that the next collective must follow (eval_tail: the eval pass's
+  // last exchange on comm_stream shares the slots' parity and the arrival counter): every
+  // collective entry point calls enter(s) first, which makes `s` wait for it once
+  void defer(hipEvent_t e) { pending_ = e; }
+  void enter(hipStream_t s) {
+    if (!pending_) return;
+    if (hipStreamWaitEvent(s, pending_, 0) != hipSuccess)
+      throw Error(PGCN_E_COMM, "comm: stream wait on the pending tail");
+    pending_ = nullptr;
+  }
+  bool pending() const { return pending_ != nullptr; }
+  // every rank has reached this point on the host (before the first device collective after
+  // seconds of per-rank host set-up, so no rank's bounded device wait starts far ahead)
+  virtual void host_barrier() {}
 
  protected:
+  hipEvent_t pending_ = nullptr;
   void count(size_t send_bytes, double factor) {
     calls++;
     bytes += factor * (double)send_bytes * (world_ - 1) / world_;
@@ -148,6 +169,8 @@ class PeerComm : public Comm {
   void reduce_scatter_sum(const float *send, float *recv, size_t recvcount,
                           hipStream_t s) override;
   const char *kind() const override { return solo_ ? "solo" : ipc_ ? "peer" : "loopback"; }
+  void host_barrier() override;
+  bool slots_uncached() const { return uncached_; }
   // The GraphSum exchange fused into the combine: sink() opens the next collective and returns
   // where this rank's rows go (rows_per_rank padded rows per owner, owner-major); after the
   // push, wait() enqueues the wait for every sender and recv() names the received slots
@@ -171,7 +194,7 @@ class PeerComm : public Comm {
   size_t slot_floats_ = 0, bytes_ = 0;
   unsigned gen_ = 0;                         // the last collective's generation
   AllGather ag_;
-  bool ipc_ = false, solo_ = false;
+  bool ipc_ = false, solo_ = false, uncached_ = false;
   std::function<void()> host_order_;
 };
 

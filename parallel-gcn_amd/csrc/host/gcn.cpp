@@ -542,6 +542,7 @@ void GCN::build(const GCNData &data) {
     ctx.tail_done = Event::create();
   }
   PGCN_HIP(hipDeviceSynchronize());
+  if (comm) comm->host_barrier();  // every rank built: the first epoch's waits start together
 }
 
 // eval_ax's Â X, computed last in build(): the engine's only long GPU work before the first
@@ -572,6 +573,9 @@ void GCN::build_eval_ax() {
     const int h = part.chunk_rows(), nk = (int)chunk_graphs.size();
     DeviceBuffer<float> partial((size_t)part.world * h * 16), own((size_t)nk * h * 16);
     for (auto &gk : chunk_graphs) gk->prepare(16);
+    // the engine's first device collective follows seconds of per-rank host set-up: every rank
+    // arrives first, so no rank's bounded wait (kPeerTimeoutTicks) starts far ahead of a peer
+    comm->host_barrier();
     ax0.record(stream.get());
     for (int c0 = 0; c0 < feats.cols; c0 += 16) {
       const int c = std::min(c0, feats.ldx - 16);
@@ -876,6 +880,7 @@ void GCN::finalize(int dst_offset, bool graph, hipStream_t s) {
   float *raw = raw_ring.get() + (size_t)dst_offset * 2;  // slot * 8 + pass * 4
   PeerSmall ps;
   auto *pc = dynamic_cast<PeerComm *>(comm.get());
+  comm->enter(s);  // (eval_tail) after the last eval pass's tail
   const bool fused = pc && pc->small_allreduce(2, &ps);  // between processes: in this launch
   launch_reduce_scalars(xent_partials.get(), ctx.xent_blocks, w1->dev_data.get(), w1->size,
                         nullptr, s, ctx.count, 0.0f, nullptr, nullptr, 1, raw,
@@ -907,6 +912,7 @@ void GCN::eval_forward(int off, bool graph) {
   if (tail) {
     ctx.tail_done.record(comm_stream.get());
     ctx.tail_pending = true;
+    comm->defer(ctx.tail_done.get());  // the next collective on any stream follows it
   }
 }
 

@@ -420,9 +420,11 @@ GsEpilogue GraphSum::backward_epilogue(const DevGraph *g) const {
 
 void GraphSum::run(const float *src, float *dst, const Stream &s, int mode,
                    const GsEpilogue *epi, bool prestaged) const {
-  if (ctx->tail_pending && !ctx->tail_stream) {
-    // the last eval pass's tail (eval_tail) still reads the partial buffer and its slots
-    ctx->tail_done.wait_on(s.get());
+  if (ctx->comm && !ctx->tail_stream) {
+    // the last eval pass's tail (eval_tail) still reads the partial buffer and its slots: every
+    // collective entry waits for it (Comm::enter; the weight-gradient all-reduce and the loss
+    // pair's too)
+    ctx->comm->enter(s.get());
     ctx->tail_pending = false;
   }
   Event e0, e1;

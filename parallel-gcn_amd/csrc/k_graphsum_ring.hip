@@ -221,6 +221,7 @@ __global__ __launch_bounds__(256) void k_gs_finish(float4 *__restrict__ y, int l
 // same sums as the reduce-scattered form with a rank-order sum)
 __global__ __launch_bounds__(256) void k_gs_gather_finish(float4 *__restrict__ y, int ld4, int n,
                                                           int vec, GsEpilogue epi, PeerRecv rv) {
+  acquire_system_workgroup();  // the peers' pushes (peer_sync.hpp)
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long r = t / vec;
   if (r >= n) return;

@@ -17,7 +17,8 @@
 //                of every peer, and resets the counter (peer_sync.hpp);
 //   consumer  -- one wave polls its own flags until every peer's reads gen (bounded: an error
 //                word and an early exit after kPeerTimeoutTicks), then the sum kernel reads
-//                the slots (stream order after the wait).
+//                the slots (stream order after the wait), each of its workgroups after a
+//                system-scope acquire (acquire_system_workgroup).
 // Slots are double-buffered by generation parity: a rank's push of generation g + 2 into
 // peer q's slot follows (in its stream) its wait for g + 1, which needs q's push of g + 1,
 // which follows (in q's stream) q's reads of generation g.
@@ -94,6 +95,7 @@ void launch_peer_allreduce_small(float *buf, int n, const PeerSink &k, const Pee
 // dst[i] = sum over q (rank order) of slot[q][i]
 template <typename T>
 __global__ __launch_bounds__(256) void k_peer_sum(PeerRecv r, T *__restrict__ dst, long long n) {
+  acquire_system_workgroup();  // the peers' pushes (peer_sync.hpp)
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   T p[kPeerMaxRanks];

@@ -6,8 +6,17 @@
 // 16-B stores; every pushing workgroup then makes them visible at system scope with ONE
 // release (an L2 write-back of its XCD's dirty lines, `buffer_wbl2 sc0 sc1`, waited for)
 // before its arrival, so when the last arrival stores the flags every slot byte has left this
-// GPU's caches.  The receiver reads them in a later kernel (a kernel boundary invalidates its
-// L1; its L2's lines of local memory are kept coherent by the memory probes).
+// GPU's caches.  The receiver reads them in a later kernel whose every workgroup starts with
+// a system-scope acquire (acquire_system_workgroup: `buffer_inv sc0 sc1`, waited for, then the
+// workgroup's barrier) -- the consumer half of the gfx942/gfx950 memory model's system-scope
+// hand-off.  That drops this CU's L1 and the XCD L2's non-coherent (NC) lines; the slots are
+// local VRAM, which the kernel driver maps MTYPE RW with the snoop bit on these parts (as it
+// maps fine-grained VRAM: the same MTYPE), so a peer's write-back over xGMI invalidates any L2
+// copy by the memory probes ("MTYPE RW and CC memory will never be stale due to the memory
+// probes", the LLVM AMDGPU memory model for GFX942 system-scope acquire).  A knob allocates
+// the slots uncached instead (`peer_uncached`, MTYPE UC: no L2 copy at all) for a machine
+// where that assumption fails; bench.py checks every N > 1 run's logits against a one-GPU
+// engine and falls back to RCCL when they differ.
 // r05, measured on one GPU (the solo form, every slot local): write-through pushes (sc0 sc1
 // stores, or uncached slots) moved 0.3 TB/s -- 49 us per GraphSum combine at W = 8 against
 // 12.7 us for the combine that writes its own rows (profiles/r05/g/rank8_breakdown.txt).
@@ -40,6 +49,17 @@ __device__ __forceinline__ void release_workgroup_stores() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
     stores_acked();
   }
+}
+
+// The receiving side of a hand-off at system scope (every thread calls it, before any early
+// exit): lane 0 of wave 0 issues the system-scope acquire and waits for it, then the
+// workgroup's barrier orders every wave's slot loads after it
+__device__ __forceinline__ void acquire_system_workgroup() {
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: buffer_inv sc0 sc1
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
 }
 
 // v -> float4 element i of the slot at `base` (bytes: the slot's size from base on: a store

@@ -35,7 +35,7 @@ def main():
     p = pg.make_params(ds)
     g = pg.GCN(p, ds, device=spec.get("device", 0), rank=rank, world=world,
                allgather=pg.torch_allgather())
-    info = [g.query(k) for k in ("world", "rank", "comm", "graphsum_lds")]
+    info = [g.query(k) for k in ("world", "rank", "comm", "graphsum_lds", "peer_uncached")]
     lines = [g.train_epoch() + g.eval(2) for _ in range(spec["epochs"])]
     for _ in range(spec.get("async", 0)):
         g.epoch_async()

@@ -1,6 +1,7 @@
 """bench.py --gpus 2 end to end on one GPU: the launcher (torch.distributed.run), the gloo
 rendezvous, two rank processes whose peer-mapped exchange opens its regions with hipIpc handles,
-the timing with its barriers and max over ranks, and rank 0's one JSON line -- the path the
+the timing with its barriers and max over ranks, the parity legs against a one-GPU engine, and
+rank 0's one JSON line -- the path the
 driver's multi-GPU bench takes, with both ranks on device 0 (PGCN_BENCH_SHARE_GPU=1, a rehearsal:
 the value is not a scaling measurement)."""
 import json
@@ -29,3 +30,11 @@ def test_bench_gpus2_shared_gpu():
     assert out["n_gpus"] == 2 and out["steps"] == 3 and out["warmup"] == 1
     assert out["value"] > 0 and out["ms_per_step"] > 0
     assert out["config"].get("exchange") == "peer", out["config"]
+    # N > 1 lines carry their own parity: every rank's rows of the logits and the epoch lines
+    # against a world-1 engine, after 2 fresh epochs and after the timed run
+    par = out["parity"]
+    assert par["pass"], par
+    assert par["logits"]["gathered_from_ranks"] == 2
+    assert par["logits"]["values"] == 232965 * 41
+    assert par["after_timed"]["epochs"] == 2 + 1 + 3 + 2, par["after_timed"]
+    assert par["after_timed"]["pass"], par["after_timed"]

@@ -97,15 +97,18 @@ def test_peer_procs_cora_world2(pgcn, datasets, loaded, tmp_path):
         helpers.assert_line_close(ours, gold[e], cnt, what=f"peer procs epoch {e + 1}")
 
 
-@pytest.mark.parametrize("world,tail", [(2, 0), (4, 0), (4, 1)])
-def test_peer_procs_lds_graph(pgcn, world, tail, tmp_path):
+@pytest.mark.parametrize("world,tail,uncached", [(2, 0, 0), (4, 0, 0), (4, 1, 0), (2, 0, 1)])
+def test_peer_procs_lds_graph(pgcn, world, tail, uncached, tmp_path):
     """140k nodes: every rank's column block takes the LDS ring GraphSum, whose combine pushes
     the partial sums into the owners' slots (k_gs_lds_combine's push mode).  tail 1: the eval
     pass's last exchange and output layer on the comm stream beside the next epoch (eval_tail),
-    the same bits as the in-process ranks (which never take it)."""
+    the same bits as the in-process ranks (which never take it).  uncached 1: the receive
+    slots in uncached memory (peer_uncached), the same bits."""
     syn = dict(n=140000, f=64, c=41, edges=1500000, seed=31)
-    spec = {"synthetic": syn, "epochs": 3, "async": 2, "knobs": {"eval_tail": tail}}
+    spec = {"synthetic": syn, "epochs": 3, "async": 2,
+            "knobs": {"eval_tail": tail, "peer_uncached": uncached}}
     procs = _run_procs(world, spec, tmp_path)
     assert procs[0]["info"][3] == 1  # graphsum_lds
+    assert procs[0]["info"][4] == uncached  # the slots' memory as asked
     ds = pgcn.Dataset.synthetic(syn["n"], syn["f"], syn["c"], syn["edges"], syn["seed"])
     _same(procs, _run_loopback(pgcn, ds, world, spec), world)
