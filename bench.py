@@ -350,13 +350,18 @@ def main():
     ref1 = [None]
 
     def compare(lines, ref_lines, rows, ref_rows, epochs, after_timed=False):
+        """losses within 1e-4 relative, every logit within rtol = atol = 1e-4 -- after the
+        timed run (~120 epochs: the two engines' different fp32 summation orders drift apart
+        slowly, 7.9e-5 after 29 epochs on the one-GPU rehearsal) the logits within 1e-3; a
+        stale or missing exchange shows as errors of O(1)"""
         cnt = helpers.split_counts(ds)
         rel = [abs(o[k] - r[k]) / abs(r[k]) for o, r in zip(lines, ref_lines) for k in (0, 2)]
         acc_rows = [abs(o[k] - r[k]) * cnt[sp] for o, r in zip(lines, ref_lines)
                     for k, sp in ((1, 1), (3, 2))]
         same_n = rows.size == ref_rows.size
+        ltol = 1e-3 if after_timed else 1e-4
         dl = np.abs(rows.astype(np.float64) - ref_rows) if same_n else np.array([np.inf])
-        within = dl <= 1e-4 + 1e-4 * np.abs(ref_rows.astype(np.float64)) if same_n else dl < 0
+        within = dl <= ltol + ltol * np.abs(ref_rows.astype(np.float64)) if same_n else dl < 0
         tol = 1e-4
         return {"against": "world-1 engine on rank 0's GPU (same data, seed and knobs; at N = 1 "
                            "bench.py checks it against the reference's own epochs)",
@@ -367,7 +372,7 @@ def main():
                 "engine_lines": [list(map(float, o)) for o in lines],
                 "reference_lines": [list(map(float, r)) for r in ref_lines],
                 "logits": {"values": int(ref_rows.size), "max_abs_err": float(dl.max()),
-                           "within_1e-4": float(within.mean()), "rtol": 1e-4, "atol": 1e-4,
+                           "within_tol": float(within.mean()), "rtol": ltol, "atol": ltol,
                            "pass": bool(same_n and within.all()),
                            "gathered_from_ranks": world}}
 
