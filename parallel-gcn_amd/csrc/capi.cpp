@@ -723,6 +723,9 @@ int pgcn_debug_set(const char *key, int value) {
   } else if (!std::strcmp(key, "eval_tail")) {
     if (!in(0, 1)) return PGCN_E_INVALID;
     pgcn::g_eval_tail = value;
+  } else if (!std::strcmp(key, "ring_pair")) {
+    if (!in(0, 1)) return PGCN_E_INVALID;
+    pgcn::g_ring_pair = value;
   } else if (!std::strcmp(key, "peer_uncached")) {
     if (!in(0, 1)) return PGCN_E_INVALID;
     pgcn::g_peer_uncached = value;

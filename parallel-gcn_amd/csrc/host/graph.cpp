@@ -506,6 +506,7 @@ void DevGraph::build_lds() {
   L->partial.allocate((size_t)h.n_blocks * n_rows_ * 16);
   L->s.n_blocks = h.n_blocks;
   L->s.ns = h.ns;
+  L->s.pair = h.pair;
   L->s.n_rows = n_rows_;
   L->s.n_cols = n_cols_;
   L->s.n_batches = h.n_batches;

@@ -43,6 +43,7 @@ std::vector<float> degree_scales(int n, const int *indptr);
 // Host image of the d = 16 LDS ring schedule (k_graphsum_ring.hip), before upload.
 struct LdsHost {
   int n_batches = 0, t_max = 0, n_blocks = 4, ns = LDS_SLOTS;
+  bool pair = false;                    // rowsets 2p, 2p+1 in lockstep (ring_pair)
   std::vector<int> nsl;                 // slices per column block
   std::vector<int2> slices;             // [block][t_max] {first column, rows}
   std::vector<int> rows;                // [batch][LDS_CW][ns][16] row | spread
@@ -61,9 +62,13 @@ int lds_slots(int n_rows, int n_cols);
 // walk as the kernel consumes it: out[row] += sum of in[col] (throws on an inconsistent
 // schedule)
 std::vector<int> ring_cuts(int n_cols, const std::vector<int> &indices, int n_blocks);
+// pair: rowsets 2p and 2p + 1 of a wave run the same step count per visit and their entry
+// blocks alternate in the stream (k_graphsum_ring<.., true>: both blocks' table reads in flight
+// under one wait); -1 = the "ring_pair" knob
 LdsHost build_ring_host(int n_rows, int n_cols, const std::vector<int> &indptr,
                         const std::vector<int> &indices, const std::vector<int> &bcut,
-                        int ns = LDS_SLOTS);
+                        int ns = LDS_SLOTS, int pair = -1);
+extern int g_ring_pair;
 void ring_emulate(const LdsHost &h, int n_rows, const float *in, double *out);
 
 class DevGraph {

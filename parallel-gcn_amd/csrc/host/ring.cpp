@@ -78,11 +78,16 @@ std::vector<int> ring_cuts(int n_cols, const std::vector<int> &indices, int n_bl
   return cut;
 }
 
+// "ring_pair" (read at schedule build): rowsets in lockstep pairs (build_ring_host)
+int g_ring_pair = 0;
+
 LdsHost build_ring_host(int n_rows, int n_cols, const std::vector<int> &indptr,
-                        const std::vector<int> &indices, const std::vector<int> &bcut, int ns) {
+                        const std::vector<int> &indices, const std::vector<int> &bcut, int ns,
+                        int pair_arg) {
   (void)n_cols;
   const int B = (int)bcut.size() - 1, SR = RING_SR, W = RING_W, K = RING_K;
   const int CW = LDS_CW, NS = ns;
+  const bool pair = pair_arg < 0 ? g_ring_pair != 0 : pair_arg != 0;
   PGCN_CHECK(ring_slots_ok(ns), PGCN_E_INVALID, "graphsum_ring: rowsets per wave");
   PGCN_CHECK(B >= 1 && kCUs % B == 0, PGCN_E_INVALID, "graphsum_ring: column blocks");
   for (int b = 0; b < B; b++)
@@ -271,16 +276,35 @@ LdsHost build_ring_host(int n_rows, int n_cols, const std::vector<int> &indptr,
           }
           nb[(size_t)w * NS + j] = (n + 3) / 4;
         }
+        // pairs: both rowsets take the longer run (the shorter one fills the extra steps with
+        // its later slices' edges, or padding)
+        if (pair)
+          for (int j = 0; j < NS; j += 2) {
+            int &a = nb[(size_t)w * NS + j], &c = nb[(size_t)w * NS + j + 1];
+            a = c = std::max(a, c);
+          }
       }
       for (int w = 0; w < CW; w++) {
+        size_t pair_base = 0;
         for (int j = 0; j < NS; j++) {
           const int S = 4 * nb[(size_t)w * NS + j];
           PGCN_CHECK(S < 65536, PGCN_E_INVALID, "graphsum_ring: visit run too long");
           counts[(size_t)(((wg * t_max + v) * CW + w) * NS + j)] = (unsigned short)S;
           Lane *lj = &lanes[((size_t)w * NS + j) * 16];
           std::vector<unsigned short> &ow = out[(size_t)w];
-          const size_t kb = ow.size() / 64;
-          ow.resize(ow.size() + (size_t)S * 16);
+          // block k of this rowset's run: kb + bstride * k (pairs: rowset 2p's blocks at the
+          // even places of the pair's run, 2p + 1's at the odd ones)
+          size_t kb;
+          const size_t bstride = pair ? 2 : 1;
+          if (!pair) {
+            kb = ow.size() / 64;
+            ow.resize(ow.size() + (size_t)S * 16);
+          } else if (j % 2 == 0) {
+            pair_base = kb = ow.size() / 64;
+            ow.resize(ow.size() + (size_t)S * 32);
+          } else {
+            kb = pair_base + 1;
+          }
           for (int st = 0; st < S; st++) {
             for (int q = 0; q < 4; q++) {
               const int *grp = kQuad[q];
@@ -334,7 +358,8 @@ LdsHost build_ring_host(int n_rows, int n_cols, const std::vector<int> &indptr,
                 } else {  // padding: the zero row of this member's residue
                   val = (K * SR + zero) * 16;
                 }
-                ow[(kb + (size_t)(st / 4)) * 64 + (size_t)(g * 4 + (st % 4))] = (unsigned short)val;
+                ow[(kb + bstride * (size_t)(st / 4)) * 64 + (size_t)(g * 4 + (st % 4))] =
+                    (unsigned short)val;
               }
             }
           }
@@ -368,6 +393,7 @@ LdsHost build_ring_host(int n_rows, int n_cols, const std::vector<int> &indptr,
   }, 0, 2);
   LdsHost h;
   h.ns = NS;
+  h.pair = pair;
   h.n_blocks = B;
   h.n_batches = nbat;
   h.t_max = t_max;
@@ -395,9 +421,19 @@ void ring_emulate(const LdsHost &h, int n_rows, const float *in, double *out) {
       for (int v = 0; v < T; v++) {
         const unsigned short *cn = &h.counts[(size_t)(((wg * h.t_max + v) * CW + w) * NS)];
         std::vector<int> seq;  // the rowset of each block, in stream order
-        for (int j = 0; j < NS; j++) {
+        for (int j = 0; j < NS; j++)
           PGCN_CHECK(cn[j] % 4 == 0, PGCN_E_INVALID, "ring schedule: steps not whole blocks");
-          for (int k = 0; k < cn[j] / 4; k++) seq.push_back(j);
+        if (h.pair) {  // pairs: blocks of rowsets 2p, 2p + 1 alternate
+          for (int j = 0; j < NS; j += 2) {
+            PGCN_CHECK(cn[j] == cn[j + 1], PGCN_E_INVALID, "ring schedule: unequal pair runs");
+            for (int k = 0; k < cn[j] / 4; k++) {
+              seq.push_back(j);
+              seq.push_back(j + 1);
+            }
+          }
+        } else {
+          for (int j = 0; j < NS; j++)
+            for (int k = 0; k < cn[j] / 4; k++) seq.push_back(j);
         }
         for (const int j : seq) {
           {

@@ -240,8 +240,11 @@ __global__ __launch_bounds__(256) void k_gs_gather_finish(float4 *__restrict__ y
   y[r * ld4 + v] = a;
 }
 
-// NS: rowsets per summing wave (LDS_SLOTS)
-template <int NS>
+// NS: rowsets per summing wave (LDS_SLOTS).  PAIR (ring_pair, host/ring.cpp): rowsets 2p and
+// 2p + 1 run the same step count per visit and their entry blocks alternate, so a wave issues
+// both blocks' eight table reads before it waits (the adds of 2p's block wait only for its own
+// four): two blocks in flight per wave instead of one, the same adds in the same order per row
+template <int NS, bool PAIR>
 __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
     const uint2 *__restrict__ entries, const long long *__restrict__ wave_off,
     const unsigned short *__restrict__ counts, int t_max, const int2 *__restrict__ slices,
@@ -329,9 +332,11 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
   // count-down, where the ring offset arithmetic and the chunk test took six scalar ops)
   unsigned ecur = ring_dst + (unsigned)(g * 8);
   const unsigned ering_end = ring_dst + (unsigned)RING_ERING_B;
-  int left = RING_CHUNK / 128;
+  constexpr int UNIT = PAIR ? 256 : 128;  // bytes of entries per step of the loop
+  int left = RING_CHUNK / UNIT;
   int chunk = 0;
   u2v e_next = ds_rd64(ecur);
+  u2v e_next1 = PAIR ? ds_rd64(ecur + 128) : u2v{0u, 0u};
   // lane (g, v) reads plane v: entry (ring row x 16 B) + this constant
   const unsigned tb = lds_base + (unsigned)(v * RING_PLANE_B);
   // One entry block: its four table addresses from the landed entries, then the next block's
@@ -357,6 +362,38 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
     a += x2;
     a += x3;
   };
+  // PAIR: block k of rowset 2p then block k of rowset 2p + 1 (256 B of entries): both blocks'
+  // addresses from the landed entries, the next pair's two entry reads, the eight table reads,
+  // 2p's adds once its four have returned (lgkmcnt(4): LDS operations complete in order), then
+  // 2p + 1's
+  auto pair_block = [&](f4v &a, f4v &b) {
+    const unsigned a0 = tb + (e_next.x & 0xffffu), a1 = tb + (e_next.x >> 16),
+                   a2 = tb + (e_next.y & 0xffffu), a3 = tb + (e_next.y >> 16);
+    const unsigned b0 = tb + (e_next1.x & 0xffffu), b1 = tb + (e_next1.x >> 16),
+                   b2 = tb + (e_next1.y & 0xffffu), b3 = tb + (e_next1.y >> 16);
+    ecur += 256;
+    if (--left == 0) {
+      left = RING_CHUNK / 256;
+      ++chunk;
+      if (ecur >= ering_end) ecur -= RING_ERING_B;
+      refill(chunk + 3);
+      asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // chunk `chunk` landed
+    }
+    ds_rd64_into(e_next, ecur);
+    ds_rd64_into(e_next1, ecur + 128);
+    f4v x0 = ds_rd128(a0), x1 = ds_rd128(a1), x2 = ds_rd128(a2), x3 = ds_rd128(a3);
+    f4v y0 = ds_rd128(b0), y1 = ds_rd128(b1), y2 = ds_rd128(b2), y3 = ds_rd128(b3);
+    lgkm_wait<4>(x0, x1, x2, x3, e_next, e_next1);
+    a += x0;
+    a += x1;
+    a += x2;
+    a += x3;
+    lgkm_wait<0>(y0, y1, y2, y3);
+    b += y0;
+    b += y1;
+    b += y2;
+    b += y3;
+  };
   for (int t = 0; t < T; t++) {
     lds_wait_ge(loaded, (unsigned)(t + RING_W));  // slices t .. t+2 and visit t's counts
     // lane l reads rowset (l % 16)'s step count; two ballots give the rowsets with blocks this
@@ -369,13 +406,26 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
         lb + RING_CNT_OFF + (t % RING_NCB) * RING_CNT_B + wave * (2 * NS));
     const unsigned cl = c16[lane & (NS - 1)];
     const unsigned nz = (unsigned)__ballot(cl != 0u), big = (unsigned)__ballot(cl > 4u);
+    if constexpr (PAIR) {
 #pragma unroll
-    for (int j = 0; j < NS; j++) {
-      if (__builtin_amdgcn_readfirstlane((int)(nz << (31 - j))) < 0) {  // bit j: the sign bit
-        block(acc[j]);
-        if ((big >> j) & 1u) {
-          const unsigned n = (unsigned)__builtin_amdgcn_readlane((int)cl, j);
-          for (unsigned k = 4; k < n; k += 4) block(acc[j]);
+      for (int j = 0; j < NS; j += 2) {
+        if (__builtin_amdgcn_readfirstlane((int)(nz << (31 - j))) < 0) {  // the pair's run
+          pair_block(acc[j], acc[j + 1]);
+          if ((big >> j) & 1u) {
+            const unsigned n = (unsigned)__builtin_amdgcn_readlane((int)cl, j);
+            for (unsigned k = 4; k < n; k += 4) pair_block(acc[j], acc[j + 1]);
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < NS; j++) {
+        if (__builtin_amdgcn_readfirstlane((int)(nz << (31 - j))) < 0) {  // bit j: the sign bit
+          block(acc[j]);
+          if ((big >> j) & 1u) {
+            const unsigned n = (unsigned)__builtin_amdgcn_readlane((int)cl, j);
+            for (unsigned k = 4; k < n; k += 4) block(acc[j]);
+          }
         }
       }
     }
@@ -493,13 +543,16 @@ void launch_graphsum_ring(const LdsSchedule &s, const float *in, int ld_in, floa
                        reinterpret_cast<const float4 *>(in), ld_in / 4, s.col_scale, s.n_cols,
                        reinterpret_cast<float4 *>(scratch_in), col_map);
   const long long n_wg = (long long)s.n_batches * s.n_blocks;
-#define RING_LAUNCH(NS_)                                                                        \
-  PGCN_LAUNCH(k_graphsum_ring<NS_>, dim3((unsigned)n_wg), dim3(LDS_THREADS), 0, st, s.entries, \
+#define RING_LAUNCH(NS_, PAIR_)                                                                 \
+  PGCN_LAUNCH((k_graphsum_ring<NS_, PAIR_>), dim3((unsigned)n_wg), dim3(LDS_THREADS), 0, st, s.entries, \
               s.wave_off, s.counts, s.t_max, s.slices, s.n_slices, s.rows,                      \
               reinterpret_cast<const char *>(scratch_in), reinterpret_cast<float4 *>(partial), \
               (long long)s.n_rows, s.n_blocks)
   PGCN_CHECK(ring_slots_ok(s.ns), PGCN_E_INVALID, "graphsum_ring: rowsets per wave");
-  RING_LAUNCH(16);
+  if (s.pair)
+    RING_LAUNCH(16, true);
+  else
+    RING_LAUNCH(16, false);
 #undef RING_LAUNCH
   const GsEpilogue none{};
   const long long post = (long long)s.n_rows * 4;

@@ -96,6 +96,13 @@ __device__ __forceinline__ void lgkm_wait(f4v &x0, f4v &x1, f4v &x2, f4v &x3, u2
                : "n"(N));
 }
 template <int N>
+__device__ __forceinline__ void lgkm_wait(f4v &x0, f4v &x1, f4v &x2, f4v &x3, u2v &e0, u2v &e1) {
+  static_assert(N >= 0 && N < 16, "lgkmcnt is 4 bits");
+  asm volatile("s_waitcnt lgkmcnt(%c6)"
+               : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "+v"(e0), "+v"(e1)
+               : "n"(N));
+}
+template <int N>
 __device__ __forceinline__ void lgkm_wait(f4v &x0, f4v &x1, f4v &x2, f4v &x3) {
   static_assert(N >= 0 && N < 16, "lgkmcnt is 4 bits");
   asm volatile("s_waitcnt lgkmcnt(%c4)" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3) : "n"(N));
