@@ -26,6 +26,7 @@ extern int g_fuse_output;           // host/gcn.cpp
 extern int g_mm_side;               // host/gcn.cpp
 extern int g_eval_tail;             // host/gcn.cpp
 extern int g_peer_uncached;         // host/comm.cpp
+extern int g_tn_fold;               // host/gcn.cpp
 extern int g_eval_ax;               // host/gcn.cpp
 extern int g_epoch_graph;           // host/gcn.cpp
 extern long long g_lds_min_bytes;   // host/graph.cpp
@@ -723,6 +724,9 @@ int pgcn_debug_set(const char *key, int value) {
   } else if (!std::strcmp(key, "eval_tail")) {
     if (!in(0, 1)) return PGCN_E_INVALID;
     pgcn::g_eval_tail = value;
+  } else if (!std::strcmp(key, "tn_fold")) {
+    if (!in(0, 1)) return PGCN_E_INVALID;
+    pgcn::g_tn_fold = value;
   } else if (!std::strcmp(key, "ring_pair")) {
     if (!in(0, 1)) return PGCN_E_INVALID;
     pgcn::g_ring_pair = value;
@@ -749,7 +753,7 @@ int pgcn_debug_set(const char *key, int value) {
     if (!in(0, 1)) return PGCN_E_INVALID;
     pgcn::g_sparse_dual = value;
   } else if (!std::strcmp(key, "co_draw")) {
-    if (!in(0, 1)) return PGCN_E_INVALID;
+    if (!in(0, 2)) return PGCN_E_INVALID;
     pgcn::g_co_draw = value;
   } else if (!std::strcmp(key, "gs_split")) {
     if (!in(0, 3)) return PGCN_E_INVALID;

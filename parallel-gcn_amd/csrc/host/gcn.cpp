@@ -47,8 +47,11 @@ int g_fuse_epilogue = kFuseTails | kFusePrestage | kFuseXstream | kFuseMatmulTai
 // 65,536 rows or on an edge-cut rank (the same sums in another grouping); 3 = ... on any graph
 int g_fuse_output = 2;
 // "co_draw" (read at engine build): the hidden dropout's mask drawn in the input dropout's
-// launch (sparse X; bit-identical)
+// launch (1: sparse X; 2: dense X too; bit-identical)
 int g_co_draw = 1;
+// "tn_fold" (read per epoch): one GPU, the weight gradients' last reduction pass runs inside
+// the Adam launch (GCN::backward_pass; bit-identical)
+int g_tn_fold = 1;
 // "sparse_dual" (read per eval forward): sparse X with train_ahead: eval's first-layer product
 // also computes the next training forward's (k_spmm_csr<true>, one pass; bit-identical)
 int g_sparse_dual = 1;
@@ -94,9 +97,9 @@ float Adam::step_size(int t) const {
          (1.0f - powf(params.beta1, (float)t));
 }
 
-void Adam::step(const Stream &s) {
+void Adam::step(const Stream &s, TnDeferList *defer) {
   step_count++;
-  launch(s, step_size(step_count), nullptr, nullptr, 1);
+  launch(s, step_size(step_count), nullptr, nullptr, 1, defer);
 }
 
 void Adam::step_each(const std::vector<hipStream_t> &streams,
@@ -114,12 +117,15 @@ void Adam::step_each(const std::vector<hipStream_t> &streams,
   }
 }
 
-void Adam::step_graph(const Stream &s, const float *table, const int *ctr, int cap) const {
-  launch(s, 0.0f, table, ctr, cap);
+void Adam::step_graph(const Stream &s, const float *table, const int *ctr, int cap,
+                      TnDeferList *defer) const {
+  launch(s, 0.0f, table, ctr, cap, defer);
 }
 
-// every weight in one launch when they fit one AdamBatch (the 2-layer model: W1 and W2)
-void Adam::launch(const Stream &s, float st, const float *table, const int *ctr, int cap) const {
+// every weight in one launch when they fit one AdamBatch (the 2-layer model: W1 and W2); a
+// deferred reduction pass that writes a tensor's whole gradient runs inside it (tn_defer)
+void Adam::launch(const Stream &s, float st, const float *table, const int *ctr, int cap,
+                  TnDeferList *defer) const {
   if (vars.size() <= (size_t)kAdamBatch) {
     AdamBatch b{};
     for (const auto &v : vars) {
@@ -129,12 +135,21 @@ void Adam::launch(const Stream &s, float st, const float *table, const int *ctr,
       b.v[b.count] = v.v.get();
       b.n[b.count] = v.w->size;
       b.decay[b.count] = v.decay ? 1 : 0;
+      for (int i = 0; defer && i < defer->n; i++) {
+        TnDeferred &d = defer->d[i];
+        if (d.src && d.C == v.w->dev_grad.get() && (long long)d.K * d.N == v.w->size) {
+          b.red[b.count] = d;
+          d.src = nullptr;  // taken
+        }
+      }
       b.count++;
     }
+    if (defer) tn_defer_flush(*defer, s.get());  // passes no tensor took: before the update
     launch_adam_multi(b, st, params.beta1, params.beta2, params.eps, params.weight_decay, s.get(),
                       table, ctr, cap);
     return;
   }
+  if (defer) tn_defer_flush(*defer, s.get());
   for (auto &v : vars)
     launch_adam(v.w->dev_data.get(), v.w->dev_grad.get(), v.m.get(), v.v.get(), v.w->size, st,
                 params.beta1, params.beta2, params.eps, params.weight_decay, v.decay ? 1 : 0,
@@ -525,7 +540,8 @@ void GCN::build(const GCNData &data) {
   // (edge-cut: the tails run in k_gs_finish on the rank's rows after the reduce-scatter)
   if (g_fuse_epilogue & kFuseTails) fuse_epilogues();
   if (g_fuse_epilogue & kFuseMatmulTails) fuse_matmul_tails();
-  if (g_co_draw && dropouts_.size() >= 2 && !feats.dense && dropouts_[0] && dropouts_[1])
+  if (g_co_draw && dropouts_.size() >= 2 && (g_co_draw == 2 || !feats.dense) && dropouts_[0] &&
+      dropouts_[1])
     const_cast<Dropout *>(dropouts_[0])->co_draw = dropouts_[1];
   if (g_fuse_output) fuse_output_layer();
   optimizer = Adam(weights, decays, adam_params);
@@ -934,19 +950,50 @@ void GCN::join_side() {
   ctx.side_pending = false;
 }
 
+// One GPU ("tn_fold"): from the training forward (the fused loss kernel's W2.grad partials) to
+// the end of the backward pass the weight gradients' last ordered reduction passes are
+// recorded for the Adam launch, which runs them (the same bits, two launches fewer per epoch;
+// tn_defer).  An edge-cut rank all-reduces finished gradients instead: no fold.
+struct GCN::FoldScope {
+  explicit FoldScope(GCN &g, TnDeferList *d) {
+    if (!g_tn_fold || g.comm) return;
+    // the deferred passes' inputs: 64 first-pass groups of every weight's [K][16-padded]
+    // gradient (reddit: 0.8 MB)
+    if (!g.tn_pool) {
+      size_t f = 0;
+      for (const auto &w : g.weights) f += (size_t)64 * w->rows * ((w->cols + 15) / 16 * 16) + 64;
+      g.tn_pool.allocate(f);
+    }
+    d->pool = g.tn_pool.get();
+    d->pool_floats = g.tn_pool.size();
+    tn_defer(d);
+  }
+  ~FoldScope() { tn_defer(nullptr); }
+  void end() { tn_defer(nullptr); }
+};
+
+// The backward modules in reverse order (src/gcn.cu:318-330), the side stream joined, the
+// gradients all-reduced (edge-cut)
+void GCN::backward_pass(FoldScope &fold) {
+  for (int i = (int)modules.size() - 1; i >= 0; i--) modules[(size_t)i]->backward(stream);
+  fold.end();
+  join_side();
+  if (comm) comm->allreduce_sum(grad_arena.get(), grad_arena.size(), stream.get());
+}
+
 // train_epoch (src/gcn.cu:307-343) + eval(2) (src/gcn.cu:293-303), host-sync free
 void GCN::enqueue_epoch(bool graph) {
   const int slot4 = graph ? 0 : (int)(epoch_count % ring_cap) * 4;
   set_split(1);
+  TnDeferList defer;
+  FoldScope fold(*this, &defer);
   for (const auto &m : modules) m->forward(true, stream);
   finalize(slot4, graph);
-  for (int i = (int)modules.size() - 1; i >= 0; i--) modules[(size_t)i]->backward(stream);
-  join_side();
-  if (comm) comm->allreduce_sum(grad_arena.get(), grad_arena.size(), stream.get());
+  backward_pass(fold);
   if (graph)
-    optimizer.step_graph(stream, step_table.get(), dev_ctr.get(), kStepTable);
+    optimizer.step_graph(stream, step_table.get(), dev_ctr.get(), kStepTable, &defer);
   else
-    optimizer.step(stream);
+    optimizer.step(stream, &defer);
   set_split(2);
   eval_forward(slot4 + 2, graph);
   if (graph) launch_counters(dev_ctr.get(), 0, 0, 0, stream.get());
@@ -1024,12 +1071,12 @@ void GCN::epoch_async() {
 std::pair<float, float> GCN::train_epoch() {
   const long long slot = epoch_count % ring_cap;
   set_split(1);
+  TnDeferList defer;
+  FoldScope fold(*this, &defer);
   for (const auto &m : modules) m->forward(true, stream);
   finalize((int)(slot * 4));
-  for (int i = (int)modules.size() - 1; i >= 0; i--) modules[(size_t)i]->backward(stream);
-  join_side();
-  if (comm) comm->allreduce_sum(grad_arena.get(), grad_arena.size(), stream.get());
-  optimizer.step(stream);
+  backward_pass(fold);
+  optimizer.step(stream, &defer);
   ctr_valid = false;
   last_forward_training = true;
   return read_slot((int)(slot * 4));

@@ -58,20 +58,24 @@ class Adam {
   Adam() = default;
   Adam(const std::vector<shared_ptr<Variable>> &weights, const std::vector<bool> &decays,
        const AdamParams &p);
-  void step(const Stream &s);
+  // defer (one GPU): the weight gradients' deferred last reduction passes (tn_defer), run by
+  // this launch for the tensors whose gradients they write, launched before it otherwise
+  void step(const Stream &s, TnDeferList *defer = nullptr);
   // the reference's per-tensor schedule (src/optim.cu:57-95): one step, tensor i on
   // streams[i], then events[i] recorded there (null: none); the same arithmetic as step()
   void step_each(const std::vector<hipStream_t> &streams, const std::vector<hipEvent_t> &events);
   size_t size() const { return vars.size(); }
   // epoch graphs: the same launches reading the step size from table[ctr[0] % cap] on the
   // device (the host counts the step with advance() at every replay)
-  void step_graph(const Stream &s, const float *table, const int *ctr, int cap) const;
+  void step_graph(const Stream &s, const float *table, const int *ctr, int cap,
+                  TnDeferList *defer = nullptr) const;
   void advance() { step_count++; }
   int steps() const { return step_count; }
   float step_size(int t) const;  // hpdga optim.cpp:24, step t (1-based)
 
  private:
-  void launch(const Stream &s, float st, const float *table, const int *ctr, int cap) const;
+  void launch(const Stream &s, float st, const float *table, const int *ctr, int cap,
+              TnDeferList *defer) const;
 };
 
 struct DistSpec {
@@ -128,6 +132,8 @@ class GCN {
   void prepare_graphs();
   void check_comm() const;
   void build_eval_ax();
+  struct FoldScope;
+  void backward_pass(FoldScope &fold);
   void join_side();
   int fused_tails_ = 0;  // GraphSum epilogues carrying ReLU / Dropout work (forward + backward)
   void set_split(int split);
@@ -181,6 +187,7 @@ class GCN {
   std::vector<shared_ptr<DropoutRng>> rngs;  // [0] input, then one per hidden layer
   std::vector<const Dropout *> dropouts_;
   Adam optimizer;
+  DeviceBuffer<float> tn_pool;  // tn_fold: the deferred reduction passes' inputs
   DeviceBuffer<float> grad_arena;  // all weight grads, one all-reduce
   DeviceBuffer<uint8_t> jump_table;
   DeviceBuffer<float> gemm_ws, gemm_ws_side;

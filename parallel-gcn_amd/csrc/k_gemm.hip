@@ -759,6 +759,32 @@ size_t gemm_tn_workspace(int M, int N, int K) {
   return ws;
 }
 
+static thread_local TnDeferList *g_tn_defer = nullptr;
+
+void tn_defer(TnDeferList *list) { g_tn_defer = list; }
+
+void tn_defer_flush(TnDeferList &list, hipStream_t s) {
+  for (int i = 0; i < list.n; i++) {
+    const TnDeferred &d = list.d[i];
+    if (!d.src) continue;
+    const long long elems = (long long)d.K * d.ldp;
+    PGCN_LAUNCH(k_gemm_tn_reduce, dim3((unsigned)ceil_div(elems, 256)), dim3(256), 0, s, d.src,
+                d.n_groups, d.K, d.N, d.ldp, d.C, d.N, d.N);
+  }
+  list.n = 0;
+  list.used = 0;
+}
+
+// the deferred list's room for a first pass of `floats` outputs, or null (launch as usual)
+static float *tn_defer_room(int N, int ldc, int nst, size_t floats) {
+  TnDeferList *l = g_tn_defer;
+  if (!l || l->n >= 4 || ldc != N || nst != N || !l->pool) return nullptr;
+  const size_t at = (l->used + 63) / 64 * 64;
+  if (at + floats > l->pool_floats) return nullptr;
+  l->used = at + floats;
+  return l->pool + at;
+}
+
 // ordered two-pass reduction of p.n_slabs partials [K][ldp] into C[K][ldc]
 // One pass over the partials when they fit one first-pass group (the same sequential sum the
 // two passes form), or up to `one_pass` partials (the small X-stream TN plan only: its 32 block
@@ -773,9 +799,23 @@ static void tn_reduce(const TnPlan &p, int M, int N, int K, float *partial, floa
                 partial, p.n_slabs, K, N, p.ldp, C, ldc, nst);
     return;
   }
+  // tn_defer: the first pass's group sums into the deferred list's pool, the last pass left to
+  // the Adam launch
+  float *room = M > 0 ? tn_defer_room(N, ldc, nst, (size_t)p.n_groups * elems) : nullptr;
+  if (room) part2 = room;
   if (M > 0)
     PGCN_LAUNCH(k_slab_reduce1, dim3((unsigned)ceil_div(elems, 256), (unsigned)p.n_groups),
                        dim3(256), 0, s, partial, p.n_slabs, elems, p.spg, part2);
+  if (room) {
+    TnDeferred &d = g_tn_defer->d[g_tn_defer->n++];
+    d.src = part2;
+    d.n_groups = p.n_groups;
+    d.K = K;
+    d.N = N;
+    d.ldp = p.ldp;
+    d.C = C;
+    return;
+  }
   PGCN_LAUNCH(k_gemm_tn_reduce, dim3((unsigned)ceil_div(elems, 256)), dim3(256), 0, s,
                      part2, M > 0 ? p.n_groups : 0, K, N, p.ldp, C, ldc, nst);
 }

@@ -341,6 +341,30 @@ void launch_adam(float *w, const float *g, float *m, float *v, long long n, floa
                  const float *step_table = nullptr, const int *ctr = nullptr, int table_cap = 1);
 // all weights of the model in one launch (<= kAdamBatch tensors; tensor t = grid row t)
 constexpr int kAdamBatch = 8;
+// The last ordered pass of a weight gradient's split reduction (k_gemm_tn_reduce), deferred
+// into the Adam launch: grad[k][j] = sum over groups q < n_groups, in order, of
+// src[q * K * ldp + k * ldp + j] (the same loads and adds: the same bits), stored to C and used
+// by the update (one GPU; an edge-cut rank all-reduces the finished gradients in between)
+struct TnDeferred {
+  const float *src = nullptr;
+  int n_groups = 0, K = 0, N = 0, ldp = 0;
+  float *C = nullptr;
+};
+struct TnDeferList {
+  int n = 0;
+  TnDeferred d[4];
+  // the deferred passes' inputs (the first pass's group sums) go here, not to the GEMM
+  // workspace that later products of the same backward pass reuse
+  float *pool = nullptr;
+  size_t pool_floats = 0, used = 0;
+};
+// while set (this host thread), tn_reduce records its last pass here instead of launching it
+// when that pass writes a whole [K][N] gradient (ldc = nst = N) from two passes and the list's
+// pool has room for the first pass's output
+void tn_defer(TnDeferList *list);
+// launches every recorded pass not taken by an Adam launch (k_gemm_tn_reduce), empties the list
+void tn_defer_flush(TnDeferList &list, hipStream_t s);
+
 struct AdamBatch {
   float *w[kAdamBatch];
   const float *g[kAdamBatch];
@@ -348,6 +372,7 @@ struct AdamBatch {
   long long n[kAdamBatch];
   int decay[kAdamBatch];
   int count;
+  TnDeferred red[kAdamBatch];  // red[t].src: tensor t's gradient reduced first (into g[t])
 };
 void launch_adam_multi(const AdamBatch &b, float step_size, float beta1, float beta2, float eps,
                        float wd, hipStream_t s, const float *step_table = nullptr,

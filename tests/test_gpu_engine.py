@@ -482,6 +482,45 @@ def test_fused_epilogue_bit_identical(loaded, pgcn, case):
             np.testing.assert_array_equal(a, b)
 
 
+@pytest.mark.parametrize("case", ["lds_dense", "cora", "lds_deep"])
+def test_fold_and_dense_co_draw_bit_identical(loaded, pgcn, case):
+    """r06 launch cuts give the bits of the launches they replace: the weight gradients' last
+    ordered reduction pass inside the Adam launch (tn_fold 1 vs 0: the X-stream TN's and the
+    fused loss kernel's W.grad partials; eager and through the epoch hipGraph) and, on dense X,
+    the hidden dropout's mask drawn in the input dropout's launch (co_draw 2 vs 1): epoch lines,
+    weights, activations and gradients; the launch counter shows the cuts."""
+    if case == "lds_dense":
+        ds, make = pgcn.Dataset.synthetic(120000, 64, 41, 1500000, 21), {}
+    elif case == "lds_deep":
+        ds = pgcn.Dataset.synthetic(70000, 32, 41, 600000, 23)
+        make = dict(hidden_dims=(128, 128, 128), dropouts=(0.5,) * 4)
+    else:
+        ds, make = loaded["cora"], {}
+    runs = {}
+    for name, kn in (("base", dict(tn_fold=0, co_draw=1)), ("cut", dict(tn_fold=1, co_draw=2)),
+                     ("graph", dict(tn_fold=1, co_draw=2, epoch_graph=1))):
+        with helpers.knobs(pgcn, **kn):
+            g = pgcn.GCN(pgcn.make_params(ds, **make), ds)
+            g.train_epoch()
+            g.eval(2)
+            pgcn.reset_path_counts()
+            for _ in range(4):
+                g.epoch_async()
+            lines = g.results(4)
+            n = pgcn.path_counts()["launches"]
+            g.train_epoch()
+            runs[name] = dict(lines=np.array(lines, np.float32), launches=n,
+                              vars=[g.get_var(i) for i in (2, 3, 5)],
+                              grads=[g.get_var(i, 1) for i in (1, 3)] + [g.get_var(2, 1)])
+            g.close()
+    a = runs["base"]
+    for b in (runs["cut"], runs["graph"]):
+        np.testing.assert_array_equal(a["lines"], b["lines"])
+        for x, y in zip(a["vars"] + a["grads"], b["vars"] + b["grads"]):
+            np.testing.assert_array_equal(x, y)
+    assert runs["cut"]["launches"] <= a["launches"] - 4, (a["launches"], runs["cut"]["launches"])
+
+
 def test_co_draw_and_split_rows_bit_identical(loaded, pgcn):
     """cora's small-graph launch cuts give the same bits as the launches they replace: the
     hidden dropout's mask drawn in the input dropout's launch (co_draw 1 vs 0), the hub rows'
