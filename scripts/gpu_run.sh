@@ -6,7 +6,8 @@
 #
 # usage: scripts/gpu_run.sh <outdir under gpurun_out> <step> [<step> ...]
 # steps (arguments after ':' are comma-separated and passed through):
-#   pytest[:<pytest args>]     python -m pytest -m gpu -v <args, default tests> (no -x)
+#   pytest[:<pytest args>]     python -m pytest -m gpu -v <args, default tests> (no -x); '~' is
+#                              a space inside an argument (-k,a~or~b)
 #   smoke                      __graft_entry__.smoke()
 #   bench:<tag>[:<args>]       bench.py <args> -> <tag>.json (+ .err)
 #   g2:<tag>[:<args>]          bench.py --gpus 2 on this one GPU (PGCN_BENCH_SHARE_GPU=1)
@@ -26,6 +27,14 @@ mkdir -p "$O"
 export TMPDIR=/tmp
 
 args_of() { echo "${1//,/ }"; }
+# the comma-separated list as an array in ARGV, '~' standing for a space inside one argument
+# (pytest -k expressions)
+argv_of() {
+  ARGV=()
+  local IFS=,
+  local x
+  for x in $1; do ARGV+=("${x//\~/ }"); done
+}
 
 run() {  # tag, seconds, command... (stdout -> tag.log)
   local tag=$1 secs=$2; shift 2
@@ -40,8 +49,10 @@ for step in "$@"; do
   IFS=: read -r kind a b c <<< "$step"
   case $kind in
     pytest)
+      argv_of "${step#pytest:}"
+      [ "$step" = pytest ] && ARGV=(tests)
       timeout -k 10 1500 python3 -u -m pytest -m gpu -v --timeout 300 \
-          --timeout-method thread $(args_of "${a:-tests}") > "$O/pytest.log" 2>&1
+          --timeout-method thread "${ARGV[@]}" > "$O/pytest.log" 2>&1
       rc=$?
       echo "[pytest] rc=$rc"
       grep -E "FAILED|ERROR" "$O/pytest.log" | head -20
