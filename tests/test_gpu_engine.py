@@ -518,7 +518,10 @@ def test_fold_and_dense_co_draw_bit_identical(loaded, pgcn, case):
         np.testing.assert_array_equal(a["lines"], b["lines"])
         for x, y in zip(a["vars"] + a["grads"], b["vars"] + b["grads"]):
             np.testing.assert_array_equal(x, y)
-    assert runs["cut"]["launches"] <= a["launches"] - 4, (a["launches"], runs["cut"]["launches"])
+    # cora's weight gradients reduce in one pass (the 32-block X-stream TN) and its masks were
+    # co-drawn already: nothing to cut there
+    cut = 0 if case == "cora" else 4
+    assert runs["cut"]["launches"] <= a["launches"] - cut, (a["launches"], runs["cut"]["launches"])
 
 
 def test_co_draw_and_split_rows_bit_identical(loaded, pgcn):
