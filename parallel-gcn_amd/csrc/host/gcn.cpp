@@ -48,7 +48,7 @@ int g_fuse_epilogue = kFuseTails | kFusePrestage | kFuseXstream | kFuseMatmulTai
 int g_fuse_output = 2;
 // "co_draw" (read at engine build): the hidden dropout's mask drawn in the input dropout's
 // launch (1: sparse X; 2: dense X too; bit-identical)
-int g_co_draw = 1;
+int g_co_draw = 2;
 // "tn_fold" (read per epoch): one GPU, the weight gradients' last reduction pass runs inside
 // the Adam launch (GCN::backward_pass; bit-identical)
 int g_tn_fold = 1;
@@ -256,15 +256,18 @@ void init_dropout_rng_range(DropoutRng &r, const uint64_t seed[2], unsigned long
   const long long chunk_hi = ceil_div(r.elem_end, kDropChunk);
   r.n_chunks = std::max(0LL, chunk_hi - r.chunk_lo);
   r.mask_base = r.elem_begin - kDropChunk * r.chunk_lo;
-  std::vector<uint64_t> st((size_t)std::max(1LL, r.n_chunks) * 2, 0);
+  // one state per r.per mask words: the stream's state at the first draw of words per * k
+  const long long n_states = ceil_div(r.n_chunks, (long long)r.per);
+  const int span = kDropChunk * r.per;
+  std::vector<uint64_t> st((size_t)std::max(1LL, n_states) * 2, 0);
   const unsigned long long base = offset + (unsigned long long)kDropChunk * r.chunk_lo;
-  parallel_for(r.n_chunks, [&](long long b, long long e) {
+  parallel_for(n_states, [&](long long b, long long e) {
     uint64_t s[2] = {seed[0], seed[1]};
-    xs_jump(s, base + (unsigned long long)kDropChunk * b);
+    xs_jump(s, base + (unsigned long long)span * b);
     for (long long c = b; c < e; c++) {
       st[(size_t)c * 2] = s[0];
       st[(size_t)c * 2 + 1] = s[1];
-      for (int k = 0; k < kDropChunk; k++) xs_advance(s);
+      for (int k = 0; k < span; k++) xs_advance(s);
     }
   });
   r.states.allocate(st.size());

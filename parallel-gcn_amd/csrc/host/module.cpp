@@ -64,7 +64,7 @@ Dropout::Dropout(shared_ptr<Variable> in_, float p_, shared_ptr<DropoutRng> rng_
 void Dropout::draw(hipStream_t s, uint64_t *mask, int max_blocks) const {
   const DropoutRng &r = *rng;
   launch_dropout_mask(r.states.get(), r.n_chunks, 64 * r.chunk_lo, r.elem_end, p, mask,
-                      ctx->jump_table, s, max_blocks);
+                      ctx->jump_table, s, max_blocks, r.per);
 }
 
 void Dropout::draw_ahead(hipStream_t s, const Event *ready) const {
@@ -78,9 +78,9 @@ void Dropout::draw_ahead(hipStream_t s, const Event *ready) const {
     // with the hidden dropout's next mask (co_draw; the eval forward uses neither)
     const DropoutRng &r = *rng, &q = co_draw->state();
     const MaskDraw a{r.states.get(), r.n_chunks, 64 * r.chunk_lo, r.elem_end, p,
-                     rng->mask_ahead.get()};
+                     rng->mask_ahead.get(), r.per};
     const MaskDraw b{q.states.get(), q.n_chunks, 64 * q.chunk_lo, q.elem_end, co_draw->p,
-                     q.mask.get()};
+                     q.mask.get(), q.per};
     launch_dropout_mask2(a, b, ctx->jump_table, s);
     co_draw->pre_drawn = true;
   } else {
@@ -123,9 +123,10 @@ void Dropout::forward(bool training, const Stream &s) const {
     pre_drawn = false;
   } else if (co_draw && !co_draw->pre_drawn && !co_draw->ahead) {
     const DropoutRng &q = co_draw->state();
-    const MaskDraw a{r.states.get(), r.n_chunks, 64 * r.chunk_lo, r.elem_end, p, r.mask.get()};
+    const MaskDraw a{r.states.get(), r.n_chunks, 64 * r.chunk_lo, r.elem_end, p, r.mask.get(),
+                     r.per};
     const MaskDraw b{q.states.get(), q.n_chunks, 64 * q.chunk_lo, q.elem_end, co_draw->p,
-                     q.mask.get()};
+                     q.mask.get(), q.per};
     launch_dropout_mask2(a, b, ctx->jump_table, s.get());
     co_draw->pre_drawn = true;
   } else {

@@ -109,51 +109,68 @@ struct MaskSeg {
   long long n_chunks = 0, elem0 = 0, elem_end = 0;
   int threshold = 0;
   uint64_t *mask = nullptr;
+  int per = 1;  // 64-draw words per stored state (MaskDraw::per)
 };
 
+// PER = 2 (r06, the engine's layout): one state per 128 draws -- a thread draws two mask words
+// from it and jumps it by the epoch's period once, where PER = 1 jumps per 64 draws (32 table
+// lookups and 64 three-input xors: 2.5 of the ~14.5 VALU ops per draw) and reads and writes
+// twice the states (35 MB per epoch on reddit's input mask)
+template <int PER>
 __device__ __forceinline__ void dropout_mask_seg(const MaskSeg &sg, const uint4 *lut, long long bid,
                                                  long long nblk) {
   uint64_t *__restrict__ states = sg.states;
   uint64_t *__restrict__ mask = sg.mask;
   const long long n_chunks = sg.n_chunks, elem0 = sg.elem0, elem_end = sg.elem_end;
+  const long long n_states = (n_chunks + PER - 1) / PER;
   const int threshold = sg.threshold;
-  // mask word of chunk c, then its state advanced by `period` draws: M^period * (a0, a1)
-  auto emit = [&](long long c, uint64_t a0, uint64_t a1, uint64_t word) {
+  // mask word of 64-draw chunk c (trimmed past elem_end; no word past n_chunks)
+  auto put = [&](long long c, uint64_t word) {
+    if (c >= n_chunks) return;
     const long long e = elem0 + 64 * c;  // first element of this chunk
     if (e + 64 > elem_end) {
       const long long valid = elem_end - e;
       word = valid <= 0 ? 0 : (word & ((valid >= 64) ? ~0ull : ((1ull << valid) - 1)));
     }
     mask[c] = word;
+  };
+  // state k advanced by `period` draws: M^period * (a0, a1)
+  auto advance = [&](long long k, uint64_t a0, uint64_t a1) {
     uint64_t n1;
     const uint64_t n0 = dmn_advance(lut, a0, a1, n1);
-    states[2 * c] = n0;
-    states[2 * c + 1] = n1;
+    states[2 * k] = n0;
+    states[2 * k + 1] = n1;
   };
   // two chunks per thread and iteration: two independent xorshift chains interleaved (each
   // draw is a serial chain of 64-bit ops; the pair hides their latency at low occupancy)
   const long long G = nblk * blockDim.x;
-  for (long long c = bid * blockDim.x + threadIdx.x; c < n_chunks; c += 2 * G) {
+  for (long long c = bid * blockDim.x + threadIdx.x; c < n_states; c += 2 * G) {
     const long long c2 = c + G;
-    const bool two = c2 < n_chunks;
+    const bool two = c2 < n_states;
     const long long cb = two ? c2 : c;
     const uint64_t a0 = states[2 * c], a1 = states[2 * c + 1];
     const uint64_t b0 = states[2 * cb], b1 = states[2 * cb + 1];
     Xs64 x{a0, a1}, y{b0, b1};
     x.thr2 = y.thr2 = (uint32_t)threshold << 1;
 #pragma unroll
-    for (int j = 0; j < 64; j++) {
-      x.step(j, threshold);
-      y.step(j, threshold);
-    }
+    for (int q = 0; q < PER; q++) {  // word q of each state's run
+#pragma unroll
+      for (int j = 0; j < 64; j++) {
+        x.step(j, threshold);
+        y.step(j, threshold);
+      }
 #if PGCN_DROP_SHIFTIN
-    x.lo = __builtin_bitreverse32(x.lo);
-    x.hi = __builtin_bitreverse32(x.hi);
-    y.lo = __builtin_bitreverse32(y.lo);
-    y.hi = __builtin_bitreverse32(y.hi);
+      x.lo = __builtin_bitreverse32(x.lo);
+      x.hi = __builtin_bitreverse32(x.hi);
+      y.lo = __builtin_bitreverse32(y.lo);
+      y.hi = __builtin_bitreverse32(y.hi);
 #endif
-    emit(c, a0, a1, ((uint64_t)x.hi << 32) | x.lo);
-    if (two) emit(c2, b0, b1, ((uint64_t)y.hi << 32) | y.lo);
+      put(PER * c + q, ((uint64_t)x.hi << 32) | x.lo);
+      if (two) put(PER * c2 + q, ((uint64_t)y.hi << 32) | y.lo);
+      x.lo = x.hi = y.lo = y.hi = 0;
+    }
+    advance(c, a0, a1);
+    if (two) advance(c2, b0, b1);
   }
 }
 
@@ -165,10 +182,14 @@ __global__ __launch_bounds__(256) void k_dropout_mask(MaskSeg a, MaskSeg b, int 
     lut[i] = table[(p >> 1) * 256 + (v << (4 * (p & 1)))];
   }
   __syncthreads();
-  if ((int)blockIdx.x < blocks_a)
-    dropout_mask_seg(a, lut, blockIdx.x, blocks_a);
+  const bool in_a = (int)blockIdx.x < blocks_a;
+  const MaskSeg &sg = in_a ? a : b;
+  const long long bid = in_a ? blockIdx.x : blockIdx.x - blocks_a;
+  const long long nblk = in_a ? blocks_a : gridDim.x - blocks_a;
+  if (sg.per == 2)
+    dropout_mask_seg<2>(sg, lut, bid, nblk);
   else
-    dropout_mask_seg(b, lut, blockIdx.x - blocks_a, gridDim.x - blocks_a);
+    dropout_mask_seg<1>(sg, lut, bid, nblk);
 }
 
 // x[i] *= bit(base + i) ? scale : 0   (Dropout::forward on a grad-carrying variable and
@@ -891,12 +912,14 @@ static int grid_for(long long work, int block = 256, int cap = 2048) {
 
 void launch_dropout_mask(uint64_t *states, long long n_chunks, long long elem0,
                          long long elem_end, float p, uint64_t *mask, const void *table,
-                         hipStream_t s, int max_blocks) {
+                         hipStream_t s, int max_blocks, int per) {
   if (n_chunks <= 0) return;
+  PGCN_CHECK(per == 1 || per == 2, PGCN_E_INVALID, "dropout_mask: words per state");
   // hpdga module.cpp:211: threshold = int(p * MY_RAND_MAX) evaluated in float
   const int threshold = (int)(p * (float)0x7fffffff);
   // 8 KB LDS: up to 8 workgroups per CU (a side-stream draw takes fewer: max_blocks)
-  const int grid = grid_for(ceil_div(n_chunks, 2), 256, max_blocks > 0 ? max_blocks : 8 * kCUs);
+  const int grid = grid_for(ceil_div(ceil_div(n_chunks, per), 2), 256,
+                            max_blocks > 0 ? max_blocks : 8 * kCUs);
   MaskSeg a;
   a.states = states;
   a.n_chunks = n_chunks;
@@ -904,6 +927,7 @@ void launch_dropout_mask(uint64_t *states, long long n_chunks, long long elem0,
   a.elem_end = elem_end;
   a.threshold = threshold;
   a.mask = mask;
+  a.per = per;
   PGCN_LAUNCH(k_dropout_mask, dim3(grid), dim3(256), 0, s, a, MaskSeg{}, grid,
               static_cast<const uint4 *>(table));
 }
@@ -920,7 +944,11 @@ void launch_dropout_mask2(const MaskDraw &d0, const MaskDraw &d1, const void *ta
     sg[i].elem_end = d[i]->elem_end;
     sg[i].threshold = (int)(d[i]->p * (float)0x7fffffff);  // as launch_dropout_mask
     sg[i].mask = d[i]->mask;
-    g[i] = sg[i].n_chunks > 0 ? grid_for(ceil_div(sg[i].n_chunks, 2), 256, 8 * kCUs) : 0;
+    PGCN_CHECK(d[i]->per == 1 || d[i]->per == 2, PGCN_E_INVALID, "dropout_mask2: words per state");
+    sg[i].per = d[i]->per;
+    g[i] = sg[i].n_chunks > 0 ? grid_for(ceil_div(ceil_div(sg[i].n_chunks, d[i]->per), 2), 256,
+                                         8 * kCUs)
+                              : 0;
   }
   if (g[0] + g[1] == 0) return;
   PGCN_LAUNCH(k_dropout_mask, dim3(g[0] + g[1]), dim3(256), 0, s, sg[0], sg[1], g[0],

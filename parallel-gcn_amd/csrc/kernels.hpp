@@ -287,13 +287,16 @@ void launch_spmm_csc_bwd(int nf, int p, int ldg, const int *csc_ptr, const int *
 
 void launch_dropout_mask(uint64_t *states, long long n_chunks, long long elem0,
                          long long elem_end, float p, uint64_t *mask, const void *table,
-                         hipStream_t s, int max_blocks = 0);
+                         hipStream_t s, int max_blocks = 0, int per = 1);
 // two variables' draws (each as launch_dropout_mask's arguments) in one launch
+// per: 64-draw mask words per stored state (1, or 2: one state per 128 draws -- half the state
+// traffic and half the period jumps per draw, the engine's layout; the C ABI's is 1)
 struct MaskDraw {
   uint64_t *states;
   long long n_chunks, elem0, elem_end;
   float p;
   uint64_t *mask;
+  int per = 1;
 };
 void launch_dropout_mask2(const MaskDraw &d0, const MaskDraw &d1, const void *table,
                           hipStream_t s);

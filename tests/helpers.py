@@ -231,7 +231,7 @@ def parse_line(line):
 ENGINE_DEFAULTS = {"train_ahead": 1, "split_rows": 0, "split_cols": 1, "eval_ax": 1,
                    "epoch_graph": 0, "fuse_epilogue": 15, "fuse_output": 2, "mm_side": 0,
                    "xstream_ring": 1, "lds_min_kb": -1, "lds_blocks": 0,
-                   "parse_threads": 0, "gs_split": 3, "gs_item_iters": 0, "co_draw": 1,
+                   "parse_threads": 0, "gs_split": 3, "gs_item_iters": 0, "co_draw": 2,
                    "gs_orig_cols": 1, "sparse_dual": 1, "eval_tail": 0, "gs16_gather": 0,
                    "peer_uncached": 0, "ring_pair": 0, "tn_fold": 1}
 
