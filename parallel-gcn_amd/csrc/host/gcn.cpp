@@ -49,6 +49,9 @@ int g_fuse_output = 2;
 // "co_draw" (read at engine build): the hidden dropout's mask drawn in the input dropout's
 // launch (1: sparse X; 2: dense X too; bit-identical)
 int g_co_draw = 2;
+// "fuse_finish" (read per pass): one GPU, the loss kernel's last block sums the pass's
+// scalars and writes its results ring slot (XentFinal; one launch fewer per pass)
+int g_fuse_finish = 1;
 // "tn_fold" (read per epoch): one GPU, the weight gradients' last reduction pass runs inside
 // the Adam launch (GCN::backward_pass; bit-identical)
 int g_tn_fold = 1;
@@ -880,11 +883,42 @@ void GCN::set_split(int split) {
   }
 }
 
+// One GPU ("fuse_finish", default on): the next pass's loss kernel finishes its scalars itself
+// into results_ring slot dst_offset (XentFinal), so finalize() launches nothing
+void GCN::arm_finish(int dst_offset, bool graph) {
+  ctx.fin = nullptr;
+  ctx.fin_taken = false;
+  if (!g_fuse_finish || comm) return;
+  if (!fin_ticket) {
+    fin_ticket.allocate(1);
+    fin_ticket.zero();
+    fin_part4.allocate((size_t)std::max(1, ctx.xent_blocks) * 4);
+  }
+  const auto &w1 = weights.front();
+  fin_desc = XentFinal{};
+  fin_desc.w = w1->dev_data.get();
+  fin_desc.n_w = w1->size;
+  fin_desc.wd = adam_params.weight_decay;
+  fin_desc.out2 = results_ring.get() + dst_offset;
+  fin_desc.ctr = graph ? dev_ctr.get() : nullptr;
+  fin_desc.ring_cap = ring_cap;
+  fin_desc.sums = sums.get();
+  fin_desc.ticket = fin_ticket.get();
+  fin_desc.part4 = reinterpret_cast<float4 *>(fin_part4.get());
+  ctx.fin = &fin_desc;
+}
+
 // loss/acc of the pass just enqueued -> results_ring slot (finalize, src/gcn.cu:440-455);
 // graph: the slot from the device epoch counter
 void GCN::finalize(int dst_offset, bool graph, hipStream_t s) {
   const auto &w1 = weights.front();
   if (!s) s = stream.get();
+  if (ctx.fin_taken) {  // the loss kernel's last block did it (fuse_finish)
+    ctx.fin_taken = false;
+    ctx.fin = nullptr;
+    return;
+  }
+  ctx.fin = nullptr;
   if (!comm) {  // one launch: reduce + compose
     launch_reduce_scalars(xent_partials.get(), ctx.xent_blocks, w1->dev_data.get(), w1->size,
                           sums.get(), stream.get(), ctx.count, adam_params.weight_decay,
@@ -913,6 +947,7 @@ void GCN::finalize(int dst_offset, bool graph, hipStream_t s) {
 // next GraphSum waits for tail_done.
 void GCN::eval_forward(int off, bool graph) {
   const bool tail = tail_gs >= 0;
+  arm_finish(off, graph);
   for (int i = 0; i < (int)modules.size(); i++) {
     if (tail && i == tail_gs) {
       ctx.tail_stream = comm_stream.get();
@@ -990,6 +1025,7 @@ void GCN::enqueue_epoch(bool graph) {
   set_split(1);
   TnDeferList defer;
   FoldScope fold(*this, &defer);
+  arm_finish(slot4, graph);
   for (const auto &m : modules) m->forward(true, stream);
   finalize(slot4, graph);
   backward_pass(fold);
@@ -1076,6 +1112,7 @@ std::pair<float, float> GCN::train_epoch() {
   set_split(1);
   TnDeferList defer;
   FoldScope fold(*this, &defer);
+  arm_finish((int)(slot * 4), false);
   for (const auto &m : modules) m->forward(true, stream);
   finalize((int)(slot * 4));
   backward_pass(fold);

@@ -188,6 +188,11 @@ class GCN {
   std::vector<const Dropout *> dropouts_;
   Adam optimizer;
   DeviceBuffer<float> tn_pool;  // tn_fold: the deferred reduction passes' inputs
+  // fuse_finish: the loss kernel's arrival ticket, per-block partials and the pass descriptor
+  DeviceBuffer<unsigned> fin_ticket;
+  DeviceBuffer<float> fin_part4;
+  XentFinal fin_desc;
+  void arm_finish(int dst_offset, bool graph);
   DeviceBuffer<float> grad_arena;  // all weight grads, one all-reduce
   DeviceBuffer<uint8_t> jump_table;
   DeviceBuffer<float> gemm_ws, gemm_ws_side;

@@ -749,7 +749,8 @@ void CrossEntropyLoss::forward(bool training, const Stream &s) const {
     launch_out_xent(Hv.dev_data.get(), Hv.ld, fused->inner(), Wv.dev_data.get(), Wv.ld,
                     logits->dev_data.get(), logits->ld, training ? logits->dev_grad.get() : nullptr,
                     ctx->truth, logits->rows, num_classes, ctx->count, training ? 1 : 0,
-                    ctx->xent_partials, s.get(), dH, Hv.ld, dWp, staged ? &tb : nullptr);
+                    ctx->xent_partials, s.get(), dH, Hv.ld, dWp, staged ? &tb : nullptr, ctx->fin);
+    ctx->fin_taken = ctx->fin != nullptr;
     if (dWp)
       launch_tn_reduce_blocks(dWp, nb, fused->inner(), num_classes, 48, Wv.dev_grad.get(), Wv.ld,
                               s.get());
@@ -761,7 +762,9 @@ void CrossEntropyLoss::forward(bool training, const Stream &s) const {
   launch_xent_fwd(L.dev_data.get(), L.ld, training ? L.dev_grad.get() : nullptr,
                   ctx->compact_n ? ctx->compact_truth : ctx->truth,
                   ctx->compact_n ? ctx->compact_n : logits->rows, num_classes, ctx->count,
-                  training ? 1 : 0, ctx->xent_partials, s.get(), ctx->compact_n ? 0 : 1);
+                  training ? 1 : 0, ctx->xent_partials, s.get(), ctx->compact_n ? 0 : 1,
+                  ctx->fin);
+  ctx->fin_taken = ctx->fin != nullptr;
 }
 
 void CrossEntropyLoss::backward(const Stream &) const {}  // module.cpp:155-156

@@ -140,6 +140,11 @@ struct ModuleContext {
   int count = 0;               // labelled rows of the current split (global)
   float *xent_partials = nullptr;
   int xent_blocks = 0;
+  // one GPU ("fuse_finish"): the pass's scalars finished by the loss kernel's last block
+  // (XentFinal); set by GCN for the pass being enqueued, fin_taken by the loss module that
+  // passed it on (GCN::finalize then launches nothing)
+  const XentFinal *fin = nullptr;
+  bool fin_taken = false;
   Comm *comm = nullptr;        // null on one GPU
   hipStream_t comm_stream = nullptr;      // edge-cut: stream of the reduce-scatters
   int local_rows = 0;                     // edge-cut: this rank's rows (the rest is padding)

@@ -336,6 +336,61 @@ __host__ __device__ inline int xent_stride(int ld) {
 }
 typedef float floatx4e __attribute__((ext_vector_type(4)));
 
+// XentFinal (kernels.hpp): the pass's scalars finished by the loss kernel's last block.  Called
+// by every thread at the end of a block whose thread 0 holds the block's (loss, wrong) in
+// red[0], red[1] (xent_tile).  Write-through partials (sc1 stores, drained, then the ticket)
+// and write-through loads in the last block: the hand-off needs no cache maintenance
+// (MI355X_MICROARCH.md, inter-workgroup visibility: sc1 stores + agent-scope atomic counter,
+// the last adder's sc1 loads after a workgroup barrier)
+__device__ __forceinline__ void xent_finish(const XentFinal &fin, int count, float *red) {
+  __shared__ float fred[16];
+  __shared__ int last;
+  // this block's slice of sum w^2 (W1 split evenly over the blocks, in index order per thread)
+  const long long per = (fin.n_w + gridDim.x - 1) / gridDim.x;
+  const long long lo = (long long)blockIdx.x * per, hi = min(fin.n_w, lo + per);
+  float q = 0.0f;
+  for (long long i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    const float v = fin.w[i];
+    q += v * v;
+  }
+  q = block_sum<XT>(q, fred);
+  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      fin.part4, 0, (int)(gridDim.x * 16), 0x00020000);
+  if (threadIdx.x == 0) {
+    const u4 d = {__float_as_uint(red[0]), __float_as_uint(red[1]), __float_as_uint(q), 0u};
+    __builtin_amdgcn_raw_buffer_store_b128(d, rs, (int)(blockIdx.x * 16), 0, 16);  // sc1
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned old =
+        __hip_atomic_fetch_add(fin.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  float l = 0.0f, wr = 0.0f, w2 = 0.0f;
+  for (int b = threadIdx.x; b < (int)gridDim.x; b += blockDim.x) {
+    const u4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, b * 16, 0, 16);  // sc1
+    l += __uint_as_float(v.x);
+    wr += __uint_as_float(v.y);
+    w2 += __uint_as_float(v.z);
+  }
+  l = block_sum<XT>(l, fred);
+  wr = block_sum<XT>(wr, fred);
+  w2 = block_sum<XT>(w2, fred);
+  if (threadIdx.x == 0) {
+    if (fin.sums) {
+      fin.sums[0] = l;
+      fin.sums[1] = wr;
+    }
+    float *o = fin.out2;
+    if (fin.ctr) o += 4 * (fin.ctr[1] % fin.ring_cap);
+    o[0] = l / (float)count + fin.wd * w2 / 2.0f;
+    o[1] = (float)(count - (int)wr) / (float)count;
+    __hip_atomic_store(fin.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+
 // a wave's LDS writes are visible to its own later LDS reads (one wave: in-order LDS pipe);
 // this keeps the compiler from moving the reads above the writes
 __device__ __forceinline__ void wave_lds_fence() {
@@ -420,7 +475,8 @@ __device__ __forceinline__ void xent_tile(float *__restrict__ logits, int ld_rt,
                                                   const float *__restrict__ H, int ldh, int kh_rt,
                                                   const float *__restrict__ W, int ldw,
                                                   float *__restrict__ dH, int lddh,
-                                                  float *__restrict__ dWp, const XentTable &tb) {
+                                                  float *__restrict__ dWp, const XentTable &tb,
+                                                  const XentFinal &fin) {
   // write_back 0: the shifted logits stay in LDS (the compact output layer's logits are read
   // by nobody after the loss; hpdga's in-place shift is kept where the variable is visible)
   extern __shared__ float smem[];
@@ -734,7 +790,10 @@ __device__ __forceinline__ void xent_tile(float *__restrict__ logits, int ld_rt,
     }
     partials[2 * blockIdx.x] = ls;
     partials[2 * blockIdx.x + 1] = ws;
+    red[0] = ls;  // (this thread's own reads of red are done)
+    red[1] = ws;
   }
+  if (fin.ticket) xent_finish(fin, count, red);
   XST(9);
 #ifdef PGCN_XENT_STAMPS
   st[11] = __builtin_amdgcn_s_memrealtime();
@@ -752,11 +811,11 @@ __device__ __forceinline__ void xent_tile(float *__restrict__ logits, int ld_rt,
   float *__restrict__ logits, int ld, float *__restrict__ grad, const int *__restrict__ truth,   \
       int n, int c, int count, int training, float *__restrict__ partials, int write_back,       \
       const float *__restrict__ H, int ldh, int kh, const float *__restrict__ W, int ldw,        \
-      float *__restrict__ dH, int lddh, float *__restrict__ dWp, XentTable tb
+      float *__restrict__ dH, int lddh, float *__restrict__ dWp, XentTable tb, XentFinal fin
 // the loss over given logits (61 VGPRs at 8 waves per SIMD would spill its copy registers)
 __global__ __launch_bounds__(XT) void k_xent_fwd(PGCN_XENT_ARGS) {
   xent_tile<false>(logits, ld, grad, truth, n, c, count, training, partials, write_back, H, ldh,
-                   kh, W, ldw, dH, lddh, dWp, tb);
+                   kh, W, ldw, dH, lddh, dWp, tb, fin);
 }
 // the fused output layer + loss at 8 waves per SIMD (<= 64 VGPRs, no spill; reddit training
 // call 45.0 -> 43.2 us, r03)
@@ -764,7 +823,7 @@ template <int CC, int LDC, int KH>
 __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(8))) void k_out_xent(
     PGCN_XENT_ARGS) {
   xent_tile<true, CC, LDC, KH>(logits, ld, grad, truth, n, c, count, training, partials,
-                               write_back, H, ldh, kh, W, ldw, dH, lddh, dWp, tb);
+                               write_back, H, ldh, kh, W, ldw, dH, lddh, dWp, tb, fin);
 }
 #undef PGCN_XENT_ARGS
 
@@ -981,21 +1040,26 @@ void launch_empty(int n, hipStream_t s) {
 }
 
 void launch_xent_fwd(float *logits, int ld, float *grad, const int *truth, int n, int c,
-                     int count, int training, float *partials, hipStream_t s, int write_back) {
+                     int count, int training, float *partials, hipStream_t s, int write_back,
+                     const XentFinal *fin) {
   if (n <= 0) return;
   PGCN_CHECK(ld <= 124 && c <= ld && ld % 4 == 0, PGCN_E_INVALID,
              "xent: classes must be <= 124 (ld a multiple of 4)");
+  PGCN_CHECK(!fin || (fin->ticket && fin->part4 && fin->out2), PGCN_E_INVALID,
+             "xent: the fused finish needs its ticket, partials and output");
   const size_t lds = (size_t)XR * xent_stride(ld) * sizeof(float);  // <= 64*124*4 = 31 KB
   PGCN_LAUNCH(k_xent_fwd, dim3(xent_blocks(n)), dim3(XT), lds, s, logits, ld, grad,
                      truth, n, c, count, training, partials, write_back, nullptr, 0, 0, nullptr, 0,
-                     nullptr, 0, nullptr, XentTable{});
+                     nullptr, 0, nullptr, XentTable{}, fin ? *fin : XentFinal{});
 }
 
 void launch_out_xent(const float *H, int ldh, int kh, const float *W, int ldw, float *logits,
                      int ld, float *grad, const int *truth, int n, int c, int count, int training,
                      float *partials, hipStream_t s, float *dH, int lddh, float *dWp,
-                     const XentTable *tb) {
+                     const XentTable *tb, const XentFinal *fin) {
   note_path(KP_OUT_XENT);
+  PGCN_CHECK(!fin || (fin->ticket && fin->part4 && fin->out2), PGCN_E_INVALID,
+             "out_xent: the fused finish needs its ticket, partials and output");
   const XentTable t = training && dH && tb ? *tb : XentTable{};
   PGCN_CHECK(!t.table || (kh == 16 && t.scale), PGCN_E_INVALID,
              "out_xent: a prescaled table of a 16-column dH");
@@ -1009,7 +1073,7 @@ void launch_out_xent(const float *H, int ldh, int kh, const float *W, int ldw, f
 #define OUT_XENT(...)                                                                          \
   PGCN_LAUNCH((k_out_xent<__VA_ARGS__>), dim3(xent_blocks(n)), dim3(XT), lds, s, logits, ld, grad, \
               truth, n, c, count, training, partials, 1, H, ldh, kh, W, ldw,                     \
-              training ? dH : nullptr, lddh, training ? dWp : nullptr, t)
+              training ? dH : nullptr, lddh, training ? dWp : nullptr, t, fin ? *fin : XentFinal{})
   if (c == 41 && ld == 44 && kh == 16)  // reddit (41 classes, hidden 16)
     OUT_XENT(41, 44, 16);
   else

@@ -320,17 +320,36 @@ struct XentTable {
   const int *pos = nullptr;
   int rows = 0;
 };
+// One GPU (r06): the pass's scalars finished inside the loss kernel -- k_reduce_scalars' work
+// done by its last-arriving block.  Every block writes {loss, wrong, its slice of sum w^2, 0}
+// to part4[block] write-through (sc1) and adds one to *ticket; the block whose add returns
+// gridDim - 1 reads every part4 write-through, sums them in block order (a fixed tree), writes
+// out2 = {loss / count + wd * l2 / 2, (count - wrong) / count} (slot 4 * (ctr[1] % ring_cap)
+// with ctr) and the optional sums {loss, wrong}, and zeroes the ticket for the next launch
+struct XentFinal {
+  const float *w = nullptr;  // W1 (the l2 term), n_w floats
+  long long n_w = 0;
+  float wd = 0.0f;
+  float *out2 = nullptr;
+  const int *ctr = nullptr;
+  int ring_cap = 1;
+  float *sums = nullptr;
+  unsigned *ticket = nullptr;  // zero between launches
+  float4 *part4 = nullptr;     // [blocks]
+};
 void launch_out_xent(const float *H, int ldh, int kh, const float *W, int ldw, float *logits,
                      int ld, float *grad, const int *truth, int n, int c, int count, int training,
                      float *partials, hipStream_t s, float *dH = nullptr, int lddh = 0,
-                     float *dWp = nullptr, const XentTable *tb = nullptr);
+                     float *dWp = nullptr, const XentTable *tb = nullptr,
+                     const XentFinal *fin = nullptr);
 // with dWp (training, <= 48 classes): per-block partials [xent_blocks(n)][kh][48] of W.grad =
 // H^T grad, reduced in block order into C [kh][ldc] (N = c columns) by:
 void launch_tn_reduce_blocks(float *partial, int n_blocks, int K, int N, int ldp, float *C, int ldc,
                              hipStream_t s);
 size_t tn_reduce_blocks_workspace(int n_blocks, int K, int ldp);
 void launch_xent_fwd(float *logits, int ld, float *grad, const int *truth, int n, int c,
-                     int count, int training, float *partials, hipStream_t s, int write_back = 1);
+                     int count, int training, float *partials, hipStream_t s, int write_back = 1,
+                     const XentFinal *fin = nullptr);
 // sums (optional): {loss sum, wrong}; out2 (optional): the composed {loss + l2, accuracy};
 // raw4 (optional): {loss sum, wrong, sum w^2, count} for a composition after an all-reduce
 void launch_reduce_scalars(const float *partials, int n_blocks, const float *w, long long n_w,
