@@ -862,6 +862,13 @@ void launch_xstream_tn(int M, int N, int K, const float *A, int lda, const float
   const int blocks = xs_tn_blocks(M, K, lda);
   const TnPlan p = xs_tn_plan(K, blocks);
   float *partial = static_cast<float *>(workspace);
+  // one ordered pass over the block partials (the small graphs' 32 blocks): under tn_defer the
+  // partials go to the deferred list's pool and the Adam launch makes that pass
+  const int one_pass = blocks == XS_TN_SMALL_BLOCKS ? TN_ONE_PASS : 0;
+  float *room = M > 0 && p.n_slabs <= std::max(one_pass, p.spg)
+                    ? tn_defer_room(N, ldc, ldc, (size_t)p.n_slabs * K * p.ldp)
+                    : nullptr;
+  if (room) partial = room;
   if (M > 0 && xstream_ring_ok(K, lda)) {
     launch_xstream_tn_ring(M, N, K, A, lda, G, ldg, maskT, a_scale, partial, XS_TN_BLOCKS, s,
                            flat);
@@ -882,7 +889,17 @@ void launch_xstream_tn(int M, int N, int K, const float *A, int lda, const float
     }
 #undef XTN_CASE
   }
-  tn_reduce(p, M, N, K, partial, C, ldc, s, -1, blocks == XS_TN_SMALL_BLOCKS ? TN_ONE_PASS : 0);
+  if (room) {
+    TnDeferred &d = g_tn_defer->d[g_tn_defer->n++];
+    d.src = partial;
+    d.n_groups = p.n_slabs;
+    d.K = K;
+    d.N = N;
+    d.ldp = p.ldp;
+    d.C = C;
+    return;
+  }
+  tn_reduce(p, M, N, K, partial, C, ldc, s, -1, one_pass);
 }
 
 static void gemm_tn_slab(int M, int N, int K, const float *A, int lda, const float *G, int ldg,

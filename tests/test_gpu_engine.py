@@ -518,10 +518,41 @@ def test_fold_and_dense_co_draw_bit_identical(loaded, pgcn, case):
         np.testing.assert_array_equal(a["lines"], b["lines"])
         for x, y in zip(a["vars"] + a["grads"], b["vars"] + b["grads"]):
             np.testing.assert_array_equal(x, y)
-    # cora's weight gradients reduce in one pass (the 32-block X-stream TN) and its masks were
-    # co-drawn already: nothing to cut there
-    cut = 0 if case == "cora" else 4
-    assert runs["cut"]["launches"] <= a["launches"] - cut, (a["launches"], runs["cut"]["launches"])
+    # (cora: its one-pass W2.grad reduce; its masks were co-drawn already)
+    assert runs["cut"]["launches"] <= a["launches"] - 4, (a["launches"], runs["cut"]["launches"])
+
+
+@pytest.mark.parametrize("case", ["cora", "lds_dense"])
+def test_fuse_finish_matches_reduce_launch(loaded, pgcn, case):
+    """fuse_finish 1: the loss kernel's last block sums the pass's (loss, wrong, W1^2) partials
+    and writes the results ring slot (one launch fewer per pass) -- the same losses and
+    accuracies as the separate k_reduce_scalars launch up to the summation order (1e-6
+    relative; the accuracies exactly), the same gradients and weights bit for bit (the scalars
+    feed nothing else); eager and through the epoch hipGraph; one launch fewer per pass."""
+    if case == "lds_dense":
+        ds = pgcn.Dataset.synthetic(120000, 64, 41, 1500000, 21)
+    else:
+        ds = loaded["cora"]
+    runs = {}
+    for name, kn in (("launch", dict(fuse_finish=0)), ("fused", dict(fuse_finish=1)),
+                     ("graph", dict(fuse_finish=1, epoch_graph=1))):
+        with helpers.knobs(pgcn, **kn):
+            g = pgcn.GCN(pgcn.make_params(ds), ds)
+            sync_lines = [g.train_epoch() + g.eval(2) for _ in range(2)]
+            pgcn.reset_path_counts()
+            for _ in range(4):
+                g.epoch_async()
+            lines = np.array(sync_lines + [tuple(x) for x in g.results(4)], np.float64)
+            n = pgcn.path_counts()["launches"]
+            runs[name] = dict(lines=lines, launches=n, w=[g.get_var(2), g.get_var(4)])
+            g.close()
+    a = runs["launch"]
+    for b in (runs["fused"], runs["graph"]):
+        np.testing.assert_allclose(b["lines"][:, [0, 2]], a["lines"][:, [0, 2]], rtol=1e-6)
+        np.testing.assert_array_equal(b["lines"][:, [1, 3]], a["lines"][:, [1, 3]])
+        for x, y in zip(a["w"], b["w"]):
+            np.testing.assert_array_equal(x, y)
+    assert runs["fused"]["launches"] == a["launches"] - 8, (a["launches"], runs["fused"]["launches"])
 
 
 def test_co_draw_and_split_rows_bit_identical(loaded, pgcn):
