@@ -251,8 +251,12 @@ void build_dev_features(DevFeatures &feats, const int *fptr, const int *indices,
 // Chunk states of a dropout over global elements [elem_begin, elem_end) whose first training
 // forward draws stream positions offset + element (hpdga: one xorshift128+ draw per element,
 // module.cpp:208-219), each 64-element chunk's state jumped to from the seed state.
+// "mask_per" (read at engine build): 64-draw mask words per stored RNG state (1 or 2)
+int g_mask_per = 2;
+
 void init_dropout_rng_range(DropoutRng &r, const uint64_t seed[2], unsigned long long offset,
                             long long elem_begin, long long elem_end) {
+  r.per = g_mask_per;
   r.elem_begin = elem_begin;
   r.elem_end = elem_end;
   r.chunk_lo = r.elem_begin / kDropChunk;

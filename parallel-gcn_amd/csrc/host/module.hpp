@@ -72,7 +72,8 @@ struct DropoutRng {
   DeviceBuffer<uint64_t> mask;    // 1 word per chunk: the last training forward's mask
   DeviceBuffer<uint64_t> mask_ahead;  // the next one, when drawn ahead (input dropout)
   long long chunk_lo = 0, n_chunks = 0;
-  // 64-draw mask words per stored state (k_dropout_mask's PER; one state per 128 draws)
+  // 64-draw mask words per stored state (k_dropout_mask's PER; one state per 128 draws;
+  // "mask_per" knob, read at engine build)
   int per = 2;
   long long elem_begin = 0, elem_end = 0;  // global element range of this rank
   long long mask_base = 0;                 // bit of local element 0 in `mask`

@@ -523,6 +523,28 @@ def test_fold_and_dense_co_draw_bit_identical(loaded, pgcn, case):
 
 
 @pytest.mark.parametrize("case", ["cora", "lds_dense"])
+def test_mask_states_per_128_draws_bit_identical(loaded, pgcn, case):
+    """mask_per 2 (one xorshift state per 128 draws, jumped by the epoch's period once) draws
+    the masks of mask_per 1 (a state per 64 draws): epoch lines, the dropped input and every
+    weight and gradient bit for bit over 4 epochs (an odd chunk count included: cora's input
+    mask has 49,216 nonzeros / 64 = 769 chunks)."""
+    ds = (pgcn.Dataset.synthetic(120000, 64, 41, 1500000, 21) if case == "lds_dense"
+          else loaded["cora"])
+    runs = []
+    for per in (1, 2):
+        with helpers.knobs(pgcn, mask_per=per):
+            g = pgcn.GCN(pgcn.make_params(ds), ds)
+            lines = [g.train_epoch() + g.eval(2) for _ in range(3)]
+            g.train_epoch()
+            runs.append(dict(lines=np.array(lines, np.float32),
+                             t=[g.get_var(i) for i in (0, 2, 3, 5)] + [g.get_var(i, 1) for i in (1, 3)]))
+            g.close()
+    np.testing.assert_array_equal(runs[0]["lines"], runs[1]["lines"])
+    for x, y in zip(runs[0]["t"], runs[1]["t"]):
+        np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.parametrize("case", ["cora", "lds_dense"])
 def test_fuse_finish_matches_reduce_launch(loaded, pgcn, case):
     """fuse_finish 1: the loss kernel's last block sums the pass's (loss, wrong, W1^2) partials
     and writes the results ring slot (one launch fewer per pass) -- the same losses and
