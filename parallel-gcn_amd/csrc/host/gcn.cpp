@@ -52,6 +52,7 @@ int g_co_draw = 2;
 // "fuse_finish" (read per pass): one GPU, the loss kernel's last block sums the pass's
 // scalars and writes its results ring slot (XentFinal; one launch fewer per pass)
 int g_fuse_finish = 1;
+constexpr int kFinishMaxBlocks = 512;
 // "tn_fold" (read per epoch): one GPU, the weight gradients' last reduction pass runs inside
 // the Adam launch (GCN::backward_pass; bit-identical)
 int g_tn_fold = 1;
@@ -892,7 +893,11 @@ void GCN::set_split(int split) {
 void GCN::arm_finish(int dst_offset, bool graph) {
   ctx.fin = nullptr;
   ctx.fin_taken = false;
-  if (!g_fuse_finish || comm) return;
+  // every block adds to ONE ticket: cheap for the small graphs' 43-310 loss blocks (cora 11.1k
+  // -> 11.8k, citeseer 10.6k -> 11.5k epochs/s, same box, profiles/r06/e), but reddit's 3,641
+  // serialised device-scope adds took the loss kernels from 21 + 39 to 58 + 69 us: there the
+  // separate one-block launch stays
+  if (!g_fuse_finish || comm || ctx.xent_blocks > kFinishMaxBlocks) return;
   if (!fin_ticket) {
     fin_ticket.allocate(1);
     fin_ticket.zero();

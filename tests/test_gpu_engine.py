@@ -544,15 +544,15 @@ def test_mask_states_per_128_draws_bit_identical(loaded, pgcn, case):
         np.testing.assert_array_equal(x, y)
 
 
-@pytest.mark.parametrize("case", ["cora", "lds_dense"])
+@pytest.mark.parametrize("case", ["cora", "pubmed_like"])
 def test_fuse_finish_matches_reduce_launch(loaded, pgcn, case):
     """fuse_finish 1: the loss kernel's last block sums the pass's (loss, wrong, W1^2) partials
     and writes the results ring slot (one launch fewer per pass) -- the same losses and
     accuracies as the separate k_reduce_scalars launch up to the summation order (1e-6
     relative; the accuracies exactly), the same gradients and weights bit for bit (the scalars
     feed nothing else); eager and through the epoch hipGraph; one launch fewer per pass."""
-    if case == "lds_dense":
-        ds = pgcn.Dataset.synthetic(120000, 64, 41, 1500000, 21)
+    if case == "pubmed_like":  # 310 loss blocks: still fused (up to 512)
+        ds = pgcn.Dataset.synthetic(19717, 64, 3, 50000, 21)
     else:
         ds = loaded["cora"]
     runs = {}
