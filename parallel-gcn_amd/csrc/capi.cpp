@@ -735,6 +735,9 @@ int pgcn_debug_set(const char *key, int value) {
   } else if (!std::strcmp(key, "tn_fold")) {
     if (!in(0, 1)) return PGCN_E_INVALID;
     pgcn::g_tn_fold = value;
+  } else if (!std::strcmp(key, "ring_window")) {
+    if (value != 0 && value != 2 && value != 3) return PGCN_E_INVALID;
+    pgcn::g_ring_window = value;
   } else if (!std::strcmp(key, "ring_pair")) {
     if (!in(0, 1)) return PGCN_E_INVALID;
     pgcn::g_ring_pair = value;
@@ -792,7 +795,9 @@ long long pgcn_debug_lds_counts(int n_rows, int n_cols, const int *indptr, const
                PGCN_E_INVALID, "lds_counts args");
     std::vector<int> ip(indptr, indptr + n_rows + 1), ix(indices, indices + indptr[n_rows]);
     const std::vector<int> cut = ring_cuts(n_cols, ix, lds_blocks(n_rows, n_cols));
-    const LdsHost h = build_ring_host(n_rows, n_cols, ip, ix, cut, lds_slots(n_rows, n_cols));
+    const LdsHost h = build_ring_host(
+        n_rows, n_cols, ip, ix, cut, lds_slots(n_rows, n_cols), -1,
+        ring_window_for(n_rows, n_cols, (long long)ix.size(), (int)cut.size() - 1));
     n = (long long)h.counts.size();
     if (dst) std::copy(h.counts.begin(), h.counts.begin() + std::min(n, cap), dst);
     if (shape5) {
@@ -813,7 +818,9 @@ int pgcn_debug_lds_check(int n_rows, int n_cols, const int *indptr, const int *i
                PGCN_E_INVALID, "lds_check args");
     std::vector<int> ip(indptr, indptr + n_rows + 1), ix(indices, indices + indptr[n_rows]);
     const std::vector<int> cut = ring_cuts(n_cols, ix, lds_blocks(n_rows, n_cols));
-    const LdsHost h = build_ring_host(n_rows, n_cols, ip, ix, cut, lds_slots(n_rows, n_cols));
+    const LdsHost h = build_ring_host(
+        n_rows, n_cols, ip, ix, cut, lds_slots(n_rows, n_cols), -1,
+        ring_window_for(n_rows, n_cols, (long long)ix.size(), (int)cut.size() - 1));
     std::vector<float> in((size_t)n_cols);
     uint64_t st[2] = {12345, 67890};
     for (auto &x : in) x = (float)((double)(xs_next(st) & 0xffffff) / (double)0x1000000 - 0.5);

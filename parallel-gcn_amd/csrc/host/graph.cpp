@@ -481,8 +481,9 @@ std::vector<int> column_cuts(int n_cols, const std::vector<int> &indices, int n_
 void DevGraph::build_lds() {
   if (lds_cut_.empty()) lds_cut_ = ring_cuts(n_cols_, h_indices_, lds_blocks(n_rows_, n_cols_));
   auto L = std::make_unique<LdsSched>();
-  LdsHost h = build_ring_host(n_rows_, n_cols_, h_indptr_, h_indices_, lds_cut_,
-                              lds_slots(n_rows_, n_cols_));
+  LdsHost h = build_ring_host(
+      n_rows_, n_cols_, h_indptr_, h_indices_, lds_cut_, lds_slots(n_rows_, n_cols_), -1,
+      ring_window_for(n_rows_, n_cols_, (long long)h_indices_.size(), (int)lds_cut_.size() - 1));
   // + 2 KB slack: ring refills read whole 512-B chunks (up to 3) past a wave's last block
   L->entries.allocate(h.entries.size() / 4 + 256);
   L->entries.upload(reinterpret_cast<const uint2 *>(h.entries.data()), h.entries.size() / 4);
@@ -507,6 +508,7 @@ void DevGraph::build_lds() {
   L->s.n_blocks = h.n_blocks;
   L->s.ns = h.ns;
   L->s.pair = h.pair;
+  L->s.w = h.w;
   L->s.n_rows = n_rows_;
   L->s.n_cols = n_cols_;
   L->s.n_batches = h.n_batches;

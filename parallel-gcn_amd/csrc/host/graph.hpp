@@ -44,6 +44,7 @@ std::vector<float> degree_scales(int n, const int *indptr);
 struct LdsHost {
   int n_batches = 0, t_max = 0, n_blocks = 4, ns = LDS_SLOTS;
   bool pair = false;                    // rowsets 2p, 2p+1 in lockstep (ring_pair)
+  int w = RING_W;                       // slices a visit reads (window)
   std::vector<int> nsl;                 // slices per column block
   std::vector<int2> slices;             // [block][t_max] {first column, rows}
   std::vector<int> rows;                // [batch][LDS_CW][ns][16] row | spread
@@ -65,10 +66,14 @@ std::vector<int> ring_cuts(int n_cols, const std::vector<int> &indices, int n_bl
 // pair: rowsets 2p and 2p + 1 of a wave run the same step count per visit and their entry
 // blocks alternate in the stream (k_graphsum_ring<.., true>: both blocks' table reads in flight
 // under one wait); -1 = the "ring_pair" knob
+// window: slices a visit reads, 2 or 3 (ring_window_for)
 LdsHost build_ring_host(int n_rows, int n_cols, const std::vector<int> &indptr,
                         const std::vector<int> &indices, const std::vector<int> &bcut,
-                        int ns = LDS_SLOTS, int pair = -1);
+                        int ns = LDS_SLOTS, int pair = -1, int window = RING_W);
 extern int g_ring_pair;
+// "ring_window" (read at schedule build): 0 = by shape (ring_window_for), 2 or 3
+extern int g_ring_window;
+int ring_window_for(int n_rows, int n_cols, long long nnz, int n_blocks);
 void ring_emulate(const LdsHost &h, int n_rows, const float *in, double *out);
 
 class DevGraph {

@@ -81,11 +81,27 @@ std::vector<int> ring_cuts(int n_cols, const std::vector<int> &indices, int n_bl
 // "ring_pair" (read at schedule build): rowsets in lockstep pairs (build_ring_host)
 int g_ring_pair = 0;
 
+int g_ring_window = 0;
+
+// The window by shape: 3 (the reddit graph's), or 2 where a visit's work is too short to cover
+// the loader's one-slice-ahead LDS-DMA (~1.3 us per 32-KB slice): r06 tall edge-cut rank
+// graphs and sparse graphs, decided on the mean entry blocks a summing wave runs per visit
+// (about rows x (nnz / rows / slices + 1) / 64 per wave at 4-step blocks)
+int ring_window_for(int n_rows, int n_cols, long long nnz, int n_blocks) {
+  if (g_ring_window) return g_ring_window;
+  (void)n_rows;
+  (void)n_cols;
+  (void)nnz;
+  (void)n_blocks;
+  return RING_W;
+}
+
 LdsHost build_ring_host(int n_rows, int n_cols, const std::vector<int> &indptr,
                         const std::vector<int> &indices, const std::vector<int> &bcut, int ns,
-                        int pair_arg) {
+                        int pair_arg, int window) {
   (void)n_cols;
-  const int B = (int)bcut.size() - 1, SR = RING_SR, W = RING_W, K = RING_K;
+  PGCN_CHECK(window == 2 || window == 3, PGCN_E_INVALID, "graphsum_ring: window 2 or 3");
+  const int B = (int)bcut.size() - 1, SR = RING_SR, W = window, K = RING_K;
   const int CW = LDS_CW, NS = ns;
   const bool pair = pair_arg < 0 ? g_ring_pair != 0 : pair_arg != 0;
   PGCN_CHECK(ring_slots_ok(ns), PGCN_E_INVALID, "graphsum_ring: rowsets per wave");
@@ -394,6 +410,7 @@ LdsHost build_ring_host(int n_rows, int n_cols, const std::vector<int> &indptr,
   LdsHost h;
   h.ns = NS;
   h.pair = pair;
+  h.w = W;
   h.n_blocks = B;
   h.n_batches = nbat;
   h.t_max = t_max;
@@ -410,7 +427,7 @@ LdsHost build_ring_host(int n_rows, int n_cols, const std::vector<int> &indptr,
 // (ring buffer t % 4 holds slice t), entry blocks in wave order, zero rows; adds each row's
 // sum of in[col] into out[row].  Throws on anything the kernel would turn into a wrong sum.
 void ring_emulate(const LdsHost &h, int n_rows, const float *in, double *out) {
-  const int B = h.n_blocks, CW = LDS_CW, NS = h.ns, SR = RING_SR, K = RING_K, W = RING_W;
+  const int B = h.n_blocks, CW = LDS_CW, NS = h.ns, SR = RING_SR, K = RING_K, W = h.w;
   const long long n_wg = (long long)h.n_batches * B;
   std::vector<double> acc((size_t)NS * 16);
   for (long long wg = 0; wg < n_wg; wg++) {

@@ -31,17 +31,17 @@ constexpr int RING_TABLE_B = 4 * RING_PLANE_B;              // 131,328 B
 constexpr int RING_CNT_USED = LDS_CW * LDS_SLOTS * 2;       // <= 480 B of counts per visit
 constexpr int RING_CNT_B = 512;
 // counts buffers: visit v's counts land with slice v + W - 1, up to K - W visits ahead of the
-// slowest wave's visit
-constexpr int RING_NCB = RING_K - RING_W + 1;
+// slowest wave's visit (K - W + 1 buffers; room for the 2-slice window's 3)
+constexpr int RING_NCB_MAX = RING_K - 1;
 constexpr int RING_CNT_OFF = RING_TABLE_B;
 // loaded, done[K] in the tail of counts buffer 0 (past the largest counts block)
 constexpr int RING_FLAG_OFF = RING_CNT_OFF + RING_CNT_USED;
 constexpr int RING_NFLAGS = 1 + RING_K;
-constexpr int RING_ERING_OFF = RING_CNT_OFF + RING_NCB * RING_CNT_B;
+constexpr int RING_ERING_OFF = RING_CNT_OFF + RING_NCB_MAX * RING_CNT_B;
 constexpr int RING_CHUNK = 512;                             // 4 entry blocks of 128 B
 constexpr int RING_ESLOTS = 4;                              // chunks: 3 in flight + 1 read
 constexpr int RING_ERING_B = RING_ESLOTS * RING_CHUNK;
-constexpr int RING_TOTAL_B = RING_ERING_OFF + LDS_CW * RING_ERING_B;  // 163,072 B
+constexpr int RING_TOTAL_B = RING_ERING_OFF + LDS_CW * RING_ERING_B;  // 163,584 B
 static_assert(RING_TOTAL_B <= 160 * 1024, "LDS budget");
 static_assert(RING_FLAG_OFF + RING_NFLAGS * 4 <= RING_CNT_OFF + RING_CNT_B,
               "hand-off words fit");
@@ -244,13 +244,18 @@ __global__ __launch_bounds__(256) void k_gs_gather_finish(float4 *__restrict__ y
 // 2p + 1 run the same step count per visit and their entry blocks alternate, so a wave issues
 // both blocks' eight table reads before it waits (the adds of 2p's block wait only for its own
 // four): two blocks in flight per wave instead of one, the same adds in the same order per row
-template <int NS, bool PAIR>
+// WIN: slices a visit reads (the schedule's window, LdsSchedule::w): 3, or 2 -- the loader
+// then runs two slices ahead of the visits, for schedules whose visits are shorter than a
+// slice's LDS-DMA (tall edge-cut rank graphs, sparse graphs)
+template <int NS, bool PAIR, int WIN>
 __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
     const uint2 *__restrict__ entries, const long long *__restrict__ wave_off,
     const unsigned short *__restrict__ counts, int t_max, const int2 *__restrict__ slices,
     const int *__restrict__ n_slices, const int *__restrict__ rows, const char *__restrict__ table,
     float4 *__restrict__ partial, long long part_stride, int n_blocks) {
   static_assert(NS == 16, "rowsets per wave");
+  static_assert(WIN >= 2 && WIN <= RING_K - 1, "ring window");
+  constexpr int RING_NCB = RING_K - WIN + 1;
   constexpr int CNT_USED = LDS_CW * NS * 2;  // counts of one visit (bytes)
   __shared__ float4 lds[RING_TOTAL_B / 16];
   const int nb = n_blocks;
@@ -278,7 +283,7 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
     const int2 *sl = slices + (long long)b * t_max;
     const char *cnt_src =
         reinterpret_cast<const char *>(counts) + (long long)blockIdx.x * t_max * CNT_USED;
-    const int iters = T + RING_W - 1;
+    const int iters = T + WIN - 1;
     for (int s = 0; s < iters; s++) {
       // buffer s % K (and counts buffer (s - W + 1) & 1) free: visit s - K done everywhere
       if (s >= RING_K)
@@ -296,7 +301,7 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
             glds16(src + p * (RING_SR * 16) + q, dst + (unsigned)(p * RING_PLANE_B + q));
         }
       }
-      const int cv = s - (RING_W - 1);  // the visit whose last slice this is
+      const int cv = s - (WIN - 1);  // the visit whose last slice this is
       if (cv >= 0 && lane * 16 < CNT_USED)
         glds16(cnt_src + (long long)cv * CNT_USED + lane * 16,
                lds_base + (unsigned)(RING_CNT_OFF + (cv % RING_NCB) * RING_CNT_B));
@@ -395,7 +400,7 @@ __global__ __launch_bounds__(LDS_THREADS) void k_graphsum_ring(
     b += y3;
   };
   for (int t = 0; t < T; t++) {
-    lds_wait_ge(loaded, (unsigned)(t + RING_W));  // slices t .. t+2 and visit t's counts
+    lds_wait_ge(loaded, (unsigned)(t + WIN));  // slices t .. t+WIN-1 and visit t's counts
     // lane l reads rowset (l % 16)'s step count; two ballots give the rowsets with blocks this
     // visit and those with more than one: per rowset a scalar bit test (the sign bit of the
     // mask shifted), the count itself only for the few longer runs (r03 late: per visit 8
@@ -543,16 +548,20 @@ void launch_graphsum_ring(const LdsSchedule &s, const float *in, int ld_in, floa
                        reinterpret_cast<const float4 *>(in), ld_in / 4, s.col_scale, s.n_cols,
                        reinterpret_cast<float4 *>(scratch_in), col_map);
   const long long n_wg = (long long)s.n_batches * s.n_blocks;
-#define RING_LAUNCH(NS_, PAIR_)                                                                 \
-  PGCN_LAUNCH((k_graphsum_ring<NS_, PAIR_>), dim3((unsigned)n_wg), dim3(LDS_THREADS), 0, st, s.entries, \
+#define RING_LAUNCH(NS_, PAIR_, WIN_)                                                           \
+  PGCN_LAUNCH((k_graphsum_ring<NS_, PAIR_, WIN_>), dim3((unsigned)n_wg), dim3(LDS_THREADS), 0, st, s.entries, \
               s.wave_off, s.counts, s.t_max, s.slices, s.n_slices, s.rows,                      \
               reinterpret_cast<const char *>(scratch_in), reinterpret_cast<float4 *>(partial), \
               (long long)s.n_rows, s.n_blocks)
   PGCN_CHECK(ring_slots_ok(s.ns), PGCN_E_INVALID, "graphsum_ring: rowsets per wave");
+  PGCN_CHECK((s.w == 2 || s.w == 3) && (!s.pair || s.w == 3), PGCN_E_INVALID,
+             "graphsum_ring: window (pairs: 3 only)");
   if (s.pair)
-    RING_LAUNCH(16, true);
+    RING_LAUNCH(16, true, 3);
+  else if (s.w == 2)
+    RING_LAUNCH(16, false, 2);
   else
-    RING_LAUNCH(16, false);
+    RING_LAUNCH(16, false, 3);
 #undef RING_LAUNCH
   const GsEpilogue none{};
   const long long post = (long long)s.n_rows * 4;

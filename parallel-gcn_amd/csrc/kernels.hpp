@@ -99,6 +99,7 @@ struct LdsSchedule {
   int t_max = 0;      // max slices per column block
   int ns = LDS_SLOTS;  // rowsets per summing wave (ring_slots_ok)
   bool pair = false;   // rowsets in lockstep pairs, their blocks alternating (host/ring.cpp)
+  int w = RING_W;      // slices a visit reads (2 or 3; k_graphsum_ring's WIN)
   const uint2 *entries = nullptr;            // [kb][16 lane groups] x 4 uint16 row offsets
   const long long *wave_off = nullptr;       // [wg][LDS_CW] first kb of each wave's stream
   const unsigned short *counts = nullptr;    // [wg][t_max][LDS_CW][ns] steps

@@ -131,6 +131,19 @@ def test_graphsum_ring_pair_vs_oracle(pgcn, n, deg, dim, hubs):
         test_graphsum_vs_oracle(pgcn, n, deg, dim, hubs)
 
 
+@pytest.mark.parametrize("n,deg,dim,hubs", [
+    (120000, 40, 16, 20),    # LDS ring path
+    (150000, 60, 16, 40),    # more hubs (spread rows)
+    (120000, 40, 128, 20),   # 8 ring passes
+])
+def test_graphsum_ring_window2_vs_oracle(pgcn, n, deg, dim, hubs):
+    """ring_window 2: visits read two resident slices and the loader runs two slices ahead
+    (k_graphsum_ring<16, false, 2>): the oracle's sums within the reordering bound, reruns
+    bit-identical."""
+    with helpers.knobs(pgcn, ring_window=2):
+        test_graphsum_vs_oracle(pgcn, n, deg, dim, hubs)
+
+
 @pytest.mark.parametrize("dim", [16, 7, 41])
 def test_graphsum_split_rows_in_kernel(pgcn, dim):
     """Rows longer than one work item on the plain path (cora's hubs): gs_split 1 (default: the
