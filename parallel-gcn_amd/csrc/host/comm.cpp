@@ -446,6 +446,18 @@ void PeerComm::allreduce_sum(float *buf, size_t n, hipStream_t s) {
   launch_peer_sum(recv(), buf, n, s);
 }
 
+bool PeerComm::allreduce_grads(float *buf, size_t n, const GradRegions &r, hipStream_t s,
+                               PeerRecv *rv) {
+  if (host_order_ || world_ == 1 || n == 0) return false;
+  enter(s);
+  count(n * sizeof(float), 2.0);
+  PeerSink k = sink(1, n);
+  k.rows_per_rank = 0;  // every receiver gets the same n floats
+  launch_peer_push_grads(buf, (long long)n, r, k, s);
+  *rv = recv();
+  return true;
+}
+
 void PeerComm::reduce_scatter_sum(const float *send, float *recv_buf, size_t recvcount,
                                   hipStream_t s) {
   enter(s);

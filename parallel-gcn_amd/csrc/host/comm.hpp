@@ -183,6 +183,11 @@ class PeerComm : public Comm {
   // (peer_allreduce_block): opens the collective and fills *p, or returns false when that
   // form does not apply (in-process ranks, n above kPeerSmallAllreduce, world 1)
   bool small_allreduce(size_t n, PeerSmall *p);
+  // The weight gradients' all-reduce between processes (or solo) with the deferred last TN
+  // passes folded into its push (launch_peer_push_grads); the sum is left to the consumer:
+  // *rv names the received slots, which the Adam launch sums in rank order.  Returns false
+  // (nothing enqueued) where that form does not apply: in-process ranks, world 1.
+  bool allreduce_grads(float *buf, size_t n, const GradRegions &r, hipStream_t s, PeerRecv *rv);
   // throws PGCN_E_COMM when a wait gave up (a peer never signalled); call after a sync
   void check() const;
 

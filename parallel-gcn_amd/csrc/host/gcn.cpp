@@ -101,9 +101,9 @@ float Adam::step_size(int t) const {
          (1.0f - powf(params.beta1, (float)t));
 }
 
-void Adam::step(const Stream &s, TnDeferList *defer) {
+void Adam::step(const Stream &s, TnDeferList *defer, const PeerRecv *peer, const float *arena) {
   step_count++;
-  launch(s, step_size(step_count), nullptr, nullptr, 1, defer);
+  launch(s, step_size(step_count), nullptr, nullptr, 1, defer, peer, arena);
 }
 
 void Adam::step_each(const std::vector<hipStream_t> &streams,
@@ -122,16 +122,19 @@ void Adam::step_each(const std::vector<hipStream_t> &streams,
 }
 
 void Adam::step_graph(const Stream &s, const float *table, const int *ctr, int cap,
-                      TnDeferList *defer) const {
-  launch(s, 0.0f, table, ctr, cap, defer);
+                      TnDeferList *defer, const PeerRecv *peer, const float *arena) const {
+  launch(s, 0.0f, table, ctr, cap, defer, peer, arena);
 }
 
 // every weight in one launch when they fit one AdamBatch (the 2-layer model: W1 and W2); a
 // deferred reduction pass that writes a tensor's whole gradient runs inside it (tn_defer)
 void Adam::launch(const Stream &s, float st, const float *table, const int *ctr, int cap,
-                  TnDeferList *defer) const {
+                  TnDeferList *defer, const PeerRecv *peer, const float *arena) const {
+  PGCN_CHECK(!peer || (arena && vars.size() <= (size_t)kAdamBatch), PGCN_E_INVALID,
+             "Adam: the all-reduce's received slots need the gradient arena and one batch");
   if (vars.size() <= (size_t)kAdamBatch) {
     AdamBatch b{};
+    if (peer) b.peer = *peer;
     for (const auto &v : vars) {
       b.w[b.count] = v.w->dev_data.get();
       b.g[b.count] = v.w->dev_grad.get();
@@ -139,6 +142,7 @@ void Adam::launch(const Stream &s, float st, const float *table, const int *ctr,
       b.v[b.count] = v.v.get();
       b.n[b.count] = v.w->size;
       b.decay[b.count] = v.decay ? 1 : 0;
+      if (peer) b.arena_off[b.count] = v.w->dev_grad.get() - arena;
       for (int i = 0; defer && i < defer->n; i++) {
         TnDeferred &d = defer->d[i];
         if (d.src && d.C == v.w->dev_grad.get() && (long long)d.K * d.N == v.w->size) {
@@ -1003,7 +1007,12 @@ void GCN::join_side() {
 // tn_defer).  An edge-cut rank all-reduces finished gradients instead: no fold.
 struct GCN::FoldScope {
   explicit FoldScope(GCN &g, TnDeferList *d) {
-    if (!g_tn_fold || g.comm) return;
+    g.adam_peer = PeerRecv{};
+    // one GPU, or the peer exchange between processes (the passes then ride the gradients'
+    // all-reduce push: GCN::backward_pass); in-process ranks and RCCL all-reduce finished
+    // gradients
+    const auto *pc = dynamic_cast<const PeerComm *>(g.comm.get());
+    if (!g_tn_fold || (g.comm && !(pc && !pc->host_ordered() && g.comm->world() > 1))) return;
     // the deferred passes' inputs: 64 first-pass groups of every weight's [K][16-padded]
     // gradient (reddit: 0.8 MB)
     if (!g.tn_pool) {
@@ -1021,11 +1030,35 @@ struct GCN::FoldScope {
 
 // The backward modules in reverse order (src/gcn.cu:318-330), the side stream joined, the
 // gradients all-reduced (edge-cut)
-void GCN::backward_pass(FoldScope &fold) {
+void GCN::backward_pass(FoldScope &fold, TnDeferList *defer) {
   for (int i = (int)modules.size() - 1; i >= 0; i--) modules[(size_t)i]->backward(stream);
   fold.end();
   join_side();
-  if (comm) comm->allreduce_sum(grad_arena.get(), grad_arena.size(), stream.get());
+  if (!comm) return;
+  auto *pc = dynamic_cast<PeerComm *>(comm.get());
+  if (pc && defer->n > 0) {
+    // the deferred passes ride the all-reduce's push (their sums pushed straight from the
+    // group partials), and the Adam launch sums the received slots (adam_peer): three launches
+    // fewer than passes + push + sum
+    GradRegions r;
+    const float *arena = grad_arena.get();
+    for (int i = 0; i < defer->n; i++) {
+      TnDeferred &d = defer->d[i];
+      const long long off = d.C - arena, len = (long long)d.K * d.N;
+      if (!d.src || off < 0 || off + len > (long long)grad_arena.size() || r.n >= 4) continue;
+      r.off[r.n] = off;
+      r.d[r.n++] = d;
+      d.src = nullptr;  // taken
+    }
+    tn_defer_flush(*defer, stream.get());  // (any pass outside the arena: before the push)
+    if (pc->allreduce_grads(grad_arena.get(), grad_arena.size(), r, stream.get(), &adam_peer))
+      return;
+    // (not applicable: nothing enqueued) the passes as launches, then the plain all-reduce
+    defer->n = 0;
+    for (int i = 0; i < r.n; i++) defer->d[defer->n++] = r.d[i];
+    tn_defer_flush(*defer, stream.get());
+  }
+  comm->allreduce_sum(grad_arena.get(), grad_arena.size(), stream.get());
 }
 
 // train_epoch (src/gcn.cu:307-343) + eval(2) (src/gcn.cu:293-303), host-sync free
@@ -1037,11 +1070,13 @@ void GCN::enqueue_epoch(bool graph) {
   arm_finish(slot4, graph);
   for (const auto &m : modules) m->forward(true, stream);
   finalize(slot4, graph);
-  backward_pass(fold);
+  backward_pass(fold, &defer);
+  const PeerRecv *pr = adam_peer.world ? &adam_peer : nullptr;
   if (graph)
-    optimizer.step_graph(stream, step_table.get(), dev_ctr.get(), kStepTable, &defer);
+    optimizer.step_graph(stream, step_table.get(), dev_ctr.get(), kStepTable, &defer, pr,
+                         grad_arena.get());
   else
-    optimizer.step(stream, &defer);
+    optimizer.step(stream, &defer, pr, grad_arena.get());
   set_split(2);
   eval_forward(slot4 + 2, graph);
   if (graph) launch_counters(dev_ctr.get(), 0, 0, 0, stream.get());
@@ -1124,8 +1159,8 @@ std::pair<float, float> GCN::train_epoch() {
   arm_finish((int)(slot * 4), false);
   for (const auto &m : modules) m->forward(true, stream);
   finalize((int)(slot * 4));
-  backward_pass(fold);
-  optimizer.step(stream, &defer);
+  backward_pass(fold, &defer);
+  optimizer.step(stream, &defer, adam_peer.world ? &adam_peer : nullptr, grad_arena.get());
   ctr_valid = false;
   last_forward_training = true;
   return read_slot((int)(slot * 4));

@@ -60,7 +60,10 @@ class Adam {
        const AdamParams &p);
   // defer (one GPU): the weight gradients' deferred last reduction passes (tn_defer), run by
   // this launch for the tensors whose gradients they write, launched before it otherwise
-  void step(const Stream &s, TnDeferList *defer = nullptr);
+  // peer (edge-cut, processes): the gradients' all-reduce left its sum to this launch --
+  // tensor t's gradient is the rank-order sum of peer's slots at its offset in `arena`
+  void step(const Stream &s, TnDeferList *defer = nullptr, const PeerRecv *peer = nullptr,
+            const float *arena = nullptr);
   // the reference's per-tensor schedule (src/optim.cu:57-95): one step, tensor i on
   // streams[i], then events[i] recorded there (null: none); the same arithmetic as step()
   void step_each(const std::vector<hipStream_t> &streams, const std::vector<hipEvent_t> &events);
@@ -68,14 +71,15 @@ class Adam {
   // epoch graphs: the same launches reading the step size from table[ctr[0] % cap] on the
   // device (the host counts the step with advance() at every replay)
   void step_graph(const Stream &s, const float *table, const int *ctr, int cap,
-                  TnDeferList *defer = nullptr) const;
+                  TnDeferList *defer = nullptr, const PeerRecv *peer = nullptr,
+                  const float *arena = nullptr) const;
   void advance() { step_count++; }
   int steps() const { return step_count; }
   float step_size(int t) const;  // hpdga optim.cpp:24, step t (1-based)
 
  private:
   void launch(const Stream &s, float st, const float *table, const int *ctr, int cap,
-              TnDeferList *defer) const;
+              TnDeferList *defer, const PeerRecv *peer, const float *arena) const;
 };
 
 struct DistSpec {
@@ -133,7 +137,8 @@ class GCN {
   void check_comm() const;
   void build_eval_ax();
   struct FoldScope;
-  void backward_pass(FoldScope &fold);
+  void backward_pass(FoldScope &fold, TnDeferList *defer);
+  PeerRecv adam_peer;  // the pass's gradient all-reduce left its sum to Adam (world > 0)
   void join_side();
   int fused_tails_ = 0;  // GraphSum epilogues carrying ReLU / Dropout work (forward + backward)
   void set_split(int split);

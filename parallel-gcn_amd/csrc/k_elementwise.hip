@@ -893,35 +893,31 @@ __global__ __launch_bounds__(1024) void k_reduce_scalars(const float *__restrict
   }
 }
 
-// grad[k][j] of a deferred reduction (TnDeferred): k_gemm_tn_reduce's loads in batches of 16
-// and its ordered adds, the same bits
-__device__ __forceinline__ float tn_deferred_sum(const TnDeferred &d, long long i) {
-  const int k = (int)(i / d.N), j = (int)(i - (long long)k * d.N);
-  const long long e = (long long)k * d.ldp + j, stride = (long long)d.K * d.ldp;
-  float s = 0.0f;
-  for (int b0 = 0; b0 < d.n_groups; b0 += 16) {
-    float v[16];
-#pragma unroll
-    for (int u = 0; u < 16; u++) v[u] = b0 + u < d.n_groups ? d.src[(b0 + u) * stride + e] : 0.0f;
-#pragma unroll
-    for (int u = 0; u < 16; u++)
-      if (b0 + u < d.n_groups) s += v[u];
-  }
-  return s;
-}
-
 // Adam (hpdga optim.cpp:25-33): double temporaries where the reference has them.  red.src:
-// the gradient's last reduction pass first (stored to g, as k_gemm_tn_reduce would)
+// the gradient's last reduction pass first (stored to g, as k_gemm_tn_reduce would); peer
+// (edge-cut, the weight gradients' all-reduce between processes): the received slots summed
+// in rank order at the tensor's arena offset first (k_peer_sum's sum, stored to g)
 __device__ __forceinline__ void adam_range(float *__restrict__ w, const float *__restrict__ g,
                                            float *__restrict__ m, float *__restrict__ v,
                                            long long n, float step_size, float beta1,
                                            float beta2, float eps, float wd, int decay,
-                                           const TnDeferred &red = TnDeferred{}) {
+                                           const TnDeferred &red = TnDeferred{},
+                                           const PeerRecv *peer = nullptr, long long off = 0) {
   const double ob1 = 1.0 - (double)beta1, ob2 = 1.0 - (double)beta2;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x) {
     float grad;
-    if (red.src) {
+    if (peer) {
+      float p[kPeerMaxRanks];
+#pragma unroll
+      for (int q = 0; q < kPeerMaxRanks; q++)
+        if (q < peer->world) p[q] = peer->slot[q][off + i];
+      grad = p[0];
+#pragma unroll
+      for (int q = 1; q < kPeerMaxRanks; q++)
+        if (q < peer->world) grad += p[q];
+      const_cast<float *>(g)[i] = grad;
+    } else if (red.src) {
       grad = tn_deferred_sum(red, i);
       const_cast<float *>(g)[i] = grad;
     } else {
@@ -944,6 +940,12 @@ __global__ __launch_bounds__(256) void k_adam_multi(AdamBatch b, float step_size
                                                     const int *__restrict__ ctr, int table_cap) {
   if (step_table) step_size = step_table[ctr[0] % table_cap];
   const int t = blockIdx.y;
+  if (b.peer.world) {
+    acquire_system_workgroup();  // the peers' pushes (peer_sync.hpp)
+    adam_range(b.w[t], b.g[t], b.m[t], b.v[t], b.n[t], step_size, beta1, beta2, eps, wd,
+               b.decay[t], TnDeferred{}, &b.peer, b.arena_off[t]);
+    return;
+  }
   adam_range(b.w[t], b.g[t], b.m[t], b.v[t], b.n[t], step_size, beta1, beta2, eps, wd,
              b.decay[t], b.red[t]);
 }

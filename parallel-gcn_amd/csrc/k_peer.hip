@@ -109,6 +109,29 @@ __global__ __launch_bounds__(256) void k_peer_sum(PeerRecv r, T *__restrict__ ds
   dst[i] = a;
 }
 
+__global__ __launch_bounds__(256) void k_peer_push_grads(const float *__restrict__ arena, long long n,
+                                                          GradRegions r, PeerSink k) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    float v = arena[i];
+    for (int t = 0; t < r.n; t++) {
+      const long long rel = i - r.off[t];
+      if (rel >= 0 && rel < (long long)r.d[t].K * r.d[t].N) v = tn_deferred_sum(r.d[t], rel);
+    }
+    for (int q = 0; q < k.world; q++) peer_store4(k.dst[q], k.slot_bytes, i, v);
+  }
+  peer_arrive(k);
+}
+
+void launch_peer_push_grads(const float *arena, long long n, const GradRegions &r,
+                            const PeerSink &k, hipStream_t s) {
+  PGCN_CHECK(k.world >= 1 && k.world <= kPeerMaxRanks && r.n >= 0 && r.n <= 4 && n > 0,
+             PGCN_E_INVALID, "peer_push_grads: shape");
+  const unsigned grid = (unsigned)std::max<long long>(1, std::min<long long>(ceil_div(n, 256), 64));
+  PGCN_LAUNCH(k_peer_push_grads, dim3(grid), dim3(256), 0, s, arena, n, r, k);
+  PGCN_HIP(hipGetLastError());
+}
+
 void launch_peer_push(const float *send, size_t count, const PeerSink &k, hipStream_t s,
                       bool same_for_all) {
   PGCN_CHECK(k.world >= 1 && k.world <= kPeerMaxRanks, PGCN_E_INVALID, "peer_push: world");

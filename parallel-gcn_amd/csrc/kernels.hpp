@@ -396,7 +396,22 @@ struct AdamBatch {
   int decay[kAdamBatch];
   int count;
   TnDeferred red[kAdamBatch];  // red[t].src: tensor t's gradient reduced first (into g[t])
+  // peer.world > 0 (edge-cut, processes): tensor t's all-reduced gradient is the rank-order sum
+  // of the received slots at arena_off[t] (stored into g[t] first; k_peer_sum's sum)
+  PeerRecv peer;
+  long long arena_off[kAdamBatch];
 };
+// The weight gradients' all-reduce push between processes (PeerComm::allreduce_grads): element
+// i of the arena, or -- inside deferred region r (arena offset offs[r]) -- the deferred pass's
+// sum, stored to every receiver's slot of this rank; the push's last workgroup signals and waits
+// (peer_arrive).  k_peer_push's job with the TN reductions' last passes folded in.
+struct GradRegions {
+  int n = 0;
+  long long off[4];
+  TnDeferred d[4];
+};
+void launch_peer_push_grads(const float *arena, long long n, const GradRegions &r,
+                            const PeerSink &k, hipStream_t s);
 void launch_adam_multi(const AdamBatch &b, float step_size, float beta1, float beta2, float eps,
                        float wd, hipStream_t s, const float *step_table = nullptr,
                        const int *ctr = nullptr, int table_cap = 1);

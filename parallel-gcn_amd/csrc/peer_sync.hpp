@@ -62,6 +62,24 @@ __device__ __forceinline__ void acquire_system_workgroup() {
   __syncthreads();
 }
 
+// grad[k][j] of a deferred reduction (TnDeferred, kernels.hpp): k_gemm_tn_reduce's loads in
+// batches of 16 and its ordered adds, the same bits (the Adam launch and the weight
+// gradients' peer push run it)
+__device__ __forceinline__ float tn_deferred_sum(const TnDeferred &d, long long i) {
+  const int k = (int)(i / d.N), j = (int)(i - (long long)k * d.N);
+  const long long e = (long long)k * d.ldp + j, stride = (long long)d.K * d.ldp;
+  float s = 0.0f;
+  for (int b0 = 0; b0 < d.n_groups; b0 += 16) {
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 16; u++) v[u] = b0 + u < d.n_groups ? d.src[(b0 + u) * stride + e] : 0.0f;
+#pragma unroll
+    for (int u = 0; u < 16; u++)
+      if (b0 + u < d.n_groups) s += v[u];
+  }
+  return s;
+}
+
 // v -> float4 element i of the slot at `base` (bytes: the slot's size from base on: a store
 // past it is dropped by the buffer resource's range check); `base` wave-uniform
 __device__ __forceinline__ void peer_store16(float *base, long long bytes, long long i, float4 v) {
