@@ -514,13 +514,15 @@ def main():
     achieved = bytes_per_call / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     traffic = None
     tpath = os.path.join(REPO, "profiles", "traffic_graphsum.json")
-    if os.path.exists(tpath) and hidden == (16,) and world == 1:
+    if os.path.exists(tpath) and world == 1:
         try:
             t = json.load(open(tpath))
-            # only PMC passes of the kernel sources this bench runs count
+            # only PMC passes of the kernel sources this bench runs count; per workload and
+            # model (the 4-layer line: "reddit-114M hidden=128,128,128")
             from stamp import graphsum_stamp
+            key = args.workload if hidden == (16,) else f"{args.workload} hidden={args.hidden}"
             if not head_knobs and t.get("source_stamp") == graphsum_stamp():
-                traffic = t.get(args.workload)
+                traffic = t.get(key)
         except (OSError, ValueError):
             traffic = None
 

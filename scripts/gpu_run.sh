@@ -15,8 +15,9 @@
 #   datasets                   tools/datasets_bench.py (cora, citeseer, pubmed_synth)
 #   trace:<tag>[:<args>]       rocprofv3 --kernel-trace --stats of bench.py --profile-only <args>,
 #                              then tools/epoch_breakdown.py
-#   traffic:<tag>[:<args>]     FETCH_SIZE / WRITE_SIZE passes (one counter group each) of the same,
-#                              then tools/traffic.py
+#   traffic:<tag>[:<args>[:<traffic.py args>]]  FETCH_SIZE / WRITE_SIZE passes (one counter
+#                              group each) of the same, then tools/traffic.py (e.g.
+#                              --epoch,11,--hidden,128+128+128,--write,r06)
 #   tool:<tag>:<script>[:<args>] python3 tools/<script> <args> -> <tag>.log
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -100,7 +101,7 @@ for step in "$@"; do
         echo "[traffic $a $ctr] rc=$rc"
         [ $rc -eq 0 ] || { tail -20 "$O/$a.$ctr.log"; exit $rc; }
       done
-      python3 tools/traffic.py "$O/$a" > "$O/$a.traffic.json" 2>&1
+      python3 tools/traffic.py "$O/$a" $(args_of "${c:-}") > "$O/$a.traffic.json" 2>&1
       cut -c1-600 "$O/$a.traffic.json" ;;
     tool)
       run "$a" 900 python3 "tools/$b" $(args_of "${c:-}") || exit $? ;;
