@@ -726,6 +726,9 @@ int pgcn_debug_set(const char *key, int value) {
   } else if (!std::strcmp(key, "eval_tail")) {
     if (!in(0, 1)) return PGCN_E_INVALID;
     pgcn::g_eval_tail = value;
+  } else if (!std::strcmp(key, "csc_tree")) {
+    if (!in(0, 1)) return PGCN_E_INVALID;
+    pgcn::g_csc_tree = value;
   } else if (!std::strcmp(key, "mask_per")) {
     if (!in(1, 2)) return PGCN_E_INVALID;
     pgcn::g_mask_per = value;

@@ -54,6 +54,11 @@ std::vector<float> Variable::to_host(int which) const {
   return out;
 }
 
+// "csc_tree" (read per launch): sparse X's W1.grad summed as a fixed tree over each feature's
+// entries (k_spmm_csc_tree) instead of hpdga's sequential scatter order (k_spmm_csc_bwd,
+// bit-exact); deterministic, within the reordering bound
+int g_csc_tree = 1;
+
 // ------------------------------------------------------------------------------------------
 // Dropout (src/module.cu:6-99; hpdga module.cpp:196-228)
 // ------------------------------------------------------------------------------------------
@@ -278,7 +283,7 @@ void SparseMatmul::backward(const Stream &s) const {
   } else {
     launch_spmm_csc_bwd(x->cols, b->cols, c->ld, x->csc_ptr.get(), x->csc_row.get(),
                         x->csc_pos.get(), x->values.get(), mask, base, scale, c->dev_grad.get(),
-                        b->dev_grad.get(), s.get(), x->nnz, x->csc_order.get());
+                        b->dev_grad.get(), s.get(), x->nnz, x->csc_order.get(), g_csc_tree != 0);
   }
 }
 

@@ -99,6 +99,8 @@ extern int g_fuse_output;
 extern int g_sparse_dual;
 
 // Shared per-GCN state the modules read (current split, comm, profiling, RNG table).
+extern int g_csc_tree;  // "csc_tree" (module.cpp)
+
 struct ModuleContext {
   bool train_ahead = true;     // eval computes the next training forward's first product too
   // (measured and removed, r01/r02: drawing the next input mask on a side stream beside the

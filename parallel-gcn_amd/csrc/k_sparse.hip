@@ -240,6 +240,65 @@ __global__ __launch_bounds__(CH) void k_spmm_csc_bwd(int nf, int p, int ldg,
   if (tid < 16 && k0 + tid < p) bgrad[(long long)f * p + k0 + tid] = sum;
 }
 
+// W1.grad over sparse X as a fixed tree (knob "csc_tree", r06): thread t of the feature's
+// workgroup sums the products of entries t, t + CH, ... in entry order (4 entries' index,
+// value, mask and grad-row loads in flight together), then the CH partial rows are added in
+// a fixed binary tree through LDS -- deterministic, within the reordering bound of the
+// sequential chain k_spmm_csc_bwd keeps (hpdga's scatter order, bit-exact), whose longest
+// column (cora: 1,083 entries) made that kernel the epoch's longest (14.8 us)
+template <int CH>
+__global__ __launch_bounds__(CH) void k_spmm_csc_tree(int nf, int p, int ldg,
+                                                      const int *__restrict__ csc_ptr,
+                                                      const int *__restrict__ csc_row,
+                                                      const int *__restrict__ csc_pos,
+                                                      const float *__restrict__ a,
+                                                      const uint64_t *__restrict__ mask,
+                                                      long long mask_base, float scale,
+                                                      const float *__restrict__ cgrad,
+                                                      float *__restrict__ bgrad,
+                                                      const int *__restrict__ order) {
+  __shared__ float red[CH / 2][17];  // [pair][column]: 17 keeps the rows' banks apart
+  const int f = order ? order[blockIdx.x] : (int)blockIdx.x, k0 = blockIdx.y * 16,
+            tid = threadIdx.x;
+  const int e0 = csc_ptr[f], e1 = csc_ptr[f + 1];
+  float acc[16];
+#pragma unroll
+  for (int c = 0; c < 16; c++) acc[c] = 0.0f;
+  constexpr int U = 4;
+  for (int b = e0 + tid; b < e1; b += U * CH) {
+    int ps[U], rw[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int e = min(b + u * CH, e1 - 1);
+      ps[u] = csc_pos[e];
+      rw[u] = csc_row[e];
+    }
+    float av[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) av[u] = drop_val(a[ps[u]], mask, mask_base + ps[u], scale);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      if (b + u * CH >= e1) break;
+      const float *g = cgrad + (long long)rw[u] * ldg + k0;
+#pragma unroll
+      for (int c = 0; c < 16; c++) acc[c] += (k0 + c < p ? g[c] : 0.0f) * av[u];
+    }
+  }
+  // the tree: at each level the upper half's rows are added into the lower half's
+  for (int h = CH / 2; h >= 1; h >>= 1) {
+    if (tid >= h && tid < 2 * h)
+#pragma unroll
+      for (int c = 0; c < 16; c++) red[tid - h][c] = acc[c];
+    __syncthreads();
+    if (tid < h)
+#pragma unroll
+      for (int c = 0; c < 16; c++) acc[c] += red[tid][c];
+    __syncthreads();
+  }
+  if (tid == 0)
+    for (int c = 0; c < 16 && k0 + c < p; c++) bgrad[(long long)f * p + k0 + c] = acc[c];
+}
+
 void launch_spmm_csr(int m, int p, int ldc, const int *indptr, const int *indices,
                      const float *a, const uint64_t *mask, long long mask_base, float scale,
                      const float *b, float *c, hipStream_t s) {
@@ -262,9 +321,14 @@ void launch_spmm_csr_dual(int m, int p, int ldc, const int *indptr, const int *i
 void launch_spmm_csc_bwd(int nf, int p, int ldg, const int *csc_ptr, const int *csc_row,
                          const int *csc_pos, const float *a, const uint64_t *mask,
                          long long mask_base, float scale, const float *cgrad, float *bgrad,
-                         hipStream_t s, long long nnz, const int *order) {
+                         hipStream_t s, long long nnz, const int *order, bool tree) {
   if (nf <= 0 || p <= 0) return;
   const dim3 grid((unsigned)nf, (unsigned)ceil_div(p, 16));
+  if (tree) {
+    PGCN_LAUNCH(k_spmm_csc_tree<256>, grid, dim3(256), 0, s, nf, p, ldg, csc_ptr, csc_row,
+                csc_pos, a, mask, mask_base, scale, cgrad, bgrad, order);
+    return;
+  }
   if (nnz > 512LL * nf)
     PGCN_LAUNCH(k_spmm_csc_bwd<1024>, grid, dim3(1024), 0, s, nf, p, ldg, csc_ptr, csc_row,
                 csc_pos, a, mask, mask_base, scale, cgrad, bgrad, order);

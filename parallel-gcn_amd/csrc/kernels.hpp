@@ -284,7 +284,8 @@ void launch_spmm_csr_dual(int m, int p, int ldc, const int *indptr, const int *i
 void launch_spmm_csc_bwd(int nf, int p, int ldg, const int *csc_ptr, const int *csc_row,
                          const int *csc_pos, const float *a, const uint64_t *mask,
                          long long mask_base, float scale, const float *cgrad, float *bgrad,
-                         hipStream_t s, long long nnz = 0, const int *order = nullptr);
+                         hipStream_t s, long long nnz = 0, const int *order = nullptr,
+                         bool tree = false);  // tree: k_spmm_csc_tree (not the chain's bits)
 
 void launch_dropout_mask(uint64_t *states, long long n_chunks, long long elem0,
                          long long elem_end, float p, uint64_t *mask, const void *table,

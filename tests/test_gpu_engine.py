@@ -544,6 +544,30 @@ def test_mask_states_per_128_draws_bit_identical(loaded, pgcn, case):
         np.testing.assert_array_equal(x, y)
 
 
+@pytest.mark.parametrize("name", ["cora", "citeseer"])
+def test_csc_tree_matches_sequential_chain(loaded, pgcn, name):
+    """csc_tree 1 (default): sparse X's W1.grad as a fixed tree over each feature's entries
+    (k_spmm_csc_tree) against hpdga's sequential scatter order (csc_tree 0, k_spmm_csc_bwd,
+    bit-exact with the reference): W1.grad within the reordering bound after an epoch, the
+    epoch lines within 1e-5 over 5 epochs, and the tree repeats its own bits."""
+    ds = loaded[name]
+    runs = []
+    for tree in (0, 1, 1):
+        with helpers.knobs(pgcn, csc_tree=tree):
+            g = pgcn.GCN(pgcn.make_params(ds), ds)
+            g.train_epoch()
+            gw1 = g.get_var(2, 1)
+            lines = [g.train_epoch() + g.eval(2) for _ in range(5)]
+            runs.append(dict(g=gw1, lines=np.array(lines, np.float64), w1=g.get_var(2)))
+            g.close()
+    seq, tree, again = runs
+    scale = np.abs(seq["g"]).max()
+    assert np.abs(tree["g"] - seq["g"]).max() <= 1e-5 * scale, np.abs(tree["g"] - seq["g"]).max()
+    np.testing.assert_allclose(tree["lines"][:, [0, 2]], seq["lines"][:, [0, 2]], rtol=1e-5)
+    np.testing.assert_array_equal(tree["g"], again["g"])
+    np.testing.assert_array_equal(tree["w1"], again["w1"])
+
+
 @pytest.mark.parametrize("case", ["cora", "pubmed_like"])
 def test_fuse_finish_matches_reduce_launch(loaded, pgcn, case):
     """fuse_finish 1: the loss kernel's last block sums the pass's (loss, wrong, W1^2) partials
