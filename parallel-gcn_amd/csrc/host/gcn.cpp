@@ -52,6 +52,8 @@ int g_co_draw = 2;
 // "fuse_finish" (read per pass): one GPU, the loss kernel's last block sums the pass's
 // scalars and writes its results ring slot (XentFinal; one launch fewer per pass)
 int g_fuse_finish = 1;
+// "mask_adam" (read per epoch): one GPU, the next input mask drawn by the Adam launch
+int g_mask_adam = 1;
 constexpr int kFinishMaxBlocks = 512;
 // "tn_fold" (read per epoch): one GPU, the weight gradients' last reduction pass runs inside
 // the Adam launch (GCN::backward_pass; bit-identical)
@@ -101,9 +103,10 @@ float Adam::step_size(int t) const {
          (1.0f - powf(params.beta1, (float)t));
 }
 
-void Adam::step(const Stream &s, TnDeferList *defer, const PeerRecv *peer, const float *arena) {
+void Adam::step(const Stream &s, TnDeferList *defer, const PeerRecv *peer, const float *arena,
+                const MaskDraw *draws, int n_draws, const void *table) {
   step_count++;
-  launch(s, step_size(step_count), nullptr, nullptr, 1, defer, peer, arena);
+  launch(s, step_size(step_count), nullptr, nullptr, 1, defer, peer, arena, draws, n_draws, table);
 }
 
 void Adam::step_each(const std::vector<hipStream_t> &streams,
@@ -129,9 +132,12 @@ void Adam::step_graph(const Stream &s, const float *table, const int *ctr, int c
 // every weight in one launch when they fit one AdamBatch (the 2-layer model: W1 and W2); a
 // deferred reduction pass that writes a tensor's whole gradient runs inside it (tn_defer)
 void Adam::launch(const Stream &s, float st, const float *table, const int *ctr, int cap,
-                  TnDeferList *defer, const PeerRecv *peer, const float *arena) const {
+                  TnDeferList *defer, const PeerRecv *peer, const float *arena,
+                  const MaskDraw *draws, int n_draws, const void *jump_table) const {
   PGCN_CHECK(!peer || (arena && vars.size() <= (size_t)kAdamBatch), PGCN_E_INVALID,
              "Adam: the all-reduce's received slots need the gradient arena and one batch");
+  PGCN_CHECK(n_draws == 0 || (vars.size() <= (size_t)kAdamBatch && !peer && !table),
+             PGCN_E_INVALID, "Adam: masks only in an eager one-batch step");
   if (vars.size() <= (size_t)kAdamBatch) {
     AdamBatch b{};
     if (peer) b.peer = *peer;
@@ -154,7 +160,7 @@ void Adam::launch(const Stream &s, float st, const float *table, const int *ctr,
     }
     if (defer) tn_defer_flush(*defer, s.get());  // passes no tensor took: before the update
     launch_adam_multi(b, st, params.beta1, params.beta2, params.eps, params.weight_decay, s.get(),
-                      table, ctr, cap);
+                      table, ctr, cap, draws, n_draws, jump_table);
     return;
   }
   if (defer) tn_defer_flush(*defer, s.get());
@@ -892,6 +898,19 @@ void GCN::set_split(int split) {
   }
 }
 
+// One GPU ("mask_adam", default on): the next training forward's input mask (and the hidden mask
+// co-drawn with it) drawn by the optimizer's launch -- the two are independent, and the masks
+// come from the same stream positions whenever they are drawn; the next forward then finds
+// them drawn ahead (Dropout::ahead_descs).  One launch fewer per epoch.
+int GCN::mask_with_adam(MaskDraw out[2]) {
+  // (not with epoch graphs: a capture after an eager epoch would find the mask drawn ahead and
+  // record a forward without its draw)
+  if (!g_mask_adam || g_epoch_graph || comm || dropouts_.empty() || !dropouts_[0] ||
+      dropouts_[0]->variable() || optimizer.size() > (size_t)kAdamBatch)
+    return 0;
+  return dropouts_[0]->ahead_descs(out);
+}
+
 // One GPU ("fuse_finish", default on): the next pass's loss kernel finishes its scalars itself
 // into results_ring slot dst_offset (XentFinal), so finalize() launches nothing
 void GCN::arm_finish(int dst_offset, bool graph) {
@@ -1072,11 +1091,14 @@ void GCN::enqueue_epoch(bool graph) {
   finalize(slot4, graph);
   backward_pass(fold, &defer);
   const PeerRecv *pr = adam_peer.world ? &adam_peer : nullptr;
-  if (graph)
+  if (graph) {
     optimizer.step_graph(stream, step_table.get(), dev_ctr.get(), kStepTable, &defer, pr,
                          grad_arena.get());
-  else
-    optimizer.step(stream, &defer, pr, grad_arena.get());
+  } else {
+    MaskDraw md[2];
+    const int nd = mask_with_adam(md);
+    optimizer.step(stream, &defer, pr, grad_arena.get(), md, nd, ctx.jump_table);
+  }
   set_split(2);
   eval_forward(slot4 + 2, graph);
   if (graph) launch_counters(dev_ctr.get(), 0, 0, 0, stream.get());
@@ -1160,7 +1182,10 @@ std::pair<float, float> GCN::train_epoch() {
   for (const auto &m : modules) m->forward(true, stream);
   finalize((int)(slot * 4));
   backward_pass(fold, &defer);
-  optimizer.step(stream, &defer, adam_peer.world ? &adam_peer : nullptr, grad_arena.get());
+  MaskDraw md[2];
+  const int nd = mask_with_adam(md);
+  optimizer.step(stream, &defer, adam_peer.world ? &adam_peer : nullptr, grad_arena.get(), md, nd,
+                 ctx.jump_table);
   ctr_valid = false;
   last_forward_training = true;
   return read_slot((int)(slot * 4));

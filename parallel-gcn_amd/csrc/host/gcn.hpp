@@ -62,8 +62,10 @@ class Adam {
   // this launch for the tensors whose gradients they write, launched before it otherwise
   // peer (edge-cut, processes): the gradients' all-reduce left its sum to this launch --
   // tensor t's gradient is the rank-order sum of peer's slots at its offset in `arena`
+  // draws (mask_adam, one GPU): the next training forward's masks drawn by the same launch
   void step(const Stream &s, TnDeferList *defer = nullptr, const PeerRecv *peer = nullptr,
-            const float *arena = nullptr);
+            const float *arena = nullptr, const MaskDraw *draws = nullptr, int n_draws = 0,
+            const void *table = nullptr);
   // the reference's per-tensor schedule (src/optim.cu:57-95): one step, tensor i on
   // streams[i], then events[i] recorded there (null: none); the same arithmetic as step()
   void step_each(const std::vector<hipStream_t> &streams, const std::vector<hipEvent_t> &events);
@@ -79,7 +81,9 @@ class Adam {
 
  private:
   void launch(const Stream &s, float st, const float *table, const int *ctr, int cap,
-              TnDeferList *defer, const PeerRecv *peer, const float *arena) const;
+              TnDeferList *defer, const PeerRecv *peer, const float *arena,
+              const MaskDraw *draws = nullptr, int n_draws = 0,
+              const void *jump_table = nullptr) const;
 };
 
 struct DistSpec {
@@ -139,6 +143,9 @@ class GCN {
   struct FoldScope;
   void backward_pass(FoldScope &fold, TnDeferList *defer);
   PeerRecv adam_peer;  // the pass's gradient all-reduce left its sum to Adam (world > 0)
+  // mask_adam: the next training forward's input (and co-drawn hidden) masks for the Adam
+  // launch; returns how many (0: not applicable, or drawn already)
+  int mask_with_adam(MaskDraw out[2]);
   void join_side();
   int fused_tails_ = 0;  // GraphSum epilogues carrying ReLU / Dropout work (forward + backward)
   void set_split(int split);

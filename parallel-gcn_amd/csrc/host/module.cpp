@@ -97,6 +97,29 @@ void Dropout::draw_ahead(hipStream_t s, const Event *ready) const {
   ahead = true;
 }
 
+int Dropout::ahead_descs(MaskDraw out[2]) const {
+  PGCN_CHECK(!in, PGCN_E_INVALID, "dropout: one mask ahead, input dropout only");
+  if (ahead) return 0;
+  if (!rng->mask_ahead) {
+    rng->mask_ahead.allocate(rng->mask.size());
+    rng->mask_ahead.zero();
+  }
+  const DropoutRng &r = *rng;
+  out[0] = MaskDraw{r.states.get(), r.n_chunks, 64 * r.chunk_lo, r.elem_end, p,
+                    rng->mask_ahead.get(), r.per};
+  int n = 1;
+  if (co_draw && !co_draw->pre_drawn && !co_draw->ahead) {
+    const DropoutRng &q = co_draw->state();
+    out[1] = MaskDraw{q.states.get(), q.n_chunks, 64 * q.chunk_lo, q.elem_end, co_draw->p,
+                      q.mask.get(), q.per};
+    co_draw->pre_drawn = true;
+    n = 2;
+  }
+  ahead_ready = nullptr;
+  ahead = true;
+  return n;
+}
+
 void Dropout::wait_ahead(hipStream_t s) const {
   if (ahead && ahead_ready) {
     ahead_ready->wait_on(s);

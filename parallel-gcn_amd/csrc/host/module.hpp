@@ -197,6 +197,9 @@ class Dropout : public Module {
   // the draw runs on stream s and `ready` is recorded after it: users of the mask on another
   // stream wait for it (wait_ahead).
   void draw_ahead(hipStream_t s, const Event *ready = nullptr) const;
+  // The same draw handed to another launch (the optimizer's, mask_adam): fills out[0] (and
+  // out[1]: co_draw's next mask) and marks both drawn; returns how many (0: already drawn)
+  int ahead_descs(MaskDraw out[2]) const;
   bool drawn_ahead() const { return ahead; }
   void wait_ahead(hipStream_t s) const;
   const uint64_t *mask_ahead() const { return rng->mask_ahead.get(); }

@@ -902,10 +902,14 @@ __device__ __forceinline__ void adam_range(float *__restrict__ w, const float *_
                                            long long n, float step_size, float beta1,
                                            float beta2, float eps, float wd, int decay,
                                            const TnDeferred &red = TnDeferred{},
-                                           const PeerRecv *peer = nullptr, long long off = 0) {
+                                           const PeerRecv *peer = nullptr, long long off = 0,
+                                           long long bid = -1, long long nblk = 0) {
   const double ob1 = 1.0 - (double)beta1, ob2 = 1.0 - (double)beta2;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (long long)gridDim.x * blockDim.x) {
+  if (bid < 0) {
+    bid = blockIdx.x;
+    nblk = gridDim.x;
+  }
+  for (long long i = bid * blockDim.x + threadIdx.x; i < n; i += nblk * blockDim.x) {
     float grad;
     if (peer) {
       float p[kPeerMaxRanks];
@@ -948,6 +952,37 @@ __global__ __launch_bounds__(256) void k_adam_multi(AdamBatch b, float step_size
   }
   adam_range(b.w[t], b.g[t], b.m[t], b.v[t], b.n[t], step_size, beta1, beta2, eps, wd,
              b.decay[t], b.red[t]);
+}
+
+// One launch for the optimizer step and the next training forward's masks (mask_adam, r06; one
+// GPU): workgroups [0, ga + gb) draw the masks as k_dropout_mask does (segment a, then b), the
+// rest are k_adam_multi's (tensor t = (block - ga - gb) / adam_blocks).  The two are
+// independent: the masks are the next epoch's, drawn from the same stream positions whenever
+// they are drawn (Dropout::ahead_descs).
+__global__ __launch_bounds__(256) void k_adam_mask(AdamBatch b, float step_size, float beta1,
+                                                   float beta2, float eps, float wd, MaskSeg ma,
+                                                   MaskSeg mb, int ga, int gb, int adam_blocks,
+                                                   const uint4 *__restrict__ table) {
+  __shared__ uint4 lut[32 * 16];
+  if ((int)blockIdx.x < ga + gb) {
+    for (int i = threadIdx.x; i < 32 * 16; i += blockDim.x) {
+      const int p = i >> 4, v = i & 15;
+      lut[i] = table[(p >> 1) * 256 + (v << (4 * (p & 1)))];
+    }
+    __syncthreads();
+    const bool in_a = (int)blockIdx.x < ga;
+    const MaskSeg &sg = in_a ? ma : mb;
+    const long long bid = in_a ? blockIdx.x : blockIdx.x - ga;
+    const long long nblk = in_a ? ga : gb;
+    if (sg.per == 2)
+      dropout_mask_seg<2>(sg, lut, bid, nblk);
+    else
+      dropout_mask_seg<1>(sg, lut, bid, nblk);
+    return;
+  }
+  const int k = (int)blockIdx.x - ga - gb, t = k / adam_blocks;
+  adam_range(b.w[t], b.g[t], b.m[t], b.v[t], b.n[t], step_size, beta1, beta2, eps, wd,
+             b.decay[t], b.red[t], nullptr, 0, k % adam_blocks, adam_blocks);
 }
 
 __global__ __launch_bounds__(256) void k_adam(float *__restrict__ w, const float *__restrict__ g,
@@ -1111,10 +1146,33 @@ void launch_counters(int *ctr, int set, int step, int epoch, hipStream_t s) {
 
 void launch_adam_multi(const AdamBatch &b, float step_size, float beta1, float beta2, float eps,
                        float wd, hipStream_t s, const float *step_table, const int *ctr,
-                       int table_cap) {
+                       int table_cap, const MaskDraw *draws, int n_draws, const void *table) {
   if (b.count <= 0) return;
   long long nmax = 0;
   for (int t = 0; t < b.count; t++) nmax = std::max(nmax, b.n[t]);
+  if (n_draws > 0) {
+    PGCN_CHECK(!step_table && !b.peer.world && n_draws <= 2 && table, PGCN_E_INVALID,
+               "adam_mask: eager one-GPU steps, at most two masks, the jump table");
+    MaskSeg sg[2];
+    int g[2] = {0, 0};
+    for (int i = 0; i < n_draws; i++) {
+      const MaskDraw &d = draws[i];
+      PGCN_CHECK(d.per == 1 || d.per == 2, PGCN_E_INVALID, "adam_mask: words per state");
+      sg[i].states = d.states;
+      sg[i].n_chunks = d.n_chunks;
+      sg[i].elem0 = d.elem0;
+      sg[i].elem_end = d.elem_end;
+      sg[i].threshold = (int)(d.p * (float)0x7fffffff);  // as launch_dropout_mask
+      sg[i].mask = d.mask;
+      sg[i].per = d.per;
+      g[i] = d.n_chunks > 0 ? grid_for(ceil_div(ceil_div(d.n_chunks, d.per), 2), 256, 8 * kCUs) : 0;
+    }
+    const int ga = grid_for(nmax);
+    PGCN_LAUNCH(k_adam_mask, dim3((unsigned)(g[0] + g[1] + ga * b.count)), dim3(256), 0, s, b,
+                step_size, beta1, beta2, eps, wd, sg[0], sg[1], g[0], g[1], ga,
+                static_cast<const uint4 *>(table));
+    return;
+  }
   PGCN_LAUNCH(k_adam_multi, dim3(grid_for(nmax), b.count), dim3(256), 0, s, b, step_size,
                      beta1, beta2, eps, wd, step_table, ctr, table_cap);
 }

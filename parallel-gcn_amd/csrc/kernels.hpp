@@ -413,9 +413,13 @@ struct GradRegions {
 };
 void launch_peer_push_grads(const float *arena, long long n, const GradRegions &r,
                             const PeerSink &k, hipStream_t s);
+// draws (optional, eager one-GPU steps): up to two masks drawn by the same launch (k_adam_mask;
+// MaskDraw and `table` as launch_dropout_mask2)
 void launch_adam_multi(const AdamBatch &b, float step_size, float beta1, float beta2, float eps,
                        float wd, hipStream_t s, const float *step_table = nullptr,
-                       const int *ctr = nullptr, int table_cap = 1);
+                       const int *ctr = nullptr, int table_cap = 1,
+                       const MaskDraw *draws = nullptr, int n_draws = 0,
+                       const void *table = nullptr);
 // set: ctr = {step, epoch}; else both += 1 (the end of a graph-replayed epoch)
 void launch_counters(int *ctr, int set, int step, int epoch, hipStream_t s);
 

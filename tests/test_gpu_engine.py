@@ -486,8 +486,9 @@ def test_fused_epilogue_bit_identical(loaded, pgcn, case):
 def test_fold_and_dense_co_draw_bit_identical(loaded, pgcn, case):
     """r06 launch cuts give the bits of the launches they replace: the weight gradients' last
     ordered reduction pass inside the Adam launch (tn_fold 1 vs 0: the X-stream TN's and the
-    fused loss kernel's W.grad partials; eager and through the epoch hipGraph) and, on dense X,
-    the hidden dropout's mask drawn in the input dropout's launch (co_draw 2 vs 1): epoch lines,
+    fused loss kernel's W.grad partials; eager and through the epoch hipGraph), on dense X the
+    hidden dropout's mask drawn in the input dropout's launch (co_draw 2 vs 1), and the next
+    epoch's masks drawn by the Adam launch (mask_adam 1 vs 0): epoch lines, the dropped input,
     weights, activations and gradients; the launch counter shows the cuts."""
     if case == "lds_dense":
         ds, make = pgcn.Dataset.synthetic(120000, 64, 41, 1500000, 21), {}
@@ -497,7 +498,8 @@ def test_fold_and_dense_co_draw_bit_identical(loaded, pgcn, case):
     else:
         ds, make = loaded["cora"], {}
     runs = {}
-    for name, kn in (("base", dict(tn_fold=0, co_draw=1)), ("cut", dict(tn_fold=1, co_draw=2)),
+    for name, kn in (("base", dict(tn_fold=0, co_draw=1, mask_adam=0)),
+                     ("cut", dict(tn_fold=1, co_draw=2, mask_adam=1)),
                      ("graph", dict(tn_fold=1, co_draw=2, epoch_graph=1))):
         with helpers.knobs(pgcn, **kn):
             g = pgcn.GCN(pgcn.make_params(ds, **make), ds)
@@ -510,7 +512,7 @@ def test_fold_and_dense_co_draw_bit_identical(loaded, pgcn, case):
             n = pgcn.path_counts()["launches"]
             g.train_epoch()
             runs[name] = dict(lines=np.array(lines, np.float32), launches=n,
-                              vars=[g.get_var(i) for i in (2, 3, 5)],
+                              vars=[g.get_var(i) for i in (0, 2, 3, 5)],
                               grads=[g.get_var(i, 1) for i in (1, 3)] + [g.get_var(2, 1)])
             g.close()
     a = runs["base"]
