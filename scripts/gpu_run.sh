@@ -15,6 +15,8 @@
 #   datasets                   tools/datasets_bench.py (cora, citeseer, pubmed_synth)
 #   trace:<tag>[:<args>]       rocprofv3 --kernel-trace --stats of bench.py --profile-only <args>,
 #                              then tools/epoch_breakdown.py
+#   dtrace:<tag>:<dataset>     rocprofv3 kernel trace of tools/datasets_bench.py on one dataset,
+#                              then tools/epoch_breakdown.py (epochs between Adam launches)
 #   traffic:<tag>[:<args>[:<traffic.py args>]]  FETCH_SIZE / WRITE_SIZE passes (one counter
 #                              group each) of the same, then tools/traffic.py (e.g.
 #                              --epoch,11,--hidden,128+128+128,--write,r06)
@@ -91,6 +93,15 @@ for step in "$@"; do
       echo "[trace $a] rc=$rc"
       [ $rc -eq 0 ] || { tail -20 "$O/$a.log"; exit $rc; }
       python3 tools/epoch_breakdown.py "$O/$a" > "$O/$a.breakdown.txt" 2>&1
+      head -30 "$O/$a.breakdown.txt" ;;
+    dtrace)  # dtrace:<tag>:<dataset>: kernel trace of tools/datasets_bench.py on one dataset
+      ( cd /tmp && cd "$ROOT" && timeout -k 10 600 rocprofv3 --kernel-trace --stats \
+          -d "$O/$a" -o run -f csv -- python3 tools/datasets_bench.py --only "${b:-cora}" --graph 0 \
+          --no-cpu --epochs 200 > "$O/$a.log" 2>&1 )
+      rc=$?
+      echo "[dtrace $a] rc=$rc"
+      [ $rc -eq 0 ] || { tail -20 "$O/$a.log"; exit $rc; }
+      python3 tools/epoch_breakdown.py "$O/$a" k_adam > "$O/$a.breakdown.txt" 2>&1
       head -30 "$O/$a.breakdown.txt" ;;
     traffic)
       for ctr in FETCH_SIZE WRITE_SIZE; do
