@@ -208,7 +208,7 @@ def main():
     ap.add_argument("--profile-only", action="store_true",
                     help="only run warmup+steps (for rocprofv3), no JSON extras")
     ap.add_argument("--hidden", default="16",
-                    help="hidden dims, comma-separated (BASELINE configs[4]: 128,128,128)")
+                    help="hidden dims, comma- (or '+'-) separated (BASELINE configs[4]: 128,128,128)")
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the secondary measurements (restricted / reference order)")
     ap.add_argument("--knob", action="append", default=[],
@@ -219,6 +219,7 @@ def main():
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: print the --gpus N partition (per-rank nnz, exchange bytes)")
     args = ap.parse_args()
+    args.hidden = args.hidden.replace("+", ",")
     if args.dry_run:
         dry_run(args)
         return

@@ -338,11 +338,14 @@ int pgcn_debug_rank_graph(int n, const int *indptr, const int *indices, int worl
  *   "gs_orig_cols" 0/1 (a column subset's plain GraphSum gathers through the original column
  *   ids instead of compacting its input, default 1), "gs16_gather" 0..2 (the blocked d = 16
  *   gather kernel: 0 (default) by mean segment length, 1 k_graphsum16, 2 interleaved slots);
- *   r06 (26 keys): "co_draw" also 2 (dense X too, the default), "tn_fold" 0/1 (one GPU and
+ *   r06 (27 keys): "co_draw" also 2 (dense X too, the default), "tn_fold" 0/1 (one GPU and
  *   edge-cut ranks between processes: the weight gradients' last reduction pass inside the
  *   Adam launch / the all-reduce push, default 1), "fuse_finish" 0/1 (one GPU, <= 512 loss
  *   blocks: the loss kernel's last block finishes the pass's scalars, default 1), "mask_per"
- *   1/2 (64-draw mask words per stored RNG state, default 2), "peer_uncached" 0/1 (the peer
+ *   1/2 (64-draw mask words per stored RNG state, default 2), "csc_tree" 0/1 (sparse X's
+ *   W1.grad as a fixed tree over each feature's entries, default 1; 0: the reference's sequential
+ *   order, bit-exact), "mask_adam" 0/1 (one GPU: the next epoch's input mask drawn by the Adam
+ *   launch, default 1, bit-identical), "peer_uncached" 0/1 (the peer
  *   exchange's receive slots in uncached memory, default 0), and the ring GraphSum's schedule
  *   shapes "ring_pair" 0/1 and "ring_window" 0/2/3 (0: the default window 3), both measured
  *   slower and off;
