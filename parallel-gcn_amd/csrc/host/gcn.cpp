@@ -68,6 +68,11 @@ int g_sparse_dual = 1;
 // stream hand-offs cost more than the ~7 us of kernels they hide)
 int g_mm_side = 0;
 constexpr int kMmSideRows = 65536;
+// "reassoc_small" (read at engine build): on graphs of fewer than kMmSideRows nodes the output
+// layer runs in the reassociated order (Â H) W even when the classes are no more than the last
+// hidden width (<= 16), so its Matmul runs inside the loss kernel: a small graph's epoch is
+// bound by its launches, not by the GraphSum's width (the fp32 order differs, like reddit's)
+int g_reassoc_small = 1;
 // "eval_tail" (read at engine build): the edge-cut eval pass's last exchange and output layer
 // on the (high-priority) comm stream beside the next epoch's mask draw and first-layer product
 // (ModuleContext::tail_stream; peer exchange between processes only; bit-identical).  Off: on
@@ -784,7 +789,8 @@ void GCN::insert_last_layer() {
   auto drop = std::make_unique<Dropout>(prev, params.dropouts.back(), rngs[(size_t)L - 1], &ctx);
   dropouts_.push_back(drop.get());
   modules.push_back(std::move(drop));
-  if (params.reassociate_last && hl < C && graph_symmetric) {
+  const bool small = g_reassoc_small && hl <= 16 && part.bounds.back() < kMmSideRows;
+  if (params.reassociate_last && (hl < C || small) && graph_symmetric) {
     // out = Â (H W) computed as (Â H) W: the same product (Â is symmetric, so the backward
     // Â dOut W^T = Â (dOut W^T) and W.grad = H^T Â dOut = (Â H)^T dOut also match), but the
     // GraphSum gathers rows of width hl instead of C.  Only the fp32 rounding order differs.

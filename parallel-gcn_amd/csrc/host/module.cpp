@@ -56,8 +56,11 @@ std::vector<float> Variable::to_host(int which) const {
 
 // "csc_tree" (read per launch): sparse X's W1.grad summed as a fixed tree over each feature's
 // entries (k_spmm_csc_tree) instead of hpdga's sequential scatter order (k_spmm_csc_bwd,
-// bit-exact); deterministic, within the reordering bound
-int g_csc_tree = 1;
+// bit-exact); deterministic, the sums in another order.  Off: measured slower where it counts
+// (same box, 400 epochs, profiles/r06/k: citeseer 11.6-11.7k vs 12.1k epochs/s, pubmed_synth
+// 6.57-6.59k vs 7.06k, cora 10.7-12.4k vs 12.3k) -- the chain's one-wave tail is not what
+// bounds the launch
+int g_csc_tree = 0;
 
 // ------------------------------------------------------------------------------------------
 // Dropout (src/module.cu:6-99; hpdga module.cpp:196-228)

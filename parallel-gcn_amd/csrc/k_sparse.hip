@@ -243,9 +243,11 @@ __global__ __launch_bounds__(CH) void k_spmm_csc_bwd(int nf, int p, int ldg,
 // W1.grad over sparse X as a fixed tree (knob "csc_tree", r06): thread t of the feature's
 // workgroup sums the products of entries t, t + CH, ... in entry order (4 entries' index,
 // value, mask and grad-row loads in flight together), then the CH partial rows are added in
-// a fixed binary tree through LDS -- deterministic, within the reordering bound of the
-// sequential chain k_spmm_csc_bwd keeps (hpdga's scatter order, bit-exact), whose longest
-// column (cora: 1,083 entries) made that kernel the epoch's longest (14.8 us)
+// a fixed binary tree (through LDS, then lane shuffles in wave 0) over the smallest power of
+// two of threads that holds the feature's entries -- deterministic, differing by the summation
+// order only from the sequential chain k_spmm_csc_bwd keeps (hpdga's scatter order, bit-exact), whose longest
+// column (cora: 1,083 entries) made that kernel the epoch's longest (14.8 us); 1,024 threads
+// per feature on matrices of > 512 entries per feature, like k_spmm_csc_bwd
 template <int CH>
 __global__ __launch_bounds__(CH) void k_spmm_csc_tree(int nf, int p, int ldg,
                                                       const int *__restrict__ csc_ptr,
@@ -284,8 +286,12 @@ __global__ __launch_bounds__(CH) void k_spmm_csc_tree(int nf, int p, int ldg,
       for (int c = 0; c < 16; c++) acc[c] += (k0 + c < p ? g[c] : 0.0f) * av[u];
     }
   }
-  // the tree: at each level the upper half's rows are added into the lower half's
-  for (int h = CH / 2; h >= 1; h >>= 1) {
+  // the tree, over the smallest power of two of threads that holds every entry (the threads
+  // past it hold zeros): at each level the upper half's rows are added into the lower half's,
+  // through LDS down to one wave, then within wave 0 by lane shuffles
+  int span = 1;
+  while (span < min(e1 - e0, CH)) span <<= 1;
+  for (int h = span / 2; h >= 64; h >>= 1) {
     if (tid >= h && tid < 2 * h)
 #pragma unroll
       for (int c = 0; c < 16; c++) red[tid - h][c] = acc[c];
@@ -294,6 +300,14 @@ __global__ __launch_bounds__(CH) void k_spmm_csc_tree(int nf, int p, int ldg,
 #pragma unroll
       for (int c = 0; c < 16; c++) acc[c] += red[tid][c];
     __syncthreads();
+  }
+  if (tid >= 64) return;
+  for (int h = min(span, 64) / 2; h >= 1; h >>= 1) {
+#pragma unroll
+    for (int c = 0; c < 16; c++) {
+      const float o = __shfl_down(acc[c], h, 64);
+      if (tid < h) acc[c] += o;
+    }
   }
   if (tid == 0)
     for (int c = 0; c < 16 && k0 + c < p; c++) bgrad[(long long)f * p + k0 + c] = acc[c];
@@ -325,8 +339,12 @@ void launch_spmm_csc_bwd(int nf, int p, int ldg, const int *csc_ptr, const int *
   if (nf <= 0 || p <= 0) return;
   const dim3 grid((unsigned)nf, (unsigned)ceil_div(p, 16));
   if (tree) {
-    PGCN_LAUNCH(k_spmm_csc_tree<256>, grid, dim3(256), 0, s, nf, p, ldg, csc_ptr, csc_row,
-                csc_pos, a, mask, mask_base, scale, cgrad, bgrad, order);
+    if (nnz > 512LL * nf)
+      PGCN_LAUNCH(k_spmm_csc_tree<1024>, grid, dim3(1024), 0, s, nf, p, ldg, csc_ptr, csc_row,
+                  csc_pos, a, mask, mask_base, scale, cgrad, bgrad, order);
+    else
+      PGCN_LAUNCH(k_spmm_csc_tree<256>, grid, dim3(256), 0, s, nf, p, ldg, csc_ptr, csc_row,
+                  csc_pos, a, mask, mask_base, scale, cgrad, bgrad, order);
     return;
   }
   if (nnz > 512LL * nf)

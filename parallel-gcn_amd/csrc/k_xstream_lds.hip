@@ -239,13 +239,22 @@ __global__ __launch_bounds__(64 * (XL_NN_LOADERS + XL_NN_CONSUMERS), 1) void k_x
   unsigned *const ready = reinterpret_cast<unsigned *>(lds + XL_LDS - XL_FLAGS);
   unsigned *const freed = ready + 8;
   if (threadIdx.x < 16) ready[threadIdx.x] = 0u;
-  {  // B^T [16][XL_BS] (zero outside [K, N]) ahead of the ring
+  {  // B^T [16][XL_BS] (zero outside [K, N]) ahead of the ring: every load of the thread's
+     // elements issued before their stores (one round trip, not one per element)
     float *bt = reinterpret_cast<float *>(lds);
-    for (int e = threadIdx.x; e < 16 * NS * 16; e += blockDim.x) {
-      const int k = e >> 4, j = e & 15;
-      float v = 0.0f;
-      if (k < K && j < N) v = trans_b ? B[(long long)j * ldb + k] : B[(long long)k * ldb + j];
-      bt[j * XL_BS + k] = v;
+    constexpr int NT = 64 * (XL_NN_LOADERS + XL_NN_CONSUMERS), PER = (16 * NS * 16 + NT - 1) / NT;
+    float v[PER];
+#pragma unroll
+    for (int u = 0; u < PER; u++) {
+      const int e = threadIdx.x + u * NT, k = e >> 4, j = e & 15;
+      v[u] = 0.0f;
+      if (e < 16 * NS * 16 && k < K && j < N)
+        v[u] = trans_b ? B[(long long)j * ldb + k] : B[(long long)k * ldb + j];
+    }
+#pragma unroll
+    for (int u = 0; u < PER; u++) {
+      const int e = threadIdx.x + u * NT, k = e >> 4, j = e & 15;
+      if (e < 16 * NS * 16) bt[j * XL_BS + k] = v[u];
     }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

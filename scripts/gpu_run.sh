@@ -17,7 +17,8 @@
 #                              then tools/epoch_breakdown.py
 #   dtrace:<tag>:<dataset>     rocprofv3 kernel trace of tools/datasets_bench.py on one dataset,
 #                              then tools/epoch_breakdown.py (epochs between Adam launches)
-#   rtrace:<tag>:<world>       the same of tools/rank_epoch.py <world> (rank 0's solo epoch)
+#   rtrace:<tag>:<world>[:<knob=v,...>]  the same of tools/rank_epoch.py <world> (rank 0's
+#                              solo epoch; the knobs through RANK_KNOBS)
 #   traffic:<tag>[:<args>[:<traffic.py args>]]  FETCH_SIZE / WRITE_SIZE passes (one counter
 #                              group each) of the same, then tools/traffic.py (e.g.
 #                              --epoch,11,--hidden,128+128+128,--write,r06)
@@ -104,8 +105,8 @@ for step in "$@"; do
       [ $rc -eq 0 ] || { tail -20 "$O/$a.log"; exit $rc; }
       python3 tools/epoch_breakdown.py "$O/$a" k_adam > "$O/$a.breakdown.txt" 2>&1
       head -30 "$O/$a.breakdown.txt" ;;
-    rtrace)  # rtrace:<tag>:<world>: kernel trace of tools/rank_epoch.py (rank 0's solo epoch)
-      ( cd /tmp && cd "$ROOT" && timeout -k 10 600 rocprofv3 --kernel-trace --stats \
+    rtrace)  # rtrace:<tag>:<world>[:<knob=v,...>]: kernel trace of tools/rank_epoch.py
+      ( cd /tmp && cd "$ROOT" && RANK_KNOBS="${c:-}" timeout -k 10 600 rocprofv3 --kernel-trace --stats \
           -d "$O/$a" -o run -f csv -- python3 tools/rank_epoch.py "${b:-8}" > "$O/$a.log" 2>&1 )
       rc=$?
       echo "[rtrace $a] rc=$rc"

@@ -25,17 +25,21 @@ def _counts(ds):
     return {s: int(((sp == s) & (lab >= 0)).sum()) for s in (1, 2, 3)}
 
 
-def _run_all(loaded, pgcn):
-    """The default engine (reassociate_last requested, output layer over every row).  With
-    hidden 16 above the class count of cora (7), citeseer (6) and pubmed (3) the output layer
-    keeps the reference's module order Â (H W2), so every intermediate is comparable tensor
-    by tensor; the reassociated order is covered by test_reassociated_* below and by
+def _run_all(loaded, pgcn, reassoc_small=0):
+    """The engine with reassociate_last requested, output layer over every row.  With
+    reassoc_small 0 (hidden 16 above the class count of cora (7), citeseer (6) and pubmed (3))
+    the output layer keeps the reference's module order Â (H W2), so every intermediate is
+    comparable tensor by tensor; with reassoc_small 1 (the default: graphs under 65,536 nodes
+    run the output layer as (Â H) W2, its Matmul inside the loss kernel) the epoch lines,
+    eval logits and weights are compared (test_epoch_lines, test_final_weights); the
+    reassociated order is also covered by test_reassociated_* below and by
     tests/test_gpu_parity_large.py."""
     out = {}
     for name in DATASETS:
         ds = loaded[name]
-        g = pgcn.GCN(pgcn.make_params(ds), ds)
-        assert g.query("reassociated") == 0
+        with helpers.knobs(pgcn, reassoc_small=reassoc_small):
+            g = pgcn.GCN(pgcn.make_params(ds), ds)
+        assert g.query("reassociated") == reassoc_small
         e1 = {}
         lines = []
         for e in range(100):
@@ -56,7 +60,18 @@ def _run_all(loaded, pgcn):
 
 @pytest.fixture(scope="module")
 def engine_runs(loaded, pgcn):
-    return _run_all(loaded, pgcn)
+    return _run_all(loaded, pgcn, reassoc_small=0)
+
+
+@pytest.fixture(scope="module")
+def engine_runs_small(loaded, pgcn):
+    return _run_all(loaded, pgcn, reassoc_small=1)
+
+
+@pytest.fixture(params=["reference_order", "reassociated"])
+def any_runs(request):
+    return request.getfixturevalue("engine_runs" if request.param == "reference_order"
+                                   else "engine_runs_small")
 
 
 @pytest.fixture(scope="module")
@@ -76,8 +91,8 @@ def oracle_ties(loaded):
 
 
 @pytest.mark.parametrize("name", DATASETS)
-def test_epoch_lines(engine_runs, oracle_ties, name):
-    runs = engine_runs
+def test_epoch_lines(any_runs, oracle_ties, name):
+    runs = any_runs
     gold = helpers.golden(name)["epoch_lines"].reshape(-1, 4)
     ours = runs[name]["lines"]
     cnt = runs[name]["counts"]
@@ -167,16 +182,38 @@ def test_epoch1_tensors(engine_runs, name):
     np.testing.assert_allclose(e1["eval_logits"], gold["e1_eval_logits"], rtol=1e-4, atol=1e-6)
 
 
+@pytest.mark.parametrize("name", ["cora", "citeseer"])
+def test_epoch1_tensors_reassociated(engine_runs_small, name):
+    """The default small-graph engine (output layer as (Â H) W2): the tensors its module
+    order shares with the reference's -- the dropped input and the first layer bit-exact, the
+    hidden activations, both weights and their gradients, the output logits and eval's
+    logits at 1e-4 (variable 4 is Â H here, not H W2)."""
+    gold = helpers.golden(name)
+    e1 = engine_runs_small[name]["e1"]
+    np.testing.assert_array_equal(e1["vars"][0], gold["e1_input"])
+    np.testing.assert_array_equal(e1["vars"][1], gold["e1_l1_var1"])
+    for i, n in enumerate(VAR_NAMES):
+        if n in ("W1", "W2"):
+            np.testing.assert_allclose(e1["grads"][i], gold[f"e1_{n}_grad"], rtol=1e-4, atol=1e-7,
+                                       err_msg=n + " grad")
+            np.testing.assert_allclose(e1["vars"][i], gold[f"e1_{n}_after_step"], rtol=1e-4,
+                                       atol=1e-7, err_msg=n)
+        elif n in ("l1_var2", "output"):
+            np.testing.assert_allclose(e1["vars"][i], gold[f"e1_{n}"], rtol=1e-4, atol=1e-6,
+                                       err_msg=n)
+    np.testing.assert_allclose(e1["eval_logits"], gold["e1_eval_logits"], rtol=1e-4, atol=1e-6)
+
+
 @pytest.mark.parametrize("name", DATASETS)
-def test_final_weights(engine_runs, name):
+def test_final_weights(any_runs, name):
     """Weights after 100 Adam epochs against the reference build's.  Adam's update is
     m/(sqrt(v)+eps): a gradient entry near zero flips the sign of its few-ulp steps, so single
     entries may drift by a few step sizes (lr = 0.01); the bulk must stay near fp32 noise
     (pubmed_synth measured: median 1.1e-4 of max|W|, 97.2 % of entries within 1e-3; its 500
     TF-IDF features make many W1 rows see near-zero gradients)."""
     gold = helpers.golden(name)
-    for ours, ref in ((engine_runs[name]["w1"], gold["final_W1"]),
-                      (engine_runs[name]["w2"], gold["final_W2"])):
+    for ours, ref in ((any_runs[name]["w1"], gold["final_W1"]),
+                      (any_runs[name]["w2"], gold["final_W2"])):
         scale = np.abs(ref).max()
         err = np.abs(ours - ref)
         assert err.max() <= 5e-3 * scale, err.max() / scale
@@ -438,8 +475,8 @@ def test_part2_configs_match_oracle(datasets, pgcn, name):
     g.close()
 
 
-def _fused_run(pgcn, ds, fuse, epochs, **make):
-    with helpers.knobs(pgcn, fuse_epilogue=fuse):
+def _fused_run(pgcn, ds, fuse, epochs, reassoc_small=1, **make):
+    with helpers.knobs(pgcn, fuse_epilogue=fuse, reassoc_small=reassoc_small):
         g = pgcn.GCN(pgcn.make_params(ds, **make), ds)
         lines = [g.train_epoch() + g.eval(2) for _ in range(epochs)]
         g.train_epoch()  # tensors of a training pass: relu/dropout forward and backward
@@ -460,7 +497,8 @@ def test_fused_epilogue_bit_identical(loaded, pgcn, case):
     X-stream product applying the eval ReLU / writing the ring tables, compared without it; and
     on cora's module order the Dropout + ReLU backward in the output Matmul's input-grad
     product (k_xstream_nn epilogue), compared without it: fuse_epilogue 15 = all, 0 = none,
-    13 = no prestaged tables, 11 = no X-stream epilogue, 7 = no Matmul tails)."""
+    13 = no prestaged tables, 11 = no X-stream epilogue, 7 = no Matmul tails; "cora" keeps
+    the reference module order with reassoc_small 0, cora_h4 is reassociated either way)."""
     if case == "lds_dense":
         ds, make, tails = pgcn.Dataset.synthetic(120000, 64, 41, 1500000, 21), {}, 2
     elif case == "lds_deep":  # 128-wide rows: the tails ride the wide (all-pass) combine
@@ -468,7 +506,7 @@ def test_fused_epilogue_bit_identical(loaded, pgcn, case):
         make, tails = dict(hidden_dims=(128, 128, 128), dropouts=(0.5,) * 4), 3
     else:
         ds = loaded["cora"]
-        make, tails = ({"hidden_dims": (4,)}, 2) if case == "cora_h4" else ({}, 2)
+        make, tails = ({"hidden_dims": (4,)}, 2) if case == "cora_h4" else ({"reassoc_small": 0}, 2)
     on = _fused_run(pgcn, ds, 15, 4, **make)
     off = _fused_run(pgcn, ds, 0, 4, **make)
     no_stage = _fused_run(pgcn, ds, 13, 4, **make)
@@ -546,10 +584,11 @@ def test_mask_states_per_128_draws_bit_identical(loaded, pgcn, case):
         np.testing.assert_array_equal(x, y)
 
 
-@pytest.mark.parametrize("name", ["cora", "citeseer"])
+@pytest.mark.parametrize("name", ["cora", "citeseer", "pubmed_synth"])  # 256 / 1024 threads
 def test_csc_tree_matches_sequential_chain(loaded, pgcn, name):
-    """csc_tree 1 (default): sparse X's W1.grad as a fixed tree over each feature's entries
-    (k_spmm_csc_tree) against hpdga's sequential scatter order (csc_tree 0, k_spmm_csc_bwd,
+    """csc_tree 1 (off by default: measured slower): sparse X's W1.grad as a fixed tree over
+    each feature's entries (k_spmm_csc_tree) against hpdga's sequential scatter order
+    (csc_tree 0, the default, k_spmm_csc_bwd,
     bit-exact with the reference): W1.grad within the reordering bound after an epoch, the
     epoch lines within 1e-5 over 5 epochs, and the tree repeats its own bits."""
     ds = loaded[name]
