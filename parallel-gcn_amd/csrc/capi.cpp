@@ -738,7 +738,7 @@ int pgcn_debug_set(const char *key, int value) {
     if (!in(0, 1)) return PGCN_E_INVALID;
     pgcn::g_csc_tree = value;
   } else if (!std::strcmp(key, "mask_per")) {
-    if (!in(1, 2)) return PGCN_E_INVALID;
+    if (!in(0, 2)) return PGCN_E_INVALID;
     pgcn::g_mask_per = value;
   } else if (!std::strcmp(key, "fuse_finish")) {
     if (!in(0, 1)) return PGCN_E_INVALID;

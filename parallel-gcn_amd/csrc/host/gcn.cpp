@@ -267,17 +267,21 @@ void build_dev_features(DevFeatures &feats, const int *fptr, const int *indices,
 // Chunk states of a dropout over global elements [elem_begin, elem_end) whose first training
 // forward draws stream positions offset + element (hpdga: one xorshift128+ draw per element,
 // module.cpp:208-219), each 64-element chunk's state jumped to from the seed state.
-// "mask_per" (read at engine build): 64-draw mask words per stored RNG state (1 or 2)
-int g_mask_per = 2;
+// "mask_per" (read at engine build): 64-draw mask words per stored RNG state (1 or 2); 0 = by
+// size: 2 from kMaskPer2Chunks words on (reddit's input mask: half the period jumps, 68.3 ->
+// 65.2 us for both masks), else 1 (a W = 8 rank's input mask, 274 k words: twice the threads,
+// each chain half as long -- 17.3 -> 14.5 us, profiles/r06/o)
+int g_mask_per = 0;
+constexpr long long kMaskPer2Chunks = 1LL << 20;
 
 void init_dropout_rng_range(DropoutRng &r, const uint64_t seed[2], unsigned long long offset,
                             long long elem_begin, long long elem_end) {
-  r.per = g_mask_per;
   r.elem_begin = elem_begin;
   r.elem_end = elem_end;
   r.chunk_lo = r.elem_begin / kDropChunk;
   const long long chunk_hi = ceil_div(r.elem_end, kDropChunk);
   r.n_chunks = std::max(0LL, chunk_hi - r.chunk_lo);
+  r.per = g_mask_per ? g_mask_per : (r.n_chunks >= kMaskPer2Chunks ? 2 : 1);
   r.mask_base = r.elem_begin - kDropChunk * r.chunk_lo;
   // one state per r.per mask words: the stream's state at the first draw of words per * k
   const long long n_states = ceil_div(r.n_chunks, (long long)r.per);

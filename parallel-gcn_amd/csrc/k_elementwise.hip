@@ -1113,6 +1113,12 @@ void launch_out_xent(const float *H, int ldh, int kh, const float *W, int ldw, f
               training ? dH : nullptr, lddh, training ? dWp : nullptr, t, fin ? *fin : XentFinal{})
   if (c == 41 && ld == 44 && kh == 16)  // reddit (41 classes, hidden 16)
     OUT_XENT(41, 44, 16);
+  else if (c == 7 && ld == 8 && kh == 16)  // cora (reassoc_small)
+    OUT_XENT(7, 8, 16);
+  else if (c == 6 && ld == 8 && kh == 16)  // citeseer
+    OUT_XENT(6, 8, 16);
+  else if (c == 3 && ld == 4 && kh == 16)  // pubmed
+    OUT_XENT(3, 4, 16);
   else
     OUT_XENT(0, 0, 0);
 #undef OUT_XENT

@@ -59,7 +59,13 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 // NN: 2 loaders + 4 consumers (two waves on two SIMDs: 2 x ~220 registers fit); TN: 1 loader +
 // 3 consumers (its accumulators need a SIMD per consumer)
 constexpr int XL_NN_LOADERS = 2, XL_NN_CONSUMERS = 4;
-constexpr int XL_TN_LOADERS = 1, XL_TN_CONSUMERS = 3;
+#ifndef PGCN_XS_TN_ABLATE
+#define PGCN_XS_TN_ABLATE 0
+#endif
+#ifndef PGCN_XS_TN_LOADERS
+#define PGCN_XS_TN_LOADERS 1
+#endif
+constexpr int XL_TN_LOADERS = PGCN_XS_TN_LOADERS, XL_TN_CONSUMERS = 4 - PGCN_XS_TN_LOADERS;
 constexpr int XL_LDS = 159 * 1024;  // ring + hand-off words (one workgroup per CU)
 constexpr int XL_FLAGS = 64;        // ready[8], freed[8] at the end
 constexpr int XL_KC = 10;           // the instantiated width: K in (576, 640] (reddit: 602)
@@ -503,6 +509,9 @@ __global__ __launch_bounds__(64 * (XL_TN_LOADERS + XL_TN_CONSUMERS), 1) void k_x
         }
       }
       xl_release(freed, slot, t, lane);
+#if PGCN_XS_TN_ABLATE & 2  // timing-only diagnostic builds: no MFMAs
+      if (M > 0) return;
+#endif
 #pragma unroll
       for (int q = 0; q < 4; q++) {
         // a uniform exit per row step (never taken: nslot >= 2) keeps hipcc from scheduling
@@ -531,6 +540,10 @@ __global__ __launch_bounds__(64 * (XL_TN_LOADERS + XL_TN_CONSUMERS), 1) void k_x
       if (t + XL_TN_CONSUMERS < T) group(t + XL_TN_CONSUMERS, bjb, mwb, bja, mwa);
     }
   }
+#if PGCN_XS_TN_ABLATE & 1  // timing-only diagnostic builds (tools/xs_scale.py): no epilogue
+  if (threadIdx.x == 0 && M < 0) partial[0] = acc[0][0][0];
+  return;
+#endif
   // consumers 1, 2 hand their accumulators to consumer 0 through the (idle) ring; 0 adds them
   // in consumer order and writes the partial
   __syncthreads();
@@ -547,9 +560,19 @@ __global__ __launch_bounds__(64 * (XL_TN_LOADERS + XL_TN_CONSUMERS), 1) void k_x
   }
   __syncthreads();
   if (wave == XL_TN_LOADERS) {
+    // per 64-column chunk: the other consumers' 16 values read together, then the adds (in
+    // consumer order) and 16 stores through a buffer resource of the partial's K rows, whose
+    // range check drops the rows k >= K -- no per-store branch, so no LDS round trip per value
+    // (r06: the branch-per-store form waited on each read: ~15 us of every TN launch)
     float *p = partial + (long long)blockIdx.x * K * 16;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(p, 0, K * 16 * 4, 0x00020000);
 #pragma unroll
-    for (int c = 0; c < KC; c++)
+    for (int c = 0; c < KC; c++) {
+      float o[16][XL_TN_CONSUMERS > 1 ? XL_TN_CONSUMERS - 1 : 1];
+#pragma unroll
+      for (int tr = 0; tr < 16; tr++)
+#pragma unroll
+        for (int q = 0; q < XL_TN_CONSUMERS - 1; q++) o[tr][q] = red[q * RED + (c * 16 + tr) * 64 + lane];
 #pragma unroll
       for (int t = 0; t < 4; t++)
 #pragma unroll
@@ -557,9 +580,10 @@ __global__ __launch_bounds__(64 * (XL_TN_LOADERS + XL_TN_CONSUMERS), 1) void k_x
           const int k = 64 * c + 4 * (4 * g + r) + t;
           float v = acc[c][t][r];
 #pragma unroll
-          for (int q = 0; q < XL_TN_CONSUMERS - 1; q++) v += red[q * RED + ((c * 4 + t) * 4 + r) * 64 + lane];
-          if (k < K) p[(long long)k * 16 + i] = v;
+          for (int q = 0; q < XL_TN_CONSUMERS - 1; q++) v += o[t * 4 + r][q];
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, (k * 16 + i) * 4, 0, 0);
         }
+    }
   }
 }
 

@@ -17,8 +17,9 @@
 #                              then tools/epoch_breakdown.py
 #   dtrace:<tag>:<dataset>     rocprofv3 kernel trace of tools/datasets_bench.py on one dataset,
 #                              then tools/epoch_breakdown.py (epochs between Adam launches)
-#   rtrace:<tag>:<world>[:<knob=v,...>]  the same of tools/rank_epoch.py <world> (rank 0's
-#                              solo epoch; the knobs through RANK_KNOBS)
+#   rtrace:<tag>:<world>[:<knob=v,...>[:<library>]]  the same of tools/rank_epoch.py <world>
+#                              (rank 0's solo epoch; knobs through RANK_KNOBS, an A/B build of
+#                              the library through PGCN_LIB)
 #   traffic:<tag>[:<args>[:<traffic.py args>]]  FETCH_SIZE / WRITE_SIZE passes (one counter
 #                              group each) of the same, then tools/traffic.py (e.g.
 #                              --epoch,11,--hidden,128+128+128,--write,r06)
@@ -51,7 +52,7 @@ run() {  # tag, seconds, command... (stdout -> tag.log)
 }
 
 for step in "$@"; do
-  IFS=: read -r kind a b c <<< "$step"
+  IFS=: read -r kind a b c d <<< "$step"
   case $kind in
     pytest)
       argv_of "${step#pytest:}"
@@ -105,8 +106,9 @@ for step in "$@"; do
       [ $rc -eq 0 ] || { tail -20 "$O/$a.log"; exit $rc; }
       python3 tools/epoch_breakdown.py "$O/$a" k_adam > "$O/$a.breakdown.txt" 2>&1
       head -30 "$O/$a.breakdown.txt" ;;
-    rtrace)  # rtrace:<tag>:<world>[:<knob=v,...>]: kernel trace of tools/rank_epoch.py
-      ( cd /tmp && cd "$ROOT" && RANK_KNOBS="${c:-}" timeout -k 10 600 rocprofv3 --kernel-trace --stats \
+    rtrace)  # rtrace:<tag>:<world>[:<knob=v,...>[:<library>]]: kernel trace of tools/rank_epoch.py
+      ( cd /tmp && cd "$ROOT" && RANK_KNOBS="${c:-}" PGCN_LIB="${d:+$ROOT/$d}" \
+          timeout -k 10 600 rocprofv3 --kernel-trace --stats \
           -d "$O/$a" -o run -f csv -- python3 tools/rank_epoch.py "${b:-8}" > "$O/$a.log" 2>&1 )
       rc=$?
       echo "[rtrace $a] rc=$rc"

@@ -234,7 +234,7 @@ ENGINE_DEFAULTS = {"train_ahead": 1, "split_rows": 0, "split_cols": 1, "eval_ax"
                    "parse_threads": 0, "gs_split": 3, "gs_item_iters": 0, "co_draw": 2,
                    "gs_orig_cols": 1, "sparse_dual": 1, "eval_tail": 0, "gs16_gather": 0,
                    "peer_uncached": 0, "ring_pair": 0, "tn_fold": 1,
-                   "fuse_finish": 1, "mask_per": 2,
+                   "fuse_finish": 1, "mask_per": 0,
                    "ring_window": 0, "csc_tree": 0, "mask_adam": 1,
                    "reassoc_small": 1}
 

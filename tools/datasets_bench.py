@@ -30,6 +30,8 @@ import numpy as np
 import torch  # noqa: F401  (one HIP runtime per process: torch's)
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if "--lib" in sys.argv:  # an A/B build of the library (as PGCN_LIB), set before it loads
+    os.environ["PGCN_LIB"] = os.path.abspath(sys.argv[sys.argv.index("--lib") + 1])
 sys.path.insert(0, os.path.join(REPO, "tests"))
 import helpers  # noqa: E402
 
@@ -102,6 +104,7 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--only", default=None, help="one dataset (e.g. under rocprofv3)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--lib", default=None, help="another build of libpgcn.so (A/B)")
     ap.add_argument("--set", action="append", default=[], metavar="KNOB=VALUE",
                     help="engine knob (pgcn_debug_set) for every engine built (A/B runs)")
     args = ap.parse_args()

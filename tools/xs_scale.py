@@ -5,7 +5,8 @@ its 1/2, 1/4, 1/8 (an edge-cut rank's share at W = 2, 4, 8).  Times each call by
 the stream it runs on, median of `reps`, and prints the fixed part: t(M) - t(M_full) * M /
 M_full.  One JSON line.
 
-usage: python3 tools/xs_scale.py [reps=30]
+usage: python3 tools/xs_scale.py [reps=30] [library path (A/B: another build, as PGCN_LIB)]
+                                [nocheck]
 """
 import ctypes
 import json
@@ -15,6 +16,8 @@ import sys
 import torch
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if len(sys.argv) > 2:
+    os.environ["PGCN_LIB"] = os.path.abspath(sys.argv[2])
 sys.path.insert(0, os.path.join(REPO, "tests"))
 import helpers  # noqa: E402
 
@@ -61,10 +64,33 @@ def timed(fn, M):
 
 
 out = {}
-for name, fn in (("nn", nn), ("tn", tn)):
+# the products against torch's fp32 (a sanity check of the build under test, not a parity test)
+for M in (MF, MF // 8):
+    with torch.cuda.stream(s):
+        nn(M)
+        tn(M)
+    s.synchronize()
+    Xm = A[:M, :K].double()
+    e_nn = ((C[:M] - (Xm @ W.double()).float()).abs().max() / C[:M].abs().max()).item()
+    e_tn = ((WG - (Xm.T @ dZ[:M].double()).float()).abs().max() / WG.abs().max()).item()
+    out[f"check_M{M}"] = {"nn_rel": e_nn, "tn_rel": e_tn}
+    if "nocheck" not in sys.argv[3:]:  # (timing-only ablation builds compute nothing)
+        assert e_nn < 1e-5 and e_tn < 1e-5, out
+arms = (("nn", nn), ("tn", tn))
+if not os.environ.get("XS_RING_ONLY"):  # the register-streamed kernels too (xstream_ring 0)
+    def _plain(fn):
+        def run(M):
+            pg.lib.pgcn_debug_set(b"xstream_ring", 0)
+            try:
+                fn(M)
+            finally:
+                pg.lib.pgcn_debug_set(b"xstream_ring", 1)
+        return run
+    arms += (("nn_plain", _plain(nn)), ("tn_plain", _plain(tn)))
+for name, fn in arms:
     full = timed(fn, MF)
     row = {"full_us": round(full, 1)}
-    for d in (2, 4, 8):
+    for d in (2, 4, 8, 16, 32, 64):
         M = MF // d
         t = timed(fn, M)
         row[f"1/{d}_us"] = round(t, 1)
