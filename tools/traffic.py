@@ -5,7 +5,7 @@ usage: python3 tools/traffic.py gpurun_out/<dir> [epoch_calls] [--write <round>]
            [--key <workload>] [--hidden <dims, '+'-separated>] [--epoch <calls per epoch>]
 
 --epoch C (r06): the bytes of every GraphSum-family launch (the wide passes' prescale and
-combines included) between the last two k_adam_multi launches -- one epoch -- divided by the
+combines included) between the last two Adam launches (k_adam_multi or k_adam_mask) -- one epoch -- divided by the
 epoch's C GraphSum calls; the 4-layer model's d = 128 calls are 8 ring passes each.  --key: the
 entry of profiles/traffic_graphsum.json to write (default reddit-114M); --write merges it into
 the file when the file's source stamp matches (else the file starts afresh).
@@ -69,7 +69,7 @@ for counter in ("FETCH_SIZE", "WRITE_SIZE"):
     allrows = per_dispatch(counter)
     rows = [r for r in allrows if any(k in r[1] for k in GS_FAMILY)]
     if per_epoch:  # one epoch between the last two Adam launches, per GraphSum call
-        adam = [d for d, name, _ in allrows if "k_adam_multi" in name]
+        adam = [d for d, name, _ in allrows if "k_adam_multi" in name or "k_adam_mask" in name]
         lo, hi = adam[-2], adam[-1]
         tot = sum(v for d, _, v in rows if lo < d < hi)
         out[counter + "_KB_per_call"] = tot / int(per_epoch)
