@@ -31,6 +31,7 @@ extern int g_fuse_finish;           // host/gcn.cpp
 extern int g_mask_per;              // host/gcn.cpp
 extern int g_mask_adam;             // host/gcn.cpp
 extern int g_reassoc_small;         // host/gcn.cpp
+extern int g_defer_small_wgrad;     // host/module.cpp
 extern int g_eval_ax;               // host/gcn.cpp
 extern int g_epoch_graph;           // host/gcn.cpp
 extern long long g_lds_min_bytes;   // host/graph.cpp
@@ -731,6 +732,9 @@ int pgcn_debug_set(const char *key, int value) {
   } else if (!std::strcmp(key, "mask_adam")) {
     if (!in(0, 1)) return PGCN_E_INVALID;
     pgcn::g_mask_adam = value;
+  } else if (!std::strcmp(key, "defer_wgrad")) {
+    if (!in(0, 1)) return PGCN_E_INVALID;
+    pgcn::g_defer_small_wgrad = value;
   } else if (!std::strcmp(key, "reassoc_small")) {
     if (!in(0, 1)) return PGCN_E_INVALID;
     pgcn::g_reassoc_small = value;

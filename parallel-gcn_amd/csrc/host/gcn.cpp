@@ -1047,6 +1047,8 @@ struct GCN::FoldScope {
     if (!g.tn_pool) {
       size_t f = 0;
       for (const auto &w : g.weights) f += (size_t)64 * w->rows * ((w->cols + 15) / 16 * 16) + 64;
+      // the small graphs' loss-kernel W.grad block partials ([16][48] per block)
+      f += (size_t)g.ctx.xent_blocks * 16 * 48 + 64;
       g.tn_pool.allocate(f);
     }
     d->pool = g.tn_pool.get();

@@ -61,6 +61,13 @@ std::vector<float> Variable::to_host(int which) const {
 // 6.57-6.59k vs 7.06k, cora 10.7-12.4k vs 12.3k) -- the chain's one-wave tail is not what
 // bounds the launch
 int g_csc_tree = 0;
+// "defer_wgrad" (read per pass): a small graph's fused loss kernel writes the output layer's
+// W.grad block partials into the deferred-reduction pool (tn_fold), summed by the Adam launch
+int g_defer_small_wgrad = 1;
+// up to this many loss blocks (cora 43, citeseer 52): pubmed_synth's 309 partials per weight
+// element made the Adam launch's sum as long as the two launches it saved (7.73-7.74k vs
+// 7.78-7.80k epochs/s, profiles/r06/s)
+constexpr int kDeferWgradMaxBlocks = 128;
 
 // ------------------------------------------------------------------------------------------
 // Dropout (src/module.cu:6-99; hpdga module.cpp:196-228)
@@ -766,6 +773,7 @@ void CrossEntropyLoss::forward(bool training, const Stream &s) const {
     float *dH = Hv.dev_grad ? Hv.dev_grad.get() : nullptr;
     const int nb = xent_blocks(logits->rows);
     float *dWp = nullptr;
+    bool deferred = false;
     // (an edge-cut rank's rows are a slice of a large graph: the block partials too)
     if (training && g_fuse_output >= 2 &&
         (g_fuse_output == 3 || logits->rows >= 65536 || ctx->comm) &&
@@ -773,6 +781,20 @@ void CrossEntropyLoss::forward(bool training, const Stream &s) const {
         !ctx->mm_side &&
         tn_reduce_blocks_workspace(nb, fused->inner(), 48) <= ctx->gemm_workspace_bytes)
       dWp = static_cast<float *>(ctx->gemm_workspace);
+    // r06: a small graph's partials straight into the deferred-reduction pool when tn_fold is
+    // on (the Adam launch sums them in block order): the output layer's W.grad needs no launch
+    // of its own (k_xstream_tn before; the same sums in another grouping)
+    // (tn_fold 0, or no room: the same one ordered pass as its own launch -- the same bits)
+    bool one_pass = false;
+    if (training && !dWp && g_fuse_output >= 2 && g_defer_small_wgrad && !ctx->comm &&
+        nb <= kDeferWgradMaxBlocks && Wv.dev_grad && logits->ld <= 48 && !ctx->mm_side) {
+      dWp = tn_defer_blocks(nb, fused->inner(), num_classes, 48, Wv.dev_grad.get(), Wv.ld);
+      deferred = dWp != nullptr;
+      if (!dWp && (size_t)nb * fused->inner() * 48 * sizeof(float) <= ctx->gemm_workspace_bytes) {
+        dWp = static_cast<float *>(ctx->gemm_workspace);
+        one_pass = true;
+      }
+    }
     // training: dH also to the ring table of the GraphSum backward that reads it
     XentTable tb;
     const bool staged = training && dH && dh_reader && fused->inner() == 16 &&
@@ -782,7 +804,10 @@ void CrossEntropyLoss::forward(bool training, const Stream &s) const {
                     ctx->truth, logits->rows, num_classes, ctx->count, training ? 1 : 0,
                     ctx->xent_partials, s.get(), dH, Hv.ld, dWp, staged ? &tb : nullptr, ctx->fin);
     ctx->fin_taken = ctx->fin != nullptr;
-    if (dWp)
+    if (one_pass)
+      launch_tn_reduce_one_pass(dWp, nb, fused->inner(), num_classes, 48, Wv.dev_grad.get(),
+                                Wv.ld, s.get());
+    else if (dWp && !deferred)
       launch_tn_reduce_blocks(dWp, nb, fused->inner(), num_classes, 48, Wv.dev_grad.get(), Wv.ld,
                               s.get());
     fused->input_grad_done = training && dH;

@@ -843,6 +843,26 @@ static TnPlan blocks_plan(int n_blocks, int ldp) {
   return p;
 }
 
+void launch_tn_reduce_one_pass(const float *partial, int n, int K, int N, int ldp, float *C,
+                               int ldc, hipStream_t s) {
+  const long long elems = (long long)K * ldp;
+  PGCN_LAUNCH(k_gemm_tn_reduce, dim3((unsigned)ceil_div(elems, 256)), dim3(256), 0, s, partial, n,
+              K, N, ldp, C, ldc, ldc);
+}
+
+float *tn_defer_blocks(int n_blocks, int K, int N, int ldp, float *C, int ldc) {
+  float *room = n_blocks > 0 ? tn_defer_room(N, ldc, ldc, (size_t)n_blocks * K * ldp) : nullptr;
+  if (!room) return nullptr;
+  TnDeferred &d = g_tn_defer->d[g_tn_defer->n++];
+  d.src = room;
+  d.n_groups = n_blocks;
+  d.K = K;
+  d.N = N;
+  d.ldp = ldp;
+  d.C = C;
+  return room;
+}
+
 size_t tn_reduce_blocks_workspace(int n_blocks, int K, int ldp) {
   return plan_bytes(blocks_plan(n_blocks, ldp), K);
 }

@@ -348,6 +348,14 @@ void launch_out_xent(const float *H, int ldh, int kh, const float *W, int ldw, f
 // H^T grad, reduced in block order into C [kh][ldc] (N = c columns) by:
 void launch_tn_reduce_blocks(float *partial, int n_blocks, int K, int N, int ldp, float *C, int ldc,
                              hipStream_t s);
+// tn_defer active (the Adam launch sums deferred passes): room in its pool for n_blocks
+// per-block partials [K][ldp] of C [K][N] (ldc == N) and the deferred entry that sums them in
+// block order (one ordered pass, k_gemm_tn_reduce's loads and adds), or null
+float *tn_defer_blocks(int n_blocks, int K, int N, int ldp, float *C, int ldc);
+// C [K][N] = the n partials [K][ldp] summed in order by one k_gemm_tn_reduce pass (the sum
+// a tn_defer_blocks entry makes in the Adam launch)
+void launch_tn_reduce_one_pass(const float *partial, int n, int K, int N, int ldp, float *C,
+                               int ldc, hipStream_t s);
 size_t tn_reduce_blocks_workspace(int n_blocks, int K, int ldp);
 void launch_xent_fwd(float *logits, int ld, float *grad, const int *truth, int n, int c,
                      int count, int training, float *partials, hipStream_t s, int write_back = 1,

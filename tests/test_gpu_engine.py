@@ -726,6 +726,46 @@ def test_fused_output_weight_grad_close(loaded, pgcn, case):
     np.testing.assert_allclose(runs[3][1][:, [0, 2]], runs[1][1][:, [0, 2]], rtol=2e-5)
 
 
+@pytest.mark.parametrize("name", ["cora", "citeseer", "pubmed_synth"])
+def test_deferred_output_wgrad_small_graph(loaded, pgcn, name):
+    """defer_wgrad 1 (default; small graphs of <= 128 loss blocks -- pubmed_synth's 309 keep
+    the k_xstream_tn path: the same lines, launches and bits; output layer reassociated): the fused loss
+    kernel's per-block W2.grad partials go to the deferred-reduction pool and the Adam launch
+    sums them in block order -- no k_xstream_tn launch.  W2.grad within 2e-6 relative of the
+    k_xstream_tn one (defer_wgrad 0: another grouping of the same sums), the epoch lines within
+    float rounding, one launch fewer per epoch; tn_fold 0 reduces the same partials in one
+    ordered pass of its own: the same bits as the Adam launch's sum."""
+    ds = loaded[name]
+    runs = {}
+    for tag, kn in (("tn", dict(defer_wgrad=0)), ("defer", dict(defer_wgrad=1)),
+                    ("pass", dict(defer_wgrad=1, tn_fold=0))):
+        with helpers.knobs(pgcn, **kn):
+            g = pgcn.GCN(pgcn.make_params(ds), ds)
+            assert g.query("reassociated") == 1
+            g.train_epoch()
+            w2g = g.get_var(5, 1).copy()
+            lines = [g.train_epoch() + g.eval(2) for _ in range(3)]
+            pgcn.reset_path_counts()
+            for _ in range(4):
+                g.epoch_async()
+            g.results(4)
+            n = pgcn.path_counts()["launches"]
+            runs[tag] = dict(g=w2g, lines=np.array(lines, np.float64), launches=n,
+                             w=g.get_var(5).copy())
+            g.close()
+    a, b, c = runs["tn"], runs["defer"], runs["pass"]
+    scale = np.abs(a["g"]).max()
+    assert np.abs(b["g"] - a["g"]).max() <= 2e-6 * scale
+    np.testing.assert_allclose(b["lines"][:, [0, 2]], a["lines"][:, [0, 2]], rtol=2e-5)
+    np.testing.assert_array_equal(b["g"], c["g"])
+    np.testing.assert_array_equal(b["w"], c["w"])
+    if name == "pubmed_synth":
+        np.testing.assert_array_equal(b["g"], a["g"])
+        assert b["launches"] == a["launches"]
+    else:
+        assert b["launches"] == a["launches"] - 4, (a["launches"], b["launches"])
+
+
 def test_early_stopping_matches_reference(datasets, pgcn):
     """GCN::run's early stopping (hpdga gcn.cpp:238-250, src/gcn.cu:377-395): after epoch e >=
     k, stop when val_loss(e) > the mean of the last k val losses (the current one included,
