@@ -577,8 +577,10 @@ def main():
     def secondary(knobs, steps2=10):
         with helpers.knobs(pgcn, **knobs):
             g2 = engine()
-            el = timed(g2, steps2, 2)
+            el, ok = timed(g2, steps2, 2)
             g2.close()
+        if not ok:
+            raise SystemExit("bench.py: a secondary engine's epochs failed")
         return steps2 / el
 
     if not args.no_extra and world == 1 and not args.edge_cut:

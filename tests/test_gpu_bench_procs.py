@@ -38,3 +38,25 @@ def test_bench_gpus2_shared_gpu():
     assert par["logits"]["values"] == 232965 * 41
     assert par["after_timed"]["epochs"] == 2 + 1 + 3 + 2, par["after_timed"]
     assert par["after_timed"]["pass"], par["after_timed"]
+
+
+def test_bench_one_gpu_default_line():
+    """bench.py at N = 1 with its secondary measurements (the restricted-output and reference-
+    order engines) -- the driver's default invocation minus the CPU leg, on the small
+    reddit-11.6M workload: one JSON line with the contract's keys, the roofline object and the
+    secondary values."""
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "3", "--warmup",
+                        "1", "--workload", "reddit-11.6M", "--no-cpu-baseline"], cwd=REPO, env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config", "roofline"):
+        assert k in out, k
+    assert out["n_gpus"] == 1 and out["steps"] == 3 and out["value"] > 0
+    assert out["roofline"]["bound"] == "hbm" and 0 < out["roofline"]["frac"] < 1
+    assert out["value_restricted"] > 0 and out["value_reference_order"] > 0
