@@ -55,6 +55,9 @@ __device__ __forceinline__ void release_workgroup_stores() {
 // exit): lane 0 of wave 0 issues the system-scope acquire and waits for it, then the
 // workgroup's barrier orders every wave's slot loads after it
 __device__ __forceinline__ void acquire_system_workgroup() {
+#ifdef PGCN_ABL_NO_ACQUIRE  // timing-only diagnostic build (the cost of the acquire): unsafe
+  return;
+#endif
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: buffer_inv sc0 sc1
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
