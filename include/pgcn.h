@@ -340,8 +340,9 @@ int pgcn_debug_rank_graph(int n, const int *indptr, const int *indices, int worl
  *   gather kernel: 0 (default) by mean segment length, 1 k_graphsum16, 2 interleaved slots);
  *   r06 (29 keys): "co_draw" also 2 (dense X too, the default), "tn_fold" 0/1 (one GPU and
  *   edge-cut ranks between processes: the weight gradients' last reduction pass inside the
- *   Adam launch / the all-reduce push, default 1), "fuse_finish" 0/1 (one GPU, <= 512 loss
- *   blocks: the loss kernel's last block finishes the pass's scalars, default 1), "mask_per"
+ *   Adam launch / the all-reduce push, default 1), "fuse_finish" 0..2 (one GPU, <= 512 loss
+ *   blocks: the loss kernel's last block finishes the pass's scalars, default 1; 2: above 512
+ *   blocks too, two levels of arrivals), "mask_per"
  *   0..2 (64-draw mask words per stored RNG state; default 0: 2 for masks of >= 2^20 words,
  *   else 1), "csc_tree" 0/1 (sparse X's
  *   W1.grad as a fixed tree over each feature's entries; default 0: the reference's sequential

@@ -745,7 +745,7 @@ int pgcn_debug_set(const char *key, int value) {
     if (!in(0, 2)) return PGCN_E_INVALID;
     pgcn::g_mask_per = value;
   } else if (!std::strcmp(key, "fuse_finish")) {
-    if (!in(0, 1)) return PGCN_E_INVALID;
+    if (!in(0, 2)) return PGCN_E_INVALID;
     pgcn::g_fuse_finish = value;
   } else if (!std::strcmp(key, "tn_fold")) {
     if (!in(0, 1)) return PGCN_E_INVALID;

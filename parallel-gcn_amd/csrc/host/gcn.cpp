@@ -50,11 +50,14 @@ int g_fuse_output = 2;
 // launch (1: sparse X; 2: dense X too; bit-identical)
 int g_co_draw = 2;
 // "fuse_finish" (read per pass): one GPU, the loss kernel's last block sums the pass's
-// scalars and writes its results ring slot (XentFinal; one launch fewer per pass)
+// scalars and writes its results ring slot (XentFinal; one launch fewer per pass): 1 (default)
+// up to kFinishMaxBlocks loss blocks, 2 also above them with two levels of arrivals (reddit:
+// measured even, 615.2-616.0 vs 615.4 epochs/s -- the loss kernels' tails grew by what the
+// reduce launches cost, profiles/r06/x)
 int g_fuse_finish = 1;
 // "mask_adam" (read per epoch): one GPU, the next input mask drawn by the Adam launch
 int g_mask_adam = 1;
-constexpr int kFinishMaxBlocks = 512;
+constexpr int kFinishMaxBlocks = 512, kFinishGroup = 64;
 // "tn_fold" (read per epoch): one GPU, the weight gradients' last reduction pass runs inside
 // the Adam launch (GCN::backward_pass; bit-identical)
 int g_tn_fold = 1;
@@ -930,11 +933,23 @@ void GCN::arm_finish(int dst_offset, bool graph) {
   // -> 11.8k, citeseer 10.6k -> 11.5k epochs/s, same box, profiles/r06/e), but reddit's 3,641
   // serialised device-scope adds took the loss kernels from 21 + 39 to 58 + 69 us: there the
   // separate one-block launch stays
-  if (!g_fuse_finish || comm || ctx.xent_blocks > kFinishMaxBlocks) return;
-  if (!fin_ticket) {
+  // r06 late (fuse_finish 2): above that, two levels -- the blocks arrive on one ticket per
+  // group of kFinishGroup, the group's last block sums the group and arrives on the top ticket
+  // (reddit: 57 groups of 64 instead of 3,641 adds on one address)
+  if (!g_fuse_finish || comm) return;
+  const bool two = ctx.xent_blocks > kFinishMaxBlocks;
+  if (two && g_fuse_finish < 2) return;
+  const int groups = two ? (ctx.xent_blocks + kFinishGroup - 1) / kFinishGroup : 0;
+  if (!fin_ticket || fin_blocks < ctx.xent_blocks) {
     fin_ticket.allocate(1);
     fin_ticket.zero();
     fin_part4.allocate((size_t)std::max(1, ctx.xent_blocks) * 4);
+    fin_blocks = ctx.xent_blocks;
+    if (two) {
+      fin_gticket.allocate((size_t)groups * 16);
+      fin_gticket.zero();
+      fin_gpart4.allocate((size_t)groups * 4);
+    }
   }
   const auto &w1 = weights.front();
   fin_desc = XentFinal{};
@@ -947,6 +962,11 @@ void GCN::arm_finish(int dst_offset, bool graph) {
   fin_desc.sums = sums.get();
   fin_desc.ticket = fin_ticket.get();
   fin_desc.part4 = reinterpret_cast<float4 *>(fin_part4.get());
+  if (two) {
+    fin_desc.group = kFinishGroup;
+    fin_desc.gticket = fin_gticket.get();
+    fin_desc.gpart4 = reinterpret_cast<float4 *>(fin_gpart4.get());
+  }
   ctx.fin = &fin_desc;
 }
 

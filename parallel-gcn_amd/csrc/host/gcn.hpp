@@ -203,6 +203,9 @@ class GCN {
   // fuse_finish: the loss kernel's arrival ticket, per-block partials and the pass descriptor
   DeviceBuffer<unsigned> fin_ticket;
   DeviceBuffer<float> fin_part4;
+  DeviceBuffer<unsigned> fin_gticket;  // two-level finish: a ticket per 64-B line per group
+  DeviceBuffer<float> fin_gpart4;
+  int fin_blocks = 0;
   XentFinal fin_desc;
   void arm_finish(int dst_offset, bool graph);
   DeviceBuffer<float> grad_arena;  // all weight grads, one all-reduce

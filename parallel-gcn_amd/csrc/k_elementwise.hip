@@ -357,22 +357,62 @@ __device__ __forceinline__ void xent_finish(const XentFinal &fin, int count, flo
   typedef unsigned int u4 __attribute__((ext_vector_type(4)));
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       fin.part4, 0, (int)(gridDim.x * 16), 0x00020000);
+  const int G = fin.group;
+  const unsigned n_top = G > 0 ? (gridDim.x + G - 1) / G : gridDim.x;  // arrivals on `ticket`
   if (threadIdx.x == 0) {
     const u4 d = {__float_as_uint(red[0]), __float_as_uint(red[1]), __float_as_uint(q), 0u};
     __builtin_amdgcn_raw_buffer_store_b128(d, rs, (int)(blockIdx.x * 16), 0, 16);  // sc1
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned old =
-        __hip_atomic_fetch_add(fin.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = old == gridDim.x - 1;
+    unsigned *tk = fin.ticket;
+    unsigned n_arr = gridDim.x;
+    if (G > 0) {
+      const unsigned g = blockIdx.x / G;
+      tk = fin.gticket + 16 * g;
+      n_arr = min((unsigned)G, gridDim.x - g * G);
+    }
+    const unsigned old = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old == n_arr - 1;
   }
   __syncthreads();
   if (!last) return;
+  if (G > 0) {
+    // the group's last block: the group's partials in block order (a fixed tree), its sum to
+    // gpart4[g] (sc1), the group ticket reset, one arrival on the top ticket
+    const unsigned g = blockIdx.x / G, b0 = g * G, nb = min((unsigned)G, gridDim.x - b0);
+    float gl = 0.0f, gw = 0.0f, gq = 0.0f;
+    for (unsigned b = threadIdx.x; b < nb; b += blockDim.x) {
+      const u4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((b0 + b) * 16), 0, 16);  // sc1
+      gl += __uint_as_float(v.x);
+      gw += __uint_as_float(v.y);
+      gq += __uint_as_float(v.z);
+    }
+    gl = block_sum<XT>(gl, fred);
+    gw = block_sum<XT>(gw, fred);
+    gq = block_sum<XT>(gq, fred);
+    const __amdgpu_buffer_rsrc_t gs = __builtin_amdgcn_make_buffer_rsrc(
+        fin.gpart4, 0, (int)(n_top * 16), 0x00020000);
+    if (threadIdx.x == 0) {
+      const u4 d = {__float_as_uint(gl), __float_as_uint(gw), __float_as_uint(gq), 0u};
+      __builtin_amdgcn_raw_buffer_store_b128(d, gs, (int)(g * 16), 0, 16);  // sc1
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(fin.gticket + 16 * g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned old =
+          __hip_atomic_fetch_add(fin.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = old == n_top - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+  }
   float l = 0.0f, wr = 0.0f, w2 = 0.0f;
-  for (int b = threadIdx.x; b < (int)gridDim.x; b += blockDim.x) {
-    const u4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, b * 16, 0, 16);  // sc1
-    l += __uint_as_float(v.x);
-    wr += __uint_as_float(v.y);
-    w2 += __uint_as_float(v.z);
+  {
+    const __amdgpu_buffer_rsrc_t ts =
+        G > 0 ? __builtin_amdgcn_make_buffer_rsrc(fin.gpart4, 0, (int)(n_top * 16), 0x00020000) : rs;
+    for (int b = threadIdx.x; b < (int)n_top; b += blockDim.x) {
+      const u4 v = __builtin_amdgcn_raw_buffer_load_b128(ts, b * 16, 0, 16);  // sc1
+      l += __uint_as_float(v.x);
+      wr += __uint_as_float(v.y);
+      w2 += __uint_as_float(v.z);
+    }
   }
   l = block_sum<XT>(l, fred);
   wr = block_sum<XT>(wr, fred);
@@ -1082,7 +1122,9 @@ void launch_xent_fwd(float *logits, int ld, float *grad, const int *truth, int n
   if (n <= 0) return;
   PGCN_CHECK(ld <= 124 && c <= ld && ld % 4 == 0, PGCN_E_INVALID,
              "xent: classes must be <= 124 (ld a multiple of 4)");
-  PGCN_CHECK(!fin || (fin->ticket && fin->part4 && fin->out2), PGCN_E_INVALID,
+  PGCN_CHECK(!fin || (fin->ticket && fin->part4 && fin->out2 &&
+                      (fin->group == 0 || (fin->group > 0 && fin->gticket && fin->gpart4))),
+             PGCN_E_INVALID,
              "xent: the fused finish needs its ticket, partials and output");
   const size_t lds = (size_t)XR * xent_stride(ld) * sizeof(float);  // <= 64*124*4 = 31 KB
   PGCN_LAUNCH(k_xent_fwd, dim3(xent_blocks(n)), dim3(XT), lds, s, logits, ld, grad,
@@ -1095,7 +1137,9 @@ void launch_out_xent(const float *H, int ldh, int kh, const float *W, int ldw, f
                      float *partials, hipStream_t s, float *dH, int lddh, float *dWp,
                      const XentTable *tb, const XentFinal *fin) {
   note_path(KP_OUT_XENT);
-  PGCN_CHECK(!fin || (fin->ticket && fin->part4 && fin->out2), PGCN_E_INVALID,
+  PGCN_CHECK(!fin || (fin->ticket && fin->part4 && fin->out2 &&
+                      (fin->group == 0 || (fin->group > 0 && fin->gticket && fin->gpart4))),
+             PGCN_E_INVALID,
              "out_xent: the fused finish needs its ticket, partials and output");
   const XentTable t = training && dH && tb ? *tb : XentTable{};
   PGCN_CHECK(!t.table || (kh == 16 && t.scale), PGCN_E_INVALID,

@@ -338,6 +338,12 @@ struct XentFinal {
   float *sums = nullptr;
   unsigned *ticket = nullptr;  // zero between launches
   float4 *part4 = nullptr;     // [blocks]
+  // two levels (large grids, r06): blocks arrive on their group's ticket (gticket[16 g]: one
+  // 64-B line each) and the group's last block sums the group's partials into gpart4[g], then
+  // arrives on `ticket`; group = 0: every block on `ticket`
+  int group = 0;
+  unsigned *gticket = nullptr;  // [groups * 16], zero between launches
+  float4 *gpart4 = nullptr;     // [groups]
 };
 void launch_out_xent(const float *H, int ldh, int kh, const float *W, int ldw, float *logits,
                      int ld, float *grad, const int *truth, int n, int c, int count, int training,

@@ -609,20 +609,24 @@ def test_csc_tree_matches_sequential_chain(loaded, pgcn, name):
     np.testing.assert_array_equal(tree["w1"], again["w1"])
 
 
-@pytest.mark.parametrize("case", ["cora", "pubmed_like"])
+@pytest.mark.parametrize("case", ["cora", "pubmed_like", "two_level"])
 def test_fuse_finish_matches_reduce_launch(loaded, pgcn, case):
-    """fuse_finish 1: the loss kernel's last block sums the pass's (loss, wrong, W1^2) partials
-    and writes the results ring slot (one launch fewer per pass) -- the same losses and
+    """fuse_finish 1 / 2: the loss kernel's last block sums the pass's (loss, wrong, W1^2)
+    partials and writes the results ring slot (one launch fewer per pass; two_level: > 512
+    blocks, each group of 64 summed by its last block first) -- the same losses and
     accuracies as the separate k_reduce_scalars launch up to the summation order (1e-6
     relative; the accuracies exactly), the same gradients and weights bit for bit (the scalars
     feed nothing else); eager and through the epoch hipGraph; one launch fewer per pass."""
+    fused = 1
     if case == "pubmed_like":  # 310 loss blocks: still fused (up to 512)
         ds = pgcn.Dataset.synthetic(19717, 64, 3, 50000, 21)
+    elif case == "two_level":  # 1,000 loss blocks: group tickets of 64, then the top ticket
+        ds, fused = pgcn.Dataset.synthetic(64000, 64, 41, 400000, 23), 2
     else:
         ds = loaded["cora"]
     runs = {}
-    for name, kn in (("launch", dict(fuse_finish=0)), ("fused", dict(fuse_finish=1)),
-                     ("graph", dict(fuse_finish=1, epoch_graph=1))):
+    for name, kn in (("launch", dict(fuse_finish=0)), ("fused", dict(fuse_finish=fused)),
+                     ("graph", dict(fuse_finish=fused, epoch_graph=1))):
         with helpers.knobs(pgcn, **kn):
             g = pgcn.GCN(pgcn.make_params(ds), ds)
             sync_lines = [g.train_epoch() + g.eval(2) for _ in range(2)]
