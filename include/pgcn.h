@@ -338,7 +338,7 @@ int pgcn_debug_rank_graph(int n, const int *indptr, const int *indices, int worl
  *   "gs_orig_cols" 0/1 (a column subset's plain GraphSum gathers through the original column
  *   ids instead of compacting its input, default 1), "gs16_gather" 0..2 (the blocked d = 16
  *   gather kernel: 0 (default) by mean segment length, 1 k_graphsum16, 2 interleaved slots);
- *   r06 (29 keys): "co_draw" also 2 (dense X too, the default), "tn_fold" 0/1 (one GPU and
+ *   r06 (30 keys): "co_draw" also 2 (dense X too, the default), "tn_fold" 0/1 (one GPU and
  *   edge-cut ranks between processes: the weight gradients' last reduction pass inside the
  *   Adam launch / the all-reduce push, default 1), "fuse_finish" 0..2 (one GPU, <= 512 loss
  *   blocks: the loss kernel's last block finishes the pass's scalars, default 1; 2: above 512
@@ -347,7 +347,9 @@ int pgcn_debug_rank_graph(int n, const int *indptr, const int *indices, int worl
  *   else 1), "csc_tree" 0/1 (sparse X's
  *   W1.grad as a fixed tree over each feature's entries; default 0: the reference's sequential
  *   order, bit-exact; the tree measured slower), "mask_adam" 0/1 (one GPU: the next epoch's
- *   input mask drawn by the Adam launch, default 1, bit-identical), "reassoc_small" 0/1 (graphs
+ *   input mask drawn by the Adam launch, default 1, bit-identical), "mask_xstream" 0/1 (dense X, eval_ax: that mask drawn by
+ *   two extra waves of eval's first-layer X-stream pass instead, bit-identical, default 0:
+ *   measured slower), "reassoc_small" 0/1 (graphs
  *   under 65,536 nodes: the output layer as (A H) W with its Matmul in the loss kernel even when
  *   the classes are no more than the last hidden width <= 16, default 1; fp32 order only),
  *   "defer_wgrad" 0/1 (one GPU, <= 128 loss blocks: the output layer's W.grad block partials

@@ -30,6 +30,7 @@ extern int g_tn_fold;               // host/gcn.cpp
 extern int g_fuse_finish;           // host/gcn.cpp
 extern int g_mask_per;              // host/gcn.cpp
 extern int g_mask_adam;             // host/gcn.cpp
+extern int g_mask_xstream;          // host/gcn.cpp
 extern int g_reassoc_small;         // host/gcn.cpp
 extern int g_defer_small_wgrad;     // host/module.cpp
 extern int g_eval_ax;               // host/gcn.cpp
@@ -729,6 +730,9 @@ int pgcn_debug_set(const char *key, int value) {
   } else if (!std::strcmp(key, "eval_tail")) {
     if (!in(0, 1)) return PGCN_E_INVALID;
     pgcn::g_eval_tail = value;
+  } else if (!std::strcmp(key, "mask_xstream")) {
+    if (!in(0, 1)) return PGCN_E_INVALID;
+    pgcn::g_mask_xstream = value;
   } else if (!std::strcmp(key, "mask_adam")) {
     if (!in(0, 1)) return PGCN_E_INVALID;
     pgcn::g_mask_adam = value;

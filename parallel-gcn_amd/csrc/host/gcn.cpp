@@ -57,6 +57,12 @@ int g_co_draw = 2;
 int g_fuse_finish = 1;
 // "mask_adam" (read per epoch): one GPU, the next input mask drawn by the Adam launch
 int g_mask_adam = 1;
+// "mask_xstream" (read per epoch): dense X with eval_ax, one GPU -- the next input mask drawn
+// by eval's first-layer X-stream pass instead (GCN::mask_in_eval).  Off: bit-identical but
+// slower -- two drawing waves per CU (all the VGPR budget leaves beside the consumers) take
+// 202 us for what k_dropout_mask's 32 waves per CU draw in 63, so the pass doubles (reddit
+// 604-605 vs 617-619 epochs/s, profiles/r06/z2)
+int g_mask_xstream = 0;
 constexpr int kFinishMaxBlocks = 512, kFinishGroup = 64;
 // "tn_fold" (read per epoch): one GPU, the weight gradients' last reduction pass runs inside
 // the Adam launch (GCN::backward_pass; bit-identical)
@@ -402,6 +408,8 @@ void GCN::init_dropout_rng(const GCNData &data, long long glorot_draws) {
   jump_table.allocate(table.size() * sizeof(uint64_t));
   jump_table.upload(reinterpret_cast<const uint8_t *>(table.data()), table.size() * sizeof(uint64_t));
   ctx.jump_table = jump_table.get();
+  mask_lut.allocate(32 * 16);
+  launch_mask_lut(jump_table.get(), mask_lut.get(), stream.get());
 
   uint64_t seed[2];
   if (params.seed) pgcn_rng_seed_glibc(params.seed, seed);
@@ -919,9 +927,19 @@ int GCN::mask_with_adam(MaskDraw out[2]) {
   // (not with epoch graphs: a capture after an eager epoch would find the mask drawn ahead and
   // record a forward without its draw)
   if (!g_mask_adam || g_epoch_graph || comm || dropouts_.empty() || !dropouts_[0] ||
-      dropouts_[0]->variable() || optimizer.size() > (size_t)kAdamBatch)
+      dropouts_[0]->variable() || optimizer.size() > (size_t)kAdamBatch || mask_in_eval())
     return 0;
   return dropouts_[0]->ahead_descs(out);
+}
+
+// One GPU, dense X with eval_ax ("mask_xstream"): the next training forward's input mask (and
+// the co-drawn hidden mask) drawn by two extra waves of eval's (A X) W1 pass -- an unmasked
+// X-stream pass, HBM-bound, whose VALU is otherwise idle -- instead of by the Adam launch
+// before it.  The same stream positions whenever they are drawn: bit-identical.  A training
+// epoch with no eval after it draws its next mask in its own forward, as without the knob.
+bool GCN::mask_in_eval() const {
+  return g_mask_xstream && !g_epoch_graph && !comm && feats.ax && !dropouts_.empty() &&
+         dropouts_[0] && !dropouts_[0]->variable();
 }
 
 // One GPU ("fuse_finish", default on): the next pass's loss kernel finishes its scalars itself
@@ -1010,6 +1028,13 @@ void GCN::finalize(int dst_offset, bool graph, hipStream_t s) {
 void GCN::eval_forward(int off, bool graph) {
   const bool tail = tail_gs >= 0;
   arm_finish(off, graph);
+  ctx.xs_draw.n = 0;
+  if (!graph && mask_in_eval()) {
+    const int n = dropouts_[0]->ahead_descs(ctx.xs_draw_md);
+    for (int i = 0; i < n; i++) ctx.xs_draw.seg[i] = mask_seg_of(ctx.xs_draw_md[i]);
+    ctx.xs_draw.lut = mask_lut.get();
+    ctx.xs_draw.n = n;
+  }
   for (int i = 0; i < (int)modules.size(); i++) {
     if (tail && i == tail_gs) {
       ctx.tail_stream = comm_stream.get();

@@ -146,6 +146,8 @@ class GCN {
   // mask_adam: the next training forward's input (and co-drawn hidden) masks for the Adam
   // launch; returns how many (0: not applicable, or drawn already)
   int mask_with_adam(MaskDraw out[2]);
+  // mask_xstream: the next training forward's masks drawn by eval's first-layer product
+  bool mask_in_eval() const;
   void join_side();
   int fused_tails_ = 0;  // GraphSum epilogues carrying ReLU / Dropout work (forward + backward)
   void set_split(int split);
@@ -210,6 +212,7 @@ class GCN {
   void arm_finish(int dst_offset, bool graph);
   DeviceBuffer<float> grad_arena;  // all weight grads, one all-reduce
   DeviceBuffer<uint8_t> jump_table;
+  DeviceBuffer<uint4> mask_lut;  // the nibble tables in global memory (mask_xstream)
   DeviceBuffer<float> gemm_ws, gemm_ws_side;
   DeviceBuffer<float> xent_partials, sums, results_ring;
   // edge-cut: per ring slot and pass, the all-reduced {loss sum, wrong, sum W1^2, count}; the

@@ -218,12 +218,30 @@ void SparseMatmul::forward(bool training, const Stream &s) const {
               consumer->fwd_next->claim_forward_table(x->rows, eval_out->ld, &e.next_scale);
         e.next_sr = RING_SR;
       }
+      // mask_xstream: the next training forward's masks drawn by extra waves of this product
+      // (an unmasked pass on the ring kernel), else by their own launch below
+      XsDraw dr;
+      if (ctx->xs_draw.n > 0 && xstream_ring_ok(x->cols, x->ldx)) {
+        dr = ctx->xs_draw;
+        e.draw = &dr;
+        ctx->xs_draw.n = 0;
+      }
       launch_xstream_nn(x->rows, b->cols, x->cols, x->ax.get(), x->ldx, b->dev_data.get(), b->ld,
                         0, eval_out->dev_data.get(), eval_out->ld, nullptr, 1.0f, s.get(), nullptr,
                         &e);
     } else
       launch_gemm_nn(x->rows, b->cols, x->cols, x->ax.get(), x->ldx, b->dev_data.get(), b->ld, 0,
                      eval_out->dev_data.get(), eval_out->ld, nullptr, 0, 0, 1.0f, s.get());
+    if (ctx->xs_draw.n > 0) {  // drawn ahead all the same: the forward expects them
+      if (ctx->xs_draw.n == 2)
+        launch_dropout_mask2(ctx->xs_draw_md[0], ctx->xs_draw_md[1], ctx->jump_table, s.get());
+      else
+        launch_dropout_mask(ctx->xs_draw_md[0].states, ctx->xs_draw_md[0].n_chunks,
+                            ctx->xs_draw_md[0].elem0, ctx->xs_draw_md[0].elem_end,
+                            ctx->xs_draw_md[0].p, ctx->xs_draw_md[0].mask, ctx->jump_table,
+                            s.get(), 0, ctx->xs_draw_md[0].per);
+      ctx->xs_draw.n = 0;
+    }
     return;
   }
   if (training && ahead_valid) {  // computed by the eval forward before this one

@@ -160,6 +160,11 @@ struct ModuleContext {
   // training split, where the loss gradient is non-zero; empty: off
   std::vector<DevGraph *> chunk_col_graphs;
   const void *jump_table = nullptr;  // M^period byte tables (device)
+  // mask_xstream: the next training forward's masks, drawn by eval's first-layer product
+  // (SparseMatmul, eval_ax) -- xs_draw for the ring NN kernel, xs_draw_md for a separate
+  // launch when that product takes another kernel; n = 0: none pending
+  XsDraw xs_draw;
+  MaskDraw xs_draw_md[2];
   void *gemm_workspace = nullptr;
   size_t gemm_workspace_bytes = 0;
   // profiling of GraphSum calls

@@ -37,6 +37,7 @@
 #include "common.hpp"
 #include "kernels.hpp"
 #include "lds_dma.hpp"
+#include "mask_draw.hpp"
 
 #ifndef PGCN_XS_CHAINS
 #define PGCN_XS_CHAINS 1
@@ -59,6 +60,10 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 // NN: 2 loaders + 4 consumers (two waves on two SIMDs: 2 x ~220 registers fit); TN: 1 loader +
 // 3 consumers (its accumulators need a SIMD per consumer)
 constexpr int XL_NN_LOADERS = 2, XL_NN_CONSUMERS = 4;
+// mask_xstream (r06): two more waves that draw the next training forward's dropout masks
+// beside an unmasked NN pass (eval's (A X) W1: HBM-bound, its VALU mostly idle); they share
+// SIMDs 2 and 3 with a consumer each (2 x ~220 VGPRs per SIMD, as the loaders do)
+constexpr int XL_NN_DRAWERS = 2;
 #ifndef PGCN_XS_TN_ABLATE
 #define PGCN_XS_TN_ABLATE 0
 #endif
@@ -233,11 +238,12 @@ __device__ __forceinline__ void xl_release(unsigned *freed, int slot, int t, int
 // (no nibble-layout pass): lane (i, g) forms its row's bits as ten 64-bit words W[c] = row bits
 // 64 c .. 64 c + 63 (v_alignbit from the slot's dwords), and step s's nibble is bits
 // 16 (s & 3) + 4 g .. + 3 of W[s >> 2] -- the nibble maskT[row][4 (s & 3) + g] holds at 4 (s >> 2)
-template <int NI, bool MASKED, bool DUAL, bool FOLD, bool FLATM>
-__global__ __launch_bounds__(64 * (XL_NN_LOADERS + XL_NN_CONSUMERS), 1) void k_xs_nn_ring(
+template <int NI, bool MASKED, bool DUAL, bool FOLD, bool FLATM, bool DRAW = false>
+__global__ __launch_bounds__(64 * (XL_NN_LOADERS + XL_NN_CONSUMERS + (DRAW ? XL_NN_DRAWERS : 0)),
+                             1) void k_xs_nn_ring(
     int M, int N, int K, const float *__restrict__ A, int lda, const float *__restrict__ B,
     int ldb, int trans_b, float *__restrict__ C, int ldc, const uint64_t *__restrict__ maskT,
-    float a_scale, float *__restrict__ C2, XsEpilogue epi, XlRing rg, XsMask mk) {
+    float a_scale, float *__restrict__ C2, XsEpilogue epi, XlRing rg, XsMask mk, XsDraw dr) {
   static_assert(!DUAL || MASKED, "dual: the second product is the masked one");
   static_assert(!FLATM || MASKED, "a flat mask is a mask");
   constexpr int NS = 4 * XL_KC;
@@ -248,7 +254,8 @@ __global__ __launch_bounds__(64 * (XL_NN_LOADERS + XL_NN_CONSUMERS), 1) void k_x
   {  // B^T [16][XL_BS] (zero outside [K, N]) ahead of the ring: every load of the thread's
      // elements issued before their stores (one round trip, not one per element)
     float *bt = reinterpret_cast<float *>(lds);
-    constexpr int NT = 64 * (XL_NN_LOADERS + XL_NN_CONSUMERS), PER = (16 * NS * 16 + NT - 1) / NT;
+    constexpr int NT = 64 * (XL_NN_LOADERS + XL_NN_CONSUMERS + (DRAW ? XL_NN_DRAWERS : 0)),
+                  PER = (16 * NS * 16 + NT - 1) / NT;
     float v[PER];
 #pragma unroll
     for (int u = 0; u < PER; u++) {
@@ -267,6 +274,21 @@ __global__ __launch_bounds__(64 * (XL_NN_LOADERS + XL_NN_CONSUMERS), 1) void k_x
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int T = xl_groups(M);
+  if constexpr (DRAW) {
+    if (wave >= XL_NN_LOADERS + XL_NN_CONSUMERS) {  // the drawing waves: k_dropout_mask's work
+      constexpr int DT = 64 * XL_NN_DRAWERS;
+      const long long t0 = (long long)blockIdx.x * DT +
+                           (threadIdx.x - 64 * (XL_NN_LOADERS + XL_NN_CONSUMERS));
+      const long long G = (long long)gridDim.x * DT;
+      for (int q = 0; q < dr.n; q++) {
+        if (dr.seg[q].per == 2)
+          dropout_mask_seg<2>(dr.seg[q], dr.lut, t0, G);
+        else
+          dropout_mask_seg<1>(dr.seg[q], dr.lut, t0, G);
+      }
+      return;
+    }
+  }
   if (wave < XL_NN_LOADERS) {
     xl_load<NI, XL_NN_LOADERS, FLATM>(A, lda, M, T, wave, lane, rg, lds, ready, freed, mk);
     return;
@@ -623,12 +645,19 @@ void launch_xstream_nn_ring(int M, int N, int K, const float *A, int lda, const 
       block(64 * (XL_NN_LOADERS + XL_NN_CONSUMERS));
   const bool fold = xl_pow2(a_scale);
   const bool masked = maskT || mk.bits;
+  const XsDraw dr = e.draw ? *e.draw : XsDraw{};
+  PGCN_CHECK(dr.n == 0 || (!masked && dr.n <= 2 && dr.lut), PGCN_E_INVALID,
+             "xstream ring: mask draws beside an unmasked product, the nibble tables");
+  const dim3 block_d(64 * (XL_NN_LOADERS + XL_NN_CONSUMERS + XL_NN_DRAWERS));
 #define XNR_LAUNCH(NI, MS, DU, FO, FL)                                                          \
   PGCN_LAUNCH((k_xs_nn_ring<NI, MS, DU, FO, FL>), grid, block, 0, s, M, N, K, A, lda, B, ldb,   \
-              trans_b, C, ldc, maskT, a_scale, C2, e, rg, mk)
+              trans_b, C, ldc, maskT, a_scale, C2, e, rg, mk, XsDraw{})
 #define XNR_CASE(NI)                                                                           \
   case NI:                                                                                     \
-    if (!masked)                                                                               \
+    if (!masked && dr.n > 0)                                                                   \
+      PGCN_LAUNCH((k_xs_nn_ring<NI, false, false, false, false, true>), grid, block_d, 0, s, M, \
+                  N, K, A, lda, B, ldb, trans_b, C, ldc, maskT, a_scale, C2, e, rg, mk, dr);    \
+    else if (!masked)                                                                          \
       XNR_LAUNCH(NI, false, false, false, false);                                              \
     else if (mk.bits) {                                                                        \
       if (C2 && fold) XNR_LAUNCH(NI, true, true, true, true);                                  \

@@ -161,6 +161,21 @@ void launch_mask_nibbles(const uint64_t *mask, long long mask_base, long long ma
 // of the GraphSum it stands for (eval from Â X; no mask: eval only), next_table = that
 // GraphSum's or the next one's prescaled ring table (next_scale[r] * value at the ring
 // layout of k_ring_prescale), so neither the ReLU nor the prescale needs a launch
+// One variable's mask draw (k_dropout_mask's segment; mask_draw.hpp draws it)
+struct MaskSeg {
+  uint64_t *states = nullptr;
+  long long n_chunks = 0, elem0 = 0, elem_end = 0;
+  int threshold = 0;
+  uint64_t *mask = nullptr;
+  int per = 1;  // 64-draw words per stored state (MaskDraw::per)
+};
+// masks drawn by extra waves of the X-stream NN kernel (`mask_xstream`): up to two segments,
+// the nibble tables (32 x 16 uint4, launch_mask_lut) in global memory
+struct XsDraw {
+  MaskSeg seg[2];
+  int n = 0;
+  const uint4 *lut = nullptr;
+};
 struct XsEpilogue {
   int relu = 0;
   // backward tails of the product's rows [M][ldc] (Matmul input grad): element e = r*ldc + j
@@ -173,6 +188,7 @@ struct XsEpilogue {
   float4 *next_table = nullptr;
   const float *next_scale = nullptr;
   int next_sr = 0;
+  const XsDraw *draw = nullptr;  // (host) masks the ring NN kernel draws beside its product
 };
 // The flat dropout bitmap of X [M][K] (keep bit of X[m][k] at bit base + m * ld + k, the
 // element order rng.cpp draws), which the X-stream ring kernels read in place of the nibble
@@ -302,6 +318,10 @@ struct MaskDraw {
 };
 void launch_dropout_mask2(const MaskDraw &d0, const MaskDraw &d1, const void *table,
                           hipStream_t s);
+// the segment k_dropout_mask draws for d (launch_dropout_mask's threshold)
+MaskSeg mask_seg_of(const MaskDraw &d);
+// lut [32 * 16] uint4 = the nibble tables k_dropout_mask stages in LDS, from the byte tables
+void launch_mask_lut(const void *table, void *lut, hipStream_t s);
 void launch_dropout_apply_based(float *x, long long n, const uint64_t *mask, long long base,
                                 float scale, hipStream_t s);
 void launch_relu_fwd(float *x, long long n, uint8_t *mask, int training, hipStream_t s);

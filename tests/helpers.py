@@ -236,7 +236,8 @@ ENGINE_DEFAULTS = {"train_ahead": 1, "split_rows": 0, "split_cols": 1, "eval_ax"
                    "peer_uncached": 0, "ring_pair": 0, "tn_fold": 1,
                    "fuse_finish": 1, "mask_per": 0,
                    "ring_window": 0, "csc_tree": 0, "mask_adam": 1,
-                   "reassoc_small": 1, "defer_wgrad": 1}
+                   "reassoc_small": 1, "defer_wgrad": 1,
+                   "mask_xstream": 0}
 
 
 @contextlib.contextmanager

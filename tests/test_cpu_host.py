@@ -577,7 +577,7 @@ def test_debug_set_refuses_out_of_range_values(pgcn):
     for key, bad in (("train_ahead", 2), ("split_rows", -1), ("split_cols", 5), ("eval_ax", 2),
                      ("epoch_graph", 3), ("fuse_epilogue", 16), ("fuse_output", 4),
                      ("mm_side", 3), ("xstream_ring", 2), ("eval_tail", 2), ("gs16_gather", 3),
-                     ("peer_uncached", 2), ("ring_pair", 2), ("tn_fold", 2), ("fuse_finish", 3), ("mask_per", 3), ("ring_window", 1), ("csc_tree", 2), ("mask_adam", 2), ("reassoc_small", 2), ("defer_wgrad", 2),
+                     ("peer_uncached", 2), ("ring_pair", 2), ("tn_fold", 2), ("fuse_finish", 3), ("mask_per", 3), ("ring_window", 1), ("csc_tree", 2), ("mask_adam", 2), ("reassoc_small", 2), ("defer_wgrad", 2), ("mask_xstream", 2),
                      ("lds_blocks", 3), ("parse_threads", -2),
                      ("gs_split", 4), ("gs_item_iters", 5), ("co_draw", 3), ("gs_orig_cols", 2), ("sparse_dual", 2)):
         assert lib.pgcn_debug_set(key.encode(), bad) < 0, key

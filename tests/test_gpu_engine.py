@@ -562,6 +562,34 @@ def test_fold_and_dense_co_draw_bit_identical(loaded, pgcn, case):
     assert runs["cut"]["launches"] <= a["launches"] - 4, (a["launches"], runs["cut"]["launches"])
 
 
+def test_mask_xstream_bit_identical(rw_ds, pgcn):
+    """mask_xstream 1 (off by default: measured slower): the next training forward's masks
+    drawn by two extra waves of
+    eval's (A X) W1 X-stream pass (reddit's feature width: the ring NN kernel) instead of by
+    the Adam launch (mask_adam) or the forward itself: the same stream positions, so the same
+    bits -- epoch lines, the dropped input, weights, activations and gradients -- over eager
+    epochs, epoch_async runs and a training epoch with no eval before the next."""
+    runs = {}
+    for name, kn in (("adam", dict(mask_xstream=0, mask_adam=1)),
+                     ("forward", dict(mask_xstream=0, mask_adam=0)),
+                     ("xstream", dict(mask_xstream=1))):
+        with helpers.knobs(pgcn, **kn):
+            g = pgcn.GCN(pgcn.make_params(rw_ds), rw_ds)
+            lines = [g.train_epoch() + g.eval(2)]
+            for _ in range(3):
+                g.epoch_async()
+            lines += [tuple(x) for x in g.results(3)]
+            lines.append(g.train_epoch() + g.train_epoch() + g.eval(2))
+            runs[name] = dict(lines=lines, vars=[g.get_var(i) for i in (0, 2, 3, 5)],
+                              grads=[g.get_var(i, 1) for i in (1, 3)] + [g.get_var(2, 1)])
+            g.close()
+    a = runs["forward"]
+    for b in (runs["adam"], runs["xstream"]):
+        assert a["lines"] == b["lines"]
+        for x, y in zip(a["vars"] + a["grads"], b["vars"] + b["grads"]):
+            np.testing.assert_array_equal(x, y)
+
+
 @pytest.mark.parametrize("case", ["cora", "lds_dense"])
 def test_mask_states_per_128_draws_bit_identical(loaded, pgcn, case):
     """mask_per 2 (one xorshift state per 128 draws, jumped by the epoch's period once) draws

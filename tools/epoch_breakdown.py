@@ -3,7 +3,7 @@
 usage: python3 tools/epoch_breakdown.py gpurun_out/<dir>/trace [marker-kernel-substring]
 
 An epoch is taken between the last two launches of the marker kernel (default: eval's
-first-layer GEMM over Â X, `k_xs_nn_ring<38, false, false, false, false>`).  Prints the epoch's span, the
+first-layer GEMM over Â X, `k_xs_nn_ring<38, false, false, false, false[, true]>`).  Prints the epoch's span, the
 sum of its kernel times, the gaps between launches and the per-kernel times in launch order.
 """
 import collections
@@ -12,7 +12,7 @@ import os
 import sys
 
 trace_dir = sys.argv[1]
-marker = sys.argv[2] if len(sys.argv) > 2 else "k_xs_nn_ring<38, false, false, false, false>"
+marker = sys.argv[2] if len(sys.argv) > 2 else "k_xs_nn_ring<38, false, false, false, false"
 rows = list(csv.DictReader(open(os.path.join(trace_dir, "run_kernel_trace.csv"))))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 idx = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
